@@ -1,0 +1,101 @@
+// amino.hpp — host encoder for the TxVote amino byte strings the hot path hashes.
+//
+// SignBytes = cdc.MarshalBinaryLengthPrefixed(CanonicalizeTxVote(chainID, vote))
+//   (types/tx_vote.go:83-89, CanonicalTxVote :177-183, CanonicalizeTxVote :185-192; encoder is
+//   go-amino v0.15.1-0.20190603130624-25d5598ed22b, external).  Field rules:
+//   Height fixed64 (0x09, omitted when 0), TxHash (0x12), TxKey (0x1a 0x20 + 32 zero bytes:
+//   CanonicalizeTxVote never copies it), Timestamp (0x22, body {0x08 uvarint(uint64 sec)}
+//   {0x10 uvarint(nanos)}, sub-fields omitted when 0, whole field omitted when empty),
+//   ChainID (0x2a, omitted when empty).  Out-of-range times make amino error -> SignBytes panics.
+// Size = len(cdc.MarshalBinaryBare(TxVote)) (types/tx_vote.go:144-150).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+namespace txv_host {
+
+constexpr int64_t kAminoMinSec = -62135596800LL;   // 0001-01-01T00:00:00Z
+constexpr int64_t kAminoMaxSec = 253402300800LL;   // 10000-01-01T00:00:00Z (exclusive)
+
+inline uint32_t put_uvarint(uint8_t* out, uint64_t v) {
+  uint32_t n = 0;
+  while (v >= 0x80) { if (out) out[n] = (uint8_t)(v | 0x80); ++n; v >>= 7; }
+  if (out) out[n] = (uint8_t)v;
+  return n + 1;
+}
+
+// time body length (or -1 when amino rejects the time)
+inline int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
+  uint32_t n = 0;
+  if (sec != 0) {
+    if (sec < kAminoMinSec || sec >= kAminoMaxSec) return -1;
+    if (out) out[n] = 0x08;
+    ++n;
+    n += put_uvarint(out ? out + n : nullptr, (uint64_t)sec);
+  }
+  if (nanos != 0) {
+    if (nanos < 0 || nanos > 999999999) return -1;
+    if (out) out[n] = 0x10;
+    ++n;
+    n += put_uvarint(out ? out + n : nullptr, (uint64_t)(uint32_t)nanos);
+  }
+  return (int)n;
+}
+
+// Writes SignBytes into out (capacity cap).  Returns length, or -1 (amino error / too long).
+inline int sign_bytes(uint8_t* out, uint32_t cap, int64_t height, const uint8_t* txhash, uint32_t txhash_len,
+                      int64_t sec, int32_t nanos, const uint8_t* chain, uint32_t chain_len) {
+  uint8_t tb[24];
+  const int tl = time_body(tb, sec, nanos);
+  if (tl < 0) return -1;
+  uint64_t body = 0;
+  if (height != 0) body += 9;
+  if (txhash_len) body += 1 + put_uvarint(nullptr, txhash_len) + txhash_len;
+  body += 34;
+  if (tl > 0) body += 1 + put_uvarint(nullptr, (uint64_t)tl) + (uint64_t)tl;
+  if (chain_len) body += 1 + put_uvarint(nullptr, chain_len) + chain_len;
+  const uint32_t pl = put_uvarint(nullptr, body);
+  if (pl + body > cap) return -1;
+  uint8_t* p = out + put_uvarint(out, body);
+  if (height != 0) {
+    *p++ = 0x09;
+    for (int i = 0; i < 8; ++i) *p++ = (uint8_t)((uint64_t)height >> (8 * i));
+  }
+  if (txhash_len) {
+    *p++ = 0x12;
+    p += put_uvarint(p, txhash_len);
+    memcpy(p, txhash, txhash_len);
+    p += txhash_len;
+  }
+  *p++ = 0x1a; *p++ = 0x20;
+  memset(p, 0, 32); p += 32;
+  if (tl > 0) {
+    *p++ = 0x22;
+    p += put_uvarint(p, (uint64_t)tl);
+    memcpy(p, tb, (size_t)tl);
+    p += tl;
+  }
+  if (chain_len) {
+    *p++ = 0x2a;
+    p += put_uvarint(p, chain_len);
+    memcpy(p, chain, chain_len);
+    p += chain_len;
+  }
+  return (int)(p - out);
+}
+
+inline int txvote_size(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t addr_len,
+                       uint32_t sig_len) {
+  const int tl = time_body(nullptr, sec, nanos);
+  if (tl < 0) return 0;
+  uint64_t n = 0;
+  if (height != 0) n += 1 + put_uvarint(nullptr, (uint64_t)height);
+  if (txhash_len) n += 1 + put_uvarint(nullptr, txhash_len) + txhash_len;
+  n += 34;
+  if (tl > 0) n += 1 + put_uvarint(nullptr, (uint64_t)tl) + (uint64_t)tl;
+  if (addr_len) n += 1 + put_uvarint(nullptr, addr_len) + addr_len;
+  if (sig_len) n += 1 + put_uvarint(nullptr, sig_len) + sig_len;
+  return (int)n;
+}
+
+}  // namespace txv_host

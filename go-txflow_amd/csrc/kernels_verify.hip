@@ -1,0 +1,274 @@
+// kernels_verify.hip — gfx950 kernels for TxVote signature work.
+//
+//   txv_k_build_tables  (K0)  per validator: address = SHA-256(pub)[:20] (tendermint
+//                              PubKeyEd25519.Address, called at types/tx_vote.go:111),
+//                              ref10 decode of A, radix-16 fixed-base Niels table of A.
+//                              Also run once on the base point B.
+//   txv_k_verify        (K1)  per vote: x/crypto ed25519.Verify (types/tx_vote.go:115)
+//                              with the B table staged in LDS and the validator's A table
+//                              gathered from HBM (L2/MALL-resident for small validator sets).
+//   txv_k_keygen / txv_k_sign  load generator mirroring MockPV.SignTxVote
+//                              (types/priv_validator.go:83-95): RFC 8032 signing on device.
+//
+// Launch geometry: 256-thread workgroups (4 waves), grid-stride over votes so each
+// workgroup stages the 55 KB B table into LDS once per launch, not once per 256 votes.
+#include "ed25519_dev.h"
+#include "txv_device.h"
+
+using namespace txv;
+
+// ---------------------------------------------------------------- K0: tables
+// one workgroup of 64 lanes per point; lane i builds position i (16^i * P times 0..8)
+__global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restrict__ pubs_le, uint32_t n_points,
+                                                          uint32_t* __restrict__ tables,
+                                                          uint8_t* __restrict__ decode_ok,
+                                                          uint32_t* __restrict__ addr_words) {
+  const uint32_t pt = blockIdx.x;
+  const int pos = threadIdx.x;
+  if (pt >= n_points) return;
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = pubs_le[pt * 8 + i];
+  if (pos == 0 && addr_words) {
+    uint32_t h[8];
+    sha256_32bytes(h, w);
+    // first 20 bytes of the big-endian digest, stored as 5 little-endian-loaded words
+#pragma unroll
+    for (int i = 0; i < 5; ++i) addr_words[pt * 5 + i] = bswap32(h[i]);
+  }
+  ge_ext A;
+  bool ok = ge_decode(A, w);
+  if (pos == 0 && decode_ok) decode_ok[pt] = ok ? 1 : 0;
+  ge_ext P = A;
+  for (int i = 0; i < 4 * pos; ++i) P = ge_dbl(P);
+  ge_ext M[8];
+  M[0] = P;
+  M[1] = ge_dbl(P);
+#pragma unroll
+  for (int j = 2; j < 8; ++j) M[j] = ge_add(M[j - 1], P);
+  // batch inversion of the 8 Z coordinates (Montgomery's trick)
+  fe pref[8];
+  pref[0] = M[0].Z;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) pref[j] = fe_mul(pref[j - 1], M[j].Z);
+  fe inv = fe_invert(pref[7]);
+  uint32_t* out = tables + (size_t)pt * kTableWords + (size_t)pos * kTabEntries * kEntryWords;
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    fe zi = j ? fe_mul(inv, pref[j - 1]) : inv;
+    if (j) inv = fe_mul(inv, M[j].Z);
+    ge_niels n = ge_to_niels(M[j], zi);
+    uint32_t* e = out + (j + 1) * kEntryWords;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { e[i] = n.ypx.v[i]; e[8 + i] = n.ymx.v[i]; e[16 + i] = n.xy2d.v[i]; }
+  }
+#pragma unroll
+  for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;   // identity (1, 1, 0)
+}
+
+// ---------------------------------------------------------------- K1: verify
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) txv_k_verify(VerifyArgs a) {
+  __shared__ uint32_t btab[kTableWords];
+  // stage the base-point table: 16-byte loads, all threads
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.btable);
+    uint4* dst = reinterpret_cast<uint4*>(btab);
+    for (int i = threadIdx.x; i < kTableWords / 4; i += BLOCK) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t stride = gridDim.x * BLOCK;
+  for (uint32_t idx = blockIdx.x * BLOCK + threadIdx.x; idx < a.n; idx += stride) {
+    const uint32_t i = a.order ? a.order[idx] : idx;
+    const uint8_t fl = a.flags[i];
+    if (!(fl & TXV_FLAG_PENDING)) continue;
+    const uint32_t v = a.val[i];
+    uint32_t s[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
+    bool bad = !(fl & TXV_FLAG_SIG64) || (s[15] & 0xE0000000u) || !a.decode_ok[v] || !sc_lt_L(s + 8);
+    uint8_t ok = 0;
+    if (!bad) {
+      const uint32_t* pw = a.pubs_le + (size_t)v * 8;
+      uint64_t pre[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pre[j] = be64_from_le32(s[2 * j], s[2 * j + 1]);
+        pre[4 + j] = be64_from_le32(pw[2 * j], pw[2 * j + 1]);
+      }
+      MsgView m{a.msg + i, a.n_pad, a.msg_words, a.msg_len[i]};
+      uint32_t dig[16];
+      sha512_prefixed(dig, pre, 8, m);
+      sc k = sc_reduce512(dig);
+      uint32_t sp[8], kp[8];
+      sc_recode16(sp, s + 8);
+      sc_recode16(kp, k.v);
+      const uint32_t* ta = a.atables + (size_t)v * kTableWords;
+      ge_ext R = double_scalarmult_fixed(btab, ta, sp, kp, true);
+      uint32_t enc[8];
+      ge_encode(enc, R);
+      uint32_t diff = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) diff |= enc[j] ^ s[j];
+      ok = diff == 0;
+    }
+    a.ok_out[i] = ok;
+  }
+}
+
+// ---------------------------------------------------------------- load generator
+// keygen: seed (32 B) -> expanded secret scalar a (mod L), prefix, public key encoding
+__global__ void __launch_bounds__(64) txv_k_keygen(const uint32_t* __restrict__ seeds_le, uint32_t n,
+                                                   const uint32_t* __restrict__ btable,
+                                                   uint32_t* __restrict__ scal_out,   // n x 8 (a mod L)
+                                                   uint32_t* __restrict__ araw_out,   // n x 8 (clamped a)
+                                                   uint32_t* __restrict__ prefix_out, // n x 8 (LE words)
+                                                   uint32_t* __restrict__ pub_out) {  // n x 8 (LE words)
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t pre[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pre[j] = be64_from_le32(seeds_le[i * 8 + 2 * j], seeds_le[i * 8 + 2 * j + 1]);
+  MsgView none{nullptr, 0, 0, 0};
+  uint32_t h[16];
+  sha512_prefixed(h, pre, 4, none);
+  h[0] &= 0xfffffff8u; h[7] &= 0x7fffffffu; h[7] |= 0x40000000u;
+  uint32_t x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = j < 8 ? h[j] : 0u;
+  sc a = sc_reduce512(x);
+  uint32_t ap[8];
+  sc_recode16(ap, a.v);
+  uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ge_ext P = double_scalarmult_fixed(btable, btable, ap, zero, false);
+  uint32_t enc[8];
+  ge_encode(enc, P);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    scal_out[i * 8 + j] = a.v[j];
+    araw_out[i * 8 + j] = h[j];
+    prefix_out[i * 8 + j] = h[8 + j];
+    pub_out[i * 8 + j] = enc[j];
+  }
+}
+
+// sign: S = (r + k*a) mod L with r = SHA-512(prefix || M), R = [r]B, k = SHA-512(R || A || M)
+__global__ void __launch_bounds__(64) txv_k_sign(SignArgs a) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t v = a.val[i];
+  MsgView m{a.msg + i, a.n_pad, a.msg_words, a.msg_len[i]};
+  uint64_t pre[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pre[j] = be64_from_le32(a.prefix[v * 8 + 2 * j], a.prefix[v * 8 + 2 * j + 1]);
+  uint32_t h[16];
+  sha512_prefixed(h, pre, 4, m);
+  sc r = sc_reduce512(h);
+  uint32_t rp[8];
+  sc_recode16(rp, r.v);
+  uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ge_ext R = double_scalarmult_fixed(a.btable, a.btable, rp, zero, false);
+  uint32_t Rw[8];
+  ge_encode(Rw, R);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = be64_from_le32(Rw[2 * j], Rw[2 * j + 1]);
+    pre[4 + j] = be64_from_le32(a.pub[v * 8 + 2 * j], a.pub[v * 8 + 2 * j + 1]);
+  }
+  sha512_prefixed(h, pre, 8, m);
+  sc k = sc_reduce512(h);
+  // k * a + r  (a = clamped raw scalar; reduction of the 512-bit sum mod L)
+  uint32_t t[16];
+  {
+    uint64_t acc = 0; uint32_t ovf = 0;
+#pragma unroll
+    for (int c = 0; c < 15; ++c) {
+#pragma unroll
+      for (int j = (c > 7 ? c - 7 : 0); j <= (c < 7 ? c : 7); ++j) mac(acc, ovf, k.v[j], a.araw[v * 8 + c - j]);
+      t[c] = (uint32_t)acc;
+      acc = (acc >> 32) | ((uint64_t)ovf << 32);
+      ovf = 0;
+    }
+    t[15] = (uint32_t)acc;
+    uint64_t cc;
+    add_cc(t[0], cc, t[0], r.v[0]);
+#pragma unroll
+    for (int j = 1; j < 16; ++j) addc_cc(t[j], cc, t[j], j < 8 ? r.v[j] : 0u, cc);
+  }
+  sc S = sc_reduce512(t);
+  // optional corruption hook for the adversarial generator is applied on the host
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a.sig[(size_t)j * a.n_pad + i] = Rw[j];
+    a.sig[(size_t)(8 + j) * a.n_pad + i] = S.v[j];
+  }
+}
+
+// ---------------------------------------------------------------- field self-test
+// op 0: a*b  1: a^2  2: a+b  3: a-b  4: canon(a)  5: invert(a)  6: sc_reduce512(a||b)
+__global__ void txv_k_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x, y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { x.v[j] = a[i * 8 + j]; y.v[j] = b[i * 8 + j]; }
+  fe r;
+  switch (op) {
+    case 0: r = fe_mul(x, y); break;
+    case 1: r = fe_sq(x); break;
+    case 2: r = fe_add(x, y); break;
+    case 3: r = fe_sub(x, y); break;
+    case 4: r = fe_canon(x); break;
+    case 5: r = fe_invert(x); break;
+    default: {
+      uint32_t t[16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { t[j] = x.v[j]; t[8 + j] = y.v[j]; }
+      sc s = sc_reduce512(t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r.v[j] = s.v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[i * 8 + j] = r.v[j];
+}
+
+// ---------------------------------------------------------------- host launchers
+extern "C" {
+
+hipError_t txv_launch_build_tables(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
+                                   uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
+  if (!n_points) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_build_tables, dim3(n_points), dim3(64), 0, st, pubs_le, n_points, tables,
+                     decode_ok, addr_words);
+  return hipGetLastError();
+}
+
+hipError_t txv_launch_verify(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
+  if (!args->n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_verify<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+  return hipGetLastError();
+}
+
+hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_t* btable, uint32_t* scal,
+                             uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_keygen, dim3((n + 63) / 64), dim3(64), 0, st, seeds_le, n, btable, scal, araw,
+                     prefix, pub);
+  return hipGetLastError();
+}
+
+hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st) {
+  if (!args->n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_sign, dim3((args->n + 63) / 64), dim3(64), 0, st, *args);
+  return hipGetLastError();
+}
+
+hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,
+                                  hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_fe_selftest, dim3((n + 63) / 64), dim3(64), 0, st, a, b, out, n, op);
+  return hipGetLastError();
+}
+
+}  // extern "C"

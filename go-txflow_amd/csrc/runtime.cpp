@@ -1,0 +1,745 @@
+// runtime.cpp — host runtime behind include/txvote.h (libtxvote.so).
+//
+// Responsibilities (the parts of the reference path that stay on the host):
+//   * validator registry: address -> index (ValidatorSet.GetByAddress, ext, called at
+//     types/vote_set.go:102), powers, quorum = Total*2/3 + 1 (types/vote_set.go:158)
+//   * TxVoteSets routing: TxHash -> dense set id, created on first sight
+//     (txflow/service.go:200-209); host mirror of sum / maj23 for the readers
+//   * amino SignBytes encoding (amino.hpp) and the SoA pack into pinned buffers
+//   * device buffers, one HIP stream per context, launch order K1 verify -> K2 tally
+// Everything numeric about a vote's verdict runs on the GPU; there is no CPU verify path.
+#include "../../include/txvote.h"
+#include "txv_device.h"
+#include "txv_tally.h"
+#include "amino.hpp"
+
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr uint32_t kTableWords = 64 * 9 * 24;
+constexpr uint32_t kSlots = 4;
+
+struct Slot {
+  uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
+  uint32_t n_touched = 0, touched_cap = 0;
+  bool staged = false, ran = false;
+  // device
+  uint32_t* d_sig = nullptr; uint64_t* d_msg = nullptr; uint32_t* d_msg_len = nullptr;
+  uint32_t* d_val = nullptr; uint32_t* d_set = nullptr; uint8_t* d_flags = nullptr;
+  uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr;
+  uint32_t* d_touched = nullptr; int64_t* d_tsum = nullptr; uint8_t* d_tmaj = nullptr; uint32_t* d_tcross = nullptr;
+  // pinned host
+  uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
+  uint32_t* h_val = nullptr; uint32_t* h_set = nullptr; uint8_t* h_flags = nullptr; uint8_t* h_status = nullptr;
+  uint32_t* h_touched = nullptr; int64_t* h_tsum = nullptr; uint8_t* h_tmaj = nullptr; uint32_t* h_tcross = nullptr;
+  std::vector<uint8_t> tmp_msg;   // SignBytes arena
+  std::vector<size_t> tmp_off;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+}  // namespace
+
+struct txv_ctx {
+  txv_config cfg{};
+  int device = 0;
+  int n_cus = 256;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::mutex mu;
+  // validator registry
+  uint32_t n_vals = 0;
+  std::vector<uint8_t> pubs, addrs, decode_ok;
+  std::vector<int64_t> powers;
+  int64_t total = 0, quorum = 0;
+  std::string chain;
+  std::unordered_map<std::string, uint32_t> addr_index;
+  uint32_t* d_pubs = nullptr; uint8_t* d_decode_ok = nullptr; uint32_t* d_atables = nullptr;
+  uint32_t* d_addr = nullptr; int64_t* d_power = nullptr;
+  uint32_t* d_btable = nullptr;
+  // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
+  uint32_t tmp_cap = 0;
+  uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
+  // tally state
+  std::unordered_map<std::string, uint32_t> tx_index;
+  std::vector<std::string> tx_keys;
+  std::vector<int64_t> h_sum;
+  std::vector<uint8_t> h_maj;
+  std::vector<uint32_t> seen_epoch;
+  uint32_t* d_acc_slot = nullptr; uint64_t* d_first_tag = nullptr; uint32_t* d_arena = nullptr;
+  uint32_t* d_arena_count = nullptr; uint32_t* d_errflags = nullptr;
+  int64_t* d_set_sum = nullptr; uint32_t* d_set_cross = nullptr; uint32_t* d_bitmap = nullptr;
+  uint32_t epoch = 0;
+  // signer slots (load generator)
+  uint32_t n_signers = 0;
+  uint32_t *d_sk_scal = nullptr, *d_sk_araw = nullptr, *d_sk_prefix = nullptr, *d_sk_pub = nullptr;
+  Slot slots[kSlots];
+};
+
+#define HIP_TRY(ctx, x)                                                                    \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      (ctx)->err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return TXV_EDEVICE;                                                                  \
+    }                                                                                      \
+  } while (0)
+
+namespace {
+
+template <typename T>
+int dalloc(txv_ctx* c, T** p, size_t count) {
+  if (*p) { (void)hipFree(*p); *p = nullptr; }
+  if (!count) return TXV_OK;
+  HIP_TRY(c, hipMalloc((void**)p, count * sizeof(T)));
+  return TXV_OK;
+}
+template <typename T>
+int halloc(txv_ctx* c, T** p, size_t count) {
+  if (*p) { (void)hipHostFree(*p); *p = nullptr; }
+  if (!count) return TXV_OK;
+  HIP_TRY(c, hipHostMalloc((void**)p, count * sizeof(T), hipHostMallocDefault));
+  return TXV_OK;
+}
+template <typename T> void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
+template <typename T> void hfree(T*& p) { if (p) { (void)hipHostFree(p); p = nullptr; } }
+
+inline uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+inline uint64_t be64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+  return v;
+}
+
+int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
+  const uint32_t need = std::max<uint32_t>(n, 64);
+  if (s.cap < need || s.msg_cap_words < msg_words) {
+    const uint32_t cap = std::max(need, s.cap);
+    const uint32_t mw = std::max(msg_words, s.msg_cap_words);
+    const size_t npad = (cap + 63) / 64 * 64;
+    int r;
+    if ((r = dalloc(c, &s.d_sig, 16 * npad)) || (r = dalloc(c, &s.d_msg, (size_t)mw * npad)) ||
+        (r = dalloc(c, &s.d_msg_len, npad)) || (r = dalloc(c, &s.d_val, npad)) || (r = dalloc(c, &s.d_set, npad)) ||
+        (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
+        (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
+        (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
+        (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)))
+      return r;
+    s.cap = cap;
+    s.msg_cap_words = mw;
+  }
+  if (s.touched_cap < need) {
+    int r;
+    if ((r = dalloc(c, &s.d_touched, need)) || (r = dalloc(c, &s.d_tsum, need)) || (r = dalloc(c, &s.d_tmaj, need)) ||
+        (r = dalloc(c, &s.d_tcross, need)) || (r = halloc(c, &s.h_touched, need)) || (r = halloc(c, &s.h_tsum, need)) ||
+        (r = halloc(c, &s.h_tmaj, need)) || (r = halloc(c, &s.h_tcross, need)))
+      return r;
+    s.touched_cap = need;
+  }
+  if (!s.ev[0])
+    for (auto& e : s.ev) HIP_TRY(c, hipEventCreate(&e));
+  return TXV_OK;
+}
+
+int alloc_tally(txv_ctx* c) {
+  const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
+  int r;
+  if ((r = dalloc(c, &c->d_acc_slot, cells)) || (r = dalloc(c, &c->d_first_tag, cells)) ||
+      (r = dalloc(c, &c->d_arena, (size_t)c->cfg.max_accepted * 16)) || (r = dalloc(c, &c->d_arena_count, 1)) ||
+      (r = dalloc(c, &c->d_errflags, 1)) || (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_cross, c->cfg.max_txs)) || (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)))
+    return r;
+  return TXV_OK;
+}
+
+int reset_tally(txv_ctx* c) {
+  const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
+  HIP_TRY(c, hipMemsetAsync(c->d_acc_slot, 0, cells * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_arena_count, 0, 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_errflags, 0, 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
+  c->epoch = 0;
+  c->tx_index.clear();
+  c->tx_keys.clear();
+  c->h_sum.clear();
+  c->h_maj.clear();
+  c->seen_epoch.clear();
+  return TXV_OK;
+}
+
+// SignBytes for every vote into s.tmp_msg (arena; offsets in s.tmp_off); returns max len
+uint32_t encode_all(txv_ctx* c, Slot& s, const txv_votes* v, const char* chain, uint32_t chain_len,
+                    std::vector<int>& lens) {
+  s.tmp_msg.clear();
+  s.tmp_msg.reserve((size_t)v->n * (160 + chain_len));
+  s.tmp_off.resize(v->n);
+  lens.resize(v->n);
+  uint32_t mx = 0;
+  for (uint32_t i = 0; i < v->n; ++i) {
+    s.tmp_off[i] = s.tmp_msg.size();
+    if (v->is_nil && v->is_nil[i]) { lens[i] = -2; continue; }
+    const uint32_t need = 32 + 10 + 10 + v->txhash_len[i] + 24 + chain_len + 16;
+    const size_t at = s.tmp_msg.size();
+    s.tmp_msg.resize(at + need);
+    const int L = txv_host::sign_bytes(s.tmp_msg.data() + at, need, v->height[i], v->txhash + v->txhash_off[i],
+                                       v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], (const uint8_t*)chain,
+                                       chain_len);
+    s.tmp_msg.resize(at + (L > 0 ? (size_t)L : 0));
+    lens[i] = L;
+    if (L > 0 && (uint32_t)L > mx) mx = (uint32_t)L;
+  }
+  (void)c;
+  return mx;
+}
+
+// column-major transposes into the slot's pinned buffers
+void pack_columns(Slot& s, const txv_votes* v, const std::vector<int>& lens) {
+  const uint32_t n = v->n, np = s.n_pad, mw = s.msg_words;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* sg = v->sig + (size_t)i * 64;
+    const uint32_t sl = v->sig_len[i] > 64 ? 64 : v->sig_len[i];
+    uint8_t tmp[64];
+    memset(tmp, 0, 64);
+    memcpy(tmp, sg, sl);
+    for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = le32(tmp + 4 * j);
+    const int L = lens[i];
+    s.h_msg_len[i] = L > 0 ? (uint32_t)L : 0;
+    const uint8_t* m = s.tmp_msg.data() + s.tmp_off[i];
+    for (uint32_t w = 0; w < mw; ++w) {
+      uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (L > 0) {
+        const int off = (int)(8 * w);
+        const int take = std::min(8, L - off);
+        if (take > 0) memcpy(b, m + off, (size_t)take);
+      }
+      s.h_msg[(size_t)w * np + i] = be64(b);
+    }
+  }
+  for (uint32_t i = n; i < np; ++i) {
+    for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = 0;
+    for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = 0;
+    s.h_msg_len[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0; s.h_flags[i] = 0; s.h_status[i] = TXV_ERR_NIL;
+  }
+}
+
+int upload_slot(txv_ctx* c, Slot& s) {
+  const size_t np = s.n_pad;
+  HIP_TRY(c, hipMemcpyAsync(s.d_sig, s.h_sig, 16 * np * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_msg, s.h_msg, (size_t)s.msg_words * np * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_val, s.h_val, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_flags, s.h_flags, np, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_status, s.h_status, np, hipMemcpyHostToDevice, c->stream));
+  if (s.n_touched)
+    HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->stream));
+  return TXV_OK;
+}
+
+uint32_t verify_grid(txv_ctx* c, uint32_t n) {
+  const uint32_t blocks = (n + TXV_VERIFY_BLOCK - 1) / TXV_VERIFY_BLOCK;
+  const uint32_t cap = (uint32_t)c->n_cus * 2;   // 2 workgroups/CU (LDS: 2 x 55 KB B table)
+  return std::max<uint32_t>(1, std::min(blocks, cap));
+}
+
+VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t* dok, const uint32_t* tabs) {
+  VerifyArgs a{};
+  a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words;
+  a.sig = s.d_sig; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val; a.flags = s.d_flags;
+  a.order = nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
+  a.ok_out = s.d_ok;
+  return a;
+}
+
+TallyArgs tally_args(txv_ctx* c, Slot& s) {
+  TallyArgs a{};
+  a.n = s.n; a.n_pad = s.n_pad; a.n_vals = c->n_vals; a.epoch_hi = 0xFFFFFFFFu - c->epoch;
+  a.quorum = c->quorum;
+  a.sig = s.d_sig; a.set = s.d_set; a.val = s.d_val; a.flags = s.d_flags; a.ok = s.d_ok; a.status = s.d_status;
+  a.acc_slot = c->d_acc_slot; a.first_tag = c->d_first_tag; a.arena = c->d_arena; a.arena_count = c->d_arena_count;
+  a.arena_cap = c->cfg.max_accepted; a.n_touched = s.n_touched; a.error_flags = c->d_errflags;
+  a.power = c->d_power; a.set_sum = c->d_set_sum; a.set_cross = c->d_set_cross; a.commit_bitmap = c->d_bitmap;
+  a.touched = s.d_touched; a.t_sum = s.d_tsum; a.t_maj = s.d_tmaj; a.t_cross = s.d_tcross;
+  return a;
+}
+
+// stage for the AddVote path: routing, pre-checks, SignBytes, pack, upload
+int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
+  if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+  if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  Slot& s = c->slots[slot];
+  std::vector<int> lens;
+  const uint32_t mx = encode_all(c, s, v, c->chain.data(), (uint32_t)c->chain.size(), lens);
+  const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
+  int r = ensure_slot(c, s, v->n, mw);
+  if (r) return r;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw;
+  // epoch used for touched-set de-duplication on the host
+  const uint32_t host_epoch = c->epoch + 1;
+  s.n_touched = 0;
+  for (uint32_t i = 0; i < v->n; ++i) {
+    s.h_flags[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0;
+    if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
+    std::string key((const char*)v->txhash + v->txhash_off[i], v->txhash_len[i]);
+    auto it = c->tx_index.find(key);
+    uint32_t sid;
+    if (it == c->tx_index.end()) {
+      sid = (uint32_t)c->tx_keys.size();
+      if (sid >= c->cfg.max_txs) { c->err = "TxVoteSets exceed max_txs"; return TXV_ECAPACITY; }
+      c->tx_index.emplace(key, sid);
+      c->tx_keys.push_back(std::move(key));
+      c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_epoch.push_back(0);
+    } else sid = it->second;
+    s.h_set[i] = sid;
+    if (c->seen_epoch[sid] != host_epoch) { c->seen_epoch[sid] = host_epoch; s.h_touched[s.n_touched++] = sid; }
+    if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
+    uint32_t vi = UINT32_MAX;
+    if (v->addr_len[i] == 20) {
+      auto a = c->addr_index.find(std::string((const char*)v->addr + (size_t)i * 20, 20));
+      if (a != c->addr_index.end()) vi = a->second;
+    }
+    if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
+    s.h_val[i] = vi;
+    if (lens[i] < 0) { s.h_status[i] = TXV_ERR_SIGNBYTES; continue; }
+    s.h_status[i] = 0xFF;
+    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
+  }
+  pack_columns(s, v, lens);
+  if ((r = upload_slot(c, s))) return r;
+  s.staged = true; s.ran = false;
+  return TXV_OK;
+}
+
+int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
+  Slot& s = c->slots[slot];
+  if (!s.staged) { c->err = "slot not staged"; return TXV_ESTATE; }
+  c->epoch++;
+  if (c->epoch == 0xFFFFFFFFu) {   // tag space exhausted: clear candidates once
+    const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
+    HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
+    c->epoch = 1;
+  }
+  HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
+  VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
+  HIP_TRY(c, txv_launch_verify(&va, verify_grid(c, s.n), c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
+  TallyArgs ta = tally_args(c, s);
+  HIP_TRY(c, txv_launch_tally(&ta, c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
+  s.ran = true;
+  if (ms) {
+    HIP_TRY(c, hipEventSynchronize(s.ev[2]));
+    HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
+    HIP_TRY(c, hipEventElapsedTime(&ms[1], s.ev[1], s.ev[2]));
+    ms[2] = ms[0] + ms[1];
+  }
+  return TXV_OK;
+}
+
+int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap, uint32_t* n_ev) {
+  Slot& s = c->slots[slot];
+  if (!s.ran) { c->err = "slot not run"; return TXV_ESTATE; }
+  HIP_TRY(c, hipMemcpyAsync(s.h_status, s.d_status, s.n, hipMemcpyDeviceToHost, c->stream));
+  if (s.n_touched) {
+    HIP_TRY(c, hipMemcpyAsync(s.h_tsum, s.d_tsum, (size_t)s.n_touched * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.h_tmaj, s.d_tmaj, s.n_touched, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.h_tcross, s.d_tcross, (size_t)s.n_touched * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  uint32_t errf = 0;
+  HIP_TRY(c, hipMemcpyAsync(&errf, c->d_errflags, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (errf & TXV_DEVERR_ARENA_FULL) { c->err = "accepted-signature arena full"; return TXV_ECAPACITY; }
+  if (status_out) memcpy(status_out, s.h_status, s.n);
+  uint32_t ne = 0;
+  for (uint32_t t = 0; t < s.n_touched; ++t) {
+    const uint32_t sid = s.h_touched[t];
+    c->h_sum[sid] = s.h_tsum[t];
+    c->h_maj[sid] = s.h_tmaj[t];
+    if (s.h_tcross[t] != TXV_NO_CROSS) {
+      if (ev && ne < ev_cap) ev[ne] = txv_commit_event{s.h_tcross[t], sid, s.h_tsum[t]};
+      ++ne;
+    }
+  }
+  if (n_ev) *n_ev = ne;
+  return TXV_OK;
+}
+
+int build_base_table(txv_ctx* c) {
+  uint32_t* d_b = nullptr;
+  int r;
+  if ((r = dalloc(c, &c->d_btable, kTableWords))) return r;
+  if ((r = dalloc(c, &d_b, 8))) return r;
+  const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  HIP_TRY(c, hipMemcpyAsync(d_b, bw, 32, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, txv_launch_build_tables(d_b, 1, c->d_btable, nullptr, nullptr, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  dfree(d_b);
+  return TXV_OK;
+}
+
+}  // namespace
+
+// ==================================================================== C ABI
+extern "C" {
+
+int txv_init(const txv_config* cfg, txv_ctx** out) {
+  if (!out) return TXV_EINVAL;
+  *out = nullptr;
+  txv_ctx* c = new (std::nothrow) txv_ctx();
+  if (!c) return TXV_ENOMEM;
+  if (cfg) c->cfg = *cfg;
+  else { c->cfg.device = -1; }
+  if (!c->cfg.max_batch) c->cfg.max_batch = 1u << 20;
+  if (!c->cfg.max_txs) c->cfg.max_txs = 1u << 20;
+  if (!c->cfg.max_validators) c->cfg.max_validators = 1024;
+  if (!c->cfg.max_accepted) c->cfg.max_accepted = (uint32_t)std::min<uint64_t>((uint64_t)c->cfg.max_txs * 128, 1u << 28);
+  if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    delete c;
+    return TXV_EDEVICE;
+  }
+  int dev = c->cfg.device;
+  if (dev < 0) { if (hipGetDevice(&dev) != hipSuccess) dev = 0; }
+  if (dev >= ndev) { delete c; return TXV_EINVAL; }
+  c->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return TXV_EDEVICE;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->n_cus = prop.multiProcessorCount;
+  if (build_base_table(c) != TXV_OK) { txv_destroy(c); return TXV_EDEVICE; }
+  *out = c;
+  return TXV_OK;
+}
+
+void txv_destroy(txv_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& s : c->slots) {
+    dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
+    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
+    hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
+    hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross);
+    for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
+  }
+  dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
+  dfree(c->d_btable); dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
+  dfree(c->d_acc_slot); dfree(c->d_first_tag); dfree(c->d_arena); dfree(c->d_arena_count); dfree(c->d_errflags);
+  dfree(c->d_set_sum); dfree(c->d_set_cross); dfree(c->d_bitmap);
+  dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* txv_last_error(txv_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int txv_device_name(txv_ctx* c, char* buf, uint32_t cap) {
+  if (!c || !buf || !cap) return TXV_EINVAL;
+  hipDeviceProp_t p;
+  HIP_TRY(c, hipGetDeviceProperties(&p, c->device));
+  snprintf(buf, cap, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+  return TXV_OK;
+}
+
+int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers, uint32_t n, const char* chain_id,
+                       uint32_t chain_len) {
+  if (!c || (!pubs32 && n) || (!powers && n)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n > c->cfg.max_validators) { c->err = "validator set exceeds max_validators"; return TXV_ECAPACITY; }
+  c->n_vals = n;
+  c->pubs.assign(pubs32, pubs32 + (size_t)n * 32);
+  c->powers.assign(powers, powers + n);
+  c->total = 0;
+  for (uint32_t i = 0; i < n; ++i) c->total += powers[i];
+  c->quorum = c->total * 2 / 3 + 1;
+  c->chain.assign(chain_id ? chain_id : "", chain_id ? chain_len : 0);
+  int r;
+  if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
+      (r = dalloc(c, &c->d_atables, (size_t)n * kTableWords)) || (r = dalloc(c, &c->d_addr, (size_t)n * 5)) ||
+      (r = dalloc(c, &c->d_power, n)))
+    return r;
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_pubs, pubs32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_power, powers, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, txv_launch_build_tables(c->d_pubs, n, c->d_atables, c->d_decode_ok, c->d_addr, c->stream));
+  }
+  c->addrs.resize((size_t)n * 20);
+  c->decode_ok.resize(n);
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->addrs.data(), c->d_addr, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->decode_ok.data(), c->d_decode_ok, n, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->addr_index.clear();
+  for (uint32_t i = 0; i < n; ++i) c->addr_index.emplace(std::string((const char*)c->addrs.data() + 20 * i, 20), i);
+  if ((r = alloc_tally(c))) return r;
+  return reset_tally(c);
+}
+
+int txv_get_validator_info(txv_ctx* c, uint8_t* addr20_out, uint8_t* decode_ok_out, uint32_t cap) {
+  if (!c) return TXV_EINVAL;
+  const uint32_t n = std::min(cap, c->n_vals);
+  if (addr20_out) memcpy(addr20_out, c->addrs.data(), (size_t)n * 20);
+  if (decode_ok_out) memcpy(decode_ok_out, c->decode_ok.data(), n);
+  return (int)c->n_vals;
+}
+
+int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint8_t* status_out) {
+  if (!c || !v || !status_out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  if (!pubs32 && !c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+  Slot& s = c->slots[kSlots - 1];
+  std::vector<int> lens;
+  const uint32_t mx = encode_all(c, s, v, c->chain.data(), (uint32_t)c->chain.size(), lens);
+  const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
+  int r = ensure_slot(c, s, v->n, mw);
+  if (r) return r;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
+  // key registry for this call
+  const uint32_t* kp = c->d_pubs; const uint8_t* kok = c->d_decode_ok; const uint32_t* ktab = c->d_atables;
+  std::vector<uint8_t> key_addr;
+  if (pubs32) {
+    std::unordered_map<std::string, uint32_t> uniq;
+    std::vector<uint8_t> ukeys;
+    std::vector<uint32_t> kidx(v->n);
+    for (uint32_t i = 0; i < v->n; ++i) {
+      std::string k((const char*)pubs32 + (size_t)i * 32, 32);
+      auto it = uniq.find(k);
+      if (it == uniq.end()) {
+        it = uniq.emplace(k, (uint32_t)uniq.size()).first;
+        ukeys.insert(ukeys.end(), k.begin(), k.end());
+      }
+      kidx[i] = it->second;
+    }
+    const uint32_t nu = (uint32_t)uniq.size();
+    if (nu > c->tmp_cap) {
+      if ((r = dalloc(c, &c->d_tmp_pubs, (size_t)nu * 8)) || (r = dalloc(c, &c->d_tmp_ok, nu)) ||
+          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * kTableWords)) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
+        return r;
+      c->tmp_cap = nu;
+    }
+    if (nu) {
+      HIP_TRY(c, hipMemcpyAsync(c->d_tmp_pubs, ukeys.data(), (size_t)nu * 32, hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(c, txv_launch_build_tables(c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
+    }
+    key_addr.resize((size_t)nu * 20);
+    if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr.data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    kp = c->d_tmp_pubs; kok = c->d_tmp_ok; ktab = c->d_tmp_tables;
+    for (uint32_t i = 0; i < v->n; ++i) {
+      s.h_flags[i] = 0; s.h_set[i] = 0; s.h_val[i] = kidx[i];
+      if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
+      const bool addr_ok = v->addr_len[i] == 20 && !memcmp(key_addr.data() + (size_t)kidx[i] * 20, v->addr + (size_t)i * 20, 20);
+      if (!addr_ok) { s.h_status[i] = TXV_ERR_INVALID_VALIDATOR_ADDRESS; continue; }
+      if (lens[i] < 0) { s.h_status[i] = TXV_ERR_SIGNBYTES; continue; }
+      s.h_status[i] = 0xFF;
+      s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
+    }
+  } else {
+    for (uint32_t i = 0; i < v->n; ++i) {
+      s.h_flags[i] = 0; s.h_set[i] = 0; s.h_val[i] = 0;
+      if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
+      uint32_t vi = UINT32_MAX;
+      if (v->addr_len[i] == 20) {
+        auto a = c->addr_index.find(std::string((const char*)v->addr + (size_t)i * 20, 20));
+        if (a != c->addr_index.end()) vi = a->second;
+      }
+      if (vi == UINT32_MAX) { s.h_status[i] = v->addr_len[i] ? TXV_ERR_UNKNOWN_VALIDATOR : TXV_ERR_EMPTY_ADDR; continue; }
+      s.h_val[i] = vi;
+      if (lens[i] < 0) { s.h_status[i] = TXV_ERR_SIGNBYTES; continue; }
+      s.h_status[i] = 0xFF;
+      s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
+    }
+  }
+  pack_columns(s, v, lens);
+  if ((r = upload_slot(c, s))) return r;
+  VerifyArgs va = verify_args(c, s, kp, kok, ktab);
+  HIP_TRY(c, txv_launch_verify(&va, verify_grid(c, s.n), c->stream));
+  std::vector<uint8_t> ok(v->n);
+  if (v->n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, v->n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < v->n; ++i) {
+    if (s.h_status[i] == 0xFF) status_out[i] = ok[i] ? TXV_ADDED : TXV_ERR_INVALID_SIGNATURE;
+    else status_out[i] = s.h_status[i];
+  }
+  return TXV_OK;
+}
+
+int txv_add_votes(txv_ctx* c, const txv_votes* v, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
+                  uint32_t* n_ev) {
+  if (!c || !v) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int r;
+  if ((r = stage_add(c, 0, v))) return r;
+  if ((r = run_slot(c, 0, nullptr))) return r;
+  return fetch_slot(c, 0, status_out, ev, ev_cap, n_ev);
+}
+
+int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->tx_index.find(std::string((const char*)txhash, len));
+  if (it == c->tx_index.end()) return 0;
+  if (sum) *sum = c->h_sum[it->second];
+  if (maj23) *maj23 = c->h_maj[it->second];
+  return 1;
+}
+
+uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? (uint32_t)c->tx_keys.size() : 0; }
+int64_t txv_total_power(txv_ctx* c) { return c ? c->total : 0; }
+
+int txv_signbytes(int64_t height, const uint8_t* txhash, uint32_t txhash_len, int64_t ts_sec, int32_t ts_nanos,
+                  const char* chain_id, uint32_t chain_len, uint8_t* out, uint32_t cap) {
+  if (!out) return TXV_EINVAL;
+  return txv_host::sign_bytes(out, cap, height, txhash, txhash_len, ts_sec, ts_nanos, (const uint8_t*)chain_id,
+                              chain_len);
+}
+
+int txv_txvote_size(int64_t height, uint32_t txhash_len, int64_t ts_sec, int32_t ts_nanos, uint32_t addr_len,
+                    uint32_t sig_len) {
+  return txv_host::txvote_size(height, txhash_len, ts_sec, ts_nanos, addr_len, sig_len);
+}
+
+int txv_keygen(txv_ctx* c, const uint8_t* seeds32, uint32_t n, uint8_t* pubs_out) {
+  if (!c || (!seeds32 && n)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  uint32_t* d_seeds = nullptr;
+  int r;
+  if ((r = dalloc(c, &d_seeds, (size_t)n * 8)) || (r = dalloc(c, &c->d_sk_scal, (size_t)n * 8)) ||
+      (r = dalloc(c, &c->d_sk_araw, (size_t)n * 8)) || (r = dalloc(c, &c->d_sk_prefix, (size_t)n * 8)) ||
+      (r = dalloc(c, &c->d_sk_pub, (size_t)n * 8)))
+    return r;
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(d_seeds, seeds32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, txv_launch_keygen(d_seeds, n, c->d_btable, c->d_sk_scal, c->d_sk_araw, c->d_sk_prefix, c->d_sk_pub,
+                                 c->stream));
+    if (pubs_out) HIP_TRY(c, hipMemcpyAsync(pubs_out, c->d_sk_pub, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  dfree(d_seeds);
+  c->n_signers = n;
+  return TXV_OK;
+}
+
+int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const char* chain_id, uint32_t chain_len,
+                   uint8_t* sig_out) {
+  if (!c || !v || !signer || !sig_out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  for (uint32_t i = 0; i < v->n; ++i)
+    if (signer[i] >= c->n_signers) { c->err = "signer index out of range"; return TXV_EINVAL; }
+  Slot& s = c->slots[kSlots - 2];
+  std::vector<int> lens;
+  const uint32_t mx = encode_all(c, s, v, chain_id, chain_len, lens);
+  const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
+  int r = ensure_slot(c, s, v->n, mw);
+  if (r) return r;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
+  for (uint32_t i = 0; i < v->n; ++i) { s.h_val[i] = signer[i]; s.h_flags[i] = 0; s.h_set[i] = 0; s.h_status[i] = 0; }
+  // sig columns are outputs; pack zeros for them (pack_columns copies caller sig bytes, so
+  // supply a zero signature view)
+  std::vector<uint8_t> zsig((size_t)v->n * 64, 0);
+  std::vector<uint32_t> zlen(v->n, 64);
+  txv_votes vz = *v;
+  vz.sig = zsig.data(); vz.sig_len = zlen.data();
+  pack_columns(s, &vz, lens);
+  if ((r = upload_slot(c, s))) return r;
+  SignArgs a{};
+  a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val;
+  a.prefix = c->d_sk_prefix; a.araw = c->d_sk_araw; a.pub = c->d_sk_pub; a.btable = c->d_btable; a.sig = s.d_sig;
+  HIP_TRY(c, txv_launch_sign(&a, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.h_sig, s.d_sig, (size_t)16 * s.n_pad * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < v->n; ++i)
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t w = s.h_sig[(size_t)j * s.n_pad + i];
+      uint8_t* o = sig_out + (size_t)i * 64 + 4 * j;
+      o[0] = (uint8_t)w; o[1] = (uint8_t)(w >> 8); o[2] = (uint8_t)(w >> 16); o[3] = (uint8_t)(w >> 24);
+    }
+  return TXV_OK;
+}
+
+int txv_stage(txv_ctx* c, uint32_t slot, const txv_votes* v) {
+  if (!c || !v || slot >= kSlots - 2) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int r = stage_add(c, slot, v);
+  if (r) return r;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+int txv_run_staged(txv_ctx* c, uint32_t slot, float* ms) {
+  if (!c || slot >= kSlots - 2) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  return run_slot(c, slot, ms);
+}
+
+int txv_fetch_staged(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
+                     uint32_t* n_ev) {
+  if (!c || slot >= kSlots - 2) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  return fetch_slot(c, slot, status_out, ev, ev_cap, n_ev);
+}
+
+int txv_commit_bitmap(txv_ctx* c, void** dev_ptr, uint64_t* bytes) {
+  if (!c || !dev_ptr || !bytes) return TXV_EINVAL;
+  *dev_ptr = c->d_bitmap;
+  *bytes = (uint64_t)(c->cfg.max_txs + 31) / 32 * 4;
+  return TXV_OK;
+}
+
+int txv_reset_tally(txv_ctx* c) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->n_vals) return TXV_OK;
+  return reset_tally(c);
+}
+
+int txv_sync(txv_ctx* c) {
+  if (!c) return TXV_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op) {
+  if (!c || !a || !b || !out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  uint32_t *da = nullptr, *db = nullptr, *dout = nullptr;
+  int r;
+  if ((r = dalloc(c, &da, (size_t)n * 8)) || (r = dalloc(c, &db, (size_t)n * 8)) || (r = dalloc(c, &dout, (size_t)n * 8)))
+    return r;
+  HIP_TRY(c, hipMemcpyAsync(da, a, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(db, b, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, txv_launch_fe_selftest(da, db, dout, n, op, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  dfree(da); dfree(db); dfree(dout);
+  return TXV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// txv_device.h — kernel argument blocks and launcher declarations shared by the
+// HIP kernels and the host runtime.  Plain structs of device pointers and sizes.
+//
+// Batch layout in HBM (column-major SoA, stride n_pad = votes rounded up to 64 so a
+// wave's lanes read consecutive words of the same field):
+//   sig[16][n_pad]      u32  signature bytes 0..63 as little-endian words (R = 0..7, S = 8..15)
+//   msg[msg_words][n_pad] u64 SignBytes as big-endian 64-bit words, zero beyond msg_len
+//   msg_len[n], val[n] (validator index), flags[n] (TXV_FLAG_*), set[n] (tx-set id)
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#ifndef TXV_VERIFY_BLOCK
+#define TXV_VERIFY_BLOCK 256
+#endif
+
+#define TXV_FLAG_PENDING 0x01u   // vote reaches the Verify step (pre-checks passed)
+#define TXV_FLAG_SIG64   0x02u   // len(Signature) == 64
+
+struct VerifyArgs {
+  uint32_t n, n_pad, msg_words, pad0;
+  const uint32_t* sig;         // [16][n_pad]
+  const uint64_t* msg;         // [msg_words][n_pad]
+  const uint32_t* msg_len;     // [n]
+  const uint32_t* val;         // [n]
+  const uint8_t* flags;        // [n]
+  const uint32_t* order;       // optional processing order (validator-grouped), may be null
+  const uint32_t* pubs_le;     // [n_vals][8]
+  const uint8_t* decode_ok;    // [n_vals]
+  const uint32_t* atables;     // [n_vals][kTableWords]
+  const uint32_t* btable;      // [kTableWords]
+  uint8_t* ok_out;             // [n]
+};
+
+struct SignArgs {
+  uint32_t n, n_pad, msg_words, pad0;
+  const uint64_t* msg;         // [msg_words][n_pad]
+  const uint32_t* msg_len;     // [n]
+  const uint32_t* val;         // [n] signer index
+  const uint32_t* prefix;      // [n_signers][8]
+  const uint32_t* araw;        // [n_signers][8] clamped secret scalar
+  const uint32_t* pub;         // [n_signers][8]
+  const uint32_t* btable;
+  uint32_t* sig;               // [16][n_pad] output
+};
+
+extern "C" {
+hipError_t txv_launch_build_tables(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
+                                   uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
+hipError_t txv_launch_verify(const VerifyArgs* args, uint32_t grid, hipStream_t st);
+hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_t* btable, uint32_t* scal,
+                             uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
+hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
+hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,
+                                  hipStream_t st);
+}

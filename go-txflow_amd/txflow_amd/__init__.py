@@ -1,0 +1,418 @@
+"""Python binding of libtxvote.so (include/txvote.h) and a host-side mirror of the
+reference's TxVote admission API (Fantom-foundation/go-txflow):
+
+    TxVote            types/tx_vote.go:48-55   (SignBytes :83-89, Verify :110-119, Size :144-150)
+    TxFlow            txflow/service.go:23-234 (TryAddVote :169-188, addVote :192-234)
+    TxVoteSetView     types/vote_set.go:178-227 readers (Stake, HasTwoThirdsMajority, ...)
+    Errors            types/tx_vote.go:30-35 sentinels + tendermint ErrVoteInvalidValidator*
+
+All verification and tallying runs in the HIP kernels of libtxvote.so; this module only
+marshals arguments.  Importing it on a machine without the built library raises, and
+creating a context without a GPU raises: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libtxvote.so")
+
+# status codes (include/txvote.h)
+ADDED, DUPLICATE, ERR_NIL, ERR_EMPTY_ADDR, ERR_UNKNOWN_VALIDATOR, ERR_NONDETERMINISTIC, \
+    ERR_INVALID_SIGNATURE, ERR_INVALID_VALIDATOR_ADDRESS, ERR_SIGNBYTES = range(9)
+STATUS_FIRED = 0x80
+STATUS_NAMES = {ADDED: "ADDED", DUPLICATE: "DUPLICATE", ERR_NIL: "ErrVoteNil",
+                ERR_EMPTY_ADDR: "ErrVoteInvalidValidatorAddress(empty)",
+                ERR_UNKNOWN_VALIDATOR: "ErrVoteInvalidValidatorIndex",
+                ERR_NONDETERMINISTIC: "ErrVoteNonDeterministicSignature",
+                ERR_INVALID_SIGNATURE: "ErrVoteInvalidSignature",
+                ERR_INVALID_VALIDATOR_ADDRESS: "ErrVoteInvalidValidatorAddress",
+                ERR_SIGNBYTES: "amino time out of range (reference panics)"}
+
+
+class TxVoteError(Exception):
+    """Sentinel-cause error mirroring the reference's error values."""
+
+    def __init__(self, code: int):
+        super().__init__(STATUS_NAMES.get(code & 0x7F, str(code)))
+        self.code = code & 0x7F
+
+
+class TxvInfraError(RuntimeError):
+    pass
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_batch", ctypes.c_uint32), ("max_txs", ctypes.c_uint32),
+                ("max_validators", ctypes.c_uint32), ("max_accepted", ctypes.c_uint32),
+                ("max_msg_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class _Votes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("is_nil", ctypes.c_void_p), ("height", ctypes.c_void_p),
+                ("txhash", ctypes.c_void_p), ("txhash_off", ctypes.c_void_p), ("txhash_len", ctypes.c_void_p),
+                ("ts_sec", ctypes.c_void_p), ("ts_nanos", ctypes.c_void_p), ("addr", ctypes.c_void_p),
+                ("addr_len", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_void_p)]
+
+
+class _Event(ctypes.Structure):
+    _fields_ = [("vote_index", ctypes.c_uint32), ("tx_index", ctypes.c_uint32), ("sum", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TxvInfraError(f"libtxvote.so not built at {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, i32, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64
+        sig = {
+            "txv_init": ([ctypes.POINTER(_Cfg), ctypes.POINTER(vp)], ctypes.c_int),
+            "txv_destroy": ([vp], None),
+            "txv_last_error": ([vp], ctypes.c_char_p),
+            "txv_device_name": ([vp, ctypes.c_char_p, u32], ctypes.c_int),
+            "txv_set_validators": ([vp, vp, vp, u32, ctypes.c_char_p, u32], ctypes.c_int),
+            "txv_get_validator_info": ([vp, vp, vp, u32], ctypes.c_int),
+            "txv_verify_batch": ([vp, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
+            "txv_add_votes": ([vp, ctypes.POINTER(_Votes), vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
+            "txv_query_tx": ([vp, ctypes.c_char_p, u32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_uint8)],
+                             ctypes.c_int),
+            "txv_num_tx_sets": ([vp], u32),
+            "txv_total_power": ([vp], i64),
+            "txv_signbytes": ([i64, ctypes.c_char_p, u32, i64, i32, ctypes.c_char_p, u32, ctypes.c_char_p, u32],
+                              ctypes.c_int),
+            "txv_txvote_size": ([i64, u32, i64, i32, u32, u32], ctypes.c_int),
+            "txv_keygen": ([vp, vp, u32, vp], ctypes.c_int),
+            "txv_sign_votes": ([vp, ctypes.POINTER(_Votes), vp, ctypes.c_char_p, u32, vp], ctypes.c_int),
+            "txv_stage": ([vp, u32, ctypes.POINTER(_Votes)], ctypes.c_int),
+            "txv_run_staged": ([vp, u32, vp], ctypes.c_int),
+            "txv_fetch_staged": ([vp, u32, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
+            "txv_commit_bitmap": ([vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_reset_tally": ([vp], ctypes.c_int),
+            "txv_sync": ([vp], ctypes.c_int),
+            "txv_fe_selftest": ([vp, vp, vp, vp, u32, ctypes.c_int], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = [
+    "txv_init", "txv_destroy", "txv_last_error", "txv_device_name", "txv_set_validators",
+    "txv_get_validator_info", "txv_verify_batch", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
+    "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
+    "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest"]
+
+
+# ------------------------------------------------------------------ host-only helpers
+def sign_bytes(height: int, txhash: bytes, ts_sec: int, ts_nanos: int, chain_id: str) -> bytes:
+    """TxVote.SignBytes(chainID) — types/tx_vote.go:83-89 (amino restatement, host C++)."""
+    out = ctypes.create_string_buffer(2048)
+    cid = chain_id.encode() if isinstance(chain_id, str) else chain_id
+    n = lib().txv_signbytes(height, txhash, len(txhash), ts_sec, ts_nanos, cid, len(cid), out, 2048)
+    if n < 0:
+        raise ValueError("amino: timestamp out of range (reference panics)")
+    return out.raw[:n]
+
+
+def txvote_size(height: int, txhash_len: int, ts_sec: int, ts_nanos: int, addr_len: int, sig_len: int) -> int:
+    """TxVote.Size() — types/tx_vote.go:144-150."""
+    return lib().txv_txvote_size(height, txhash_len, ts_sec, ts_nanos, addr_len, sig_len)
+
+
+# ------------------------------------------------------------------ vote batches
+@dataclass
+class TxVote:
+    """types/tx_vote.go:48-55.  Timestamp as (Unix seconds, nanoseconds)."""
+    Height: int = 0
+    TxHash: str = ""
+    TxKey: bytes = b"\0" * 32
+    Timestamp: tuple = (0, 0)
+    ValidatorAddress: bytes = b""
+    Signature: Optional[bytes] = None
+
+    def SignBytes(self, chain_id: str) -> bytes:
+        return sign_bytes(self.Height, self.TxHash.encode(), self.Timestamp[0], self.Timestamp[1], chain_id)
+
+    def Size(self) -> int:
+        return txvote_size(self.Height, len(self.TxHash), self.Timestamp[0], self.Timestamp[1],
+                           len(self.ValidatorAddress), len(self.Signature or b""))
+
+
+class VoteBatch:
+    """Structure-of-arrays TxVote batch matching txv_votes (include/txvote.h)."""
+
+    def __init__(self, n: int, *, height, txhash_arena, txhash_off, txhash_len, ts_sec, ts_nanos,
+                 addr, addr_len, sig, sig_len, is_nil=None):
+        self.n = int(n)
+        c = np.ascontiguousarray
+        self.height = c(height, dtype=np.int64)
+        self.txhash_arena = c(np.frombuffer(txhash_arena, np.uint8) if isinstance(txhash_arena, (bytes, bytearray))
+                              else txhash_arena, dtype=np.uint8)
+        if self.txhash_arena.size == 0:
+            self.txhash_arena = np.zeros(1, np.uint8)
+        self.txhash_off = c(txhash_off, dtype=np.uint32)
+        self.txhash_len = c(txhash_len, dtype=np.uint32)
+        self.ts_sec = c(ts_sec, dtype=np.int64)
+        self.ts_nanos = c(ts_nanos, dtype=np.int32)
+        self.addr = c(addr, dtype=np.uint8).reshape(-1)
+        self.addr_len = c(addr_len, dtype=np.uint32)
+        self.sig = c(sig, dtype=np.uint8).reshape(-1)
+        self.sig_len = c(sig_len, dtype=np.uint32)
+        self.is_nil = None if is_nil is None else c(is_nil, dtype=np.uint8)
+        assert self.addr.size == 20 * self.n and self.sig.size == 64 * self.n
+
+    @classmethod
+    def from_votes(cls, votes: Sequence[Optional[TxVote]]) -> "VoteBatch":
+        n = len(votes)
+        arena = bytearray()
+        off = np.zeros(n, np.uint32); ln = np.zeros(n, np.uint32)
+        h = np.zeros(n, np.int64); ts = np.zeros(n, np.int64); tn = np.zeros(n, np.int32)
+        addr = np.zeros((n, 20), np.uint8); al = np.zeros(n, np.uint32)
+        sig = np.zeros((n, 64), np.uint8); sl = np.zeros(n, np.uint32)
+        nil = np.zeros(n, np.uint8)
+        for i, v in enumerate(votes):
+            if v is None:
+                nil[i] = 1
+                continue
+            th = v.TxHash.encode() if isinstance(v.TxHash, str) else v.TxHash
+            off[i] = len(arena); ln[i] = len(th); arena += th
+            h[i] = v.Height; ts[i], tn[i] = v.Timestamp
+            a = v.ValidatorAddress or b""
+            al[i] = len(a); addr[i, :min(20, len(a))] = np.frombuffer(a[:20], np.uint8)
+            s = v.Signature or b""
+            sl[i] = len(s); sig[i, :min(64, len(s))] = np.frombuffer(s[:64], np.uint8)
+        return cls(n, height=h, txhash_arena=bytes(arena), txhash_off=off, txhash_len=ln, ts_sec=ts,
+                   ts_nanos=tn, addr=addr, addr_len=al, sig=sig, sig_len=sl, is_nil=nil)
+
+    def c_struct(self) -> _Votes:
+        v = _Votes()
+        v.n = self.n
+        v.is_nil = None if self.is_nil is None else self.is_nil.ctypes.data
+        v.height = self.height.ctypes.data
+        v.txhash = self.txhash_arena.ctypes.data
+        v.txhash_off = self.txhash_off.ctypes.data
+        v.txhash_len = self.txhash_len.ctypes.data
+        v.ts_sec = self.ts_sec.ctypes.data
+        v.ts_nanos = self.ts_nanos.ctypes.data
+        v.addr = self.addr.ctypes.data
+        v.addr_len = self.addr_len.ctypes.data
+        v.sig = self.sig.ctypes.data
+        v.sig_len = self.sig_len.ctypes.data
+        return v
+
+    def txhash(self, i: int) -> bytes:
+        o, l = int(self.txhash_off[i]), int(self.txhash_len[i])
+        return self.txhash_arena[o:o + l].tobytes()
+
+
+# ------------------------------------------------------------------ context
+class Context:
+    """Owns a txv_ctx (one GPU).  Thin wrapper; every call raises on infrastructure errors."""
+
+    def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
+                 max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256):
+        cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes, 0)
+        h = ctypes.c_void_p()
+        rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise TxvInfraError(f"txv_init failed ({rc}): no usable HIP device")
+        self._h = h
+        self.n_vals = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().txv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, rc: int, what: str):
+        if rc < 0:
+            raise TxvInfraError(f"{what} failed ({rc}): {lib().txv_last_error(self._h).decode()}")
+        return rc
+
+    def device_name(self) -> str:
+        buf = ctypes.create_string_buffer(256)
+        self._chk(lib().txv_device_name(self._h, buf, 256), "txv_device_name")
+        return buf.value.decode()
+
+    def set_validators(self, pubs: Sequence[bytes], powers: Sequence[int], chain_id: str):
+        pubs_b = b"".join(pubs)
+        pw = np.ascontiguousarray(np.asarray(powers, dtype=np.int64))
+        cid = chain_id.encode()
+        self._chk(lib().txv_set_validators(self._h, pubs_b, pw.ctypes.data if len(pw) else None, len(pubs),
+                                           cid, len(cid)), "txv_set_validators")
+        self.n_vals = len(pubs)
+
+    def validator_info(self):
+        n = self.n_vals
+        addr = np.zeros((max(n, 1), 20), np.uint8)
+        ok = np.zeros(max(n, 1), np.uint8)
+        self._chk(lib().txv_get_validator_info(self._h, addr.ctypes.data, ok.ctypes.data, n), "info")
+        return [addr[i].tobytes() for i in range(n)], ok[:n].astype(bool)
+
+    def verify_batch(self, batch: VoteBatch, pubs: Optional[np.ndarray] = None) -> np.ndarray:
+        out = np.zeros(max(batch.n, 1), np.uint8)
+        vs = batch.c_struct()
+        pp = None
+        if pubs is not None:
+            pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1)
+            assert pubs.size == 32 * batch.n
+            pp = pubs.ctypes.data
+        self._chk(lib().txv_verify_batch(self._h, ctypes.byref(vs), pp, out.ctypes.data), "txv_verify_batch")
+        return out[:batch.n]
+
+    def add_votes(self, batch: VoteBatch, ev_cap: int = 0):
+        out = np.zeros(max(batch.n, 1), np.uint8)
+        ev_cap = ev_cap or max(batch.n, 1)
+        evs = (_Event * ev_cap)()
+        nev = ctypes.c_uint32()
+        vs = batch.c_struct()
+        self._chk(lib().txv_add_votes(self._h, ctypes.byref(vs), out.ctypes.data, evs, ev_cap, ctypes.byref(nev)),
+                  "txv_add_votes")
+        return out[:batch.n], [(e.vote_index, e.tx_index, e.sum) for e in evs[:min(nev.value, ev_cap)]]
+
+    def query_tx(self, txhash: bytes):
+        s = ctypes.c_int64(); m = ctypes.c_uint8()
+        r = self._chk(lib().txv_query_tx(self._h, txhash, len(txhash), ctypes.byref(s), ctypes.byref(m)), "query")
+        return (s.value, bool(m.value)) if r == 1 else None
+
+    def num_tx_sets(self) -> int:
+        return lib().txv_num_tx_sets(self._h)
+
+    def total_power(self) -> int:
+        return lib().txv_total_power(self._h)
+
+    def keygen(self, seeds: Sequence[bytes]) -> List[bytes]:
+        sb = b"".join(seeds)
+        out = ctypes.create_string_buffer(32 * max(len(seeds), 1))
+        self._chk(lib().txv_keygen(self._h, sb, len(seeds), out), "txv_keygen")
+        return [out.raw[32 * i:32 * i + 32] for i in range(len(seeds))]
+
+    def sign_votes(self, batch: VoteBatch, signer: np.ndarray, chain_id: str) -> np.ndarray:
+        signer = np.ascontiguousarray(signer, dtype=np.uint32)
+        out = np.zeros((max(batch.n, 1), 64), np.uint8)
+        vs = batch.c_struct()
+        cid = chain_id.encode()
+        self._chk(lib().txv_sign_votes(self._h, ctypes.byref(vs), signer.ctypes.data, cid, len(cid), out.ctypes.data),
+                  "txv_sign_votes")
+        return out[:batch.n]
+
+    def stage(self, slot: int, batch: VoteBatch):
+        vs = batch.c_struct()
+        self._chk(lib().txv_stage(self._h, slot, ctypes.byref(vs)), "txv_stage")
+
+    def run_staged(self, slot: int, timed: bool = False):
+        ms = (ctypes.c_float * 3)()
+        self._chk(lib().txv_run_staged(self._h, slot, ms if timed else None), "txv_run_staged")
+        return (ms[0], ms[1], ms[2]) if timed else None
+
+    def fetch_staged(self, slot: int, n: int, ev_cap: int = 0):
+        out = np.zeros(max(n, 1), np.uint8)
+        ev_cap = ev_cap or max(n, 1)
+        evs = (_Event * ev_cap)()
+        nev = ctypes.c_uint32()
+        self._chk(lib().txv_fetch_staged(self._h, slot, out.ctypes.data, evs, ev_cap, ctypes.byref(nev)), "fetch")
+        return out[:n], [(e.vote_index, e.tx_index, e.sum) for e in evs[:min(nev.value, ev_cap)]]
+
+    def commit_bitmap(self):
+        p = ctypes.c_void_p(); nb = ctypes.c_uint64()
+        self._chk(lib().txv_commit_bitmap(self._h, ctypes.byref(p), ctypes.byref(nb)), "bitmap")
+        return p.value, nb.value
+
+    def reset_tally(self):
+        self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")
+
+    def sync(self):
+        self._chk(lib().txv_sync(self._h), "txv_sync")
+
+    def fe_selftest(self, a: np.ndarray, b: np.ndarray, op: int) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint32); b = np.ascontiguousarray(b, dtype=np.uint32)
+        n = a.shape[0]
+        out = np.zeros((n, 8), np.uint32)
+        self._chk(lib().txv_fe_selftest(self._h, a.ctypes.data, b.ctypes.data, out.ctypes.data, n, op), "selftest")
+        return out
+
+
+# ------------------------------------------------------------------ reference-shaped API
+class TxVoteSetView:
+    """Readers of a TxVoteSet (types/vote_set.go:178-227) backed by the device tally."""
+
+    def __init__(self, flow: "TxFlow", txhash: str):
+        self._flow, self.TxHash = flow, txhash
+
+    def _q(self):
+        return self._flow.ctx.query_tx(self.TxHash.encode())
+
+    def Stake(self) -> int:
+        q = self._q()
+        return -1 if q is None else q[0]
+
+    def HasTwoThirdsMajority(self) -> bool:
+        q = self._q()
+        return bool(q and q[1])
+
+    IsCommit = HasTwoThirdsMajority
+
+    def HasTwoThirdsAny(self) -> bool:
+        q = self._q()
+        return bool(q) and q[0] > self._flow.ctx.total_power() * 2 // 3
+
+    def TotalStake(self) -> int:
+        return self._flow.ctx.total_power() * 2 // 3
+
+    def HasAll(self) -> bool:
+        q = self._q()
+        return bool(q) and q[0] == self._flow.ctx.total_power()
+
+
+class TxFlow:
+    """txflow/service.go: TryAddVote/addVote over the GPU tally.  AddVotes is the batched
+    form the single-goroutine checkMaj23Routine (service.go:123-166) becomes."""
+
+    def __init__(self, ctx: Context, pubs: Sequence[bytes], powers: Sequence[int], chain_id: str):
+        self.ctx = ctx
+        self.chain_id = chain_id
+        ctx.set_validators(pubs, powers, chain_id)
+        self.commits: List[tuple] = []
+
+    def AddVotes(self, votes: Sequence[Optional[TxVote]]):
+        batch = VoteBatch.from_votes(votes)
+        status, events = self.ctx.add_votes(batch)
+        for vi, _ti, s in events:
+            self.commits.append((votes[vi].TxHash, s))
+        return status
+
+    def TryAddVote(self, vote: TxVote):
+        """(added, err) like service.go:169-188 (err carries the sentinel cause)."""
+        st = int(self.AddVotes([vote])[0])
+        code = st & 0x7F
+        if code in (ADDED,):
+            return True, None
+        if code == DUPLICATE:
+            return False, None
+        return False, TxVoteError(code)
+
+    def TxVoteSet(self, txhash: str) -> Optional[TxVoteSetView]:
+        return TxVoteSetView(self, txhash) if self.ctx.query_tx(txhash.encode()) is not None else None
+
+
+def verify(ctx: Context, vote: TxVote, chain_id_unused: str, pub: bytes):
+    """TxVote.Verify(chainID, pubKey) (types/tx_vote.go:110-119) for one vote; the chain id of
+    the context is used.  Returns None or a TxVoteError."""
+    b = VoteBatch.from_votes([vote])
+    st = int(ctx.verify_batch(b, np.frombuffer(pub, np.uint8).reshape(1, 32))[0])
+    return None if st == ADDED else TxVoteError(st)

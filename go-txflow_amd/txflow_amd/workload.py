@@ -1,0 +1,83 @@
+"""Synthetic TxVote workloads of BASELINE.json / SURVEY.md §8d (deterministic by seed).
+
+    chainID "test_chain_id", Height 1, Timestamp = 1.7e9 s + (i+1) ns (non-zero nanos),
+    tx_j = le64(j) || 24 PRNG bytes, TxHash = upper-hex(SHA-256(tx_j))  (types/tx_vote.go:43-45),
+    validator seeds = SHA-512("txflow-val" || le32(i))[:32], keys derived on the GPU (RFC 8032).
+Signatures are produced by the device signer (txv_sign_votes, mirroring MockPV.SignTxVote,
+types/priv_validator.go:83-95).  The PRNG is numpy PCG64 seeded with the config seed.
+"""
+from __future__ import annotations
+
+import hashlib
+import struct
+
+import numpy as np
+
+from . import Context, VoteBatch
+
+CHAIN_ID = "test_chain_id"
+SEEDS = {"c1": 0x7478763031, "c2": 0x7478763032, "c3": 0x7478763033, "c4": 0x7478763034, "c5": 0x7478763035}
+
+
+def validator_seeds(n: int, offset: int = 0):
+    return [hashlib.sha512(b"txflow-val" + struct.pack("<I", offset + i)).digest()[:32] for i in range(n)]
+
+
+def tx_hashes(n_txs: int, rng: np.random.Generator, first: int = 0) -> np.ndarray:
+    """[n_txs, 64] uint8 upper-hex TxHash strings."""
+    tail = rng.integers(0, 256, size=(n_txs, 24), dtype=np.uint8)
+    out = np.zeros((n_txs, 64), np.uint8)
+    for j in range(n_txs):
+        tx = struct.pack("<Q", first + j) + tail[j].tobytes()
+        out[j] = np.frombuffer(hashlib.sha256(tx).hexdigest().upper().encode(), np.uint8)
+    return out
+
+
+class Workload:
+    """Every validator votes every tx (C1/C2/C3 shape), arrival order shuffled."""
+
+    def __init__(self, ctx: Context, n_vals: int, n_txs: int, seed: int, powers=None, shard=None, n_shards=1,
+                 tx_first: int = 0):
+        self.rng = np.random.default_rng(seed)
+        self.n_vals, self.n_txs = n_vals, n_txs
+        self.seeds = validator_seeds(n_vals)
+        self.pubs = ctx.keygen(self.seeds)
+        self.powers = np.ones(n_vals, np.int64) if powers is None else np.asarray(powers, np.int64)
+        ctx.set_validators(self.pubs, self.powers, CHAIN_ID)
+        addrs, ok = ctx.validator_info()
+        assert ok.all()
+        self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(n_vals, 20)
+        hashes = tx_hashes(n_txs, self.rng, tx_first)
+        if n_shards > 1:
+            # shard = SHA-256(TxHash)[0] mod G
+            keep = np.array([hashlib.sha256(h.tobytes()).digest()[0] % n_shards == shard for h in hashes])
+            hashes = hashes[keep]
+        self.hashes = hashes
+        self.n_txs = len(hashes)
+        n = self.n_txs * n_vals
+        tx_of = np.repeat(np.arange(self.n_txs, dtype=np.uint32), n_vals)
+        val_of = np.tile(np.arange(n_vals, dtype=np.uint32), self.n_txs)
+        perm = self.rng.permutation(n)
+        self.tx_of, self.val_of = tx_of[perm], val_of[perm]
+        self.n = n
+        self.batch = VoteBatch(
+            n, height=np.ones(n, np.int64), txhash_arena=self.hashes.reshape(-1),
+            txhash_off=self.tx_of.astype(np.uint32) * 64, txhash_len=np.full(n, 64, np.uint32),
+            ts_sec=np.full(n, 1_700_000_000, np.int64), ts_nanos=(np.arange(n, dtype=np.int64) % 999_999_999 + 1),
+            addr=self.addrs[self.val_of], addr_len=np.full(n, 20, np.uint32),
+            sig=np.zeros((n, 64), np.uint8), sig_len=np.full(n, 64, np.uint32))
+        chunk = 1 << 18
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            sub = VoteBatch(e - s, height=self.batch.height[s:e], txhash_arena=self.batch.txhash_arena,
+                            txhash_off=self.batch.txhash_off[s:e], txhash_len=self.batch.txhash_len[s:e],
+                            ts_sec=self.batch.ts_sec[s:e], ts_nanos=self.batch.ts_nanos[s:e],
+                            addr=self.batch.addr[20 * s:20 * e], addr_len=self.batch.addr_len[s:e],
+                            sig=self.batch.sig[64 * s:64 * e], sig_len=self.batch.sig_len[s:e])
+            self.batch.sig[64 * s:64 * e] = ctx.sign_votes(sub, self.val_of[s:e], CHAIN_ID).reshape(-1)
+
+    def vote(self, i: int) -> dict:
+        """oracle-style dict of vote i"""
+        return dict(height=1, txhash=self.batch.txhash(i), ts_sec=int(self.batch.ts_sec[i]),
+                    ts_nanos=int(self.batch.ts_nanos[i]), addr=self.batch.addr[20 * i:20 * i + 20].tobytes(),
+                    sig=self.batch.sig[64 * i:64 * i + 64].tobytes())

@@ -1,0 +1,167 @@
+/*
+ * txvote.h — C ABI of libtxvote.so, the MI355X-native TxVote admission path of go-txflow.
+ *
+ * This is the drop-in boundary: every entry point is what the reference's Go code would
+ * bind through cgo for this path (the binding is shown in INTEGRATION.md).  Plain
+ * pointers and sizes only; no HIP or torch types.  Caller buffers are read/written only
+ * during the call (cgo pointer rules); the library copies into its own pinned host and
+ * device buffers.  Return value: TXV_OK or a negative infrastructure error; per-vote
+ * verdicts are never reported through the return value.
+ *
+ * Reference interfaces replaced (file:line in Fantom-foundation/go-txflow):
+ *   txv_verify_batch   <- func (vote *TxVote) Verify(chainID string, pubKey crypto.PubKey) error
+ *                         types/tx_vote.go:110-119  (ed25519 via tendermint VerifyBytes, :115)
+ *   txv_add_votes      <- func (txR *TxFlow) TryAddVote(vote *types.TxVote) (bool, error)
+ *                         txflow/service.go:169-188 -> addVote :192-234
+ *                         -> func (voteSet *TxVoteSet) AddVote(vote *TxVote) (bool, error)
+ *                         types/vote_set.go:81-131, addVerifiedVote :143-166
+ *   txv_query_tx       <- TxVoteSet.Stake / HasTwoThirdsMajority / HasTwoThirdsAny / HasAll
+ *                         types/vote_set.go:178-227
+ *   txv_set_validators <- NewTxVoteSet(chainID, height, txHash, txKey, valSet)
+ *                         types/vote_set.go:34-51 (state.ChainID / state.Validators, txflow/service.go:200-209)
+ *   txv_signbytes      <- func (vote *TxVote) SignBytes(chainID string) []byte   types/tx_vote.go:83-89
+ *   txv_txvote_size    <- func (vote *TxVote) Size() int                         types/tx_vote.go:144-150
+ *   txv_keygen/txv_sign_votes <- MockPV.SignTxVote types/priv_validator.go:83-95 (load generator)
+ */
+#ifndef TXVOTE_H
+#define TXVOTE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TXV_ABI_VERSION 1
+
+/* ---- return codes (infrastructure) ---- */
+#define TXV_OK 0
+#define TXV_EINVAL (-22)
+#define TXV_ENOMEM (-12)
+#define TXV_EDEVICE (-5)      /* HIP error or no device */
+#define TXV_ECAPACITY (-28)   /* configured capacity exceeded */
+#define TXV_ESTATE (-1)       /* call order (e.g. no validator set) */
+
+/* ---- per-vote status codes (status_out low 7 bits) ----
+ * Mirror the (added, err) results of TxVoteSet.AddVote / TxVote.Verify:
+ *   TXV_ADDED                 (true, nil)
+ *   TXV_DUPLICATE             (false, nil)                            vote_set.go:110-111
+ *   TXV_ERR_NIL               ErrVoteNil                              vote_set.go:93-95
+ *   TXV_ERR_EMPTY_ADDR        ErrVoteInvalidValidatorAddress "Empty"  vote_set.go:97-99
+ *   TXV_ERR_UNKNOWN_VALIDATOR ErrVoteInvalidValidatorIndex            vote_set.go:102-106
+ *   TXV_ERR_NONDETERMINISTIC  ErrVoteNonDeterministicSignature        vote_set.go:112-113
+ *   TXV_ERR_INVALID_SIGNATURE ErrVoteInvalidSignature                 tx_vote.go:115-117
+ *   TXV_ERR_INVALID_VALIDATOR_ADDRESS ErrVoteInvalidValidatorAddress  tx_vote.go:111-113 (Verify only)
+ *   TXV_ERR_SIGNBYTES         amino rejects the timestamp: the reference panics in SignBytes
+ * Bit 7 (TXV_STATUS_FIRED) is set when the reference would run its commit side effects for
+ * this vote: added && HasTwoThirdsMajority() (txflow/service.go:216), which re-fires on every
+ * later added vote of a committed tx. */
+#define TXV_ADDED 0
+#define TXV_DUPLICATE 1
+#define TXV_ERR_NIL 2
+#define TXV_ERR_EMPTY_ADDR 3
+#define TXV_ERR_UNKNOWN_VALIDATOR 4
+#define TXV_ERR_NONDETERMINISTIC 5
+#define TXV_ERR_INVALID_SIGNATURE 6
+#define TXV_ERR_INVALID_VALIDATOR_ADDRESS 7
+#define TXV_ERR_SIGNBYTES 8
+#define TXV_STATUS_FIRED 0x80
+
+typedef struct txv_ctx txv_ctx;
+
+typedef struct {
+  int32_t  device;          /* HIP device ordinal; -1 = current device */
+  uint32_t max_batch;       /* votes per call (default 1<<20) */
+  uint32_t max_txs;         /* TxVoteSets capacity (default 1<<20) */
+  uint32_t max_validators;  /* default 1024 */
+  uint32_t max_accepted;    /* accepted-signature arena capacity (default max_txs * 128) */
+  uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
+  uint32_t flags;           /* reserved, 0 */
+} txv_config;
+
+/* A batch of TxVotes (types/tx_vote.go:48-55) in structure-of-arrays form. */
+typedef struct {
+  uint32_t n;
+  const uint8_t*  is_nil;      /* [n] or NULL: 1 = nil *TxVote */
+  const int64_t*  height;      /* [n] Height */
+  const uint8_t*  txhash;      /* TxHash string bytes, arena */
+  const uint32_t* txhash_off;  /* [n] */
+  const uint32_t* txhash_len;  /* [n] */
+  const int64_t*  ts_sec;      /* [n] Timestamp: Unix seconds */
+  const int32_t*  ts_nanos;    /* [n] Timestamp: nanoseconds [0, 1e9) */
+  const uint8_t*  addr;        /* [n][20] ValidatorAddress bytes */
+  const uint32_t* addr_len;    /* [n] len(ValidatorAddress) (0 = empty) */
+  const uint8_t*  sig;         /* [n][64] Signature bytes (first 64) */
+  const uint32_t* sig_len;     /* [n] len(Signature) */
+} txv_votes;
+
+typedef struct {
+  uint32_t vote_index;   /* index in the batch of the vote whose addition crossed 2/3 */
+  uint32_t tx_index;     /* internal tx-set id */
+  int64_t  sum;          /* stake of the set after the batch */
+} txv_commit_event;
+
+int  txv_init(const txv_config* cfg, txv_ctx** out);
+void txv_destroy(txv_ctx* ctx);
+const char* txv_last_error(txv_ctx* ctx);
+int  txv_device_name(txv_ctx* ctx, char* buf, uint32_t cap);
+
+/* Validator set + chain id.  pubs32: n x 32-byte ed25519 keys; powers: VotingPower.
+ * Builds the per-validator tables on the device (K0).  Resets all tally state. */
+int txv_set_validators(txv_ctx* ctx, const uint8_t* pubs32, const int64_t* powers, uint32_t n,
+                       const char* chain_id, uint32_t chain_len);
+/* addresses (n x 20, SHA-256(pub)[:20] computed on device) and decode flags of the set */
+int txv_get_validator_info(txv_ctx* ctx, uint8_t* addr20_out, uint8_t* decode_ok_out, uint32_t cap);
+
+/* TxVote.Verify(chainID, pubKey) for each vote.  pubs32: n x 32 caller-supplied keys, or NULL
+ * to use the registry key whose address equals the vote's ValidatorAddress.  status_out:
+ * TXV_ADDED (= nil error) / TXV_ERR_INVALID_VALIDATOR_ADDRESS / TXV_ERR_INVALID_SIGNATURE /
+ * TXV_ERR_SIGNBYTES (and TXV_ERR_UNKNOWN_VALIDATOR when pubs32 == NULL and no key matches). */
+int txv_verify_batch(txv_ctx* ctx, const txv_votes* votes, const uint8_t* pubs32, uint8_t* status_out);
+
+/* TxFlow.TryAddVote for each vote in arrival order (votes[0] first).  Semantics are exactly
+ * the sequential loop's; see SURVEY.md Appendix A.3.  ev_out (capacity ev_cap) receives one
+ * event per tx whose 2/3 crossing happened in this batch; *n_ev its count. */
+int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
+                  txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev);
+
+/* Tally readers for the TxVoteSet of txhash.  Returns 1 if the set exists, 0 if not. */
+int txv_query_tx(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23);
+uint32_t txv_num_tx_sets(txv_ctx* ctx);
+int64_t  txv_total_power(txv_ctx* ctx);
+
+/* amino encodings (host, no device work) */
+int txv_signbytes(int64_t height, const uint8_t* txhash, uint32_t txhash_len, int64_t ts_sec,
+                  int32_t ts_nanos, const char* chain_id, uint32_t chain_len, uint8_t* out, uint32_t cap);
+int txv_txvote_size(int64_t height, uint32_t txhash_len, int64_t ts_sec, int32_t ts_nanos,
+                    uint32_t addr_len, uint32_t sig_len);
+
+/* ---- load generator (device signing, RFC 8032 deterministic) ---- */
+/* seeds: n x 32 bytes -> pubs n x 32 bytes.  Keys are retained in ctx as signer slots. */
+int txv_keygen(txv_ctx* ctx, const uint8_t* seeds32, uint32_t n, uint8_t* pubs_out);
+/* Signs SignBytes(chain_id) of each vote with signer slot signer[i]; writes sig_out n x 64. */
+int txv_sign_votes(txv_ctx* ctx, const txv_votes* votes, const uint32_t* signer, const char* chain_id,
+                   uint32_t chain_len, uint8_t* sig_out);
+
+/* ---- device-resident batches (benchmark / pipelined ingest) ----
+ * txv_stage: pack + upload a batch into device slot `slot` (host work + H2D, not timed).
+ * txv_run_staged: run verify + tally on the staged batch entirely on device; results stay
+ *   on device until txv_fetch_staged.  kernel_ms_out (optional, 3 entries): verify / tally /
+ *   total device time of this run measured with HIP events on the stream the kernels run on. */
+int txv_stage(txv_ctx* ctx, uint32_t slot, const txv_votes* votes);
+int txv_run_staged(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
+int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commit_event* ev_out,
+                     uint32_t ev_cap, uint32_t* n_ev);
+/* device pointer + byte size of the per-set committed bitmap (1 bit per tx-set id) */
+int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
+/* reset tally state (all TxVoteSets) keeping the validator set */
+int txv_reset_tally(txv_ctx* ctx);
+int txv_sync(txv_ctx* ctx);
+
+/* ---- self-test hook: field/scalar ops on device (tests only) ---- */
+int txv_fe_selftest(txv_ctx* ctx, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

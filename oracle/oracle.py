@@ -1,0 +1,207 @@
+"""ctypes binding to the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, always as the checker.  The product (go-txflow_amd/) never imports it.
+See oracle.h for the reference file:line each function restates.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+ADDED, DUPLICATE, ERR_NIL, ERR_EMPTY_ADDR, ERR_UNKNOWN_VALIDATOR, ERR_NONDETERMINISTIC, \
+    ERR_INVALID_SIGNATURE, ERR_INVALID_VALIDATOR_ADDRESS, ERR_SIGNBYTES = range(9)
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c_u8p = ctypes.c_char_p
+        L.orc_sha512.argtypes = [c_u8p, ctypes.c_size_t, ctypes.c_char_p]
+        L.orc_sha256.argtypes = [c_u8p, ctypes.c_size_t, ctypes.c_char_p]
+        L.orc_ed25519_verify.argtypes = [c_u8p, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t]
+        L.orc_ed25519_verify.restype = ctypes.c_int
+        L.orc_ed25519_pubkey.argtypes = [c_u8p, ctypes.c_char_p]
+        L.orc_ed25519_sign.argtypes = [c_u8p, c_u8p, ctypes.c_size_t, ctypes.c_char_p]
+        L.orc_ed25519_decode_ok.argtypes = [c_u8p]
+        L.orc_sc_reduce64.argtypes = [c_u8p, ctypes.c_char_p]
+        L.orc_sc_minimal.argtypes = [c_u8p]
+        L.orc_scalarmult.argtypes = [c_u8p, c_u8p, ctypes.c_char_p]
+        L.orc_scalarmult_base.argtypes = [c_u8p, ctypes.c_char_p]
+        L.orc_point_canonical.argtypes = [c_u8p, ctypes.c_char_p]
+        L.orc_signbytes.argtypes = [ctypes.c_int64, c_u8p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int32,
+                                    c_u8p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_txvote_size.argtypes = [ctypes.c_int64, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_size_t, ctypes.c_size_t]
+        L.orc_flow_new.restype = ctypes.c_void_p
+        L.orc_flow_new.argtypes = [c_u8p, ctypes.c_void_p, ctypes.c_uint32, c_u8p, ctypes.c_size_t]
+        L.orc_flow_free.argtypes = [ctypes.c_void_p]
+        L.orc_flow_add_votes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_flow_query.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
+        L.orc_flow_num_sets.argtypes = [ctypes.c_void_p]
+        L.orc_flow_num_sets.restype = ctypes.c_uint32
+        L.orc_flow_num_verifies.argtypes = [ctypes.c_void_p]
+        L.orc_flow_num_verifies.restype = ctypes.c_uint64
+        L.orc_verify_many.restype = ctypes.c_double
+        L.orc_verify_many.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def sha512(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    lib().orc_sha512(b, len(b), out)
+    return out.raw
+
+
+def sha256(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_sha256(b, len(b), out)
+    return out.raw
+
+
+def verify(pub: bytes, msg: bytes, sig: bytes) -> bool:
+    assert len(pub) == 32
+    return bool(lib().orc_ed25519_verify(pub, msg, len(msg), sig, len(sig)))
+
+
+def pubkey(seed: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_ed25519_pubkey(seed, out)
+    return out.raw
+
+
+def sign(seed: bytes, msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    lib().orc_ed25519_sign(seed, msg, len(msg), out)
+    return out.raw
+
+
+def decode_ok(pub: bytes) -> bool:
+    return bool(lib().orc_ed25519_decode_ok(pub))
+
+
+def sc_reduce64(h: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_sc_reduce64(h, out)
+    return out.raw
+
+
+def sc_minimal(s: bytes) -> bool:
+    return bool(lib().orc_sc_minimal(s))
+
+
+def scalarmult(k: bytes, p: bytes):
+    out = ctypes.create_string_buffer(32)
+    return out.raw if lib().orc_scalarmult(k, p, out) else None
+
+
+def scalarmult_base(k: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_scalarmult_base(k, out)
+    return out.raw
+
+
+def point_canonical(p: bytes):
+    out = ctypes.create_string_buffer(32)
+    return out.raw if lib().orc_point_canonical(p, out) else None
+
+
+def signbytes(height: int, txhash: bytes, ts_sec: int, ts_nanos: int, chain_id: bytes):
+    out = ctypes.create_string_buffer(2048)
+    n = lib().orc_signbytes(height, txhash, len(txhash), ts_sec, ts_nanos, chain_id, len(chain_id), out, 2048)
+    return None if n < 0 else out.raw[:n]
+
+
+def txvote_size(height, txhash_len, ts_sec, ts_nanos, addr_len, sig_len) -> int:
+    return lib().orc_txvote_size(height, txhash_len, ts_sec, ts_nanos, addr_len, sig_len)
+
+
+class _Vote(ctypes.Structure):
+    _fields_ = [("is_nil", ctypes.c_int32), ("height", ctypes.c_int64),
+                ("txhash", ctypes.c_void_p), ("txhash_len", ctypes.c_uint32),
+                ("ts_sec", ctypes.c_int64), ("ts_nanos", ctypes.c_int32),
+                ("addr", ctypes.c_void_p), ("addr_len", ctypes.c_uint32),
+                ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_uint32)]
+
+
+class Flow:
+    """Sequential TxFlow.addVote/TxVoteSet.AddVote restatement (txflow/service.go:192-234,
+    types/vote_set.go:81-166).  votes: list of dicts with keys
+    nil, height, txhash (bytes), ts_sec, ts_nanos, addr (bytes), sig (bytes)."""
+
+    def __init__(self, pubs, powers, chain_id: bytes):
+        import numpy as np
+        self._np = np
+        L = lib()
+        pw = np.ascontiguousarray(np.asarray(powers, dtype=np.int64))
+        self._h = L.orc_flow_new(b"".join(pubs), pw.ctypes.data, len(pubs), chain_id, len(chain_id))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_flow_free(self._h)
+            self._h = None
+
+    def add_votes(self, votes, verdicts=None):
+        np = self._np
+        n = len(votes)
+        arr = (_Vote * max(n, 1))()
+        keep = []
+        for i, v in enumerate(votes):
+            if v.get("nil"):
+                arr[i].is_nil = 1
+                continue
+            bufs = [ctypes.create_string_buffer(bytes(v[k]) or b"\0", max(len(v[k]), 1))
+                    for k in ("txhash", "addr", "sig")]
+            keep.append(bufs)
+            arr[i].is_nil = 0
+            arr[i].height = v.get("height", 0)
+            arr[i].txhash = ctypes.addressof(bufs[0]); arr[i].txhash_len = len(v["txhash"])
+            arr[i].ts_sec = v.get("ts_sec", 0); arr[i].ts_nanos = v.get("ts_nanos", 0)
+            arr[i].addr = ctypes.addressof(bufs[1]); arr[i].addr_len = len(v["addr"])
+            arr[i].sig = ctypes.addressof(bufs[2]); arr[i].sig_len = len(v["sig"])
+        status = np.zeros(max(n, 1), np.uint8)
+        sums = np.zeros(max(n, 1), np.int64)
+        fired = np.zeros(max(n, 1), np.uint8)
+        vp = None
+        if verdicts is not None:
+            vd = np.ascontiguousarray(np.asarray(verdicts, dtype=np.uint8))
+            vp = vd.ctypes.data
+        lib().orc_flow_add_votes(self._h, ctypes.addressof(arr), n, vp, status.ctypes.data,
+                                 sums.ctypes.data, fired.ctypes.data)
+        return status[:n], sums[:n], fired[:n]
+
+    def query(self, txhash: bytes):
+        s = ctypes.c_int64(); m = ctypes.c_int32()
+        ok = lib().orc_flow_query(self._h, txhash, len(txhash), ctypes.byref(s), ctypes.byref(m))
+        return (s.value, bool(m.value)) if ok else None
+
+    def num_sets(self):
+        return lib().orc_flow_num_sets(self._h)
+
+    def num_verifies(self):
+        return lib().orc_flow_num_verifies(self._h)
+
+
+def verify_many(pubs32, val_idx, arena, msg_off, msg_len, sigs64, threads=1):
+    """Timed CPU verify (bench cpu_baseline).  Returns (seconds, ok uint8 array)."""
+    import numpy as np
+    n = len(val_idx)
+    out = np.zeros(n, np.uint8)
+    arrs = [np.ascontiguousarray(a) for a in (pubs32, val_idx.astype(np.uint32), arena,
+                                              msg_off.astype(np.uint32), msg_len.astype(np.uint16), sigs64)]
+    t = lib().orc_verify_many(*[a.ctypes.data for a in arrs], n, threads, out.ctypes.data)
+    return t, out

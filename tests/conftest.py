@@ -1,0 +1,30 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "go-txflow_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"),
+          os.path.join(ROOT, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libtxvote.so")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256)
+    yield ctx
+    ctx.close()

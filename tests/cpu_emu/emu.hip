@@ -1,0 +1,94 @@
+// emu.hip — TEST-ONLY host emulation of the device math in go-txflow_amd/csrc.
+//
+// Compiles the very same __host__ __device__ headers (fe.h, sc.h, sha2.h, ge.h,
+// ed25519_dev.h) for the host so logic errors in the kernel source can be localised on a
+// machine without a GPU.  It is not linked into libtxvote.so and the product never calls it.
+#include "../../go-txflow_amd/csrc/ed25519_dev.h"
+#include <cstring>
+#include <vector>
+
+using namespace txv;
+
+static void build_table(std::vector<uint32_t>& tab, const uint32_t w[8], bool* ok_out) {
+  tab.assign(kTableWords, 0);
+  ge_ext A;
+  bool ok = ge_decode(A, w);
+  if (ok_out) *ok_out = ok;
+  for (int pos = 0; pos < 64; ++pos) {
+    ge_ext P = A;
+    for (int i = 0; i < 4 * pos; ++i) P = ge_dbl(P);
+    ge_ext M[8];
+    M[0] = P;
+    M[1] = ge_dbl(P);
+    for (int j = 2; j < 8; ++j) M[j] = ge_add(M[j - 1], P);
+    uint32_t* out = tab.data() + pos * kTabEntries * kEntryWords;
+    for (int j = 0; j < 8; ++j) {
+      ge_niels n = ge_to_niels(M[j], fe_invert(M[j].Z));
+      uint32_t* e = out + (j + 1) * kEntryWords;
+      for (int i = 0; i < 8; ++i) { e[i] = n.ypx.v[i]; e[8 + i] = n.ymx.v[i]; e[16 + i] = n.xy2d.v[i]; }
+    }
+    for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;
+  }
+}
+
+extern "C" {
+
+int emu_fe(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
+  fe x, y, r;
+  for (int j = 0; j < 8; ++j) { x.v[j] = a[j]; y.v[j] = b[j]; }
+  switch (op) {
+    case 0: r = fe_mul(x, y); break;
+    case 1: r = fe_sq(x); break;
+    case 2: r = fe_add(x, y); break;
+    case 3: r = fe_sub(x, y); break;
+    case 4: r = fe_canon(x); break;
+    case 5: r = fe_invert(x); break;
+    default: {
+      uint32_t t[16];
+      for (int j = 0; j < 8; ++j) { t[j] = x.v[j]; t[8 + j] = y.v[j]; }
+      sc s = sc_reduce512(t);
+      for (int j = 0; j < 8; ++j) r.v[j] = s.v[j];
+    }
+  }
+  for (int j = 0; j < 8; ++j) out[j] = r.v[j];
+  return 0;
+}
+
+// kernel-K1 logic for one vote; msg given as raw bytes
+int emu_verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const uint8_t* sig, uint32_t sig_len) {
+  static std::vector<uint32_t> btab;
+  if (btab.empty()) {
+    uint32_t bw[8];
+    base_point_words(bw);
+    build_table(btab, bw, nullptr);
+  }
+  if (sig_len != 64) return 0;
+  uint32_t s[16], pw[8];
+  memcpy(s, sig, 64);
+  memcpy(pw, pub, 32);
+  std::vector<uint32_t> atab;
+  bool dok;
+  build_table(atab, pw, &dok);
+  if ((s[15] & 0xE0000000u) || !dok || !sc_lt_L(s + 8)) return 0;
+  uint64_t pre[8];
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = be64_from_le32(s[2 * j], s[2 * j + 1]);
+    pre[4 + j] = be64_from_le32(pw[2 * j], pw[2 * j + 1]);
+  }
+  const uint32_t nw = (len + 7) / 8;
+  std::vector<uint64_t> words(nw + 1, 0);
+  for (uint32_t i = 0; i < len; ++i) words[i / 8] |= (uint64_t)msg[i] << (56 - 8 * (i % 8));
+  MsgView m{words.data(), 1, nw, len};
+  uint32_t dig[16];
+  sha512_prefixed(dig, pre, 8, m);
+  sc k = sc_reduce512(dig);
+  uint32_t sp[8], kp[8];
+  sc_recode16(sp, s + 8);
+  sc_recode16(kp, k.v);
+  ge_ext R = double_scalarmult_fixed(btab.data(), atab.data(), sp, kp, true);
+  uint32_t enc[8];
+  ge_encode(enc, R);
+  return memcmp(enc, s, 32) == 0;
+}
+
+}  // extern "C"

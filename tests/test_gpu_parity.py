@@ -1,0 +1,223 @@
+"""GPU parity tests: libtxvote.so (HIP, gfx950) against the CPU oracle on identical inputs.
+
+Bit-exact for every integer/byte result: field and scalar ops, public keys, signatures,
+per-vote accept/reject, per-vote (added, err) codes incl. the commit-fire bit, per-tx sums."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+P = 2 ** 255 - 19
+L = 2 ** 252 + 27742317777372353535851937790883648493
+
+
+def to_words(x: int) -> list:
+    return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+
+
+def from_words(w) -> int:
+    return sum(int(v) << (32 * i) for i, v in enumerate(w))
+
+
+def _edge_values():
+    vals = [0, 1, 2, 19, 38, P - 1, P, P + 1, P + 18, 2 ** 255 - 1, 2 ** 255, 2 ** 256 - 1, 2 ** 256 - 38,
+            2 ** 256 - 39, 2 ** 32 - 1, 2 ** 64 - 1, 2 ** 224, (2 ** 256 - 1) // 3]
+    return vals
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4, 5])
+def test_field_ops_bit_exact(gpu_ctx, op):
+    rnd = random.Random(op)
+    A = _edge_values() + [rnd.getrandbits(256) for _ in range(2000)]
+    B = list(reversed(_edge_values())) + [rnd.getrandbits(256) for _ in range(2000)]
+    a = np.array([to_words(x) for x in A], np.uint32)
+    b = np.array([to_words(x) for x in B], np.uint32)
+    out = gpu_ctx.fe_selftest(a, b, op)
+    for x, y, w in zip(A, B, out):
+        r = from_words(w)
+        assert r < 2 ** 256
+        if op == 0:
+            exp = x * y % P
+        elif op == 1:
+            exp = x * x % P
+        elif op == 2:
+            exp = (x + y) % P
+        elif op == 3:
+            exp = (x - y) % P
+        elif op == 4:
+            exp = x % P
+            assert r == exp  # canonical
+        else:
+            exp = pow(x, P - 2, P)
+        assert r % P == exp, (op, hex(x), hex(y), hex(r))
+
+
+def test_scalar_reduce_bit_exact(gpu_ctx):
+    rnd = random.Random(7)
+    X = [rnd.getrandbits(512) for _ in range(3000)] + [0, L, L - 1, 2 * L, 2 ** 512 - 1, L * (2 ** 259)]
+    a = np.array([to_words(x & (2 ** 256 - 1)) for x in X], np.uint32)
+    b = np.array([to_words(x >> 256) for x in X], np.uint32)
+    out = gpu_ctx.fe_selftest(a, b, 6)
+    for x, w in zip(X, out):
+        assert from_words(w) == x % L
+
+
+def test_keygen_matches_oracle(gpu_ctx, oracle_lib):
+    rnd = random.Random(3)
+    seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(64)]
+    pubs = gpu_ctx.keygen(seeds)
+    for s, p in zip(seeds, pubs):
+        assert p == oracle_lib.pubkey(s)
+
+
+def _mini_votes(T, n, rnd, chain_len_var=False):
+    votes = []
+    for i in range(n):
+        h = "".join(rnd.choice("0123456789ABCDEF") for _ in range(64 if i % 7 else rnd.randrange(0, 300)))
+        votes.append(T.TxVote(Height=rnd.choice([0, 1, 5, -3, 2 ** 40]), TxHash=h,
+                              Timestamp=(rnd.choice([1_700_000_000, 0, -5, 253402300799]), rnd.randrange(0, 10 ** 9)),
+                              ValidatorAddress=b"", Signature=b""))
+    return votes
+
+
+def test_sign_matches_oracle(gpu_ctx, oracle_lib):
+    import txflow_amd as T
+    rnd = random.Random(11)
+    seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(8)]
+    pubs = gpu_ctx.keygen(seeds)
+    votes = _mini_votes(T, 300, rnd)
+    batch = T.VoteBatch.from_votes(votes)
+    signer = np.array([rnd.randrange(8) for _ in votes], np.uint32)
+    sigs = gpu_ctx.sign_votes(batch, signer, "test_chain_id")
+    for i, v in enumerate(votes):
+        msg = oracle_lib.signbytes(v.Height, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], b"test_chain_id")
+        assert msg is not None
+        assert sigs[i].tobytes() == oracle_lib.sign(seeds[signer[i]], msg), i
+
+
+def test_signbytes_host_encoder_matches_oracle(oracle_lib):
+    import txflow_amd as T
+    rnd = random.Random(5)
+    for _ in range(500):
+        h = bytes(rnd.choice(b"0123456789ABCDEF") for _ in range(rnd.choice([0, 1, 64, 127, 128, 300])))
+        height = rnd.choice([0, 1, -1, 2 ** 63 - 1, -2 ** 63, 12345])
+        sec = rnd.choice([0, 1, -1, 1_700_000_000, -62135596800, 253402300799, -62135596801, 253402300800])
+        nanos = rnd.choice([0, 1, 999_999_999, 2 ** 28, 2 ** 28 - 1])
+        chain = rnd.choice([b"", b"test_chain_id", b"x" * 200])
+        exp = oracle_lib.signbytes(height, h, sec, nanos, chain)
+        try:
+            got = T.sign_bytes(height, h, sec, nanos, chain)
+        except ValueError:
+            got = None
+        assert got == exp
+
+
+def _signed_set(gpu_ctx, T, n_vals, n_votes, rnd, n_txs=None):
+    seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(n_vals)]
+    pubs = gpu_ctx.keygen(seeds)
+    gpu_ctx.set_validators(pubs, [1 + (i % 3) for i in range(n_vals)], "test_chain_id")
+    addrs, ok = gpu_ctx.validator_info()
+    assert ok.all()
+    n_txs = n_txs or max(1, n_votes // n_vals)
+    hashes = ["".join(rnd.choice("0123456789ABCDEF") for _ in range(64)) for _ in range(n_txs)]
+    votes, signer = [], []
+    for i in range(n_votes):
+        vi = rnd.randrange(n_vals)
+        votes.append(T.TxVote(Height=1, TxHash=rnd.choice(hashes), Timestamp=(1_700_000_000, i + 1),
+                              ValidatorAddress=addrs[vi], Signature=b""))
+        signer.append(vi)
+    b = T.VoteBatch.from_votes(votes)
+    sigs = gpu_ctx.sign_votes(b, np.array(signer, np.uint32), "test_chain_id")
+    for v, s in zip(votes, sigs):
+        v.Signature = s.tobytes()
+    return seeds, pubs, addrs, votes, signer
+
+
+def test_verify_batch_valid_and_corrupt(gpu_ctx, oracle_lib):
+    import txflow_amd as T
+    rnd = random.Random(21)
+    seeds, pubs, addrs, votes, signer = _signed_set(gpu_ctx, T, 16, 2000, rnd)
+    # corrupt a third of them in assorted ways
+    kinds = []
+    for i, v in enumerate(votes):
+        k = i % 9
+        s = bytearray(v.Signature)
+        if k == 1:
+            s[rnd.randrange(32)] ^= 1 << rnd.randrange(8)          # R bit flip
+        elif k == 2:
+            s[32 + rnd.randrange(31)] ^= 1 << rnd.randrange(8)     # S bit flip
+        elif k == 3:
+            S = int.from_bytes(s[32:], "little") + L                # non-canonical s (s + L)
+            if S < 2 ** 256:
+                s[32:] = S.to_bytes(32, "little")
+        elif k == 4:
+            s[63] |= 0xE0
+        elif k == 5:
+            v.Timestamp = (v.Timestamp[0], v.Timestamp[1] + 1)     # message changed after signing
+        elif k == 6:
+            s = s[:63]                                              # length != 64
+        v.Signature = bytes(s)
+        kinds.append(k)
+    b = T.VoteBatch.from_votes(votes)
+    st = gpu_ctx.verify_batch(b)
+    for i, v in enumerate(votes):
+        msg = oracle_lib.signbytes(1, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], b"test_chain_id")
+        exp = oracle_lib.verify(pubs[signer[i]], msg, v.Signature)
+        assert (st[i] == T.ADDED) == exp, (i, kinds[i], st[i])
+    # explicit (caller-supplied) pubkeys: wrong key -> ErrVoteInvalidValidatorAddress
+    keys = np.array([np.frombuffer(pubs[(signer[i] + (1 if i % 5 == 0 else 0)) % len(pubs)], np.uint8)
+                     for i in range(len(votes))])
+    st2 = gpu_ctx.verify_batch(b, keys)
+    for i in range(len(votes)):
+        if i % 5 == 0:
+            assert st2[i] == T.ERR_INVALID_VALIDATOR_ADDRESS
+        else:
+            assert st2[i] == st[i]
+
+
+def test_add_votes_matches_sequential_oracle(gpu_ctx, oracle_lib):
+    import txflow_amd as T
+    rnd = random.Random(33)
+    seeds, pubs, addrs, votes, signer = _signed_set(gpu_ctx, T, 10, 3000, rnd, n_txs=40)
+    # add replays, conflicts, bad sigs, unknown/empty validators, nil votes
+    extra = []
+    for i in range(600):
+        base = rnd.choice(votes)
+        k = i % 6
+        v = T.TxVote(Height=base.Height, TxHash=base.TxHash, Timestamp=base.Timestamp,
+                     ValidatorAddress=base.ValidatorAddress, Signature=base.Signature)
+        if k == 1:
+            v.Timestamp = (v.Timestamp[0], v.Timestamp[1] + 7)       # conflicting (different sig later)
+        elif k == 2:
+            s = bytearray(v.Signature); s[5] ^= 0x10; v.Signature = bytes(s)
+        elif k == 3:
+            v.ValidatorAddress = bytes(20)
+        elif k == 4:
+            v.ValidatorAddress = b""
+        elif k == 5:
+            v = None
+        extra.append(v)
+    allv = votes + extra
+    rnd.shuffle(allv)
+    flow = oracle_lib.Flow(pubs, [1 + (i % 3) for i in range(len(pubs))], b"test_chain_id")
+    gpu_ctx.set_validators(pubs, [1 + (i % 3) for i in range(len(pubs))], "test_chain_id")
+    # two batches to exercise cross-batch state
+    cut = len(allv) // 2
+    for part in (allv[:cut], allv[cut:]):
+        b = T.VoteBatch.from_votes(part)
+        st, ev = gpu_ctx.add_votes(b)
+        od = [dict(nil=True) if v is None else dict(height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0],
+                                                     ts_nanos=v.Timestamp[1], addr=v.ValidatorAddress,
+                                                     sig=v.Signature) for v in part]
+        ost, osum, ofired = flow.add_votes(od)
+        exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+        bad = np.nonzero(st != exp)[0]
+        assert len(bad) == 0, [(int(i), int(st[i]), int(exp[i])) for i in bad[:10]]
+    for v in allv:
+        if v is None:
+            continue
+        assert gpu_ctx.query_tx(v.TxHash.encode()) == flow.query(v.TxHash.encode())
+    assert gpu_ctx.num_tx_sets() == flow.num_sets()
