@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""bench.py — verified+tallied TxVotes/sec on MI355X (BASELINE.json metric).
+
+Workload: per GPU, 100 validators (power 1, quorum 67) x 10,000 txs
+= 1,000,000 ed25519-signed TxVotes in shuffled arrival order (config C2 at N=1; at N>1 each
+rank holds its shard = SHA-256(TxHash)[0] mod N of N x 10,000 txs, the C3 layout, weak
+scaling).  Signatures come from the device signer; inputs are staged in HBM before timing.
+
+One step = one pass of the hot path over the resident batch: empty all TxVoteSets
+(device memsets), K1 verify every vote, K2 tally (first-accepted resolution, stake sums,
+2/3 crossings, commit bitmap), read back per-vote statuses; at N>1 also an RCCL all-gather
+of the per-shard commit bitmaps.  value = votes processed by all ranks / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+
+import numpy as np  # noqa: E402
+
+W_ALG = 2.5e5   # int32 VALU lane-ops per verified vote, SURVEY.md §8d (Straus reference algorithm)
+TALLY_BYTES_PER_VOTE = 16.0   # SURVEY.md §8d algorithmic tally traffic
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(wl, threads: int, serial_votes: int, parallel_votes: int):
+    """The oracle's C restatement of the reference path on this host (kind "port"):
+    serial = TxFlow.addVote loop with verification inside (1 goroutine, txflow/service.go:123-166);
+    parallel = verify on `threads` host threads + the sequential tally with those verdicts."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    n = wl.n
+    # serial: sequential AddVote with verification
+    idx = np.arange(min(serial_votes, n))
+    votes = [wl.vote(int(i)) for i in idx]
+    flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
+    flow.add_votes(votes)
+    ts = flow.last_seconds
+    serial_rate = len(votes) / ts
+    # parallel verify + sequential tally
+    m = min(parallel_votes, n)
+    msgs = [O.signbytes(1, wl.batch.txhash(i), int(wl.batch.ts_sec[i]), int(wl.batch.ts_nanos[i]), b"test_chain_id")
+            for i in range(m)]
+    arena = np.frombuffer(b"".join(msgs), np.uint8)
+    lens = np.array([len(x) for x in msgs], np.uint16)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint32)
+    pubs = np.frombuffer(b"".join(wl.pubs), np.uint8)
+    tv, ok = O.verify_many(pubs, wl.val_of[:m], arena, offs, lens, wl.batch.sig[:64 * m], threads)
+    flow2 = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
+    pv = [wl.vote(i) for i in range(m)]
+    flow2.add_votes(pv, verdicts=ok)
+    tt = flow2.last_seconds
+    par_rate = m / (tv + tt)
+    assert ok.all()
+    return dict(value=round(par_rate, 1), unit="votes/s", cores=threads, kind="port",
+                sample=f"first {m} votes of the same workload: {threads}-thread oracle ed25519 verify "
+                       f"({tv:.2f}s) + sequential TxFlow.addVote tally ({tt:.2f}s); "
+                       f"serial 1-thread verify-inside-AddVote on {len(votes)} votes = {serial_rate:.1f} votes/s",
+                serial_value=round(serial_rate, 1), serial_cores=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--validators", type=int, default=100)
+    ap.add_argument("--txs-per-gpu", type=int, default=10_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-serial-votes", type=int, default=20_000)
+    ap.add_argument("--cpu-parallel-votes", type=int, default=200_000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")   # RCCL over xGMI
+
+    import txflow_amd as T
+    from txflow_amd.workload import Workload, SEEDS
+
+    n_txs_global = args.txs_per_gpu * world
+    t_setup = time.perf_counter()
+    max_txs = n_txs_global if world > 1 else args.txs_per_gpu
+    ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
+                    max_validators=max(args.validators, 1))
+    wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
+                  shard=rank, n_shards=world)
+    ctx.stage(0, wl.batch)
+    log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
+        f"staged in {time.perf_counter() - t_setup:.1f}s")
+
+    bm_ptr, bm_bytes = ctx.commit_bitmap()
+    gathered = None
+    if dist is not None:
+        import torch
+        bm_local = torch.zeros(bm_bytes // 4, dtype=torch.int32, device=f"cuda:{local}")
+        gathered = torch.zeros(world * (bm_bytes // 4), dtype=torch.int32, device=f"cuda:{local}")
+
+    step_ms, verify_ms, tally_ms = [], [], []
+
+    def step(record: bool):
+        t0 = time.perf_counter()
+        ctx.reset_tally()
+        ms = ctx.run_staged(0, timed=True)
+        st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1)
+        if dist is not None:
+            ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)
+            dist.all_gather_into_tensor(gathered, bm_local)
+            torch.cuda.synchronize()
+        if record:
+            step_ms.append((time.perf_counter() - t0) * 1e3)
+            verify_ms.append(ms[0])
+            tally_ms.append(ms[1])
+        return st, ev
+
+    for _ in range(args.warmup):
+        st, ev = step(False)
+    # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once
+    st, ev = step(False)
+    n_added = int(np.count_nonzero((st & 0x7F) == T.ADDED))
+    n_fired = int(np.count_nonzero(st & 0x80))
+    quorum = ctx.total_power() * 2 // 3 + 1
+    exp_fired = wl.n_txs * (args.validators - quorum + 1)
+    if n_added != wl.n or len(ev) != wl.n_txs or n_fired != exp_fired:
+        log(f"[rank {rank}] CORRECTNESS FAILURE: added {n_added}/{wl.n}, events {len(ev)}/{wl.n_txs}, "
+            f"fired {n_fired}/{exp_fired}")
+        sys.exit(2)
+
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    ctx.sync()
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        nv = torch.tensor([wl.n], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(nv)
+        total_votes = int(nv.item())
+    else:
+        total_votes = wl.n
+
+    value = total_votes * args.steps / elapsed
+    v_ms = statistics.median(verify_ms)
+    t_ms = statistics.median(tally_ms)
+    if rank == 0:
+        add_rate, mad_rate = ctx.valu_probe()
+        achieved = wl.n * W_ALG / (v_ms * 1e-3) / 1e12
+        peak = add_rate / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(args.cpu_threads, os.cpu_count() or 1)
+            cpu = cpu_baseline(wl, threads, args.cpu_serial_votes, args.cpu_parallel_votes)
+        out = {
+            "metric": "verified+tallied TxVotes/sec",
+            "value": round(value, 1),
+            "unit": "votes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: device-signed ed25519 TxVotes (RFC 8032), SURVEY.md §8d seeds",
+            "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
+                                    f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
+                                    f"100 validators, ~1M votes/GPU, RCCL bitmap all-gather"),
+                       "validators": args.validators, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
+                       "parallelism": f"shard{world}"},
+            "p50_batch_ms": round(statistics.median(step_ms), 3),
+            "verify_kernel_ms": round(v_ms, 3),
+            "tally_kernels_ms": round(t_ms, 3),
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 3),
+                         "unit": "Tlane-op/s (int32 VALU)", "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "kernel": "txv_k_verify", "w_alg_lane_ops_per_vote": W_ALG,
+                         "peak_source": "live v_add_u32 issue-rate probe (txv_valu_probe)",
+                         "mad_u64_u32_peak": round(mad_rate / 1e12, 3),
+                         "tally_GBps": round(wl.n * TALLY_BYTES_PER_VOTE / (t_ms * 1e-3) / 1e9, 1)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

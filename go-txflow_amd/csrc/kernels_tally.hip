@@ -31,7 +31,8 @@ __device__ __forceinline__ uint64_t tag_of(uint32_t epoch_hi, uint32_t seq) {
 __global__ void __launch_bounds__(256) txv_k_tally_mark(TallyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  if (a.status[i] != TXV_ST_PENDING) return;
+  const uint8_t pre = a.pre[i];
+  if (pre != TXV_ST_PENDING) { a.status[i] = pre; return; }
   const uint64_t key = (uint64_t)a.set[i] * a.n_vals + a.val[i];
   const uint32_t slot = a.acc_slot[key];
   if (slot) {

@@ -272,3 +272,32 @@ hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- integer-VALU peak probe
+// Measures the chip's issue rate of the two ops a field multiply is made of, so bench.py
+// prices roofline.peak on the box it runs on (P must be measured).
+template <int OP>
+__global__ void __launch_bounds__(256) txv_k_valu_probe(uint32_t* out, uint32_t seed, int iters) {
+  uint32_t a[8];
+  uint64_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { a[i] = seed + threadIdx.x + i; m[i] = a[i]; }
+  const uint32_t b = seed * 3u + 1u, c = seed ^ 0x9e3779b9u;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+      else asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(m[i]) : "v"(b), "v"(c) : "s0", "s1");
+    }
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= a[i] ^ (uint32_t)m[i] ^ (uint32_t)(m[i] >> 32);
+  out[blockIdx.x * 256 + threadIdx.x] = r;
+}
+
+extern "C" hipError_t txv_launch_valu_probe(int op, uint32_t* out, uint32_t blocks, int iters, hipStream_t st) {
+  if (op == 0) hipLaunchKernelGGL(txv_k_valu_probe<0>, dim3(blocks), dim3(256), 0, st, out, 7u, iters);
+  else hipLaunchKernelGGL(txv_k_valu_probe<1>, dim3(blocks), dim3(256), 0, st, out, 7u, iters);
+  return hipGetLastError();
+}

@@ -34,7 +34,7 @@ struct Slot {
   // device
   uint32_t* d_sig = nullptr; uint64_t* d_msg = nullptr; uint32_t* d_msg_len = nullptr;
   uint32_t* d_val = nullptr; uint32_t* d_set = nullptr; uint8_t* d_flags = nullptr;
-  uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr;
+  uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr; uint8_t* d_pre = nullptr;
   uint32_t* d_touched = nullptr; int64_t* d_tsum = nullptr; uint8_t* d_tmaj = nullptr; uint32_t* d_tcross = nullptr;
   // pinned host
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
@@ -130,6 +130,7 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
     if ((r = dalloc(c, &s.d_sig, 16 * npad)) || (r = dalloc(c, &s.d_msg, (size_t)mw * npad)) ||
         (r = dalloc(c, &s.d_msg_len, npad)) || (r = dalloc(c, &s.d_val, npad)) || (r = dalloc(c, &s.d_set, npad)) ||
         (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
+        (r = dalloc(c, &s.d_pre, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
         (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)))
@@ -161,7 +162,7 @@ int alloc_tally(txv_ctx* c) {
   return TXV_OK;
 }
 
-int reset_tally(txv_ctx* c) {
+int reset_tally(txv_ctx* c, bool keep_ids = false) {
   const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
   HIP_TRY(c, hipMemsetAsync(c->d_acc_slot, 0, cells * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
@@ -170,6 +171,12 @@ int reset_tally(txv_ctx* c) {
   HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
   c->epoch = 0;
+  if (keep_ids) {
+    std::fill(c->h_sum.begin(), c->h_sum.end(), 0);
+    std::fill(c->h_maj.begin(), c->h_maj.end(), 0);
+    std::fill(c->seen_epoch.begin(), c->seen_epoch.end(), 0);
+    return TXV_OK;
+  }
   c->tx_index.clear();
   c->tx_keys.clear();
   c->h_sum.clear();
@@ -241,7 +248,7 @@ int upload_slot(txv_ctx* c, Slot& s) {
   HIP_TRY(c, hipMemcpyAsync(s.d_val, s.h_val, np * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_flags, s.h_flags, np, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_status, s.h_status, np, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, np, hipMemcpyHostToDevice, c->stream));
   if (s.n_touched)
     HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->stream));
   return TXV_OK;
@@ -266,7 +273,8 @@ TallyArgs tally_args(txv_ctx* c, Slot& s) {
   TallyArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.n_vals = c->n_vals; a.epoch_hi = 0xFFFFFFFFu - c->epoch;
   a.quorum = c->quorum;
-  a.sig = s.d_sig; a.set = s.d_set; a.val = s.d_val; a.flags = s.d_flags; a.ok = s.d_ok; a.status = s.d_status;
+  a.sig = s.d_sig; a.set = s.d_set; a.val = s.d_val; a.flags = s.d_flags; a.ok = s.d_ok;
+  a.pre = s.d_pre; a.status = s.d_status;
   a.acc_slot = c->d_acc_slot; a.first_tag = c->d_first_tag; a.arena = c->d_arena; a.arena_count = c->d_arena_count;
   a.arena_cap = c->cfg.max_accepted; a.n_touched = s.n_touched; a.error_flags = c->d_errflags;
   a.power = c->d_power; a.set_sum = c->d_set_sum; a.set_cross = c->d_set_cross; a.commit_bitmap = c->d_bitmap;
@@ -432,7 +440,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
-    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
+    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
     hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
@@ -716,12 +724,55 @@ int txv_reset_tally(txv_ctx* c) {
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   if (!c->n_vals) return TXV_OK;
-  return reset_tally(c);
+  return reset_tally(c, true);
 }
 
 int txv_sync(txv_ctx* c) {
   if (!c) return TXV_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+int txv_copy_commit_bitmap(txv_ctx* c, void* dst_dev, uint64_t bytes) {
+  if (!c || !dst_dev) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t have = (uint64_t)(c->cfg.max_txs + 31) / 32 * 4;
+  HIP_TRY(c, hipMemcpyAsync(dst_dev, c->d_bitmap, std::min(bytes, have), hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+int txv_valu_probe(txv_ctx* c, double* add_lane_ops_per_s, double* mad_lane_ops_per_s) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t blocks = (uint32_t)c->n_cus * 8;   // 32 waves per CU
+  const int iters = 1 << 14;
+  uint32_t* d = nullptr;
+  int r;
+  if ((r = dalloc(c, &d, (size_t)blocks * 256))) return r;
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  double* outs[2] = {add_lane_ops_per_s, mad_lane_ops_per_s};
+  for (int op = 0; op < 2; ++op) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {
+      HIP_TRY(c, hipEventRecord(e0, c->stream));
+      HIP_TRY(c, txv_launch_valu_probe(op, d, blocks, iters, c->stream));
+      HIP_TRY(c, hipEventRecord(e1, c->stream));
+      HIP_TRY(c, hipEventSynchronize(e1));
+      float ms;
+      HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+      if (rep && ms < best) best = ms;   // first launch is warm-up
+    }
+    const double lane_ops = (double)blocks * 256.0 * iters * 8.0;
+    if (outs[op]) *outs[op] = lane_ops / (best * 1e-3);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  dfree(d);
   return TXV_OK;
 }
 

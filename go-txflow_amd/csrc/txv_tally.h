@@ -24,7 +24,9 @@ struct TallyArgs {
   const uint32_t* val;          // [n]
   const uint8_t* flags;         // [n]
   const uint8_t* ok;            // [n] verify verdicts
-  uint8_t* status;              // [n] in: 0xFF pending / pre-check code; out: final code | fired bit
+  const uint8_t* pre;           // [n] host pre-check: 0xFF pending, else the final error code
+  uint8_t* status;              // [n] out: final code | fired bit (pre is never modified, so a
+                                //      staged batch can be re-run)
   uint32_t* acc_slot;
   uint64_t* first_tag;
   uint32_t* arena;

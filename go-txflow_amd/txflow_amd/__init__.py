@@ -99,6 +99,8 @@ def lib():
             "txv_reset_tally": ([vp], ctypes.c_int),
             "txv_sync": ([vp], ctypes.c_int),
             "txv_fe_selftest": ([vp, vp, vp, vp, u32, ctypes.c_int], ctypes.c_int),
+            "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
+            "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -112,7 +114,8 @@ EXPORTED_SYMBOLS = [
     "txv_init", "txv_destroy", "txv_last_error", "txv_device_name", "txv_set_validators",
     "txv_get_validator_info", "txv_verify_batch", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
-    "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest"]
+    "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest",
+    "txv_copy_commit_bitmap", "txv_valu_probe"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -332,6 +335,15 @@ class Context:
         p = ctypes.c_void_p(); nb = ctypes.c_uint64()
         self._chk(lib().txv_commit_bitmap(self._h, ctypes.byref(p), ctypes.byref(nb)), "bitmap")
         return p.value, nb.value
+
+    def copy_commit_bitmap(self, dst_dev_ptr: int, nbytes: int):
+        self._chk(lib().txv_copy_commit_bitmap(self._h, ctypes.c_void_p(dst_dev_ptr), nbytes), "bitmap copy")
+
+    def valu_probe(self):
+        """(v_add_u32, v_mad_u64_u32) lane-ops/s measured on this device"""
+        a = ctypes.c_double(); m = ctypes.c_double()
+        self._chk(lib().txv_valu_probe(self._h, ctypes.byref(a), ctypes.byref(m)), "valu probe")
+        return a.value, m.value
 
     def reset_tally(self):
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")

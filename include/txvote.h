@@ -154,7 +154,12 @@ int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commi
                      uint32_t ev_cap, uint32_t* n_ev);
 /* device pointer + byte size of the per-set committed bitmap (1 bit per tx-set id) */
 int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
-/* reset tally state (all TxVoteSets) keeping the validator set */
+/* device-to-device copy of the commit bitmap into caller device memory (e.g. an RCCL buffer) */
+int txv_copy_commit_bitmap(txv_ctx* ctx, void* dst_dev, uint64_t bytes);
+/* measured integer-VALU issue rates of this device (lane-ops/s): v_add_u32 and v_mad_u64_u32 */
+int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
+/* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids
+ * already assigned stay assigned (their sets read as empty) */
 int txv_reset_tally(txv_ctx* ctx);
 int txv_sync(txv_ctx* ctx);
 

@@ -180,8 +180,11 @@ class Flow:
         if verdicts is not None:
             vd = np.ascontiguousarray(np.asarray(verdicts, dtype=np.uint8))
             vp = vd.ctypes.data
+        import time
+        t0 = time.perf_counter()
         lib().orc_flow_add_votes(self._h, ctypes.addressof(arr), n, vp, status.ctypes.data,
                                  sums.ctypes.data, fired.ctypes.data)
+        self.last_seconds = time.perf_counter() - t0   # the C loop only (bench cpu_baseline)
         return status[:n], sums[:n], fired[:n]
 
     def query(self, txhash: bytes):
