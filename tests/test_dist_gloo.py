@@ -1,0 +1,89 @@
+"""Multi-rank path on CPU (gloo, world_size 2): votes sharded by SHA-256(TxHash)[0] mod G,
+per-shard sequential tallies (oracle stands in for the per-GPU engine), one all-gather of the
+per-shard commit bitmaps; the merged committed set and per-tx stakes must equal a single
+global sequential run (the tally is shard-local, so sharding changes nothing)."""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _scenario():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rnd = random.Random(77)
+    seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(5)]
+    pubs = [O.pubkey(s) for s in seeds]
+    addrs = [O.sha256(p)[:20] for p in pubs]
+    txs = [("%064X" % rnd.getrandbits(256)).encode() for _ in range(24)]
+    votes = []
+    for i in range(260):
+        t = rnd.choice(txs)
+        v = rnd.randrange(5)
+        ts = (1_700_000_000, rnd.randrange(1, 4))   # few timestamps -> duplicates and conflicts
+        msg = O.signbytes(1, t, ts[0], ts[1], b"test_chain_id")
+        sig = O.sign(seeds[v], msg)
+        if rnd.random() < 0.1:
+            sig = sig[:10] + bytes([sig[10] ^ 1]) + sig[11:]
+        votes.append(dict(height=1, txhash=t, ts_sec=ts[0], ts_nanos=ts[1], addr=addrs[v], sig=sig))
+    return O, pubs, txs, votes
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+    from txflow_amd import sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    O, pubs, txs, votes = _scenario()
+    parts = sharding.partition([v["txhash"] for v in votes], world)
+    mine = [votes[i] for i in parts[rank]]
+    flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
+    st, _, _ = flow.add_votes(mine)
+    # local set ids in first-seen order (the engine's dense ids)
+    local_keys = []
+    for v in mine:
+        if v["txhash"] not in local_keys:
+            local_keys.append(v["txhash"])
+    committed = [i for i, k in enumerate(local_keys) if flow.query(k)[1]]
+    bm = torch.from_numpy(sharding.pack_bitmap(committed, 64).view(np.int32).copy())
+    out = torch.zeros(world * bm.numel(), dtype=torch.int32)
+    dist.all_gather_into_tensor(out, bm)
+    keys_all = [None] * world
+    dist.all_gather_object(keys_all, local_keys)
+    merged = sharding.merge_gathered(out.numpy().view(np.uint32), world, keys_all)
+    stakes = {k: flow.query(k)[0] for k in local_keys}
+    q.put((rank, sorted(merged), stakes))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_tally_matches_global():
+    world, port = 2, 29500 + random.Random().randrange(1000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    O, pubs, txs, votes = _scenario()
+    flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
+    flow.add_votes(votes)
+    glob_commit = sorted(t for t in set(v["txhash"] for v in votes) if flow.query(t)[1])
+    for _, merged, _ in res:
+        assert merged == glob_commit
+    stakes = {}
+    for _, _, s in res:
+        stakes.update(s)
+    for t in set(v["txhash"] for v in votes):
+        assert stakes[t] == flow.query(t)[0]
+    assert len(glob_commit) > 0
