@@ -19,6 +19,15 @@
 
 #define TXV_HD __host__ __device__ __forceinline__
 
+// Scheduling fence: keeps the compiler from interleaving independent field multiplies,
+// which buys ILP at the cost of registers; with >= 4 waves per SIMD latency is hidden by
+// the other waves instead (DESIGN.md §K1 register budget).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TXV_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TXV_SCHED_FENCE() ((void)0)
+#endif
+
 namespace txv {
 
 // ---------------------------------------------------------------- carry primitives
@@ -112,19 +121,42 @@ TXV_HD fe fe_reduce512(const uint32_t t[16]) {
   return r;
 }
 
+// Product scanning with the reduction folded into the high columns: as soon as column
+// k >= 8 is complete its word is multiplied by 38 and added into result word k-8, so the
+// upper half of the 512-bit product is never held in registers.
 TXV_HD fe fe_mul(const fe& a, const fe& b) {
-  uint32_t t[16];
+  fe r;
   uint64_t acc = 0; uint32_t ovf = 0;
 #pragma unroll
-  for (int k = 0; k < 15; ++k) {
+  for (int k = 0; k < 8; ++k) {
 #pragma unroll
-    for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); ++i) mac(acc, ovf, a.v[i], b.v[k - i]);
-    t[k] = (uint32_t)acc;
+    for (int i = 0; i <= k; ++i) mac(acc, ovf, a.v[i], b.v[k - i]);
+    r.v[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)ovf << 32);
     ovf = 0;
   }
-  t[15] = (uint32_t)acc;
-  return fe_reduce512(t);
+  uint32_t fc = 0;   // fold carry (<= 39)
+#pragma unroll
+  for (int k = 8; k < 16; ++k) {
+    if (k < 15) {
+#pragma unroll
+      for (int i = k - 7; i <= 7; ++i) mac(acc, ovf, a.v[i], b.v[k - i]);
+    }
+    const uint32_t w = (uint32_t)acc;
+    if (k < 15) { acc = (acc >> 32) | ((uint64_t)ovf << 32); ovf = 0; }
+    uint64_t f = mad64(w, 38u, (uint64_t)r.v[k - 8] + fc);
+    r.v[k - 8] = (uint32_t)f;
+    fc = (uint32_t)(f >> 32);
+  }
+  // r += 38 * fc, then a possible final wrap
+  uint64_t c;
+  uint64_t f = mad64(fc, 38u, (uint64_t)r.v[0]);
+  r.v[0] = (uint32_t)f;
+  add_cc(r.v[1], c, r.v[1], (uint32_t)(f >> 32));
+#pragma unroll
+  for (int i = 2; i < 8; ++i) addc_cc(r.v[i], c, r.v[i], 0u, c);
+  r.v[0] += sel_c(c, 38u, 0u);
+  return r;
 }
 
 TXV_HD fe fe_sq(const fe& a) {

@@ -25,14 +25,24 @@ TXV_HD ge_ext ge_madd(const ge_ext& p, const ge_niels& q, bool neg) {
   fe qp = fe_select(neg, q.ymx, q.ypx);
   fe qm = fe_select(neg, q.ypx, q.ymx);
   fe A = fe_mul(fe_sub(p.Y, p.X), qm);
+  TXV_SCHED_FENCE();
   fe B = fe_mul(fe_add(p.Y, p.X), qp);
-  fe C = fe_mul(p.T, q.xy2d);
-  fe D = fe_dbl(p.Z);
+  TXV_SCHED_FENCE();
   fe E = fe_sub(B, A), H = fe_add(B, A);
+  fe C = fe_mul(p.T, q.xy2d);
+  TXV_SCHED_FENCE();
+  fe D = fe_dbl(p.Z);
   fe Gp = fe_add(D, C), Fm = fe_sub(D, C);
   fe G = fe_select(neg, Fm, Gp), F = fe_select(neg, Gp, Fm);
   ge_ext r;
-  r.X = fe_mul(E, F); r.Y = fe_mul(G, H); r.Z = fe_mul(F, G); r.T = fe_mul(E, H);
+  r.X = fe_mul(E, F);
+  TXV_SCHED_FENCE();
+  r.Y = fe_mul(G, H);
+  TXV_SCHED_FENCE();
+  r.Z = fe_mul(F, G);
+  TXV_SCHED_FENCE();
+  r.T = fe_mul(E, H);
+  TXV_SCHED_FENCE();
   return r;
 }
 

@@ -67,8 +67,42 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
 }
 
 // ---------------------------------------------------------------- K1: verify
+// K1 is split in two launches so each phase gets its own register allocation (one fused
+// kernel kept the signature words and digits live across SHA-512 and the table walk and
+// needed 272 VGPRs = 1 wave/SIMD):
+//   K1a txv_k_challenge   per vote: length / top-bit / s < L / decode checks, k = SHA-512(R||A||M) mod L
+//                         -> k[8][n_pad] (32 B/vote, HBM) and the "go" flag in ok_out
+//   K1b txv_k_scalarmult  per vote, in validator-grouped order: [s]B + [k](-A), encode, compare with R
+
+__global__ void __launch_bounds__(256) txv_k_challenge(VerifyArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint8_t fl = a.flags[i];
+  if (!(fl & TXV_FLAG_PENDING)) return;
+  const uint32_t v = a.val[i];
+  uint32_t s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
+  const bool bad = !(fl & TXV_FLAG_SIG64) || (s[15] & 0xE0000000u) || !a.decode_ok[v] || !sc_lt_L(s + 8);
+  if (bad) { a.ok_out[i] = 0; return; }
+  const uint32_t* pw = a.pubs_le + (size_t)v * 8;
+  uint64_t pre[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = be64_from_le32(s[2 * j], s[2 * j + 1]);
+    pre[4 + j] = be64_from_le32(pw[2 * j], pw[2 * j + 1]);
+  }
+  MsgView m{a.msg + i, a.n_pad, a.msg_words, a.msg_len[i]};
+  uint32_t dig[16];
+  sha512_prefixed(dig, pre, 8, m);
+  sc k = sc_reduce512(dig);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a.kbuf[(size_t)j * a.n_pad + i] = k.v[j];
+  a.ok_out[i] = 2;   // passed the scalar checks; K1b decides
+}
+
 template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) txv_k_verify(VerifyArgs a) {
+__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult(VerifyArgs a) {
   __shared__ uint32_t btab[kTableWords];
   // stage the base-point table: 16-byte loads, all threads
   {
@@ -78,41 +112,26 @@ __global__ void __launch_bounds__(BLOCK) txv_k_verify(VerifyArgs a) {
   }
   __syncthreads();
   const uint32_t stride = gridDim.x * BLOCK;
-  for (uint32_t idx = blockIdx.x * BLOCK + threadIdx.x; idx < a.n; idx += stride) {
+  for (uint32_t idx = blockIdx.x * BLOCK + threadIdx.x; idx < a.n_work; idx += stride) {
     const uint32_t i = a.order ? a.order[idx] : idx;
-    const uint8_t fl = a.flags[i];
-    if (!(fl & TXV_FLAG_PENDING)) continue;
+    if (a.ok_out[i] != 2) continue;
     const uint32_t v = a.val[i];
-    uint32_t s[16];
+    uint32_t sp[8], kp[8];
+    {
+      uint32_t s[8], k[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
-    bool bad = !(fl & TXV_FLAG_SIG64) || (s[15] & 0xE0000000u) || !a.decode_ok[v] || !sc_lt_L(s + 8);
-    uint8_t ok = 0;
-    if (!bad) {
-      const uint32_t* pw = a.pubs_le + (size_t)v * 8;
-      uint64_t pre[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pre[j] = be64_from_le32(s[2 * j], s[2 * j + 1]);
-        pre[4 + j] = be64_from_le32(pw[2 * j], pw[2 * j + 1]);
-      }
-      MsgView m{a.msg + i, a.n_pad, a.msg_words, a.msg_len[i]};
-      uint32_t dig[16];
-      sha512_prefixed(dig, pre, 8, m);
-      sc k = sc_reduce512(dig);
-      uint32_t sp[8], kp[8];
-      sc_recode16(sp, s + 8);
-      sc_recode16(kp, k.v);
-      const uint32_t* ta = a.atables + (size_t)v * kTableWords;
-      ge_ext R = double_scalarmult_fixed(btab, ta, sp, kp, true);
-      uint32_t enc[8];
-      ge_encode(enc, R);
-      uint32_t diff = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) diff |= enc[j] ^ s[j];
-      ok = diff == 0;
+      for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
+      sc_recode16(sp, s);
+      sc_recode16(kp, k);
     }
-    a.ok_out[i] = ok;
+    const uint32_t* ta = a.atables + (size_t)v * kTableWords;
+    ge_ext R = double_scalarmult_fixed(btab, ta, sp, kp, true);
+    uint32_t enc[8];
+    ge_encode(enc, R);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * a.n_pad + i];
+    a.ok_out[i] = diff == 0;
   }
 }
 
@@ -246,7 +265,9 @@ hipError_t txv_launch_build_tables(const uint32_t* pubs_le, uint32_t n_points, u
 
 hipError_t txv_launch_verify(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (!args->n) return hipSuccess;
-  hipLaunchKernelGGL(txv_k_verify<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+  hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
+  if (args->n_work)
+    hipLaunchKernelGGL(txv_k_scalarmult<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
   return hipGetLastError();
 }
 

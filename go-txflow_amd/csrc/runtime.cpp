@@ -35,6 +35,8 @@ struct Slot {
   uint32_t* d_sig = nullptr; uint64_t* d_msg = nullptr; uint32_t* d_msg_len = nullptr;
   uint32_t* d_val = nullptr; uint32_t* d_set = nullptr; uint8_t* d_flags = nullptr;
   uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr; uint8_t* d_pre = nullptr;
+  uint32_t* d_kbuf = nullptr; uint32_t* d_order = nullptr; uint32_t* h_order = nullptr;
+  uint32_t n_work = 0;
   uint32_t* d_touched = nullptr; int64_t* d_tsum = nullptr; uint8_t* d_tmaj = nullptr; uint32_t* d_tcross = nullptr;
   // pinned host
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
@@ -130,7 +132,8 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
     if ((r = dalloc(c, &s.d_sig, 16 * npad)) || (r = dalloc(c, &s.d_msg, (size_t)mw * npad)) ||
         (r = dalloc(c, &s.d_msg_len, npad)) || (r = dalloc(c, &s.d_val, npad)) || (r = dalloc(c, &s.d_set, npad)) ||
         (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
-        (r = dalloc(c, &s.d_pre, npad)) ||
+        (r = dalloc(c, &s.d_pre, npad)) || (r = dalloc(c, &s.d_kbuf, 8 * npad)) ||
+        (r = dalloc(c, &s.d_order, npad)) || (r = halloc(c, &s.h_order, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
         (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)))
@@ -251,12 +254,29 @@ int upload_slot(txv_ctx* c, Slot& s) {
   HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, np, hipMemcpyHostToDevice, c->stream));
   if (s.n_touched)
     HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->stream));
+  if (s.n_work)
+    HIP_TRY(c, hipMemcpyAsync(s.d_order, s.h_order, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
   return TXV_OK;
+}
+
+// Counting sort of the pending votes by validator: K1b then runs waves whose lanes mostly
+// share one validator's A table (L1/L2-resident gathers instead of scattered MALL reads).
+void build_order(Slot& s) {
+  uint32_t n_keys = 0;
+  for (uint32_t i = 0; i < s.n; ++i)
+    if ((s.h_flags[i] & TXV_FLAG_PENDING) && s.h_val[i] + 1 > n_keys) n_keys = s.h_val[i] + 1;
+  std::vector<uint32_t> cnt((size_t)n_keys + 1, 0);
+  for (uint32_t i = 0; i < s.n; ++i)
+    if (s.h_flags[i] & TXV_FLAG_PENDING) cnt[s.h_val[i] + 1]++;
+  for (uint32_t k = 0; k < n_keys; ++k) cnt[k + 1] += cnt[k];
+  s.n_work = cnt[n_keys];
+  for (uint32_t i = 0; i < s.n; ++i)
+    if (s.h_flags[i] & TXV_FLAG_PENDING) s.h_order[cnt[s.h_val[i]]++] = i;
 }
 
 uint32_t verify_grid(txv_ctx* c, uint32_t n) {
   const uint32_t blocks = (n + TXV_VERIFY_BLOCK - 1) / TXV_VERIFY_BLOCK;
-  const uint32_t cap = (uint32_t)c->n_cus * 2;   // 2 workgroups/CU (LDS: 2 x 55 KB B table)
+  const uint32_t cap = (uint32_t)c->n_cus * 2;   // 2 x 512-thread workgroups per CU (LDS: 2 x 55 KB B table)
   return std::max<uint32_t>(1, std::min(blocks, cap));
 }
 
@@ -264,7 +284,8 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   VerifyArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words;
   a.sig = s.d_sig; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val; a.flags = s.d_flags;
-  a.order = nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
+  a.n_work = s.n_work; a.kbuf = s.d_kbuf;
+  a.order = s.d_order; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
   return a;
 }
@@ -323,6 +344,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     s.h_status[i] = 0xFF;
     s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
   }
+  build_order(s);
   pack_columns(s, v, lens);
   if ((r = upload_slot(c, s))) return r;
   s.staged = true; s.ran = false;
@@ -440,7 +462,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
-    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
+    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_order); hfree(s.h_order); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
     hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
@@ -577,6 +599,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
       s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
     }
   }
+  build_order(s);
   pack_columns(s, v, lens);
   if ((r = upload_slot(c, s))) return r;
   VerifyArgs va = verify_args(c, s, kp, kok, ktab);

@@ -11,14 +11,15 @@
 #include <hip/hip_runtime.h>
 
 #ifndef TXV_VERIFY_BLOCK
-#define TXV_VERIFY_BLOCK 256
+#define TXV_VERIFY_BLOCK 512   // 8 waves share one LDS copy of the B table; 2 blocks/CU
 #endif
 
 #define TXV_FLAG_PENDING 0x01u   // vote reaches the Verify step (pre-checks passed)
 #define TXV_FLAG_SIG64   0x02u   // len(Signature) == 64
 
 struct VerifyArgs {
-  uint32_t n, n_pad, msg_words, pad0;
+  uint32_t n, n_pad, msg_words, n_work;   // n_work: entries of order[] (pending votes)
+  uint32_t* kbuf;              // [8][n_pad] challenge scalars k (K1a -> K1b)
   const uint32_t* sig;         // [16][n_pad]
   const uint64_t* msg;         // [msg_words][n_pad]
   const uint32_t* msg_len;     // [n]
