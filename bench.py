@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--txs-per-gpu", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--table-w", type=int, default=8, choices=(4, 8))
     ap.add_argument("--cpu-serial-votes", type=int, default=20_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=200_000)
     args = ap.parse_args()
@@ -101,7 +102,7 @@ def main():
     t_setup = time.perf_counter()
     max_txs = n_txs_global if world > 1 else args.txs_per_gpu
     ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
-                    max_validators=max(args.validators, 1))
+                    max_validators=max(args.validators, 1), table_w=args.table_w)
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
     ctx.stage(0, wl.batch)
@@ -202,7 +203,7 @@ def main():
             "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
                                     f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
                                     f"100 validators, ~1M votes/GPU, RCCL bitmap all-gather"),
-                       "validators": args.validators, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
+                       "validators": args.validators, "table_window": args.table_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
                        "parallelism": f"shard{world}"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
             "verify_kernel_ms": round(v_ms, 3),

@@ -5,11 +5,13 @@
 // reference calls it at types/tx_vote.go:115 via tendermint PubKeyEd25519.VerifyBytes):
 //   reject len(sig) != 64 | sig[63] & 0xE0 | undecodable A | s >= L,
 //   k = SHA-512(R || A || M) mod L, accept iff encode([s]B + [k](-A)) == R bytewise.
-// The double scalar multiplication is evaluated doubling-free over fixed-base radix-16
-// tables (ge.h Niels entries): T_P[i][j] = j * 16^i * P for i < 64, j <= 8 (j = 0 the
-// identity), so [s]B + [k](-A) = sum_i T_B[i][s_i] - T_A[i][k_i] with signed digits.
-// This is exact group arithmetic, hence the same point and encoding as x/crypto's
+// The double scalar multiplication is evaluated doubling-free over fixed-base radix-2^W
+// tables (ge.h Niels entries): T_P[i][j] = j * 2^(W i) * P for i < 256/W, j <= 2^(W-1)
+// (j = 0 the identity), so [s]B + [k](-A) = sum_i T_B[i][s_i] - T_A[i][k_i] with signed
+// digits.  This is exact group arithmetic, hence the same point and encoding as x/crypto's
 // sliding-window GeDoubleScalarMultVartime.
+//   W = 4: 64 positions x 9 entries x 96 B =  55,296 B per point (B fits in LDS)
+//   W = 8: 32 positions x 129 entries x 96 B = 396,288 B per point (L2/MALL resident)
 #pragma once
 #include "fe.h"
 #include "sc.h"
@@ -18,13 +20,22 @@
 
 namespace txv {
 
-constexpr int kTabPositions = 64;      // radix-16 digits of a 253-bit scalar
-constexpr int kTabEntries = 9;         // |digit| in 0..8 (0 = identity)
 constexpr int kEntryWords = 24;        // y+x, y-x, 2dxy: 3 x 8 limbs
-constexpr int kTableWords = kTabPositions * kTabEntries * kEntryWords;   // 13824 words = 55296 B
+
+template <int W>
+struct Tab {
+  static constexpr int kPositions = (256 + W - 1) / W;
+  static constexpr int kEntries = (1 << (W - 1)) + 1;
+  static constexpr int kWords = kPositions * kEntries * kEntryWords;
+  static constexpr int kDigitsPerWord = 32 / W;
+};
+
+// legacy W = 4 names (keygen/sign and the host emulation)
+constexpr int kTabPositions = Tab<4>::kPositions;
+constexpr int kTabEntries = Tab<4>::kEntries;
+constexpr int kTableWords = Tab<4>::kWords;
 
 // message words are stored big-endian (SHA-native), zero beyond the message length.
-// Hash-input word gw of (prefix || M || padding) with a prefix of `pre_words` 64-bit words.
 struct MsgView {
   const uint64_t* words;   // column base for this lane: words[w * stride]
   uint32_t stride;         // column stride (in u64 words)
@@ -69,10 +80,38 @@ TXV_HD void sha512_prefixed(uint32_t digest_le[16], const uint64_t* pre, int pre
   }
 }
 
+// Signed radix-2^W recoding of a scalar < 2^253: a = sum_i e_i 2^(W i), e_i in [-2^(W-1), 2^(W-1)),
+// packed W bits per digit (two's complement), 32/W digits per word.
+template <int W>
+TXV_HD void sc_recode(uint32_t packed[8], const uint32_t a[8]) {
+  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j < 32 / W; ++j) {
+      const uint32_t d = ((a[w] >> (W * j)) & mask) + carry;   // [0, 2^W]
+      carry = (d + half) >> W;                                  // 1 iff d >= 2^(W-1)
+      out |= ((d - (carry << W)) & mask) << (W * j);
+    }
+    packed[w] = out;
+  }
+}
+
+template <int W>
+TXV_HD int sc_digit(uint32_t word, int j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sbfe((int)word, W * j, W);
+#else
+  return ((int)(word << (32 - W - W * j))) >> (32 - W);
+#endif
+}
+
 // table entry fetch: T[pos][idx] from a flat word array
-template <typename Ptr>
-TXV_HD ge_niels load_entry(Ptr tab, int pos, int idx) {
-  const int base = (pos * kTabEntries + idx) * kEntryWords;
+template <int W, typename Ptr>
+TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
+  const int base = (pos * Tab<W>::kEntries + idx) * kEntryWords;
   ge_niels e;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -82,30 +121,53 @@ TXV_HD ge_niels load_entry(Ptr tab, int pos, int idx) {
   }
   return e;
 }
+template <typename Ptr>
+TXV_HD ge_niels load_entry(Ptr tab, int pos, int idx) { return load_entry_w<4>(tab, pos, idx); }
 
-// sum_i T_B[i][s_i] + T_A[i][-k_i]   (negA: digits of k are negated, giving [k](-A))
-template <typename PtrB, typename PtrA>
-TXV_HD ge_ext double_scalarmult_fixed(PtrB tb, PtrA ta, const uint32_t s_packed[8],
-                                      const uint32_t k_packed[8], bool use_a) {
+// sum_i T_B[i][s_i] + T_A[i][-k_i]   (digits of k are negated, giving [k](-A))
+template <int W, typename PtrB, typename PtrA>
+TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_packed[8], const uint32_t k_packed[8],
+                                  bool use_a) {
+  constexpr int D = Tab<W>::kDigitsPerWord;
+  constexpr int WORDS = (Tab<W>::kPositions + D - 1) / D;
   ge_ext P = ge_identity();
   uint32_t ps[8], pk[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { ps[i] = s_packed[i]; pk[i] = k_packed[i]; }
-  for (int w = 0; w < 8; ++w) {
+  for (int w = 0; w < WORDS; ++w) {
     const uint32_t ws = ps[0], wk = pk[0];
 #pragma unroll
     for (int i = 0; i < 7; ++i) { ps[i] = ps[i + 1]; pk[i] = pk[i + 1]; }
-    for (int j = 0; j < 8; ++j) {
-      const int pos = 8 * w + j;
-      const int ds = sc_nibble(ws, j);
-      P = ge_madd(P, load_entry(tb, pos, ds < 0 ? -ds : ds), ds < 0);
+    for (int j = 0; j < D; ++j) {
+      const int pos = D * w + j;
+      const int ds = sc_digit<W>(ws, j);
+      P = ge_madd(P, load_entry_w<W>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
       if (use_a) {
-        const int dk = sc_nibble(wk, j);
-        P = ge_madd(P, load_entry(ta, pos, dk < 0 ? -dk : dk), dk > 0);
+        const int dk = sc_digit<W>(wk, j);
+        P = ge_madd(P, load_entry_w<W>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
       }
     }
   }
   return P;
+}
+
+// legacy W = 4 entry points
+TXV_HD void sc_recode16(uint32_t packed[8], const uint32_t a[8]) { sc_recode<4>(packed, a); }
+template <typename PtrB, typename PtrA>
+TXV_HD ge_ext double_scalarmult_fixed(PtrB tb, PtrA ta, const uint32_t s_packed[8], const uint32_t k_packed[8],
+                                      bool use_a) {
+  return double_scalarmult_w<4>(tb, ta, s_packed, k_packed, use_a);
+}
+
+// [m]P for a small positive m (double-and-add from the top bit)
+TXV_HD ge_ext ge_mul_small(const ge_ext& P, uint32_t m) {
+  ge_ext R = P;
+  int top = 31 - __builtin_clz(m);
+  for (int b = top - 1; b >= 0; --b) {
+    R = ge_dbl(R);
+    if ((m >> b) & 1u) R = ge_add(R, P);
+  }
+  return R;
 }
 
 // the base point's canonical encoding (little-endian words)

@@ -18,18 +18,24 @@
 using namespace txv;
 
 // ---------------------------------------------------------------- K0: tables
-// one workgroup of 64 lanes per point; lane i builds position i (16^i * P times 0..8)
+// One lane per (point, position, chunk of 8 multiples): P_i = 2^(W i) A by W*i doublings,
+// then (8c+1..8c+8) * P_i, batch-inverted (Montgomery's trick) into affine Niels entries.
+template <int W>
 __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restrict__ pubs_le, uint32_t n_points,
                                                           uint32_t* __restrict__ tables,
                                                           uint8_t* __restrict__ decode_ok,
                                                           uint32_t* __restrict__ addr_words) {
-  const uint32_t pt = blockIdx.x;
-  const int pos = threadIdx.x;
+  constexpr int chunks = (Tab<W>::kEntries - 1) / 8;
+  constexpr int per_point = Tab<W>::kPositions * chunks;
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t pt = gid / per_point;
+  const int t = (int)(gid % per_point);
   if (pt >= n_points) return;
+  const int pos = t / chunks, c = t % chunks;
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = pubs_le[pt * 8 + i];
-  if (pos == 0 && addr_words) {
+  if (t == 0 && addr_words) {
     uint32_t h[8];
     sha256_32bytes(h, w);
     // first 20 bytes of the big-endian digest, stored as 5 little-endian-loaded words
@@ -38,32 +44,32 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
   }
   ge_ext A;
   bool ok = ge_decode(A, w);
-  if (pos == 0 && decode_ok) decode_ok[pt] = ok ? 1 : 0;
+  if (t == 0 && decode_ok) decode_ok[pt] = ok ? 1 : 0;
   ge_ext P = A;
-  for (int i = 0; i < 4 * pos; ++i) P = ge_dbl(P);
+  for (int i = 0; i < W * pos; ++i) P = ge_dbl(P);
   ge_ext M[8];
-  M[0] = P;
-  M[1] = ge_dbl(P);
+  M[0] = ge_mul_small(P, 8u * c + 1u);
 #pragma unroll
-  for (int j = 2; j < 8; ++j) M[j] = ge_add(M[j - 1], P);
-  // batch inversion of the 8 Z coordinates (Montgomery's trick)
+  for (int j = 1; j < 8; ++j) M[j] = ge_add(M[j - 1], P);
   fe pref[8];
   pref[0] = M[0].Z;
 #pragma unroll
   for (int j = 1; j < 8; ++j) pref[j] = fe_mul(pref[j - 1], M[j].Z);
   fe inv = fe_invert(pref[7]);
-  uint32_t* out = tables + (size_t)pt * kTableWords + (size_t)pos * kTabEntries * kEntryWords;
+  uint32_t* out = tables + (size_t)pt * Tab<W>::kWords + (size_t)pos * Tab<W>::kEntries * kEntryWords;
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
     fe zi = j ? fe_mul(inv, pref[j - 1]) : inv;
     if (j) inv = fe_mul(inv, M[j].Z);
     ge_niels n = ge_to_niels(M[j], zi);
-    uint32_t* e = out + (j + 1) * kEntryWords;
+    uint32_t* e = out + (8 * c + j + 1) * kEntryWords;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { e[i] = n.ypx.v[i]; e[8 + i] = n.ymx.v[i]; e[16 + i] = n.xy2d.v[i]; }
   }
+  if (c == 0) {
 #pragma unroll
-  for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;   // identity (1, 1, 0)
+    for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;   // identity (1, 1, 0)
+  }
 }
 
 // ---------------------------------------------------------------- K1: verify
@@ -101,18 +107,9 @@ __global__ void __launch_bounds__(256) txv_k_challenge(VerifyArgs a) {
   a.ok_out[i] = 2;   // passed the scalar checks; K1b decides
 }
 
-template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult(VerifyArgs a) {
-  __shared__ uint32_t btab[kTableWords];
-  // stage the base-point table: 16-byte loads, all threads
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.btable);
-    uint4* dst = reinterpret_cast<uint4*>(btab);
-    for (int i = threadIdx.x; i < kTableWords / 4; i += BLOCK) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t stride = gridDim.x * BLOCK;
-  for (uint32_t idx = blockIdx.x * BLOCK + threadIdx.x; idx < a.n_work; idx += stride) {
+template <int W, typename PtrB>
+__device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, uint32_t first, uint32_t stride) {
+  for (uint32_t idx = first; idx < a.n_work; idx += stride) {
     const uint32_t i = a.order ? a.order[idx] : idx;
     if (a.ok_out[i] != 2) continue;
     const uint32_t v = a.val[i];
@@ -121,11 +118,11 @@ __global__ void __launch_bounds__(BLOCK) txv_k_scalarmult(VerifyArgs a) {
       uint32_t s[8], k[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-      sc_recode16(sp, s);
-      sc_recode16(kp, k);
+      sc_recode<W>(sp, s);
+      sc_recode<W>(kp, k);
     }
-    const uint32_t* ta = a.atables + (size_t)v * kTableWords;
-    ge_ext R = double_scalarmult_fixed(btab, ta, sp, kp, true);
+    const uint32_t* ta = a.atables + (size_t)v * Tab<W>::kWords;
+    ge_ext R = double_scalarmult_w<W>(btab, ta, sp, kp, true);
     uint32_t enc[8];
     ge_encode(enc, R);
     uint32_t diff = 0;
@@ -133,6 +130,25 @@ __global__ void __launch_bounds__(BLOCK) txv_k_scalarmult(VerifyArgs a) {
     for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * a.n_pad + i];
     a.ok_out[i] = diff == 0;
   }
+}
+
+// W = 4: the 55 KB B table is staged in LDS (8 waves per 512-thread block share it)
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w4(VerifyArgs a) {
+  __shared__ uint32_t btab[Tab<4>::kWords];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.btable);
+    uint4* dst = reinterpret_cast<uint4*>(btab);
+    for (int i = threadIdx.x; i < Tab<4>::kWords / 4; i += BLOCK) dst[i] = src[i];
+  }
+  __syncthreads();
+  scalarmult_loop<4>(a, (const uint32_t*)btab, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK);
+}
+
+// W = 8: both 396 KB tables are gathered from L2 / MALL (B is hot in every XCD's L2)
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w8(VerifyArgs a) {
+  scalarmult_loop<8>(a, a.btable, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK);
 }
 
 // ---------------------------------------------------------------- load generator
@@ -255,19 +271,30 @@ __global__ void txv_k_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t
 // ---------------------------------------------------------------- host launchers
 extern "C" {
 
-hipError_t txv_launch_build_tables(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
+hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
   if (!n_points) return hipSuccess;
-  hipLaunchKernelGGL(txv_k_build_tables, dim3(n_points), dim3(64), 0, st, pubs_le, n_points, tables,
-                     decode_ok, addr_words);
+  if (w == 8) {
+    const uint32_t lanes = n_points * Tab<8>::kPositions * ((Tab<8>::kEntries - 1) / 8);
+    hipLaunchKernelGGL(txv_k_build_tables<8>, dim3((lanes + 63) / 64), dim3(64), 0, st, pubs_le, n_points, tables,
+                       decode_ok, addr_words);
+  } else {
+    const uint32_t lanes = n_points * Tab<4>::kPositions;
+    hipLaunchKernelGGL(txv_k_build_tables<4>, dim3((lanes + 63) / 64), dim3(64), 0, st, pubs_le, n_points, tables,
+                       decode_ok, addr_words);
+  }
   return hipGetLastError();
 }
 
-hipError_t txv_launch_verify(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
+hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (!args->n) return hipSuccess;
   hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
-  if (args->n_work)
-    hipLaunchKernelGGL(txv_k_scalarmult<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+  if (args->n_work) {
+    if (w == 8)
+      hipLaunchKernelGGL(txv_k_scalarmult_w8<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+    else
+      hipLaunchKernelGGL(txv_k_scalarmult_w4<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+  }
   return hipGetLastError();
 }
 

@@ -24,7 +24,9 @@
 
 namespace {
 
-constexpr uint32_t kTableWords = 64 * 9 * 24;
+constexpr uint32_t kTableWords4 = 64 * 9 * 24;     // radix-16 table words per point
+constexpr uint32_t kTableWords8 = 32 * 129 * 24;   // radix-256 table words per point
+inline uint32_t table_words(int w) { return w == 8 ? kTableWords8 : kTableWords4; }
 constexpr uint32_t kSlots = 4;
 
 struct Slot {
@@ -65,7 +67,10 @@ struct txv_ctx {
   std::unordered_map<std::string, uint32_t> addr_index;
   uint32_t* d_pubs = nullptr; uint8_t* d_decode_ok = nullptr; uint32_t* d_atables = nullptr;
   uint32_t* d_addr = nullptr; int64_t* d_power = nullptr;
-  uint32_t* d_btable = nullptr;
+  uint32_t* d_btable = nullptr;    // B table for the verify window tab_w
+  uint32_t* d_btable4 = nullptr;   // radix-16 B table (keygen / sign)
+  uint32_t* d_btable8 = nullptr;
+  int tab_w = 8;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;
   uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
@@ -362,7 +367,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   }
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
-  HIP_TRY(c, txv_launch_verify(&va, verify_grid(c, s.n), c->stream));
+  HIP_TRY(c, txv_launch_verify(c->tab_w, &va, verify_grid(c, s.n), c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
   TallyArgs ta = tally_args(c, s);
   HIP_TRY(c, txv_launch_tally(&ta, c->stream));
@@ -408,13 +413,15 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
 int build_base_table(txv_ctx* c) {
   uint32_t* d_b = nullptr;
   int r;
-  if ((r = dalloc(c, &c->d_btable, kTableWords))) return r;
+  if ((r = dalloc(c, &c->d_btable4, kTableWords4)) || (r = dalloc(c, &c->d_btable8, kTableWords8))) return r;
   if ((r = dalloc(c, &d_b, 8))) return r;
   const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                           0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   HIP_TRY(c, hipMemcpyAsync(d_b, bw, 32, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, txv_launch_build_tables(d_b, 1, c->d_btable, nullptr, nullptr, c->stream));
+  HIP_TRY(c, txv_launch_build_tables(4, d_b, 1, c->d_btable4, nullptr, nullptr, c->stream));
+  HIP_TRY(c, txv_launch_build_tables(8, d_b, 1, c->d_btable8, nullptr, nullptr, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->d_btable = c->tab_w == 8 ? c->d_btable8 : c->d_btable4;
   dfree(d_b);
   return TXV_OK;
 }
@@ -436,6 +443,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (!c->cfg.max_validators) c->cfg.max_validators = 1024;
   if (!c->cfg.max_accepted) c->cfg.max_accepted = (uint32_t)std::min<uint64_t>((uint64_t)c->cfg.max_txs * 128, 1u << 28);
   if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
+  c->tab_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 8;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     delete c;
@@ -468,7 +476,7 @@ void txv_destroy(txv_ctx* c) {
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
-  dfree(c->d_btable); dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
+  dfree(c->d_btable4); dfree(c->d_btable8); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_acc_slot); dfree(c->d_first_tag); dfree(c->d_arena); dfree(c->d_arena_count); dfree(c->d_errflags);
   dfree(c->d_set_sum); dfree(c->d_set_cross); dfree(c->d_bitmap);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
@@ -501,13 +509,13 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   c->chain.assign(chain_id ? chain_id : "", chain_id ? chain_len : 0);
   int r;
   if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
-      (r = dalloc(c, &c->d_atables, (size_t)n * kTableWords)) || (r = dalloc(c, &c->d_addr, (size_t)n * 5)) ||
+      (r = dalloc(c, &c->d_atables, (size_t)n * table_words(c->tab_w))) || (r = dalloc(c, &c->d_addr, (size_t)n * 5)) ||
       (r = dalloc(c, &c->d_power, n)))
     return r;
   if (n) {
     HIP_TRY(c, hipMemcpyAsync(c->d_pubs, pubs32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_power, powers, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, txv_launch_build_tables(c->d_pubs, n, c->d_atables, c->d_decode_ok, c->d_addr, c->stream));
+    HIP_TRY(c, txv_launch_build_tables(c->tab_w, c->d_pubs, n, c->d_atables, c->d_decode_ok, c->d_addr, c->stream));
   }
   c->addrs.resize((size_t)n * 20);
   c->decode_ok.resize(n);
@@ -562,13 +570,13 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
     const uint32_t nu = (uint32_t)uniq.size();
     if (nu > c->tmp_cap) {
       if ((r = dalloc(c, &c->d_tmp_pubs, (size_t)nu * 8)) || (r = dalloc(c, &c->d_tmp_ok, nu)) ||
-          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * kTableWords)) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
+          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * table_words(c->tab_w))) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
         return r;
       c->tmp_cap = nu;
     }
     if (nu) {
       HIP_TRY(c, hipMemcpyAsync(c->d_tmp_pubs, ukeys.data(), (size_t)nu * 32, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(c, txv_launch_build_tables(c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
+      HIP_TRY(c, txv_launch_build_tables(c->tab_w, c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
     }
     key_addr.resize((size_t)nu * 20);
     if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr.data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
@@ -603,7 +611,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   pack_columns(s, v, lens);
   if ((r = upload_slot(c, s))) return r;
   VerifyArgs va = verify_args(c, s, kp, kok, ktab);
-  HIP_TRY(c, txv_launch_verify(&va, verify_grid(c, s.n), c->stream));
+  HIP_TRY(c, txv_launch_verify(c->tab_w, &va, verify_grid(c, s.n), c->stream));
   std::vector<uint8_t> ok(v->n);
   if (v->n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, v->n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -662,7 +670,7 @@ int txv_keygen(txv_ctx* c, const uint8_t* seeds32, uint32_t n, uint8_t* pubs_out
     return r;
   if (n) {
     HIP_TRY(c, hipMemcpyAsync(d_seeds, seeds32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, txv_launch_keygen(d_seeds, n, c->d_btable, c->d_sk_scal, c->d_sk_araw, c->d_sk_prefix, c->d_sk_pub,
+    HIP_TRY(c, txv_launch_keygen(d_seeds, n, c->d_btable4,c->d_sk_scal, c->d_sk_araw, c->d_sk_prefix, c->d_sk_pub,
                                  c->stream));
     if (pubs_out) HIP_TRY(c, hipMemcpyAsync(pubs_out, c->d_sk_pub, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
   }
@@ -697,7 +705,7 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
   if ((r = upload_slot(c, s))) return r;
   SignArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val;
-  a.prefix = c->d_sk_prefix; a.araw = c->d_sk_araw; a.pub = c->d_sk_pub; a.btable = c->d_btable; a.sig = s.d_sig;
+  a.prefix = c->d_sk_prefix; a.araw = c->d_sk_araw; a.pub = c->d_sk_pub; a.btable = c->d_btable4; a.sig = s.d_sig;
   HIP_TRY(c, txv_launch_sign(&a, c->stream));
   HIP_TRY(c, hipMemcpyAsync(s.h_sig, s.d_sig, (size_t)16 * s.n_pad * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -86,31 +86,6 @@ TXV_HD sc sc_reduce512(const uint32_t x[16]) {
   return out;
 }
 
-// Signed radix-16 recoding of a scalar < 2^253: a = sum_{i<64} e_i 16^i with e_i in [-8, 7].
-// Packed as 4-bit two's-complement nibbles, 8 per word (nibble i at word i/8, bits 4(i%8)).
-TXV_HD void sc_recode16(uint32_t packed[8], const uint32_t a[8]) {
-  uint32_t carry = 0;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    uint32_t out = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint32_t nib = ((a[w] >> (4 * j)) & 15u) + carry;   // [0, 16]
-      carry = (nib + 8u) >> 4;                            // 1 iff nib >= 8
-      uint32_t e = (nib - (carry << 4)) & 15u;            // nib - 16*carry as 4-bit two's complement
-      out |= e << (4 * j);
-    }
-    packed[w] = out;
-  }
-}
-
-// signed nibble i of a packed word (bits 4*j .. 4*j+3), sign-extended
-TXV_HD int sc_nibble(uint32_t word, int j) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_sbfe((int)word, 4 * j, 4);
-#else
-  return ((int)(word << (28 - 4 * j))) >> 28;
-#endif
-}
+// (signed radix-2^W recoding lives in ed25519_dev.h: sc_recode<W>, sc_digit<W>)
 
 }  // namespace txv

@@ -46,9 +46,10 @@ struct SignArgs {
 };
 
 extern "C" {
-hipError_t txv_launch_build_tables(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
+// w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
+hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
-hipError_t txv_launch_verify(const VerifyArgs* args, uint32_t grid, hipStream_t st);
+hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipStream_t st);
 hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_t* btable, uint32_t* scal,
                              uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);

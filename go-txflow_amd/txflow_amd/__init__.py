@@ -225,8 +225,11 @@ class Context:
     """Owns a txv_ctx (one GPU).  Thin wrapper; every call raises on infrastructure errors."""
 
     def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
-                 max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256):
-        cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes, 0)
+                 max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256, table_w: int = 8):
+        if table_w not in (4, 8):
+            raise ValueError("table_w must be 4 or 8")
+        cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes, 1 if table_w == 4 else 0)
+        self.table_w = table_w
         h = ctypes.c_void_p()
         rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

@@ -76,8 +76,11 @@ typedef struct {
   uint32_t max_validators;  /* default 1024 */
   uint32_t max_accepted;    /* accepted-signature arena capacity (default max_txs * 128) */
   uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
-  uint32_t flags;           /* reserved, 0 */
+  uint32_t flags;           /* TXV_CFG_* bits */
 } txv_config;
+/* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the default
+ * radix-256 tables (L2/MALL resident, 396 KB/validator, half the point additions) */
+#define TXV_CFG_TABLE_W4 0x1u
 
 /* A batch of TxVotes (types/tx_vote.go:48-55) in structure-of-arrays form. */
 typedef struct {

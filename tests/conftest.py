@@ -22,9 +22,10 @@ def oracle_lib():
     return oracle
 
 
-@pytest.fixture(scope="session")
-def gpu_ctx():
+@pytest.fixture(scope="session", params=[8, 4], ids=["w8", "w4"])
+def gpu_ctx(request):
+    """One context per verify-table window (radix-256 L2/MALL tables, radix-16 LDS tables)."""
     import txflow_amd as T
-    ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256)
+    ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256, table_w=request.param)
     yield ctx
     ctx.close()
