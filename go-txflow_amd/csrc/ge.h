@@ -71,15 +71,15 @@ TXV_HD ge_ext ge_dbl(const ge_ext& p) {
   return r;
 }
 
-// canonical 32-byte encoding as 8 little-endian words: y with bit 255 = parity(x)
-TXV_HD void ge_encode(uint32_t out[8], const ge_ext& p) {
-  fe zi = fe_invert(p.Z);
-  fe x = fe_canon(fe_mul(p.X, zi));
-  fe y = fe_canon(fe_mul(p.Y, zi));
+// canonical 32-byte encoding as 8 little-endian words: y with bit 255 = parity(x), given 1/Z
+TXV_HD void ge_encode_zinv(uint32_t out[8], const fe& X, const fe& Y, const fe& zi) {
+  fe x = fe_canon(fe_mul(X, zi));
+  fe y = fe_canon(fe_mul(Y, zi));
 #pragma unroll
   for (int i = 0; i < 8; ++i) out[i] = y.v[i];
   out[7] |= (x.v[0] & 1u) << 31;
 }
+TXV_HD void ge_encode(uint32_t out[8], const ge_ext& p) { ge_encode_zinv(out, p.X, p.Y, fe_invert(p.Z)); }
 
 // ref10 ExtendedGroupElement.FromBytes (x/crypto@c2843e01d9a2):
 // y = low 255 bits (y >= p accepted), reject only if (y^2-1)/(dy^2+1) has no square root,
