@@ -80,9 +80,10 @@ def main():
     ap.add_argument("--txs-per-gpu", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--table-w", type=int, default=8, choices=(4, 8))
-    ap.add_argument("--cpu-serial-votes", type=int, default=20_000)
-    ap.add_argument("--cpu-parallel-votes", type=int, default=200_000)
+    ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16),
+                    help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
+    ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
+    ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,7 +103,7 @@ def main():
     t_setup = time.perf_counter()
     max_txs = n_txs_global if world > 1 else args.txs_per_gpu
     ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
-                    max_validators=max(args.validators, 1), table_w=args.table_w)
+                    max_validators=max(args.validators, 1), table_w=args.table_w or None)
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
     ctx.stage(0, wl.batch)
@@ -118,19 +119,27 @@ def main():
 
     step_ms, verify_ms, tally_ms = [], [], []
 
+    phases = {"reset": [], "run": [], "fetch": [], "gather": []}
+
     def step(record: bool):
         t0 = time.perf_counter()
         ctx.reset_tally()
+        t1 = time.perf_counter()
         ms = ctx.run_staged(0, timed=True)
+        t2 = time.perf_counter()
         st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1)
+        t3 = time.perf_counter()
         if dist is not None:
             ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)
             dist.all_gather_into_tensor(gathered, bm_local)
             torch.cuda.synchronize()
+        t4 = time.perf_counter()
         if record:
-            step_ms.append((time.perf_counter() - t0) * 1e3)
+            step_ms.append((t4 - t0) * 1e3)
             verify_ms.append(ms[0])
             tally_ms.append(ms[1])
+            for k, a_, b_ in (("reset", t0, t1), ("run", t1, t2), ("fetch", t2, t3), ("gather", t3, t4)):
+                phases[k].append((b_ - a_) * 1e3)
         return st, ev
 
     for _ in range(args.warmup):
@@ -173,16 +182,28 @@ def main():
     t_ms = statistics.median(tally_ms)
     if rank == 0:
         add_rate, mad_rate = ctx.valu_probe()
-        achieved = wl.n * W_ALG / (v_ms * 1e-3) / 1e12
         peak = add_rate / 1e12
-        traffic = None
+        # roofline.achieved = algorithmic work per launch / verify launch time: SURVEY.md §8d's
+        # W_alg = 2.5e5 int32 lane-ops per verified vote x votes per launch / (K1a+K1b) HIP-event
+        # time.  The executed work (rocprofv3 PMC pass of this kernel build, committed in
+        # profiles/pmc_verify.json: SQ_INSTS_VALU with 64-bit-class ops counted twice, in
+        # full-rate lane-op issue slots) is reported beside it as exec_*; traffic = HBM bytes
+        # per launch from FETCH_SIZE (x2 gfx950 correction) + WRITE_SIZE.
+        w_exec, traffic, pmc_src, pmc_w = None, None, None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
         if os.path.exists(pmc):
             try:
                 with open(pmc) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch")
+                    pj = json.load(f)
+                pmc_w = pj.get("table_window")
+                if pmc_w == ctx.table_w:
+                    w_exec = pj.get("verify_w_exec_lane_slots_per_vote")
+                    traffic = pj.get("hbm_bytes_per_launch")
+                    pmc_src = pj.get("source")
             except Exception:
-                traffic = None
+                pass
+        achieved = wl.n * W_ALG / (v_ms * 1e-3) / 1e12
+        exec_rate = wl.n * w_exec / (v_ms * 1e-3) / 1e12 if w_exec else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = min(args.cpu_threads, os.cpu_count() or 1)
@@ -203,14 +224,20 @@ def main():
             "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
                                     f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
                                     f"100 validators, ~1M votes/GPU, RCCL bitmap all-gather"),
-                       "validators": args.validators, "table_window": args.table_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
+                       "validators": args.validators, "table_window": ctx.table_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
                        "parallelism": f"shard{world}"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
+            "step_phases_ms_p50": {k: round(statistics.median(v), 3) for k, v in phases.items() if v},
             "verify_kernel_ms": round(v_ms, 3),
             "tally_kernels_ms": round(t_ms, 3),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 3),
                          "unit": "Tlane-op/s (int32 VALU)", "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "kernel": "txv_k_verify", "w_alg_lane_ops_per_vote": W_ALG,
+                         "kernel": "txv_k_challenge + txv_k_scalarmult (verify pair)",
+                         "alg_lane_ops_per_vote": W_ALG, "alg_source": "SURVEY.md §8d W_alg (Straus, w=8 NAF)",
+                         "exec_lane_slots_per_vote": w_exec,
+                         "exec_achieved": None if exec_rate is None else round(exec_rate, 3),
+                         "exec_frac": None if exec_rate is None else round(exec_rate / peak, 4),
+                         "pmc_source": pmc_src,
                          "peak_source": "live v_add_u32 issue-rate probe (txv_valu_probe)",
                          "mad_u64_u32_peak": round(mad_rate / 1e12, 3),
                          "tally_GBps": round(wl.n * TALLY_BYTES_PER_VOTE / (t_ms * 1e-3) / 1e9, 1)},

@@ -10,8 +10,10 @@
 // (j = 0 the identity), so [s]B + [k](-A) = sum_i T_B[i][s_i] - T_A[i][k_i] with signed
 // digits.  This is exact group arithmetic, hence the same point and encoding as x/crypto's
 // sliding-window GeDoubleScalarMultVartime.
-//   W = 4: 64 positions x 9 entries x 96 B =  55,296 B per point (B fits in LDS)
-//   W = 8: 32 positions x 129 entries x 96 B = 396,288 B per point (L2/MALL resident)
+//   W = 4:  64 positions x    9 entries x 96 B =    55,296 B per point (B fits in LDS)
+//   W = 8:  32 positions x  129 entries x 96 B =   396,288 B per point (L2/MALL resident)
+//   W = 12: 22 positions x 2049 entries x 96 B = 4,327,488 B per point (MALL/HBM resident)
+// 2 * ceil(256/W) mixed additions per verification: 128 / 64 / 44.
 #pragma once
 #include "fe.h"
 #include "sc.h"
@@ -27,7 +29,6 @@ struct Tab {
   static constexpr int kPositions = (256 + W - 1) / W;
   static constexpr int kEntries = (1 << (W - 1)) + 1;
   static constexpr int kWords = kPositions * kEntries * kEntryWords;
-  static constexpr int kDigitsPerWord = 32 / W;
 };
 
 // legacy W = 4 names (keygen/sign and the host emulation)
@@ -80,34 +81,6 @@ TXV_HD void sha512_prefixed(uint32_t digest_le[16], const uint64_t* pre, int pre
   }
 }
 
-// Signed radix-2^W recoding of a scalar < 2^253: a = sum_i e_i 2^(W i), e_i in [-2^(W-1), 2^(W-1)),
-// packed W bits per digit (two's complement), 32/W digits per word.
-template <int W>
-TXV_HD void sc_recode(uint32_t packed[8], const uint32_t a[8]) {
-  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
-  uint32_t carry = 0;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    uint32_t out = 0;
-#pragma unroll
-    for (int j = 0; j < 32 / W; ++j) {
-      const uint32_t d = ((a[w] >> (W * j)) & mask) + carry;   // [0, 2^W]
-      carry = (d + half) >> W;                                  // 1 iff d >= 2^(W-1)
-      out |= ((d - (carry << W)) & mask) << (W * j);
-    }
-    packed[w] = out;
-  }
-}
-
-template <int W>
-TXV_HD int sc_digit(uint32_t word, int j) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_sbfe((int)word, W * j, W);
-#else
-  return ((int)(word << (32 - W - W * j))) >> (32 - W);
-#endif
-}
-
 // table entry fetch: T[pos][idx] from a flat word array
 template <int W, typename Ptr>
 TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
@@ -124,39 +97,43 @@ TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
 template <typename Ptr>
 TXV_HD ge_niels load_entry(Ptr tab, int pos, int idx) { return load_entry_w<4>(tab, pos, idx); }
 
-// sum_i T_B[i][s_i] + T_A[i][-k_i]   (digits of k are negated, giving [k](-A))
+// Streaming signed radix-2^W digit of a 256-bit scalar held in 8 words: returns the low
+// digit in [-2^(W-1), 2^(W-1)) (with the running carry) and shifts the scalar right by W.
+// Works for any W <= 16 (digits may straddle words); ~10 VALU ops per digit.
+template <int W>
+TXV_HD int next_digit(uint32_t s[8], uint32_t& carry) {
+  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
+  const uint32_t d = (s[0] & mask) + carry;        // [0, 2^W]
+  carry = (d + half) >> W;                          // 1 iff d >= 2^(W-1)
+#pragma unroll
+  for (int i = 0; i < 7; ++i) s[i] = (s[i] >> W) | (s[i + 1] << (32 - W));
+  s[7] >>= W;
+  return (int)d - (int)(carry << W);
+}
+
+// sum_i T_B[i][s_i] + T_A[i][-k_i] over raw scalars s, k < 2^253 (digits of k negated,
+// giving [k](-A)); digits are produced on the fly, so any window W <= 16 works.
 template <int W, typename PtrB, typename PtrA>
-TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_packed[8], const uint32_t k_packed[8],
-                                  bool use_a) {
-  constexpr int D = Tab<W>::kDigitsPerWord;
-  constexpr int WORDS = (Tab<W>::kPositions + D - 1) / D;
+TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {
   ge_ext P = ge_identity();
-  uint32_t ps[8], pk[8];
+  uint32_t s[8], k[8], cs = 0, ck = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { ps[i] = s_packed[i]; pk[i] = k_packed[i]; }
-  for (int w = 0; w < WORDS; ++w) {
-    const uint32_t ws = ps[0], wk = pk[0];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) { ps[i] = ps[i + 1]; pk[i] = pk[i + 1]; }
-    for (int j = 0; j < D; ++j) {
-      const int pos = D * w + j;
-      const int ds = sc_digit<W>(ws, j);
-      P = ge_madd(P, load_entry_w<W>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
-      if (use_a) {
-        const int dk = sc_digit<W>(wk, j);
-        P = ge_madd(P, load_entry_w<W>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
-      }
+  for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
+  for (int pos = 0; pos < Tab<W>::kPositions; ++pos) {
+    const int ds = next_digit<W>(s, cs);
+    P = ge_madd(P, load_entry_w<W>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
+    if (use_a) {
+      const int dk = next_digit<W>(k, ck);
+      P = ge_madd(P, load_entry_w<W>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
     }
   }
   return P;
 }
 
-// legacy W = 4 entry points
-TXV_HD void sc_recode16(uint32_t packed[8], const uint32_t a[8]) { sc_recode<4>(packed, a); }
+// [s]B (+ [k](-A)) with the radix-16 tables (keygen / sign / host emulation)
 template <typename PtrB, typename PtrA>
-TXV_HD ge_ext double_scalarmult_fixed(PtrB tb, PtrA ta, const uint32_t s_packed[8], const uint32_t k_packed[8],
-                                      bool use_a) {
-  return double_scalarmult_w<4>(tb, ta, s_packed, k_packed, use_a);
+TXV_HD ge_ext double_scalarmult_fixed(PtrB tb, PtrA ta, const uint32_t s[8], const uint32_t k[8], bool use_a) {
+  return double_scalarmult_w<4>(tb, ta, s, k, use_a);
 }
 
 // [m]P for a small positive m (double-and-add from the top bit)

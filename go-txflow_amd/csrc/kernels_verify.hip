@@ -27,8 +27,8 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
                                                           uint32_t* __restrict__ addr_words) {
   constexpr int chunks = (Tab<W>::kEntries - 1) / 8;
   constexpr int per_point = Tab<W>::kPositions * chunks;
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t pt = gid / per_point;
+  const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint32_t pt = (uint32_t)(gid / per_point);
   const int t = (int)(gid % per_point);
   if (pt >= n_points) return;
   const int pos = t / chunks, c = t % chunks;
@@ -113,16 +113,11 @@ __device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, 
     const uint32_t i = a.order ? a.order[idx] : idx;
     if (a.ok_out[i] != 2) continue;
     const uint32_t v = a.val[i];
-    uint32_t sp[8], kp[8];
-    {
-      uint32_t s[8], k[8];
+    uint32_t s[8], k[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-      sc_recode<W>(sp, s);
-      sc_recode<W>(kp, k);
-    }
+    for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
     const uint32_t* ta = a.atables + (size_t)v * Tab<W>::kWords;
-    ge_ext R = double_scalarmult_w<W>(btab, ta, sp, kp, true);
+    ge_ext R = double_scalarmult_w<W>(btab, ta, s, k, true);
     uint32_t enc[8];
     ge_encode(enc, R);
     uint32_t diff = 0;
@@ -134,7 +129,7 @@ __device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, 
 
 // W = 4: the 55 KB B table is staged in LDS (8 waves per 512-thread block share it)
 template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w4(VerifyArgs a) {
+__global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_w4(VerifyArgs a) {
   __shared__ uint32_t btab[Tab<4>::kWords];
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.btable);
@@ -145,17 +140,25 @@ __global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w4(VerifyArgs a) {
   scalarmult_loop<4>(a, (const uint32_t*)btab, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK);
 }
 
-// W = 8: both 396 KB tables are gathered from L2 / MALL (B is hot in every XCD's L2).
-// Each lane verifies two votes and shares ONE field inversion between them (Montgomery's
-// trick: 1/(Z0 Z1) then 1/Z0 = Z1/(Z0 Z1), 1/Z1 = Z0/(Z0 Z1)), saving ~1 inversion
-// (~250 squarings) per vote pair.  The first vote's (X, Y, Z) waits in LDS (column-major,
-// conflict-free) while the second is computed, so it costs no VGPRs.
-template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w8(VerifyArgs a) {
+// W >= 8: both tables are gathered from L2 / MALL / HBM (the B table is hot in every XCD's
+// L2 at W = 8).  Each lane verifies two votes and shares ONE field inversion between them
+// (Montgomery's trick: 1/(Z0 Z1) then 1/Z0 = Z1/(Z0 Z1), 1/Z1 = Z0/(Z0 Z1)), saving ~1
+// inversion (~250 squarings) per vote pair.  The first vote's (X, Y, Z) waits in LDS
+// (column-major, conflict-free) while the second is computed, so it costs no VGPRs.
+template <int BLOCK, int W>
+__global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(VerifyArgs a) {
   __shared__ uint32_t park[24][BLOCK];
-  const uint32_t stride = gridDim.x * BLOCK;
+  // XCD-aware split (speed only): blocks b and b+8 share an XCD under round-robin dispatch,
+  // so the blocks of one XCD walk one contiguous eighth of the validator-sorted work list.
+  // At any moment an XCD then touches a handful of validators' 396 KB A tables, which fit
+  // its 4 MB L2, instead of slices of all of them (MI355X_MICROARCH.md §Workgroup dispatch).
   const uint32_t n_pairs = (a.n_work + 1) / 2;
-  for (uint32_t pr = blockIdx.x * BLOCK + threadIdx.x; pr < n_pairs; pr += stride) {
+  const uint32_t groups = gridDim.x >= 8 ? 8u : 1u;
+  const uint32_t grp = blockIdx.x % groups, blocks_in_grp = gridDim.x / groups + (grp < gridDim.x % groups);
+  const uint32_t chunk = (n_pairs + groups - 1) / groups;
+  const uint32_t lo = grp * chunk, hi = min(n_pairs, lo + chunk);
+  const uint32_t stride = blocks_in_grp * BLOCK;
+  for (uint32_t pr = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; pr < hi; pr += stride) {
     uint32_t vi[2];
     bool act[2];
 #pragma unroll
@@ -170,15 +173,10 @@ __global__ void __launch_bounds__(BLOCK) txv_k_scalarmult_w8(VerifyArgs a) {
       const uint32_t i = vi[h];
       if (act[h]) {
         const uint32_t v = a.val[i];
-        uint32_t sp[8], kp[8];
-        {
-          uint32_t s[8], k[8];
+        uint32_t s[8], k[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-          sc_recode<8>(sp, s);
-          sc_recode<8>(kp, k);
-        }
-        R = double_scalarmult_w<8>(a.btable, a.atables + (size_t)v * Tab<8>::kWords, sp, kp, true);
+        for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
+        R = double_scalarmult_w<W>(a.btable, a.atables + (size_t)v * Tab<W>::kWords, s, k, true);
       } else {
         R = ge_identity();
       }
@@ -235,10 +233,8 @@ __global__ void __launch_bounds__(64) txv_k_keygen(const uint32_t* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] = j < 8 ? h[j] : 0u;
   sc a = sc_reduce512(x);
-  uint32_t ap[8];
-  sc_recode16(ap, a.v);
   uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  ge_ext P = double_scalarmult_fixed(btable, btable, ap, zero, false);
+  ge_ext P = double_scalarmult_fixed(btable, btable, a.v, zero, false);
   uint32_t enc[8];
   ge_encode(enc, P);
 #pragma unroll
@@ -262,10 +258,8 @@ __global__ void __launch_bounds__(64) txv_k_sign(SignArgs a) {
   uint32_t h[16];
   sha512_prefixed(h, pre, 4, m);
   sc r = sc_reduce512(h);
-  uint32_t rp[8];
-  sc_recode16(rp, r.v);
   uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  ge_ext R = double_scalarmult_fixed(a.btable, a.btable, rp, zero, false);
+  ge_ext R = double_scalarmult_fixed(a.btable, a.btable, r.v, zero, false);
   uint32_t Rw[8];
   ge_encode(Rw, R);
 #pragma unroll
@@ -334,17 +328,29 @@ __global__ void txv_k_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t
 // ---------------------------------------------------------------- host launchers
 extern "C" {
 
+}  // extern "C"
+
+template <int W>
+static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables, uint8_t* decode_ok,
+                         uint32_t* addr_words, hipStream_t st) {
+  const uint64_t lanes = (uint64_t)n_points * Tab<W>::kPositions * ((Tab<W>::kEntries - 1) / 8);
+  hipLaunchKernelGGL(txv_k_build_tables<W>, dim3((uint32_t)((lanes + 63) / 64)), dim3(64), 0, st, pubs_le, n_points,
+                     tables, decode_ok, addr_words);
+}
+
+extern "C" {
+
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
   if (!n_points) return hipSuccess;
-  if (w == 8) {
-    const uint32_t lanes = n_points * Tab<8>::kPositions * ((Tab<8>::kEntries - 1) / 8);
-    hipLaunchKernelGGL(txv_k_build_tables<8>, dim3((lanes + 63) / 64), dim3(64), 0, st, pubs_le, n_points, tables,
-                       decode_ok, addr_words);
-  } else {
-    const uint32_t lanes = n_points * Tab<4>::kPositions;
-    hipLaunchKernelGGL(txv_k_build_tables<4>, dim3((lanes + 63) / 64), dim3(64), 0, st, pubs_le, n_points, tables,
-                       decode_ok, addr_words);
+  switch (w) {
+    case 4: launch_build<4>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 8: launch_build<8>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 10: launch_build<10>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 12: launch_build<12>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 14: launch_build<14>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -353,10 +359,16 @@ hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipSt
   if (!args->n) return hipSuccess;
   hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
   if (args->n_work) {
-    if (w == 8)
-      hipLaunchKernelGGL(txv_k_scalarmult_w8<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
-    else
-      hipLaunchKernelGGL(txv_k_scalarmult_w4<TXV_VERIFY_BLOCK>, dim3(grid), dim3(TXV_VERIFY_BLOCK), 0, st, *args);
+    constexpr int B = TXV_VERIFY_BLOCK;
+    switch (w) {
+      case 4: hipLaunchKernelGGL(txv_k_scalarmult_w4<B>, dim3(grid), dim3(B), 0, st, *args); break;
+      case 8: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 8>), dim3(grid), dim3(B), 0, st, *args); break;
+      case 10: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 10>), dim3(grid), dim3(B), 0, st, *args); break;
+      case 12: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 12>), dim3(grid), dim3(B), 0, st, *args); break;
+      case 14: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 14>), dim3(grid), dim3(B), 0, st, *args); break;
+      case 16: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 16>), dim3(grid), dim3(B), 0, st, *args); break;
+      default: return hipErrorInvalidValue;
+    }
   }
   return hipGetLastError();
 }

@@ -24,9 +24,10 @@
 
 namespace {
 
-constexpr uint32_t kTableWords4 = 64 * 9 * 24;     // radix-16 table words per point
-constexpr uint32_t kTableWords8 = 32 * 129 * 24;   // radix-256 table words per point
-inline uint32_t table_words(int w) { return w == 8 ? kTableWords8 : kTableWords4; }
+// fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 24
+inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 24; }
+constexpr uint32_t kTableWords4 = 64 * 9 * 24;
+inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16; }
 constexpr uint32_t kSlots = 4;
 
 struct Slot {
@@ -69,10 +70,13 @@ struct txv_ctx {
   uint32_t* d_addr = nullptr; int64_t* d_power = nullptr;
   uint32_t* d_btable = nullptr;    // B table for the verify window tab_w
   uint32_t* d_btable4 = nullptr;   // radix-16 B table (keygen / sign)
-  uint32_t* d_btable8 = nullptr;
-  int tab_w = 8;
+  uint32_t* d_btable8 = nullptr;   // B table for window btable_w (>= 8)
+  int btable_w = 0;
+  int cfg_w = 0;                   // requested window, 0 = auto (largest that fits the budget)
+  int tab_w = 0;                   // window of the current validator tables
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;
+  int tmp_w = 0;
   uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
   // tally state
   std::unordered_map<std::string, uint32_t> tx_index;
@@ -410,19 +414,43 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
   return TXV_OK;
 }
 
-int build_base_table(txv_ctx* c) {
+// base-point table for window w (w = 4 lives in d_btable4, built at init for keygen/sign)
+int build_base_table(txv_ctx* c, int w) {
   uint32_t* d_b = nullptr;
   int r;
-  if ((r = dalloc(c, &c->d_btable4, kTableWords4)) || (r = dalloc(c, &c->d_btable8, kTableWords8))) return r;
   if ((r = dalloc(c, &d_b, 8))) return r;
   const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                           0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   HIP_TRY(c, hipMemcpyAsync(d_b, bw, 32, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, txv_launch_build_tables(4, d_b, 1, c->d_btable4, nullptr, nullptr, c->stream));
-  HIP_TRY(c, txv_launch_build_tables(8, d_b, 1, c->d_btable8, nullptr, nullptr, c->stream));
+  if (w == 4) {
+    if ((r = dalloc(c, &c->d_btable4, kTableWords4))) return r;
+    HIP_TRY(c, txv_launch_build_tables(4, d_b, 1, c->d_btable4, nullptr, nullptr, c->stream));
+  } else if (c->btable_w != w) {
+    if ((r = dalloc(c, &c->d_btable8, table_words(w)))) return r;
+    HIP_TRY(c, txv_launch_build_tables(w, d_b, 1, c->d_btable8, nullptr, nullptr, c->stream));
+    c->btable_w = w;
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  c->d_btable = c->tab_w == 8 ? c->d_btable8 : c->d_btable4;
   dfree(d_b);
+  return TXV_OK;
+}
+
+// Largest window whose per-validator tables for n keys fit the table budget (more table
+// memory = fewer point additions per vote: 2 * ceil(256 / W)).
+int choose_window(const txv_ctx* c, uint32_t n) {
+  if (c->cfg_w) return c->cfg_w;
+  const uint64_t budget = (uint64_t)c->cfg.table_budget_mb << 20;
+  for (int w : {16, 14, 12, 10, 8})
+    if ((uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
+  return 4;
+}
+
+// make tab_w = w current: its B table exists and d_btable points at it
+int select_window(txv_ctx* c, int w) {
+  int r;
+  if (w != 4 && (r = build_base_table(c, w))) return r;
+  c->tab_w = w;
+  c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   return TXV_OK;
 }
 
@@ -443,7 +471,10 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (!c->cfg.max_validators) c->cfg.max_validators = 1024;
   if (!c->cfg.max_accepted) c->cfg.max_accepted = (uint32_t)std::min<uint64_t>((uint64_t)c->cfg.max_txs * 128, 1u << 28);
   if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
-  c->tab_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 8;
+  if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 8192;
+  c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
+  if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
+  if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     delete c;
@@ -459,7 +490,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->n_cus = prop.multiProcessorCount;
-  if (build_base_table(c) != TXV_OK) { txv_destroy(c); return TXV_EDEVICE; }
+  if (build_base_table(c, 4) != TXV_OK) { txv_destroy(c); return TXV_EDEVICE; }
   *out = c;
   return TXV_OK;
 }
@@ -508,6 +539,7 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   c->quorum = c->total * 2 / 3 + 1;
   c->chain.assign(chain_id ? chain_id : "", chain_id ? chain_len : 0);
   int r;
+  if ((r = select_window(c, choose_window(c, n)))) return r;
   if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
       (r = dalloc(c, &c->d_atables, (size_t)n * table_words(c->tab_w))) || (r = dalloc(c, &c->d_addr, (size_t)n * 5)) ||
       (r = dalloc(c, &c->d_power, n)))
@@ -553,6 +585,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
   // key registry for this call
   const uint32_t* kp = c->d_pubs; const uint8_t* kok = c->d_decode_ok; const uint32_t* ktab = c->d_atables;
+  int w_keys = c->tab_w;
   std::vector<uint8_t> key_addr;
   if (pubs32) {
     std::unordered_map<std::string, uint32_t> uniq;
@@ -568,15 +601,25 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
       kidx[i] = it->second;
     }
     const uint32_t nu = (uint32_t)uniq.size();
-    if (nu > c->tmp_cap) {
+    // caller-supplied keys get throw-away tables: the registry's window if they fit the budget
+    // (its B table already exists), else the 55 KB radix-16 tables.  Without a registry the
+    // window is chosen for these keys alone.
+    if (c->tab_w) {
+      w_keys = (uint64_t)nu * table_words(c->tab_w) * 4 <= ((uint64_t)c->cfg.table_budget_mb << 20) ? c->tab_w : 4;
+    } else {
+      w_keys = choose_window(c, nu);
+      if (w_keys != 4 && (r = build_base_table(c, w_keys))) return r;
+    }
+    if (nu > c->tmp_cap || w_keys != c->tmp_w) {
       if ((r = dalloc(c, &c->d_tmp_pubs, (size_t)nu * 8)) || (r = dalloc(c, &c->d_tmp_ok, nu)) ||
-          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * table_words(c->tab_w))) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
+          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * table_words(w_keys))) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
         return r;
       c->tmp_cap = nu;
+      c->tmp_w = w_keys;
     }
     if (nu) {
       HIP_TRY(c, hipMemcpyAsync(c->d_tmp_pubs, ukeys.data(), (size_t)nu * 32, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(c, txv_launch_build_tables(c->tab_w, c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
+      HIP_TRY(c, txv_launch_build_tables(w_keys, c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
     }
     key_addr.resize((size_t)nu * 20);
     if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr.data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
@@ -611,7 +654,8 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   pack_columns(s, v, lens);
   if ((r = upload_slot(c, s))) return r;
   VerifyArgs va = verify_args(c, s, kp, kok, ktab);
-  HIP_TRY(c, txv_launch_verify(c->tab_w, &va, verify_grid(c, s.n), c->stream));
+  va.btable = w_keys == 4 ? c->d_btable4 : c->d_btable8;
+  HIP_TRY(c, txv_launch_verify(w_keys, &va, verify_grid(c, s.n), c->stream));
   std::vector<uint8_t> ok(v->n);
   if (v->n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, v->n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -806,6 +850,8 @@ int txv_valu_probe(txv_ctx* c, double* add_lane_ops_per_s, double* mad_lane_ops_
   dfree(d);
   return TXV_OK;
 }
+
+int txv_table_window(txv_ctx* c) { return c ? c->tab_w : TXV_EINVAL; }
 
 int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op) {
   if (!c || !a || !b || !out) return TXV_EINVAL;

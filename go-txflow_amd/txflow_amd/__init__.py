@@ -50,7 +50,8 @@ class TxvInfraError(RuntimeError):
 class _Cfg(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_batch", ctypes.c_uint32), ("max_txs", ctypes.c_uint32),
                 ("max_validators", ctypes.c_uint32), ("max_accepted", ctypes.c_uint32),
-                ("max_msg_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("max_msg_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("table_budget_mb", ctypes.c_uint32)]
 
 
 class _Votes(ctypes.Structure):
@@ -62,6 +63,9 @@ class _Votes(ctypes.Structure):
 
 class _Event(ctypes.Structure):
     _fields_ = [("vote_index", ctypes.c_uint32), ("tx_index", ctypes.c_uint32), ("sum", ctypes.c_int64)]
+
+
+EVENT_DTYPE = np.dtype([("vote_index", "<u4"), ("tx_index", "<u4"), ("sum", "<i8")])   # txv_commit_event
 
 
 _lib = None
@@ -101,6 +105,7 @@ def lib():
             "txv_fe_selftest": ([vp, vp, vp, vp, u32, ctypes.c_int], ctypes.c_int),
             "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+            "txv_table_window": ([vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -115,7 +120,7 @@ EXPORTED_SYMBOLS = [
     "txv_get_validator_info", "txv_verify_batch", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest",
-    "txv_copy_commit_bitmap", "txv_valu_probe"]
+    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -225,11 +230,14 @@ class Context:
     """Owns a txv_ctx (one GPU).  Thin wrapper; every call raises on infrastructure errors."""
 
     def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
-                 max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256, table_w: int = 8):
-        if table_w not in (4, 8):
-            raise ValueError("table_w must be 4 or 8")
-        cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes, 1 if table_w == 4 else 0)
-        self.table_w = table_w
+                 max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
+                 table_w: int | None = None, table_budget_mb: int = 0):
+        """table_w: fixed-base window (4, 8, 10, 12, 14, 16) or None = the largest whose
+        per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
+        if table_w not in (None, 4, 8, 10, 12, 14, 16):
+            raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16")
+        cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
+                   ((table_w or 0) & 0xFF) << 8, table_budget_mb)
         h = ctypes.c_void_p()
         rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
@@ -284,12 +292,12 @@ class Context:
     def add_votes(self, batch: VoteBatch, ev_cap: int = 0):
         out = np.zeros(max(batch.n, 1), np.uint8)
         ev_cap = ev_cap or max(batch.n, 1)
-        evs = (_Event * ev_cap)()
+        evs = np.zeros(ev_cap, EVENT_DTYPE)
         nev = ctypes.c_uint32()
         vs = batch.c_struct()
-        self._chk(lib().txv_add_votes(self._h, ctypes.byref(vs), out.ctypes.data, evs, ev_cap, ctypes.byref(nev)),
-                  "txv_add_votes")
-        return out[:batch.n], [(e.vote_index, e.tx_index, e.sum) for e in evs[:min(nev.value, ev_cap)]]
+        self._chk(lib().txv_add_votes(self._h, ctypes.byref(vs), out.ctypes.data, evs.ctypes.data, ev_cap,
+                                      ctypes.byref(nev)), "txv_add_votes")
+        return out[:batch.n], evs[:min(nev.value, ev_cap)]
 
     def query_tx(self, txhash: bytes):
         s = ctypes.c_int64(); m = ctypes.c_uint8()
@@ -329,10 +337,11 @@ class Context:
     def fetch_staged(self, slot: int, n: int, ev_cap: int = 0):
         out = np.zeros(max(n, 1), np.uint8)
         ev_cap = ev_cap or max(n, 1)
-        evs = (_Event * ev_cap)()
+        evs = np.zeros(ev_cap, EVENT_DTYPE)
         nev = ctypes.c_uint32()
-        self._chk(lib().txv_fetch_staged(self._h, slot, out.ctypes.data, evs, ev_cap, ctypes.byref(nev)), "fetch")
-        return out[:n], [(e.vote_index, e.tx_index, e.sum) for e in evs[:min(nev.value, ev_cap)]]
+        self._chk(lib().txv_fetch_staged(self._h, slot, out.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev)),
+                  "fetch")
+        return out[:n], evs[:min(nev.value, ev_cap)]
 
     def commit_bitmap(self):
         p = ctypes.c_void_p(); nb = ctypes.c_uint64()
@@ -347,6 +356,11 @@ class Context:
         a = ctypes.c_double(); m = ctypes.c_double()
         self._chk(lib().txv_valu_probe(self._h, ctypes.byref(a), ctypes.byref(m)), "valu probe")
         return a.value, m.value
+
+    @property
+    def table_w(self) -> int:
+        """fixed-base window of the validator tables in use (0 before set_validators)"""
+        return int(lib().txv_table_window(self._h))
 
     def reset_tally(self):
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")
@@ -407,8 +421,8 @@ class TxFlow:
     def AddVotes(self, votes: Sequence[Optional[TxVote]]):
         batch = VoteBatch.from_votes(votes)
         status, events = self.ctx.add_votes(batch)
-        for vi, _ti, s in events:
-            self.commits.append((votes[vi].TxHash, s))
+        for e in events:
+            self.commits.append((votes[int(e["vote_index"])].TxHash, int(e["sum"])))
         return status
 
     def TryAddVote(self, vote: TxVote):

@@ -77,10 +77,17 @@ typedef struct {
   uint32_t max_accepted;    /* accepted-signature arena capacity (default max_txs * 128) */
   uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
   uint32_t flags;           /* TXV_CFG_* bits */
+  uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 8192):
+                               the default window is the largest of 16/14/12/10/8 that fits */
 } txv_config;
 /* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the default
  * radix-256 tables (L2/MALL resident, 396 KB/validator, half the point additions) */
 #define TXV_CFG_TABLE_W4 0x1u
+/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14 or 16; 0 = auto by table_budget_mb):
+ * per validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB, and
+ * 128 / 64 / 52 / 44 / 38 / 32 point additions per verified vote */
+#define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
+#define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 
 /* A batch of TxVotes (types/tx_vote.go:48-55) in structure-of-arrays form. */
 typedef struct {
@@ -161,6 +168,8 @@ int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 int txv_copy_commit_bitmap(txv_ctx* ctx, void* dst_dev, uint64_t bytes);
 /* measured integer-VALU issue rates of this device (lane-ops/s): v_add_u32 and v_mad_u64_u32 */
 int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
+/* fixed-base window of the current validator tables (4..16), 0 before txv_set_validators */
+int txv_table_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids
  * already assigned stay assigned (their sets read as empty) */
 int txv_reset_tally(txv_ctx* ctx);

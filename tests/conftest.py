@@ -22,9 +22,10 @@ def oracle_lib():
     return oracle
 
 
-@pytest.fixture(scope="session", params=[8, 4], ids=["w8", "w4"])
+@pytest.fixture(scope="session", params=[None, 4, 8, 12], ids=["wauto", "w4", "w8", "w12"])
 def gpu_ctx(request):
-    """One context per verify-table window (radix-256 L2/MALL tables, radix-16 LDS tables)."""
+    """One context per verify-table window: auto (radix-2^16 for the small test registries),
+    radix-16 LDS-resident B table, radix-256 and radix-4096 L2/MALL tables."""
     import txflow_amd as T
     ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256, table_w=request.param)
     yield ctx

@@ -82,10 +82,7 @@ int emu_verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const ui
   uint32_t dig[16];
   sha512_prefixed(dig, pre, 8, m);
   sc k = sc_reduce512(dig);
-  uint32_t sp[8], kp[8];
-  sc_recode16(sp, s + 8);
-  sc_recode16(kp, k.v);
-  ge_ext R = double_scalarmult_fixed(btab.data(), atab.data(), sp, kp, true);
+  ge_ext R = double_scalarmult_fixed(btab.data(), atab.data(), s + 8, k.v, true);
   uint32_t enc[8];
   ge_encode(enc, R);
   return memcmp(enc, s, 32) == 0;

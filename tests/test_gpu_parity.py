@@ -221,3 +221,45 @@ def test_add_votes_matches_sequential_oracle(gpu_ctx, oracle_lib):
             continue
         assert gpu_ctx.query_tx(v.TxHash.encode()) == flow.query(v.TxHash.encode())
     assert gpu_ctx.num_tx_sets() == flow.num_sets()
+
+
+def _table_mb(w: int) -> float:
+    return -(-256 // w) * ((1 << (w - 1)) + 1) * 24 * 4 / 2 ** 20
+
+
+@pytest.mark.parametrize("budget_mb,exp_w", [(1, 4), (100, 12), (0, 16)])
+def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
+    """Auto window = largest of 16/14/12/10/8 whose per-validator tables fit the budget
+    (0 = 8 GiB default), else 4; every window verifies bit-exactly like the oracle, through
+    the registry and through caller-supplied keys on a context without a registry."""
+    import txflow_amd as T
+    n_vals = 16
+    exp_fit = max([w for w in (8, 10, 12, 14, 16) if n_vals * _table_mb(w) <= (budget_mb or 8192)], default=4)
+    assert exp_fit == exp_w
+    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=64, table_budget_mb=budget_mb)
+    try:
+        assert ctx.table_w == 0
+        rnd = random.Random(100 + exp_w)
+        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, n_vals, 1500, rnd)
+        assert ctx.table_w == exp_w
+        for i, v in enumerate(votes):
+            if i % 4 == 1:
+                s = bytearray(v.Signature); s[rnd.randrange(64)] ^= 1 << rnd.randrange(8); v.Signature = bytes(s)
+        b = T.VoteBatch.from_votes(votes)
+        st = ctx.verify_batch(b)
+        exp = np.array([oracle_lib.verify(pubs[signer[i]], oracle_lib.signbytes(
+            1, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], b"test_chain_id"), v.Signature)
+            for i, v in enumerate(votes)])
+        assert np.array_equal(st == T.ADDED, exp)
+        keys = np.array([np.frombuffer(pubs[signer[i]], np.uint8) for i in range(len(votes))])
+        assert np.array_equal(ctx.verify_batch(b, keys), st)
+    finally:
+        ctx.close()
+    # caller-supplied keys against an empty registry (chain id only): their tables use the
+    # registry's window when they fit the budget, else radix-16
+    ctx2 = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=64, table_budget_mb=budget_mb)
+    try:
+        ctx2.set_validators([], [], "test_chain_id")
+        assert np.array_equal(ctx2.verify_batch(b, keys), st)
+    finally:
+        ctx2.close()

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output (kernel trace + PMC passes) for the verify/tally kernels.
+
+usage: python tools/profile/summarize.py gpurun_out/<tag> [--votes N] [--out profiles/<name>.json]
+
+HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KB per dispatch;
+on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so the corrected read
+bytes are 2 x FETCH_SIZE x 1024 (the raw value is kept beside it).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+from collections import defaultdict
+
+
+def rows(path_glob):
+    out = []
+    for p in glob.glob(path_glob, recursive=True):
+        with open(p) as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").strip()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--votes", type=float, default=1e6)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    res = {"source": a.root, "votes_per_launch": a.votes, "kernels": {}}
+    bj = os.path.join(a.root, "bench_kt.json")
+    if os.path.exists(bj):
+        with open(bj) as f:
+            line = [x for x in f.read().splitlines() if x.startswith("{")]
+        if line:
+            b = json.loads(line[-1])
+            res["table_window"] = b["config"].get("table_window")
+            res["bench_line_under_profiler"] = {k: b[k] for k in ("value", "ms_per_step", "verify_kernel_ms",
+                                                                  "tally_kernels_ms") if k in b}
+    kt = rows(os.path.join(a.root, "kt", "**", "*kernel_stats.csv"))
+    for r in kt:
+        res["kernels"].setdefault(short(r["Name"]), {}).update(
+            calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), pct=float(r["Percentage"]))
+    pmc = defaultdict(lambda: defaultdict(list))
+    for r in rows(os.path.join(a.root, "pmc_*", "**", "*counter_collection.csv")):
+        pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in pmc.items():
+        d = res["kernels"].setdefault(k, {})
+        for c, vals in cs.items():
+            d[c] = statistics.median(vals)
+    for k, d in res["kernels"].items():
+        if "FETCH_SIZE" in d:
+            d["hbm_read_bytes_raw"] = d["FETCH_SIZE"] * 1024
+            d["hbm_read_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in d:
+            d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+        if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
+            d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        if "SQ_ACTIVE_INST_VALU" in d and "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
+            d["valu_active_frac_of_wave_cycles"] = d["SQ_ACTIVE_INST_VALU"] / d["SQ_WAVE_CYCLES"]
+        if "SQ_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
+            d["note"] = "SQ_* cycle counters are per-SE sums in quad-cycles (MI355X_MICROARCH.md)"
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and (d["TCC_HIT_sum"] + d["TCC_MISS_sum"]):
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+    # the verify pair: K1a (challenge) + K1b (scalar mult), per launch of 1 batch
+    pair = [d for k, d in res["kernels"].items() if k.startswith(("txv_k_challenge", "txv_k_scalarmult"))]
+    if pair and all("SQ_INSTS_VALU" in d and "SQ_INSTS_VALU_INT64" in d for d in pair):
+        # issue slots in full-rate lane-op units: 64-bit-class VALU ops (v_mad_u64_u32,
+        # 64-bit shifts/adds) issue at half rate, so they count twice
+        slots = sum((d["SQ_INSTS_VALU"] + d["SQ_INSTS_VALU_INT64"]) * 64 for d in pair)
+        res["verify_w_exec_lane_slots_per_vote"] = slots / a.votes
+        res["verify_valu_lane_insts_per_vote"] = sum(d["SQ_INSTS_VALU"] * 64 for d in pair) / a.votes
+    if pair and all("hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d for d in pair):
+        res["hbm_bytes_per_launch"] = sum(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"] for d in pair)
+        res["hbm_bytes_per_launch_raw_fetch"] = sum(d["hbm_read_bytes_raw"] + d["hbm_write_bytes"] for d in pair)
+    txt = json.dumps(res, indent=1, sort_keys=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt + "\n")
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
