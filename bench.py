@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
+    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 3, 4),
+                    help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
     args = ap.parse_args()
@@ -103,7 +105,8 @@ def main():
     t_setup = time.perf_counter()
     max_txs = n_txs_global if world > 1 else args.txs_per_gpu
     ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
-                    max_validators=max(args.validators, 1), table_w=args.table_w or None)
+                    max_validators=max(args.validators, 1), table_w=args.table_w or None,
+                    lane_votes=args.lane_votes)
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
     ctx.stage(0, wl.batch)

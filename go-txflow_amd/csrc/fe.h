@@ -100,6 +100,10 @@ struct fe { uint32_t v[8]; };
 TXV_HD fe fe_zero() { fe r; for (int i = 0; i < 8; ++i) r.v[i] = 0; return r; }
 TXV_HD fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#include "fe_asm.h"
+#endif
+
 // reduce a 512-bit product t[16] to [0, 2^256) using 2^256 = 38 (mod p)
 TXV_HD fe fe_reduce512(const uint32_t t[16]) {
   uint64_t p[8];
@@ -126,6 +130,10 @@ TXV_HD fe fe_reduce512(const uint32_t t[16]) {
 // upper half of the 512-bit product is never held in registers.
 TXV_HD fe fe_mul(const fe& a, const fe& b) {
   fe r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe_mul_dev(r, a, b);   // the same column scan + fold as one asm block (fe_asm.h)
+  return r;
+#else
   uint64_t acc = 0; uint32_t ovf = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -157,9 +165,15 @@ TXV_HD fe fe_mul(const fe& a, const fe& b) {
   for (int i = 2; i < 8; ++i) addc_cc(r.v[i], c, r.v[i], 0u, c);
   r.v[0] += sel_c(c, 38u, 0u);
   return r;
+#endif
 }
 
 TXV_HD fe fe_sq(const fe& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe r;
+  fe_sq_dev(r, a);
+  return r;
+#else
   // off-diagonal triangle U = sum_{i<j} a_i a_j 2^(32(i+j))
   uint32_t u[16];
   uint64_t acc = 0; uint32_t ovf = 0;
@@ -189,14 +203,21 @@ TXV_HD fe fe_sq(const fe& a) {
     addc_cc(t[2 * i + 1], c, s1, (uint32_t)(d >> 32), c);
   }
   return fe_reduce512(t);
+#endif
 }
 
 TXV_HD fe fe_sqn(fe a, int n) {
+#pragma nounroll
   for (int i = 0; i < n; ++i) a = fe_sq(a);
   return a;
 }
 
 TXV_HD fe fe_add(const fe& a, const fe& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe r;
+  fe_add_dev(r, a, b);
+  return r;
+#else
   fe r; uint64_t c;
   add_cc(r.v[0], c, a.v[0], b.v[0]);
 #pragma unroll
@@ -208,9 +229,15 @@ TXV_HD fe fe_add(const fe& a, const fe& b) {
   for (int i = 1; i < 8; ++i) addc_cc(r.v[i], c, r.v[i], 0u, c);
   r.v[0] += sel_c(c, 38u, 0u);   // second wrap leaves r tiny: no further carry
   return r;
+#endif
 }
 
 TXV_HD fe fe_sub(const fe& a, const fe& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe r;
+  fe_sub_dev(r, a, b);
+  return r;
+#else
   fe r; uint64_t c;
   sub_cc(r.v[0], c, a.v[0], b.v[0]);
 #pragma unroll
@@ -222,6 +249,7 @@ TXV_HD fe fe_sub(const fe& a, const fe& b) {
   for (int i = 1; i < 8; ++i) subb_cc(r.v[i], c, r.v[i], 0u, c);
   r.v[0] -= sel_c(c, 38u, 0u);   // second borrow leaves r near 2^256: no further borrow
   return r;
+#endif
 }
 
 TXV_HD fe fe_dbl(const fe& a) { return fe_add(a, a); }

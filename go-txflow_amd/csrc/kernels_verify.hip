@@ -212,6 +212,100 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
   }
 }
 
+// W >= 8, V votes per lane sharing ONE field inversion (Montgomery's trick over the V
+// results: P_h = Z_0 ... Z_h; 1/Z_h = P_{h-1} / P_{V-1} walking back).  The first V-1
+// results wait in a global scratch buffer (wave-interleaved: coalesced, L2-resident,
+// 128 B per parked vote each way), so the register budget of the scalar multiply is
+// unchanged.  V = 4 saves 3/4 of an inversion (~190 squarings) per vote versus V = 1 and
+// fills 4 waves/SIMD in one round for a 1M-vote batch on 256 CUs.
+template <int BLOCK, int W, int V>
+__global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
+  const uint32_t n_grp = (a.n_work + V - 1) / V;
+  // XCD-aware split as in the pair kernel: the blocks of one XCD walk one contiguous
+  // eighth of the validator-sorted work list (its A tables stay in that XCD's L2).
+  const uint32_t groups = gridDim.x >= 8 ? 8u : 1u;
+  const uint32_t grp = blockIdx.x % groups, blocks_in_grp = gridDim.x / groups + (grp < gridDim.x % groups);
+  const uint32_t chunk = (n_grp + groups - 1) / groups;
+  const uint32_t lo = grp * chunk, hi = min(n_grp, lo + chunk);
+  const uint32_t stride = blocks_in_grp * BLOCK;
+  // park layout: [wave][slot h][word][64 lanes]: a wave's stores of one word are one
+  // contiguous 256-byte line and every offset is a compile-time immediate
+  const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  uint32_t* park = a.park + (size_t)gwave * (V - 1) * TXV_PARK_WORDS * 64 + (threadIdx.x & 63);
+  for (uint32_t g = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; g < hi; g += stride) {
+    uint32_t act = 0;
+#pragma unroll
+    for (int h = 0; h < V; ++h) {
+      const uint32_t idx = V * g + h;
+      if (idx < a.n_work && a.ok_out[a.order ? a.order[idx] : idx] == 2) act |= 1u << h;
+    }
+    if (!act) continue;
+    ge_ext R;
+    fe P;
+#pragma unroll 1
+    for (int h = 0; h < V; ++h) {
+      if (act >> h & 1u) {
+        const uint32_t idx = V * g + h;
+        const uint32_t i = a.order ? a.order[idx] : idx;
+        const uint32_t v = a.val[i];
+        uint32_t s[8], k[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
+        R = double_scalarmult_w<W>(a.btable, a.atables + (size_t)v * Tab<W>::kWords, s, k, true);
+      } else {
+        R = ge_identity();
+      }
+      P = h ? fe_mul(P, R.Z) : R.Z;
+      if (h < V - 1) {
+        uint32_t* slot = park + h * TXV_PARK_WORDS * 64;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          slot[j * 64] = R.X.v[j];
+          slot[(8 + j) * 64] = R.Y.v[j];
+          slot[(16 + j) * 64] = P.v[j];
+          slot[(24 + j) * 64] = R.Z.v[j];
+        }
+      }
+    }
+    fe inv = fe_invert(P);
+#pragma unroll 1
+    for (int h = V - 1; h >= 0; --h) {
+      fe X, Y, Z, zi;
+      if (h == V - 1) {
+        X = R.X; Y = R.Y; Z = R.Z;
+      } else {
+        const uint32_t* slot = park + h * TXV_PARK_WORDS * 64;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          X.v[j] = slot[j * 64];
+          Y.v[j] = slot[(8 + j) * 64];
+          Z.v[j] = slot[(24 + j) * 64];
+        }
+      }
+      if (h) {
+        const uint32_t* prev = park + (h - 1) * TXV_PARK_WORDS * 64;
+        fe Pp;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Pp.v[j] = prev[(16 + j) * 64];
+        zi = fe_mul(inv, Pp);          // 1/Z_h = P_{h-1} / P_h
+        inv = fe_mul(inv, Z);          // 1/P_{h-1}
+      } else {
+        zi = inv;
+      }
+      if (act >> h & 1u) {
+        const uint32_t idx = V * g + h;
+        const uint32_t i = a.order ? a.order[idx] : idx;
+        uint32_t enc[8];
+        ge_encode_zinv(enc, X, Y, zi);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * a.n_pad + i];
+        a.ok_out[i] = diff == 0;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- load generator
 // keygen: seed (32 B) -> expanded secret scalar a (mod L), prefix, public key encoding
 __global__ void __launch_bounds__(64) txv_k_keygen(const uint32_t* __restrict__ seeds_le, uint32_t n,
@@ -338,6 +432,18 @@ static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* t
                      tables, decode_ok, addr_words);
 }
 
+// V = 2: the LDS-parked pair kernel; V = 3, 4: parked in args->park (sized by the runtime)
+template <int B, int W>
+static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
+  switch (args->lane_votes) {
+    case 2: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, W>), dim3(grid), dim3(B), 0, st, *args); break;
+    case 3: hipLaunchKernelGGL((txv_k_scalarmult_multi<B, W, 3>), dim3(grid), dim3(B), 0, st, *args); break;
+    case 4: hipLaunchKernelGGL((txv_k_scalarmult_multi<B, W, 4>), dim3(grid), dim3(B), 0, st, *args); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipSuccess;
+}
+
 extern "C" {
 
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
@@ -362,11 +468,11 @@ hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipSt
     constexpr int B = TXV_VERIFY_BLOCK;
     switch (w) {
       case 4: hipLaunchKernelGGL(txv_k_scalarmult_w4<B>, dim3(grid), dim3(B), 0, st, *args); break;
-      case 8: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 8>), dim3(grid), dim3(B), 0, st, *args); break;
-      case 10: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 10>), dim3(grid), dim3(B), 0, st, *args); break;
-      case 12: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 12>), dim3(grid), dim3(B), 0, st, *args); break;
-      case 14: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 14>), dim3(grid), dim3(B), 0, st, *args); break;
-      case 16: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, 16>), dim3(grid), dim3(B), 0, st, *args); break;
+      case 8: if (hipError_t e = launch_multi<B, 8>(args, grid, st)) return e; break;
+      case 10: if (hipError_t e = launch_multi<B, 10>(args, grid, st)) return e; break;
+      case 12: if (hipError_t e = launch_multi<B, 12>(args, grid, st)) return e; break;
+      case 14: if (hipError_t e = launch_multi<B, 14>(args, grid, st)) return e; break;
+      case 16: if (hipError_t e = launch_multi<B, 16>(args, grid, st)) return e; break;
       default: return hipErrorInvalidValue;
     }
   }

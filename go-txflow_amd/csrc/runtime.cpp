@@ -74,6 +74,9 @@ struct txv_ctx {
   int btable_w = 0;
   int cfg_w = 0;                   // requested window, 0 = auto (largest that fits the budget)
   int tab_w = 0;                   // window of the current validator tables
+  uint32_t lane_votes = 4;         // K1b votes per lane (one shared inversion)
+  uint32_t* d_park = nullptr;      // K1b parked points: [V-1][32][grid x block]
+  size_t park_words = 0;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;
   int tmp_w = 0;
@@ -296,7 +299,19 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   a.n_work = s.n_work; a.kbuf = s.d_kbuf;
   a.order = s.d_order; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
+  a.park = c->d_park;
+  a.lane_votes = c->lane_votes;
   return a;
+}
+
+// scratch for the V-1 parked results per K1b lane (the grid never exceeds verify_grid's cap)
+int ensure_park(txv_ctx* c) {
+  const size_t words = (size_t)(c->lane_votes - 1) * TXV_PARK_WORDS * (size_t)c->n_cus * 2 * TXV_VERIFY_BLOCK;
+  if (words <= c->park_words) return TXV_OK;
+  int r;
+  if ((r = dalloc(c, &c->d_park, words))) return r;
+  c->park_words = words;
+  return TXV_OK;
 }
 
 TallyArgs tally_args(txv_ctx* c, Slot& s) {
@@ -369,6 +384,8 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
     HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
     c->epoch = 1;
   }
+  int r;
+  if ((r = ensure_park(c))) return r;
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
   HIP_TRY(c, txv_launch_verify(c->tab_w, &va, verify_grid(c, s.n), c->stream));
@@ -475,6 +492,8 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }
+  if (TXV_CFG_LANE_VOTES(c->cfg.flags)) c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags);
+  if (c->lane_votes < 2 || c->lane_votes > TXV_MAX_LANE_VOTES) { delete c; return TXV_EINVAL; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     delete c;
@@ -507,7 +526,7 @@ void txv_destroy(txv_ctx* c) {
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
-  dfree(c->d_btable4); dfree(c->d_btable8); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
+  dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_acc_slot); dfree(c->d_first_tag); dfree(c->d_arena); dfree(c->d_arena_count); dfree(c->d_errflags);
   dfree(c->d_set_sum); dfree(c->d_set_cross); dfree(c->d_bitmap);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
@@ -652,7 +671,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   }
   build_order(s);
   pack_columns(s, v, lens);
-  if ((r = upload_slot(c, s))) return r;
+  if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
   VerifyArgs va = verify_args(c, s, kp, kok, ktab);
   va.btable = w_keys == 4 ? c->d_btable4 : c->d_btable8;
   HIP_TRY(c, txv_launch_verify(w_keys, &va, verify_grid(c, s.n), c->stream));

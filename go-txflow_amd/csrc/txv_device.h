@@ -31,7 +31,12 @@ struct VerifyArgs {
   const uint32_t* atables;     // [n_vals][kTableWords]
   const uint32_t* btable;      // [kTableWords]
   uint8_t* ok_out;             // [n]
+  uint32_t* park;              // [V-1][32][lanes] parked points of the multi-vote K1b (lanes = grid x block)
+  uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2, 3 or 4)
 };
+
+#define TXV_PARK_WORDS 32          // X, Y, prefix product, Z of one parked vote
+#define TXV_MAX_LANE_VOTES 4
 
 struct SignArgs {
   uint32_t n, n_pad, msg_words, pad0;

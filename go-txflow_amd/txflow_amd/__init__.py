@@ -231,13 +231,15 @@ class Context:
 
     def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
                  max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
-                 table_w: int | None = None, table_budget_mb: int = 0):
+                 table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0):
         """table_w: fixed-base window (4, 8, 10, 12, 14, 16) or None = the largest whose
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
         if table_w not in (None, 4, 8, 10, 12, 14, 16):
             raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16")
+        if lane_votes not in (0, 2, 3, 4):
+            raise ValueError("lane_votes must be 0 (default) or 2..4")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
-                   ((table_w or 0) & 0xFF) << 8, table_budget_mb)
+                   (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16), table_budget_mb)
         h = ctypes.c_void_p()
         rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

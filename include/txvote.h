@@ -88,6 +88,10 @@ typedef struct {
  * 128 / 64 / 52 / 44 / 38 / 32 point additions per verified vote */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
+/* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19
+ * (2, 3 or 4; 0 = default 4) */
+#define TXV_CFG_LANE_VOTES(flags) (((flags) >> 16) & 0xFu)
+#define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
 
 /* A batch of TxVotes (types/tx_vote.go:48-55) in structure-of-arrays form. */
 typedef struct {
