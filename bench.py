@@ -82,7 +82,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
-    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 3, 4),
+    ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
+                    help="base-point table window (0 = library default)")
+    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
@@ -106,7 +108,7 @@ def main():
     max_txs = n_txs_global if world > 1 else args.txs_per_gpu
     ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
                     max_validators=max(args.validators, 1), table_w=args.table_w or None,
-                    lane_votes=args.lane_votes)
+                    lane_votes=args.lane_votes, base_w=args.base_w)
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
     ctx.stage(0, wl.batch)
@@ -227,7 +229,7 @@ def main():
             "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
                                     f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
                                     f"100 validators, ~1M votes/GPU, RCCL bitmap all-gather"),
-                       "validators": args.validators, "table_window": ctx.table_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
+                       "validators": args.validators, "table_window": ctx.table_w, "base_window": ctx.base_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
                        "parallelism": f"shard{world}"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
             "step_phases_ms_p50": {k: round(statistics.median(v), 3) for k, v in phases.items() if v},

@@ -28,7 +28,7 @@ template <int W>
 struct Tab {
   static constexpr int kPositions = (256 + W - 1) / W;
   static constexpr int kEntries = (1 << (W - 1)) + 1;
-  static constexpr int kWords = kPositions * kEntries * kEntryWords;
+  static constexpr size_t kWords = (size_t)kPositions * kEntries * kEntryWords;   // > 2^31 at W = 24
 };
 
 // legacy W = 4 names (keygen/sign and the host emulation)
@@ -84,7 +84,7 @@ TXV_HD void sha512_prefixed(uint32_t digest_le[16], const uint64_t* pre, int pre
 // table entry fetch: T[pos][idx] from a flat word array
 template <int W, typename Ptr>
 TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
-  const int base = (pos * Tab<W>::kEntries + idx) * kEntryWords;
+  const size_t base = (size_t)(uint32_t)(pos * Tab<W>::kEntries + idx) * kEntryWords;
   ge_niels e;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -112,22 +112,31 @@ TXV_HD int next_digit(uint32_t s[8], uint32_t& carry) {
 }
 
 // sum_i T_B[i][s_i] + T_A[i][-k_i] over raw scalars s, k < 2^253 (digits of k negated,
-// giving [k](-A)); digits are produced on the fly, so any window W <= 16 works.
-template <int W, typename PtrB, typename PtrA>
-TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {
+// giving [k](-A)); digits are produced on the fly, so any windows < 32 work.  The base
+// point's table may use a wider window WB than the validators' WA (one table serves every
+// vote, so it can take gigabytes of HBM): ceil(256/WB) + ceil(256/WA) mixed additions.
+template <int WB, int WA, typename PtrB, typename PtrA>
+TXV_HD ge_ext double_scalarmult_w2(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {
+  static_assert(WB >= WA, "B window must be at least the A window");
   ge_ext P = ge_identity();
   uint32_t s[8], k[8], cs = 0, ck = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
-  for (int pos = 0; pos < Tab<W>::kPositions; ++pos) {
-    const int ds = next_digit<W>(s, cs);
-    P = ge_madd(P, load_entry_w<W>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
+  for (int pos = 0; pos < Tab<WA>::kPositions; ++pos) {
+    if (pos < Tab<WB>::kPositions) {
+      const int ds = next_digit<WB>(s, cs);
+      P = ge_madd(P, load_entry_w<WB>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
+    }
     if (use_a) {
-      const int dk = next_digit<W>(k, ck);
-      P = ge_madd(P, load_entry_w<W>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
+      const int dk = next_digit<WA>(k, ck);
+      P = ge_madd(P, load_entry_w<WA>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
     }
   }
   return P;
+}
+template <int W, typename PtrB, typename PtrA>
+TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {
+  return double_scalarmult_w2<W, W>(tb, ta, s_in, k_in, use_a);
 }
 
 // [s]B (+ [k](-A)) with the radix-16 tables (keygen / sign / host emulation)

@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 // 128 B per parked vote each way), so the register budget of the scalar multiply is
 // unchanged.  V = 4 saves 3/4 of an inversion (~190 squarings) per vote versus V = 1 and
 // fills 4 waves/SIMD in one round for a 1M-vote batch on 256 CUs.
-template <int BLOCK, int W, int V>
+template <int BLOCK, int WB, int WA, int V>
 __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
   const uint32_t n_grp = (a.n_work + V - 1) / V;
   // XCD-aware split as in the pair kernel: the blocks of one XCD walk one contiguous
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
         uint32_t s[8], k[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-        R = double_scalarmult_w<W>(a.btable, a.atables + (size_t)v * Tab<W>::kWords, s, k, true);
+        R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)v * Tab<WA>::kWords, s, k, true);
       } else {
         R = ge_identity();
       }
@@ -432,14 +432,15 @@ static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* t
                      tables, decode_ok, addr_words);
 }
 
-// V = 2: the LDS-parked pair kernel; V = 3, 4: parked in args->park (sized by the runtime)
-template <int B, int W>
+// V = 2: the LDS-parked pair kernel (WB = WA only); V = 4: parked in args->park
+template <int B, int WB, int WA>
 static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
-  switch (args->lane_votes) {
-    case 2: hipLaunchKernelGGL((txv_k_scalarmult_pair<B, W>), dim3(grid), dim3(B), 0, st, *args); break;
-    case 3: hipLaunchKernelGGL((txv_k_scalarmult_multi<B, W, 3>), dim3(grid), dim3(B), 0, st, *args); break;
-    case 4: hipLaunchKernelGGL((txv_k_scalarmult_multi<B, W, 4>), dim3(grid), dim3(B), 0, st, *args); break;
-    default: return hipErrorInvalidValue;
+  if (args->lane_votes == 4) {
+    hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 4>), dim3(grid), dim3(B), 0, st, *args);
+  } else if (args->lane_votes == 2 && WB == WA) {
+    hipLaunchKernelGGL((txv_k_scalarmult_pair<B, WA>), dim3(grid), dim3(B), 0, st, *args);
+  } else {
+    return hipErrorInvalidValue;
   }
   return hipSuccess;
 }
@@ -456,25 +457,41 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
     case 12: launch_build<12>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 14: launch_build<14>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
+// (wb, wa): base-point and validator windows; supported pairs are (w, w) for every table
+// window and the wide base tables wb in {20, 22, 24} over wa = 16
+bool txv_verify_windows_supported(int wb, int wa) {
+  if (wb == wa) return wa == 4 || wa == 8 || wa == 10 || wa == 12 || wa == 14 || wa == 16;
+  return wa == 16 && (wb == 20 || wb == 22 || wb == 24);
+}
+
+hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (!args->n) return hipSuccess;
+  if (!txv_verify_windows_supported(wb, wa)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
   if (args->n_work) {
     constexpr int B = TXV_VERIFY_BLOCK;
-    switch (w) {
-      case 4: hipLaunchKernelGGL(txv_k_scalarmult_w4<B>, dim3(grid), dim3(B), 0, st, *args); break;
-      case 8: if (hipError_t e = launch_multi<B, 8>(args, grid, st)) return e; break;
-      case 10: if (hipError_t e = launch_multi<B, 10>(args, grid, st)) return e; break;
-      case 12: if (hipError_t e = launch_multi<B, 12>(args, grid, st)) return e; break;
-      case 14: if (hipError_t e = launch_multi<B, 14>(args, grid, st)) return e; break;
-      case 16: if (hipError_t e = launch_multi<B, 16>(args, grid, st)) return e; break;
+    hipError_t e = hipSuccess;
+    switch (wb * 100 + wa) {
+      case 404: hipLaunchKernelGGL(txv_k_scalarmult_w4<B>, dim3(grid), dim3(B), 0, st, *args); break;
+      case 808: e = launch_multi<B, 8, 8>(args, grid, st); break;
+      case 1010: e = launch_multi<B, 10, 10>(args, grid, st); break;
+      case 1212: e = launch_multi<B, 12, 12>(args, grid, st); break;
+      case 1414: e = launch_multi<B, 14, 14>(args, grid, st); break;
+      case 1616: e = launch_multi<B, 16, 16>(args, grid, st); break;
+      case 2016: e = launch_multi<B, 20, 16>(args, grid, st); break;
+      case 2216: e = launch_multi<B, 22, 16>(args, grid, st); break;
+      case 2416: e = launch_multi<B, 24, 16>(args, grid, st); break;
       default: return hipErrorInvalidValue;
     }
+    if (e != hipSuccess) return e;
   }
   return hipGetLastError();
 }

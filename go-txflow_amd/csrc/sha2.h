@@ -1,9 +1,10 @@
 // sha2.h — SHA-512 (ed25519 challenge hash) and SHA-256 (tendermint address, pool
 // cache key) compression functions, one message per lane.
 //
-// 64-bit words are left to the compiler, which lowers rotates to v_alignbit_b32 pairs and
-// adds to v_add_co/v_addc pairs; the 80-round loop is fully unrolled with a 16-word
-// ring so every schedule word stays in VGPRs (no scratch).  Callers supply already
+// 64-bit rotates and shifts are written as v_alignbit_b32 pairs (hipcc otherwise emits
+// two half-rate 64-bit shifts and two ORs per rotate); 64-bit adds lower to one
+// v_lshl_add_u64.  The 80-round loop is fully unrolled with a 16-word ring so every
+// schedule word stays in VGPRs (no scratch).  Callers supply already
 // padded big-endian blocks: the host packs SignBytes with the FIPS 180-4 padding of the
 // full R || A || M input (DESIGN.md §Data layout), so the device never branches on length.
 #pragma once
@@ -11,7 +12,27 @@
 
 namespace txv {
 
-TXV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// n is a compile-time constant at every call site (the rounds are unrolled)
+TXV_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t a = n < 32 ? hi : lo, b = n < 32 ? lo : hi;   // rotate by 32 = swap halves
+  const int m = n & 31;
+  if (m == 0) return ((uint64_t)a << 32) | b;
+  return ((uint64_t)__builtin_amdgcn_alignbit(b, a, m) << 32) | __builtin_amdgcn_alignbit(a, b, m);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+// x >> n for 0 < n < 32
+TXV_HD uint64_t shr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
 TXV_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 TXV_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -52,30 +73,43 @@ TXV_HD void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
-// one compression; w[16] is consumed (overwritten by the schedule)
+// one compression; w[16] is consumed (overwritten by the schedule).  Rounds 0-15 are
+// unrolled; rounds 16-79 run as 4 iterations of a 16-round unrolled body, so every w[]
+// index is static (no indexed register access) and the 8 working variables return to
+// their registers at each back-edge.
+#define TXV_SHA512_ROUND(I, J, SCHED)                                                       \
+  {                                                                                        \
+    uint64_t wi;                                                                           \
+    if (SCHED) {                                                                           \
+      const uint64_t w15 = w[((J) + 1) & 15], w2 = w[((J) + 14) & 15];                      \
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);                 \
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);                  \
+      wi = w[(J) & 15] + s0 + w[((J) + 9) & 15] + s1;                                      \
+      w[(J) & 15] = wi;                                                                    \
+    } else {                                                                               \
+      wi = w[J];                                                                           \
+    }                                                                                      \
+    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);                     \
+    const uint64_t ch = g ^ (e & (f ^ g));                                                 \
+    const uint64_t t1 = h + S1 + ch + sha512_k(I) + wi;                                     \
+    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);                     \
+    const uint64_t mj = (a & b) | (c & (a | b));                                           \
+    const uint64_t t2 = S0 + mj;                                                           \
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;                    \
+  }
+
 TXV_HD void sha512_block(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
-  for (int i = 0; i < 80; ++i) {
-    uint64_t wi;
-    if (i < 16) wi = w[i];
-    else {
-      uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    uint64_t ch = g ^ (e & (f ^ g));
-    uint64_t t1 = h + S1 + ch + sha512_k(i) + wi;
-    uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    uint64_t mj = (a & b) | (c & (a | b));
-    uint64_t t2 = S0 + mj;
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  for (int j = 0; j < 16; ++j) TXV_SHA512_ROUND(j, j, false)
+#pragma unroll 1
+  for (int i0 = 16; i0 < 80; i0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) TXV_SHA512_ROUND(i0 + j, j, true)
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+#undef TXV_SHA512_ROUND
 
 TXV_HD uint32_t sha256_k(int i) {
   const uint32_t K[64] = {

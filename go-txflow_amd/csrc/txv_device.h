@@ -32,7 +32,7 @@ struct VerifyArgs {
   const uint32_t* btable;      // [kTableWords]
   uint8_t* ok_out;             // [n]
   uint32_t* park;              // [V-1][32][lanes] parked points of the multi-vote K1b (lanes = grid x block)
-  uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2, 3 or 4)
+  uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2 or 4)
 };
 
 #define TXV_PARK_WORDS 32          // X, Y, prefix product, Z of one parked vote
@@ -54,7 +54,8 @@ extern "C" {
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
-hipError_t txv_launch_verify(int w, const VerifyArgs* args, uint32_t grid, hipStream_t st);
+bool txv_verify_windows_supported(int wb, int wa);
+hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st);
 hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_t* btable, uint32_t* scal,
                              uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);

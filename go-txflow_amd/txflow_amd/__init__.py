@@ -106,6 +106,7 @@ def lib():
             "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "txv_table_window": ([vp], ctypes.c_int),
+            "txv_base_window": ([vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -120,7 +121,7 @@ EXPORTED_SYMBOLS = [
     "txv_get_validator_info", "txv_verify_batch", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest",
-    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window"]
+    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -231,15 +232,17 @@ class Context:
 
     def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
                  max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
-                 table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0):
+                 table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0,
+                 base_w: int = 0):
         """table_w: fixed-base window (4, 8, 10, 12, 14, 16) or None = the largest whose
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
         if table_w not in (None, 4, 8, 10, 12, 14, 16):
             raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16")
-        if lane_votes not in (0, 2, 3, 4):
-            raise ValueError("lane_votes must be 0 (default) or 2..4")
+        if lane_votes not in (0, 2, 4):
+            raise ValueError("lane_votes must be 0 (default), 2 or 4")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
-                   (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16), table_budget_mb)
+                   (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16) | ((base_w & 0xFF) << 20),
+                   table_budget_mb)
         h = ctypes.c_void_p()
         rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
@@ -358,6 +361,11 @@ class Context:
         a = ctypes.c_double(); m = ctypes.c_double()
         self._chk(lib().txv_valu_probe(self._h, ctypes.byref(a), ctypes.byref(m)), "valu probe")
         return a.value, m.value
+
+    @property
+    def base_w(self) -> int:
+        """window of the base-point table used by the verify kernel"""
+        return int(lib().txv_base_window(self._h))
 
     @property
     def table_w(self) -> int:

@@ -89,9 +89,14 @@ typedef struct {
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19
- * (2, 3 or 4; 0 = default 4) */
+ * (2 or 4; 0 = default 4) */
 #define TXV_CFG_LANE_VOTES(flags) (((flags) >> 16) & 0xFu)
 #define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
+/* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 8.9 GB, over radix-2^16
+ * validator tables; else the validator window), or 20 / 22 / 24 with window-16 validator
+ * tables (0.65 / 2.4 / 8.9 GB, 13 / 12 / 11 additions for [s]B), or equal to the window */
+#define TXV_CFG_B_WINDOW(flags) (((flags) >> 20) & 0xFFu)
+#define TXV_CFG_SET_B_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 20)
 
 /* A batch of TxVotes (types/tx_vote.go:48-55) in structure-of-arrays form. */
 typedef struct {
@@ -174,6 +179,8 @@ int txv_copy_commit_bitmap(txv_ctx* ctx, void* dst_dev, uint64_t bytes);
 int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
 /* fixed-base window of the current validator tables (4..16), 0 before txv_set_validators */
 int txv_table_window(txv_ctx* ctx);
+/* window of the base-point table the verify kernel uses (>= the validator window) */
+int txv_base_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids
  * already assigned stay assigned (their sets read as empty) */
 int txv_reset_tally(txv_ctx* ctx);

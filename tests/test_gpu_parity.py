@@ -263,3 +263,26 @@ def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
         assert np.array_equal(ctx2.verify_batch(b, keys), st)
     finally:
         ctx2.close()
+
+
+@pytest.mark.parametrize("base_w", [20, 24])
+def test_wide_base_table_parity(oracle_lib, base_w):
+    """Radix-2^20 / 2^24 base-point tables (0.65 / 8.9 GB) over radix-2^16 validator
+    tables: the same verdicts as the oracle on valid and corrupted votes."""
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16, table_w=16, base_w=base_w)
+    try:
+        rnd = random.Random(base_w)
+        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 4, 800, rnd)
+        assert (ctx.table_w, ctx.base_w) == (16, base_w)
+        for i, v in enumerate(votes):
+            if i % 3 == 1:
+                s = bytearray(v.Signature); s[rnd.randrange(64)] ^= 1 << rnd.randrange(8); v.Signature = bytes(s)
+        st = ctx.verify_batch(T.VoteBatch.from_votes(votes))
+        exp = np.array([oracle_lib.verify(pubs[signer[i]], oracle_lib.signbytes(
+            1, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], b"test_chain_id"), v.Signature)
+            for i, v in enumerate(votes)])
+        assert np.array_equal(st == T.ADDED, exp)
+        assert exp.sum() > len(votes) // 2
+    finally:
+        ctx.close()
