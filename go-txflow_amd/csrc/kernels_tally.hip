@@ -4,133 +4,173 @@
 // Sequential semantics being reproduced (types/vote_set.go:92-166, txflow/service.go:192-234):
 // votes of one (tx, validator) group are decided in arrival order; a vote is
 //   DUPLICATE / NONDETERMINISTIC if the group already holds an accepted vote (signature
-//     bytes equal / different) — decided BEFORE verification;
-//   INVALID_SIGNATURE if it fails Verify (not stored, so a later vote may still be added);
+//     bytes equal / different) — decided BEFORE verification (and before SignBytes);
+//   INVALID_SIGNATURE (or the SignBytes error) if it fails Verify: not stored, so a later
+//     vote of the group may still be added;
 //   ADDED otherwise: sum += power, maj23 |= sum >= Total*2/3 + 1.
-// Parallel form: f = the smallest arrival index in the group whose vote verifies (one
-// 64-bit atomicMin per verified vote on an epoch-tagged key, so no per-batch clearing of
-// the [set][validator] table is needed); votes before f keep their verify verdict, f is
-// ADDED, later votes compare their signature with f's.  Per set, the commit crossing is the
-// first arrival index at which prior_sum + (power of ADDED votes up to it) reaches quorum;
-// it is found by one wave per touched set with a bisection over arrival index using
-// cross-lane reductions (DPP-lowered __shfl_xor sums).
 //
-// HBM traffic per vote (algorithmic): set/val/flags/status/ok 4+4+1+1+1, slot 4, tag 8,
-// power 8 (L2-resident) ~ 31 B; per ADDED vote +64 B arena write.
+// Set-major form (K2a, one wave per touched TxVoteSet): the host stages the batch's pending
+// votes grouped by (set, validator) with arrival order kept inside each group (two stable
+// counting sorts).  A wave walks its set's votes 64 at a time:
+//   * an inclusive segmented min-scan (segments = validator groups, value = position if the
+//     vote verified) gives every vote the first verified position F of its group so far:
+//     F == none -> INVALID_SIGNATURE, F == own position -> ADDED, F earlier -> compare
+//     signature bytes with the vote at F (DUPLICATE / NONDETERMINISTIC);
+//   * a group whose validator already has an accepted vote from an earlier batch compares
+//     against the arena row of that vote instead;
+//   * the ADDED votes (at most one per validator) are listed; each one's stake prefix in
+//     arrival order is a loop over that short list, the smallest arrival index whose prefix
+//     reaches quorum is the commit crossing, and ADDED votes at or after it fire.
+// K2b (arrival order, coalesced) writes the pre-check statuses and copies each ADDED vote's
+// signature into arena row arena_base + i, so K2a's per-set traffic stays contiguous.
+//
+// HBM traffic per vote (algorithmic): tvote/tval 8, ok 1, status 1, acc_slot 4 (per set row,
+// contiguous), sig 64 read + 64 arena write per ADDED vote ~ 142 B.
 #include "txv_device.h"
 #include "txv_tally.h"
 
 #define TXV_ST_PENDING 0xFFu
-#define TXV_ST_OPEN 0xFEu
+#define TXV_ERR_SIGNBYTES_DEV 8u
+#define TXV_INF 0xFFFFFFFFu
 
-__device__ __forceinline__ uint64_t tag_of(uint32_t epoch_hi, uint32_t seq) {
-  return ((uint64_t)epoch_hi << 32) | seq;
-}
-
-// K2a: groups with an accepted vote from an earlier batch; first-verified candidates
-__global__ void __launch_bounds__(256) txv_k_tally_mark(TallyArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  const uint8_t pre = a.pre[i];
-  if (pre != TXV_ST_PENDING) { a.status[i] = pre; return; }
-  const uint64_t key = (uint64_t)a.set[i] * a.n_vals + a.val[i];
-  const uint32_t slot = a.acc_slot[key];
-  if (slot) {
-    uint8_t st = TXV_ERR_NONDETERMINISTIC_DEV;
-    if (a.flags[i] & TXV_FLAG_SIG64) {
-      const uint32_t* acc = a.arena + (size_t)(slot - 1) * 16;
-      uint32_t d = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) d |= acc[j] ^ a.sig[(size_t)j * a.n_pad + i];
-      if (!d) st = TXV_DUPLICATE_DEV;
-    }
-    a.status[i] = st;
-    return;
-  }
-  a.status[i] = TXV_ST_OPEN;
-  if (a.ok[i]) atomicMin((unsigned long long*)&a.first_tag[key], (unsigned long long)tag_of(a.epoch_hi, i));
-}
-
-// K2b: resolve open votes against the group's first verified vote of this batch
-__global__ void __launch_bounds__(256) txv_k_tally_resolve(TallyArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  if (a.status[i] != TXV_ST_OPEN) return;
-  const uint64_t key = (uint64_t)a.set[i] * a.n_vals + a.val[i];
-  const uint64_t t = a.first_tag[key];
-  uint8_t st;
-  if ((uint32_t)(t >> 32) != a.epoch_hi || i < (uint32_t)t) {
-    st = TXV_ERR_INVALID_SIGNATURE_DEV;           // failed Verify before (or without) an accepted vote
-  } else if (i == (uint32_t)t) {
-    st = TXV_ADDED_DEV;
-    const uint32_t slot = atomicAdd(a.arena_count, 1u);
-    if (slot < a.arena_cap) {
-      // whole 64-byte line per lane in four 16-byte stores (4-byte scattered stores cost a
-      // partial-line write each: ~480 B of HBM writes per vote measured)
-      uint4* dst = reinterpret_cast<uint4*>(a.arena + (size_t)slot * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = make_uint4(a.sig[(size_t)(4 * q) * a.n_pad + i], a.sig[(size_t)(4 * q + 1) * a.n_pad + i],
-                            a.sig[(size_t)(4 * q + 2) * a.n_pad + i], a.sig[(size_t)(4 * q + 3) * a.n_pad + i]);
-      a.acc_slot[key] = slot + 1;
-    } else {
-      atomicOr(a.error_flags, TXV_DEVERR_ARENA_FULL);
-    }
-  } else {
-    const uint32_t f = (uint32_t)t;
-    st = TXV_ERR_NONDETERMINISTIC_DEV;
-    if (a.flags[i] & TXV_FLAG_SIG64) {
-      uint32_t d = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) d |= a.sig[(size_t)j * a.n_pad + f] ^ a.sig[(size_t)j * a.n_pad + i];
-      if (!d) st = TXV_DUPLICATE_DEV;
-    }
-  }
-  a.status[i] = st;
-}
+// tval packs the validator index with the per-vote flags the tally needs
+#define TXV_TVAL_SIG64 0x80000000u
+#define TXV_TVAL_BADMSG 0x40000000u
+#define TXV_TVAL_MASK 0x3FFFFFFFu
 
 __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
 }
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
 
-// K2c: one wave per touched set: batch power, crossing index, sum/maj23 update
+// signature of vote i (column-major sig[16][n_pad]) equals 16 words at q?
+__device__ __forceinline__ bool sig_equals_row(const TallyArgs& a, uint32_t i, const uint32_t* q) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d |= a.sig[(size_t)j * a.n_pad + i] ^ q[j];
+  return d == 0;
+}
+__device__ __forceinline__ bool sig_equals_vote(const TallyArgs& a, uint32_t i, uint32_t f) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d |= a.sig[(size_t)j * a.n_pad + i] ^ a.sig[(size_t)j * a.n_pad + f];
+  return d == 0;
+}
+
 __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
   const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= a.n_touched) return;
   const uint32_t set = a.touched[t];
-  const uint64_t base = (uint64_t)set * a.n_vals;
-  int64_t part = 0;
-  for (uint32_t v = lane; v < a.n_vals; v += 64) {
-    const uint64_t e = a.first_tag[base + v];
-    if ((uint32_t)(e >> 32) == a.epoch_hi) part += a.power[v];
+  const uint32_t beg = a.toff[t], end = a.toff[t + 1];
+  const size_t row = (size_t)set * a.n_vals;
+
+  // pass 1: group resolution, chunk by chunk, carrying the open group across chunks
+  uint32_t carry_val = TXV_INF, carry_first = TXV_INF;
+  uint32_t k = 0;            // ADDED votes listed so far (wave-uniform)
+  int64_t batch = 0;         // their stake (lane partials)
+  for (uint32_t base = beg; base < end; base += 64) {
+    const uint32_t p = base + lane;
+    const bool valid = p < end;
+    const uint32_t i = valid ? a.tvote[p] : 0u;
+    const uint32_t tv = valid ? a.tval[p] : TXV_INF;
+    const uint32_t v = tv & TXV_TVAL_MASK;
+    const bool okv = valid && a.ok[i] == 1 && !(tv & TXV_TVAL_BADMSG);
+    const uint32_t prev_v = (uint32_t)__shfl_up((int)v, 1, 64);
+    bool head = lane == 0 ? (v != carry_val) : (v != prev_v);
+    uint32_t x = okv ? p : TXV_INF;
+    if (lane == 0 && !head) x = min(x, carry_first);
+    if (!valid) head = true;
+    // inclusive segmented min-scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+      const bool g = __shfl_up((int)head, d, 64) != 0;
+      if (lane >= d && !head) { x = min(x, y); head = g; }
+    }
+    carry_val = (uint32_t)__shfl((int)v, 63, 64);
+    carry_first = (uint32_t)__shfl((int)x, 63, 64);
+    bool added = false;
+    if (valid) {
+      const uint32_t slot = a.acc_slot[row + v];
+      uint8_t st;
+      if (slot) {
+        st = (tv & TXV_TVAL_SIG64) && sig_equals_row(a, i, a.arena + (size_t)(slot - 1) * 16)
+                 ? TXV_DUPLICATE_DEV : TXV_ERR_NONDETERMINISTIC_DEV;
+      } else if (x == TXV_INF) {
+        st = (tv & TXV_TVAL_BADMSG) ? TXV_ERR_SIGNBYTES_DEV : TXV_ERR_INVALID_SIGNATURE_DEV;
+      } else if (x == p) {
+        added = true;
+        st = TXV_ADDED_DEV;
+      } else {
+        st = (tv & TXV_TVAL_SIG64) && sig_equals_vote(a, i, a.tvote[x]) ? TXV_DUPLICATE_DEV
+                                                                         : TXV_ERR_NONDETERMINISTIC_DEV;
+      }
+      if (!added) a.status[i] = st;
+    }
+    // list the ADDED votes (compacted in lane order) at beg + k ..
+    const uint64_t m = __ballot(added);
+    if (added) {
+      const uint32_t e = beg + k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      const int64_t pw = a.power[v];
+      a.ent_vote[e] = i;
+      a.ent_power[e] = pw;
+      a.ent_val[e] = v;
+      batch += pw;
+    }
+    k += (uint32_t)__popcll(m);
   }
-  const int64_t batch = wave_sum64(part);
+  __threadfence_block();   // the list written above is read back by other lanes of the wave
+
+  // pass 2: the commit crossing in arrival order
   const int64_t prior = a.set_sum[set];
-  const int64_t total = prior + batch;
+  const int64_t total = prior + wave_sum64(batch);
   uint32_t cross = TXV_NO_CROSS;
   if (prior >= a.quorum) {
-    cross = 0;                                       // already committed: every ADDED vote re-fires
+    cross = 0;                                   // already committed: every ADDED vote re-fires
   } else if (total >= a.quorum) {
-    // smallest s with prior + sum_{seq <= s} power >= quorum
-    uint32_t lo = 0, hi = a.n - 1;
-    while (lo < hi) {
-      const uint32_t mid = lo + ((hi - lo) >> 1);
-      int64_t p = 0;
-      for (uint32_t v = lane; v < a.n_vals; v += 64) {
-        const uint64_t e = a.first_tag[base + v];
-        if ((uint32_t)(e >> 32) == a.epoch_hi && (uint32_t)e <= mid) p += a.power[v];
+    // stake prefix of each listed vote in arrival order: entries are loaded 64 at a time
+    // (coalesced) and broadcast lane by lane with readlane, so the k x k comparison costs no
+    // memory round trips beyond k/64 + (k/64)^2 vector loads
+    uint32_t best = TXV_INF;
+    for (uint32_t cj = 0; cj < k; cj += 64) {
+      const bool hasj = cj + lane < k;
+      const uint32_t ij = hasj ? a.ent_vote[beg + cj + lane] : TXV_INF;
+      int64_t pre = 0;
+      for (uint32_t cl = 0; cl < k; cl += 64) {
+        const bool hasl = cl + lane < k;
+        const uint32_t il = hasl ? a.ent_vote[beg + cl + lane] : TXV_INF;
+        const int64_t pl = hasl ? a.ent_power[beg + cl + lane] : 0;
+        const uint32_t nl = min(64u, k - cl);
+        const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)((uint64_t)pl >> 32);
+        for (uint32_t l = 0; l < nl; ++l) {   // l is wave-uniform: v_readlane into SGPRs
+          const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)il, (int)l);
+          const uint64_t pw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pl_hi, (int)l) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, (int)l);
+          if (fl <= ij) pre += (int64_t)pw;
+        }
       }
-      if (prior + wave_sum64(p) >= a.quorum) hi = mid; else lo = mid + 1;
+      if (hasj && prior + pre >= a.quorum) best = min(best, ij);
     }
-    cross = lo;
+    cross = wave_min32(best);
+  }
+
+  // pass 3: ADDED statuses (+ fired bit) and the accepted-vote rows
+  for (uint32_t e = lane; e < k; e += 64) {
+    const uint32_t ie = a.ent_vote[beg + e];
+    const bool fire = cross != TXV_NO_CROSS && ie >= cross;
+    a.status[ie] = TXV_ADDED_DEV | (fire ? 0x80u : 0u);
+    a.acc_slot[row + a.ent_val[beg + e]] = a.arena_base + ie + 1u;
   }
   if (lane == 0) {
     a.set_sum[set] = total;
     const bool maj = total >= a.quorum;
-    a.set_cross[set] = cross;
     a.t_sum[t] = total;
     a.t_maj[t] = maj ? 1 : 0;
     a.t_cross[t] = (prior >= a.quorum) ? TXV_NO_CROSS : cross;   // event only on the transition
@@ -138,22 +178,25 @@ __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
   }
 }
 
-// K2d: commit side effects fire for ADDED votes at or after the set's crossing
-__global__ void __launch_bounds__(256) txv_k_tally_fire(TallyArgs a) {
+// K2b: pre-check statuses, and the ADDED votes' signatures into their arena rows
+__global__ void __launch_bounds__(256) txv_k_tally_finish(TallyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  if (a.status[i] != TXV_ADDED_DEV) return;
-  const uint32_t c = a.set_cross[a.set[i]];
-  if (c != TXV_NO_CROSS && i >= c) a.status[i] = TXV_ADDED_DEV | 0x80u;
+  const uint8_t pre = a.pre[i];
+  if (pre != TXV_ST_PENDING) { a.status[i] = pre; return; }
+  if ((a.status[i] & 0x7Fu) != TXV_ADDED_DEV) return;
+  // whole 64-byte row per lane in four 16-byte stores
+  uint4* dst = reinterpret_cast<uint4*>(a.arena + (size_t)(a.arena_base + i) * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    dst[q] = make_uint4(a.sig[(size_t)(4 * q) * a.n_pad + i], a.sig[(size_t)(4 * q + 1) * a.n_pad + i],
+                        a.sig[(size_t)(4 * q + 2) * a.n_pad + i], a.sig[(size_t)(4 * q + 3) * a.n_pad + i]);
 }
 
 extern "C" hipError_t txv_launch_tally(const TallyArgs* args, hipStream_t st) {
   if (!args->n) return hipSuccess;
-  const uint32_t g = (args->n + 255) / 256;
-  hipLaunchKernelGGL(txv_k_tally_mark, dim3(g), dim3(256), 0, st, *args);
-  hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *args);
   if (args->n_touched)
     hipLaunchKernelGGL(txv_k_tally_sets, dim3((args->n_touched + 3) / 4), dim3(256), 0, st, *args);
-  hipLaunchKernelGGL(txv_k_tally_fire, dim3(g), dim3(256), 0, st, *args);
+  hipLaunchKernelGGL(txv_k_tally_finish, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
   return hipGetLastError();
 }

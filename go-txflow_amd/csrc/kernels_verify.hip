@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(256) txv_k_challenge(VerifyArgs a) {
   uint32_t s[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
-  const bool bad = !(fl & TXV_FLAG_SIG64) || (s[15] & 0xE0000000u) || !a.decode_ok[v] || !sc_lt_L(s + 8);
+  const bool bad = !(fl & TXV_FLAG_SIG64) || (fl & TXV_FLAG_BADMSG) || (s[15] & 0xE0000000u) || !a.decode_ok[v] ||
+                   !sc_lt_L(s + 8);
   if (bad) { a.ok_out[i] = 0; return; }
   const uint32_t* pw = a.pubs_le + (size_t)v * 8;
   uint64_t pre[8];

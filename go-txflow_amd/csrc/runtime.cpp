@@ -40,6 +40,11 @@ struct Slot {
   uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr; uint8_t* d_pre = nullptr;
   uint32_t* d_kbuf = nullptr; uint32_t* d_order = nullptr; uint32_t* h_order = nullptr;
   uint32_t n_work = 0;
+  // set-major tally order: pending votes grouped by (set, validator), arrival order inside
+  uint32_t* d_toff = nullptr; uint32_t* h_toff = nullptr;
+  uint32_t* d_tvote = nullptr; uint32_t* h_tvote = nullptr;
+  uint32_t* d_tval = nullptr; uint32_t* h_tval = nullptr;
+  uint32_t* d_ent_vote = nullptr; int64_t* d_ent_power = nullptr; uint32_t* d_ent_val = nullptr;
   uint32_t* d_touched = nullptr; int64_t* d_tsum = nullptr; uint8_t* d_tmaj = nullptr; uint32_t* d_tcross = nullptr;
   // pinned host
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
@@ -90,11 +95,11 @@ struct txv_ctx {
   std::vector<std::string> tx_keys;
   std::vector<int64_t> h_sum;
   std::vector<uint8_t> h_maj;
-  std::vector<uint32_t> seen_epoch;
-  uint32_t* d_acc_slot = nullptr; uint64_t* d_first_tag = nullptr; uint32_t* d_arena = nullptr;
-  uint32_t* d_arena_count = nullptr; uint32_t* d_errflags = nullptr;
-  int64_t* d_set_sum = nullptr; uint32_t* d_set_cross = nullptr; uint32_t* d_bitmap = nullptr;
-  uint32_t epoch = 0;
+  std::vector<uint32_t> seen_stage, set_tidx;   // per set: last staging that touched it, its index there
+  uint32_t stage_count = 0;
+  uint32_t* d_acc_slot = nullptr; uint32_t* d_arena = nullptr;
+  int64_t* d_set_sum = nullptr; uint32_t* d_bitmap = nullptr;
+  uint64_t arena_used = 0;          // arena rows reserved by the batches run since the last reset
   // signer slots (load generator)
   uint32_t n_signers = 0;
   uint32_t *d_sk_scal = nullptr, *d_sk_araw = nullptr, *d_sk_prefix = nullptr, *d_sk_pub = nullptr;
@@ -150,6 +155,10 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
         (r = dalloc(c, &s.d_pre, npad)) || (r = dalloc(c, &s.d_kbuf, 8 * npad)) ||
         (r = dalloc(c, &s.d_order, npad)) || (r = halloc(c, &s.h_order, npad)) ||
+        (r = dalloc(c, &s.d_tvote, npad)) || (r = halloc(c, &s.h_tvote, npad)) ||
+        (r = dalloc(c, &s.d_tval, npad)) || (r = halloc(c, &s.h_tval, npad)) ||
+        (r = dalloc(c, &s.d_ent_vote, npad)) || (r = dalloc(c, &s.d_ent_power, npad)) ||
+        (r = dalloc(c, &s.d_ent_val, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
         (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)))
@@ -160,6 +169,7 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
   if (s.touched_cap < need) {
     int r;
     if ((r = dalloc(c, &s.d_touched, need)) || (r = dalloc(c, &s.d_tsum, need)) || (r = dalloc(c, &s.d_tmaj, need)) ||
+        (r = dalloc(c, &s.d_toff, need + 1)) || (r = halloc(c, &s.h_toff, need + 1)) ||
         (r = dalloc(c, &s.d_tcross, need)) || (r = halloc(c, &s.h_touched, need)) || (r = halloc(c, &s.h_tsum, need)) ||
         (r = halloc(c, &s.h_tmaj, need)) || (r = halloc(c, &s.h_tcross, need)))
       return r;
@@ -173,10 +183,8 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
 int alloc_tally(txv_ctx* c) {
   const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
   int r;
-  if ((r = dalloc(c, &c->d_acc_slot, cells)) || (r = dalloc(c, &c->d_first_tag, cells)) ||
-      (r = dalloc(c, &c->d_arena, (size_t)c->cfg.max_accepted * 16)) || (r = dalloc(c, &c->d_arena_count, 1)) ||
-      (r = dalloc(c, &c->d_errflags, 1)) || (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
-      (r = dalloc(c, &c->d_set_cross, c->cfg.max_txs)) || (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)))
+  if ((r = dalloc(c, &c->d_acc_slot, cells)) || (r = dalloc(c, &c->d_arena, (size_t)c->cfg.max_accepted * 16)) ||
+      (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) || (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)))
     return r;
   return TXV_OK;
 }
@@ -184,23 +192,20 @@ int alloc_tally(txv_ctx* c) {
 int reset_tally(txv_ctx* c, bool keep_ids = false) {
   const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
   HIP_TRY(c, hipMemsetAsync(c->d_acc_slot, 0, cells * 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_arena_count, 0, 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_errflags, 0, 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
-  c->epoch = 0;
+  c->arena_used = 0;
   if (keep_ids) {
     std::fill(c->h_sum.begin(), c->h_sum.end(), 0);
     std::fill(c->h_maj.begin(), c->h_maj.end(), 0);
-    std::fill(c->seen_epoch.begin(), c->seen_epoch.end(), 0);
     return TXV_OK;
   }
   c->tx_index.clear();
   c->tx_keys.clear();
   c->h_sum.clear();
   c->h_maj.clear();
-  c->seen_epoch.clear();
+  c->seen_stage.clear();
+  c->set_tidx.clear();
   return TXV_OK;
 }
 
@@ -275,6 +280,29 @@ int upload_slot(txv_ctx* c, Slot& s) {
   return TXV_OK;
 }
 
+// set-major tally order (AddVote path): stable counting sort of the validator-sorted pending
+// votes (h_order) by touched-set index gives (set, validator, arrival) order
+int build_set_order(txv_ctx* c, Slot& s) {
+  uint32_t* off = s.h_toff;
+  std::fill(off, off + s.n_touched + 1, 0u);
+  for (uint32_t q = 0; q < s.n_work; ++q) off[c->set_tidx[s.h_set[s.h_order[q]]] + 1]++;
+  for (uint32_t t = 0; t < s.n_touched; ++t) off[t + 1] += off[t];
+  std::vector<uint32_t> cur(off, off + s.n_touched);
+  for (uint32_t q = 0; q < s.n_work; ++q) {
+    const uint32_t i = s.h_order[q];
+    const uint32_t p = cur[c->set_tidx[s.h_set[i]]]++;
+    s.h_tvote[p] = i;
+    s.h_tval[p] = s.h_val[i] | ((s.h_flags[i] & TXV_FLAG_SIG64) ? 0x80000000u : 0u) |
+                  ((s.h_flags[i] & TXV_FLAG_BADMSG) ? 0x40000000u : 0u);
+  }
+  HIP_TRY(c, hipMemcpyAsync(s.d_toff, s.h_toff, (size_t)(s.n_touched + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  if (s.n_work) {
+    HIP_TRY(c, hipMemcpyAsync(s.d_tvote, s.h_tvote, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_tval, s.h_tval, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  return TXV_OK;
+}
+
 // Counting sort of the pending votes by validator: K1b then runs waves whose lanes mostly
 // share one validator's A table (L1/L2-resident gathers instead of scattered MALL reads).
 void build_order(Slot& s) {
@@ -318,16 +346,16 @@ int ensure_park(txv_ctx* c) {
   return TXV_OK;
 }
 
-TallyArgs tally_args(txv_ctx* c, Slot& s) {
+TallyArgs tally_args(txv_ctx* c, Slot& s, uint32_t arena_base) {
   TallyArgs a{};
-  a.n = s.n; a.n_pad = s.n_pad; a.n_vals = c->n_vals; a.epoch_hi = 0xFFFFFFFFu - c->epoch;
-  a.quorum = c->quorum;
-  a.sig = s.d_sig; a.set = s.d_set; a.val = s.d_val; a.flags = s.d_flags; a.ok = s.d_ok;
-  a.pre = s.d_pre; a.status = s.d_status;
-  a.acc_slot = c->d_acc_slot; a.first_tag = c->d_first_tag; a.arena = c->d_arena; a.arena_count = c->d_arena_count;
-  a.arena_cap = c->cfg.max_accepted; a.n_touched = s.n_touched; a.error_flags = c->d_errflags;
-  a.power = c->d_power; a.set_sum = c->d_set_sum; a.set_cross = c->d_set_cross; a.commit_bitmap = c->d_bitmap;
-  a.touched = s.d_touched; a.t_sum = s.d_tsum; a.t_maj = s.d_tmaj; a.t_cross = s.d_tcross;
+  a.n = s.n; a.n_pad = s.n_pad; a.n_vals = c->n_vals; a.n_touched = s.n_touched;
+  a.quorum = c->quorum; a.arena_base = arena_base;
+  a.sig = s.d_sig; a.ok = s.d_ok; a.pre = s.d_pre; a.status = s.d_status;
+  a.touched = s.d_touched; a.toff = s.d_toff; a.tvote = s.d_tvote; a.tval = s.d_tval;
+  a.ent_vote = s.d_ent_vote; a.ent_power = s.d_ent_power; a.ent_val = s.d_ent_val;
+  a.acc_slot = c->d_acc_slot; a.arena = c->d_arena;
+  a.power = c->d_power; a.set_sum = c->d_set_sum; a.commit_bitmap = c->d_bitmap;
+  a.t_sum = s.d_tsum; a.t_maj = s.d_tmaj; a.t_cross = s.d_tcross;
   return a;
 }
 
@@ -342,8 +370,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   int r = ensure_slot(c, s, v->n, mw);
   if (r) return r;
   s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw;
-  // epoch used for touched-set de-duplication on the host
-  const uint32_t host_epoch = c->epoch + 1;
+  // staging counter for touched-set de-duplication on the host
+  const uint32_t stage_id = ++c->stage_count;
   s.n_touched = 0;
   for (uint32_t i = 0; i < v->n; ++i) {
     s.h_flags[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0;
@@ -356,10 +384,14 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       if (sid >= c->cfg.max_txs) { c->err = "TxVoteSets exceed max_txs"; return TXV_ECAPACITY; }
       c->tx_index.emplace(key, sid);
       c->tx_keys.push_back(std::move(key));
-      c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_epoch.push_back(0);
+      c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_stage.push_back(0); c->set_tidx.push_back(0);
     } else sid = it->second;
     s.h_set[i] = sid;
-    if (c->seen_epoch[sid] != host_epoch) { c->seen_epoch[sid] = host_epoch; s.h_touched[s.n_touched++] = sid; }
+    if (c->seen_stage[sid] != stage_id) {
+      c->seen_stage[sid] = stage_id;
+      c->set_tidx[sid] = s.n_touched;
+      s.h_touched[s.n_touched++] = sid;
+    }
     if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
     uint32_t vi = UINT32_MAX;
     if (v->addr_len[i] == 20) {
@@ -368,13 +400,14 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     }
     if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
     s.h_val[i] = vi;
-    if (lens[i] < 0) { s.h_status[i] = TXV_ERR_SIGNBYTES; continue; }
+    // a SignBytes failure is only reached after the accepted-vote check (AddVote order), so
+    // the vote stays pending with BADMSG: it never verifies and the tally resolves it
     s.h_status[i] = 0xFF;
-    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
+    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
   }
   build_order(s);
   pack_columns(s, v, lens);
-  if ((r = upload_slot(c, s))) return r;
+  if ((r = upload_slot(c, s)) || (r = build_set_order(c, s))) return r;
   s.staged = true; s.ran = false;
   return TXV_OK;
 }
@@ -382,19 +415,17 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
 int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   Slot& s = c->slots[slot];
   if (!s.staged) { c->err = "slot not staged"; return TXV_ESTATE; }
-  c->epoch++;
-  if (c->epoch == 0xFFFFFFFFu) {   // tag space exhausted: clear candidates once
-    const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
-    HIP_TRY(c, hipMemsetAsync(c->d_first_tag, 0xFF, cells * 8, c->stream));
-    c->epoch = 1;
-  }
+  // arena rows [arena_used, arena_used + n) are this batch's (row = base + arrival index)
+  if (c->arena_used + s.n > c->cfg.max_accepted) { c->err = "accepted-signature arena full"; return TXV_ECAPACITY; }
+  const uint32_t arena_base = (uint32_t)c->arena_used;
+  c->arena_used += s.n;
   int r;
   if ((r = ensure_park(c))) return r;
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
-  TallyArgs ta = tally_args(c, s);
+  TallyArgs ta = tally_args(c, s, arena_base);
   HIP_TRY(c, txv_launch_tally(&ta, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
   s.ran = true;
@@ -416,10 +447,7 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
     HIP_TRY(c, hipMemcpyAsync(s.h_tmaj, s.d_tmaj, s.n_touched, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(s.h_tcross, s.d_tcross, (size_t)s.n_touched * 4, hipMemcpyDeviceToHost, c->stream));
   }
-  uint32_t errf = 0;
-  HIP_TRY(c, hipMemcpyAsync(&errf, c->d_errflags, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if (errf & TXV_DEVERR_ARENA_FULL) { c->err = "accepted-signature arena full"; return TXV_ECAPACITY; }
   if (status_out) memcpy(status_out, s.h_status, s.n);
   uint32_t ne = 0;
   for (uint32_t t = 0; t < s.n_touched; ++t) {
@@ -558,15 +586,16 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
-    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_order); hfree(s.h_order); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
+    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_order); hfree(s.h_order);
+    dfree(s.d_toff); hfree(s.h_toff); dfree(s.d_tvote); hfree(s.h_tvote); dfree(s.d_tval); hfree(s.h_tval);
+    dfree(s.d_ent_vote); dfree(s.d_ent_power); dfree(s.d_ent_val); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
     hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
-  dfree(c->d_acc_slot); dfree(c->d_first_tag); dfree(c->d_arena); dfree(c->d_arena_count); dfree(c->d_errflags);
-  dfree(c->d_set_sum); dfree(c->d_set_cross); dfree(c->d_bitmap);
+  dfree(c->d_acc_slot); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_bitmap);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;

@@ -16,6 +16,8 @@
 
 #define TXV_FLAG_PENDING 0x01u   // vote reaches the Verify step (pre-checks passed)
 #define TXV_FLAG_SIG64   0x02u   // len(Signature) == 64
+#define TXV_FLAG_BADMSG  0x04u   // SignBytes failed (amino time range): never verifies; the
+                                 // tally still resolves it against an accepted vote first
 
 struct VerifyArgs {
   uint32_t n, n_pad, msg_words, n_work;   // n_work: entries of order[] (pending votes)

@@ -1,10 +1,13 @@
 // txv_tally.h — argument block of the tally kernels (kernels_tally.hip).
 //
 // Device tally state (persistent across batches, HBM):
-//   acc_slot[max_txs * n_vals]  u32  0 = no accepted vote, else arena index + 1
-//   first_tag[max_txs * n_vals] u64  epoch-tagged smallest verified arrival index (atomicMin)
+//   acc_slot[max_txs * n_vals]  u32  0 = no accepted vote, else arena row + 1
 //   arena[max_accepted][16]     u32  accepted signature bytes (for dup/conflict compares)
-//   set_sum[max_txs] i64, set_cross[max_txs] u32, commit_bitmap[max_txs/32] u32
+//   set_sum[max_txs] i64, commit_bitmap[max_txs/32] u32
+// Per batch (staged by the host with the votes, set-major):
+//   toff[n_touched + 1]   u32  vote range of touched set t in tvote/tval
+//   tvote[n_work], tval[n_work]  pending votes grouped by (set, validator), arrival order
+//                              inside each group (stable counting sorts on the host)
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>
@@ -14,30 +17,29 @@
 #define TXV_ERR_NONDETERMINISTIC_DEV 5u
 #define TXV_ERR_INVALID_SIGNATURE_DEV 6u
 #define TXV_NO_CROSS 0xFFFFFFFFu
-#define TXV_DEVERR_ARENA_FULL 1u
 
 struct TallyArgs {
-  uint32_t n, n_pad, n_vals, epoch_hi;
+  uint32_t n, n_pad, n_vals, n_touched;
   int64_t quorum;
+  uint32_t arena_base;          // arena rows [arena_base, arena_base + n) belong to this batch
+  uint32_t pad0;
   const uint32_t* sig;          // [16][n_pad]
-  const uint32_t* set;          // [n]
-  const uint32_t* val;          // [n]
-  const uint8_t* flags;         // [n]
-  const uint8_t* ok;            // [n] verify verdicts
+  const uint8_t* ok;            // [n] verify verdicts (1 = valid)
   const uint8_t* pre;           // [n] host pre-check: 0xFF pending, else the final error code
   uint8_t* status;              // [n] out: final code | fired bit (pre is never modified, so a
                                 //      staged batch can be re-run)
+  const uint32_t* touched;      // [n_touched] set ids present in the batch
+  const uint32_t* toff;         // [n_touched + 1]
+  const uint32_t* tvote;        // [n_work]
+  const uint32_t* tval;         // [n_work]
+  uint32_t* ent_vote;           // [n_work] scratch: ADDED votes of set t at toff[t]..
+  int64_t* ent_power;           // [n_work]
+  uint32_t* ent_val;            // [n_work]
   uint32_t* acc_slot;
-  uint64_t* first_tag;
   uint32_t* arena;
-  uint32_t* arena_count;
-  uint32_t arena_cap, n_touched;
-  uint32_t* error_flags;
   const int64_t* power;         // [n_vals]
   int64_t* set_sum;
-  uint32_t* set_cross;
   uint32_t* commit_bitmap;
-  const uint32_t* touched;      // [n_touched] set ids present in the batch
   int64_t* t_sum;               // [n_touched] outputs
   uint8_t* t_maj;
   uint32_t* t_cross;

@@ -74,7 +74,9 @@ typedef struct {
   uint32_t max_batch;       /* votes per call (default 1<<20) */
   uint32_t max_txs;         /* TxVoteSets capacity (default 1<<20) */
   uint32_t max_validators;  /* default 1024 */
-  uint32_t max_accepted;    /* accepted-signature arena capacity (default max_txs * 128) */
+  uint32_t max_accepted;    /* accepted-signature arena rows (default min(max_txs * 128, 2^28)); every
+                               txv_add_votes / txv_run_staged batch reserves one row per vote
+                               until txv_reset_tally (TXV_ECAPACITY when exhausted) */
   uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
   uint32_t flags;           /* TXV_CFG_* bits */
   uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 8192):

@@ -59,6 +59,17 @@ def scenario_votes(O):
     out.append(("TestConflicts", c, [6, 0, 5], [0, 0, 0]))
     # nil / empty address
     out.append(("NilAndEmpty", [dict(nil=True), dict(_vote(O, seeds[4], addrs[4], tx1), addr=b"")], [2, 3], [0, 0]))
+    # SignBytes is only reached inside Verify, AFTER the accepted-vote check (vote_set.go:108-117):
+    # an out-of-amino-range timestamp (year 10000) is a SignBytes error only when the group has
+    # no accepted vote; against an accepted vote it is a duplicate / non-deterministic signature.
+    far = (253402300800, 0)
+    ok5 = _vote(O, seeds[5], addrs[5], tx1, ts=(1_700_000_000, 300))
+    sb = [dict(ok5, ts_sec=far[0], ts_nanos=far[1], sig=_vote(O, seeds[5], addrs[5], tx1)["sig"]),
+          ok5,
+          dict(ok5, ts_sec=far[0], ts_nanos=far[1]),
+          dict(ok5, ts_sec=far[0], ts_nanos=far[1], sig=bytes(64)),
+          dict(_vote(O, seeds[6], addrs[6], tx1), ts_sec=far[0], ts_nanos=far[1])]
+    out.append(("SignBytesAfterAccepted", sb, [8, 0, 1, 5, 8], [0] * 5))
     return pubs, out
 
 
