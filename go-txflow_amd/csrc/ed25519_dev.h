@@ -84,7 +84,11 @@ TXV_HD void sha512_prefixed(uint32_t digest_le[16], const uint64_t* pre, int pre
 // table entry fetch: T[pos][idx] from a flat word array
 template <int W, typename Ptr>
 TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
+#if defined(TXV_EXP_L2_TABLES)   // experiment only: every lookup hits one entry (L1/L2 resident)
+  const size_t base = (size_t)(1 + (idx & 1)) * kEntryWords;
+#else
   const size_t base = (size_t)(uint32_t)(pos * Tab<W>::kEntries + idx) * kEntryWords;
+#endif
   ge_niels e;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {

@@ -80,18 +80,18 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
 //                         -> k[8][n_pad] (32 B/vote, HBM) and the "go" flag in ok_out
 //   K1b txv_k_scalarmult  per vote, in validator-grouped order: [s]B + [k](-A), encode, compare with R
 
-__global__ void __launch_bounds__(256) txv_k_challenge(VerifyArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
+// Prechecks + challenge of vote i: false if the vote is rejected before the group equation
+// (length, sig[63] & 0xE0, undecodable A, s >= L, SignBytes failure), else k = SHA-512(R||A||M)
+// mod L and the S half of the signature.
+__device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, uint32_t k_out[8], uint32_t s_out[8]) {
   const uint8_t fl = a.flags[i];
-  if (!(fl & TXV_FLAG_PENDING)) return;
   const uint32_t v = a.val[i];
   uint32_t s[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
   const bool bad = !(fl & TXV_FLAG_SIG64) || (fl & TXV_FLAG_BADMSG) || (s[15] & 0xE0000000u) || !a.decode_ok[v] ||
                    !sc_lt_L(s + 8);
-  if (bad) { a.ok_out[i] = 0; return; }
+  if (bad) return false;
   const uint32_t* pw = a.pubs_le + (size_t)v * 8;
   uint64_t pre[8];
 #pragma unroll
@@ -104,7 +104,19 @@ __global__ void __launch_bounds__(256) txv_k_challenge(VerifyArgs a) {
   sha512_prefixed(dig, pre, 8, m);
   sc k = sc_reduce512(dig);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a.kbuf[(size_t)j * a.n_pad + i] = k.v[j];
+  for (int j = 0; j < 8; ++j) { k_out[j] = k.v[j]; s_out[j] = s[8 + j]; }
+  return true;
+}
+
+// K1a: challenges of every pending vote into kbuf (99 VGPRs: 5 waves/SIMD)
+__global__ void __launch_bounds__(256, 4) txv_k_challenge(VerifyArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  if (!(a.flags[i] & TXV_FLAG_PENDING)) return;
+  uint32_t k[8], s[8];
+  if (!vote_challenge(a, i, k, s)) { a.ok_out[i] = 0; return; }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a.kbuf[(size_t)j * a.n_pad + i] = k[j];
   a.ok_out[i] = 2;   // passed the scalar checks; K1b decides
 }
 
@@ -248,11 +260,10 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
       if (act >> h & 1u) {
         const uint32_t idx = V * g + h;
         const uint32_t i = a.order ? a.order[idx] : idx;
-        const uint32_t v = a.val[i];
         uint32_t s[8], k[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-        R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)v * Tab<WA>::kWords, s, k, true);
+        R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)a.val[i] * Tab<WA>::kWords, s, k, true);
       } else {
         R = ge_identity();
       }
@@ -476,6 +487,8 @@ bool txv_verify_windows_supported(int wb, int wa) {
 hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (!args->n) return hipSuccess;
   if (!txv_verify_windows_supported(wb, wa)) return hipErrorInvalidValue;
+  // K1a stays a separate launch: fused into the 4-vote kernel (128-VGPR budget) the SHA-512
+  // phase spilled and every wave hit its memory stalls at the same time (2.29 vs 2.12 ms)
   hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
   if (args->n_work) {
     constexpr int B = TXV_VERIFY_BLOCK;

@@ -84,7 +84,7 @@ struct txv_ctx {
   uint32_t* d_btable_wide = nullptr;   // base-point table for b_w > tab_w (gigabytes at b_w >= 22)
   int btable_wide_w = 0;
   uint32_t lane_votes = 4;         // K1b votes per lane (one shared inversion)
-  uint32_t* d_park = nullptr;      // K1b parked points: [V-1][32][grid x block]
+  uint32_t* d_park = nullptr;      // K1b parked points: [wave][V-1][32][64]
   size_t park_words = 0;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;

@@ -33,7 +33,7 @@ struct VerifyArgs {
   const uint32_t* atables;     // [n_vals][kTableWords]
   const uint32_t* btable;      // [kTableWords]
   uint8_t* ok_out;             // [n]
-  uint32_t* park;              // [V-1][32][lanes] parked points of the multi-vote K1b (lanes = grid x block)
+  uint32_t* park;              // [waves][V-1][32][64] parked points of the multi-vote K1b
   uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2 or 4)
 };
 

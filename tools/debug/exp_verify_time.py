@@ -1,0 +1,26 @@
+"""Time K1 (verify) and K2 (tally) of the C2 workload against an alternative libtxvote build
+(experiments: python tools/debug/exp_verify_time.py build_exp/libX.so ...).  Statuses are
+not checked: experiment builds may compute wrong verdicts on purpose."""
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "go-txflow_amd"))
+import txflow_amd as T  # noqa: E402
+from txflow_amd.workload import Workload, SEEDS  # noqa: E402
+
+for path in sys.argv[1:]:
+    T._lib = None
+    T.LIB_PATH = os.path.abspath(path)
+    ctx = T.Context(max_batch=2 * 1_000_000, max_txs=10_064, max_validators=100)
+    wl = Workload(ctx, 100, 10_000, SEEDS["c2"])
+    ctx.stage(0, wl.batch)
+    v, t = [], []
+    for rep in range(6):
+        ctx.reset_tally()
+        ms = ctx.run_staged(0, timed=True)
+        ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1)
+        if rep:
+            v.append(ms[0]); t.append(ms[1])
+    print(f"{os.path.basename(path)}: verify {statistics.median(v):.3f} ms  tally {statistics.median(t):.3f} ms", flush=True)
+    ctx.close()
