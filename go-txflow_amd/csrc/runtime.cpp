@@ -532,6 +532,79 @@ int select_window(txv_ctx* c, int w) {
   return TXV_OK;
 }
 
+// Key registry a verify-only call runs against: the validator registry, or a throw-away set
+// built from caller-supplied keys.
+struct KeySet {
+  const uint32_t* pubs;
+  const uint8_t* ok;
+  const uint32_t* tables;
+  int w;
+};
+
+KeySet registry_keys(const txv_ctx* c) { return KeySet{c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w}; }
+
+// Caller-supplied keys (txv_verify_batch with pubs32, txv_verify_bytes): de-duplicated into
+// throw-away tables -- the registry's window when they fit the table budget (its B table
+// already exists), else the 55 KB radix-16 tables; without a registry the window is chosen
+// for these keys alone.  kidx[i] = key slot of item i; key_addr (optional) receives
+// SHA-256(key)[:20] per slot, computed on the device by K0.
+int prepare_keys(txv_ctx* c, const uint8_t* pubs32, uint32_t n, std::vector<uint32_t>& kidx,
+                 std::vector<uint8_t>* key_addr, KeySet& ks) {
+  std::unordered_map<std::string, uint32_t> uniq;
+  std::vector<uint8_t> ukeys;
+  kidx.resize(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    std::string k((const char*)pubs32 + (size_t)i * 32, 32);
+    auto it = uniq.find(k);
+    if (it == uniq.end()) {
+      it = uniq.emplace(k, (uint32_t)uniq.size()).first;
+      ukeys.insert(ukeys.end(), k.begin(), k.end());
+    }
+    kidx[i] = it->second;
+  }
+  const uint32_t nu = (uint32_t)uniq.size();
+  int r, w_keys;
+  if (c->tab_w) {
+    w_keys = (uint64_t)nu * table_words(c->tab_w) * 4 <= ((uint64_t)c->cfg.table_budget_mb << 20) ? c->tab_w : 4;
+  } else {
+    w_keys = choose_window(c, nu);
+    if (w_keys != 4 && (r = build_base_table(c, w_keys))) return r;
+  }
+  if (nu > c->tmp_cap || w_keys != c->tmp_w) {
+    if ((r = dalloc(c, &c->d_tmp_pubs, (size_t)nu * 8)) || (r = dalloc(c, &c->d_tmp_ok, nu)) ||
+        (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * table_words(w_keys))) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
+      return r;
+    c->tmp_cap = nu;
+    c->tmp_w = w_keys;
+  }
+  if (nu) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_tmp_pubs, ukeys.data(), (size_t)nu * 32, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, txv_launch_build_tables(w_keys, c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
+  }
+  if (key_addr) {
+    key_addr->resize((size_t)nu * 20);
+    if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr->data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  ks = KeySet{c->d_tmp_pubs, c->d_tmp_ok, c->d_tmp_tables, w_keys};
+  return TXV_OK;
+}
+
+// Upload slot s and run K1 (verify only) against key set ks; ok[i] = 1 when vote i verified.
+int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) {
+  int r;
+  if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
+  VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables);
+  const bool reg_w = ks.w == c->tab_w;
+  const int w_base = reg_w ? c->b_w : ks.w;
+  va.btable = reg_w ? c->d_btable : (ks.w == 4 ? c->d_btable4 : c->d_btable8);
+  HIP_TRY(c, txv_launch_verify(w_base, ks.w, &va, verify_grid(c, s.n), c->stream));
+  ok.resize(s.n);
+  if (s.n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, s.n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
 }  // namespace
 
 // ==================================================================== C ABI
@@ -669,48 +742,11 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   int r = ensure_slot(c, s, v->n, mw);
   if (r) return r;
   s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
-  // key registry for this call
-  const uint32_t* kp = c->d_pubs; const uint8_t* kok = c->d_decode_ok; const uint32_t* ktab = c->d_atables;
-  int w_keys = c->tab_w;
-  std::vector<uint8_t> key_addr;
+  KeySet ks = registry_keys(c);
   if (pubs32) {
-    std::unordered_map<std::string, uint32_t> uniq;
-    std::vector<uint8_t> ukeys;
-    std::vector<uint32_t> kidx(v->n);
-    for (uint32_t i = 0; i < v->n; ++i) {
-      std::string k((const char*)pubs32 + (size_t)i * 32, 32);
-      auto it = uniq.find(k);
-      if (it == uniq.end()) {
-        it = uniq.emplace(k, (uint32_t)uniq.size()).first;
-        ukeys.insert(ukeys.end(), k.begin(), k.end());
-      }
-      kidx[i] = it->second;
-    }
-    const uint32_t nu = (uint32_t)uniq.size();
-    // caller-supplied keys get throw-away tables: the registry's window if they fit the budget
-    // (its B table already exists), else the 55 KB radix-16 tables.  Without a registry the
-    // window is chosen for these keys alone.
-    if (c->tab_w) {
-      w_keys = (uint64_t)nu * table_words(c->tab_w) * 4 <= ((uint64_t)c->cfg.table_budget_mb << 20) ? c->tab_w : 4;
-    } else {
-      w_keys = choose_window(c, nu);
-      if (w_keys != 4 && (r = build_base_table(c, w_keys))) return r;
-    }
-    if (nu > c->tmp_cap || w_keys != c->tmp_w) {
-      if ((r = dalloc(c, &c->d_tmp_pubs, (size_t)nu * 8)) || (r = dalloc(c, &c->d_tmp_ok, nu)) ||
-          (r = dalloc(c, &c->d_tmp_tables, (size_t)nu * table_words(w_keys))) || (r = dalloc(c, &c->d_tmp_addr, (size_t)nu * 5)))
-        return r;
-      c->tmp_cap = nu;
-      c->tmp_w = w_keys;
-    }
-    if (nu) {
-      HIP_TRY(c, hipMemcpyAsync(c->d_tmp_pubs, ukeys.data(), (size_t)nu * 32, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(c, txv_launch_build_tables(w_keys, c->d_tmp_pubs, nu, c->d_tmp_tables, c->d_tmp_ok, c->d_tmp_addr, c->stream));
-    }
-    key_addr.resize((size_t)nu * 20);
-    if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr.data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    kp = c->d_tmp_pubs; kok = c->d_tmp_ok; ktab = c->d_tmp_tables;
+    std::vector<uint32_t> kidx;
+    std::vector<uint8_t> key_addr;
+    if ((r = prepare_keys(c, pubs32, v->n, kidx, &key_addr, ks))) return r;
     for (uint32_t i = 0; i < v->n; ++i) {
       s.h_flags[i] = 0; s.h_set[i] = 0; s.h_val[i] = kidx[i];
       if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
@@ -738,18 +774,54 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   }
   build_order(s);
   pack_columns(s, v, lens);
-  if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
-  VerifyArgs va = verify_args(c, s, kp, kok, ktab);
-  const int w_base = (w_keys == c->tab_w) ? c->b_w : w_keys;
-  va.btable = w_base == c->b_w && w_keys == c->tab_w ? c->d_btable : (w_keys == 4 ? c->d_btable4 : c->d_btable8);
-  HIP_TRY(c, txv_launch_verify(w_base, w_keys, &va, verify_grid(c, s.n), c->stream));
-  std::vector<uint8_t> ok(v->n);
-  if (v->n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, v->n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::vector<uint8_t> ok;
+  if ((r = run_verify(c, s, ks, ok))) return r;
   for (uint32_t i = 0; i < v->n; ++i) {
-    if (s.h_status[i] == 0xFF) status_out[i] = ok[i] ? TXV_ADDED : TXV_ERR_INVALID_SIGNATURE;
+    if (s.h_status[i] == 0xFF) status_out[i] = ok[i] == 1 ? TXV_ADDED : TXV_ERR_INVALID_SIGNATURE;
     else status_out[i] = s.h_status[i];
   }
+  return TXV_OK;
+}
+
+int txv_verify_bytes(txv_ctx* c, const uint8_t* pubs32, const uint8_t* msgs, const uint32_t* msg_off,
+                     const uint32_t* msg_len, const uint8_t* sigs64, const uint32_t* sig_len, uint32_t n,
+                     uint8_t* ok_out) {
+  if (!c || (n && (!pubs32 || !msg_off || !msg_len || !sigs64 || !sig_len || !ok_out))) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  if (!n) return TXV_OK;
+  Slot& s = c->slots[kSlots - 1];
+  // the messages go to the device as they are (SHA-512 input R || A || msg)
+  std::vector<int> lens(n);
+  s.tmp_msg.clear();
+  s.tmp_off.resize(n);
+  uint32_t mx = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (msg_len[i] > TXV_MAX_RAW_MSG || (msg_len[i] && !msgs)) { c->err = "bad message length"; return TXV_EINVAL; }
+    s.tmp_off[i] = s.tmp_msg.size();
+    s.tmp_msg.insert(s.tmp_msg.end(), msgs + (msg_len[i] ? msg_off[i] : 0), msgs + (msg_len[i] ? msg_off[i] + msg_len[i] : 0));
+    lens[i] = (int)msg_len[i];
+    mx = std::max(mx, msg_len[i]);
+  }
+  const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
+  int r = ensure_slot(c, s, n, mw);
+  if (r) return r;
+  s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
+  std::vector<uint32_t> kidx;
+  KeySet ks;
+  if ((r = prepare_keys(c, pubs32, n, kidx, nullptr, ks))) return r;
+  for (uint32_t i = 0; i < n; ++i) {
+    s.h_set[i] = 0; s.h_val[i] = kidx[i]; s.h_status[i] = 0xFF;
+    s.h_flags[i] = TXV_FLAG_PENDING | (sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
+  }
+  build_order(s);
+  txv_votes view{};
+  view.n = n; view.sig = sigs64; view.sig_len = sig_len;
+  pack_columns(s, &view, lens);
+  std::vector<uint8_t> ok;
+  if ((r = run_verify(c, s, ks, ok))) return r;
+  for (uint32_t i = 0; i < n; ++i) ok_out[i] = ok[i] == 1 ? 1 : 0;
   return TXV_OK;
 }
 

@@ -86,6 +86,7 @@ def lib():
             "txv_set_validators": ([vp, vp, vp, u32, ctypes.c_char_p, u32], ctypes.c_int),
             "txv_get_validator_info": ([vp, vp, vp, u32], ctypes.c_int),
             "txv_verify_batch": ([vp, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
+            "txv_verify_bytes": ([vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_add_votes": ([vp, ctypes.POINTER(_Votes), vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_query_tx": ([vp, ctypes.c_char_p, u32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_uint8)],
                              ctypes.c_int),
@@ -118,7 +119,7 @@ def lib():
 
 EXPORTED_SYMBOLS = [
     "txv_init", "txv_destroy", "txv_last_error", "txv_device_name", "txv_set_validators",
-    "txv_get_validator_info", "txv_verify_batch", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
+    "txv_get_validator_info", "txv_verify_batch", "txv_verify_bytes", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window"]
@@ -293,6 +294,26 @@ class Context:
             pp = pubs.ctypes.data
         self._chk(lib().txv_verify_batch(self._h, ctypes.byref(vs), pp, out.ctypes.data), "txv_verify_batch")
         return out[:batch.n]
+
+    def verify_bytes(self, pubs: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> np.ndarray:
+        """PubKeyEd25519.VerifyBytes(msg, sig) per (pub, msg, sig) triple (the call at
+        types/tx_vote.go:115); signatures of any length (only len 64 can verify)."""
+        n = len(pubs)
+        assert len(msgs) == n and len(sigs) == n
+        pk = np.frombuffer(b"".join(pubs), np.uint8) if n else np.zeros(32, np.uint8)
+        assert pk.size == 32 * max(n, 1) or n == 0
+        arena = np.frombuffer(b"".join(msgs) or b"\0", np.uint8)
+        ln = np.array([len(m) for m in msgs] or [0], np.uint32)
+        off = np.concatenate([[0], np.cumsum(ln[:-1], dtype=np.uint64)]).astype(np.uint32)
+        sg = np.zeros((max(n, 1), 64), np.uint8)
+        sl = np.zeros(max(n, 1), np.uint32)
+        for i, s in enumerate(sigs):
+            sl[i] = len(s)
+            sg[i, :min(64, len(s))] = np.frombuffer(s[:64], np.uint8)
+        out = np.zeros(max(n, 1), np.uint8)
+        self._chk(lib().txv_verify_bytes(self._h, pk.ctypes.data, arena.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                                         sg.ctypes.data, sl.ctypes.data, n, out.ctypes.data), "txv_verify_bytes")
+        return out[:n].astype(bool)
 
     def add_votes(self, batch: VoteBatch, ev_cap: int = 0):
         out = np.zeros(max(batch.n, 1), np.uint8)

@@ -11,6 +11,8 @@
  * Reference interfaces replaced (file:line in Fantom-foundation/go-txflow):
  *   txv_verify_batch   <- func (vote *TxVote) Verify(chainID string, pubKey crypto.PubKey) error
  *                         types/tx_vote.go:110-119  (ed25519 via tendermint VerifyBytes, :115)
+ *   txv_verify_bytes   <- crypto.PubKey.VerifyBytes(msg, sig []byte) bool (tendermint
+ *                         PubKeyEd25519, external; the call at types/tx_vote.go:115)
  *   txv_add_votes      <- func (txR *TxFlow) TryAddVote(vote *types.TxVote) (bool, error)
  *                         txflow/service.go:169-188 -> addVote :192-234
  *                         -> func (voteSet *TxVoteSet) AddVote(vote *TxVote) (bool, error)
@@ -139,6 +141,16 @@ int txv_get_validator_info(txv_ctx* ctx, uint8_t* addr20_out, uint8_t* decode_ok
  * TXV_ADDED (= nil error) / TXV_ERR_INVALID_VALIDATOR_ADDRESS / TXV_ERR_INVALID_SIGNATURE /
  * TXV_ERR_SIGNBYTES (and TXV_ERR_UNKNOWN_VALIDATOR when pubs32 == NULL and no key matches). */
 int txv_verify_batch(txv_ctx* ctx, const txv_votes* votes, const uint8_t* pubs32, uint8_t* status_out);
+
+/* crypto.PubKey.VerifyBytes(msg, sig) for n raw (pub, msg, sig) triples: tendermint
+ * PubKeyEd25519.VerifyBytes (external, called at types/tx_vote.go:115) = len(sig) != 64 -> false,
+ * else x/crypto ed25519.Verify(pub, msg, sig).  pubs32: n x 32 bytes; msgs: byte arena with
+ * msg_off[i] / msg_len[i] (msg_len[i] <= TXV_MAX_RAW_MSG); sigs64: n x 64 bytes holding the first
+ * 64 bytes of each signature, sig_len[i] its true length.  ok_out[i] = 1 accept, 0 reject. */
+#define TXV_MAX_RAW_MSG 16384
+int txv_verify_bytes(txv_ctx* ctx, const uint8_t* pubs32, const uint8_t* msgs, const uint32_t* msg_off,
+                     const uint32_t* msg_len, const uint8_t* sigs64, const uint32_t* sig_len, uint32_t n,
+                     uint8_t* ok_out);
 
 /* TxFlow.TryAddVote for each vote in arrival order (votes[0] first).  Semantics are exactly
  * the sequential loop's; see SURVEY.md Appendix A.3.  ev_out (capacity ev_cap) receives one
