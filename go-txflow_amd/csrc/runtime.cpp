@@ -961,6 +961,14 @@ int txv_reset_tally(txv_ctx* c) {
   return reset_tally(c, true);
 }
 
+int txv_reset_flow(txv_ctx* c) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->n_vals) return TXV_OK;
+  return reset_tally(c, false);
+}
+
 int txv_sync(txv_ctx* c) {
   if (!c) return TXV_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -102,6 +102,7 @@ def lib():
             "txv_fetch_staged": ([vp, u32, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_commit_bitmap": ([vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_reset_tally": ([vp], ctypes.c_int),
+            "txv_reset_flow": ([vp], ctypes.c_int),
             "txv_sync": ([vp], ctypes.c_int),
             "txv_fe_selftest": ([vp, vp, vp, vp, u32, ctypes.c_int], ctypes.c_int),
             "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
@@ -121,7 +122,7 @@ EXPORTED_SYMBOLS = [
     "txv_init", "txv_destroy", "txv_last_error", "txv_device_name", "txv_set_validators",
     "txv_get_validator_info", "txv_verify_batch", "txv_verify_bytes", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
-    "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_sync", "txv_fe_selftest",
+    "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window"]
 
 
@@ -395,6 +396,10 @@ class Context:
 
     def reset_tally(self):
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")
+
+    def reset_flow(self):
+        """forget every TxVoteSet (a fresh TxFlow, txflow/service.go:71); validators stay"""
+        self._chk(lib().txv_reset_flow(self._h), "txv_reset_flow")
 
     def sync(self):
         self._chk(lib().txv_sync(self._h), "txv_sync")

@@ -198,6 +198,9 @@ int txv_base_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids
  * already assigned stay assigned (their sets read as empty) */
 int txv_reset_tally(txv_ctx* ctx);
+/* a fresh TxFlow: forget every TxVoteSet and its tx id (TxVoteSets = make(map...) in NewTxFlow,
+ * txflow/service.go:71), keeping the validator set and its tables */
+int txv_reset_flow(txv_ctx* ctx);
 int txv_sync(txv_ctx* ctx);
 
 /* ---- self-test hook: field/scalar ops on device (tests only) ---- */

@@ -95,6 +95,24 @@ void orc_flow_free(orc_flow*);
  * the oracle does not verify; otherwise it verifies each vote that reaches step 4. */
 void orc_flow_add_votes(orc_flow*, const orc_vote* votes, uint32_t n, const uint8_t* verdicts,
                         uint8_t* status, int64_t* sum_after, uint8_t* fired);
+/* A batch in the txv_votes SoA layout (include/txvote.h): addr n x 20 and sig n x 64 hold
+ * the first 20 / 64 bytes, addr_len / sig_len the true lengths; is_nil may be NULL. */
+typedef struct {
+  uint32_t n;
+  const uint8_t* is_nil; const int64_t* height;
+  const uint8_t* txhash; const uint32_t* txhash_off; const uint32_t* txhash_len;
+  const int64_t* ts_sec; const int32_t* ts_nanos;
+  const uint8_t* addr; const uint32_t* addr_len;
+  const uint8_t* sig; const uint32_t* sig_len;
+} orc_soa;
+/* orc_flow_add_votes over an SoA batch; TxVote.Verify runs on `threads` threads first (for every
+ * vote whose address is a validator's), then the sequential loop consumes those outcomes. */
+void orc_flow_add_votes_soa(orc_flow*, const orc_soa* batch, int threads, uint8_t* status,
+                            int64_t* sum_after, uint8_t* fired);
+/* TxVote.Verify(chainID, pubKey) per vote of an SoA batch with caller-supplied keys pubs32[i]
+ * (n x 32); nil votes -> ORC_ERR_NIL.  out[i] = ORC_ADDED (nil error) or the error code. */
+void orc_txvote_verify_soa(const orc_soa* batch, const uint8_t* pubs32, const uint8_t* chain_id,
+                           size_t chain_len, int threads, uint8_t* out);
 /* Query a TxVoteSet: returns 0 if the tx has no set, else 1 and fills sum/maj23. */
 int orc_flow_query(orc_flow*, const uint8_t* txhash, uint32_t txhash_len, int64_t* sum, int32_t* maj23);
 uint32_t orc_flow_num_sets(orc_flow*);

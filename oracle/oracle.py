@@ -49,6 +49,10 @@ def lib():
         L.orc_flow_free.argtypes = [ctypes.c_void_p]
         L.orc_flow_add_votes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_flow_add_votes_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_txvote_verify_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_u8p, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_void_p]
         L.orc_flow_query.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint32,
                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
         L.orc_flow_num_sets.argtypes = [ctypes.c_void_p]
@@ -138,6 +142,32 @@ class _Vote(ctypes.Structure):
                 ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_uint32)]
 
 
+class _Soa(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32)] + [(k, ctypes.c_void_p) for k in (
+        "is_nil", "height", "txhash", "txhash_off", "txhash_len", "ts_sec", "ts_nanos", "addr", "addr_len",
+        "sig", "sig_len")]
+
+
+def _soa(b) -> _Soa:
+    return _Soa(b.n, None if b.is_nil is None else b.is_nil.ctypes.data, b.height.ctypes.data,
+                b.txhash_arena.ctypes.data, b.txhash_off.ctypes.data, b.txhash_len.ctypes.data,
+                b.ts_sec.ctypes.data, b.ts_nanos.ctypes.data, b.addr.ctypes.data, b.addr_len.ctypes.data,
+                b.sig.ctypes.data, b.sig_len.ctypes.data)
+
+
+def txvote_verify_batch(b, pubs32, chain_id: bytes, threads: int = 1):
+    """TxVote.Verify(chainID, pubs32[i]) for every vote of a VoteBatch-shaped object
+    (types/tx_vote.go:110-119); returns the status codes (ADDED = nil error)."""
+    import numpy as np
+    pk = np.ascontiguousarray(np.asarray(pubs32, np.uint8).reshape(-1, 32))
+    assert pk.shape[0] >= b.n
+    out = np.zeros(max(b.n, 1), np.uint8)
+    soa = _soa(b)
+    lib().orc_txvote_verify_soa(ctypes.addressof(soa), pk.ctypes.data, chain_id, len(chain_id), threads,
+                                out.ctypes.data)
+    return out[:b.n]
+
+
 class Flow:
     """Sequential TxFlow.addVote/TxVoteSet.AddVote restatement (txflow/service.go:192-234,
     types/vote_set.go:81-166).  votes: list of dicts with keys
@@ -185,6 +215,20 @@ class Flow:
         lib().orc_flow_add_votes(self._h, ctypes.addressof(arr), n, vp, status.ctypes.data,
                                  sums.ctypes.data, fired.ctypes.data)
         self.last_seconds = time.perf_counter() - t0   # the C loop only (bench cpu_baseline)
+        return status[:n], sums[:n], fired[:n]
+
+    def add_batch(self, b, threads: int = 1):
+        """orc_flow_add_votes_soa over a txflow_amd.VoteBatch-shaped object (the txv_votes SoA
+        layout): Verify on `threads` threads, then the sequential loop.  Returns
+        (status, sum_after, fired)."""
+        np = self._np
+        n = b.n
+        soa = _soa(b)
+        status = np.zeros(max(n, 1), np.uint8)
+        sums = np.zeros(max(n, 1), np.int64)
+        fired = np.zeros(max(n, 1), np.uint8)
+        lib().orc_flow_add_votes_soa(self._h, ctypes.addressof(soa), threads, status.ctypes.data,
+                                     sums.ctypes.data, fired.ctypes.data)
         return status[:n], sums[:n], fired[:n]
 
     def query(self, txhash: bytes):

@@ -14,6 +14,7 @@
  * Height and TxKey are never checked by the code.
  */
 #include "oracle.h"
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -203,37 +204,124 @@ static int sig_equal(const acc_sig* a, const uint8_t* sig, uint32_t len) {
   return memcmp(a->sig, sig, len) == 0;
 }
 
+/* One vote through TxFlow.addVote.  code >= 0: the Verify outcome is supplied (ORC_ADDED,
+ * ORC_ERR_INVALID_SIGNATURE or ORC_ERR_SIGNBYTES); code < 0: verify here when reached. */
+static uint8_t flow_add_one(orc_flow* f, const orc_vote* v, int code, int64_t* sum_after, uint8_t* fired) {
+  if (fired) *fired = 0;
+  if (v->is_nil) { if (sum_after) *sum_after = 0; return ORC_ERR_NIL; }
+  uint32_t s = get_or_create_set(f, v->txhash, v->txhash_len);
+  uint8_t st;
+  int64_t vi = -1;
+  if (v->addr_len == 0) st = ORC_ERR_EMPTY_ADDR;
+  else if ((vi = val_by_addr(f, v->addr, v->addr_len)) < 0) st = ORC_ERR_UNKNOWN_VALIDATOR;
+  else {
+    uint64_t key = ((uint64_t)(s + 1) << 32) | (uint64_t)vi;
+    acc_sig* ex = acc_find(f, key);
+    if (ex) st = sig_equal(ex, v->sig, v->sig_len) ? ORC_DUPLICATE : ORC_ERR_NONDETERMINISTIC;
+    else {
+      int ok = code;
+      if (ok < 0) { ok = orc_txvote_verify(v, f->chain, f->chain_len, f->pubs + 32 * vi); f->n_verifies++; }
+      if (ok == ORC_ADDED) {
+        acc_insert(f, key, v->sig, v->sig_len);
+        f->set_sum[s] += f->powers[vi];
+        if (f->quorum <= f->set_sum[s]) f->set_maj23[s] = 1;
+        st = ORC_ADDED;
+        if (fired && f->set_maj23[s]) *fired = 1;
+      } else st = (uint8_t)ok;
+    }
+  }
+  if (sum_after) *sum_after = f->set_sum[s];
+  return st;
+}
+
 void orc_flow_add_votes(orc_flow* f, const orc_vote* votes, uint32_t n, const uint8_t* verdicts,
                         uint8_t* status, int64_t* sum_after, uint8_t* fired) {
   for (uint32_t i = 0; i < n; ++i) {
-    const orc_vote* v = &votes[i];
-    if (fired) fired[i] = 0;
-    if (v->is_nil) { status[i] = ORC_ERR_NIL; if (sum_after) sum_after[i] = 0; continue; }
-    uint32_t s = get_or_create_set(f, v->txhash, v->txhash_len);
-    uint8_t st;
-    int64_t vi = -1;
-    if (v->addr_len == 0) st = ORC_ERR_EMPTY_ADDR;
-    else if ((vi = val_by_addr(f, v->addr, v->addr_len)) < 0) st = ORC_ERR_UNKNOWN_VALIDATOR;
-    else {
-      uint64_t key = ((uint64_t)(s + 1) << 32) | (uint64_t)vi;
-      acc_sig* ex = acc_find(f, key);
-      if (ex) st = sig_equal(ex, v->sig, v->sig_len) ? ORC_DUPLICATE : ORC_ERR_NONDETERMINISTIC;
-      else {
-        int ok;
-        if (verdicts) ok = verdicts[i] ? ORC_ADDED : ORC_ERR_INVALID_SIGNATURE;
-        else { ok = orc_txvote_verify(v, f->chain, f->chain_len, f->pubs + 32 * vi); f->n_verifies++; }
-        if (ok == ORC_ADDED) {
-          acc_insert(f, key, v->sig, v->sig_len);
-          f->set_sum[s] += f->powers[vi];
-          if (f->quorum <= f->set_sum[s]) f->set_maj23[s] = 1;
-          st = ORC_ADDED;
-          if (fired && f->set_maj23[s]) fired[i] = 1;
-        } else st = (uint8_t)ok;
-      }
-    }
-    status[i] = st;
-    if (sum_after) sum_after[i] = f->set_sum[s];
+    int code = verdicts ? (verdicts[i] ? ORC_ADDED : ORC_ERR_INVALID_SIGNATURE) : -1;
+    status[i] = flow_add_one(f, &votes[i], code, sum_after ? sum_after + i : 0, fired ? fired + i : 0);
   }
+}
+
+/* ---- SoA batches (the txv_votes layout): verify in parallel, then the sequential loop ---- */
+typedef struct {
+  const orc_flow* f;
+  const orc_soa* b;
+  uint8_t* code;
+  uint32_t begin, end;
+} soa_job;
+
+static orc_vote soa_vote(const orc_soa* b, uint32_t i) {
+  orc_vote v;
+  v.is_nil = b->is_nil ? b->is_nil[i] : 0;
+  v.height = b->height[i];
+  v.txhash = b->txhash + b->txhash_off[i]; v.txhash_len = b->txhash_len[i];
+  v.ts_sec = b->ts_sec[i]; v.ts_nanos = b->ts_nanos[i];
+  v.addr = b->addr + 20 * (size_t)i; v.addr_len = b->addr_len[i];
+  v.sig = b->sig + 64 * (size_t)i; v.sig_len = b->sig_len[i];
+  return v;
+}
+
+static void* soa_verify(void* p) {
+  soa_job* j = (soa_job*)p;
+  for (uint32_t i = j->begin; i < j->end; ++i) {
+    orc_vote v = soa_vote(j->b, i);
+    int64_t vi = v.is_nil ? -1 : val_by_addr(j->f, v.addr, v.addr_len);
+    /* votes that cannot reach Verify keep 0xFF; the sequential pass never reads their code */
+    j->code[i] = vi < 0 ? 0xFF : (uint8_t)orc_txvote_verify(&v, j->f->chain, j->f->chain_len, j->f->pubs + 32 * vi);
+  }
+  return 0;
+}
+
+void orc_flow_add_votes_soa(orc_flow* f, const orc_soa* b, int threads, uint8_t* status, int64_t* sum_after,
+                            uint8_t* fired) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  uint8_t* code = (uint8_t*)malloc(b->n ? b->n : 1);
+  soa_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (soa_job){f, b, code, (uint32_t)((uint64_t)b->n * t / threads), (uint32_t)((uint64_t)b->n * (t + 1) / threads)};
+    if (threads == 1) soa_verify(&jobs[0]);
+    else pthread_create(&th[t], 0, soa_verify, &jobs[t]);
+  }
+  if (threads > 1) for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  for (uint32_t i = 0; i < b->n; ++i) {
+    orc_vote v = soa_vote(b, i);
+    status[i] = flow_add_one(f, &v, code[i] == 0xFF ? -1 : code[i], sum_after ? sum_after + i : 0, fired ? fired + i : 0);
+  }
+  free(code);
+}
+
+typedef struct {
+  const orc_soa* b;
+  const uint8_t* pubs;
+  const uint8_t* chain; size_t chain_len;
+  uint8_t* out;
+  uint32_t begin, end;
+} verify_job;
+
+static void* soa_txvote_verify(void* p) {
+  verify_job* j = (verify_job*)p;
+  for (uint32_t i = j->begin; i < j->end; ++i) {
+    orc_vote v = soa_vote(j->b, i);
+    j->out[i] = v.is_nil ? ORC_ERR_NIL : (uint8_t)orc_txvote_verify(&v, j->chain, j->chain_len, j->pubs + 32 * (size_t)i);
+  }
+  return 0;
+}
+
+void orc_txvote_verify_soa(const orc_soa* b, const uint8_t* pubs32, const uint8_t* chain_id, size_t chain_len,
+                           int threads, uint8_t* out) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  verify_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (verify_job){b, pubs32, chain_id, chain_len, out, (uint32_t)((uint64_t)b->n * t / threads),
+                           (uint32_t)((uint64_t)b->n * (t + 1) / threads)};
+    if (threads == 1) soa_txvote_verify(&jobs[0]);
+    else pthread_create(&th[t], 0, soa_txvote_verify, &jobs[t]);
+  }
+  if (threads > 1) for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
 }
 
 int orc_flow_query(orc_flow* f, const uint8_t* txhash, uint32_t len, int64_t* sum, int32_t* maj23) {

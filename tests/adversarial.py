@@ -1,0 +1,369 @@
+"""C4 adversarial TxVote stream and its bit-exact gate.
+
+TEST INFRASTRUCTURE: builds the adversarial batches (using the product's device signer for the
+honest votes and tests/golden/ed_math.py + the oracle to forge signatures for crafted keys),
+runs each batch through libtxvote.so (txv_add_votes, the TxFlow.addVote/TxVoteSet.AddVote
+boundary) and through the sequential CPU oracle (oracle/txflow.c, TxVote.Verify on host
+threads), and compares every per-vote (added, err) code, every commit-fire bit, every commit
+event and, at the end of each epoch, every TxVoteSet's (sum, maj23).  The direct
+TxVote.Verify path (types/tx_vote.go:110-119, caller-supplied key, address mismatch) is
+checked on a slice of every batch through txv_verify_batch.
+
+Mix per batch (fractions of all votes; Appendix C): 10% bad = R bit-flip 2%, S bit-flip 2%,
+signed field changed after signing 2% (Height, Timestamp or TxHash), s+L 1%, s top-3 bits 0.5%,
+sig length != 64 0.5%, unknown validator 0.5%, empty address 0.25%, nil 0.1%; crafted-key votes 2%
+(of which non-canonical R encodings of the identity 0.5%); 5% exact replays and 5% conflicting
+re-signed votes (same validator + tx, new timestamp), sourced from this batch or the previous one
+(cross-batch state).  Crafted validators: identity (canonical, y+p, x=0 with sign bit), order 2,
+order 4 (both roots, y+p encoding), order 8, mixed-order A+T4 / A+T8, and an undecodable key.
+Forgeries: R = [r]B, s = r + k*a (a = 0 for pure torsion keys), valid exactly when [k]T = 0.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+for p in (HERE, os.path.join(HERE, "golden"), os.path.join(os.path.dirname(HERE), "oracle"),
+          os.path.join(os.path.dirname(HERE), "go-txflow_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import ed_math as E  # noqa: E402
+
+CHAIN = "test_chain_id"
+N_HONEST = 100
+
+
+def _expand(seed: bytes):
+    h = hashlib.sha512(seed).digest()
+    a = int.from_bytes(h[:32], "little")
+    a &= (1 << 254) - 8
+    a |= 1 << 254
+    return a
+
+
+def crafted_keys():
+    """[(name, pub bytes, secret a of the prime-order part)] -- see the module docstring."""
+    tors = E.torsion_points()
+    t2 = next(t for t in tors if E.order(t) == 2)
+    t4 = next(t for t in tors if E.order(t) == 4)
+    t4b = next(t for t in tors if E.order(t) == 4 and t != t4)
+    t8 = next(t for t in tors if E.order(t) == 8)
+    keys = [("identity", E.encode((0, 1)), 0),
+            ("identity_y+p", E.encode_raw(1 + E.P, 0), 0),
+            ("identity_negzero", E.encode_raw(1, 1), 0),
+            ("order2", E.encode(t2), 0),
+            ("order4", E.encode(t4), 0),
+            ("order4_other", E.encode(t4b), 0),
+            ("order4_y+p", E.encode_raw(t4[1] + E.P, t4[0] & 1), 0) if t4[1] + E.P < 2 ** 255 else None,
+            ("order8", E.encode(t8), 0)]
+    for name, t, s in (("mixed4", t4, b"c4-mixed4"), ("mixed8", t8, b"c4-mixed8")):
+        a = _expand(hashlib.sha256(s).digest())
+        keys.append((name, E.encode(E.add(E.mul(a, E.B), t)), a))
+    y = 2
+    while E.recover_x(y, 0) is not None:
+        y += 1
+    keys.append(("undecodable", E.encode_raw(y, 0), None))
+    return [k for k in keys if k is not None]
+
+
+class C4Stream:
+    """Deterministic C4 stream.  One epoch = a fresh TxFlow (txv_reset_flow + a new oracle Flow)
+    over `epoch_txs` transactions; each epoch is `batches_per_epoch` batches of `batch` votes."""
+
+    def __init__(self, ctx, seed: int = 0x7478763034, batch: int = 1 << 20, batches_per_epoch: int = 4,
+                 oracle_threads: int = 16, verify_slice: int = 4096):
+        import oracle as O
+        from txflow_amd.workload import validator_seeds
+        self.ctx, self.O = ctx, O
+        self.rng = np.random.default_rng(seed)
+        self.batch, self.bpe = batch, batches_per_epoch
+        self.threads = oracle_threads
+        self.verify_slice = verify_slice
+        self.seeds = validator_seeds(N_HONEST)
+        honest = ctx.keygen(self.seeds)
+        self.crafted = crafted_keys()
+        self.pubs = honest + [k[1] for k in self.crafted]
+        self.n_vals = len(self.pubs)
+        self.powers = np.ones(self.n_vals, np.int64)
+        ctx.set_validators(self.pubs, self.powers, CHAIN)
+        addrs, ok = ctx.validator_info()
+        self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(self.n_vals, 20)
+        exp_ok = [O.decode_ok(p) for p in self.pubs]
+        assert list(ok.astype(bool)) == exp_ok, "validator decode flags differ from the oracle"
+        # forgery pool: (r, [r]B)
+        self.pool_r = [int(x) for x in self.rng.integers(1, 2 ** 62, size=256)]
+        self.pool_R = [O.scalarmult_base(r.to_bytes(32, "little")) for r in self.pool_r]
+        # epoch size: every honest validator votes every tx once as a base vote
+        base_frac = 1.0 - 0.05 - 0.05 - 0.02 - 0.005 - 0.0025 - 0.001
+        self.epoch_txs = max(1, int(batch * batches_per_epoch * base_frac) // N_HONEST)
+        self.epoch = -1
+        self.stats = dict(votes=0, batches=0, epochs=0, mismatches=0, verify_checked=0, events=0,
+                          txs_checked=0, by_status={})
+
+    # ---------------------------------------------------------------- epoch state
+    def _new_epoch(self):
+        O = self.O
+        self.epoch += 1
+        self.ctx.reset_flow()
+        self.flow = O.Flow(self.pubs, self.powers, CHAIN.encode())
+        first = (self.epoch + 1) << 32
+        from txflow_amd.workload import tx_hashes
+        self.hashes = tx_hashes(self.epoch_txs, self.rng, first)          # [T, 64] u8
+        pairs = np.arange(self.epoch_txs * N_HONEST, dtype=np.int64)
+        self.pairs = self.rng.permutation(pairs)                          # (tx, val) = divmod(pair, 100)
+        self.pair_pos = 0
+        self.prev = None
+        self.nanos = 1
+        self.committed = set()
+        self.stats["epochs"] += 1
+
+    # ---------------------------------------------------------------- batch construction
+    def _forge(self, vi: int, msg: bytes, pick: int):
+        """forged (R || s) for crafted validator vi (index into self.crafted)"""
+        name, pub, a = self.crafted[vi]
+        r, R = self.pool_r[pick], self.pool_R[pick]
+        k = int.from_bytes(hashlib.sha512(R + pub + msg).digest(), "little") % E.L
+        s = (r + k * (a or 0)) % E.L
+        return R + s.to_bytes(32, "little")
+
+    def next_batch(self):
+        if self.epoch < 0 or (self.stats["batches"] % self.bpe) == 0:
+            self._new_epoch()
+        import txflow_amd as T
+        rng, n = self.rng, self.batch
+        n_rep, n_conf = int(n * 0.05), int(n * 0.05)
+        n_craft, n_nc = int(n * 0.015), int(n * 0.005)
+        n_unknown, n_empty, n_nil = int(n * 0.005), int(n * 0.0025), int(n * 0.001)
+        n_base = n - n_rep - n_conf - n_craft - n_nc - n_unknown - n_empty - n_nil
+        n_base = min(n_base, len(self.pairs) - self.pair_pos)
+        n_prim = n_base + n_craft + n_nc + n_unknown + n_empty + n_nil
+        # primary votes: base (honest pairs), crafted, non-canonical-R identity, unknown, empty, nil
+        tx = np.empty(n_prim, np.int64)
+        val = np.empty(n_prim, np.int64)
+        pr = self.pairs[self.pair_pos:self.pair_pos + n_base]
+        self.pair_pos += n_base
+        tx[:n_base], val[:n_base] = pr // N_HONEST, pr % N_HONEST
+        o = n_base
+        tx[o:] = rng.integers(0, self.epoch_txs, n_prim - o)
+        n_cr = len(self.crafted)
+        val[o:o + n_craft] = N_HONEST + rng.integers(0, n_cr, n_craft)
+        o += n_craft
+        id_keys = [N_HONEST + i for i, k in enumerate(self.crafted) if k[0].startswith("identity")]
+        val[o:o + n_nc] = rng.choice(id_keys, n_nc)
+        o += n_nc
+        val[o:] = -1                     # unknown / empty / nil: no validator
+        kind = np.zeros(n_prim, np.int8)  # 0 base 1 crafted 2 noncanon-R 3 unknown 4 empty 5 nil
+        kind[n_base:n_base + n_craft] = 1
+        kind[n_base + n_craft:n_base + n_craft + n_nc] = 2
+        o = n_base + n_craft + n_nc
+        kind[o:o + n_unknown] = 3
+        kind[o + n_unknown:o + n_unknown + n_empty] = 4
+        kind[o + n_unknown + n_empty:] = 5
+        perm = rng.permutation(n_prim)
+        tx, val, kind = tx[perm], val[perm], kind[perm]
+
+        # conflict and replay sources: 70% this batch's primaries, 30% the previous batch
+        def sources(m):
+            from_prev = (rng.random(m) < 0.3) if self.prev is not None else np.zeros(m, bool)
+            j = rng.integers(0, n_prim, m)
+            if self.prev is not None:
+                j[from_prev] = rng.integers(0, self.prev["n"], int(from_prev.sum()))
+            return from_prev, j
+
+        c_prev, c_j = sources(n_conf)
+        r_prev, r_j = sources(n_rep)
+
+        n_all = n_prim + n_conf + n_rep
+        f = dict(tx=np.zeros(n_all, np.int64), val=np.zeros(n_all, np.int64), kind=np.zeros(n_all, np.int8),
+                 height=np.ones(n_all, np.int64), ts_nanos=np.zeros(n_all, np.int32),
+                 addr=np.zeros((n_all, 20), np.uint8), addr_len=np.full(n_all, 20, np.uint32),
+                 sig=np.zeros((n_all, 64), np.uint8), sig_len=np.full(n_all, 64, np.uint32),
+                 is_nil=np.zeros(n_all, np.uint8), txoff=np.zeros(n_all, np.uint32))
+        f["tx"][:n_prim], f["val"][:n_prim], f["kind"][:n_prim] = tx, val, kind
+        nanos = self.nanos + np.arange(n_all, dtype=np.int64)
+        self.nanos += n_all
+        f["ts_nanos"][:] = (nanos % 999_999_999 + 1).astype(np.int32)
+        known = f["val"][:n_prim] >= 0
+        f["addr"][:n_prim][known] = self.addrs[f["val"][:n_prim][known]]
+        f["addr"][:n_prim][kind == 3] = rng.integers(0, 256, (int((kind == 3).sum()), 20), dtype=np.uint8)
+        f["addr_len"][:n_prim][kind == 4] = 0
+        f["is_nil"][:n_prim][kind == 5] = 1
+        f["txoff"][:n_prim] = (f["tx"][:n_prim] * 64).astype(np.uint32)
+
+        # conflicts: same validator + tx as the source, new timestamp, fresh valid signature
+        def src_field(key, from_prev, j):
+            out = f[key][:n_prim][np.where(from_prev, 0, j)]
+            if from_prev.any():
+                out[from_prev] = self.prev[key][j[from_prev]]
+            return out
+
+        cs = slice(n_prim, n_prim + n_conf)
+        for key in ("tx", "val", "kind", "addr", "addr_len", "is_nil", "txoff"):
+            f[key][cs] = src_field(key, c_prev, c_j)
+        # conflicts on unknown / empty / nil sources stay what they are (no key to sign with)
+
+        hashes_arena = self.hashes.reshape(-1)   # previous-batch sources share it (same epoch)
+
+        # device signing of base + conflict votes by honest validators
+        honest = np.zeros(n_all, bool)
+        honest[:n_prim] = f["kind"][:n_prim] == 0
+        honest[cs] = (f["kind"][cs] == 0) & (f["val"][cs] >= 0) & (f["val"][cs] < N_HONEST)
+        hi = np.nonzero(honest)[0]
+        sub = T.VoteBatch(len(hi), height=f["height"][hi], txhash_arena=hashes_arena, txhash_off=f["txoff"][hi],
+                          txhash_len=np.full(len(hi), 64, np.uint32), ts_sec=np.full(len(hi), 1_700_000_000, np.int64),
+                          ts_nanos=f["ts_nanos"][hi], addr=f["addr"][hi], addr_len=f["addr_len"][hi],
+                          sig=np.zeros((len(hi), 64), np.uint8), sig_len=np.full(len(hi), 64, np.uint32))
+        f["sig"][hi] = self.ctx.sign_votes(sub, f["val"][hi].astype(np.uint32), CHAIN)
+
+        # crafted-key votes (primaries and conflicts): forged
+        ci = np.nonzero(((f["kind"] == 1) | (f["kind"] == 2)) & (np.arange(n_all) < n_prim + n_conf))[0]
+        picks = rng.integers(0, len(self.pool_r), len(ci))
+        nc_form = rng.integers(0, 3, len(ci))
+        for q, i in enumerate(ci):
+            vi = int(f["val"][i]) - N_HONEST
+            if f["kind"][i] == 2:
+                # identity key, r = 0: R = identity (canonical / x=0 with sign bit / y+p), s = 0
+                R = (E.encode((0, 1)), E.encode_raw(1, 1), E.encode_raw(1 + E.P, 0))[nc_form[q]]
+                f["sig"][i] = np.frombuffer(R + bytes(32), np.uint8)
+                continue
+            msg = T.sign_bytes(int(f["height"][i]), self.hashes[f["tx"][i]].tobytes(), 1_700_000_000,
+                               int(f["ts_nanos"][i]), CHAIN)
+            f["sig"][i] = np.frombuffer(self._forge(vi, msg, int(picks[q])), np.uint8)
+        # unknown-validator primaries carry some honest signature bytes
+        uk = np.nonzero(f["kind"][:n_prim] == 3)[0]
+        if len(hi):
+            f["sig"][uk] = f["sig"][hi[rng.integers(0, len(hi), len(uk))]]
+
+        # mutations of base primaries (after signing)
+        base_idx = np.nonzero(f["kind"][:n_prim] == 0)[0]
+        mut = rng.permutation(base_idx)
+        cuts = np.cumsum([int(n * x) for x in (0.02, 0.02, 0.02, 0.01, 0.005, 0.005)])
+        g_r, g_s, g_field, g_sl, g_top, g_len = np.split(mut[:cuts[-1]], cuts[:-1])
+        bits = rng.integers(0, 256, len(g_r))
+        f["sig"][g_r, bits // 8] ^= (1 << (bits % 8)).astype(np.uint8)
+        bits = rng.integers(0, 256, len(g_s))
+        f["sig"][g_s, 32 + bits // 8] ^= (1 << (bits % 8)).astype(np.uint8)
+        which = rng.integers(0, 3, len(g_field))
+        f["height"][g_field[which == 0]] += 1
+        f["ts_nanos"][g_field[which == 1]] = (f["ts_nanos"][g_field[which == 1]] % 999_999_998) + 2
+        tx_new = rng.integers(0, self.epoch_txs, int((which == 2).sum()))
+        f["tx"][g_field[which == 2]] = tx_new
+        f["txoff"][g_field[which == 2]] = (tx_new * 64).astype(np.uint32)
+        for i in g_sl:       # s + L (< 2^254, so only ScMinimal or the top-bit check can reject it)
+            s = int.from_bytes(f["sig"][i, 32:].tobytes(), "little") + E.L
+            f["sig"][i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        f["sig"][g_top, 63] |= (np.uint8(0x20) << rng.integers(0, 3, len(g_top)).astype(np.uint8))
+        f["sig_len"][g_len] = rng.choice(np.array([0, 63, 65], np.uint32), len(g_len))
+
+        # exact replays of final (post-mutation) votes
+        rs = slice(n_prim + n_conf, n_all)
+        for key in ("tx", "val", "kind", "height", "ts_nanos", "addr", "addr_len", "sig", "sig_len", "is_nil", "txoff"):
+            f[key][rs] = src_field(key, r_prev, r_j)
+
+        # arrival order: a derived vote comes after its source when the source is in this batch
+        sort_key = np.empty(n_all)
+        sort_key[:n_prim] = np.arange(n_prim)
+        for sl_, from_prev, j in ((cs, c_prev, c_j), (rs, r_prev, r_j)):
+            u = rng.random(len(j))
+            k = j + 0.5 + u * (n_prim - j)
+            k[from_prev] = u[from_prev] * n_prim
+            sort_key[sl_] = k
+        order = np.argsort(sort_key, kind="stable")
+        for key in f:
+            f[key] = f[key][order]
+        f["n"] = n_all
+        self.prev = f
+        batch = T.VoteBatch(n_all, height=f["height"], txhash_arena=hashes_arena, txhash_off=f["txoff"],
+                            txhash_len=np.full(n_all, 64, np.uint32),
+                            ts_sec=np.full(n_all, 1_700_000_000, np.int64), ts_nanos=f["ts_nanos"],
+                            addr=f["addr"], addr_len=f["addr_len"], sig=f["sig"], sig_len=f["sig_len"],
+                            is_nil=f["is_nil"])
+        return batch, f
+
+    # ---------------------------------------------------------------- the gate
+    def run_batch(self):
+        import txflow_amd as T
+        O = self.O
+        batch, f = self.next_batch()
+        st, ev = self.ctx.add_votes(batch, ev_cap=batch.n)
+        ost, osum, ofired = self.flow.add_batch(batch, self.threads)
+        exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+        bad = np.nonzero(st != exp)[0]
+        # commit events: one per tx whose 2/3 crossing happened in this batch, at the crossing vote
+        fired_first = []
+        seen = set()
+        for i in np.nonzero(ofired)[0]:
+            h = batch.txhash(int(i))
+            if h in self.committed:
+                continue
+            if h not in seen:
+                seen.add(h)
+                fired_first.append(int(i))
+        self.committed.update(seen)
+        ev_idx = sorted(int(e["vote_index"]) for e in ev)
+        ev_ok = ev_idx == sorted(fired_first)
+        # direct TxVote.Verify on a slice with caller-supplied keys (1 in 8 of them wrong)
+        m = min(self.verify_slice, batch.n)
+        vmis = 0
+        if m:
+            sl = np.arange(m)
+            vals = np.where(f["val"][:m] >= 0, f["val"][:m], 0)
+            wrong = self.rng.random(m) < 0.125
+            vals = np.where(wrong, (vals + 1) % self.n_vals, vals)
+            pubs = np.frombuffer(b"".join(self.pubs), np.uint8).reshape(-1, 32)[vals]
+            sub = T.VoteBatch(m, height=f["height"][sl], txhash_arena=batch.txhash_arena, txhash_off=f["txoff"][sl],
+                              txhash_len=np.full(m, 64, np.uint32), ts_sec=np.full(m, 1_700_000_000, np.int64),
+                              ts_nanos=f["ts_nanos"][sl], addr=f["addr"][sl], addr_len=f["addr_len"][sl],
+                              sig=f["sig"][sl], sig_len=f["sig_len"][sl], is_nil=f["is_nil"][sl])
+            vst = self.ctx.verify_batch(sub, pubs)
+            ovst = O.txvote_verify_batch(sub, pubs, CHAIN.encode(), self.threads)
+            vmis = int(np.count_nonzero(vst != ovst))
+            self.stats["verify_checked"] += m
+        self.stats["votes"] += batch.n
+        self.stats["batches"] += 1
+        self.stats["events"] += len(ev)
+        for code, cnt in zip(*np.unique(exp & 0x7F, return_counts=True)):
+            nm = T.STATUS_NAMES.get(int(code), str(code))
+            self.stats["by_status"][nm] = self.stats["by_status"].get(nm, 0) + int(cnt)
+        mism = len(bad) + (0 if ev_ok else 1) + vmis
+        # end of epoch: every TxVoteSet's (sum, maj23)
+        if self.stats["batches"] % self.bpe == 0:
+            mism += self.check_sets()
+        self.stats["mismatches"] += mism
+        return dict(n=batch.n, status_mismatches=len(bad), events_ok=ev_ok, verify_mismatches=vmis,
+                    first_bad=[(int(i), int(st[i]), int(exp[i])) for i in bad[:5]])
+
+    def check_sets(self):
+        bad = 0
+        for j in range(self.epoch_txs):
+            h = self.hashes[j].tobytes()
+            g = self.ctx.query_tx(h)
+            o = self.flow.query(h)
+            if (g if g is None else (int(g[0]), bool(g[1]))) != o:
+                bad += 1
+        self.stats["txs_checked"] += self.epoch_txs
+        return bad
+
+
+
+def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int = 4, threads: int = 16,
+             log=print, seed: int = 0x7478763034):
+    """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0)."""
+    s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads)
+    t0 = time.time()
+    while s.stats["votes"] < total_votes:
+        r = s.run_batch()
+        log(f"[c4] batch {s.stats['batches']} epoch {s.epoch}: {r['n']} votes, status mismatches "
+            f"{r['status_mismatches']}, events ok {r['events_ok']}, verify mismatches {r['verify_mismatches']}; "
+            f"total {s.stats['votes']} votes, {s.stats['mismatches']} mismatches, {time.time() - t0:.0f}s"
+            + (f" first_bad={r['first_bad']}" if r["first_bad"] else ""))
+    if s.stats["batches"] % s.bpe:
+        s.stats["mismatches"] += s.check_sets()
+    s.stats["seconds"] = round(time.time() - t0, 1)
+    return s.stats

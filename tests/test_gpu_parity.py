@@ -308,3 +308,20 @@ def test_golden_vectors_verify_bytes(gpu_ctx):
     bad = [(c[4], bool(g)) for c, g in zip(cases, got) if bool(g) != c[3]]
     assert not bad, bad[:10]
     assert sum(c[3] for c in cases) > 60 and sum(not c[3] for c in cases) > 100
+
+
+def test_c4_adversarial_stream_gate(oracle_lib):
+    """C4 at test size: 3 batches x 64k adversarial votes across two
+    TxFlow epochs -- bad signatures of every kind, crafted torsion / mixed-order / non-canonical
+    keys with forged signatures, replays and conflicts across batches -- every per-vote status,
+    fire bit, commit event, direct-Verify verdict and per-tx (sum, maj23) equal to the oracle's.
+    The 10^8-vote run of the same stream is tools/gate/c4_gate.py."""
+    import adversarial as A
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 17, max_txs=1 << 14, max_validators=256)
+    try:
+        st = A.run_gate(ctx, 3 * 65536, batch=65536, batches_per_epoch=2, threads=8, log=lambda s: None)
+        assert st["mismatches"] == 0, st
+        assert st["by_status"].get("ErrVoteInvalidSignature", 0) > 0 and st["events"] > 0
+    finally:
+        ctx.close()

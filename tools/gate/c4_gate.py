@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""C4 bit-exact gate (BASELINE.json config 4): stream N adversarial TxVotes
+through libtxvote.so on cuda:0 and through the sequential CPU oracle; every per-vote status,
+commit-fire bit, commit event, direct-Verify verdict (slice) and per-tx (sum, maj23) must agree.
+
+    python tools/gate/c4_gate.py --votes 100000000 --out gpurun_out/c4/gate.json
+
+Prints one progress line per batch; writes the final stats as JSON."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "go-txflow_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--votes", type=int, default=10_000_000)
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--batches-per-epoch", type=int, default=4)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    import oracle
+    oracle.build()
+    import txflow_amd as T
+    import adversarial as A
+    ctx = T.Context(device=0, max_batch=args.batch + args.batch // 4, max_txs=1 << 17, max_validators=256)
+    t0 = time.time()
+    st = A.run_gate(ctx, args.votes, batch=args.batch, batches_per_epoch=args.batches_per_epoch,
+                    threads=args.threads, log=lambda s: print(s, flush=True))
+    st.update(device=ctx.device_name(), table_window=ctx.table_w, base_window=ctx.base_w,
+              validators=len(A.crafted_keys()) + A.N_HONEST, wall_s=round(time.time() - t0, 1),
+              oracle_threads=args.threads, batch=args.batch, batches_per_epoch=args.batches_per_epoch)
+    print(json.dumps(st), flush=True)
+    if args.out:
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+        with open(args.out, "w") as f:
+            json.dump(st, f, indent=1)
+    ctx.close()
+    sys.exit(0 if st["mismatches"] == 0 else 1)
+
+
+if __name__ == "__main__":
+    main()
