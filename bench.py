@@ -71,6 +71,46 @@ def cpu_baseline(wl, threads: int, serial_votes: int, parallel_votes: int):
                 serial_value=round(serial_rate, 1), serial_cores=1)
 
 
+def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
+    """C5: 1000 weighted validators, the stream cut into `batch`-vote batches fed
+    through txv_add_votes (host amino + routing + pack, H2D, verify + tally kernels, statuses and
+    commit events back).  Latency-to-commit of a tx = return of the call that reported its commit
+    event - submission of the batch holding its first vote."""
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals,
+                    max_accepted=n_txs * n_vals + 4 * batch)
+    wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch)
+    for b in wl.batches[:2]:
+        ctx.add_votes(b, ev_cap=b.n)
+    ctx.reset_flow()
+    submit, done, commit_t, added = [], [], {}, 0
+    t0 = time.perf_counter()
+    for k, b in enumerate(wl.batches):
+        ts = time.perf_counter()
+        st, ev = ctx.add_votes(b, ev_cap=b.n)
+        te = time.perf_counter()
+        submit.append(ts)
+        done.append(te)
+        added += int(np.count_nonzero((st & 0x7F) == T.ADDED))
+        for e in ev:
+            tx = int(wl.tx_of[k * batch + int(e["vote_index"])])
+            assert tx not in commit_t, "tx committed twice"
+            commit_t[tx] = te
+    total = time.perf_counter() - t0
+    ok = added == wl.n and len(commit_t) == wl.n_txs
+    lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
+    bl = (np.array(done) - np.array(submit)) * 1e3
+    out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n} votes in {batch}-vote batches "
+                       f"through txv_add_votes", "correct": ok, "votes_per_s": round(wl.n / total, 1),
+           "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
+           "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
+           "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
+           "table_window": ctx.table_w, "base_window": ctx.base_w}
+    ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,6 +126,8 @@ def main():
                     help="base-point table window (0 = library default)")
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
+    ap.add_argument("--c5-txs", type=int, default=2048)
     ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
     args = ap.parse_args()
@@ -248,6 +290,9 @@ def main():
                          "tally_GBps": round(wl.n * TALLY_BYTES_PER_VOTE / (t_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,
         }
+        if world == 1 and not args.no_c5:
+            ctx.close()
+            out["c5_streaming"] = c5_streaming(local, 1000, args.c5_txs, 65536)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

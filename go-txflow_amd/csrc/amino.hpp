@@ -42,6 +42,19 @@ inline int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
   return (int)n;
 }
 
+// SignBytes length (or -1 when amino rejects the time), without encoding
+inline int sign_bytes_len(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t chain_len) {
+  const int tl = time_body(nullptr, sec, nanos);
+  if (tl < 0) return -1;
+  uint64_t body = 0;
+  if (height != 0) body += 9;
+  if (txhash_len) body += 1 + put_uvarint(nullptr, txhash_len) + txhash_len;
+  body += 34;
+  if (tl > 0) body += 1 + put_uvarint(nullptr, (uint64_t)tl) + (uint64_t)tl;
+  if (chain_len) body += 1 + put_uvarint(nullptr, chain_len) + chain_len;
+  return (int)(put_uvarint(nullptr, body) + body);
+}
+
 // Writes SignBytes into out (capacity cap).  Returns length, or -1 (amino error / too long).
 inline int sign_bytes(uint8_t* out, uint32_t cap, int64_t height, const uint8_t* txhash, uint32_t txhash_len,
                       int64_t sec, int32_t nanos, const uint8_t* chain, uint32_t chain_len) {

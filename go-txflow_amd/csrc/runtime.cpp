@@ -12,12 +12,17 @@
 #include "txv_device.h"
 #include "txv_tally.h"
 #include "amino.hpp"
+#include "host_pack.hpp"
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <random>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -50,8 +55,11 @@ struct Slot {
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
   uint32_t* h_val = nullptr; uint32_t* h_set = nullptr; uint8_t* h_flags = nullptr; uint8_t* h_status = nullptr;
   uint32_t* h_touched = nullptr; int64_t* h_tsum = nullptr; uint8_t* h_tmaj = nullptr; uint32_t* h_tcross = nullptr;
-  std::vector<uint8_t> tmp_msg;   // SignBytes arena
+  std::vector<uint8_t> tmp_msg;   // SignBytes arena (verify-only paths)
   std::vector<size_t> tmp_off;
+  std::vector<int> lens;           // AddVote pack: SignBytes length (-1 amino error, -2 nil)
+  std::vector<uint64_t> khash;     // AddVote pack: seeded hash of the TxHash bytes
+  std::vector<uint32_t> vidx;      // AddVote pack: validator index or UINT32_MAX
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -71,6 +79,7 @@ struct txv_ctx {
   int64_t total = 0, quorum = 0;
   std::string chain;
   std::unordered_map<std::string, uint32_t> addr_index;
+  txv_host::AddrTable addr_tab;    // same map, lock-free reads for the parallel pack
   uint32_t* d_pubs = nullptr; uint8_t* d_decode_ok = nullptr; uint32_t* d_atables = nullptr;
   uint32_t* d_addr = nullptr; int64_t* d_power = nullptr;
   uint32_t* d_btable = nullptr;    // B table for the verify window tab_w
@@ -91,8 +100,8 @@ struct txv_ctx {
   int tmp_w = 0;
   uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
   // tally state
-  std::unordered_map<std::string, uint32_t> tx_index;
-  std::vector<std::string> tx_keys;
+  txv_host::TxTable tx_tab{std::random_device{}() * 0x9e3779b97f4a7c15ULL + 0x7478};   // TxHash -> set id
+  std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
   std::vector<int64_t> h_sum;
   std::vector<uint8_t> h_maj;
   std::vector<uint32_t> seen_stage, set_tidx;   // per set: last staging that touched it, its index there
@@ -200,8 +209,7 @@ int reset_tally(txv_ctx* c, bool keep_ids = false) {
     std::fill(c->h_maj.begin(), c->h_maj.end(), 0);
     return TXV_OK;
   }
-  c->tx_index.clear();
-  c->tx_keys.clear();
+  c->tx_tab.clear();
   c->h_sum.clear();
   c->h_maj.clear();
   c->seen_stage.clear();
@@ -364,28 +372,44 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
   Slot& s = c->slots[slot];
-  std::vector<int> lens;
-  const uint32_t mx = encode_all(c, s, v, c->chain.data(), (uint32_t)c->chain.size(), lens);
-  const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
-  int r = ensure_slot(c, s, v->n, mw);
+  const uint32_t n = v->n;
+  const uint8_t* chain = (const uint8_t*)c->chain.data();
+  const uint32_t chain_len = (uint32_t)c->chain.size();
+  // phase A (parallel): SignBytes lengths, TxHash hashes, validator lookups
+  s.lens.resize(n); s.khash.resize(n); s.vidx.resize(n);
+  std::atomic<uint32_t> mx{0};
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    uint32_t m = 0;
+    for (uint32_t i = lo; i < hi; ++i) {
+      if (v->is_nil && v->is_nil[i]) { s.lens[i] = -2; continue; }
+      const int L = txv_host::sign_bytes_len(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], chain_len);
+      s.lens[i] = L;
+      if (L > 0 && (uint32_t)L > m) m = (uint32_t)L;
+      s.khash[i] = c->tx_tab.hash(v->txhash + v->txhash_off[i], v->txhash_len[i]);
+      s.vidx[i] = v->addr_len[i] == 20 ? c->addr_tab.find(v->addr + (size_t)i * 20) : UINT32_MAX;
+    }
+    uint32_t cur = mx.load();
+    while (m > cur && !mx.compare_exchange_weak(cur, m)) {}
+  });
+  const uint32_t mw = std::max<uint32_t>(1, (mx.load() + 7) / 8);
+  int r = ensure_slot(c, s, n, mw);
   if (r) return r;
-  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw;
-  // staging counter for touched-set de-duplication on the host
+  s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
+  // phase B (sequential, arrival order): TxHash -> set id, created on first sight
+  // (txflow/service.go:200-209, also for votes that then fail), touched-set list, the
+  // AddVote pre-checks (types/vote_set.go:92-105)
   const uint32_t stage_id = ++c->stage_count;
   s.n_touched = 0;
-  for (uint32_t i = 0; i < v->n; ++i) {
+  for (uint32_t i = 0; i < n; ++i) {
     s.h_flags[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0;
-    if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
-    std::string key((const char*)v->txhash + v->txhash_off[i], v->txhash_len[i]);
-    auto it = c->tx_index.find(key);
-    uint32_t sid;
-    if (it == c->tx_index.end()) {
-      sid = (uint32_t)c->tx_keys.size();
-      if (sid >= c->cfg.max_txs) { c->err = "TxVoteSets exceed max_txs"; return TXV_ECAPACITY; }
-      c->tx_index.emplace(key, sid);
-      c->tx_keys.push_back(std::move(key));
+    if (s.lens[i] == -2) { s.h_status[i] = TXV_ERR_NIL; continue; }
+    bool created;
+    const uint32_t sid = c->tx_tab.intern(v->txhash + v->txhash_off[i], v->txhash_len[i], s.khash[i], &created,
+                                          c->cfg.max_txs);
+    if (sid == UINT32_MAX) { c->err = "TxVoteSets exceed max_txs"; return TXV_ECAPACITY; }
+    if (created) {
       c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_stage.push_back(0); c->set_tidx.push_back(0);
-    } else sid = it->second;
+    }
     s.h_set[i] = sid;
     if (c->seen_stage[sid] != stage_id) {
       c->seen_stage[sid] = stage_id;
@@ -393,20 +417,40 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       s.h_touched[s.n_touched++] = sid;
     }
     if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
-    uint32_t vi = UINT32_MAX;
-    if (v->addr_len[i] == 20) {
-      auto a = c->addr_index.find(std::string((const char*)v->addr + (size_t)i * 20, 20));
-      if (a != c->addr_index.end()) vi = a->second;
-    }
+    const uint32_t vi = s.vidx[i];
     if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
     s.h_val[i] = vi;
     // a SignBytes failure is only reached after the accepted-vote check (AddVote order), so
     // the vote stays pending with BADMSG: it never verifies and the tally resolves it
     s.h_status[i] = 0xFF;
-    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
+    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
   }
+  // phase C (parallel): column-major SoA -- signature words, SignBytes as big-endian words
+  const uint32_t np = s.n_pad;
+  c->pool->parallel_for(np, [&](uint32_t lo, uint32_t hi) {
+    std::vector<uint8_t> buf((size_t)mw * 8 + 8);
+    for (uint32_t i = lo; i < hi; ++i) {
+      if (i >= n) {
+        for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = 0;
+        for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = 0;
+        s.h_msg_len[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0; s.h_flags[i] = 0; s.h_status[i] = TXV_ERR_NIL;
+        continue;
+      }
+      uint8_t sg[64];
+      const uint32_t sl = v->sig_len[i] > 64 ? 64 : v->sig_len[i];
+      memset(sg, 0, 64);
+      memcpy(sg, v->sig + (size_t)i * 64, sl);
+      for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = le32(sg + 4 * j);
+      const int L = s.lens[i];
+      s.h_msg_len[i] = L > 0 ? (uint32_t)L : 0;
+      std::fill(buf.begin(), buf.end(), 0);
+      if (L > 0)
+        txv_host::sign_bytes(buf.data(), (uint32_t)L, v->height[i], v->txhash + v->txhash_off[i], v->txhash_len[i],
+                             v->ts_sec[i], v->ts_nanos[i], chain, chain_len);
+      for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = be64(buf.data() + 8 * w);
+    }
+  }, 1024);
   build_order(s);
-  pack_columns(s, v, lens);
   if ((r = upload_slot(c, s)) || (r = build_set_order(c, s))) return r;
   s.staged = true; s.ran = false;
   return TXV_OK;
@@ -649,6 +693,12 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->n_cus = prop.multiProcessorCount;
   if (build_base_table(c, 4) != TXV_OK) { txv_destroy(c); return TXV_EDEVICE; }
+  {
+    // host pack threads: TXV_HOST_THREADS, else min(16, hardware threads)
+    unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("TXV_HOST_THREADS")) nt = (unsigned)std::max(1, std::min(256, atoi(e)));
+    c->pool.reset(new txv_host::WorkerPool(nt));
+  }
   *out = c;
   return TXV_OK;
 }
@@ -717,6 +767,7 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->addr_index.clear();
   for (uint32_t i = 0; i < n; ++i) c->addr_index.emplace(std::string((const char*)c->addrs.data() + 20 * i, 20), i);
+  c->addr_tab.build(c->addrs.data(), n);
   if ((r = alloc_tally(c))) return r;
   return reset_tally(c);
 }
@@ -839,14 +890,15 @@ int txv_add_votes(txv_ctx* c, const txv_votes* v, uint8_t* status_out, txv_commi
 int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23) {
   if (!c) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  auto it = c->tx_index.find(std::string((const char*)txhash, len));
-  if (it == c->tx_index.end()) return 0;
-  if (sum) *sum = c->h_sum[it->second];
-  if (maj23) *maj23 = c->h_maj[it->second];
+  if (!txhash && len) return TXV_EINVAL;
+  const uint32_t sid = c->tx_tab.find(txhash, len, c->tx_tab.hash(txhash, len));
+  if (sid == UINT32_MAX) return 0;
+  if (sum) *sum = c->h_sum[sid];
+  if (maj23) *maj23 = c->h_maj[sid];
   return 1;
 }
 
-uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? (uint32_t)c->tx_keys.size() : 0; }
+uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? c->tx_tab.size() : 0; }
 int64_t txv_total_power(txv_ctx* c) { return c ? c->total : 0; }
 
 int txv_signbytes(int64_t height, const uint8_t* txhash, uint32_t txhash_len, int64_t ts_sec, int32_t ts_nanos,

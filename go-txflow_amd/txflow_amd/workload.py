@@ -81,3 +81,46 @@ class Workload:
         return dict(height=1, txhash=self.batch.txhash(i), ts_sec=int(self.batch.ts_sec[i]),
                     ts_nanos=int(self.batch.ts_nanos[i]), addr=self.batch.addr[20 * i:20 * i + 20].tobytes(),
                     sig=self.batch.sig[64 * i:64 * i + 64].tobytes())
+
+
+class StreamWorkload:
+    """C5: `n_vals` validators with power 1 + (rand mod 10^6), every validator
+    votes every tx, arrival order = tx index + U(0, window) so a tx's votes straddle a few
+    consecutive `batch`-vote batches; the stream is cut into batches in arrival order."""
+
+    def __init__(self, ctx: Context, n_vals: int, n_txs: int, seed: int, batch: int = 65536, window: int = 128):
+        self.rng = np.random.default_rng(seed)
+        self.n_vals, self.n_txs, self.batch_size = n_vals, n_txs, batch
+        self.seeds = validator_seeds(n_vals)
+        self.pubs = ctx.keygen(self.seeds)
+        self.powers = 1 + (self.rng.integers(0, 1 << 62, n_vals) % 1_000_000).astype(np.int64)
+        ctx.set_validators(self.pubs, self.powers, CHAIN_ID)
+        addrs, ok = ctx.validator_info()
+        assert ok.all()
+        self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(n_vals, 20)
+        self.hashes = tx_hashes(n_txs, self.rng, 1 << 40)
+        n = n_txs * n_vals
+        tx_of = np.repeat(np.arange(n_txs, dtype=np.int64), n_vals)
+        val_of = np.tile(np.arange(n_vals, dtype=np.int64), n_txs)
+        order = np.argsort(tx_of + self.rng.random(n) * window, kind="stable")
+        self.tx_of, self.val_of = tx_of[order], val_of[order]
+        self.n = n
+        sig = np.zeros((n, 64), np.uint8)
+        self.batches = []
+        for s in range(0, n, batch):
+            e = min(n, s + batch)
+            m = e - s
+            b = VoteBatch(m, height=np.ones(m, np.int64), txhash_arena=self.hashes.reshape(-1),
+                          txhash_off=(self.tx_of[s:e] * 64).astype(np.uint32), txhash_len=np.full(m, 64, np.uint32),
+                          ts_sec=np.full(m, 1_700_000_000, np.int64),
+                          ts_nanos=(np.arange(s, e, dtype=np.int64) % 999_999_999 + 1),
+                          addr=self.addrs[self.val_of[s:e]], addr_len=np.full(m, 20, np.uint32),
+                          sig=sig[s:e], sig_len=np.full(m, 64, np.uint32))
+            b.sig = ctx.sign_votes(b, self.val_of[s:e].astype(np.uint32), CHAIN_ID).reshape(-1)
+            self.batches.append(b)
+        first = np.full(n_txs, -1, np.int64)
+        bidx = np.arange(n) // batch
+        # batch index of each tx's first vote
+        rev = np.arange(n)[::-1]
+        first[self.tx_of[rev]] = bidx[rev]
+        self.first_batch = first

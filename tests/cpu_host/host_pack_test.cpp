@@ -1,0 +1,75 @@
+// CPU test of go-txflow_amd/csrc/host_pack.hpp (the host pack's worker pool and lookup tables);
+// built by tests/test_host_pack.py with -fsanitize=thread (pool) / address,undefined (tables).
+#include "../../go-txflow_amd/csrc/host_pack.hpp"
+#include <cstdio>
+#include <map>
+#include <random>
+#include <string>
+
+using namespace txv_host;
+
+static int fail(const char* what, long a, long b) { printf("FAIL %s: %ld vs %ld\n", what, a, b); return 1; }
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 300;
+  // pool: back-to-back jobs of varying size; every index visited exactly once per job
+  {
+    WorkerPool pool(16);
+    std::vector<uint32_t> hits(100000);
+    for (int it = 0; it < iters; ++it) {
+      const uint32_t n = 1 + (uint32_t)((it * 7919u) % 99999u);
+      std::fill(hits.begin(), hits.begin() + n, 0u);
+      pool.parallel_for(n, [&](uint32_t lo, uint32_t hi) { for (uint32_t i = lo; i < hi; ++i) hits[i]++; }, 512);
+      for (uint32_t i = 0; i < n; ++i) if (hits[i] != 1) return fail("pool hit count", i, hits[i]);
+    }
+  }
+  // TxTable: ids in first-seen order, find after rehash, limit respected, clear
+  {
+    TxTable t(12345);
+    std::mt19937_64 rng(7);
+    std::map<std::string, uint32_t> ref;
+    std::vector<std::string> keys;
+    for (int i = 0; i < 50000; ++i) {
+      std::string k;
+      const int len = (int)(rng() % 80);   // includes empty keys and non-multiple-of-8 lengths
+      for (int j = 0; j < len; ++j) k.push_back((char)(rng() % 16 + 'A'));
+      if (rng() % 3 == 0 && !keys.empty()) k = keys[rng() % keys.size()];
+      keys.push_back(k);
+      bool created;
+      const uint32_t id = t.intern((const uint8_t*)k.data(), (uint32_t)k.size(), t.hash((const uint8_t*)k.data(), (uint32_t)k.size()), &created);
+      auto it = ref.find(k);
+      if (it == ref.end()) {
+        if (!created || id != ref.size()) return fail("intern new id", id, (long)ref.size());
+        ref.emplace(k, id);
+      } else if (created || id != it->second) return fail("intern existing id", id, it->second);
+    }
+    for (auto& kv : ref) {
+      const uint32_t id = t.find((const uint8_t*)kv.first.data(), (uint32_t)kv.first.size(),
+                                 t.hash((const uint8_t*)kv.first.data(), (uint32_t)kv.first.size()));
+      if (id != kv.second) return fail("find", id, kv.second);
+    }
+    if (t.size() != ref.size()) return fail("size", t.size(), (long)ref.size());
+    bool created;
+    const uint8_t nk[3] = {1, 2, 3};
+    if (t.intern(nk, 3, t.hash(nk, 3), &created, t.size()) != UINT32_MAX || created) return fail("limit", 0, 1);
+    t.clear();
+    if (t.size() != 0 || t.find(nk, 3, t.hash(nk, 3)) != UINT32_MAX) return fail("clear", t.size(), 0);
+  }
+  // AddrTable: exact 20-byte match, first index wins on a repeated address, misses
+  {
+    std::mt19937_64 rng(9);
+    std::vector<uint8_t> addrs(20 * 1000);
+    for (auto& b : addrs) b = (uint8_t)rng();
+    memcpy(addrs.data() + 20 * 999, addrs.data() + 20 * 5, 20);
+    AddrTable a;
+    a.build(addrs.data(), 1000);
+    for (uint32_t v = 0; v < 999; ++v) if (a.find(addrs.data() + 20 * v) != v) return fail("addr find", v, a.find(addrs.data() + 20 * v));
+    if (a.find(addrs.data() + 20 * 999) != 5) return fail("addr dup", a.find(addrs.data() + 20 * 999), 5);
+    uint8_t miss[20];
+    memcpy(miss, addrs.data(), 20);
+    miss[19] ^= 1;
+    if (a.find(miss) != UINT32_MAX) return fail("addr miss", 0, 1);
+  }
+  printf("ok\n");
+  return 0;
+}
