@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--txs-per-gpu", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16),
+    ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
     ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
                     help="base-point table window (0 = library default)")

@@ -469,6 +469,7 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
     case 12: launch_build<12>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 14: launch_build<14>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 18: launch_build<18>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
@@ -481,7 +482,8 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
 // window and the wide base tables wb in {20, 22, 24} over wa = 16
 bool txv_verify_windows_supported(int wb, int wa) {
   if (wb == wa) return wa == 4 || wa == 8 || wa == 10 || wa == 12 || wa == 14 || wa == 16;
-  return wa == 16 && (wb == 20 || wb == 22 || wb == 24);
+  if (wb == 24) return wa == 12 || wa == 14 || wa == 16 || wa == 18 || wa == 20;
+  return wa == 16 && (wb == 20 || wb == 22);
 }
 
 hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
@@ -502,7 +504,11 @@ hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t gr
       case 1616: e = launch_multi<B, 16, 16>(args, grid, st); break;
       case 2016: e = launch_multi<B, 20, 16>(args, grid, st); break;
       case 2216: e = launch_multi<B, 22, 16>(args, grid, st); break;
+      case 2412: e = launch_multi<B, 24, 12>(args, grid, st); break;
+      case 2414: e = launch_multi<B, 24, 14>(args, grid, st); break;
       case 2416: e = launch_multi<B, 24, 16>(args, grid, st); break;
+      case 2418: e = launch_multi<B, 24, 18>(args, grid, st); break;
+      case 2420: e = launch_multi<B, 24, 20>(args, grid, st); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

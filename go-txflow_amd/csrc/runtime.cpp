@@ -32,7 +32,7 @@ namespace {
 // fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 24
 inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 24; }
 constexpr uint32_t kTableWords4 = 64 * 9 * 24;
-inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16; }
+inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
 constexpr uint32_t kSlots = 4;
 
 struct Slot {
@@ -533,8 +533,8 @@ int build_base_table(txv_ctx* c, int w) {
 int choose_window(const txv_ctx* c, uint32_t n) {
   if (c->cfg_w) return c->cfg_w;
   const uint64_t budget = (uint64_t)c->cfg.table_budget_mb << 20;
-  for (int w : {16, 14, 12, 10, 8})
-    if ((uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
+  for (int w : {20, 18, 16, 14, 12, 10, 8})
+    if ((w <= 16 || c->lane_votes == 4) && (uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
   return 4;
 }
 
@@ -545,11 +545,12 @@ int choose_window(const txv_ctx* c, uint32_t n) {
 // when the wide table cannot be allocated.  d_btable = table of b_w.
 int select_window(txv_ctx* c, int w) {
   int r;
-  if (w != 4 && (r = build_base_table(c, w))) return r;
+  // radix-2^18 / 2^20 validator tables only run against the radix-2^24 base table
+  if (w != 4 && w <= 16 && (r = build_base_table(c, w))) return r;
   c->tab_w = w;
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
-  int bw = c->cfg_bw ? c->cfg_bw : (w == 16 ? 24 : w);
+  int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
   if (c->lane_votes != 4 || !txv_verify_windows_supported(bw, w)) bw = w;
   if (bw != w) {
     if (c->btable_wide_w != bw) {
@@ -573,6 +574,7 @@ int select_window(txv_ctx* c, int w) {
     c->b_w = bw;
     c->d_btable = c->d_btable_wide;
   }
+  if (!txv_verify_windows_supported(c->b_w, w)) { c->err = "no verify kernel for this table window"; return TXV_ENOMEM; }
   return TXV_OK;
 }
 
@@ -611,7 +613,7 @@ int prepare_keys(txv_ctx* c, const uint8_t* pubs32, uint32_t n, std::vector<uint
   if (c->tab_w) {
     w_keys = (uint64_t)nu * table_words(c->tab_w) * 4 <= ((uint64_t)c->cfg.table_budget_mb << 20) ? c->tab_w : 4;
   } else {
-    w_keys = choose_window(c, nu);
+    w_keys = std::min(choose_window(c, nu), 16);   // windows > 16 need the registry's wide B table
     if (w_keys != 4 && (r = build_base_table(c, w_keys))) return r;
   }
   if (nu > c->tmp_cap || w_keys != c->tmp_w) {
@@ -666,7 +668,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (!c->cfg.max_validators) c->cfg.max_validators = 1024;
   if (!c->cfg.max_accepted) c->cfg.max_accepted = (uint32_t)std::min<uint64_t>((uint64_t)c->cfg.max_txs * 128, 1u << 28);
   if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
-  if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 8192;
+  if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 80u << 10;   // 80 GiB of the 288 GB HBM
   c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }

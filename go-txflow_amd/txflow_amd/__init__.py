@@ -236,10 +236,10 @@ class Context:
                  max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
                  table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0,
                  base_w: int = 0):
-        """table_w: fixed-base window (4, 8, 10, 12, 14, 16) or None = the largest whose
+        """table_w: fixed-base window (4, 8, 10, 12, 14, 16, 18, 20) or None = the largest whose
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
-        if table_w not in (None, 4, 8, 10, 12, 14, 16):
-            raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16")
+        if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20):
+            raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16, 18, 20")
         if lane_votes not in (0, 2, 4):
             raise ValueError("lane_votes must be 0 (default), 2 or 4")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,

@@ -81,15 +81,18 @@ typedef struct {
                                until txv_reset_tally (TXV_ECAPACITY when exhausted) */
   uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
   uint32_t flags;           /* TXV_CFG_* bits */
-  uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 8192):
-                               the default window is the largest of 16/14/12/10/8 that fits */
+  uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 81920 =
+                               80 GiB): the default window is the largest of 20/18/16/14/12/10/8
+                               whose tables fit (100 validators: radix-2^20, 65 GB) */
 } txv_config;
 /* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the default
  * radix-256 tables (L2/MALL resident, 396 KB/validator, half the point additions) */
 #define TXV_CFG_TABLE_W4 0x1u
-/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14 or 16; 0 = auto by table_budget_mb):
- * per validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB, and
- * 128 / 64 / 52 / 44 / 38 / 32 point additions per verified vote */
+/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18 or 20; 0 = auto by
+ * table_budget_mb): per validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB / 189 MB /
+ * 654 MB.  Windows >= 12 run against the 8.9 GB radix-2^24 base-point table: 11 + ceil(256/W)
+ * point additions per verified vote (33 / 30 / 27 / 26 / 24 at W = 12..20); W = 4 / 8 / 10:
+ * 2 * ceil(256/W) = 128 / 64 / 52 */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19

@@ -227,14 +227,14 @@ def _table_mb(w: int) -> float:
     return -(-256 // w) * ((1 << (w - 1)) + 1) * 24 * 4 / 2 ** 20
 
 
-@pytest.mark.parametrize("budget_mb,exp_w", [(1, 4), (100, 12), (0, 16)])
+@pytest.mark.parametrize("budget_mb,exp_w", [(1, 4), (100, 12), (1000, 16), (4000, 18), (0, 20)])
 def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
-    """Auto window = largest of 16/14/12/10/8 whose per-validator tables fit the budget
-    (0 = 8 GiB default), else 4; every window verifies bit-exactly like the oracle, through
+    """Auto window = largest of 20/18/16/14/12/10/8 whose per-validator tables fit the budget
+    (0 = 80 GiB default), else 4; every window verifies bit-exactly like the oracle, through
     the registry and through caller-supplied keys on a context without a registry."""
     import txflow_amd as T
     n_vals = 16
-    exp_fit = max([w for w in (8, 10, 12, 14, 16) if n_vals * _table_mb(w) <= (budget_mb or 8192)], default=4)
+    exp_fit = max([w for w in (8, 10, 12, 14, 16, 18, 20) if n_vals * _table_mb(w) <= (budget_mb or 81920)], default=4)
     assert exp_fit == exp_w
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=64, table_budget_mb=budget_mb)
     try:
@@ -265,16 +265,16 @@ def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
         ctx2.close()
 
 
-@pytest.mark.parametrize("base_w", [20, 24])
-def test_wide_base_table_parity(oracle_lib, base_w):
-    """Radix-2^20 / 2^24 base-point tables (0.65 / 8.9 GB) over radix-2^16 validator
+@pytest.mark.parametrize("table_w,base_w", [(16, 20), (16, 24), (12, 24), (14, 24), (18, 24), (20, 24)])
+def test_wide_base_table_parity(oracle_lib, table_w, base_w):
+    """Radix-2^20 / 2^24 base-point tables (0.65 / 8.9 GB) over radix-2^12..2^20 validator
     tables: the same verdicts as the oracle on valid and corrupted votes."""
     import txflow_amd as T
-    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16, table_w=16, base_w=base_w)
+    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16, table_w=table_w, base_w=base_w)
     try:
-        rnd = random.Random(base_w)
+        rnd = random.Random(base_w * 100 + table_w)
         seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 4, 800, rnd)
-        assert (ctx.table_w, ctx.base_w) == (16, base_w)
+        assert (ctx.table_w, ctx.base_w) == (table_w, base_w)
         for i, v in enumerate(votes):
             if i % 3 == 1:
                 s = bytearray(v.Signature); s[rnd.randrange(64)] ^= 1 << rnd.randrange(8); v.Signature = bytes(s)
