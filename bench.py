@@ -124,7 +124,7 @@ def main():
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
     ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
                     help="base-point table window (0 = library default)")
-    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4),
+    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
@@ -167,6 +167,8 @@ def main():
     step_ms, verify_ms, tally_ms = [], [], []
 
     phases = {"reset": [], "run": [], "fetch": [], "gather": []}
+    st_buf = np.zeros(wl.n, np.uint8)          # result buffers reused every step
+    ev_buf = np.zeros(wl.n_txs + 1, T.EVENT_DTYPE)
 
     def step(record: bool):
         t0 = time.perf_counter()
@@ -174,7 +176,7 @@ def main():
         t1 = time.perf_counter()
         ms = ctx.run_staged(0, timed=True)
         t2 = time.perf_counter()
-        st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1)
+        st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf, evs=ev_buf)
         t3 = time.perf_counter()
         if dist is not None:
             ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)

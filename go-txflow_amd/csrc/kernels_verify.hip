@@ -449,6 +449,9 @@ template <int B, int WB, int WA>
 static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (args->lane_votes == 4) {
     hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 4>), dim3(grid), dim3(B), 0, st, *args);
+  } else if (args->lane_votes == 8) {
+    if constexpr (WB == 24) hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+    else return hipErrorInvalidValue;
   } else if (args->lane_votes == 2 && WB == WA) {
     hipLaunchKernelGGL((txv_k_scalarmult_pair<B, WA>), dim3(grid), dim3(B), 0, st, *args);
   } else {

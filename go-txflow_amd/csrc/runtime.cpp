@@ -534,7 +534,7 @@ int choose_window(const txv_ctx* c, uint32_t n) {
   if (c->cfg_w) return c->cfg_w;
   const uint64_t budget = (uint64_t)c->cfg.table_budget_mb << 20;
   for (int w : {20, 18, 16, 14, 12, 10, 8})
-    if ((w <= 16 || c->lane_votes == 4) && (uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
+    if ((w <= 16 || c->lane_votes >= 4) && (uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
   return 4;
 }
 
@@ -551,7 +551,7 @@ int select_window(txv_ctx* c, int w) {
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
   int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
-  if (c->lane_votes != 4 || !txv_verify_windows_supported(bw, w)) bw = w;
+  if (c->lane_votes < 4 || !txv_verify_windows_supported(bw, w)) bw = w;
   if (bw != w) {
     if (c->btable_wide_w != bw) {
       dfree(c->d_btable_wide);
@@ -673,7 +673,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }
   if (TXV_CFG_LANE_VOTES(c->cfg.flags)) c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags);
-  if (c->lane_votes != 2 && c->lane_votes != 4) { delete c; return TXV_EINVAL; }
+  if (c->lane_votes != 2 && c->lane_votes != 4 && c->lane_votes != 8) { delete c; return TXV_EINVAL; }
   c->cfg_bw = (int)TXV_CFG_B_WINDOW(c->cfg.flags);
   if (c->cfg_bw && c->cfg_bw != 4 && !valid_window(c->cfg_bw) && c->cfg_bw != 20 && c->cfg_bw != 22 && c->cfg_bw != 24) {
     delete c;

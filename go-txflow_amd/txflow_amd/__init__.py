@@ -240,8 +240,8 @@ class Context:
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
         if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20):
             raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16, 18, 20")
-        if lane_votes not in (0, 2, 4):
-            raise ValueError("lane_votes must be 0 (default), 2 or 4")
+        if lane_votes not in (0, 2, 4, 8):
+            raise ValueError("lane_votes must be 0 (default), 2, 4 or 8")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
                    (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16) | ((base_w & 0xFF) << 20),
                    table_budget_mb)
@@ -361,10 +361,15 @@ class Context:
         self._chk(lib().txv_run_staged(self._h, slot, ms if timed else None), "txv_run_staged")
         return (ms[0], ms[1], ms[2]) if timed else None
 
-    def fetch_staged(self, slot: int, n: int, ev_cap: int = 0):
-        out = np.zeros(max(n, 1), np.uint8)
+    def fetch_staged(self, slot: int, n: int, ev_cap: int = 0, out: np.ndarray | None = None,
+                     evs: np.ndarray | None = None):
+        """statuses and commit events of a staged run; `out` / `evs` may be caller-owned buffers
+        (reused across calls: no fresh pages to fault in on the hot path)"""
+        if out is None or out.size < max(n, 1) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            out = np.zeros(max(n, 1), np.uint8)
         ev_cap = ev_cap or max(n, 1)
-        evs = np.zeros(ev_cap, EVENT_DTYPE)
+        if evs is None or evs.size < ev_cap or evs.dtype != EVENT_DTYPE:
+            evs = np.zeros(ev_cap, EVENT_DTYPE)
         nev = ctypes.c_uint32()
         self._chk(lib().txv_fetch_staged(self._h, slot, out.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev)),
                   "fetch")
