@@ -73,8 +73,9 @@ def cpu_baseline(wl, threads: int, serial_votes: int, parallel_votes: int):
 
 def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     """C5: 1000 weighted validators, the stream cut into `batch`-vote batches fed
-    through txv_add_votes (host amino + routing + pack, H2D, verify + tally kernels, statuses and
-    commit events back).  Latency-to-commit of a tx = return of the call that reported its commit
+    through the pool ingest (txv_pool_check: SHA-256(Signature) keys on the GPU, LRU + pool list on
+    the host) and txv_add_votes (host amino + routing + pack, H2D, verify + tally kernels, statuses
+    and commit events back).  Latency-to-commit of a tx = return of the call that reported its commit
     event - submission of the batch holding its first vote."""
     import txflow_amd as T
     from txflow_amd.workload import StreamWorkload, SEEDS
@@ -84,12 +85,19 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     for b in wl.batches[:2]:
         ctx.add_votes(b, ev_cap=b.n)
     ctx.reset_flow()
-    submit, done, commit_t, added = [], [], {}, 0
+    # Reactor.Receive -> TxVotePool.CheckTxWithInfo (GPU keys + host LRU) -> TxFlow.TryAddVote
+    pool = T.TxVotePool(ctx, size=wl.n + 1, cache_size=wl.n + 1, max_txs_bytes=1 << 40)
+    submit, done, commit_t, added, pool_ms = [], [], {}, 0, []
     t0 = time.perf_counter()
     for k, b in enumerate(wl.batches):
         ts = time.perf_counter()
+        ps = pool.check_batch(b)
+        tp = time.perf_counter()
+        if not (ps == T.POOL_OK).all():
+            raise RuntimeError("C5: pool rejected a unique vote")
         st, ev = ctx.add_votes(b, ev_cap=b.n)
         te = time.perf_counter()
+        pool_ms.append((tp - ts) * 1e3)
         submit.append(ts)
         done.append(te)
         added += int(np.count_nonzero((st & 0x7F) == T.ADDED))
@@ -101,8 +109,12 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     ok = added == wl.n and len(commit_t) == wl.n_txs
     lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
     bl = (np.array(done) - np.array(submit)) * 1e3
+    ok = ok and pool.Size() == wl.n
+    pool.close()
     out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n} votes in {batch}-vote batches "
-                       f"through txv_add_votes", "correct": ok, "votes_per_s": round(wl.n / total, 1),
+                       f"through txv_pool_check (TxVotePool.CheckTx) + txv_add_votes (TxFlow.TryAddVote)",
+           "correct": ok, "votes_per_s": round(wl.n / total, 1),
+           "p50_pool_check_ms": round(float(np.median(pool_ms)), 3),
            "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
            "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
            "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,

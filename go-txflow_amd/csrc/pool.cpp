@@ -1,0 +1,223 @@
+// pool.cpp — TxVotePool (txvotepool/txvotepool.go) behind include/txvote.h.
+//
+// A batch of CheckTx calls is split the MI355X way: the per-vote work that is independent of
+// order -- txVoteKey = SHA-256(Signature) (:467-469) on the GPU (txv_sig_keys), TxVote.Size
+// (types/tx_vote.go:144-150) on the host threads -- runs for the whole batch first; then the
+// order-dependent part runs sequentially in arrival order exactly as CheckTxWithInfo does it
+// per vote (:187-261):
+//   1. Size() >= config.Size || txSize + TxsBytes() > config.MaxTxsBytes -> ErrMempoolIsFull
+//   2. txSize > MaxMsgBytes - aminoOverheadForTxMessage (8, reactor.go:27,379) -> ErrTxTooLarge
+//   3. cache.Push(key) false (key present: moved to the back) -> ErrTxInCache
+//      (mapTxCache.Push :416-438: evicts the front when full; nopTxCache when CacheSize == 0)
+//   4. addTx (:265-270): txs.PushBack, txsMap[key] = element, txsBytes += Size()
+// Update (:329-359) pushes every committed key to the cache and removes the pool element
+// txsMap[key] (removeTx :275-284, which subtracts the *committed* vote's Size()).
+// Sender bookkeeping (MempoolTxVote.Senders), the WAL and metrics carry no verdicts and are
+// not restated.
+#include "../../include/txvote.h"
+#include "amino.hpp"
+
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+struct Key {
+  uint8_t b[32];
+  bool operator==(const Key& o) const { return memcmp(b, o.b, 32) == 0; }
+};
+struct KeyHash {
+  size_t operator()(const Key& k) const {   // SHA-256 output: any 8 bytes are uniform
+    uint64_t h;
+    memcpy(&h, k.b, 8);
+    return (size_t)(h ^ (h >> 29));
+  }
+};
+
+// doubly linked list in a vector (stable indices), with a key -> node map
+struct KeyList {
+  struct Node { Key k; uint32_t size; int32_t prev, next; };
+  std::vector<Node> nodes;
+  std::vector<int32_t> free_;
+  int32_t head = -1, tail = -1;
+  size_t len = 0;
+  int32_t push_back(const Key& k, uint32_t size) {
+    int32_t i;
+    if (!free_.empty()) { i = free_.back(); free_.pop_back(); }
+    else { i = (int32_t)nodes.size(); nodes.push_back(Node{}); }
+    nodes[i] = Node{k, size, tail, -1};
+    if (tail >= 0) nodes[tail].next = i; else head = i;
+    tail = i;
+    ++len;
+    return i;
+  }
+  void unlink(int32_t i) {
+    Node& n = nodes[i];
+    if (n.prev >= 0) nodes[n.prev].next = n.next; else head = n.next;
+    if (n.next >= 0) nodes[n.next].prev = n.prev; else tail = n.prev;
+    free_.push_back(i);
+    --len;
+  }
+  void move_to_back(int32_t i) {
+    if (i == tail) return;
+    Node& n = nodes[i];
+    if (n.prev >= 0) nodes[n.prev].next = n.next; else head = n.next;
+    nodes[n.next].prev = n.prev;
+    n.prev = tail; n.next = -1;
+    nodes[tail].next = i;
+    tail = i;
+  }
+  void clear() { nodes.clear(); free_.clear(); head = tail = -1; len = 0; }
+};
+
+}  // namespace
+
+struct txv_pool {
+  txv_pool_config cfg{};
+  bool cache_on = true;
+  int64_t height = 0;
+  std::mutex mu;                                   // proxyMtx
+  KeyList cache;                                   // mapTxCache.list
+  std::unordered_map<Key, int32_t, KeyHash> cache_map;
+  KeyList txs;                                     // txs (clist of MempoolTxVote)
+  std::unordered_map<Key, int32_t, KeyHash> txs_map;
+  int64_t txs_bytes = 0;
+  std::vector<uint8_t> keys;                       // batch scratch
+
+  bool cache_push(const Key& k) {                  // mapTxCache.Push
+    if (!cache_on) return true;
+    auto it = cache_map.find(k);
+    if (it != cache_map.end()) { cache.move_to_back(it->second); return false; }
+    if (cache.len >= cfg.cache_size && cache.head >= 0) {
+      cache_map.erase(cache.nodes[cache.head].k);
+      cache.unlink(cache.head);
+    }
+    cache_map[k] = cache.push_back(k, 0);
+    return true;
+  }
+};
+
+namespace {
+
+int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off) {
+  p->keys.resize((size_t)v->n * 32 + 32);
+  return txv_sig_keys(ctx, v, sig_full, sig_full_off, p->keys.data());
+}
+
+inline uint32_t vote_size(const txv_votes* v, uint32_t i) {
+  return (uint32_t)txv_host::txvote_size(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], v->addr_len[i],
+                                         v->sig_len[i]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out) {
+  if (!out) return TXV_EINVAL;
+  txv_pool* p = new (std::nothrow) txv_pool();
+  if (!p) return TXV_ENOMEM;
+  if (cfg) p->cfg = *cfg;
+  // tendermint config.DefaultMempoolConfig (external): Size 5000, CacheSize 10000,
+  // MaxTxsBytes 1 GiB, MaxMsgBytes 1 MiB
+  if (!p->cfg.size) p->cfg.size = 5000;
+  if (!p->cfg.cache_size) p->cfg.cache_size = 10000;
+  if (!p->cfg.max_txs_bytes) p->cfg.max_txs_bytes = 1ull << 30;
+  if (!p->cfg.max_msg_bytes) p->cfg.max_msg_bytes = 1u << 20;
+  p->cache_on = p->cfg.cache_size != TXV_POOL_NO_CACHE;
+  p->height = height;
+  if (p->cache_on) p->cache_map.reserve(std::min<uint32_t>(p->cfg.cache_size, 1u << 22));
+  *out = p;
+  return TXV_OK;
+}
+
+void txv_pool_free(txv_pool* p) { delete p; }
+
+int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
+                   const uint64_t* sig_full_off, uint8_t* status_out) {
+  if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
+  if (r) return r;
+  const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
+  for (uint32_t i = 0; i < v->n; ++i) {
+    const uint32_t sz = vote_size(v, i);
+    if (!sz) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
+    if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
+      status_out[i] = TXV_POOL_ERR_FULL;
+      continue;
+    }
+    if ((int64_t)sz > max_tx) { status_out[i] = TXV_POOL_ERR_TOO_LARGE; continue; }
+    Key k;
+    memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
+    if (!p->cache_push(k)) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
+    p->txs_map[k] = p->txs.push_back(k, sz);        // addTx
+    p->txs_bytes += sz;
+    status_out[i] = TXV_POOL_OK;
+  }
+  return TXV_OK;
+}
+
+int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
+                    const uint64_t* sig_full_off) {
+  if (!p || !ctx || !v) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->height = height;
+  int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
+  if (r) return r;
+  for (uint32_t i = 0; i < v->n; ++i) {
+    Key k;
+    memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
+    (void)p->cache_push(k);
+    auto it = p->txs_map.find(k);
+    if (it != p->txs_map.end()) {                   // removeTx(tx, e, false)
+      p->txs.unlink(it->second);
+      p->txs_map.erase(it);
+      p->txs_bytes -= vote_size(v, i);
+    }
+  }
+  return TXV_OK;
+}
+
+int txv_pool_reap(txv_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap, uint64_t* n_out) {
+  if (!p) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  if (max < 0) max = (int64_t)p->txs.len;
+  uint64_t n = 0;
+  for (int32_t e = p->txs.head; e >= 0 && (int64_t)n <= max; e = p->txs.nodes[e].next, ++n) {
+    if (n < cap) {
+      if (keys_out) memcpy(keys_out + 32 * n, p->txs.nodes[e].k.b, 32);
+      if (sizes_out) sizes_out[n] = p->txs.nodes[e].size;
+    }
+  }
+  if (n_out) *n_out = n;
+  return TXV_OK;
+}
+
+int txv_pool_flush(txv_pool* p) {
+  if (!p) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->cache.clear(); p->cache_map.clear();
+  p->txs.clear(); p->txs_map.clear();
+  p->txs_bytes = 0;
+  return TXV_OK;
+}
+
+int64_t txv_pool_size(txv_pool* p) { return p ? (int64_t)p->txs.len : 0; }
+int64_t txv_pool_txs_bytes(txv_pool* p) { return p ? p->txs_bytes : 0; }
+int64_t txv_pool_height(txv_pool* p) { return p ? p->height : 0; }
+
+int txv_pool_cache_keys(txv_pool* p, uint8_t* keys_out, uint64_t cap, uint64_t* n_out) {
+  if (!p) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  uint64_t n = 0;
+  for (int32_t e = p->cache.head; e >= 0; e = p->cache.nodes[e].next, ++n)
+    if (keys_out && n < cap) memcpy(keys_out + 32 * n, p->cache.nodes[e].k.b, 32);
+  if (n_out) *n_out = n;
+  return TXV_OK;
+}
+
+}  // extern "C"

@@ -13,6 +13,7 @@
 #include "txv_tally.h"
 #include "amino.hpp"
 #include "host_pack.hpp"
+#include "sha2.h"
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -113,6 +114,10 @@ struct txv_ctx {
   uint32_t n_signers = 0;
   uint32_t *d_sk_scal = nullptr, *d_sk_araw = nullptr, *d_sk_prefix = nullptr, *d_sk_pub = nullptr;
   Slot slots[kSlots];
+  // txv_sig_keys scratch: signatures [n][16] u32, lengths, keys [n][8] u32
+  uint32_t pk_cap = 0;
+  uint32_t *d_pk_sig = nullptr, *d_pk_len = nullptr, *d_pk_keys = nullptr;
+  uint32_t *h_pk_sig = nullptr, *h_pk_len = nullptr, *h_pk_keys = nullptr;
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -722,6 +727,7 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_acc_slot); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_bitmap);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
+  dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1013,6 +1019,61 @@ int txv_reset_tally(txv_ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (!c->n_vals) return TXV_OK;
   return reset_tally(c, true);
+}
+
+// SHA-256 of an arbitrary byte string on the host (signatures longer than 64 bytes only)
+static void sha256_host(const uint8_t* p, uint64_t n, uint8_t out[32]) {
+  uint32_t st[8], w[16];
+  txv::sha256_init(st);
+  const uint64_t total = n + 9, nblk = (total + 63) / 64;
+  for (uint64_t b = 0; b < nblk; ++b) {
+    uint8_t blk[64];
+    for (int j = 0; j < 64; ++j) {
+      const uint64_t g = b * 64 + (uint64_t)j;
+      blk[j] = g < n ? p[g] : (g == n ? 0x80 : 0);
+    }
+    if (b == nblk - 1)
+      for (int j = 0; j < 8; ++j) blk[56 + j] = (uint8_t)((n * 8) >> (56 - 8 * j));
+    for (int t = 0; t < 16; ++t)
+      w[t] = ((uint32_t)blk[4 * t] << 24) | ((uint32_t)blk[4 * t + 1] << 16) | ((uint32_t)blk[4 * t + 2] << 8) | blk[4 * t + 3];
+    txv::sha256_block(st, w);
+  }
+  for (int j = 0; j < 8; ++j)
+    for (int b = 0; b < 4; ++b) out[4 * j + b] = (uint8_t)(st[j] >> (24 - 8 * b));
+}
+
+int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                 uint8_t* keys_out) {
+  if (!c || !v || (v->n && (!v->sig || !v->sig_len || !keys_out))) return TXV_EINVAL;
+  const uint32_t n = v->n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (v->sig_len[i] > 64 && (!sig_full || !sig_full_off)) { c->err = "signature > 64 bytes without sig_full"; return TXV_EINVAL; }
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!n) return TXV_OK;
+  if (n > c->pk_cap) {
+    int r;
+    if ((r = dalloc(c, &c->d_pk_sig, (size_t)n * 16)) || (r = dalloc(c, &c->d_pk_len, n)) ||
+        (r = dalloc(c, &c->d_pk_keys, (size_t)n * 8)) || (r = halloc(c, &c->h_pk_sig, (size_t)n * 16)) ||
+        (r = halloc(c, &c->h_pk_len, n)) || (r = halloc(c, &c->h_pk_keys, (size_t)n * 8)))
+      return r;
+    c->pk_cap = n;
+  }
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+    memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+  }, 8192);
+  HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig, c->h_pk_sig, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
+    for (uint32_t i = lo; i < hi; ++i)
+      if (v->sig_len[i] > 64) sha256_host(sig_full + sig_full_off[i], v->sig_len[i], keys_out + (size_t)i * 32);
+  }, 8192);
+  return TXV_OK;
 }
 
 int txv_reset_flow(txv_ctx* c) {

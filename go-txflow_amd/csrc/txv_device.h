@@ -62,6 +62,8 @@ hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_
                              uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
 hipError_t txv_launch_valu_probe(int op, uint32_t* out, uint32_t blocks, int iters, hipStream_t st);
+hipError_t txv_launch_sig_keys(const uint32_t* sig, const uint32_t* sig_len, uint32_t n, uint32_t* keys,
+                                hipStream_t st);
 hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,
                                   hipStream_t st);
 }

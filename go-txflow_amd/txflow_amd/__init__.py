@@ -61,6 +61,11 @@ class _Votes(ctypes.Structure):
                 ("addr_len", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_void_p)]
 
 
+class _PoolCfg(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint32), ("cache_size", ctypes.c_uint32), ("max_txs_bytes", ctypes.c_uint64),
+                ("max_msg_bytes", ctypes.c_uint32), ("pad0", ctypes.c_uint32)]
+
+
 class _Event(ctypes.Structure):
     _fields_ = [("vote_index", ctypes.c_uint32), ("tx_index", ctypes.c_uint32), ("sum", ctypes.c_int64)]
 
@@ -109,6 +114,17 @@ def lib():
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "txv_table_window": ([vp], ctypes.c_int),
             "txv_base_window": ([vp], ctypes.c_int),
+            "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
+            "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
+            "txv_pool_free": ([vp], None),
+            "txv_pool_check": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
+            "txv_pool_update": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
+            "txv_pool_reap": ([vp, i64, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_pool_flush": ([vp], ctypes.c_int),
+            "txv_pool_size": ([vp], i64),
+            "txv_pool_txs_bytes": ([vp], i64),
+            "txv_pool_height": ([vp], i64),
+            "txv_pool_cache_keys": ([vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -123,7 +139,9 @@ EXPORTED_SYMBOLS = [
     "txv_get_validator_info", "txv_verify_batch", "txv_verify_bytes", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
-    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window"]
+    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
+    "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
+    "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -316,6 +334,15 @@ class Context:
                                          sg.ctypes.data, sl.ctypes.data, n, out.ctypes.data), "txv_verify_bytes")
         return out[:n].astype(bool)
 
+    def sig_keys(self, batch: VoteBatch, long_sigs: Optional[dict] = None) -> np.ndarray:
+        """txVoteKey = SHA-256(Signature) per vote ([n, 32] u8), hashed on the GPU;
+        long_sigs: {index: full signature bytes} for votes with sig_len > 64."""
+        out = np.zeros((max(batch.n, 1), 32), np.uint8)
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        self._chk(lib().txv_sig_keys(self._h, ctypes.byref(vs), full, off, out.ctypes.data), "txv_sig_keys")
+        return out[:batch.n]
+
     def add_votes(self, batch: VoteBatch, ev_cap: int = 0):
         out = np.zeros(max(batch.n, 1), np.uint8)
         ev_cap = ev_cap or max(batch.n, 1)
@@ -415,6 +442,93 @@ class Context:
         out = np.zeros((n, 8), np.uint32)
         self._chk(lib().txv_fe_selftest(self._h, a.ctypes.data, b.ctypes.data, out.ctypes.data, n, op), "selftest")
         return out
+
+
+def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):
+    """(arena ptr, offsets ptr) for txv_* calls taking sig_full / sig_full_off, or (None, None)"""
+    if not long_sigs:
+        return None, None
+    arena = bytearray()
+    off = np.zeros(max(batch.n, 1), np.uint64)
+    for i, s in long_sigs.items():
+        assert len(s) == int(batch.sig_len[i]), "long_sigs entry does not match sig_len"
+        off[i] = len(arena)
+        arena += s
+    a = np.frombuffer(bytes(arena) or b"\0", np.uint8)
+    _long_sig_arena.keep = (a, off)     # alive for the duration of the call
+    return a.ctypes.data, off.ctypes.data
+
+
+POOL_OK, POOL_ERR_FULL, POOL_ERR_TOO_LARGE, POOL_ERR_IN_CACHE, POOL_ERR_ENCODING = range(5)
+POOL_NO_CACHE = 0xFFFFFFFF
+
+
+class TxVotePool:
+    """TxVotePool (txvotepool/txvotepool.go) over libtxvote.so: CheckTx (:180-261) per vote in
+    arrival order with the txVoteKey = SHA-256(Signature) keys computed on the GPU of `ctx`,
+    Update (:329-359), ReapMaxTxs (:310-324), Flush (:146-159), Size (:136), TxsBytes (:141).
+    cache_size POOL_NO_CACHE selects nopTxCache; 0 fields take tendermint's defaults."""
+
+    def __init__(self, ctx: Context, size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
+                 max_msg_bytes: int = 0, height: int = 0):
+        self.ctx = ctx
+        cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes, 0)
+        h = ctypes.c_void_p()
+        rc = lib().txv_pool_new(ctypes.byref(cfg), height, ctypes.byref(h))
+        if rc != 0:
+            raise TxvInfraError(f"txv_pool_new failed ({rc})")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().txv_pool_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def check_batch(self, batch: VoteBatch, long_sigs: Optional[dict] = None) -> np.ndarray:
+        out = np.zeros(max(batch.n, 1), np.uint8)
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        self.ctx._chk(lib().txv_pool_check(self._h, self.ctx._h, ctypes.byref(vs), full, off, out.ctypes.data),
+                      "txv_pool_check")
+        return out[:batch.n]
+
+    def update(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        self.ctx._chk(lib().txv_pool_update(self._h, self.ctx._h, height, ctypes.byref(vs), full, off),
+                      "txv_pool_update")
+
+    def reap(self, max_txs: int = -1):
+        """ReapMaxTxs: ([k, 32] keys, [k] sizes) in pool order"""
+        n = ctypes.c_uint64()
+        lib().txv_pool_reap(self._h, max_txs, None, None, 0, ctypes.byref(n))
+        k = n.value
+        keys = np.zeros((max(k, 1), 32), np.uint8)
+        sizes = np.zeros(max(k, 1), np.uint32)
+        lib().txv_pool_reap(self._h, max_txs, keys.ctypes.data, sizes.ctypes.data, k, ctypes.byref(n))
+        return keys[:k], sizes[:k]
+
+    def cache_keys(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        lib().txv_pool_cache_keys(self._h, None, 0, ctypes.byref(n))
+        keys = np.zeros((max(n.value, 1), 32), np.uint8)
+        lib().txv_pool_cache_keys(self._h, keys.ctypes.data, n.value, ctypes.byref(n))
+        return keys[:n.value]
+
+    def flush(self):
+        lib().txv_pool_flush(self._h)
+
+    def Size(self) -> int:
+        return int(lib().txv_pool_size(self._h))
+
+    def TxsBytes(self) -> int:
+        return int(lib().txv_pool_txs_bytes(self._h))
+
+    def Height(self) -> int:
+        return int(lib().txv_pool_height(self._h))
 
 
 # ------------------------------------------------------------------ reference-shaped API

@@ -24,6 +24,11 @@
  *   txv_signbytes      <- func (vote *TxVote) SignBytes(chainID string) []byte   types/tx_vote.go:83-89
  *   txv_txvote_size    <- func (vote *TxVote) Size() int                         types/tx_vote.go:144-150
  *   txv_keygen/txv_sign_votes <- MockPV.SignTxVote types/priv_validator.go:83-95 (load generator)
+ *   txv_sig_keys       <- txVoteKey(tx) = sha256.Sum256(tx.Signature)   txvotepool/txvotepool.go:467-469
+ *   txv_pool_*         <- TxVotePool (txvotepool/txvotepool.go): NewTxVotePool :56-75,
+ *                         CheckTx/CheckTxWithInfo :180-261 (+ mapTxCache.Push :416-438, addTx :265-270),
+ *                         Update :329-359, ReapMaxTxs :310-324, Flush :146-159, Size :136,
+ *                         TxsBytes :141; removeTx :275-284
  */
 #ifndef TXVOTE_H
 #define TXVOTE_H
@@ -205,6 +210,55 @@ int txv_reset_tally(txv_ctx* ctx);
  * txflow/service.go:71), keeping the validator set and its tables */
 int txv_reset_flow(txv_ctx* ctx);
 int txv_sync(txv_ctx* ctx);
+
+/* ---- TxVotePool ingest (txvotepool/txvotepool.go) ----
+ * Long signatures: txv_votes.sig holds the first 64 bytes of each signature.  Calls taking
+ * sig_full / sig_full_off (optional) read signature i from sig_full + sig_full_off[i]
+ * (sig_len[i] bytes) when sig_len[i] > 64; without them such a vote is TXV_EINVAL. */
+
+/* txVoteKey for n votes: keys_out[i] (32 bytes) = SHA-256(Signature_i), hashed on the GPU
+ * (signatures > 64 bytes on the host). */
+int txv_sig_keys(txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                 uint8_t* keys_out);
+
+typedef struct {
+  uint32_t size;            /* MempoolConfig.Size: max txs in the pool (0 -> 5000, tendermint default) */
+  uint32_t cache_size;      /* MempoolConfig.CacheSize: LRU entries; 0 -> 10000; TXV_POOL_NO_CACHE = nopTxCache */
+  uint64_t max_txs_bytes;   /* MempoolConfig.MaxTxsBytes (0 -> 1 GiB) */
+  uint32_t max_msg_bytes;   /* MempoolConfig.MaxMsgBytes (0 -> 1 MiB); max tx size = this - 8 (reactor.go:379) */
+  uint32_t pad0;
+} txv_pool_config;
+#define TXV_POOL_NO_CACHE 0xFFFFFFFFu
+typedef struct txv_pool txv_pool;
+
+/* per-vote CheckTx results (nil error / the reference's error values) */
+#define TXV_POOL_OK 0            /* added to the pool (nil) */
+#define TXV_POOL_ERR_FULL 1      /* mempool.ErrMempoolIsFull */
+#define TXV_POOL_ERR_TOO_LARGE 2 /* ErrTxTooLarge */
+#define TXV_POOL_ERR_IN_CACHE 3  /* mempool.ErrTxInCache */
+#define TXV_POOL_ERR_ENCODING 4  /* TxVote.Size(): amino rejects the timestamp (the reference panics) */
+
+int  txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out);
+void txv_pool_free(txv_pool* pool);
+/* CheckTxWithInfo for each vote in arrival order (keys on ctx's GPU); status_out[i] = TXV_POOL_*. */
+int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
+                   const uint64_t* sig_full_off, uint8_t* status_out);
+/* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
+ * leaves the pool if its key is there. */
+int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,
+                    const uint8_t* sig_full, const uint64_t* sig_full_off);
+/* ReapMaxTxs(max) in pool order: keys (32 B) and TxVote.Size of the reaped entries; the
+ * reference loop condition `len(txs) <= max` reaps max + 1 entries when available; max < 0 = all.
+ * keys_out / sizes_out capacity `cap`; *n_out = entries reaped (may exceed cap: truncated). */
+int txv_pool_reap(txv_pool* pool, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap,
+                  uint64_t* n_out);
+/* Flush: empty pool and cache. */
+int txv_pool_flush(txv_pool* pool);
+int64_t txv_pool_size(txv_pool* pool);
+int64_t txv_pool_txs_bytes(txv_pool* pool);
+int64_t txv_pool_height(txv_pool* pool);
+/* LRU cache keys front (oldest) to back; *n_out = cache length (test hook: cache_test.go). */
+int txv_pool_cache_keys(txv_pool* pool, uint8_t* keys_out, uint64_t cap, uint64_t* n_out);
 
 /* ---- self-test hook: field/scalar ops on device (tests only) ---- */
 int txv_fe_selftest(txv_ctx* ctx, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op);

@@ -119,6 +119,21 @@ uint32_t orc_flow_num_sets(orc_flow*);
 /* count of ed25519 verifications performed (for baseline accounting) */
 uint64_t orc_flow_num_verifies(orc_flow*);
 
+/* ---- TxVotePool (txvotepool/txvotepool.go) restatement ----
+ * cache_size 0xFFFFFFFF = nopTxCache.  orc_pool_check returns 0 ok, 1 ErrMempoolIsFull,
+ * 2 ErrTxTooLarge, 3 ErrTxInCache, 4 amino error in Size() (the reference panics). */
+typedef struct orc_pool orc_pool;
+orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_bytes, uint32_t max_msg_bytes,
+                       int64_t height);
+void orc_pool_free(orc_pool*);
+int orc_pool_check(orc_pool*, const orc_vote* v);
+void orc_pool_update(orc_pool*, int64_t height, const orc_vote* votes, uint32_t n);
+uint64_t orc_pool_reap(orc_pool*, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap);
+void orc_pool_flush(orc_pool*);
+int64_t orc_pool_size(orc_pool*);
+int64_t orc_pool_txs_bytes(orc_pool*);
+uint64_t orc_pool_cache_keys(orc_pool*, uint8_t* keys_out, uint64_t cap);
+
 /* ---- CPU baseline: parallel verify with T threads (T = 1 mirrors checkMaj23Routine). ---- */
 /* Verifies n (pub,msg,sig) triples; msgs in an arena with offsets/lengths. Returns seconds. */
 double orc_verify_many(const uint8_t* pubs32, const uint32_t* val_idx,

@@ -53,6 +53,20 @@ def lib():
                                              ctypes.c_void_p, ctypes.c_void_p]
         L.orc_txvote_verify_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_u8p, ctypes.c_size_t, ctypes.c_int,
                                             ctypes.c_void_p]
+        L.orc_pool_new.restype = ctypes.c_void_p
+        L.orc_pool_new.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64]
+        L.orc_pool_free.argtypes = [ctypes.c_void_p]
+        L.orc_pool_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_pool_reap.restype = ctypes.c_uint64
+        L.orc_pool_reap.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_pool_flush.argtypes = [ctypes.c_void_p]
+        L.orc_pool_size.restype = ctypes.c_int64
+        L.orc_pool_size.argtypes = [ctypes.c_void_p]
+        L.orc_pool_txs_bytes.restype = ctypes.c_int64
+        L.orc_pool_txs_bytes.argtypes = [ctypes.c_void_p]
+        L.orc_pool_cache_keys.restype = ctypes.c_uint64
+        L.orc_pool_cache_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.orc_flow_query.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint32,
                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
         L.orc_flow_num_sets.argtypes = [ctypes.c_void_p]
@@ -252,3 +266,65 @@ def verify_many(pubs32, val_idx, arena, msg_off, msg_len, sigs64, threads=1):
                                               msg_off.astype(np.uint32), msg_len.astype(np.uint16), sigs64)]
     t = lib().orc_verify_many(*[a.ctypes.data for a in arrs], n, threads, out.ctypes.data)
     return t, out
+
+
+def _orc_vote(v, keep):
+    """orc_vote from an oracle-style dict (nil, height, txhash, ts_sec, ts_nanos, addr, sig)"""
+    ov = _Vote()
+    bufs = [ctypes.create_string_buffer(bytes(v.get(k, b"")) or b"\0", max(len(v.get(k, b"")), 1))
+            for k in ("txhash", "addr", "sig")]
+    keep.append(bufs)
+    ov.is_nil = 1 if v.get("nil") else 0
+    ov.height = v.get("height", 0)
+    ov.txhash = ctypes.addressof(bufs[0]); ov.txhash_len = len(v.get("txhash", b""))
+    ov.ts_sec = v.get("ts_sec", 0); ov.ts_nanos = v.get("ts_nanos", 0)
+    ov.addr = ctypes.addressof(bufs[1]); ov.addr_len = len(v.get("addr", b""))
+    ov.sig = ctypes.addressof(bufs[2]); ov.sig_len = len(v.get("sig", b""))
+    return ov
+
+
+class Pool:
+    """Sequential TxVotePool restatement (oracle/pool.c); votes as oracle-style dicts with the
+    FULL signature bytes."""
+
+    def __init__(self, size=5000, cache_size=10000, max_txs_bytes=1 << 30, max_msg_bytes=1 << 20, height=0):
+        self._h = lib().orc_pool_new(size, cache_size, max_txs_bytes, max_msg_bytes, height)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_pool_free(self._h)
+            self._h = None
+
+    def check(self, votes):
+        import numpy as np
+        keep = []
+        return np.array([lib().orc_pool_check(self._h, ctypes.byref(_orc_vote(v, keep))) for v in votes], np.uint8)
+
+    def update(self, height, votes):
+        keep = []
+        arr = (_Vote * max(len(votes), 1))(*[_orc_vote(v, keep) for v in votes])
+        lib().orc_pool_update(self._h, height, ctypes.addressof(arr), len(votes))
+
+    def reap(self, max_txs=-1):
+        import numpy as np
+        n = lib().orc_pool_reap(self._h, max_txs, None, None, 0)
+        keys = np.zeros((max(n, 1), 32), np.uint8)
+        sizes = np.zeros(max(n, 1), np.uint32)
+        lib().orc_pool_reap(self._h, max_txs, keys.ctypes.data, sizes.ctypes.data, n)
+        return keys[:n], sizes[:n]
+
+    def cache_keys(self):
+        import numpy as np
+        n = lib().orc_pool_cache_keys(self._h, None, 0)
+        keys = np.zeros((max(n, 1), 32), np.uint8)
+        lib().orc_pool_cache_keys(self._h, keys.ctypes.data, n)
+        return keys[:n]
+
+    def flush(self):
+        lib().orc_pool_flush(self._h)
+
+    def size(self):
+        return lib().orc_pool_size(self._h)
+
+    def txs_bytes(self):
+        return lib().orc_pool_txs_bytes(self._h)

@@ -1,0 +1,159 @@
+/*
+ * pool.c — sequential restatement of TxVotePool.CheckTxWithInfo / Update / ReapMaxTxs / Flush
+ * and mapTxCache (txvotepool/txvotepool.go).  TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ *   :187-261  CheckTxWithInfo: full (Size() >= config.Size || size + TxsBytes > MaxTxsBytes),
+ *             too large (size > MaxMsgBytes - 8, reactor.go:27,379), cache.Push false ->
+ *             ErrTxInCache, else addTx (:265-270)
+ *   :416-438  mapTxCache.Push: present -> MoveToBack, false; full -> remove Front; PushBack
+ *   :457-459  nopTxCache (CacheSize == 0 in the reference config; here cache_size == ~0u)
+ *   :329-359  Update: cache.Push(tx); txsMap hit -> removeTx(tx, e, false) (:275-284, which
+ *             subtracts the committed tx's Size())
+ *   :310-324  ReapMaxTxs: loop while len(txs) <= max (max + 1 entries), max < 0 -> all
+ *   :467-469  txVoteKey = sha256.Sum256(Signature)
+ * Every list is a plain doubly linked list of heap nodes; lookups walk a chained hash.
+ */
+#include "oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct pnode {
+  uint8_t key[32];
+  uint32_t size;
+  int mapped;                   /* txs: this element is txsMap[key] (a later push of the key overwrites) */
+  struct pnode *prev, *next;    /* list order */
+  struct pnode *hnext;          /* hash chain */
+} pnode;
+
+typedef struct {
+  pnode *head, *tail;
+  size_t len;
+  pnode** bucket;
+  size_t nb;
+} plist;
+
+struct orc_pool {
+  uint32_t size, cache_size, max_msg_bytes;
+  uint64_t max_txs_bytes;
+  int cache_on;
+  int64_t height, txs_bytes;
+  plist cache, txs;
+};
+
+static size_t bidx(const plist* l, const uint8_t* k) {
+  uint64_t h = 0;
+  for (int i = 0; i < 8; ++i) h = (h << 8) | k[i];
+  return (size_t)(h % l->nb);
+}
+static void pl_init(plist* l) { memset(l, 0, sizeof *l); l->nb = 65521; l->bucket = (pnode**)calloc(l->nb, sizeof(pnode*)); }
+static pnode* pl_find(const plist* l, const uint8_t* k) {   /* the mapped node with key k */
+  for (pnode* n = l->bucket[bidx(l, k)]; n; n = n->hnext)
+    if (n->mapped && !memcmp(n->key, k, 32)) return n;
+  return 0;
+}
+static pnode* pl_push_back(plist* l, const uint8_t* k, uint32_t size) {
+  pnode* old = pl_find(l, k);
+  if (old) old->mapped = 0;     /* txsMap.Store / cache map assignment replaces the entry */
+  pnode* n = (pnode*)calloc(1, sizeof *n);
+  n->mapped = 1;
+  memcpy(n->key, k, 32);
+  n->size = size;
+  n->prev = l->tail;
+  if (l->tail) l->tail->next = n; else l->head = n;
+  l->tail = n;
+  size_t b = bidx(l, k);
+  n->hnext = l->bucket[b];
+  l->bucket[b] = n;
+  l->len++;
+  return n;
+}
+static void pl_remove(plist* l, pnode* n) {
+  if (n->prev) n->prev->next = n->next; else l->head = n->next;
+  if (n->next) n->next->prev = n->prev; else l->tail = n->prev;
+  pnode** pp = &l->bucket[bidx(l, n->key)];
+  while (*pp != n) pp = &(*pp)->hnext;
+  *pp = n->hnext;
+  l->len--;
+  free(n);
+}
+static void pl_clear(plist* l) {
+  while (l->head) pl_remove(l, l->head);
+}
+static void pl_free(plist* l) { pl_clear(l); free(l->bucket); }
+
+orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_bytes, uint32_t max_msg_bytes,
+                       int64_t height) {
+  orc_pool* p = (orc_pool*)calloc(1, sizeof *p);
+  p->size = size; p->cache_size = cache_size; p->max_txs_bytes = max_txs_bytes; p->max_msg_bytes = max_msg_bytes;
+  p->cache_on = cache_size != 0xFFFFFFFFu;
+  p->height = height;
+  pl_init(&p->cache);
+  pl_init(&p->txs);
+  return p;
+}
+void orc_pool_free(orc_pool* p) {
+  if (!p) return;
+  pl_free(&p->cache); pl_free(&p->txs);
+  free(p);
+}
+
+static int cache_push(orc_pool* p, const uint8_t* k) {
+  if (!p->cache_on) return 1;
+  pnode* n = pl_find(&p->cache, k);
+  if (n) {   /* MoveToBack: re-append (the cache never holds a key twice) */
+    pl_remove(&p->cache, n);
+    pl_push_back(&p->cache, k, 0);
+    return 0;
+  }
+  if (p->cache.len >= p->cache_size && p->cache.head) pl_remove(&p->cache, p->cache.head);
+  pl_push_back(&p->cache, k, 0);
+  return 1;
+}
+
+static void vote_key(const orc_vote* v, uint8_t key[32]) { orc_sha256(v->sig, v->sig_len, key); }
+
+int orc_pool_check(orc_pool* p, const orc_vote* v) {
+  const int sz = orc_txvote_size(v->height, v->txhash_len, v->ts_sec, v->ts_nanos, v->addr_len, v->sig_len);
+  if (sz <= 0) return 4;                                   /* amino error: the reference panics */
+  if ((int64_t)p->txs.len >= (int64_t)p->size || (int64_t)sz + p->txs_bytes > (int64_t)p->max_txs_bytes) return 1;
+  if ((int64_t)sz > (int64_t)p->max_msg_bytes - 8) return 2;
+  uint8_t k[32];
+  vote_key(v, k);
+  if (!cache_push(p, k)) return 3;
+  pl_push_back(&p->txs, k, (uint32_t)sz);
+  p->txs_bytes += sz;
+  return 0;
+}
+
+void orc_pool_update(orc_pool* p, int64_t height, const orc_vote* votes, uint32_t n) {
+  p->height = height;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint8_t k[32];
+    vote_key(&votes[i], k);
+    (void)cache_push(p, k);
+    pnode* e = pl_find(&p->txs, k);
+    if (e) {
+      pl_remove(&p->txs, e);
+      p->txs_bytes -= orc_txvote_size(votes[i].height, votes[i].txhash_len, votes[i].ts_sec, votes[i].ts_nanos,
+                                      votes[i].addr_len, votes[i].sig_len);
+    }
+  }
+}
+
+uint64_t orc_pool_reap(orc_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap) {
+  if (max < 0) max = (int64_t)p->txs.len;
+  uint64_t n = 0;
+  for (pnode* e = p->txs.head; e && (int64_t)n <= max; e = e->next, ++n)
+    if (n < cap) { memcpy(keys_out + 32 * n, e->key, 32); if (sizes_out) sizes_out[n] = e->size; }
+  return n;
+}
+
+void orc_pool_flush(orc_pool* p) { pl_clear(&p->cache); pl_clear(&p->txs); p->txs_bytes = 0; }
+int64_t orc_pool_size(orc_pool* p) { return (int64_t)p->txs.len; }
+int64_t orc_pool_txs_bytes(orc_pool* p) { return p->txs_bytes; }
+uint64_t orc_pool_cache_keys(orc_pool* p, uint8_t* keys_out, uint64_t cap) {
+  uint64_t n = 0;
+  for (pnode* e = p->cache.head; e; e = e->next, ++n)
+    if (n < cap) memcpy(keys_out + 32 * n, e->key, 32);
+  return n;
+}

@@ -1,0 +1,188 @@
+"""TxVotePool ingest (txvotepool/txvotepool.go): the oracle restatement (oracle/pool.c) against
+the reference's own pool tests restated on the code semantics (several of them were written for
+Tendermint's CListMempool and contradict this code, e.g. TestMempoolTxsBytes expects TxsBytes 1
+for a vote whose TxVote.Size() is ~100), and libtxvote.so (txv_sig_keys on the GPU + the host
+LRU / pool list) against the oracle on random streams.
+
+Reference tests restated (Fantom-foundation/go-txflow):
+  TestCacheRemove              txvotepool/cache_test.go:16-34   (pushes grow the cache list and map)
+  TestCacheAfterUpdate         txvotepool/cache_test.go:36-99   (Update pushes to the cache; order)
+  TestMempoolUpdateAddsTxsToCache txvotepool/txvotepool_test.go:110-120
+  TestSerialReap               txvotepool/txvotepool_test.go:166-251 (dupes cached, Update, redeliver)
+  TestMempoolMaxMsgSize        txvotepool/txvotepool_test.go:305-355 (ErrTxTooLarge boundary)
+  TestMempoolTxsBytes          txvotepool/txvotepool_test.go:357-413 (TxsBytes, Update, Flush, full)
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+OK, FULL, TOO_LARGE, IN_CACHE, ENCODING = range(5)
+ZERO_TIME = -62135596800          # Go time.Time{} in Unix seconds
+
+
+def vote(sig, txhash=b"AB" * 32, height=1, ts=(1_700_000_000, 5), addr=b"\x01" * 20):
+    return dict(height=height, txhash=txhash, ts_sec=ts[0], ts_nanos=ts[1], addr=addr, sig=sig)
+
+
+def key(sig):
+    return hashlib.sha256(sig).digest()
+
+
+# ------------------------------------------------------------------ oracle vs reference tests
+def test_cache_push_grows_list_and_map(oracle_lib):
+    p = oracle_lib.Pool(cache_size=100)
+    for i in range(10):
+        assert p.check([vote(bytes([i]))])[0] == OK
+        assert len(p.cache_keys()) == i + 1
+    assert [bytes(k) for k in p.cache_keys()] == [key(bytes([i])) for i in range(10)]
+
+
+def test_cache_after_update(oracle_lib):
+    """cache_test.go:36-99 on the code: Update pushes committed keys to the back of the LRU
+    (existing keys move), re-adding after Update is ErrTxInCache and makes no duplicate."""
+    p = oracle_lib.Pool()
+    assert list(p.check([vote(b"\x00"), vote(b"\x01")])) == [OK, OK]
+    p.update(1, [vote(b"\x01")])
+    assert [bytes(k) for k in p.cache_keys()] == [key(b"\x00"), key(b"\x01")]
+    p.update(1, [vote(b"\x02")])
+    assert [bytes(k) for k in p.cache_keys()] == [key(b"\x00"), key(b"\x01"), key(b"\x02")]
+    p.update(1, [vote(b"\x00")])                       # moves 0 to the back
+    assert [bytes(k) for k in p.cache_keys()] == [key(b"\x01"), key(b"\x02"), key(b"\x00")]
+    assert list(p.check([vote(b"\x01")])) == [IN_CACHE]
+    assert len(p.cache_keys()) == 3 and p.size() == 0   # both pooled votes were committed
+    keys, _ = p.reap()
+    assert len(keys) == 0
+
+
+def test_update_adds_txs_to_cache(oracle_lib):
+    """txvotepool_test.go:110-120: Update(0, [TxVote{}]) then CheckTx(TxVote{}) -> ErrTxInCache"""
+    p = oracle_lib.Pool()
+    empty = dict(height=0, txhash=b"", ts_sec=ZERO_TIME, ts_nanos=0, addr=b"", sig=b"")
+    p.update(0, [empty])
+    assert list(p.check([empty])) == [IN_CACHE]
+
+
+def test_serial_reap(oracle_lib):
+    """txvotepool_test.go:166-251 (code semantics): every first CheckTx of a new signature is
+    added, every repeat is ErrTxInCache; after Update(0..500) those votes leave the pool but stay
+    cached; redelivering 900..1100 adds only the 100 new ones."""
+    p = oracle_lib.Pool()
+    sig = lambda i: i.to_bytes(8, "big")
+    st = p.check([vote(sig(i)) for i in range(100)] + [vote(sig(i)) for i in range(100)])
+    assert list(st[:100]) == [OK] * 100 and list(st[100:]) == [IN_CACHE] * 100
+    st = p.check([vote(sig(i)) for i in range(1000)])
+    assert list(st[:100]) == [IN_CACHE] * 100 and list(st[100:]) == [OK] * 900
+    assert p.size() == 1000
+    p.update(3, [vote(sig(i)) for i in range(500)])
+    assert p.size() == 500
+    st = p.check([vote(sig(i)) for i in range(900, 1100)])
+    assert list(st[:100]) == [IN_CACHE] * 100 and list(st[100:]) == [OK] * 100
+    keys, _ = p.reap()
+    assert [bytes(k) for k in keys] == [key(sig(i)) for i in list(range(500, 1000)) + list(range(1000, 1100))]
+    keys, _ = p.reap(9)
+    assert len(keys) == 10                      # ReapMaxTxs loop condition len(txs) <= max
+
+
+def test_max_msg_size(oracle_lib):
+    """txvotepool_test.go:305-355: ErrTxTooLarge exactly when Size() > MaxMsgBytes - 8."""
+    max_msg = 400
+    p = oracle_lib.Pool(max_msg_bytes=max_msg)
+    base = oracle_lib.txvote_size(1, 64, 1_700_000_000, 5, 20, 0)
+    for L in range(max_msg - 8 - base - 6, max_msg - 8 - base + 6):
+        if L < 0:
+            continue
+        sg = bytes([L % 256]) * L + L.to_bytes(4, "little")
+        sz = oracle_lib.txvote_size(1, 64, 1_700_000_000, 5, 20, len(sg))
+        st = p.check([vote(sg)])[0]
+        assert st == (TOO_LARGE if sz > max_msg - 8 else OK), (L, sz)
+
+
+def test_txs_bytes(oracle_lib):
+    """txvotepool_test.go:357-413 (code semantics): TxsBytes = sum of Size(); Update removes;
+    Flush zeroes; ErrMempoolIsFull once MaxTxsBytes would be exceeded."""
+    v1 = vote(b"\x01")
+    sz = oracle_lib.txvote_size(1, 64, 1_700_000_000, 5, 20, 1)
+    p = oracle_lib.Pool(max_txs_bytes=2 * sz + sz // 2)
+    assert p.txs_bytes() == 0
+    assert list(p.check([v1])) == [OK] and p.txs_bytes() == sz
+    p.update(1, [v1])
+    assert p.txs_bytes() == 0
+    assert list(p.check([vote(b"\x02")])) == [OK] and p.txs_bytes() == sz
+    p.flush()
+    assert p.txs_bytes() == 0 and p.size() == 0
+    assert list(p.check([vote(b"\x04"), vote(b"\x05"), vote(b"\x06")])) == [OK, OK, FULL]
+
+
+# ------------------------------------------------------------------ GPU parity
+def _random_stream(rnd, n, n_sigs, long_frac=0.02):
+    votes = []
+    pool_of = [bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 1, 55, 56, 63, 64, 64, 64, 64, 65, 119, 120, 200])))
+               for _ in range(n_sigs)]
+    for i in range(n):
+        s = rnd.choice(pool_of)
+        votes.append(vote(s, txhash=bytes(rnd.choice(b"0123456789ABCDEF") for _ in range(rnd.choice([0, 64, 64, 300]))),
+                          height=rnd.choice([0, 1, 7]),
+                          ts=rnd.choice([(1_700_000_000, i % 1000 + 1), (ZERO_TIME, 0), (0, 0), (10 ** 13, 1)]),
+                          addr=bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 20, 20, 33])))))
+    return votes
+
+
+def _batch(T, votes):
+    vs = [T.TxVote(Height=v["height"], TxHash=v["txhash"], Timestamp=(v["ts_sec"], v["ts_nanos"]),
+                   ValidatorAddress=v["addr"], Signature=v["sig"]) for v in votes]
+    b = T.VoteBatch.from_votes(vs)
+    long_sigs = {i: v["sig"] for i, v in enumerate(votes) if len(v["sig"]) > 64}
+    return b, long_sigs
+
+
+@pytest.mark.gpu
+def test_sig_keys_match_sha256(gpu_ctx):
+    import txflow_amd as T
+    rnd = random.Random(5)
+    votes = [vote(bytes(rnd.getrandbits(8) for _ in range(L))) for L in list(range(0, 131)) * 3]
+    b, long_sigs = _batch(T, votes)
+    keys = gpu_ctx.sig_keys(b, long_sigs)
+    for v, k in zip(votes, keys):
+        assert bytes(k) == key(v["sig"]), len(v["sig"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [dict(size=700, cache_size=300), dict(size=2000, cache_size=0xFFFFFFFF),
+                                 dict(size=100000, cache_size=50, max_txs_bytes=60000, max_msg_bytes=300)],
+                         ids=["small-cache", "no-cache", "byte-limits"])
+def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
+    """Random streams with repeated / empty / long (> 64 B) signatures, zero and out-of-range
+    timestamps, long TxHashes: per-vote CheckTx results, Update, ReapMaxTxs order + sizes,
+    TxsBytes, Size and the LRU order equal the oracle's, across several batches."""
+    import txflow_amd as T
+    rnd = random.Random(hash(tuple(sorted(cfg.items()))) & 0xFFFF)
+    pool = T.TxVotePool(gpu_ctx, **cfg)
+    ref = oracle_lib.Pool(**{k: v for k, v in cfg.items()})
+    try:
+        seen = set()
+        for rnd_batch in range(4):
+            votes = _random_stream(rnd, 1500, 900)
+            b, long_sigs = _batch(T, votes)
+            st = pool.check_batch(b, long_sigs)
+            exp = ref.check(votes)
+            assert np.array_equal(st, exp), np.nonzero(st != exp)[0][:10]
+            committed = rnd.sample(votes, 200)
+            cb, clong = _batch(T, committed)
+            pool.update(rnd_batch + 1, cb, clong)
+            ref.update(rnd_batch + 1, committed)
+            assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+            for m in (-1, 0, 17):
+                gk, gs = pool.reap(m)
+                ok, os_ = ref.reap(m)
+                assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+            assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+            seen |= set(int(x) for x in np.unique(exp))
+        want = {OK, ENCODING, FULL} | ({IN_CACHE} if cfg["cache_size"] != 0xFFFFFFFF else set()) | \
+            ({TOO_LARGE} if "max_msg_bytes" in cfg else set())
+        assert seen >= want, (seen, want)
+        pool.flush(); ref.flush()
+        assert pool.Size() == 0 and pool.TxsBytes() == 0 and len(pool.cache_keys()) == 0
+    finally:
+        pool.close()
