@@ -17,10 +17,13 @@
 #include "../../include/txvote.h"
 #include "amino.hpp"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <sys/mman.h>
 #include <mutex>
 #include <new>
-#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -37,7 +40,88 @@ struct KeyHash {
   }
 };
 
-// doubly linked list in a vector (stable indices), with a key -> node map
+// open-addressing index Key -> node of a KeyList (linear probing, backward-shift deletion, no
+// tombstones).  A slot is 8 bytes (32-bit hash tag + node index; the key itself is compared in
+// the list node), and the table sits on transparent huge pages: the CheckTx loop is bound by
+// one random access per map per vote, so TLB reach and slot size decide its speed.
+struct KeyList;
+struct FlatIndex {
+  struct Slot { uint32_t tag; int32_t idx; };     // tag 0 = empty
+  Slot* t = nullptr;
+  size_t cap = 0, mask = 0, n = 0;
+  const KeyList* owner = nullptr;
+  explicit FlatIndex(const KeyList* o) : owner(o) { alloc(1024); }
+  ~FlatIndex() { free(t); }
+  FlatIndex(const FlatIndex&) = delete;
+  FlatIndex& operator=(const FlatIndex&) = delete;
+  static uint64_t h(const Key& k) { uint64_t v; memcpy(&v, k.b, 8); return v ^ (v >> 29); }
+  static uint32_t tag(uint64_t hv) { return (uint32_t)(hv >> 32) | 1u; }
+  void alloc(size_t c) {
+    const size_t bytes = c * sizeof(Slot);
+    const size_t align = bytes >= (2u << 20) ? (2u << 20) : 64;
+    t = (Slot*)aligned_alloc(align, (bytes + align - 1) / align * align);
+#ifdef MADV_HUGEPAGE
+    if (align == (2u << 20)) madvise(t, bytes, MADV_HUGEPAGE);
+#endif
+    memset(t, 0, bytes);
+    cap = c; mask = c - 1; n = 0;
+  }
+  inline const Key& key_of(int32_t idx) const;
+  void prefetch(const Key& k) const { __builtin_prefetch(&t[h(k) & mask]); }
+  int32_t find(const Key& k) const {
+    const uint64_t hv = h(k);
+    const uint32_t tg = tag(hv);
+    for (size_t i = hv & mask; t[i].tag; i = (i + 1) & mask)
+      if (t[i].tag == tg && key_of(t[i].idx) == k) return t[i].idx;
+    return -1;
+  }
+  void put(const Key& k, int32_t idx) {    // insert or overwrite
+    if ((n + 1) * 2 > cap) grow();
+    const uint64_t hv = h(k);
+    const uint32_t tg = tag(hv);
+    size_t i = hv & mask;
+    for (; t[i].tag; i = (i + 1) & mask)
+      if (t[i].tag == tg && key_of(t[i].idx) == k) { t[i].idx = idx; return; }
+    t[i] = Slot{tg, idx};
+    ++n;
+  }
+  bool erase(const Key& k) {
+    const uint64_t hv = h(k);
+    const uint32_t tg = tag(hv);
+    size_t i = hv & mask;
+    for (; t[i].tag; i = (i + 1) & mask)
+      if (t[i].tag == tg && key_of(t[i].idx) == k) break;
+    if (!t[i].tag) return false;
+    size_t j = i;
+    for (;;) {   // backward shift: entry j moves into hole i iff i lies cyclically in [home(j), j)
+      j = (j + 1) & mask;
+      if (!t[j].tag) break;
+      const size_t home = h(key_of(t[j].idx)) & mask;
+      if (((j - home) & mask) >= ((j - i) & mask)) { t[i] = t[j]; i = j; }
+    }
+    t[i].tag = 0;
+    --n;
+    return true;
+  }
+  void clear() { memset(t, 0, cap * sizeof(Slot)); n = 0; }   // keeps the capacity
+  void reserve(size_t m) { if (m * 2 > cap) { size_t c = cap; while (m * 2 > c) c *= 2; rehash(c); } }
+  void grow() { rehash(cap * 2); }
+  void rehash(size_t c) {
+    Slot* old = t;
+    const size_t oc = cap;
+    alloc(c);
+    for (size_t i = 0; i < oc; ++i)
+      if (old[i].tag) {
+        size_t j = h(key_of(old[i].idx)) & mask;
+        while (t[j].tag) j = (j + 1) & mask;
+        t[j] = old[i];
+        ++n;
+      }
+    free(old);
+  }
+};
+
+// doubly linked list in a vector (stable indices)
 struct KeyList {
   struct Node { Key k; uint32_t size; int32_t prev, next; };
   std::vector<Node> nodes;
@@ -73,6 +157,8 @@ struct KeyList {
   void clear() { nodes.clear(); free_.clear(); head = tail = -1; len = 0; }
 };
 
+inline const Key& FlatIndex::key_of(int32_t idx) const { return owner->nodes[idx].k; }
+
 }  // namespace
 
 struct txv_pool {
@@ -81,21 +167,21 @@ struct txv_pool {
   int64_t height = 0;
   std::mutex mu;                                   // proxyMtx
   KeyList cache;                                   // mapTxCache.list
-  std::unordered_map<Key, int32_t, KeyHash> cache_map;
+  FlatIndex cache_map{&cache};                     // mapTxCache.map_
   KeyList txs;                                     // txs (clist of MempoolTxVote)
-  std::unordered_map<Key, int32_t, KeyHash> txs_map;
+  FlatIndex txs_map{&txs};                         // txsMap
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
-    auto it = cache_map.find(k);
-    if (it != cache_map.end()) { cache.move_to_back(it->second); return false; }
+    const int32_t e = cache_map.find(k);
+    if (e >= 0) { cache.move_to_back(e); return false; }
     if (cache.len >= cfg.cache_size && cache.head >= 0) {
-      cache_map.erase(cache.nodes[cache.head].k);
+      cache_map.erase(cache.nodes[cache.head].k);   // before unlink: the index reads the node's key
       cache.unlink(cache.head);
     }
-    cache_map[k] = cache.push_back(k, 0);
+    cache_map.put(k, cache.push_back(k, 0));
     return true;
   }
 };
@@ -130,6 +216,7 @@ int txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out) {
   p->cache_on = p->cfg.cache_size != TXV_POOL_NO_CACHE;
   p->height = height;
   if (p->cache_on) p->cache_map.reserve(std::min<uint32_t>(p->cfg.cache_size, 1u << 22));
+  p->txs_map.reserve(std::min<uint32_t>(p->cfg.size, 1u << 22));
   *out = p;
   return TXV_OK;
 }
@@ -140,10 +227,18 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
                    const uint64_t* sig_full_off, uint8_t* status_out) {
   if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  const auto t0 = std::chrono::steady_clock::now();
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
+  const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
+  const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
+  constexpr uint32_t kAhead = 16;   // the loop is DRAM-latency bound: prefetch the hash slots ahead
   for (uint32_t i = 0; i < v->n; ++i) {
+    if (i + kAhead < v->n) {
+      if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
+      p->txs_map.prefetch(keys[i + kAhead]);
+    }
     const uint32_t sz = vote_size(v, i);
     if (!sz) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
     if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
@@ -154,9 +249,14 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     Key k;
     memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
     if (!p->cache_push(k)) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
-    p->txs_map[k] = p->txs.push_back(k, sz);        // addTx
+    p->txs_map.put(k, p->txs.push_back(k, sz));     // addTx (txsMap.Store overwrites)
     p->txs_bytes += sz;
     status_out[i] = TXV_POOL_OK;
+  }
+  if (getenv("TXV_PROFILE_HOST")) {
+    const auto t2 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[txv pool] keys=%.3fms lru=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count(), v->n);
   }
   return TXV_OK;
 }
@@ -168,14 +268,19 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
   p->height = height;
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
+  const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
   for (uint32_t i = 0; i < v->n; ++i) {
+    if (i + 16 < v->n) {
+      if (p->cache_on) p->cache_map.prefetch(keys[i + 16]);
+      p->txs_map.prefetch(keys[i + 16]);
+    }
     Key k;
     memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
     (void)p->cache_push(k);
-    auto it = p->txs_map.find(k);
-    if (it != p->txs_map.end()) {                   // removeTx(tx, e, false)
-      p->txs.unlink(it->second);
-      p->txs_map.erase(it);
+    const int32_t e = p->txs_map.find(k);
+    if (e >= 0) {                                   // removeTx(tx, e, false)
+      p->txs_map.erase(k);
+      p->txs.unlink(e);
       p->txs_bytes -= vote_size(v, i);
     }
   }

@@ -17,6 +17,7 @@
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -103,6 +104,7 @@ struct txv_ctx {
   // tally state
   txv_host::TxTable tx_tab{std::random_device{}() * 0x9e3779b97f4a7c15ULL + 0x7478};   // TxHash -> set id
   std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
+  bool profile_host = false;                    // TXV_PROFILE_HOST
   std::vector<int64_t> h_sum;
   std::vector<uint8_t> h_maj;
   std::vector<uint32_t> seen_stage, set_tidx;   // per set: last staging that touched it, its index there
@@ -130,6 +132,23 @@ struct txv_ctx {
   } while (0)
 
 namespace {
+
+// TXV_PROFILE_HOST=1: per-phase wall times of the host pack on stderr
+struct HostTimer {
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  std::string line;
+  explicit HostTimer(bool o) : on(o), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.3fms", what, std::chrono::duration<double, std::milli>(now - t).count());
+    line += b;
+    t = now;
+  }
+  ~HostTimer() { if (on && !line.empty()) fprintf(stderr, "[txv host]%s\n", line.c_str()); }
+};
 
 template <typename T>
 int dalloc(txv_ctx* c, T** p, size_t count) {
@@ -380,6 +399,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   const uint32_t n = v->n;
   const uint8_t* chain = (const uint8_t*)c->chain.data();
   const uint32_t chain_len = (uint32_t)c->chain.size();
+  HostTimer ht(c->profile_host);
   // phase A (parallel): SignBytes lengths, TxHash hashes, validator lookups
   s.lens.resize(n); s.khash.resize(n); s.vidx.resize(n);
   std::atomic<uint32_t> mx{0};
@@ -397,6 +417,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     while (m > cur && !mx.compare_exchange_weak(cur, m)) {}
   });
   const uint32_t mw = std::max<uint32_t>(1, (mx.load() + 7) / 8);
+  ht.mark("A");
   int r = ensure_slot(c, s, n, mw);
   if (r) return r;
   s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
@@ -430,6 +451,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     s.h_status[i] = 0xFF;
     s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
   }
+  ht.mark("B");
   // phase C (parallel): column-major SoA -- signature words, SignBytes as big-endian words
   const uint32_t np = s.n_pad;
   c->pool->parallel_for(np, [&](uint32_t lo, uint32_t hi) {
@@ -455,8 +477,11 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = be64(buf.data() + 8 * w);
     }
   }, 1024);
+  ht.mark("C");
   build_order(s);
+  ht.mark("order");
   if ((r = upload_slot(c, s)) || (r = build_set_order(c, s))) return r;
+  ht.mark("upload+set_order");
   s.staged = true; s.ran = false;
   return TXV_OK;
 }
@@ -705,6 +730,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char* e = getenv("TXV_HOST_THREADS")) nt = (unsigned)std::max(1, std::min(256, atoi(e)));
     c->pool.reset(new txv_host::WorkerPool(nt));
+    c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
   }
   *out = c;
   return TXV_OK;
