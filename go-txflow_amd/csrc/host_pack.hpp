@@ -11,6 +11,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -56,6 +59,12 @@ class WorkerPool {
     for (auto& t : th_) t.join();
   }
   unsigned size() const { return (unsigned)th_.size() + 1; }
+  // pin every worker thread to `set` (the GPU-local NUMA node's CPUs); false if any call failed
+  bool set_affinity(const cpu_set_t& set) {
+    bool ok = true;
+    for (auto& t : th_) ok &= pthread_setaffinity_np(t.native_handle(), sizeof(cpu_set_t), &set) == 0;
+    return ok;
+  }
   // fn(lo, hi) over [0, n) in chunks; the caller thread takes part.  Small n runs inline.
   // Each call is its own Job: a worker still draining an earlier job only sees that job's
   // (exhausted) counters, never the new one's.

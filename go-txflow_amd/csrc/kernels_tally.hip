@@ -18,9 +18,9 @@
 //     signature bytes with the vote at F (DUPLICATE / NONDETERMINISTIC);
 //   * a group whose validator already has an accepted vote from an earlier batch compares
 //     against the arena row of that vote instead;
-//   * the ADDED votes (at most one per validator) are listed; each one's stake prefix in
-//     arrival order is a loop over that short list, the smallest arrival index whose prefix
-//     reaches quorum is the commit crossing, and ADDED votes at or after it fire.
+//   * the ADDED votes (at most one per validator) are listed; the commit crossing (smallest
+//     arrival index whose stake prefix reaches quorum) is found by binary lifting over the
+//     arrival-index bits, one list pass + wave sum per bit; ADDED votes at or after it fire.
 // K2b (arrival order, coalesced) writes the pre-check statuses and copies each ADDED vote's
 // signature into arena row arena_base + i, so K2a's per-set traffic stays contiguous.
 //
@@ -135,30 +135,21 @@ __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
   if (prior >= a.quorum) {
     cross = 0;                                   // already committed: every ADDED vote re-fires
   } else if (total >= a.quorum) {
-    // stake prefix of each listed vote in arrival order: entries are loaded 64 at a time
-    // (coalesced) and broadcast lane by lane with readlane, so the k x k comparison costs no
-    // memory round trips beyond k/64 + (k/64)^2 vector loads
-    uint32_t best = TXV_INF;
-    for (uint32_t cj = 0; cj < k; cj += 64) {
-      const bool hasj = cj + lane < k;
-      const uint32_t ij = hasj ? a.ent_vote[beg + cj + lane] : TXV_INF;
-      int64_t pre = 0;
-      for (uint32_t cl = 0; cl < k; cl += 64) {
-        const bool hasl = cl + lane < k;
-        const uint32_t il = hasl ? a.ent_vote[beg + cl + lane] : TXV_INF;
-        const int64_t pl = hasl ? a.ent_power[beg + cl + lane] : 0;
-        const uint32_t nl = min(64u, k - cl);
-        const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)((uint64_t)pl >> 32);
-        for (uint32_t l = 0; l < nl; ++l) {   // l is wave-uniform: v_readlane into SGPRs
-          const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)il, (int)l);
-          const uint64_t pw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pl_hi, (int)l) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, (int)l);
-          if (fl <= ij) pre += (int64_t)pw;
-        }
-      }
-      if (hasj && prior + pre >= a.quorum) best = min(best, ij);
+    // crossing = the arrival index T at which the stake prefix (in arrival order) first reaches
+    // quorum: with g(t) = stake of listed votes with arrival < t (monotone), T is the largest t
+    // with prior + g(t) < quorum, found by binary lifting over the bits of t; each probe is one
+    // pass over the list (k/64 coalesced, L1-resident loads per lane) and one wave sum, so the
+    // cost is O(k log n) instead of a k x k prefix comparison
+    const int64_t need = a.quorum - prior;
+    uint32_t T = 0;
+    for (int b = 31 - __builtin_clz(max(a.n, 2u) - 1u); b >= 0; --b) {
+      const uint32_t cand = T | (1u << b);
+      int64_t s = 0;
+      for (uint32_t c = lane; c < k; c += 64)
+        if (a.ent_vote[beg + c] < cand) s += a.ent_power[beg + c];
+      if (wave_sum64(s) < need) T = cand;
     }
-    cross = wave_min32(best);
+    cross = T;
   }
 
   // pass 3: ADDED statuses (+ fired bit) and the accepted-vote rows
@@ -183,8 +174,14 @@ __global__ void __launch_bounds__(256) txv_k_tally_finish(TallyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
   const uint8_t pre = a.pre[i];
-  if (pre != TXV_ST_PENDING) { a.status[i] = pre; return; }
-  if ((a.status[i] & 0x7Fu) != TXV_ADDED_DEV) return;
+  if (pre != TXV_ST_PENDING) {
+    a.status[i] = pre;
+    a.status_host[i] = pre;
+    return;
+  }
+  const uint8_t st = a.status[i];
+  a.status_host[i] = st;
+  if ((st & 0x7Fu) != TXV_ADDED_DEV) return;
   // whole 64-byte row per lane in four 16-byte stores
   uint4* dst = reinterpret_cast<uint4*>(a.arena + (size_t)(a.arena_base + i) * 16);
 #pragma unroll

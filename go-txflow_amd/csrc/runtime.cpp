@@ -19,7 +19,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cctype>
 #include <cstdlib>
+#include <sched.h>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -57,12 +59,18 @@ struct Slot {
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
   uint32_t* h_val = nullptr; uint32_t* h_set = nullptr; uint8_t* h_flags = nullptr; uint8_t* h_status = nullptr;
   uint32_t* h_touched = nullptr; int64_t* h_tsum = nullptr; uint8_t* h_tmaj = nullptr; uint32_t* h_tcross = nullptr;
+  // results, written by the tally kernels straight into mapped host memory (m_* = device views)
+  uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
+  int64_t* m_tsum = nullptr; uint8_t* m_tmaj = nullptr; uint32_t* m_tcross = nullptr;
   std::vector<uint8_t> tmp_msg;   // SignBytes arena (verify-only paths)
   std::vector<size_t> tmp_off;
   std::vector<int> lens;           // AddVote pack: SignBytes length (-1 amino error, -2 nil)
   std::vector<uint64_t> khash;     // AddVote pack: seeded hash of the TxHash bytes
   std::vector<uint32_t> vidx;      // AddVote pack: validator index or UINT32_MAX
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // 0..2 kernel timing, 3 = the slot's uploads are done (copy stream), 4 = its results are in
+  // the pinned buffers (compute stream)
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint64_t ticket = 0;    // txv_submit_votes ticket in flight on this slot (0 = none)
 };
 
 }  // namespace
@@ -71,7 +79,10 @@ struct txv_ctx {
   txv_config cfg{};
   int device = 0;
   int n_cus = 256;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;        // compute: verify + tally kernels, result copies
+  hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
+  hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest) runs beside in-flight batches
+  uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   std::string err;
   std::mutex mu;
   // validator registry
@@ -158,10 +169,19 @@ int dalloc(txv_ctx* c, T** p, size_t count) {
   return TXV_OK;
 }
 template <typename T>
-int halloc(txv_ctx* c, T** p, size_t count) {
+int halloc(txv_ctx* c, T** p, size_t count, unsigned flags = hipHostMallocDefault) {
   if (*p) { (void)hipHostFree(*p); *p = nullptr; }
   if (!count) return TXV_OK;
-  HIP_TRY(c, hipHostMalloc((void**)p, count * sizeof(T), hipHostMallocDefault));
+  HIP_TRY(c, hipHostMalloc((void**)p, count * sizeof(T), flags));
+  return TXV_OK;
+}
+// host buffer the kernels write into directly over PCIe (results: no D2H copy to schedule)
+template <typename T>
+int halloc_mapped(txv_ctx* c, T** p, T** dev, size_t count) {
+  int r = halloc(c, p, count, hipHostMallocMapped);
+  if (r) return r;
+  *dev = nullptr;
+  if (*p) HIP_TRY(c, hipHostGetDevicePointer((void**)dev, *p, 0));
   return TXV_OK;
 }
 template <typename T> void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
@@ -194,7 +214,8 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = dalloc(c, &s.d_ent_val, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
-        (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)))
+        (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)) ||
+        (r = halloc_mapped(c, &s.h_out, &s.m_out, npad)))
       return r;
     s.cap = cap;
     s.msg_cap_words = mw;
@@ -203,8 +224,9 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
     int r;
     if ((r = dalloc(c, &s.d_touched, need)) || (r = dalloc(c, &s.d_tsum, need)) || (r = dalloc(c, &s.d_tmaj, need)) ||
         (r = dalloc(c, &s.d_toff, need + 1)) || (r = halloc(c, &s.h_toff, need + 1)) ||
-        (r = dalloc(c, &s.d_tcross, need)) || (r = halloc(c, &s.h_touched, need)) || (r = halloc(c, &s.h_tsum, need)) ||
-        (r = halloc(c, &s.h_tmaj, need)) || (r = halloc(c, &s.h_tcross, need)))
+        (r = dalloc(c, &s.d_tcross, need)) || (r = halloc(c, &s.h_touched, need)) ||
+        (r = halloc_mapped(c, &s.h_tsum, &s.m_tsum, need)) || (r = halloc_mapped(c, &s.h_tmaj, &s.m_tmaj, need)) ||
+        (r = halloc_mapped(c, &s.h_tcross, &s.m_tcross, need)))
       return r;
     s.touched_cap = need;
   }
@@ -298,17 +320,18 @@ void pack_columns(Slot& s, const txv_votes* v, const std::vector<int>& lens) {
 
 int upload_slot(txv_ctx* c, Slot& s) {
   const size_t np = s.n_pad;
-  HIP_TRY(c, hipMemcpyAsync(s.d_sig, s.h_sig, 16 * np * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_msg, s.h_msg, (size_t)s.msg_words * np * 8, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, np * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_val, s.h_val, np * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_flags, s.h_flags, np, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, np, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_sig, s.h_sig, 16 * np * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_msg, s.h_msg, (size_t)s.msg_words * np * 8, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, np * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_val, s.h_val, np * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_flags, s.h_flags, np, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, np, hipMemcpyHostToDevice, c->copy_stream));
   if (s.n_touched)
-    HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->copy_stream));
   if (s.n_work)
-    HIP_TRY(c, hipMemcpyAsync(s.d_order, s.h_order, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_order, s.h_order, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // kernels on c->stream wait for it
   return TXV_OK;
 }
 
@@ -327,11 +350,12 @@ int build_set_order(txv_ctx* c, Slot& s) {
     s.h_tval[p] = s.h_val[i] | ((s.h_flags[i] & TXV_FLAG_SIG64) ? 0x80000000u : 0u) |
                   ((s.h_flags[i] & TXV_FLAG_BADMSG) ? 0x40000000u : 0u);
   }
-  HIP_TRY(c, hipMemcpyAsync(s.d_toff, s.h_toff, (size_t)(s.n_touched + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_toff, s.h_toff, (size_t)(s.n_touched + 1) * 4, hipMemcpyHostToDevice, c->copy_stream));
   if (s.n_work) {
-    HIP_TRY(c, hipMemcpyAsync(s.d_tvote, s.h_tvote, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(s.d_tval, s.h_tval, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_tvote, s.h_tvote, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_tval, s.h_tval, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
   }
+  HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
   return TXV_OK;
 }
 
@@ -387,7 +411,8 @@ TallyArgs tally_args(txv_ctx* c, Slot& s, uint32_t arena_base) {
   a.ent_vote = s.d_ent_vote; a.ent_power = s.d_ent_power; a.ent_val = s.d_ent_val;
   a.acc_slot = c->d_acc_slot; a.arena = c->d_arena;
   a.power = c->d_power; a.set_sum = c->d_set_sum; a.commit_bitmap = c->d_bitmap;
-  a.t_sum = s.d_tsum; a.t_maj = s.d_tmaj; a.t_cross = s.d_tcross;
+  a.t_sum = s.m_tsum; a.t_maj = s.m_tmaj; a.t_cross = s.m_tcross;   // mapped host memory
+  a.status_host = s.m_out;
   return a;
 }
 
@@ -495,6 +520,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   c->arena_used += s.n;
   int r;
   if ((r = ensure_park(c))) return r;
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
@@ -502,6 +528,9 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   TallyArgs ta = tally_args(c, s, arena_base);
   HIP_TRY(c, txv_launch_tally(&ta, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
+  // the tally kernels wrote the statuses and per-set results into mapped host memory (no copy
+  // engine in the loop); fetch_slot only waits for the kernels
+  HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
   s.ran = true;
   if (ms) {
     HIP_TRY(c, hipEventSynchronize(s.ev[2]));
@@ -515,14 +544,11 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
 int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap, uint32_t* n_ev) {
   Slot& s = c->slots[slot];
   if (!s.ran) { c->err = "slot not run"; return TXV_ESTATE; }
-  HIP_TRY(c, hipMemcpyAsync(s.h_status, s.d_status, s.n, hipMemcpyDeviceToHost, c->stream));
-  if (s.n_touched) {
-    HIP_TRY(c, hipMemcpyAsync(s.h_tsum, s.d_tsum, (size_t)s.n_touched * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(s.h_tmaj, s.d_tmaj, s.n_touched, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(s.h_tcross, s.d_tcross, (size_t)s.n_touched * 4, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if (status_out) memcpy(status_out, s.h_status, s.n);
+  HostTimer ht(c->profile_host);
+  HIP_TRY(c, hipEventSynchronize(s.ev[4]));
+  ht.mark("fetch_sync");
+  if (status_out) memcpy(status_out, s.h_out, s.n);
+  ht.mark("fetch_copy");
   uint32_t ne = 0;
   for (uint32_t t = 0; t < s.n_touched; ++t) {
     const uint32_t sid = s.h_touched[t];
@@ -670,6 +696,7 @@ int prepare_keys(txv_ctx* c, const uint8_t* pubs32, uint32_t n, std::vector<uint
 int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) {
   int r;
   if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables);
   const bool reg_w = ks.w == c->tab_w;
   const int w_base = reg_w ? c->b_w : ks.w;
@@ -679,6 +706,36 @@ int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) 
   if (s.n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, s.n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return TXV_OK;
+}
+
+// txv_submit_votes ring: ticket t runs in slot (t - 1) % 2; a slot is reused only after
+// its ticket was waited for (its pinned and device buffers are free again)
+int submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
+  const uint64_t t = c->next_ticket;
+  const uint32_t slot = (uint32_t)((t - 1) % 2);
+  Slot& s = c->slots[slot];
+  if (s.ticket) { c->err = "two batches already in flight: wait for the older one first"; return TXV_ESTATE; }
+  int r;
+  if ((r = stage_add(c, slot, v))) return r;
+  if ((r = run_slot(c, slot, nullptr))) return r;
+  s.ticket = t;
+  c->next_ticket = t + 1;
+  *ticket = t;
+  return TXV_OK;
+}
+
+int wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
+               uint32_t* n_ev) {
+  if (!ticket) return TXV_EINVAL;
+  Slot& s = c->slots[(ticket - 1) % 2];
+  if (s.ticket != ticket) { c->err = "unknown or already waited ticket"; return TXV_ESTATE; }
+  const uint32_t other = (uint32_t)(ticket % 2);   // the other ring slot
+  if (c->slots[other].ticket && c->slots[other].ticket < ticket) {
+    c->err = "tickets must be waited in submission order";
+    return TXV_ESTATE;
+  }
+  s.ticket = 0;
+  return fetch_slot(c, (uint32_t)((ticket - 1) % 2), status_out, ev, ev_cap, n_ev);
 }
 
 }  // namespace
@@ -718,7 +775,9 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (dev < 0) { if (hipGetDevice(&dev) != hipSuccess) dev = 0; }
   if (dev >= ndev) { delete c; return TXV_EINVAL; }
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TXV_EDEVICE;
   }
@@ -740,13 +799,15 @@ void txv_destroy(txv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  if (c->key_stream) (void)hipStreamSynchronize(c->key_stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
     dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_order); hfree(s.h_order);
     dfree(s.d_toff); hfree(s.h_toff); dfree(s.d_tvote); hfree(s.h_tvote); dfree(s.d_tval); hfree(s.h_tval);
     dfree(s.d_ent_vote); dfree(s.d_ent_power); dfree(s.d_ent_val); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
-    hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross);
+    hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross); hfree(s.h_out);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
@@ -755,6 +816,8 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
   dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->key_stream) (void)hipStreamDestroy(c->key_stream);
   delete c;
 }
 
@@ -915,10 +978,25 @@ int txv_add_votes(txv_ctx* c, const txv_votes* v, uint8_t* status_out, txv_commi
   if (!c || !v) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
-  int r;
-  if ((r = stage_add(c, 0, v))) return r;
-  if ((r = run_slot(c, 0, nullptr))) return r;
-  return fetch_slot(c, 0, status_out, ev, ev_cap, n_ev);
+  uint64_t t;
+  int r = submit_votes(c, v, &t);
+  if (r) return r;
+  return wait_votes(c, t, status_out, ev, ev_cap, n_ev);
+}
+
+int txv_submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
+  if (!c || !v || !ticket) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  return submit_votes(c, v, ticket);
+}
+
+int txv_wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
+                   uint32_t* n_ev) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  return wait_votes(c, ticket, status_out, ev, ev_cap, n_ev);
 }
 
 int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23) {
@@ -992,6 +1070,7 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
   vz.sig = zsig.data(); vz.sig_len = zlen.data();
   pack_columns(s, &vz, lens);
   if ((r = upload_slot(c, s))) return r;
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   SignArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val;
   a.prefix = c->d_sk_prefix; a.araw = c->d_sk_araw; a.pub = c->d_sk_pub; a.btable = c->d_btable4; a.sig = s.d_sig;
@@ -1013,7 +1092,7 @@ int txv_stage(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   HIP_TRY(c, hipSetDevice(c->device));
   int r = stage_add(c, slot, v);
   if (r) return r;
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->copy_stream));   // resident before any timed run
   return TXV_OK;
 }
 
@@ -1089,16 +1168,53 @@ int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const 
     memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
     memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
   }, 8192);
-  HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig, c->h_pk_sig, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig, c->h_pk_sig, (size_t)n * 64, hipMemcpyHostToDevice, c->key_stream));
+  HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
+  HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->key_stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->key_stream));
+  HIP_TRY(c, hipStreamSynchronize(c->key_stream));
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
     for (uint32_t i = lo; i < hi; ++i)
       if (v->sig_len[i] > 64) sha256_host(sig_full + sig_full_off[i], v->sig_len[i], keys_out + (size_t)i * 32);
   }, 8192);
+  return TXV_OK;
+}
+
+// CPUs of the NUMA node the GPU hangs off (sysfs local_cpulist of its PCI function)
+static bool gpu_local_cpuset(int dev, cpu_set_t* out) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, dev) != hipSuccess) return false;
+  for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+  std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char line[4096] = {0};
+  const bool got = fgets(line, sizeof line, f) != nullptr;
+  fclose(f);
+  if (!got) return false;
+  CPU_ZERO(out);
+  int n = 0;
+  for (char* tok = strtok(line, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    int a = -1, b = -1;
+    if (sscanf(tok, "%d-%d", &a, &b) == 2) { for (int i = a; i <= b && i < CPU_SETSIZE; ++i) { CPU_SET(i, out); ++n; } }
+    else if (sscanf(tok, "%d", &a) == 1 && a < CPU_SETSIZE) { CPU_SET(a, out); ++n; }
+  }
+  return n > 0;
+}
+
+int txv_bind_host_numa(txv_ctx* c) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  cpu_set_t local, allowed, both;
+  if (!gpu_local_cpuset(c->device, &local)) { c->err = "GPU NUMA locality unknown"; return TXV_ESTATE; }
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) { c->err = "sched_getaffinity failed"; return TXV_ESTATE; }
+  CPU_AND(&both, &local, &allowed);
+  if (CPU_COUNT(&both) == 0) { c->err = "no allowed CPU on the GPU's NUMA node"; return TXV_ESTATE; }
+  if (sched_setaffinity(0, sizeof both, &both) != 0 || !c->pool->set_affinity(both)) {
+    c->err = "setting the CPU affinity failed";
+    return TXV_ESTATE;
+  }
   return TXV_OK;
 }
 

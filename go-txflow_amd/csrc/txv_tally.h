@@ -40,9 +40,10 @@ struct TallyArgs {
   const int64_t* power;         // [n_vals]
   int64_t* set_sum;
   uint32_t* commit_bitmap;
-  int64_t* t_sum;               // [n_touched] outputs
+  int64_t* t_sum;               // [n_touched] outputs (mapped host memory)
   uint8_t* t_maj;
   uint32_t* t_cross;
+  uint8_t* status_host;         // [n] final statuses, mapped host memory (written by K2b)
 };
 
 extern "C" hipError_t txv_launch_tally(const TallyArgs* args, hipStream_t st);

@@ -115,6 +115,9 @@ def lib():
             "txv_table_window": ([vp], ctypes.c_int),
             "txv_base_window": ([vp], ctypes.c_int),
             "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
+            "txv_bind_host_numa": ([vp], ctypes.c_int),
+            "txv_submit_votes": ([vp, ctypes.POINTER(_Votes), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_wait_votes": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
             "txv_pool_free": ([vp], None),
             "txv_pool_check": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
@@ -140,6 +143,7 @@ EXPORTED_SYMBOLS = [
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
+    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys"]
 
@@ -353,6 +357,25 @@ class Context:
                                       ctypes.byref(nev)), "txv_add_votes")
         return out[:batch.n], evs[:min(nev.value, ev_cap)]
 
+    def submit_votes(self, batch: VoteBatch) -> int:
+        """asynchronous TryAddVote batch (txv_submit_votes): returns a ticket for wait_votes"""
+        t = ctypes.c_uint64()
+        vs = batch.c_struct()
+        self._chk(lib().txv_submit_votes(self._h, ctypes.byref(vs), ctypes.byref(t)), "txv_submit_votes")
+        self._inflight = getattr(self, "_inflight", {})
+        self._inflight[t.value] = batch.n
+        return t.value
+
+    def wait_votes(self, ticket: int, ev_cap: int = 0):
+        n = self._inflight.pop(ticket)
+        out = np.zeros(max(n, 1), np.uint8)
+        ev_cap = ev_cap or max(n, 1)
+        evs = np.zeros(ev_cap, EVENT_DTYPE)
+        nev = ctypes.c_uint32()
+        self._chk(lib().txv_wait_votes(self._h, ticket, out.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev)),
+                  "txv_wait_votes")
+        return out[:n], evs[:min(nev.value, ev_cap)]
+
     def query_tx(self, txhash: bytes):
         s = ctypes.c_int64(); m = ctypes.c_uint8()
         r = self._chk(lib().txv_query_tx(self._h, txhash, len(txhash), ctypes.byref(s), ctypes.byref(m)), "query")
@@ -428,6 +451,10 @@ class Context:
 
     def reset_tally(self):
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")
+
+    def bind_host_numa(self) -> bool:
+        """pin this thread and the library's pack threads to the GPU-local NUMA node (True on success)"""
+        return lib().txv_bind_host_numa(self._h) == 0
 
     def reset_flow(self):
         """forget every TxVoteSet (a fresh TxFlow, txflow/service.go:71); validators stay"""

@@ -166,6 +166,17 @@ int txv_verify_bytes(txv_ctx* ctx, const uint8_t* pubs32, const uint8_t* msgs, c
 int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
                   txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev);
 
+/* txv_add_votes split for pipelining (north_star: pinned SoA batches uploaded on a side stream):
+ * txv_submit_votes packs the batch on the host, queues its upload on the copy stream and its
+ * verify + tally kernels and result copies on the compute stream, and returns a ticket without
+ * waiting; txv_wait_votes(ticket) waits for those results and reports exactly what txv_add_votes
+ * would have.  At most two batches may be in flight; tickets are waited in submission order.
+ * The host pack of batch k+1 (and its upload) overlaps the kernels of batch k.  TxVoteSet
+ * readers (txv_query_tx) reflect a batch once it has been waited for. */
+int txv_submit_votes(txv_ctx* ctx, const txv_votes* votes, uint64_t* ticket);
+int txv_wait_votes(txv_ctx* ctx, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev_out, uint32_t ev_cap,
+                   uint32_t* n_ev);
+
 /* Tally readers for the TxVoteSet of txhash.  Returns 1 if the set exists, 0 if not. */
 int txv_query_tx(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23);
 uint32_t txv_num_tx_sets(txv_ctx* ctx);
@@ -210,6 +221,10 @@ int txv_reset_tally(txv_ctx* ctx);
  * txflow/service.go:71), keeping the validator set and its tables */
 int txv_reset_flow(txv_ctx* ctx);
 int txv_sync(txv_ctx* ctx);
+/* bind the calling thread and the library's host pack threads to the CPUs of the NUMA node the
+ * GPU is attached to (sysfs local_cpulist), so the pinned batch buffers and the pack run next to
+ * the GPU's PCIe root; TXV_ESTATE when the locality is unknown or no such CPU is allowed */
+int txv_bind_host_numa(txv_ctx* ctx);
 
 /* ---- TxVotePool ingest (txvotepool/txvotepool.go) ----
  * Long signatures: txv_votes.sig holds the first 64 bytes of each signature.  Calls taking

@@ -325,3 +325,35 @@ def test_c4_adversarial_stream_gate(oracle_lib):
         assert st["by_status"].get("ErrVoteInvalidSignature", 0) > 0 and st["events"] > 0
     finally:
         ctx.close()
+
+
+def test_pipelined_submit_wait_matches_oracle(oracle_lib):
+    """txv_submit_votes / txv_wait_votes with two batches in flight (uploads on the copy stream
+    overlapping the previous batch's kernels) give exactly the sequential oracle's per-vote
+    codes, fire bits and per-tx sums on a C4 adversarial stream (replays / conflicts across
+    batches); waiting out of order is refused."""
+    import adversarial as A
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 16, max_txs=1 << 14, max_validators=256)
+    try:
+        s = A.C4Stream(ctx, batch=20000, batches_per_epoch=8, oracle_threads=8)
+        batches = [s.next_batch()[0] for _ in range(5)]
+        exp = []
+        for b in batches:
+            st, _, fired = s.flow.add_batch(b, 8)
+            exp.append(st.astype(np.uint8) | (fired.astype(np.uint8) << 7))
+        got, inflight = [], []
+        for b in batches:
+            if len(inflight) == 2:
+                got.append(ctx.wait_votes(inflight.pop(0))[0])
+            inflight.append(ctx.submit_votes(b))
+            if len(inflight) == 2 and len(got) == 0:
+                with pytest.raises(T.TxvInfraError):
+                    ctx.submit_votes(b)          # a third batch in flight is refused
+        while inflight:
+            got.append(ctx.wait_votes(inflight.pop(0))[0])
+        for g, e in zip(got, exp):
+            assert np.array_equal(g, e), np.nonzero(g != e)[0][:10]
+        assert s.check_sets() == 0
+    finally:
+        ctx.close()
