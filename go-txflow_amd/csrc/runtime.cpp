@@ -64,6 +64,13 @@ struct Slot {
   int64_t* m_tsum = nullptr; uint8_t* m_tmaj = nullptr; uint32_t* m_tcross = nullptr;
   std::vector<uint8_t> tmp_msg;   // SignBytes arena (verify-only paths)
   std::vector<size_t> tmp_off;
+  // device SignBytes inputs (kernels_signbytes.hip): pinned staging + device copies
+  int64_t *h_fh = nullptr, *h_fs = nullptr, *d_fh = nullptr, *d_fs = nullptr;     // height, ts_sec
+  int32_t *h_fn = nullptr, *d_fn = nullptr;                                        // ts_nanos
+  uint32_t *h_fo = nullptr, *h_fl = nullptr, *d_fo = nullptr, *d_fl = nullptr;     // txhash off / len
+  uint8_t *h_arena = nullptr, *d_arena_th = nullptr;                               // TxHash arena
+  size_t arena_cap = 0;
+  bool msg_on_device = false;      // this staging's SignBytes are built by txv_k_signbytes
   std::vector<int> lens;           // AddVote pack: SignBytes length (-1 amino error, -2 nil)
   std::vector<uint64_t> khash;     // AddVote pack: seeded hash of the TxHash bytes
   std::vector<uint32_t> vidx;      // AddVote pack: validator index or UINT32_MAX
@@ -91,6 +98,8 @@ struct txv_ctx {
   std::vector<int64_t> powers;
   int64_t total = 0, quorum = 0;
   std::string chain;
+  uint8_t* d_chain = nullptr; uint32_t d_chain_cap = 0;             // chain id for txv_k_signbytes
+  uint8_t* d_chain_sign = nullptr; uint32_t d_chain_sign_cap = 0;   // txv_sign_votes' chain id
   std::unordered_map<std::string, uint32_t> addr_index;
   txv_host::AddrTable addr_tab;    // same map, lock-free reads for the parallel pack
   uint32_t* d_pubs = nullptr; uint8_t* d_decode_ok = nullptr; uint32_t* d_atables = nullptr;
@@ -215,7 +224,11 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
         (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)) ||
-        (r = halloc_mapped(c, &s.h_out, &s.m_out, npad)))
+        (r = halloc_mapped(c, &s.h_out, &s.m_out, npad)) ||
+        (r = halloc(c, &s.h_fh, npad)) || (r = halloc(c, &s.h_fs, npad)) || (r = halloc(c, &s.h_fn, npad)) ||
+        (r = halloc(c, &s.h_fo, npad)) || (r = halloc(c, &s.h_fl, npad)) || (r = dalloc(c, &s.d_fh, npad)) ||
+        (r = dalloc(c, &s.d_fs, npad)) || (r = dalloc(c, &s.d_fn, npad)) || (r = dalloc(c, &s.d_fo, npad)) ||
+        (r = dalloc(c, &s.d_fl, npad)))
       return r;
     s.cap = cap;
     s.msg_cap_words = mw;
@@ -291,6 +304,7 @@ uint32_t encode_all(txv_ctx* c, Slot& s, const txv_votes* v, const char* chain, 
 // column-major transposes into the slot's pinned buffers
 void pack_columns(Slot& s, const txv_votes* v, const std::vector<int>& lens) {
   const uint32_t n = v->n, np = s.n_pad, mw = s.msg_words;
+  s.msg_on_device = false;
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t* sg = v->sig + (size_t)i * 64;
     const uint32_t sl = v->sig_len[i] > 64 ? 64 : v->sig_len[i];
@@ -321,7 +335,8 @@ void pack_columns(Slot& s, const txv_votes* v, const std::vector<int>& lens) {
 int upload_slot(txv_ctx* c, Slot& s) {
   const size_t np = s.n_pad;
   HIP_TRY(c, hipMemcpyAsync(s.d_sig, s.h_sig, 16 * np * 4, hipMemcpyHostToDevice, c->copy_stream));
-  HIP_TRY(c, hipMemcpyAsync(s.d_msg, s.h_msg, (size_t)s.msg_words * np * 8, hipMemcpyHostToDevice, c->copy_stream));
+  if (!s.msg_on_device)
+    HIP_TRY(c, hipMemcpyAsync(s.d_msg, s.h_msg, (size_t)s.msg_words * np * 8, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, np * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_val, s.h_val, np * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->copy_stream));
@@ -417,21 +432,71 @@ TallyArgs tally_args(txv_ctx* c, Slot& s, uint32_t arena_base) {
 }
 
 // stage for the AddVote path: routing, pre-checks, SignBytes, pack, upload
+// Device SignBytes for slot s: stage the raw fields + the TxHash arena prefix
+// [0, arena_end) into pinned buffers (parallel), upload them on the copy stream and build the
+// column-major message words there with txv_k_signbytes.  s.h_msg_len must be set already.
+int encode_signbytes_device(txv_ctx* c, Slot& s, const txv_votes* v, const uint8_t* d_chain, uint32_t chain_len,
+                            uint64_t arena_end) {
+  const uint32_t n = s.n, np = s.n_pad;
+  if (arena_end + 1 > s.arena_cap) {
+    int r;
+    const size_t cap = std::max<size_t>((size_t)arena_end + 1, s.arena_cap * 2);
+    if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
+    s.arena_cap = cap;
+  }
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    memcpy(s.h_fh + lo, v->height + lo, (size_t)(hi - lo) * 8);
+    memcpy(s.h_fs + lo, v->ts_sec + lo, (size_t)(hi - lo) * 8);
+    memcpy(s.h_fn + lo, v->ts_nanos + lo, (size_t)(hi - lo) * 4);
+    memcpy(s.h_fo + lo, v->txhash_off + lo, (size_t)(hi - lo) * 4);
+    memcpy(s.h_fl + lo, v->txhash_len + lo, (size_t)(hi - lo) * 4);
+  }, 16384);
+  if (arena_end) memcpy(s.h_arena, v->txhash, (size_t)arena_end);
+  HIP_TRY(c, hipMemcpyAsync(s.d_fh, s.h_fh, (size_t)n * 8, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_fs, s.h_fs, (size_t)n * 8, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_fn, s.h_fn, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_fo, s.h_fo, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_fl, s.h_fl, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
+  if (arena_end) HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, (size_t)arena_end, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, (size_t)np * 4, hipMemcpyHostToDevice, c->copy_stream));
+  SignBytesArgs a{};
+  a.n = n; a.n_pad = np; a.msg_words = s.msg_words; a.chain_len = chain_len;
+  a.height = s.d_fh; a.ts_sec = s.d_fs; a.ts_nanos = s.d_fn; a.txhash_off = s.d_fo; a.txhash_len = s.d_fl;
+  a.txhash = s.d_arena_th; a.chain = d_chain; a.msg_len = s.d_msg_len; a.msg = s.d_msg;
+  HIP_TRY(c, txv_launch_signbytes(&a, c->copy_stream));
+  s.msg_on_device = true;
+  return TXV_OK;
+}
+
+// txv_set_validators / txv_sign_votes chain ids on the device
+int upload_chain(txv_ctx* c, const char* chain, uint32_t len, uint8_t** d, uint32_t* cap) {
+  if (len + 1 > *cap) {
+    int r;
+    if ((r = dalloc(c, d, (size_t)len + 1))) return r;
+    *cap = len + 1;
+  }
+  if (len) HIP_TRY(c, hipMemcpyAsync(*d, chain, len, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
+  return TXV_OK;
+}
+
 int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
   Slot& s = c->slots[slot];
   const uint32_t n = v->n;
-  const uint8_t* chain = (const uint8_t*)c->chain.data();
   const uint32_t chain_len = (uint32_t)c->chain.size();
   HostTimer ht(c->profile_host);
   // phase A (parallel): SignBytes lengths, TxHash hashes, validator lookups
   s.lens.resize(n); s.khash.resize(n); s.vidx.resize(n);
   std::atomic<uint32_t> mx{0};
+  std::atomic<uint64_t> arena_end{0};
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     uint32_t m = 0;
+    uint64_t ae = 0;
     for (uint32_t i = lo; i < hi; ++i) {
       if (v->is_nil && v->is_nil[i]) { s.lens[i] = -2; continue; }
+      ae = std::max<uint64_t>(ae, (uint64_t)v->txhash_off[i] + v->txhash_len[i]);
       const int L = txv_host::sign_bytes_len(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], chain_len);
       s.lens[i] = L;
       if (L > 0 && (uint32_t)L > m) m = (uint32_t)L;
@@ -440,6 +505,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     }
     uint32_t cur = mx.load();
     while (m > cur && !mx.compare_exchange_weak(cur, m)) {}
+    uint64_t ca = arena_end.load();
+    while (ae > ca && !arena_end.compare_exchange_weak(ca, ae)) {}
   });
   const uint32_t mw = std::max<uint32_t>(1, (mx.load() + 7) / 8);
   ht.mark("A");
@@ -477,14 +544,13 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
   }
   ht.mark("B");
-  // phase C (parallel): column-major SoA -- signature words, SignBytes as big-endian words
+  // phase C (parallel): column-major signature words and lengths; the SignBytes words are
+  // built on the device (encode_signbytes_device)
   const uint32_t np = s.n_pad;
   c->pool->parallel_for(np, [&](uint32_t lo, uint32_t hi) {
-    std::vector<uint8_t> buf((size_t)mw * 8 + 8);
     for (uint32_t i = lo; i < hi; ++i) {
       if (i >= n) {
         for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = 0;
-        for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = 0;
         s.h_msg_len[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0; s.h_flags[i] = 0; s.h_status[i] = TXV_ERR_NIL;
         continue;
       }
@@ -493,18 +559,13 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       memset(sg, 0, 64);
       memcpy(sg, v->sig + (size_t)i * 64, sl);
       for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = le32(sg + 4 * j);
-      const int L = s.lens[i];
-      s.h_msg_len[i] = L > 0 ? (uint32_t)L : 0;
-      std::fill(buf.begin(), buf.end(), 0);
-      if (L > 0)
-        txv_host::sign_bytes(buf.data(), (uint32_t)L, v->height[i], v->txhash + v->txhash_off[i], v->txhash_len[i],
-                             v->ts_sec[i], v->ts_nanos[i], chain, chain_len);
-      for (uint32_t w = 0; w < mw; ++w) s.h_msg[(size_t)w * np + i] = be64(buf.data() + 8 * w);
+      s.h_msg_len[i] = s.lens[i] > 0 ? (uint32_t)s.lens[i] : 0;
     }
   }, 1024);
   ht.mark("C");
   build_order(s);
   ht.mark("order");
+  if ((r = encode_signbytes_device(c, s, v, c->d_chain, chain_len, arena_end.load()))) return r;
   if ((r = upload_slot(c, s)) || (r = build_set_order(c, s))) return r;
   ht.mark("upload+set_order");
   s.staged = true; s.ran = false;
@@ -808,12 +869,15 @@ void txv_destroy(txv_ctx* c) {
     dfree(s.d_ent_vote); dfree(s.d_ent_power); dfree(s.d_ent_val); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
     hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross); hfree(s.h_out);
+    hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
+    dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_acc_slot); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_bitmap);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
+  dfree(c->d_chain); dfree(c->d_chain_sign);
   dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -844,6 +908,10 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   for (uint32_t i = 0; i < n; ++i) c->total += powers[i];
   c->quorum = c->total * 2 / 3 + 1;
   c->chain.assign(chain_id ? chain_id : "", chain_id ? chain_len : 0);
+  {
+    int rr = upload_chain(c, c->chain.data(), (uint32_t)c->chain.size(), &c->d_chain, &c->d_chain_cap);
+    if (rr) return rr;
+  }
   int r;
   if ((r = select_window(c, choose_window(c, n)))) return r;
   if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
@@ -1055,21 +1123,29 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
   for (uint32_t i = 0; i < v->n; ++i)
     if (signer[i] >= c->n_signers) { c->err = "signer index out of range"; return TXV_EINVAL; }
   Slot& s = c->slots[kSlots - 2];
-  std::vector<int> lens;
-  const uint32_t mx = encode_all(c, s, v, chain_id, chain_len, lens);
+  // SignBytes are built on the device (txv_k_signbytes), the same encoder the AddVote path uses
+  std::vector<int> lens(v->n);
+  uint32_t mx = 0;
+  uint64_t ae = 0;
+  for (uint32_t i = 0; i < v->n; ++i) {
+    if (v->is_nil && v->is_nil[i]) { lens[i] = -2; continue; }
+    lens[i] = txv_host::sign_bytes_len(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], chain_len);
+    if (lens[i] > 0) mx = std::max(mx, (uint32_t)lens[i]);
+    ae = std::max<uint64_t>(ae, (uint64_t)v->txhash_off[i] + v->txhash_len[i]);
+  }
   const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
   int r = ensure_slot(c, s, v->n, mw);
   if (r) return r;
-  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
-  for (uint32_t i = 0; i < v->n; ++i) { s.h_val[i] = signer[i]; s.h_flags[i] = 0; s.h_set[i] = 0; s.h_status[i] = 0; }
-  // sig columns are outputs; pack zeros for them (pack_columns copies caller sig bytes, so
-  // supply a zero signature view)
-  std::vector<uint8_t> zsig((size_t)v->n * 64, 0);
-  std::vector<uint32_t> zlen(v->n, 64);
-  txv_votes vz = *v;
-  vz.sig = zsig.data(); vz.sig_len = zlen.data();
-  pack_columns(s, &vz, lens);
-  if ((r = upload_slot(c, s))) return r;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0; s.n_work = 0;
+  for (uint32_t i = 0; i < s.n_pad; ++i) {
+    const bool in = i < v->n;
+    s.h_val[i] = in ? signer[i] : 0; s.h_flags[i] = 0; s.h_set[i] = 0; s.h_status[i] = 0;
+    s.h_msg_len[i] = in && lens[i] > 0 ? (uint32_t)lens[i] : 0;
+    for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * s.n_pad + i] = 0;
+  }
+  if ((r = upload_chain(c, chain_id, chain_len, &c->d_chain_sign, &c->d_chain_sign_cap)) ||
+      (r = encode_signbytes_device(c, s, v, c->d_chain_sign, chain_len, ae)) || (r = upload_slot(c, s)))
+    return r;
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   SignArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val;

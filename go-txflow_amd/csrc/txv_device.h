@@ -40,6 +40,20 @@ struct VerifyArgs {
 #define TXV_PARK_WORDS 32          // X, Y, prefix product, Z of one parked vote
 #define TXV_MAX_LANE_VOTES 4
 
+// TxVote.SignBytes on the device (kernels_signbytes.hip): fields in, msg words out
+struct SignBytesArgs {
+  uint32_t n, n_pad, msg_words, chain_len;
+  const int64_t* height;       // [n]
+  const int64_t* ts_sec;       // [n]
+  const int32_t* ts_nanos;     // [n]
+  const uint32_t* txhash_off;  // [n] into txhash
+  const uint32_t* txhash_len;  // [n]
+  const uint8_t* txhash;       // TxHash arena
+  const uint8_t* chain;        // [chain_len]
+  const uint32_t* msg_len;     // [n] SignBytes length, 0 = none (nil / amino error)
+  uint64_t* msg;               // [msg_words][n_pad] out
+};
+
 struct SignArgs {
   uint32_t n, n_pad, msg_words, pad0;
   const uint64_t* msg;         // [msg_words][n_pad]
@@ -62,6 +76,7 @@ hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_
                              uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
 hipError_t txv_launch_valu_probe(int op, uint32_t* out, uint32_t blocks, int iters, hipStream_t st);
+hipError_t txv_launch_signbytes(const SignBytesArgs* args, hipStream_t st);
 hipError_t txv_launch_sig_keys(const uint32_t* sig, const uint32_t* sig_len, uint32_t n, uint32_t* keys,
                                 hipStream_t st);
 hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,

@@ -19,6 +19,7 @@
  *   Pinned by txvotepool/txvotepool_test.go:102 (Size()==114 for a 20-byte-tx vote).
  */
 #include "oracle.h"
+#include <stdlib.h>
 #include <string.h>
 
 #define AMINO_MIN_SEC (-62135596800LL)
@@ -52,9 +53,9 @@ static int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
 int orc_signbytes(int64_t height, const uint8_t* txhash, size_t txhash_len,
                   int64_t ts_sec, int32_t ts_nanos,
                   const uint8_t* chain_id, size_t chain_len, uint8_t* out, size_t out_cap) {
-  uint8_t body[1024];
+  uint8_t* body = (uint8_t*)malloc(txhash_len + chain_len + 128);
   size_t n = 0;
-  if (txhash_len > 512 || chain_len > 256) return -1;
+  if (!body) return -1;
   if (height != 0) {
     body[n++] = 0x09;
     for (int i = 0; i < 8; ++i) body[n++] = (uint8_t)((uint64_t)height >> (8 * i));
@@ -68,7 +69,7 @@ int orc_signbytes(int64_t height, const uint8_t* txhash, size_t txhash_len,
   memset(body + n, 0, 32); n += 32;
   uint8_t tb[32];
   int tl = time_body(tb, ts_sec, ts_nanos);
-  if (tl < 0) return -1;
+  if (tl < 0) { free(body); return -1; }
   if (tl > 0) {
     body[n++] = 0x22;
     n += uvarint(body + n, (uint64_t)tl);
@@ -80,9 +81,10 @@ int orc_signbytes(int64_t height, const uint8_t* txhash, size_t txhash_len,
     memcpy(body + n, chain_id, chain_len); n += chain_len;
   }
   size_t pl = uvarint(0, n);
-  if (pl + n > out_cap) return -1;
+  if (pl + n > out_cap) { free(body); return -1; }
   uvarint(out, n);
   memcpy(out + pl, body, n);
+  free(body);
   return (int)(pl + n);
 }
 

@@ -357,3 +357,49 @@ def test_pipelined_submit_wait_matches_oracle(oracle_lib):
         assert s.check_sets() == 0
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("chain", [b"", b"c", b"test_chain_id", b"x" * 127, b"y" * 128, b"z" * 300])
+def test_device_signbytes_edge_fields(gpu_ctx, oracle_lib, chain):
+    """txv_k_signbytes byte-exact with the oracle's amino encoder on edge fields:
+    Height 0 / negative / extremes (omitted field, 8-byte LE), Timestamp at the epoch (omitted),
+    negative and extreme seconds (10-byte uvarint), nanos 0 / max, TxHash lengths across uvarint
+    and word boundaries, chain ids of 0..300 bytes.  Checked through the device signer (which
+    hashes the device-built SignBytes) against RFC 8032 signatures of the oracle's bytes, and
+    through the AddVote path (the same votes must verify)."""
+    import txflow_amd as T
+    rnd = random.Random(len(chain) + 7)
+    seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(3)]
+    pubs = gpu_ctx.keygen(seeds)
+    heights = [0, 1, -1, 2 ** 63 - 1, -2 ** 63, 127, 128, 1 << 40]
+    secs = [0, 1, -1, -62135596800, 253402300799, 1_700_000_000, 2 ** 35]
+    nanos = [0, 1, 999_999_999, 127, 128]
+    hlens = [0, 1, 7, 8, 63, 64, 127, 128, 200, 300]
+    votes, signer = [], []
+    for i in range(240):
+        h = rnd.choice(heights)
+        ts = (rnd.choice(secs), rnd.choice(nanos))
+        th = "".join(rnd.choice("0123456789ABCDEF") for _ in range(rnd.choice(hlens)))
+        votes.append(T.TxVote(Height=h, TxHash=th, Timestamp=ts, ValidatorAddress=b""))
+        signer.append(i % 3)
+    b = T.VoteBatch.from_votes(votes)
+    sigs = gpu_ctx.sign_votes(b, np.array(signer, np.uint32), chain.decode())
+    for i, v in enumerate(votes):
+        msg = oracle_lib.signbytes(v.Height, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], chain)
+        assert msg is not None
+        assert sigs[i].tobytes() == oracle_lib.sign(seeds[signer[i]], msg), (i, v)
+    # the AddVote path builds the same bytes: every vote verifies and is ADDED (one per tx+val)
+    ctx = T.Context(max_batch=1 << 12, max_txs=1 << 10, max_validators=8, table_w=8)
+    try:
+        ctx.set_validators(pubs, [1, 1, 1], chain.decode())
+        addrs, _ = ctx.validator_info()
+        for v, s, k in zip(votes, sigs, signer):
+            v.ValidatorAddress = addrs[k]
+            v.Signature = s.tobytes()
+        st, _ = ctx.add_votes(T.VoteBatch.from_votes(votes))
+        ok = (st & 0x7F)
+        assert set(np.unique(ok)) <= {T.ADDED, T.DUPLICATE, T.ERR_NONDETERMINISTIC}, np.unique(ok)
+        assert np.count_nonzero(ok == T.ADDED) > 0
+        assert not np.any(ok == T.ERR_INVALID_SIGNATURE)
+    finally:
+        ctx.close()
