@@ -125,6 +125,54 @@ class WorkerPool {
   bool stop_ = false;
 };
 
+// ------------------------------------------------------------------ parallel stable counting sort
+// Items [0, n) with key(i) in [0, K) (UINT32_MAX = drop) are scattered by emit(pos, i) into key
+// order, arrival order kept inside each key: per-chunk histograms (contiguous chunks), one
+// exclusive scan over (key, chunk), per-chunk scatter.  Returns the number of items kept;
+// starts (optional, K + 1 entries) receives each key's first position.
+template <class KeyF, class EmitF>
+uint32_t counting_sort(WorkerPool& pool, uint32_t n, uint32_t K, KeyF key, EmitF emit, uint32_t* starts = nullptr) {
+  const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(pool.size() * 2, n / 8192));
+  std::vector<uint32_t> hist((size_t)P * K, 0);
+  auto range = [&](uint32_t p, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)((uint64_t)n * p / P); hi = (uint32_t)((uint64_t)n * (p + 1) / P);
+  };
+  pool.parallel_for(P, [&](uint32_t p0, uint32_t p1) {
+    for (uint32_t p = p0; p < p1; ++p) {
+      uint32_t lo, hi;
+      range(p, lo, hi);
+      uint32_t* hp = hist.data() + (size_t)p * K;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t k = key(i);
+        if (k != UINT32_MAX) hp[k]++;
+      }
+    }
+  }, 1);
+  uint32_t run = 0;
+  for (uint32_t k = 0; k < K; ++k) {
+    if (starts) starts[k] = run;
+    for (uint32_t p = 0; p < P; ++p) {
+      uint32_t& c = hist[(size_t)p * K + k];
+      const uint32_t t = c;
+      c = run;
+      run += t;
+    }
+  }
+  if (starts) starts[K] = run;
+  pool.parallel_for(P, [&](uint32_t p0, uint32_t p1) {
+    for (uint32_t p = p0; p < p1; ++p) {
+      uint32_t lo, hi;
+      range(p, lo, hi);
+      uint32_t* hp = hist.data() + (size_t)p * K;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t k = key(i);
+        if (k != UINT32_MAX) emit(hp[k]++, i);
+      }
+    }
+  }, 1);
+  return run;
+}
+
 // ------------------------------------------------------------------ TxHash -> set id
 class TxTable {
  public:

@@ -353,18 +353,15 @@ int upload_slot(txv_ctx* c, Slot& s) {
 // set-major tally order (AddVote path): stable counting sort of the validator-sorted pending
 // votes (h_order) by touched-set index gives (set, validator, arrival) order
 int build_set_order(txv_ctx* c, Slot& s) {
-  uint32_t* off = s.h_toff;
-  std::fill(off, off + s.n_touched + 1, 0u);
-  for (uint32_t q = 0; q < s.n_work; ++q) off[c->set_tidx[s.h_set[s.h_order[q]]] + 1]++;
-  for (uint32_t t = 0; t < s.n_touched; ++t) off[t + 1] += off[t];
-  std::vector<uint32_t> cur(off, off + s.n_touched);
-  for (uint32_t q = 0; q < s.n_work; ++q) {
-    const uint32_t i = s.h_order[q];
-    const uint32_t p = cur[c->set_tidx[s.h_set[i]]]++;
-    s.h_tvote[p] = i;
-    s.h_tval[p] = s.h_val[i] | ((s.h_flags[i] & TXV_FLAG_SIG64) ? 0x80000000u : 0u) |
-                  ((s.h_flags[i] & TXV_FLAG_BADMSG) ? 0x40000000u : 0u);
-  }
+  // stable by touched-set index over the validator-sorted pending votes
+  txv_host::counting_sort(*c->pool, s.n_work, s.n_touched,
+      [&](uint32_t q) { return c->set_tidx[s.h_set[s.h_order[q]]]; },
+      [&](uint32_t p, uint32_t q) {
+        const uint32_t i = s.h_order[q];
+        s.h_tvote[p] = i;
+        s.h_tval[p] = s.h_val[i] | ((s.h_flags[i] & TXV_FLAG_SIG64) ? 0x80000000u : 0u) |
+                      ((s.h_flags[i] & TXV_FLAG_BADMSG) ? 0x40000000u : 0u);
+      }, s.h_toff);
   HIP_TRY(c, hipMemcpyAsync(s.d_toff, s.h_toff, (size_t)(s.n_touched + 1) * 4, hipMemcpyHostToDevice, c->copy_stream));
   if (s.n_work) {
     HIP_TRY(c, hipMemcpyAsync(s.d_tvote, s.h_tvote, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
@@ -376,17 +373,11 @@ int build_set_order(txv_ctx* c, Slot& s) {
 
 // Counting sort of the pending votes by validator: K1b then runs waves whose lanes mostly
 // share one validator's A table (L1/L2-resident gathers instead of scattered MALL reads).
-void build_order(Slot& s) {
-  uint32_t n_keys = 0;
-  for (uint32_t i = 0; i < s.n; ++i)
-    if ((s.h_flags[i] & TXV_FLAG_PENDING) && s.h_val[i] + 1 > n_keys) n_keys = s.h_val[i] + 1;
-  std::vector<uint32_t> cnt((size_t)n_keys + 1, 0);
-  for (uint32_t i = 0; i < s.n; ++i)
-    if (s.h_flags[i] & TXV_FLAG_PENDING) cnt[s.h_val[i] + 1]++;
-  for (uint32_t k = 0; k < n_keys; ++k) cnt[k + 1] += cnt[k];
-  s.n_work = cnt[n_keys];
-  for (uint32_t i = 0; i < s.n; ++i)
-    if (s.h_flags[i] & TXV_FLAG_PENDING) s.h_order[cnt[s.h_val[i]]++] = i;
+// keys = validator (or caller-key) index < n_keys
+void build_order(txv_ctx* c, Slot& s, uint32_t n_keys) {
+  s.n_work = txv_host::counting_sort(*c->pool, s.n, std::max<uint32_t>(n_keys, 1),
+      [&](uint32_t i) { return (s.h_flags[i] & TXV_FLAG_PENDING) ? s.h_val[i] : UINT32_MAX; },
+      [&](uint32_t p, uint32_t i) { s.h_order[p] = i; });
 }
 
 uint32_t verify_grid(txv_ctx* c, uint32_t n) {
@@ -563,11 +554,14 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     }
   }, 1024);
   ht.mark("C");
-  build_order(s);
+  build_order(c, s, c->n_vals);
   ht.mark("order");
   if ((r = encode_signbytes_device(c, s, v, c->d_chain, chain_len, arena_end.load()))) return r;
-  if ((r = upload_slot(c, s)) || (r = build_set_order(c, s))) return r;
-  ht.mark("upload+set_order");
+  ht.mark("signbytes");
+  if ((r = upload_slot(c, s))) return r;
+  ht.mark("upload");
+  if ((r = build_set_order(c, s))) return r;
+  ht.mark("set_order");
   s.staged = true; s.ran = false;
   return TXV_OK;
 }
@@ -959,10 +953,12 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   if (r) return r;
   s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
   KeySet ks = registry_keys(c);
+  uint32_t n_keys = c->n_vals;
   if (pubs32) {
     std::vector<uint32_t> kidx;
     std::vector<uint8_t> key_addr;
     if ((r = prepare_keys(c, pubs32, v->n, kidx, &key_addr, ks))) return r;
+    n_keys = (uint32_t)(key_addr.size() / 20);
     for (uint32_t i = 0; i < v->n; ++i) {
       s.h_flags[i] = 0; s.h_set[i] = 0; s.h_val[i] = kidx[i];
       if (v->is_nil && v->is_nil[i]) { s.h_status[i] = TXV_ERR_NIL; continue; }
@@ -988,7 +984,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
       s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
     }
   }
-  build_order(s);
+  build_order(c, s, n_keys);
   pack_columns(s, v, lens);
   std::vector<uint8_t> ok;
   if ((r = run_verify(c, s, ks, ok))) return r;
@@ -1031,7 +1027,7 @@ int txv_verify_bytes(txv_ctx* c, const uint8_t* pubs32, const uint8_t* msgs, con
     s.h_set[i] = 0; s.h_val[i] = kidx[i]; s.h_status[i] = 0xFF;
     s.h_flags[i] = TXV_FLAG_PENDING | (sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0);
   }
-  build_order(s);
+  build_order(c, s, kidx.empty() ? 1u : *std::max_element(kidx.begin(), kidx.end()) + 1);
   txv_votes view{};
   view.n = n; view.sig = sigs64; view.sig_len = sig_len;
   pack_columns(s, &view, lens);

@@ -70,6 +70,27 @@ int main(int argc, char** argv) {
     miss[19] ^= 1;
     if (a.find(miss) != UINT32_MAX) return fail("addr miss", 0, 1);
   }
+  // counting_sort: stable by key, dropped keys skipped, key starts
+  {
+    WorkerPool pool(8);
+    std::mt19937_64 rng(11);
+    for (int it = 0; it < 4; ++it) {
+      const uint32_t n = (uint32_t)(rng() % 120000), K = 1 + (uint32_t)(rng() % 700);
+      std::vector<uint32_t> key(n);
+      for (auto& k : key) k = (rng() % 7 == 0) ? UINT32_MAX : (uint32_t)(rng() % K);
+      std::vector<uint32_t> out(n, 0xdead), starts(K + 1);
+      const uint32_t m = counting_sort(pool, n, K, [&](uint32_t i) { return key[i]; },
+                                       [&](uint32_t p, uint32_t i) { out[p] = i; }, starts.data());
+      std::vector<std::vector<uint32_t>> byk(K);
+      for (uint32_t i = 0; i < n; ++i) if (key[i] != UINT32_MAX) byk[key[i]].push_back(i);
+      uint32_t p = 0;
+      for (uint32_t k = 0; k < K; ++k) {
+        if (starts[k] != p) return fail("sort starts", starts[k], p);
+        for (uint32_t i : byk[k]) if (out[p++] != i) return fail("sort order", out[p - 1], i);
+      }
+      if (m != p || starts[K] != p) return fail("sort count", m, p);
+    }
+  }
   printf("ok\n");
   return 0;
 }
