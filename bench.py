@@ -157,19 +157,24 @@ def main():
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl = RCCL over xGMI (the measured path); gloo = CPU-side rehearsal of the N>1 "
+                         "code path (with --same-gpu, several ranks on one GPU)")
+    ap.add_argument("--same-gpu", action="store_true", help="every rank uses device 0 (rehearsal only)")
     ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    gloo = args.dist_backend == "gloo"
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")   # RCCL over xGMI
+        dist.init_process_group(args.dist_backend)   # nccl = RCCL over xGMI
 
     import txflow_amd as T
     from txflow_amd.workload import Workload, SEEDS
@@ -192,7 +197,18 @@ def main():
     if dist is not None:
         import torch
         bm_local = torch.zeros(bm_bytes // 4, dtype=torch.int32, device=f"cuda:{local}")
-        gathered = torch.zeros(world * (bm_bytes // 4), dtype=torch.int32, device=f"cuda:{local}")
+        gathered = torch.zeros(world * (bm_bytes // 4), dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
+    red_dev = "cpu" if gloo else f"cuda:{local}"
+
+    def all_gather_bitmaps():
+        """per-shard commit bitmaps -> every rank (RCCL all-gather; gloo: through host tensors)"""
+        ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)
+        if gloo:
+            torch.cuda.synchronize()
+            dist.all_gather(list(gathered.chunk(world)), bm_local.cpu())
+        else:
+            dist.all_gather_into_tensor(gathered, bm_local)
+            torch.cuda.synchronize()
 
     step_ms, verify_ms, tally_ms = [], [], []
 
@@ -209,9 +225,7 @@ def main():
         st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf, evs=ev_buf)
         t3 = time.perf_counter()
         if dist is not None:
-            ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)
-            dist.all_gather_into_tensor(gathered, bm_local)
-            torch.cuda.synchronize()
+            all_gather_bitmaps()
         t4 = time.perf_counter()
         if record:
             step_ms.append((t4 - t0) * 1e3)
@@ -247,10 +261,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        nv = torch.tensor([wl.n], dtype=torch.int64, device=f"cuda:{local}")
+        nv = torch.tensor([wl.n], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nv)
         total_votes = int(nv.item())
     else:
