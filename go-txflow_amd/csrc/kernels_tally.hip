@@ -190,6 +190,26 @@ __global__ void __launch_bounds__(256) txv_k_tally_finish(TallyArgs a) {
                         a.sig[(size_t)(4 * q + 2) * a.n_pad + i], a.sig[(size_t)(4 * q + 3) * a.n_pad + i]);
 }
 
+// TxVoteSet.GetVotes / GetByAddress readers: per validator of one set, the accepted vote's
+// arena row (0 = none) and its signature bytes
+__global__ void __launch_bounds__(256) txv_k_set_votes(const uint32_t* __restrict__ acc_row, uint32_t n_vals,
+                                                       const uint32_t* __restrict__ arena, uint32_t* __restrict__ rows,
+                                                       uint32_t* __restrict__ sigs) {
+  const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= n_vals) return;
+  const uint32_t slot = acc_row[v];
+  rows[v] = slot;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) sigs[(size_t)v * 16 + j] = slot ? arena[(size_t)(slot - 1) * 16 + j] : 0u;
+}
+
+extern "C" hipError_t txv_launch_set_votes(const uint32_t* acc_row, uint32_t n_vals, const uint32_t* arena, uint32_t* rows,
+                                           uint32_t* sigs, hipStream_t st) {
+  if (!n_vals) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_set_votes, dim3((n_vals + 255) / 256), dim3(256), 0, st, acc_row, n_vals, arena, rows, sigs);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t txv_launch_tally(const TallyArgs* args, hipStream_t st) {
   if (!args->n) return hipSuccess;
   if (args->n_touched)

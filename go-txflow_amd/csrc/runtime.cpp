@@ -1074,6 +1074,40 @@ int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, 
   return 1;
 }
 
+int txv_get_votes(txv_ctx* c, const uint8_t* txhash, uint32_t len, uint32_t* val_out, uint64_t* seq_out,
+                  uint8_t* sig_out, uint32_t cap, uint32_t* n_out) {
+  if (!c || (!txhash && len) || !n_out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  *n_out = 0;
+  const uint32_t sid = c->tx_tab.find(txhash, len, c->tx_tab.hash(txhash, len));
+  if (sid == UINT32_MAX || !c->n_vals) return TXV_OK;
+  uint32_t *d_rows = nullptr, *d_sigs = nullptr;
+  int r;
+  if ((r = dalloc(c, &d_rows, c->n_vals)) || (r = dalloc(c, &d_sigs, (size_t)c->n_vals * 16))) { dfree(d_rows); return r; }
+  std::vector<uint32_t> rows(c->n_vals), sigs((size_t)c->n_vals * 16);
+  // stream order: after every batch already submitted on this context
+  hipError_t e = txv_launch_set_votes(c->d_acc_slot + (size_t)sid * c->n_vals, c->n_vals, c->d_arena, d_rows, d_sigs,
+                                      c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d_rows, (size_t)c->n_vals * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(sigs.data(), d_sigs, (size_t)c->n_vals * 64, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d_rows); dfree(d_sigs);
+  HIP_TRY(c, e);
+  uint32_t k = 0;
+  for (uint32_t v = 0; v < c->n_vals; ++v) {
+    if (!rows[v]) continue;
+    if (k < cap) {
+      if (val_out) val_out[k] = v;
+      if (seq_out) seq_out[k] = rows[v] - 1;
+      if (sig_out) memcpy(sig_out + (size_t)k * 64, sigs.data() + (size_t)v * 16, 64);
+    }
+    ++k;
+  }
+  *n_out = k;
+  return TXV_OK;
+}
+
 uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? c->tx_tab.size() : 0; }
 int64_t txv_total_power(txv_ctx* c) { return c ? c->total : 0; }
 

@@ -47,3 +47,5 @@ struct TallyArgs {
 };
 
 extern "C" hipError_t txv_launch_tally(const TallyArgs* args, hipStream_t st);
+extern "C" hipError_t txv_launch_set_votes(const uint32_t* acc_row, uint32_t n_vals, const uint32_t* arena, uint32_t* rows,
+                                           uint32_t* sigs, hipStream_t st);

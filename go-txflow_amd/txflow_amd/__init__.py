@@ -116,6 +116,7 @@ def lib():
             "txv_base_window": ([vp], ctypes.c_int),
             "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
             "txv_bind_host_numa": ([vp], ctypes.c_int),
+            "txv_get_votes": ([vp, ctypes.c_char_p, u32, vp, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_submit_votes": ([vp, ctypes.POINTER(_Votes), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_wait_votes": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
@@ -143,7 +144,7 @@ EXPORTED_SYMBOLS = [
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
-    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa",
+    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys"]
 
@@ -375,6 +376,18 @@ class Context:
         self._chk(lib().txv_wait_votes(self._h, ticket, out.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev)),
                   "txv_wait_votes")
         return out[:n], evs[:min(nev.value, ev_cap)]
+
+    def get_votes(self, txhash: bytes):
+        """TxVoteSet.GetVotes: [(validator index, vote sequence number, signature bytes)] in
+        validator order"""
+        n = ctypes.c_uint32()
+        self._chk(lib().txv_get_votes(self._h, txhash, len(txhash), None, None, None, 0, ctypes.byref(n)), "get_votes")
+        k = n.value
+        vals = np.zeros(max(k, 1), np.uint32); seqs = np.zeros(max(k, 1), np.uint64)
+        sigs = np.zeros((max(k, 1), 64), np.uint8)
+        self._chk(lib().txv_get_votes(self._h, txhash, len(txhash), vals.ctypes.data, seqs.ctypes.data,
+                                      sigs.ctypes.data, k, ctypes.byref(n)), "get_votes")
+        return [(int(vals[j]), int(seqs[j]), sigs[j].tobytes()) for j in range(k)]
 
     def query_tx(self, txhash: bytes):
         s = ctypes.c_int64(); m = ctypes.c_uint8()

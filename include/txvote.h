@@ -19,6 +19,7 @@
  *                         types/vote_set.go:81-131, addVerifiedVote :143-166
  *   txv_query_tx       <- TxVoteSet.Stake / HasTwoThirdsMajority / HasTwoThirdsAny / HasAll
  *                         types/vote_set.go:178-227
+ *   txv_get_votes      <- TxVoteSet.GetVotes / GetByAddress types/vote_set.go:57-64, 169-176
  *   txv_set_validators <- NewTxVoteSet(chainID, height, txHash, txKey, valSet)
  *                         types/vote_set.go:34-51 (state.ChainID / state.Validators, txflow/service.go:200-209)
  *   txv_signbytes      <- func (vote *TxVote) SignBytes(chainID string) []byte   types/tx_vote.go:83-89
@@ -176,6 +177,17 @@ int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
 int txv_submit_votes(txv_ctx* ctx, const txv_votes* votes, uint64_t* ticket);
 int txv_wait_votes(txv_ctx* ctx, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev_out, uint32_t ev_cap,
                    uint32_t* n_ev);
+
+/* TxVoteSet.GetVotes / GetByAddress (types/vote_set.go:57-64, :169-176) for the set of txhash,
+ * e.g. for the commit side effects (MakeCommit :242-259, TxVotePool.Update with GetVotes(),
+ * txflow/service.go:222-226): the accepted vote of every validator that has one, in validator
+ * index order (the reference iterates a Go map: unordered), as val_out[k] = validator index,
+ * seq_out[k] = the vote's sequence number (count of votes passed to txv_add_votes /
+ * txv_submit_votes / txv_run_staged since the last txv_reset_* before it + its index in its
+ * batch), sig_out[k] = its 64 signature bytes.  *n_out = count (entries beyond cap are not
+ * written).  Reflects every batch submitted so far. */
+int txv_get_votes(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, uint32_t* val_out, uint64_t* seq_out,
+                  uint8_t* sig_out, uint32_t cap, uint32_t* n_out);
 
 /* Tally readers for the TxVoteSet of txhash.  Returns 1 if the set exists, 0 if not. */
 int txv_query_tx(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23);

@@ -116,6 +116,10 @@ void orc_txvote_verify_soa(const orc_soa* batch, const uint8_t* pubs32, const ui
 /* Query a TxVoteSet: returns 0 if the tx has no set, else 1 and fills sum/maj23. */
 int orc_flow_query(orc_flow*, const uint8_t* txhash, uint32_t txhash_len, int64_t* sum, int32_t* maj23);
 uint32_t orc_flow_num_sets(orc_flow*);
+/* TxVoteSet.GetVotes (types/vote_set.go:57-64) in validator index order: count of accepted votes;
+ * val_out / sig_out (64 B each) receive up to cap of them */
+uint32_t orc_flow_get_votes(orc_flow*, const uint8_t* txhash, uint32_t len, uint32_t* val_out, uint8_t* sig_out,
+                            uint32_t cap);
 /* count of ed25519 verifications performed (for baseline accounting) */
 uint64_t orc_flow_num_verifies(orc_flow*);
 

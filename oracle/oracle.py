@@ -67,6 +67,9 @@ def lib():
         L.orc_pool_txs_bytes.argtypes = [ctypes.c_void_p]
         L.orc_pool_cache_keys.restype = ctypes.c_uint64
         L.orc_pool_cache_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_flow_get_votes.restype = ctypes.c_uint32
+        L.orc_flow_get_votes.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32]
         L.orc_flow_query.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_uint32,
                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]
         L.orc_flow_num_sets.argtypes = [ctypes.c_void_p]
@@ -249,6 +252,15 @@ class Flow:
         s = ctypes.c_int64(); m = ctypes.c_int32()
         ok = lib().orc_flow_query(self._h, txhash, len(txhash), ctypes.byref(s), ctypes.byref(m))
         return (s.value, bool(m.value)) if ok else None
+
+    def get_votes(self, txhash: bytes):
+        """TxVoteSet.GetVotes in validator order: [(validator index, signature bytes)]"""
+        np = self._np
+        n = lib().orc_flow_get_votes(self._h, txhash, len(txhash), None, None, 0)
+        vals = np.zeros(max(n, 1), np.uint32)
+        sigs = np.zeros((max(n, 1), 64), np.uint8)
+        lib().orc_flow_get_votes(self._h, txhash, len(txhash), vals.ctypes.data, sigs.ctypes.data, n)
+        return [(int(vals[j]), sigs[j].tobytes()) for j in range(n)]
 
     def num_sets(self):
         return lib().orc_flow_num_sets(self._h)

@@ -331,5 +331,22 @@ int orc_flow_query(orc_flow* f, const uint8_t* txhash, uint32_t len, int64_t* su
   if (maj23) *maj23 = f->set_maj23[s];
   return 1;
 }
+uint32_t orc_flow_get_votes(orc_flow* f, const uint8_t* txhash, uint32_t len, uint32_t* val_out, uint8_t* sig_out,
+                            uint32_t cap) {
+  int64_t s = find_set(f, txhash, len);
+  if (s < 0) return 0;
+  uint32_t k = 0;
+  for (uint32_t v = 0; v < f->n_vals; ++v) {
+    acc_sig* a = acc_find(f, ((uint64_t)(s + 1) << 32) | v);
+    if (!a) continue;
+    if (k < cap) {
+      if (val_out) val_out[k] = v;
+      if (sig_out) memcpy(sig_out + 64 * (size_t)k, a->sig, 64);
+    }
+    ++k;
+  }
+  return k;
+}
+
 uint32_t orc_flow_num_sets(orc_flow* f) { return f->n_sets; }
 uint64_t orc_flow_num_verifies(orc_flow* f) { return f->n_verifies; }

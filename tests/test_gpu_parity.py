@@ -355,6 +355,18 @@ def test_pipelined_submit_wait_matches_oracle(oracle_lib):
         for g, e in zip(got, exp):
             assert np.array_equal(g, e), np.nonzero(g != e)[0][:10]
         assert s.check_sets() == 0
+        # TxVoteSet.GetVotes: same accepted (validator, signature) per set as the oracle, and each
+        # sequence number points at that vote in the submitted stream
+        base = np.cumsum([0] + [b.n for b in batches])
+        for j in range(0, s.epoch_txs, max(1, s.epoch_txs // 50)):
+            h = s.hashes[j].tobytes()
+            gv = ctx.get_votes(h)
+            ov = s.flow.get_votes(h)
+            assert [(v, sg) for v, _, sg in gv] == ov
+            for v, seq, sg in gv:
+                bi = int(np.searchsorted(base, seq, side="right") - 1)
+                b, i = batches[bi], int(seq - base[bi])
+                assert b.sig[64 * i:64 * i + 64].tobytes() == sg and b.txhash(i) == h
     finally:
         ctx.close()
 
