@@ -192,22 +192,27 @@ def main():
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
         f"staged in {time.perf_counter() - t_setup:.1f}s")
 
+    # per-shard commit state all-gathered every step: the commit bitmap of the shard's
+    # set ids and their stake sums, packed in one buffer -> one RCCL all-gather over xGMI
     bm_ptr, bm_bytes = ctx.commit_bitmap()
     gathered = None
     if dist is not None:
         import torch
-        bm_local = torch.zeros(bm_bytes // 4, dtype=torch.int32, device=f"cuda:{local}")
-        gathered = torch.zeros(world * (bm_bytes // 4), dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
+        cap = 2 * args.txs_per_gpu                    # local set ids (shards are ~txs_per_gpu each)
+        bm_words = (cap + 31) // 32
+        state = torch.zeros(bm_words + 2 * cap, dtype=torch.int32, device=f"cuda:{local}")
+        gathered = torch.zeros(world * state.numel(), dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
     red_dev = "cpu" if gloo else f"cuda:{local}"
 
     def all_gather_bitmaps():
-        """per-shard commit bitmaps -> every rank (RCCL all-gather; gloo: through host tensors)"""
-        ctx.copy_commit_bitmap(bm_local.data_ptr(), bm_bytes)
+        """per-shard commit bitmap + stake sums -> every rank (RCCL all-gather; gloo: host tensors)"""
+        ctx.copy_commit_bitmap(state.data_ptr(), 4 * bm_words)
+        ctx.copy_set_sums(state.data_ptr() + 4 * bm_words, cap)
         if gloo:
             torch.cuda.synchronize()
-            dist.all_gather(list(gathered.chunk(world)), bm_local.cpu())
+            dist.all_gather(list(gathered.chunk(world)), state.cpu())
         else:
-            dist.all_gather_into_tensor(gathered, bm_local)
+            dist.all_gather_into_tensor(gathered, state)
             torch.cuda.synchronize()
 
     step_ms, verify_ms, tally_ms = [], [], []
@@ -249,6 +254,16 @@ def main():
         sys.exit(2)
 
     if dist is not None:
+        # the gathered global state: every tx of every shard committed with the full stake
+        g = gathered.cpu().view(world, -1)
+        bits = int(sum(bin(int(w) & 0xFFFFFFFF).count("1") for w in g[:, :bm_words].flatten().tolist()))
+        sums = g[:, bm_words:].contiguous().view(torch.int64)
+        nt = torch.tensor([wl.n_txs], dtype=torch.int64, device=red_dev)
+        dist.all_reduce(nt)
+        committed_sums = int((sums == ctx.total_power()).sum())
+        if bits != int(nt.item()) or committed_sums != bits:
+            log(f"[rank {rank}] GATHER CHECK FAILURE: {bits} commit bits / {committed_sums} full sums for {int(nt.item())} txs")
+            sys.exit(3)
         dist.barrier()
         torch.cuda.synchronize()
     ctx.sync()
@@ -316,7 +331,7 @@ def main():
             "data": "synthetic: device-signed ed25519 TxVotes (RFC 8032), SURVEY.md §8d seeds",
             "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
                                     f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
-                                    f"100 validators, ~1M votes/GPU, RCCL bitmap all-gather"),
+                                    f"100 validators, ~1M votes/GPU, RCCL all-gather of commit bitmaps + stake sums"),
                        "validators": args.validators, "table_window": ctx.table_w, "base_window": ctx.base_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
                        "parallelism": f"shard{world}", "host_numa_bound": numa},
             "p50_batch_ms": round(statistics.median(step_ms), 3),

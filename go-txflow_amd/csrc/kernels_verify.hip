@@ -108,8 +108,11 @@ __device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, 
   return true;
 }
 
-// K1a: challenges of every pending vote into kbuf (99 VGPRs: 5 waves/SIMD)
-__global__ void __launch_bounds__(256, 4) txv_k_challenge(VerifyArgs a) {
+// K1a: challenges of every pending vote into kbuf
+#ifndef TXV_K1A_WAVES
+#define TXV_K1A_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, TXV_K1A_WAVES) txv_k_challenge(VerifyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
   if (!(a.flags[i] & TXV_FLAG_PENDING)) return;

@@ -1348,6 +1348,16 @@ int txv_copy_commit_bitmap(txv_ctx* c, void* dst_dev, uint64_t bytes) {
   return TXV_OK;
 }
 
+int txv_copy_set_sums(txv_ctx* c, void* dst_dev, uint32_t n_sets) {
+  if (!c || (!dst_dev && n_sets)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t n = std::min(n_sets, c->cfg.max_txs);
+  if (n) HIP_TRY(c, hipMemcpyAsync(dst_dev, c->d_set_sum, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
 int txv_valu_probe(txv_ctx* c, double* add_lane_ops_per_s, double* mad_lane_ops_per_s) {
   if (!c) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);

@@ -21,6 +21,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libtxvote.so")
+if os.environ.get("TXV_LIB_PATH"):          # experiment builds (tools/); the product default is in-tree
+    LIB_PATH = os.environ["TXV_LIB_PATH"]
 
 # status codes (include/txvote.h)
 ADDED, DUPLICATE, ERR_NIL, ERR_EMPTY_ADDR, ERR_UNKNOWN_VALIDATOR, ERR_NONDETERMINISTIC, \
@@ -116,6 +118,7 @@ def lib():
             "txv_base_window": ([vp], ctypes.c_int),
             "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
             "txv_bind_host_numa": ([vp], ctypes.c_int),
+            "txv_copy_set_sums": ([vp, vp, u32], ctypes.c_int),
             "txv_get_votes": ([vp, ctypes.c_char_p, u32, vp, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_submit_votes": ([vp, ctypes.POINTER(_Votes), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_wait_votes": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
@@ -144,7 +147,7 @@ EXPORTED_SYMBOLS = [
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
-    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes",
+    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys"]
 
@@ -445,6 +448,9 @@ class Context:
 
     def copy_commit_bitmap(self, dst_dev_ptr: int, nbytes: int):
         self._chk(lib().txv_copy_commit_bitmap(self._h, ctypes.c_void_p(dst_dev_ptr), nbytes), "bitmap copy")
+
+    def copy_set_sums(self, dst_dev_ptr: int, n_sets: int):
+        self._chk(lib().txv_copy_set_sums(self._h, ctypes.c_void_p(dst_dev_ptr), n_sets), "set sums copy")
 
     def valu_probe(self):
         """(v_add_u32, v_mad_u64_u32) lane-ops/s measured on this device"""

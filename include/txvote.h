@@ -220,6 +220,9 @@ int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commi
 int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 /* device-to-device copy of the commit bitmap into caller device memory (e.g. an RCCL buffer) */
 int txv_copy_commit_bitmap(txv_ctx* ctx, void* dst_dev, uint64_t bytes);
+/* device-to-device copy of the per-set stake sums (int64, set ids 0..n_sets-1) into caller device
+ * memory: with the commit bitmap, the per-shard state a multi-GPU run all-gathers */
+int txv_copy_set_sums(txv_ctx* ctx, void* dst_dev, uint32_t n_sets);
 /* measured integer-VALU issue rates of this device (lane-ops/s): v_add_u32 and v_mad_u64_u32 */
 int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
 /* fixed-base window of the current validator tables (4..16), 0 before txv_set_validators */
