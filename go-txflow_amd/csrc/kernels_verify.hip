@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
 // needed 272 VGPRs = 1 wave/SIMD):
 //   K1a txv_k_challenge   per vote: length / top-bit / s < L / decode checks, k = SHA-512(R||A||M) mod L
 //                         -> k[8][n_pad] (32 B/vote, HBM) and the "go" flag in ok_out
-//   K1b txv_k_scalarmult  per vote, in validator-grouped order: [s]B + [k](-A), encode, compare with R
+//   K1b txv_k_scalarmult  per vote (validator-grouped list for w <= 12, arrival order above): [s]B + [k](-A), encode, compare with R
 
 // Prechecks + challenge of vote i: false if the vote is rejected before the group equation
 // (length, sig[63] & 0xE0, undecodable A, s >= L, SignBytes failure), else k = SHA-512(R||A||M)
@@ -115,7 +115,7 @@ __device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, 
 __global__ void __launch_bounds__(256, TXV_K1A_WAVES) txv_k_challenge(VerifyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
-  if (!(a.flags[i] & TXV_FLAG_PENDING)) return;
+  if (!(a.flags[i] & TXV_FLAG_PENDING)) { a.ok_out[i] = 0; return; }   // K1b may walk every vote
   uint32_t k[8], s[8];
   if (!vote_challenge(a, i, k, s)) { a.ok_out[i] = 0; return; }
 #pragma unroll
@@ -236,12 +236,16 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 // fills 4 waves/SIMD in one round for a 1M-vote batch on 256 CUs.
 template <int BLOCK, int WB, int WA, int V>
 __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
-  const uint32_t n_grp = (a.n_work + V - 1) / V;
+  // lane group g = 64 w + l takes the work-list entries 64 V w + 64 h + l (h < V): the lanes of
+  // a wave read 64 consecutive entries per vote slot, so the vote-column reads (sig, kbuf) of an
+  // arrival-ordered list are two lines per column per wave
+  const uint32_t n_grp = (a.n_work + 64u * V - 1u) / (64u * V) * 64u;
   // XCD-aware split as in the pair kernel: the blocks of one XCD walk one contiguous
-  // eighth of the validator-sorted work list (its A tables stay in that XCD's L2).
+  // eighth of the work list (with a validator-sorted list its A tables stay in that XCD's L2);
+  // the eighths are whole waves' worth of groups
   const uint32_t groups = gridDim.x >= 8 ? 8u : 1u;
   const uint32_t grp = blockIdx.x % groups, blocks_in_grp = gridDim.x / groups + (grp < gridDim.x % groups);
-  const uint32_t chunk = (n_grp + groups - 1) / groups;
+  const uint32_t chunk = ((n_grp + groups - 1) / groups + 63u) & ~63u;
   const uint32_t lo = grp * chunk, hi = min(n_grp, lo + chunk);
   const uint32_t stride = blocks_in_grp * BLOCK;
   // park layout: [wave][slot h][word][64 lanes]: a wave's stores of one word are one
@@ -252,7 +256,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
     uint32_t act = 0;
 #pragma unroll
     for (int h = 0; h < V; ++h) {
-      const uint32_t idx = V * g + h;
+      const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
       if (idx < a.n_work && a.ok_out[a.order ? a.order[idx] : idx] == 2) act |= 1u << h;
     }
     if (!act) continue;
@@ -261,7 +265,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
 #pragma unroll 1
     for (int h = 0; h < V; ++h) {
       if (act >> h & 1u) {
-        const uint32_t idx = V * g + h;
+        const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
         const uint32_t i = a.order ? a.order[idx] : idx;
         uint32_t s[8], k[8];
 #pragma unroll
@@ -308,7 +312,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
         zi = inv;
       }
       if (act >> h & 1u) {
-        const uint32_t idx = V * g + h;
+        const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
         const uint32_t i = a.order ? a.order[idx] : idx;
         uint32_t enc[8];
         ge_encode_zinv(enc, X, Y, zi);

@@ -371,9 +371,9 @@ int build_set_order(txv_ctx* c, Slot& s) {
   return TXV_OK;
 }
 
-// Counting sort of the pending votes by validator: K1b then runs waves whose lanes mostly
-// share one validator's A table (L1/L2-resident gathers instead of scattered MALL reads).
-// keys = validator (or caller-key) index < n_keys
+// Counting sort of the pending votes by validator (keys = validator or caller-key index <
+// n_keys).  The tally's set-major order is built from it; K1b walks it only with the small
+// tables (verify_args).
 void build_order(txv_ctx* c, Slot& s, uint32_t n_keys) {
   s.n_work = txv_host::counting_sort(*c->pool, s.n, std::max<uint32_t>(n_keys, 1),
       [&](uint32_t i) { return (s.h_flags[i] & TXV_FLAG_PENDING) ? s.h_val[i] : UINT32_MAX; },
@@ -386,12 +386,20 @@ uint32_t verify_grid(txv_ctx* c, uint32_t n) {
   return std::max<uint32_t>(1, std::min(blocks, cap));
 }
 
-VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t* dok, const uint32_t* tabs) {
+// K1b's work list.  With the small tables (w <= 12: at most 4.3 MB per validator) it is the
+// validator-sorted pending list, so the lanes of a wave mostly share one validator's A table
+// (L2-resident gathers).  With wider tables a validator's table is tens to hundreds of MB and
+// every gather misses L2 whatever the order, while the validator order scatters the vote-column
+// reads (sig, kbuf: 24 words per vote at a stride of ~n_vals votes) over 24 distinct lines per
+// vote (measured at w = 20: 59 L2 line misses per vote, 36 of them table lines); there K1b walks
+// the votes in arrival order (order = null, n_work = n; K1a marks non-pending votes ok = 0).
+VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t* dok, const uint32_t* tabs, int w) {
   VerifyArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words;
   a.sig = s.d_sig; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val; a.flags = s.d_flags;
-  a.n_work = s.n_work; a.kbuf = s.d_kbuf;
-  a.order = s.d_order; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
+  const bool by_val = w <= 12;
+  a.n_work = by_val || !s.n_work ? s.n_work : s.n; a.kbuf = s.d_kbuf;
+  a.order = by_val ? s.d_order : nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
   a.park = c->d_park;
   a.lane_votes = c->lane_votes;
@@ -577,7 +585,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   if ((r = ensure_park(c))) return r;
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
-  VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables);
+  VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
   TallyArgs ta = tally_args(c, s, arena_base);
@@ -752,7 +760,7 @@ int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) 
   int r;
   if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
-  VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables);
+  VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables, ks.w);
   const bool reg_w = ks.w == c->tab_w;
   const int w_base = reg_w ? c->b_w : ks.w;
   va.btable = reg_w ? c->d_btable : (ks.w == 4 ? c->d_btable4 : c->d_btable8);

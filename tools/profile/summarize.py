@@ -5,7 +5,10 @@ usage: python tools/profile/summarize.py gpurun_out/<tag> [--votes N] [--out pro
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KB per dispatch;
 on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so the corrected read
-bytes are 2 x FETCH_SIZE x 1024 (the raw value is kept beside it).
+bytes are 2 x FETCH_SIZE x 1024 (the raw value is kept beside it).  The same factor holds for
+the verify kernels' scattered 16-byte table gathers: tools/microbench/gather_calib.hip measures
+2 x FETCH_SIZE x 1024 = the bytes of distinct 128-B lines touched within 2.5 %
+(profiles/r01/fetch_calibration.json).
 """
 import argparse
 import csv
