@@ -140,6 +140,49 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     return out
 
 
+WIRE_OUT_BYTES = 157   # per decoded message: status 1, height 8, ts 8 + 4, 5 x u32, TxKey 32, addr 20, sig 64
+
+
+def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
+    """Reactor.Receive's decodeMsg for the C2 votes as received TxVoteMessage wire
+    bytes (txv_encode_msgs = the sender's MarshalBinaryBare), decoded on the GPU (txv_k_decode_msgs)
+    from a batch resident in HBM.  Roofline: HBM, algorithmic bytes = wire bytes + 12 B of offset /
+    length per message read + 157 B of columns written.  Also the host-inclusive rate (upload,
+    decode, results copied into the caller's arrays) and the oracle's C decoder on one host thread."""
+    import txflow_amd as T
+    wb = T.encode_msgs(wl.batch)
+    ctx.decode_stage(wb)
+    ctx.decode_run(reps=2)
+    kms = ctx.decode_run(reps=reps)
+    d = ctx.decode_fetch(wb)
+    n = wb.n
+    b = wl.batch
+    ok = bool((d.status[:n] == T.WIRE_OK).all() and (d.height[:n] == b.height).all() and
+              (d.ts_sec[:n] == b.ts_sec).all() and (d.ts_nanos[:n] == b.ts_nanos).all() and
+              (d.sig[:n].reshape(-1) == b.sig).all() and (d.addr[:n].reshape(-1) == b.addr).all() and
+              (d.txhash_len[:n] == b.txhash_len).all() and (d.sig_len[:n] == b.sig_len).all())
+    alg = wb.nbytes + n * (12 + WIRE_OUT_BYTES)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        ctx.decode_msgs(wb)
+    host_s = (time.perf_counter() - t0) / 3
+    out = {"workload": f"C2 votes as {n} TxVoteMessage wire messages ({wb.nbytes / n:.1f} B avg), batch resident in HBM",
+           "correct": ok, "msgs_per_s": round(n / (kms * 1e-3), 1), "kernel_ms": round(kms, 4),
+           "roofline": {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": 8000.0,
+                        "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / 8000.0, 4),
+                        "alg_bytes_per_launch": alg, "traffic": None},
+           "host_inclusive_msgs_per_s": round(n / host_s, 1)}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        m = min(n, 500_000)
+        secs, st = O.wire_decode_many(wb.wire, wb.off[:m], wb.len[:m])
+        out["cpu_baseline"] = {"value": round(m / secs, 1), "unit": "msgs/s", "cores": 1, "kind": "port",
+                               "sample": f"first {m} messages, oracle/wire.c decoder on one thread"}
+        out["correct"] = ok and bool((st == 0).all())
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +199,7 @@ def main():
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
+    ap.add_argument("--no-wire", action="store_true", help="skip the TxVoteMessage wire-decode leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (the measured path); gloo = CPU-side rehearsal of the N>1 "
@@ -351,6 +395,8 @@ def main():
                          "tally_GBps": round(wl.n * TALLY_BYTES_PER_VOTE / (t_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,
         }
+        if world == 1 and not args.no_wire:
+            out["wire_decode"] = wire_decode_leg(ctx, wl, not args.no_cpu_baseline)
         if world == 1 and not args.no_c5:
             ctx.close()
             out["c5_streaming"] = c5_streaming(local, 1000, args.c5_txs, 65536)

@@ -111,4 +111,37 @@ inline int txvote_size(int64_t height, uint32_t txhash_len, int64_t sec, int32_t
   return (int)n;
 }
 
+// cdc.MarshalBinaryBare(&TxVoteMessage{Tx: vote}) (txvotepool/reactor.go:248, registered as
+// "tendermint/txvotepool/TxVoteMessage" :273-276): 4 prefix bytes, field 1 (0x0a) + uvarint(len) +
+// the TxVote bare body (fields as txvote_size).  out == nullptr: length only.  -1 on an amino time error.
+inline int64_t txvote_msg(uint8_t* out, const uint8_t prefix[4], int64_t height, const uint8_t* txhash,
+                          uint32_t txhash_len, const uint8_t* txkey, int64_t sec, int32_t nanos, const uint8_t* addr,
+                          uint32_t addr_len, const uint8_t* sig, uint32_t sig_len) {
+  uint8_t tb[24];
+  const int tl = time_body(tb, sec, nanos);
+  if (tl < 0) return -1;
+  const uint64_t body = (uint64_t)txvote_size(height, txhash_len, sec, nanos, addr_len, sig_len);
+  const uint64_t total = 5 + put_uvarint(nullptr, body) + body;
+  if (!out) return (int64_t)total;
+  memcpy(out, prefix, 4);
+  out[4] = 0x0a;
+  uint8_t* p = out + 5 + put_uvarint(out + 5, body);
+  auto bytes_field = [&](uint8_t key, const uint8_t* b, uint32_t len) {
+    if (!len) return;
+    *p++ = key;
+    p += put_uvarint(p, len);
+    memcpy(p, b, len);
+    p += len;
+  };
+  if (height != 0) { *p++ = 0x08; p += put_uvarint(p, (uint64_t)height); }
+  bytes_field(0x12, txhash, txhash_len);
+  *p++ = 0x1a; *p++ = 0x20;
+  if (txkey) memcpy(p, txkey, 32); else memset(p, 0, 32);
+  p += 32;
+  bytes_field(0x22, tb, (uint32_t)tl);
+  bytes_field(0x2a, addr, addr_len);
+  bytes_field(0x32, sig, sig_len);
+  return (int64_t)(p - out);
+}
+
 }  // namespace txv_host

@@ -23,6 +23,8 @@
 #include <cstring>
 #include <sys/mman.h>
 #include <mutex>
+#include <thread>
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -193,6 +195,26 @@ int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig
   return txv_sig_keys(ctx, v, sig_full, sig_full_off, p->keys.data());
 }
 
+}  // namespace
+
+void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // runtime.cpp
+
+namespace {
+
+// amino nameToDisfix("tendermint/txvotepool/TxVoteMessage") (go-amino, external): SHA-256 of the
+// registered name, zero bytes skipped, 3 disambiguation bytes, zero bytes skipped, 4 prefix bytes
+void txvote_msg_disfix(uint8_t disamb[3], uint8_t prefix[4]) {
+  static const char name[] = "tendermint/txvotepool/TxVoteMessage";
+  uint8_t h[32];
+  txv_sha256_bytes(reinterpret_cast<const uint8_t*>(name), sizeof name - 1, h);
+  int i = 0;
+  while (h[i] == 0) ++i;
+  memcpy(disamb, h + i, 3);
+  i += 3;
+  while (h[i] == 0) ++i;
+  memcpy(prefix, h + i, 4);
+}
+
 inline uint32_t vote_size(const txv_votes* v, uint32_t i) {
   return (uint32_t)txv_host::txvote_size(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], v->addr_len[i],
                                          v->sig_len[i]);
@@ -299,6 +321,88 @@ int txv_pool_reap(txv_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_o
     }
   }
   if (n_out) *n_out = n;
+  return TXV_OK;
+}
+
+int txv_pool_receive(txv_pool* p, txv_ctx* ctx, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                     const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!p || !ctx || (n && (!wire_status || !pool_status))) return TXV_EINVAL;
+  // decodeMsg for the batch (GPU), then the decoded TxVoteMessages in arrival order
+  std::vector<int64_t> height(n), ts_sec(n);
+  std::vector<int32_t> ts_nanos(n);
+  std::vector<uint32_t> th_off(n), th_len(n), addr_len(n), sig_len(n);
+  std::vector<uint64_t> sig_off(n);
+  std::vector<uint8_t> addr((size_t)n * 20), sig((size_t)n * 64);
+  txv_wire_votes w{};
+  w.status = wire_status; w.height = height.data(); w.txhash_off = th_off.data(); w.txhash_len = th_len.data();
+  w.ts_sec = ts_sec.data(); w.ts_nanos = ts_nanos.data(); w.addr = addr.data(); w.addr_len = addr_len.data();
+  w.sig = sig.data(); w.sig_len = sig_len.data(); w.sig_off = sig_off.data();
+  uint32_t max_msg;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    max_msg = p->cfg.max_msg_bytes;
+  }
+  int r = txv_decode_msgs(ctx, wire, wire_bytes, msg_off, msg_len, n, max_msg, &w);
+  if (r) return r;
+  std::vector<uint32_t> ok;   // compact the decoded messages (the others never reach CheckTx)
+  ok.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    pool_status[i] = TXV_POOL_NOT_CHECKED;
+    if (wire_status[i] == TXV_WIRE_OK) ok.push_back(i);
+  }
+  if (ok.empty()) return TXV_OK;
+  if (ok.size() != n) {
+    for (size_t j = 0; j < ok.size(); ++j) {
+      const uint32_t i = ok[j];
+      height[j] = height[i]; ts_sec[j] = ts_sec[i]; ts_nanos[j] = ts_nanos[i]; th_off[j] = th_off[i];
+      th_len[j] = th_len[i]; addr_len[j] = addr_len[i]; sig_len[j] = sig_len[i]; sig_off[j] = sig_off[i];
+      memmove(addr.data() + j * 20, addr.data() + (size_t)i * 20, 20);
+      memmove(sig.data() + j * 64, sig.data() + (size_t)i * 64, 64);
+    }
+  }
+  txv_votes v{};
+  v.n = (uint32_t)ok.size();
+  v.height = height.data(); v.txhash = wire; v.txhash_off = th_off.data(); v.txhash_len = th_len.data();
+  v.ts_sec = ts_sec.data(); v.ts_nanos = ts_nanos.data(); v.addr = addr.data(); v.addr_len = addr_len.data();
+  v.sig = sig.data(); v.sig_len = sig_len.data();
+  std::vector<uint8_t> st(v.n);
+  r = txv_pool_check(p, ctx, &v, wire, sig_off.data(), st.data());
+  if (r) return r;
+  for (size_t j = 0; j < ok.size(); ++j) pool_status[ok[j]] = st[j];
+  return TXV_OK;
+}
+
+int txv_encode_msgs(const txv_votes* v, const uint8_t* txkey, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                    uint8_t* out, uint64_t cap, uint64_t* off_out, uint32_t* len_out, uint64_t* bytes_out) {
+  if (!v || (v->n && (!off_out || !len_out))) return TXV_EINVAL;
+  uint8_t disamb[3], prefix[4];
+  txvote_msg_disfix(disamb, prefix);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < v->n; ++i) {   // lengths and offsets
+    if ((v->is_nil && v->is_nil[i]) || v->addr_len[i] > 20 || (v->sig_len[i] > 64 && (!sig_full || !sig_full_off)))
+      return TXV_EINVAL;
+    const int64_t m = txv_host::txvote_msg(nullptr, prefix, v->height[i], nullptr, v->txhash_len[i], nullptr,
+                                          v->ts_sec[i], v->ts_nanos[i], nullptr, v->addr_len[i], nullptr, v->sig_len[i]);
+    if (m < 0) return TXV_EINVAL;           // MustMarshalBinaryBare panics
+    off_out[i] = total;
+    len_out[i] = (uint32_t)m;
+    total += (uint64_t)m;
+  }
+  if (bytes_out) *bytes_out = total;
+  if (total > cap || (total && !out)) return TXV_ECAPACITY;
+  const uint32_t n = v->n;
+  const uint32_t nt = std::max(1u, std::min<uint32_t>(16, n / 16384));
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i) {
+        const uint8_t* sig = v->sig_len[i] > 64 ? sig_full + sig_full_off[i] : v->sig + (size_t)i * 64;
+        txv_host::txvote_msg(out + off_out[i], prefix, v->height[i], v->txhash + v->txhash_off[i], v->txhash_len[i],
+                             txkey ? txkey + (size_t)i * 32 : nullptr, v->ts_sec[i], v->ts_nanos[i],
+                             v->addr + (size_t)i * 20, v->addr_len[i], sig, v->sig_len[i]);
+      }
+    });
+  for (auto& x : th) x.join();
   return TXV_OK;
 }
 

@@ -140,6 +140,15 @@ struct txv_ctx {
   uint32_t pk_cap = 0;
   uint32_t *d_pk_sig = nullptr, *d_pk_len = nullptr, *d_pk_keys = nullptr;
   uint32_t *h_pk_sig = nullptr, *h_pk_len = nullptr, *h_pk_keys = nullptr;
+  // txv_decode_* (TxVoteMessage wire decode): staged messages, packed outputs (one D2H copy)
+  uint32_t wd_n = 0, wd_cap = 0;
+  uint64_t wd_bytes = 0, wd_bytes_cap = 0;
+  bool wd_ran = false;
+  uint8_t *d_wd_wire = nullptr, *h_wd_wire = nullptr;
+  uint64_t *d_wd_off = nullptr, *h_wd_off = nullptr;
+  uint32_t *d_wd_len = nullptr, *h_wd_len = nullptr;
+  uint8_t *d_wd_out = nullptr, *h_wd_out = nullptr;
+  hipEvent_t wd_ev[2] = {nullptr, nullptr};
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -881,6 +890,9 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
   dfree(c->d_chain); dfree(c->d_chain_sign);
   dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
+  dfree(c->d_wd_wire); hfree(c->h_wd_wire); dfree(c->d_wd_off); hfree(c->h_wd_off); dfree(c->d_wd_len); hfree(c->h_wd_len);
+  dfree(c->d_wd_out); hfree(c->h_wd_out);
+  for (auto& e : c->wd_ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->key_stream) (void)hipStreamDestroy(c->key_stream);
@@ -1261,6 +1273,13 @@ static void sha256_host(const uint8_t* p, uint64_t n, uint8_t out[32]) {
     for (int b = 0; b < 4; ++b) out[4 * j + b] = (uint8_t)(st[j] >> (24 - 8 * b));
 }
 
+}  // extern "C"
+
+// internal (pool.cpp): SHA-256 on the host
+void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]) { sha256_host(p, n, out); }
+
+extern "C" {
+
 int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
                  uint8_t* keys_out) {
   if (!c || !v || (v->n && (!v->sig || !v->sig_len || !keys_out))) return TXV_EINVAL;
@@ -1417,6 +1436,159 @@ int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* 
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   dfree(da); dfree(db); dfree(dout);
   return TXV_OK;
+}
+
+}  // extern "C"
+
+// ---- TxVoteMessage wire decode (Reactor.Receive / decodeMsg, txvotepool/reactor.go:170-190, 278-284) ----
+
+namespace {
+
+// packed per-message outputs of txv_k_decode_msgs, column blocks in this order
+struct WireCols {
+  uint8_t* status; int64_t* height; int64_t* ts_sec; int32_t* ts_nanos;
+  uint32_t *txhash_off, *txhash_len, *addr_len, *sig_off, *sig_len, *txkey, *addr, *sig;
+};
+constexpr size_t kWireOutBytes = 8 + 8 + 4 + 5 * 4 + 32 + 20 + 64 + 1;   // per message
+WireCols wire_cols(uint8_t* base, uint32_t cap) {
+  WireCols w;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { uint8_t* p = base + o; o += (bytes * cap + 255) / 256 * 256; return p; };
+  w.height = (int64_t*)take(8); w.ts_sec = (int64_t*)take(8); w.ts_nanos = (int32_t*)take(4);
+  w.txhash_off = (uint32_t*)take(4); w.txhash_len = (uint32_t*)take(4); w.addr_len = (uint32_t*)take(4);
+  w.sig_off = (uint32_t*)take(4); w.sig_len = (uint32_t*)take(4);
+  w.txkey = (uint32_t*)take(32); w.addr = (uint32_t*)take(20); w.sig = (uint32_t*)take(64);
+  w.status = take(1);
+  return w;
+}
+size_t wire_out_bytes(uint32_t cap) { return kWireOutBytes * cap + 12 * 256; }
+
+// amino nameToDisfix("tendermint/txvotepool/TxVoteMessage") (go-amino, external): SHA-256 of the
+// registered name, leading zero bytes skipped, 3 disambiguation bytes, zero bytes skipped, 4 prefix bytes
+void txvote_msg_disfix(uint32_t* disamb, uint32_t* prefix) {
+  static const char name[] = "tendermint/txvotepool/TxVoteMessage";
+  uint8_t h[32];
+  sha256_host(reinterpret_cast<const uint8_t*>(name), sizeof name - 1, h);
+  int i = 0;
+  while (h[i] == 0) ++i;
+  *disamb = (uint32_t)h[i] | ((uint32_t)h[i + 1] << 8) | ((uint32_t)h[i + 2] << 16);
+  i += 3;
+  while (h[i] == 0) ++i;
+  *prefix = le32(h + i);
+}
+
+}  // namespace
+
+extern "C" {
+
+int txv_decode_stage(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                     const uint32_t* msg_len, uint32_t n) {
+  if (!c || (n && (!wire || !msg_off || !msg_len))) return TXV_EINVAL;
+  if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
+  for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernel trusts these
+    if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
+      c->err = "message " + std::to_string(i) + " outside the wire buffer";
+      return TXV_EINVAL;
+    }
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int r;
+  if (n > c->wd_cap) {
+    const uint32_t cap = std::max<uint32_t>(n, 1024);
+    if ((r = dalloc(c, &c->d_wd_off, cap)) || (r = halloc(c, &c->h_wd_off, cap)) || (r = dalloc(c, &c->d_wd_len, cap)) ||
+        (r = halloc(c, &c->h_wd_len, cap)) || (r = dalloc(c, &c->d_wd_out, wire_out_bytes(cap))) ||
+        (r = halloc(c, &c->h_wd_out, wire_out_bytes(cap))))
+      return r;
+    c->wd_cap = cap;
+  }
+  if (wire_bytes + 64 > c->wd_bytes_cap) {
+    const uint64_t cap = std::max<uint64_t>(wire_bytes + 64, 1u << 20);
+    if ((r = dalloc(c, &c->d_wd_wire, cap)) || (r = halloc(c, &c->h_wd_wire, cap))) return r;
+    c->wd_bytes_cap = cap;
+  }
+  if (!c->wd_ev[0]) { HIP_TRY(c, hipEventCreate(&c->wd_ev[0])); HIP_TRY(c, hipEventCreate(&c->wd_ev[1])); }
+  c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
+    const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
+    memcpy(c->h_wd_wire + a, wire + a, b - a);
+  }, 16);
+  memset(c->h_wd_wire + wire_bytes, 0, 64);
+  memcpy(c->h_wd_off, msg_off, (size_t)n * 8);
+  memcpy(c->h_wd_len, msg_len, (size_t)n * 4);
+  HIP_TRY(c, hipMemcpyAsync(c->d_wd_wire, c->h_wd_wire, wire_bytes + 64, hipMemcpyHostToDevice, c->key_stream));
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_wd_off, c->h_wd_off, (size_t)n * 8, hipMemcpyHostToDevice, c->key_stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_wd_len, c->h_wd_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+  c->wd_n = n;
+  c->wd_bytes = wire_bytes;
+  c->wd_ran = false;
+  return TXV_OK;
+}
+
+int txv_decode_run(txv_ctx* c, uint32_t max_msg_bytes, uint32_t reps, float* kernel_ms_avg) {
+  if (!c) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->wd_ev[0]) { c->err = "txv_decode_run before txv_decode_stage"; return TXV_ESTATE; }
+  WireArgs a{};
+  a.n = c->wd_n;
+  a.max_msg_bytes = max_msg_bytes;
+  txvote_msg_disfix(&a.disamb, &a.prefix);
+  a.wire = c->d_wd_wire; a.off = c->d_wd_off; a.len = c->d_wd_len;
+  const WireCols w = wire_cols(c->d_wd_out, c->wd_cap);
+  a.status = w.status; a.height = w.height; a.ts_sec = w.ts_sec; a.ts_nanos = w.ts_nanos;
+  a.txhash_off = w.txhash_off; a.txhash_len = w.txhash_len; a.addr_len = w.addr_len; a.sig_off = w.sig_off;
+  a.sig_len = w.sig_len; a.txkey = w.txkey; a.addr = w.addr; a.sig = w.sig;
+  if (!reps) reps = 1;
+  HIP_TRY(c, hipEventRecord(c->wd_ev[0], c->key_stream));
+  for (uint32_t k = 0; k < reps; ++k) HIP_TRY(c, txv_launch_decode_msgs(&a, c->key_stream));
+  HIP_TRY(c, hipEventRecord(c->wd_ev[1], c->key_stream));
+  HIP_TRY(c, hipEventSynchronize(c->wd_ev[1]));
+  if (kernel_ms_avg) {
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->wd_ev[0], c->wd_ev[1]));
+    *kernel_ms_avg = ms / (float)reps;
+  }
+  c->wd_ran = true;
+  return TXV_OK;
+}
+
+int txv_decode_fetch(txv_ctx* c, const txv_wire_votes* out) {
+  if (!c || !out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->wd_ran) { c->err = "txv_decode_fetch before txv_decode_run"; return TXV_ESTATE; }
+  const uint32_t n = c->wd_n;
+  if (!n) return TXV_OK;
+  HIP_TRY(c, hipMemcpyAsync(c->h_wd_out, c->d_wd_out, wire_out_bytes(c->wd_cap), hipMemcpyDeviceToHost, c->key_stream));
+  HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+  const WireCols w = wire_cols(c->h_wd_out, c->wd_cap);
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    const size_t m = hi - lo;
+    if (out->status) memcpy(out->status + lo, w.status + lo, m);
+    if (out->height) memcpy(out->height + lo, w.height + lo, m * 8);
+    if (out->ts_sec) memcpy(out->ts_sec + lo, w.ts_sec + lo, m * 8);
+    if (out->ts_nanos) memcpy(out->ts_nanos + lo, w.ts_nanos + lo, m * 4);
+    if (out->txhash_off) memcpy(out->txhash_off + lo, w.txhash_off + lo, m * 4);
+    if (out->txhash_len) memcpy(out->txhash_len + lo, w.txhash_len + lo, m * 4);
+    if (out->addr_len) memcpy(out->addr_len + lo, w.addr_len + lo, m * 4);
+    if (out->sig_len) memcpy(out->sig_len + lo, w.sig_len + lo, m * 4);
+    if (out->sig_off) for (uint32_t i = lo; i < hi; ++i) out->sig_off[i] = w.sig_off[i];
+    if (out->txkey) memcpy(out->txkey + (size_t)lo * 32, w.txkey + (size_t)lo * 8, m * 32);
+    if (out->addr) memcpy(out->addr + (size_t)lo * 20, w.addr + (size_t)lo * 5, m * 20);
+    if (out->sig) memcpy(out->sig + (size_t)lo * 64, w.sig + (size_t)lo * 16, m * 64);
+  }, 8192);
+  return TXV_OK;
+}
+
+int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                    const uint32_t* msg_len, uint32_t n, uint32_t max_msg_bytes, const txv_wire_votes* out) {
+  if (!c || !out) return TXV_EINVAL;
+  int r = txv_decode_stage(c, wire, wire_bytes, msg_off, msg_len, n);
+  if (!r) r = txv_decode_run(c, max_msg_bytes, 1, nullptr);
+  if (!r) r = txv_decode_fetch(c, out);
+  return r;
 }
 
 }  // extern "C"

@@ -66,7 +66,26 @@ struct SignArgs {
   uint32_t* sig;               // [16][n_pad] output
 };
 
+// TxVoteMessage wire decode (kernels_wire.hip): statuses are include/txvote.h's TXV_WIRE_*
+// (0 ok, 1 too large, 2 amino error, 3 empty/nil); offsets are absolute into `wire`
+struct WireArgs {
+  uint32_t n, max_msg_bytes;
+  uint32_t disamb, prefix;     // amino disambiguation (3 bytes) / prefix (4 bytes), little-endian packed
+  const uint8_t* wire;         // messages, padded by >= 16 bytes
+  const uint64_t* off;         // [n]
+  const uint32_t* len;         // [n]
+  uint8_t* status;             // [n]
+  int64_t* height;             // [n]
+  int64_t* ts_sec;             // [n]
+  int32_t* ts_nanos;           // [n]
+  uint32_t *txhash_off, *txhash_len, *addr_len, *sig_off, *sig_len;   // [n]
+  uint32_t* txkey;             // [n][8]
+  uint32_t* addr;              // [n][5]  first 20 bytes, zero beyond the length
+  uint32_t* sig;               // [n][16] first 64 bytes, zero beyond the length
+};
+
 extern "C" {
+hipError_t txv_launch_decode_msgs(const WireArgs* args, hipStream_t st);
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);

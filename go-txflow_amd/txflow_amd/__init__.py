@@ -68,6 +68,11 @@ class _PoolCfg(ctypes.Structure):
                 ("max_msg_bytes", ctypes.c_uint32), ("pad0", ctypes.c_uint32)]
 
 
+class _WireVotes(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_void_p) for f in ("status", "height", "txhash_off", "txhash_len", "txkey", "ts_sec",
+                                              "ts_nanos", "addr", "addr_len", "sig", "sig_len", "sig_off")]
+
+
 class _Event(ctypes.Structure):
     _fields_ = [("vote_index", ctypes.c_uint32), ("tx_index", ctypes.c_uint32), ("sum", ctypes.c_int64)]
 
@@ -132,6 +137,13 @@ def lib():
             "txv_pool_txs_bytes": ([vp], i64),
             "txv_pool_height": ([vp], i64),
             "txv_pool_cache_keys": ([vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_decode_msgs": ([vp, vp, ctypes.c_uint64, vp, vp, u32, u32, ctypes.POINTER(_WireVotes)], ctypes.c_int),
+            "txv_decode_stage": ([vp, vp, ctypes.c_uint64, vp, vp, u32], ctypes.c_int),
+            "txv_decode_run": ([vp, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "txv_decode_fetch": ([vp, ctypes.POINTER(_WireVotes)], ctypes.c_int),
+            "txv_pool_receive": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp], ctypes.c_int),
+            "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
+                                 ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -149,7 +161,8 @@ EXPORTED_SYMBOLS = [
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
-    "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys"]
+    "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys",
+    "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -252,6 +265,103 @@ class VoteBatch:
     def txhash(self, i: int) -> bytes:
         o, l = int(self.txhash_off[i]), int(self.txhash_len[i])
         return self.txhash_arena[o:o + l].tobytes()
+
+
+# ------------------------------------------------------------------ received wire messages
+WIRE_OK, WIRE_TOO_LARGE, WIRE_ERR_DECODE, WIRE_NIL = range(4)   # TXV_WIRE_*
+POOL_NOT_CHECKED = 0xFF
+
+
+class WireBatch:
+    """n received TxVoteMessage wire messages (Reactor.Receive msgBytes) packed in one buffer."""
+
+    def __init__(self, msgs: Sequence[bytes] = (), *, wire=None, off=None, length=None):
+        if wire is None:
+            lens = np.array([len(m) for m in msgs], np.uint32)
+            off = np.zeros(len(msgs), np.uint64)
+            if len(msgs) > 1:
+                off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            wire = np.frombuffer(b"".join(msgs), np.uint8) if msgs else np.zeros(0, np.uint8)
+            length = lens
+        self.wire = np.ascontiguousarray(wire, dtype=np.uint8)
+        if self.wire.size == 0:
+            self.wire = np.zeros(1, np.uint8)
+            self.nbytes = 0
+        else:
+            self.nbytes = int(self.wire.size)
+        self.off = np.ascontiguousarray(off, dtype=np.uint64)
+        self.len = np.ascontiguousarray(length, dtype=np.uint32)
+        self.n = int(self.off.size)
+
+    def msg(self, i: int) -> bytes:
+        o, l = int(self.off[i]), int(self.len[i])
+        return self.wire[o:o + l].tobytes()
+
+
+def encode_msgs(batch: "VoteBatch", txkey: Optional[np.ndarray] = None) -> WireBatch:
+    """cdc.MustMarshalBinaryBare(&TxVoteMessage{tx}) for every vote of `batch` (txv_encode_msgs)."""
+    vs = batch.c_struct()
+    n = batch.n
+    off = np.zeros(max(n, 1), np.uint64)
+    ln = np.zeros(max(n, 1), np.uint32)
+    total = ctypes.c_uint64()
+    tk = None if txkey is None else np.ascontiguousarray(txkey, np.uint8).ctypes.data
+    rc = lib().txv_encode_msgs(ctypes.byref(vs), tk, None, None, None, 0, off.ctypes.data, ln.ctypes.data,
+                               ctypes.byref(total))
+    if rc not in (0, -28):
+        raise TxvInfraError(f"txv_encode_msgs failed ({rc})")
+    wire = np.zeros(max(total.value, 1), np.uint8)
+    rc = lib().txv_encode_msgs(ctypes.byref(vs), tk, None, None, wire.ctypes.data, total.value, off.ctypes.data,
+                               ln.ctypes.data, ctypes.byref(total))
+    if rc != 0:
+        raise TxvInfraError(f"txv_encode_msgs failed ({rc})")
+    return WireBatch(wire=wire[:total.value], off=off[:n], length=ln[:n])
+
+
+class DecodedMsgs:
+    """txv_wire_votes results: status, the votes as a VoteBatch over the wire buffer, TxKey, sig offsets"""
+
+    def __init__(self, wb: WireBatch):
+        n = max(wb.n, 1)
+        self.status = np.zeros(n, np.uint8)
+        self.height = np.zeros(n, np.int64)
+        self.txhash_off = np.zeros(n, np.uint32)
+        self.txhash_len = np.zeros(n, np.uint32)
+        self.txkey = np.zeros((n, 32), np.uint8)
+        self.ts_sec = np.zeros(n, np.int64)
+        self.ts_nanos = np.zeros(n, np.int32)
+        self.addr = np.zeros((n, 20), np.uint8)
+        self.addr_len = np.zeros(n, np.uint32)
+        self.sig = np.zeros((n, 64), np.uint8)
+        self.sig_len = np.zeros(n, np.uint32)
+        self.sig_off = np.zeros(n, np.uint64)
+        self.n = wb.n
+        self.wb = wb
+
+    def c_struct(self) -> _WireVotes:
+        w = _WireVotes()
+        for f, _ in _WireVotes._fields_:
+            setattr(w, f, getattr(self, f).ctypes.data)
+        return w
+
+    def batch(self) -> VoteBatch:
+        """all n messages as a VoteBatch (fields zero where status != WIRE_OK); TxHash arena = the wire"""
+        n = self.n
+        return VoteBatch(n, height=self.height[:n], txhash_arena=self.wb.wire, txhash_off=self.txhash_off[:n],
+                         txhash_len=self.txhash_len[:n], ts_sec=self.ts_sec[:n], ts_nanos=self.ts_nanos[:n],
+                         addr=self.addr[:n], addr_len=self.addr_len[:n], sig=self.sig[:n], sig_len=self.sig_len[:n])
+
+    def vote(self, i: int) -> Optional[TxVote]:
+        if self.status[i] != WIRE_OK:
+            return None
+        w = self.wb.wire
+        o, l = int(self.txhash_off[i]), int(self.txhash_len[i])
+        so, sl = int(self.sig_off[i]), int(self.sig_len[i])
+        al = int(self.addr_len[i])
+        return TxVote(Height=int(self.height[i]), TxHash=w[o:o + l].tobytes().decode("latin-1"),
+                      TxKey=self.txkey[i].tobytes(), Timestamp=(int(self.ts_sec[i]), int(self.ts_nanos[i])),
+                      ValidatorAddress=self.addr[i, :min(al, 20)].tobytes() if al <= 20 else b"?" * al,
+                      Signature=w[so:so + sl].tobytes() if sl else None)
 
 
 # ------------------------------------------------------------------ context
@@ -482,6 +592,29 @@ class Context:
     def sync(self):
         self._chk(lib().txv_sync(self._h), "txv_sync")
 
+    def decode_msgs(self, wb: WireBatch, max_msg_bytes: int = 1 << 20) -> DecodedMsgs:
+        """Reactor.decodeMsg for a batch of received messages, on the GPU (txv_decode_msgs)."""
+        d = DecodedMsgs(wb)
+        ws = d.c_struct()
+        self._chk(lib().txv_decode_msgs(self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                        wb.len.ctypes.data, wb.n, max_msg_bytes, ctypes.byref(ws)), "txv_decode_msgs")
+        return d
+
+    def decode_stage(self, wb: WireBatch):
+        self._chk(lib().txv_decode_stage(self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                         wb.len.ctypes.data, wb.n), "txv_decode_stage")
+
+    def decode_run(self, max_msg_bytes: int = 1 << 20, reps: int = 1) -> float:
+        ms = ctypes.c_float()
+        self._chk(lib().txv_decode_run(self._h, max_msg_bytes, reps, ctypes.byref(ms)), "txv_decode_run")
+        return ms.value
+
+    def decode_fetch(self, wb: WireBatch) -> DecodedMsgs:
+        d = DecodedMsgs(wb)
+        ws = d.c_struct()
+        self._chk(lib().txv_decode_fetch(self._h, ctypes.byref(ws)), "txv_decode_fetch")
+        return d
+
     def fe_selftest(self, a: np.ndarray, b: np.ndarray, op: int) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint32); b = np.ascontiguousarray(b, dtype=np.uint32)
         n = a.shape[0]
@@ -540,6 +673,16 @@ class TxVotePool:
         self.ctx._chk(lib().txv_pool_check(self._h, self.ctx._h, ctypes.byref(vs), full, off, out.ctypes.data),
                       "txv_pool_check")
         return out[:batch.n]
+
+    def receive(self, wb: WireBatch):
+        """Reactor.Receive (txvotepool/reactor.go:170-190) for a batch of messages in arrival order:
+        (wire status TXV_WIRE_*, pool status TXV_POOL_* or POOL_NOT_CHECKED) per message."""
+        ws = np.zeros(max(wb.n, 1), np.uint8)
+        ps = np.zeros(max(wb.n, 1), np.uint8)
+        self.ctx._chk(lib().txv_pool_receive(self._h, self.ctx._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                             wb.len.ctypes.data, wb.n, ws.ctypes.data, ps.ctypes.data),
+                      "txv_pool_receive")
+        return ws[:wb.n], ps[:wb.n]
 
     def update(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
         full, off = _long_sig_arena(batch, long_sigs)

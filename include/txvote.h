@@ -30,6 +30,12 @@
  *                         CheckTx/CheckTxWithInfo :180-261 (+ mapTxCache.Push :416-438, addTx :265-270),
  *                         Update :329-359, ReapMaxTxs :310-324, Flush :146-159, Size :136,
  *                         TxsBytes :141; removeTx :275-284
+ *   txv_decode_msgs    <- Reactor.decodeMsg / cdc.UnmarshalBinaryBare(bz, &msg) into *TxVoteMessage
+ *                         txvotepool/reactor.go:278-291 (codec: reactor.go:273-276, codec.go)
+ *   txv_encode_msgs    <- cdc.MustMarshalBinaryBare(&TxVoteMessage{tx}) in broadcastTxRoutine
+ *                         txvotepool/reactor.go:248 (the sending side of the same wire format)
+ *   txv_pool_receive   <- func (txR *Reactor) Receive(chID byte, src p2p.Peer, msgBytes []byte)
+ *                         txvotepool/reactor.go:170-190 (decodeMsg + CheckTxWithInfo per message)
  */
 #ifndef TXVOTE_H
 #define TXVOTE_H
@@ -289,6 +295,55 @@ int64_t txv_pool_txs_bytes(txv_pool* pool);
 int64_t txv_pool_height(txv_pool* pool);
 /* LRU cache keys front (oldest) to back; *n_out = cache length (test hook: cache_test.go). */
 int txv_pool_cache_keys(txv_pool* pool, uint8_t* keys_out, uint64_t cap, uint64_t* n_out);
+
+/* ---- TxVoteMessage wire decode (Reactor.Receive, txvotepool/reactor.go:170-190, 273-291) ----
+ * n received messages (message i = wire[msg_off[i] .. + msg_len[i]), wire < 4 GiB) decoded on
+ * the GPU, amino UnmarshalBinaryBare of the TxpoolMessage interface whose one registered
+ * concrete is &TxVoteMessage{Tx types.TxVote} ("tendermint/txvotepool/TxVoteMessage"), straight
+ * into the txv_votes layout.  TxHash bytes and signatures stay in the caller's buffer:
+ * txhash_off / sig_off index `wire`, so txv_votes{txhash = wire, txhash_off, ...} with
+ * sig_full = wire, sig_full_off = sig_off feeds txv_pool_check / txv_add_votes directly. */
+#define TXV_WIRE_OK 0          /* *TxVoteMessage -> CheckTxWithInfo(msg.Tx) */
+#define TXV_WIRE_TOO_LARGE 1   /* len > MaxMsgBytes: decodeMsg's ErrTxTooLarge (peer stopped) */
+#define TXV_WIRE_ERR_DECODE 2  /* amino decode error (peer stopped) */
+#define TXV_WIRE_NIL 3         /* empty message: nil msg, "Unknown message type" (ignored) */
+typedef struct {             /* caller-owned [n] arrays; any pointer may be NULL (not written) */
+  uint8_t*  status;          /* TXV_WIRE_*; the fields below are zero unless TXV_WIRE_OK */
+  int64_t*  height;
+  uint32_t* txhash_off;      /* TxHash bytes at wire + txhash_off */
+  uint32_t* txhash_len;
+  uint8_t*  txkey;           /* [n][32] TxKey */
+  int64_t*  ts_sec;          /* Timestamp (absent = the Unix epoch, amino's default time) */
+  int32_t*  ts_nanos;
+  uint8_t*  addr;            /* [n][20] first 20 bytes of ValidatorAddress, zero beyond its length */
+  uint32_t* addr_len;
+  uint8_t*  sig;             /* [n][64] first 64 bytes of Signature, zero beyond its length */
+  uint32_t* sig_len;
+  uint64_t* sig_off;         /* Signature bytes at wire + sig_off */
+} txv_wire_votes;
+int txv_decode_msgs(txv_ctx* ctx, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                    const uint32_t* msg_len, uint32_t n, uint32_t max_msg_bytes, const txv_wire_votes* out);
+/* the same in three steps (bench / pipelining): upload, decode `reps` times on the device
+ * (average kernel time), copy the results of the last run out */
+int txv_decode_stage(txv_ctx* ctx, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                     const uint32_t* msg_len, uint32_t n);
+int txv_decode_run(txv_ctx* ctx, uint32_t max_msg_bytes, uint32_t reps, float* kernel_ms_avg);
+int txv_decode_fetch(txv_ctx* ctx, const txv_wire_votes* out);
+/* Reactor.Receive for n messages in arrival order: decode (GPU) with the pool's MaxMsgBytes, then
+ * CheckTxWithInfo for every decoded TxVoteMessage.  wire_status_out[i] = TXV_WIRE_*;
+ * pool_status_out[i] = TXV_POOL_* for TXV_WIRE_OK messages, TXV_POOL_NOT_CHECKED otherwise. */
+#define TXV_POOL_NOT_CHECKED 0xFF
+/* the sending side, broadcastTxRoutine's cdc.MustMarshalBinaryBare(&TxVoteMessage{tx})
+ * (txvotepool/reactor.go:248), for a batch on host threads: message i at out + off_out[i],
+ * len_out[i] bytes; txkey [n][32] or NULL (zero TxKey); signatures > 64 bytes from sig_full +
+ * sig_full_off[i].  Nil votes, addresses > 20 bytes and times amino rejects (the reference panics)
+ * are TXV_EINVAL.  *bytes_out = total size; TXV_ECAPACITY (nothing written) when it exceeds cap. */
+int txv_encode_msgs(const txv_votes* votes, const uint8_t* txkey, const uint8_t* sig_full,
+                    const uint64_t* sig_full_off, uint8_t* out, uint64_t cap, uint64_t* off_out, uint32_t* len_out,
+                    uint64_t* bytes_out);
+int txv_pool_receive(txv_pool* pool, txv_ctx* ctx, const uint8_t* wire, uint64_t wire_bytes,
+                     const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status_out,
+                     uint8_t* pool_status_out);
 
 /* ---- self-test hook: field/scalar ops on device (tests only) ---- */
 int txv_fe_selftest(txv_ctx* ctx, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op);

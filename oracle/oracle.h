@@ -12,6 +12,7 @@
  *   - golang.org/x/crypto@c2843e01d9a2 ed25519.Verify (external)
  *   - types/vote_set.go:81-166        TxVoteSet.AddVote / addVote / addVerifiedVote
  *   - txflow/service.go:192-234       TxFlow.addVote routing by TxHash
+ *   - txvotepool/reactor.go:170-190,273-291  Reactor.Receive / decodeMsg (TxVoteMessage amino wire codec)
  *
  * Parity pinning: the reference's Go code cannot be built here (no Go toolchain,
  * modules not vendored).  ed25519 results are pinned against
@@ -137,6 +138,29 @@ void orc_pool_flush(orc_pool*);
 int64_t orc_pool_size(orc_pool*);
 int64_t orc_pool_txs_bytes(orc_pool*);
 uint64_t orc_pool_cache_keys(orc_pool*, uint8_t* keys_out, uint64_t cap);
+
+/* ---- TxVoteMessage wire codec (txvotepool/reactor.go:170-190, 273-291; oracle/wire.c) ---- */
+#define ORC_WIRE_OK 0          /* *TxVoteMessage decoded -> CheckTxWithInfo */
+#define ORC_WIRE_TOO_LARGE 1   /* len > MaxMsgBytes: ErrTxTooLarge (decodeMsg) */
+#define ORC_WIRE_ERR_DECODE 2  /* amino UnmarshalBinaryBare error */
+#define ORC_WIRE_NIL 3         /* empty message: nil msg, "Unknown message type" */
+typedef struct {
+  int64_t height;
+  uint32_t txhash_off, txhash_len;   /* offsets into the message bytes */
+  uint8_t txkey[32];
+  int64_t ts_sec;
+  int32_t ts_nanos;
+  uint32_t addr_off, addr_len, sig_off, sig_len;
+} orc_wire_vote;
+int orc_wire_decode(const uint8_t* bz, size_t len, uint32_t max_msg_bytes, orc_wire_vote* out);
+/* cdc.MarshalBinaryBare(&TxVoteMessage{Tx: vote}); returns length, -1 on an amino time error or cap */
+int orc_wire_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
+                    int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
+                    const uint8_t* sig, size_t sig_len, uint8_t* out, size_t cap);
+void orc_wire_prefix(uint8_t disamb[3], uint8_t prefix[4]);
+/* CPU baseline: n messages decoded on one thread (status_out [n], out [n]); returns seconds */
+double orc_wire_decode_many(const uint8_t* wire, const uint64_t* off, const uint32_t* len, uint32_t n,
+                            uint32_t max_msg_bytes, uint8_t* status_out, orc_wire_vote* out);
 
 /* ---- CPU baseline: parallel verify with T threads (T = 1 mirrors checkMaj23Routine). ---- */
 /* Verifies n (pub,msg,sig) triples; msgs in an arena with offsets/lengths. Returns seconds. */

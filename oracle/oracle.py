@@ -78,6 +78,13 @@ def lib():
         L.orc_flow_num_verifies.restype = ctypes.c_uint64
         L.orc_verify_many.restype = ctypes.c_double
         L.orc_verify_many.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        L.orc_wire_decode.argtypes = [c_u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p]
+        L.orc_wire_encode.argtypes = [ctypes.c_int64, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_int64, ctypes.c_int32,
+                                      c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_wire_prefix.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_wire_decode_many.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                                  ctypes.c_void_p]
+        L.orc_wire_decode_many.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -340,3 +347,52 @@ class Pool:
 
     def txs_bytes(self):
         return lib().orc_pool_txs_bytes(self._h)
+
+
+# ---- TxVoteMessage wire codec (oracle/wire.c; txvotepool/reactor.go:170-190, 273-291) ----
+WIRE_OK, WIRE_TOO_LARGE, WIRE_ERR_DECODE, WIRE_NIL = range(4)
+
+
+class _WireVote(ctypes.Structure):
+    _fields_ = [("height", ctypes.c_int64), ("txhash_off", ctypes.c_uint32), ("txhash_len", ctypes.c_uint32),
+                ("txkey", ctypes.c_uint8 * 32), ("ts_sec", ctypes.c_int64), ("ts_nanos", ctypes.c_int32),
+                ("addr_off", ctypes.c_uint32), ("addr_len", ctypes.c_uint32), ("sig_off", ctypes.c_uint32),
+                ("sig_len", ctypes.c_uint32)]
+
+
+def wire_prefix():
+    d, p = ctypes.create_string_buffer(3), ctypes.create_string_buffer(4)
+    lib().orc_wire_prefix(d, p)
+    return d.raw, p.raw
+
+
+def wire_encode(height, txhash: bytes, ts_sec, ts_nanos, addr: bytes, sig: bytes, txkey: bytes = bytes(32)):
+    """cdc.MarshalBinaryBare(&TxVoteMessage{Tx: vote}); None when amino rejects the timestamp."""
+    cap = 64 + len(txhash) + len(addr) + len(sig) + 64
+    out = ctypes.create_string_buffer(cap)
+    n = lib().orc_wire_encode(height, txhash, len(txhash), txkey, ts_sec, ts_nanos, addr, len(addr), sig, len(sig),
+                              out, cap)
+    return None if n < 0 else out.raw[:n]
+
+
+def wire_decode(bz: bytes, max_msg_bytes: int = 1 << 20):
+    """decodeMsg + the *TxVoteMessage type switch: (status, fields dict or None)."""
+    o = _WireVote()
+    st = lib().orc_wire_decode(bz, len(bz), max_msg_bytes, ctypes.byref(o))
+    if st != WIRE_OK:
+        return st, None
+    return st, dict(height=o.height, txhash=bz[o.txhash_off:o.txhash_off + o.txhash_len], txkey=bytes(o.txkey),
+                    ts_sec=o.ts_sec, ts_nanos=o.ts_nanos, addr=bz[o.addr_off:o.addr_off + o.addr_len],
+                    sig=bz[o.sig_off:o.sig_off + o.sig_len], txhash_off=o.txhash_off, addr_off=o.addr_off,
+                    sig_off=o.sig_off)
+
+
+def wire_decode_many(wire, off, length, max_msg_bytes=1 << 20):
+    """(seconds, statuses) for the C decoder over n messages on one thread (CPU baseline)"""
+    import numpy as np
+    n = len(off)
+    st = np.zeros(max(n, 1), np.uint8)
+    out = (_WireVote * max(n, 1))()
+    secs = lib().orc_wire_decode_many(wire.ctypes.data, off.ctypes.data, length.ctypes.data, n, max_msg_bytes,
+                                      st.ctypes.data, out)
+    return secs, st[:n]

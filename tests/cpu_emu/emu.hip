@@ -4,6 +4,7 @@
 // ed25519_dev.h) for the host so logic errors in the kernel source can be localised on a
 // machine without a GPU.  It is not linked into libtxvote.so and the product never calls it.
 #include "../../go-txflow_amd/csrc/ed25519_dev.h"
+#include "../../go-txflow_amd/csrc/wire_dev.h"
 #include <cstring>
 #include <vector>
 
@@ -86,6 +87,29 @@ int emu_verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const ui
   uint32_t enc[8];
   ge_encode(enc, R);
   return memcmp(enc, s, 32) == 0;
+}
+
+
+// TxVoteMessage decode through wire_dev.h (txv_k_decode_msgs' parser and row copies, global-memory
+// form): the message sits at byte `shift` (0..3) of a word buffer.  Returns the TXV_WIRE_* status;
+// i64: height, ts_sec; u32: ts_nanos, txhash_off, txhash_len, addr_len, sig_off, sig_len;
+// rows: TxKey 8 words, address 5, signature 16.
+int emu_wire_decode(const uint8_t* msg, uint32_t len, uint32_t max_msg, uint32_t disamb, uint32_t prefix,
+                    uint32_t shift, int64_t* i64, uint32_t* u32, uint32_t* rows) {
+  using namespace txv::wire;
+  std::vector<uint32_t> words((len + shift + 3) / 4 + 4, 0xA5A5A5A5u);
+  uint8_t* bytes = reinterpret_cast<uint8_t*>(words.data());
+  memcpy(bytes + shift, msg, len);
+  Parsed o{};
+  uint32_t st = len == 0 ? 3u : (len > max_msg ? 1u : parse_msg((const uint8_t*)(bytes + shift), len, disamb, prefix, o));
+  if (st != 0) o = Parsed{};
+  copy_row<8>((const uint32_t*)words.data(), shift + o.key_off, o.has_key ? 32u : 0u, rows);
+  copy_row<5>((const uint32_t*)words.data(), shift + o.addr_off, o.addr_len < 20 ? o.addr_len : 20u, rows + 8);
+  copy_row<16>((const uint32_t*)words.data(), shift + o.sig_off, o.sig_len < 64 ? o.sig_len : 64u, rows + 13);
+  i64[0] = o.height; i64[1] = o.sec;
+  u32[0] = (uint32_t)o.nanos; u32[1] = o.th_off; u32[2] = o.th_len; u32[3] = o.addr_len; u32[4] = o.sig_off;
+  u32[5] = o.sig_len;
+  return (int)st;
 }
 
 }  // extern "C"

@@ -21,12 +21,14 @@ L = 2 ** 252 + 27742317777372353535851937790883648493
 def emu():
     src = os.path.join(EMU_DIR, "emu.hip")
     deps = [src] + [os.path.join(HERE, "..", "go-txflow_amd", "csrc", f)
-                    for f in ("fe.h", "sc.h", "sha2.h", "ge.h", "ed25519_dev.h")]
+                    for f in ("fe.h", "sc.h", "sha2.h", "ge.h", "ed25519_dev.h", "wire_dev.h")]
     if not os.path.exists(EMU) or any(os.path.getmtime(d) > os.path.getmtime(EMU) for d in deps):
         os.makedirs(os.path.dirname(EMU), exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "-shared", src, "-o", EMU], check=True)
     E = ctypes.CDLL(EMU)
     E.emu_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
+    E.emu_wire_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return E
 
 
@@ -64,3 +66,32 @@ def test_verify_vectors_through_kernel_source(emu):
         pub, msg, sig = bytes.fromhex(v["pub"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])
         got = bool(emu.emu_verify(pub, msg, len(msg), sig, len(sig)))
         assert got == v["expect"], v["kind"]
+
+
+def test_wire_decoder_source_vs_oracle(emu):
+    """txv_k_decode_msgs' parser (wire_dev.h) on the host against oracle/wire.c over the mixed
+    canonical / non-canonical / corrupted stream of tests/wire_gen.py, at every source alignment."""
+    import numpy as np
+    import oracle as O
+    import wire_gen as G
+    d, p = O.wire_prefix()
+    disamb, prefix = int.from_bytes(d, "little"), int.from_bytes(p, "little")
+    i64 = np.zeros(2, np.int64)
+    u32 = np.zeros(6, np.uint32)
+    rows = np.zeros(29, np.uint32)
+    for k, m in enumerate(G.messages(6000, seed=5)):
+        mx = 300 if k % 5 == 0 else 1 << 20
+        st = emu.emu_wire_decode(m, len(m), mx, disamb, prefix, k % 4, i64.ctypes.data, u32.ctypes.data,
+                                 rows.ctypes.data)
+        est, f = O.wire_decode(m, mx)
+        assert st == est, (k, m.hex())
+        if st != O.WIRE_OK:
+            continue
+        rb = rows.view(np.uint8).tobytes()
+        al, sl = len(f["addr"]), len(f["sig"])
+        assert (int(i64[0]), int(i64[1]), int(u32[0])) == (f["height"], f["ts_sec"], f["ts_nanos"]), k
+        assert (int(u32[1]), int(u32[2]), int(u32[3]), int(u32[5])) == (f["txhash_off"], len(f["txhash"]), al, sl), k
+        assert sl == 0 or int(u32[4]) == f["sig_off"], k
+        assert rb[:32] == f["txkey"], k
+        assert rb[32:52] == f["addr"][:20] + bytes(20 - min(al, 20)), k
+        assert rb[52:116] == f["sig"][:64] + bytes(64 - min(sl, 64)), k
