@@ -22,13 +22,16 @@ using namespace txv::wire;
 
 namespace {
 
-constexpr uint32_t kWireBlock = 256;
-constexpr uint32_t kWireLds = 56 * 1024;
+#ifndef TXV_WIRE_BLOCK
+#define TXV_WIRE_BLOCK 128
+#endif
+constexpr uint32_t kWireBlock = TXV_WIRE_BLOCK;        // messages per block
+constexpr uint32_t kWireLds = kWireBlock * 224;        // staged bytes per block
 
 }  // namespace
 
 __global__ void __launch_bounds__(kWireBlock) txv_k_decode_msgs(WireArgs a) {
-  __shared__ uint32_t lds_w[kWireLds / 4 + 4];
+  __shared__ uint32_t lds_w[kWireLds / 4 + 24];   // + slack for the row reads
   __shared__ unsigned long long span_lo, span_hi;
   const uint32_t i = blockIdx.x * kWireBlock + threadIdx.x;
   const bool live = i < a.n;
@@ -44,61 +47,101 @@ __global__ void __launch_bounds__(kWireBlock) txv_k_decode_msgs(WireArgs a) {
   __syncthreads();
   const uint64_t lo = span_lo & ~15ull, hi = span_hi;
   const bool staged = hi > lo && hi - lo <= kWireLds;
-  if (staged) {   // 16-byte coalesced loads of [lo, hi rounded up); the device buffer is padded
+  if (staged) {   // 16-byte coalesced loads of [lo, hi rounded up); the device buffer is padded.
+    // All of a lane's loads are issued before the first LDS store so they are in flight together.
     const uint32_t nvec = (uint32_t)((hi - lo + 15) >> 4);
     const uint4* src = reinterpret_cast<const uint4*>(a.wire + lo);
     uint4* dst = reinterpret_cast<uint4*>(lds_w);
-    for (uint32_t v = threadIdx.x; v < nvec; v += kWireBlock) dst[v] = src[v];
+    constexpr uint32_t kPer = (kWireLds / 16 + kWireBlock - 1) / kWireBlock;
+    uint4 r[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t v = threadIdx.x + k * kWireBlock;
+      r[k] = src[v < nvec ? v : nvec - 1];   // clamped: unconditional, all in flight
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t v = threadIdx.x + k * kWireBlock;
+      if (v < nvec) dst[v] = r[k];
+    }
   }
   __syncthreads();
-  if (!live) return;
 
   Parsed o{};
   uint32_t st = 1;   // TXV_WIRE_TOO_LARGE
   if (len == 0) st = 3;
   else if (parse) {
-    if (staged) {
-      const uint8_t* b = reinterpret_cast<const uint8_t*>(lds_w) + (uint32_t)(off - lo);
-      st = parse_msg(b, len, a.disamb, a.prefix, o);
+    // canonical layout: branch-free fast path; everything else: the general parser
+#ifdef TXV_WIRE_NOPARSE   // experiment: memory structure only
+    const bool fast = true;
+    o.sig_len = 64; o.sig_off = (uint32_t)(off & 7u); o.addr_len = 20; o.has_key = true;
+#else
+    const bool fast = staged ? fast_msg(lds_w, (uint32_t)(off - lo), len, a.prefix, o)
+                             : fast_msg(reinterpret_cast<const uint32_t*>(a.wire) + (off >> 2), (uint32_t)(off & 3u),
+                                        len, a.prefix, o);
+#endif
+    if (fast) {
+      st = 0;
     } else {
-      st = parse_msg(a.wire + off, len, a.disamb, a.prefix, o);
+      o = Parsed{};
+      if (staged) {
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(lds_w) + (uint32_t)(off - lo);
+        st = parse_msg(b, len, a.disamb, a.prefix, o);
+      } else {
+        st = parse_msg(a.wire + off, len, a.disamb, a.prefix, o);
+      }
     }
   }
   if (st != 0) o = Parsed{};
 
-  uint32_t key[8], addr[5], sig[16];
+  // rows: only fields that exist are read (reads run up to 4 * (W + 1) bytes past a field's aligned
+  // start: LDS slack / 128 bytes of padding behind the wire buffer)
+  uint32_t key[8] = {}, addr[5] = {}, sig[16] = {};
   const uint32_t sig_n = o.sig_len < 64 ? o.sig_len : 64u, addr_n = o.addr_len < 20 ? o.addr_len : 20u;
-  if (staged) {
-    const uint32_t base = (uint32_t)(off - lo);
-    copy_row<8>(lds_w, base + o.key_off, o.has_key ? 32u : 0u, key);
-    copy_row<5>(lds_w, base + o.addr_off, addr_n, addr);
-    copy_row<16>(lds_w, base + o.sig_off, sig_n, sig);
-  } else {
-    const uint32_t* gw = reinterpret_cast<const uint32_t*>(a.wire);
-    const uint64_t base = off;
-    // global rows: re-base the word pointer at the message's aligned start
-    const uint32_t* mw = gw + (base >> 2);
-    const uint32_t b3 = (uint32_t)(base & 3u);
-    copy_row<8>(mw, b3 + o.key_off, o.has_key ? 32u : 0u, key);
-    copy_row<5>(mw, b3 + o.addr_off, addr_n, addr);
-    copy_row<16>(mw, b3 + o.sig_off, sig_n, sig);
+  if (st == 0) {
+    if (staged) {
+      const uint32_t base = (uint32_t)(off - lo);
+      if (o.has_key) copy_row<8>(lds_w, base + o.key_off, 32u, key);
+      if (addr_n) copy_row<5>(lds_w, base + o.addr_off, addr_n, addr);
+      if (sig_n) copy_row<16>(lds_w, base + o.sig_off, sig_n, sig);
+    } else {   // word pointer re-based at the message's aligned start
+      const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.wire) + (off >> 2);
+      const uint32_t b3 = (uint32_t)(off & 3u);
+      if (o.has_key) copy_row<8>(mw, b3 + o.key_off, 32u, key);
+      if (addr_n) copy_row<5>(mw, b3 + o.addr_off, addr_n, addr);
+      if (sig_n) copy_row<16>(mw, b3 + o.sig_off, sig_n, sig);
+    }
   }
-  a.status[i] = (uint8_t)st;
-  a.height[i] = o.height;
-  a.ts_sec[i] = o.sec;
-  a.ts_nanos[i] = o.nanos;
-  const uint32_t moff = (uint32_t)off;   // wire_bytes < 2^32 (host check)
-  a.txhash_off[i] = st == 0 ? moff + o.th_off : 0u;
-  a.txhash_len[i] = o.th_len;
-  a.addr_len[i] = o.addr_len;
-  a.sig_off[i] = st == 0 ? moff + o.sig_off : 0u;
-  a.sig_len[i] = o.sig_len;
+  if (live) {   // per-message columns: lane i writes element i (coalesced)
+    a.status[i] = (uint8_t)st;
+    a.height[i] = o.height;
+    a.ts_sec[i] = o.sec;
+    a.ts_nanos[i] = o.nanos;
+    const uint32_t moff = (uint32_t)off;   // wire_bytes < 2^32 (host check)
+    a.txhash_off[i] = st == 0 ? moff + o.th_off : 0u;
+    a.txhash_len[i] = o.th_len;
+    a.addr_len[i] = o.addr_len;
+    a.sig_off[i] = st == 0 ? moff + o.sig_off : 0u;
+    a.sig_len[i] = o.sig_len;
+  }
+  // rows (TxKey 8, address 5, signature 16 words per message): transposed through LDS so every
+  // store instruction writes 64 consecutive words instead of one word per 32/20/64-byte row
+  constexpr uint32_t R = 29;   // odd stride: conflict-free row writes
+  static_assert(kWireBlock * R <= kWireLds / 4, "row stage does not fit the LDS buffer");
+  __syncthreads();             // every lane is done reading the staged messages
+  uint32_t* row = lds_w + threadIdx.x * R;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a.txkey[(size_t)i * 8 + j] = key[j];
+  for (int j = 0; j < 8; ++j) row[j] = key[j];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) a.addr[(size_t)i * 5 + j] = addr[j];
+  for (int j = 0; j < 5; ++j) row[8 + j] = addr[j];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) a.sig[(size_t)i * 16 + j] = sig[j];
+  for (int j = 0; j < 16; ++j) row[13 + j] = sig[j];
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * kWireBlock;
+  const uint32_t nb = a.n - i0 < kWireBlock ? a.n - i0 : kWireBlock;   // messages of this block
+  for (uint32_t w = threadIdx.x; w < nb * 8; w += kWireBlock) a.txkey[(size_t)i0 * 8 + w] = lds_w[(w >> 3) * R + (w & 7)];
+  for (uint32_t w = threadIdx.x; w < nb * 5; w += kWireBlock) a.addr[(size_t)i0 * 5 + w] = lds_w[(w / 5) * R + 8 + w % 5];
+  for (uint32_t w = threadIdx.x; w < nb * 16; w += kWireBlock) a.sig[(size_t)i0 * 16 + w] = lds_w[(w >> 4) * R + 13 + (w & 15)];
 }
 
 extern "C" hipError_t txv_launch_decode_msgs(const WireArgs* a, hipStream_t st) {

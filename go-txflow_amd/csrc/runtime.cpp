@@ -1501,8 +1501,8 @@ int txv_decode_stage(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const
       return r;
     c->wd_cap = cap;
   }
-  if (wire_bytes + 64 > c->wd_bytes_cap) {
-    const uint64_t cap = std::max<uint64_t>(wire_bytes + 64, 1u << 20);
+  if (wire_bytes + 128 > c->wd_bytes_cap) {   // 128 bytes of padding: kernels_wire.hip row reads
+    const uint64_t cap = std::max<uint64_t>(wire_bytes + 128, 1u << 20);
     if ((r = dalloc(c, &c->d_wd_wire, cap)) || (r = halloc(c, &c->h_wd_wire, cap))) return r;
     c->wd_bytes_cap = cap;
   }
@@ -1511,10 +1511,10 @@ int txv_decode_stage(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const
     const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
     memcpy(c->h_wd_wire + a, wire + a, b - a);
   }, 16);
-  memset(c->h_wd_wire + wire_bytes, 0, 64);
+  memset(c->h_wd_wire + wire_bytes, 0, 128);
   memcpy(c->h_wd_off, msg_off, (size_t)n * 8);
   memcpy(c->h_wd_len, msg_len, (size_t)n * 4);
-  HIP_TRY(c, hipMemcpyAsync(c->d_wd_wire, c->h_wd_wire, wire_bytes + 64, hipMemcpyHostToDevice, c->key_stream));
+  HIP_TRY(c, hipMemcpyAsync(c->d_wd_wire, c->h_wd_wire, wire_bytes + 128, hipMemcpyHostToDevice, c->key_stream));
   if (n) {
     HIP_TRY(c, hipMemcpyAsync(c->d_wd_off, c->h_wd_off, (size_t)n * 8, hipMemcpyHostToDevice, c->key_stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_wd_len, c->h_wd_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));

@@ -71,7 +71,7 @@ struct SignArgs {
 struct WireArgs {
   uint32_t n, max_msg_bytes;
   uint32_t disamb, prefix;     // amino disambiguation (3 bytes) / prefix (4 bytes), little-endian packed
-  const uint8_t* wire;         // messages, padded by >= 16 bytes
+  const uint8_t* wire;         // messages, padded by >= 128 bytes
   const uint64_t* off;         // [n]
   const uint32_t* len;         // [n]
   uint8_t* status;             // [n]

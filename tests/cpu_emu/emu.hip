@@ -94,18 +94,32 @@ int emu_verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const ui
 // form): the message sits at byte `shift` (0..3) of a word buffer.  Returns the TXV_WIRE_* status;
 // i64: height, ts_sec; u32: ts_nanos, txhash_off, txhash_len, addr_len, sig_off, sig_len;
 // rows: TxKey 8 words, address 5, signature 16.
+static uint64_t fast_hits = 0;
+uint64_t emu_wire_fast_hits() { return fast_hits; }
+// general parser only (the oracle-independent reference for the fast path)
+int emu_wire_decode_general(const uint8_t* msg, uint32_t len, uint32_t disamb, uint32_t prefix) {
+  using namespace txv::wire;
+  Parsed o{};
+  return len ? (int)parse_msg(msg, len, disamb, prefix, o) : 3;
+}
 int emu_wire_decode(const uint8_t* msg, uint32_t len, uint32_t max_msg, uint32_t disamb, uint32_t prefix,
                     uint32_t shift, int64_t* i64, uint32_t* u32, uint32_t* rows) {
   using namespace txv::wire;
-  std::vector<uint32_t> words((len + shift + 3) / 4 + 4, 0xA5A5A5A5u);
+  std::vector<uint32_t> words((len + shift + 3) / 4 + 24, 0xA5A5A5A5u);   // kernel: 128 B padding
   uint8_t* bytes = reinterpret_cast<uint8_t*>(words.data());
   memcpy(bytes + shift, msg, len);
   Parsed o{};
-  uint32_t st = len == 0 ? 3u : (len > max_msg ? 1u : parse_msg((const uint8_t*)(bytes + shift), len, disamb, prefix, o));
+  uint32_t st = len == 0 ? 3u : (len > max_msg ? 1u : 4u);
+  if (st == 4u) {   // as the kernel: fast path, else the general parser (fast_hits counts the former)
+    if (fast_msg((const uint32_t*)words.data(), shift, len, prefix, o)) { st = 0; ++fast_hits; }
+    else { o = Parsed{}; st = parse_msg((const uint8_t*)(bytes + shift), len, disamb, prefix, o); }
+  }
   if (st != 0) o = Parsed{};
-  copy_row<8>((const uint32_t*)words.data(), shift + o.key_off, o.has_key ? 32u : 0u, rows);
-  copy_row<5>((const uint32_t*)words.data(), shift + o.addr_off, o.addr_len < 20 ? o.addr_len : 20u, rows + 8);
-  copy_row<16>((const uint32_t*)words.data(), shift + o.sig_off, o.sig_len < 64 ? o.sig_len : 64u, rows + 13);
+  memset(rows, 0, 29 * 4);
+  const uint32_t an = o.addr_len < 20 ? o.addr_len : 20u, sn = o.sig_len < 64 ? o.sig_len : 64u;
+  if (o.has_key) copy_row<8>((const uint32_t*)words.data(), shift + o.key_off, 32u, rows);
+  if (an) copy_row<5>((const uint32_t*)words.data(), shift + o.addr_off, an, rows + 8);
+  if (sn) copy_row<16>((const uint32_t*)words.data(), shift + o.sig_off, sn, rows + 13);
   i64[0] = o.height; i64[1] = o.sec;
   u32[0] = (uint32_t)o.nanos; u32[1] = o.th_off; u32[2] = o.th_len; u32[3] = o.addr_len; u32[4] = o.sig_off;
   u32[5] = o.sig_len;

@@ -27,6 +27,7 @@ def emu():
         subprocess.run(["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "-shared", src, "-o", EMU], check=True)
     E = ctypes.CDLL(EMU)
     E.emu_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
+    E.emu_wire_fast_hits.restype = ctypes.c_uint64
     E.emu_wire_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return E
@@ -79,7 +80,13 @@ def test_wire_decoder_source_vs_oracle(emu):
     i64 = np.zeros(2, np.int64)
     u32 = np.zeros(6, np.uint32)
     rows = np.zeros(29, np.uint32)
-    for k, m in enumerate(G.messages(6000, seed=5)):
+    import random
+    rng = random.Random(9)
+    canon = [G.message(G.rand_vote(rng), rng, False) for _ in range(3000)]
+    mixed = G.messages(6000, seed=5)
+    near = [G.mutate(m, rng) for m in canon[:3000]]   # one edit away from the fast path's layout
+    h0 = emu.emu_wire_fast_hits()
+    for k, m in enumerate(mixed + canon + near):
         mx = 300 if k % 5 == 0 else 1 << 20
         st = emu.emu_wire_decode(m, len(m), mx, disamb, prefix, k % 4, i64.ctypes.data, u32.ctypes.data,
                                  rows.ctypes.data)
@@ -95,3 +102,4 @@ def test_wire_decoder_source_vs_oracle(emu):
         assert rb[:32] == f["txkey"], k
         assert rb[32:52] == f["addr"][:20] + bytes(20 - min(al, 20)), k
         assert rb[52:116] == f["sig"][:64] + bytes(64 - min(sl, 64)), k
+    assert emu.emu_wire_fast_hits() - h0 > 2500   # canonical messages with <= 7-byte varints: fast path
