@@ -140,14 +140,14 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     return out
 
 
-WIRE_OUT_BYTES = 157   # per decoded message: status 1, height 8, ts 8 + 4, 5 x u32, TxKey 32, addr 20, sig 64
+WIRE_OUT_BYTES = 160   # per decoded message: one record (status, height, ts, offsets, lengths, TxKey, addr, sig)
 
 
 def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
     """Reactor.Receive's decodeMsg for the C2 votes as received TxVoteMessage wire
     bytes (txv_encode_msgs = the sender's MarshalBinaryBare), decoded on the GPU (txv_k_decode_msgs)
     from a batch resident in HBM.  Roofline: HBM, algorithmic bytes = wire bytes + 12 B of offset /
-    length per message read + 157 B of columns written.  Also the host-inclusive rate (upload,
+    length per message read + a 160 B record written.  Also the host-inclusive rate (upload,
     decode, results copied into the caller's arrays) and the oracle's C decoder on one host thread."""
     import txflow_amd as T
     wb = T.encode_msgs(wl.batch)

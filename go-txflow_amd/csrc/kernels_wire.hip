@@ -112,36 +112,37 @@ __global__ void __launch_bounds__(kWireBlock) txv_k_decode_msgs(WireArgs a) {
       if (sig_n) copy_row<16>(mw, b3 + o.sig_off, sig_n, sig);
     }
   }
-  if (live) {   // per-message columns: lane i writes element i (coalesced)
-    a.status[i] = (uint8_t)st;
-    a.height[i] = o.height;
-    a.ts_sec[i] = o.sec;
-    a.ts_nanos[i] = o.nanos;
-    const uint32_t moff = (uint32_t)off;   // wire_bytes < 2^32 (host check)
-    a.txhash_off[i] = st == 0 ? moff + o.th_off : 0u;
-    a.txhash_len[i] = o.th_len;
-    a.addr_len[i] = o.addr_len;
-    a.sig_off[i] = st == 0 ? moff + o.sig_off : 0u;
-    a.sig_len[i] = o.sig_len;
-  }
-  // rows (TxKey 8, address 5, signature 16 words per message): transposed through LDS so every
-  // store instruction writes 64 consecutive words instead of one word per 32/20/64-byte row
-  constexpr uint32_t R = 29;   // odd stride: conflict-free row writes
-  static_assert(kWireBlock * R <= kWireLds / 4, "row stage does not fit the LDS buffer");
-  __syncthreads();             // every lane is done reading the staged messages
+  // one 160-byte record per message, transposed through LDS so the block writes its records as one
+  // contiguous stream of 16-byte stores (instead of one word per lane per 32/20/64-byte row)
+  constexpr uint32_t R = TXV_WIRE_REC_WORDS + 1;   // odd stride: conflict-free record writes
+  static_assert(kWireBlock * R <= kWireLds / 4, "record stage does not fit the LDS buffer");
+  __syncthreads();                                  // every lane is done reading the staged messages
   uint32_t* row = lds_w + threadIdx.x * R;
+  const uint32_t moff = (uint32_t)off;              // wire_bytes < 2^32 (host check)
+  row[0] = st;
+  row[1] = (uint32_t)(uint64_t)o.height; row[2] = (uint32_t)((uint64_t)o.height >> 32);
+  row[3] = (uint32_t)(uint64_t)o.sec; row[4] = (uint32_t)((uint64_t)o.sec >> 32);
+  row[5] = (uint32_t)o.nanos;
+  row[6] = st == 0 ? moff + o.th_off : 0u;
+  row[7] = o.th_len;
+  row[8] = o.addr_len;
+  row[9] = st == 0 ? moff + o.sig_off : 0u;
+  row[10] = o.sig_len;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) row[j] = key[j];
+  for (int j = 0; j < 8; ++j) row[11 + j] = key[j];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) row[8 + j] = addr[j];
+  for (int j = 0; j < 5; ++j) row[19 + j] = addr[j];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) row[13 + j] = sig[j];
+  for (int j = 0; j < 16; ++j) row[24 + j] = sig[j];
   __syncthreads();
   const uint32_t i0 = blockIdx.x * kWireBlock;
   const uint32_t nb = a.n - i0 < kWireBlock ? a.n - i0 : kWireBlock;   // messages of this block
-  for (uint32_t w = threadIdx.x; w < nb * 8; w += kWireBlock) a.txkey[(size_t)i0 * 8 + w] = lds_w[(w >> 3) * R + (w & 7)];
-  for (uint32_t w = threadIdx.x; w < nb * 5; w += kWireBlock) a.addr[(size_t)i0 * 5 + w] = lds_w[(w / 5) * R + 8 + w % 5];
-  for (uint32_t w = threadIdx.x; w < nb * 16; w += kWireBlock) a.sig[(size_t)i0 * 16 + w] = lds_w[(w >> 4) * R + 13 + (w & 15)];
+  constexpr uint32_t C = TXV_WIRE_REC_WORDS / 4;                        // 16-byte chunks per record
+  uint4* dst = reinterpret_cast<uint4*>(a.rec + (size_t)i0 * TXV_WIRE_REC_WORDS);
+  for (uint32_t c = threadIdx.x; c < nb * C; c += kWireBlock) {
+    const uint32_t* r = lds_w + (c / C) * R + 4 * (c % C);
+    dst[c] = make_uint4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 extern "C" hipError_t txv_launch_decode_msgs(const WireArgs* a, hipStream_t st) {

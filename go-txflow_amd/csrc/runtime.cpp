@@ -1444,24 +1444,8 @@ int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* 
 
 namespace {
 
-// packed per-message outputs of txv_k_decode_msgs, column blocks in this order
-struct WireCols {
-  uint8_t* status; int64_t* height; int64_t* ts_sec; int32_t* ts_nanos;
-  uint32_t *txhash_off, *txhash_len, *addr_len, *sig_off, *sig_len, *txkey, *addr, *sig;
-};
-constexpr size_t kWireOutBytes = 8 + 8 + 4 + 5 * 4 + 32 + 20 + 64 + 1;   // per message
-WireCols wire_cols(uint8_t* base, uint32_t cap) {
-  WireCols w;
-  size_t o = 0;
-  auto take = [&](size_t bytes) { uint8_t* p = base + o; o += (bytes * cap + 255) / 256 * 256; return p; };
-  w.height = (int64_t*)take(8); w.ts_sec = (int64_t*)take(8); w.ts_nanos = (int32_t*)take(4);
-  w.txhash_off = (uint32_t*)take(4); w.txhash_len = (uint32_t*)take(4); w.addr_len = (uint32_t*)take(4);
-  w.sig_off = (uint32_t*)take(4); w.sig_len = (uint32_t*)take(4);
-  w.txkey = (uint32_t*)take(32); w.addr = (uint32_t*)take(20); w.sig = (uint32_t*)take(64);
-  w.status = take(1);
-  return w;
-}
-size_t wire_out_bytes(uint32_t cap) { return kWireOutBytes * cap + 12 * 256; }
+// records of txv_k_decode_msgs (TXV_WIRE_REC_WORDS u32 per message, txv_device.h)
+size_t wire_out_bytes(uint32_t cap) { return (size_t)cap * TXV_WIRE_REC_WORDS * 4; }
 
 // amino nameToDisfix("tendermint/txvotepool/TxVoteMessage") (go-amino, external): SHA-256 of the
 // registered name, leading zero bytes skipped, 3 disambiguation bytes, zero bytes skipped, 4 prefix bytes
@@ -1536,10 +1520,7 @@ int txv_decode_run(txv_ctx* c, uint32_t max_msg_bytes, uint32_t reps, float* ker
   a.max_msg_bytes = max_msg_bytes;
   txvote_msg_disfix(&a.disamb, &a.prefix);
   a.wire = c->d_wd_wire; a.off = c->d_wd_off; a.len = c->d_wd_len;
-  const WireCols w = wire_cols(c->d_wd_out, c->wd_cap);
-  a.status = w.status; a.height = w.height; a.ts_sec = w.ts_sec; a.ts_nanos = w.ts_nanos;
-  a.txhash_off = w.txhash_off; a.txhash_len = w.txhash_len; a.addr_len = w.addr_len; a.sig_off = w.sig_off;
-  a.sig_len = w.sig_len; a.txkey = w.txkey; a.addr = w.addr; a.sig = w.sig;
+  a.rec = reinterpret_cast<uint32_t*>(c->d_wd_out);
   if (!reps) reps = 1;
   HIP_TRY(c, hipEventRecord(c->wd_ev[0], c->key_stream));
   for (uint32_t k = 0; k < reps; ++k) HIP_TRY(c, txv_launch_decode_msgs(&a, c->key_stream));
@@ -1561,23 +1542,25 @@ int txv_decode_fetch(txv_ctx* c, const txv_wire_votes* out) {
   if (!c->wd_ran) { c->err = "txv_decode_fetch before txv_decode_run"; return TXV_ESTATE; }
   const uint32_t n = c->wd_n;
   if (!n) return TXV_OK;
-  HIP_TRY(c, hipMemcpyAsync(c->h_wd_out, c->d_wd_out, wire_out_bytes(c->wd_cap), hipMemcpyDeviceToHost, c->key_stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_wd_out, c->d_wd_out, wire_out_bytes(n), hipMemcpyDeviceToHost, c->key_stream));
   HIP_TRY(c, hipStreamSynchronize(c->key_stream));
-  const WireCols w = wire_cols(c->h_wd_out, c->wd_cap);
-  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-    const size_t m = hi - lo;
-    if (out->status) memcpy(out->status + lo, w.status + lo, m);
-    if (out->height) memcpy(out->height + lo, w.height + lo, m * 8);
-    if (out->ts_sec) memcpy(out->ts_sec + lo, w.ts_sec + lo, m * 8);
-    if (out->ts_nanos) memcpy(out->ts_nanos + lo, w.ts_nanos + lo, m * 4);
-    if (out->txhash_off) memcpy(out->txhash_off + lo, w.txhash_off + lo, m * 4);
-    if (out->txhash_len) memcpy(out->txhash_len + lo, w.txhash_len + lo, m * 4);
-    if (out->addr_len) memcpy(out->addr_len + lo, w.addr_len + lo, m * 4);
-    if (out->sig_len) memcpy(out->sig_len + lo, w.sig_len + lo, m * 4);
-    if (out->sig_off) for (uint32_t i = lo; i < hi; ++i) out->sig_off[i] = w.sig_off[i];
-    if (out->txkey) memcpy(out->txkey + (size_t)lo * 32, w.txkey + (size_t)lo * 8, m * 32);
-    if (out->addr) memcpy(out->addr + (size_t)lo * 20, w.addr + (size_t)lo * 5, m * 20);
-    if (out->sig) memcpy(out->sig + (size_t)lo * 64, w.sig + (size_t)lo * 16, m * 64);
+  const uint32_t* rec = reinterpret_cast<const uint32_t*>(c->h_wd_out);
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {   // records -> the caller's columns
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t* r = rec + (size_t)i * TXV_WIRE_REC_WORDS;
+      if (out->status) out->status[i] = (uint8_t)r[0];
+      if (out->height) out->height[i] = (int64_t)((uint64_t)r[1] | ((uint64_t)r[2] << 32));
+      if (out->ts_sec) out->ts_sec[i] = (int64_t)((uint64_t)r[3] | ((uint64_t)r[4] << 32));
+      if (out->ts_nanos) out->ts_nanos[i] = (int32_t)r[5];
+      if (out->txhash_off) out->txhash_off[i] = r[6];
+      if (out->txhash_len) out->txhash_len[i] = r[7];
+      if (out->addr_len) out->addr_len[i] = r[8];
+      if (out->sig_off) out->sig_off[i] = r[9];
+      if (out->sig_len) out->sig_len[i] = r[10];
+      if (out->txkey) memcpy(out->txkey + (size_t)i * 32, r + 11, 32);
+      if (out->addr) memcpy(out->addr + (size_t)i * 20, r + 19, 20);
+      if (out->sig) memcpy(out->sig + (size_t)i * 64, r + 24, 64);
+    }
   }, 8192);
   return TXV_OK;
 }

@@ -67,21 +67,19 @@ struct SignArgs {
 };
 
 // TxVoteMessage wire decode (kernels_wire.hip): statuses are include/txvote.h's TXV_WIRE_*
-// (0 ok, 1 too large, 2 amino error, 3 empty/nil); offsets are absolute into `wire`
+// (0 ok, 1 too large, 2 amino error, 3 empty/nil).  Output: one 160-byte record per message
+// (TXV_WIRE_REC_WORDS u32, written as one contiguous stream), word layout:
+//   0 status | 1-2 height | 3-4 ts_sec | 5 ts_nanos | 6 txhash_off | 7 txhash_len | 8 addr_len |
+//   9 sig_off | 10 sig_len | 11-18 TxKey | 19-23 address (first 20 bytes) | 24-39 signature (first 64)
+// offsets are absolute into `wire`; row bytes beyond a field's length are zero.
+#define TXV_WIRE_REC_WORDS 40
 struct WireArgs {
   uint32_t n, max_msg_bytes;
   uint32_t disamb, prefix;     // amino disambiguation (3 bytes) / prefix (4 bytes), little-endian packed
   const uint8_t* wire;         // messages, padded by >= 128 bytes
   const uint64_t* off;         // [n]
   const uint32_t* len;         // [n]
-  uint8_t* status;             // [n]
-  int64_t* height;             // [n]
-  int64_t* ts_sec;             // [n]
-  int32_t* ts_nanos;           // [n]
-  uint32_t *txhash_off, *txhash_len, *addr_len, *sig_off, *sig_len;   // [n]
-  uint32_t* txkey;             // [n][8]
-  uint32_t* addr;              // [n][5]  first 20 bytes, zero beyond the length
-  uint32_t* sig;               // [n][16] first 64 bytes, zero beyond the length
+  uint32_t* rec;               // [n][TXV_WIRE_REC_WORDS]
 };
 
 extern "C" {

@@ -23,6 +23,6 @@ ctx.decode_run(reps=3)
 best = min(ctx.decode_run(reps=reps) for _ in range(3))
 d = ctx.decode_fetch(wb)
 ok = bool((d.status[:n] == 0).all() and (d.sig[:n].reshape(-1) == b.sig).all() and (d.height[:n] == 1).all())
-alg = wb.nbytes + n * (12 + 157)
+alg = wb.nbytes + n * (12 + 160)
 print(f"{os.environ.get('TXV_LIB_PATH', 'default')}: n={n} {wb.nbytes / n:.1f} B/msg  kernel {best:.4f} ms  "
       f"{n / best / 1e6:.2f} G msgs/s  {alg / best / 1e6:.0f} GB/s  ok={ok}", flush=True)
