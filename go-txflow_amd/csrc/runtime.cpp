@@ -148,6 +148,7 @@ struct txv_ctx {
   uint64_t *d_wd_off = nullptr, *h_wd_off = nullptr;
   uint32_t *d_wd_len = nullptr, *h_wd_len = nullptr;
   uint8_t *d_wd_out = nullptr, *h_wd_out = nullptr;
+  uint64_t *d_wd_span = nullptr, *h_wd_span = nullptr;   // [chunks][2] byte span of each 128-message chunk
   hipEvent_t wd_ev[2] = {nullptr, nullptr};
 };
 
@@ -891,7 +892,7 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_chain); dfree(c->d_chain_sign);
   dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
   dfree(c->d_wd_wire); hfree(c->h_wd_wire); dfree(c->d_wd_off); hfree(c->h_wd_off); dfree(c->d_wd_len); hfree(c->h_wd_len);
-  dfree(c->d_wd_out); hfree(c->h_wd_out);
+  dfree(c->d_wd_out); hfree(c->h_wd_out); dfree(c->d_wd_span); hfree(c->h_wd_span);
   for (auto& e : c->wd_ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -1481,7 +1482,9 @@ int txv_decode_stage(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     if ((r = dalloc(c, &c->d_wd_off, cap)) || (r = halloc(c, &c->h_wd_off, cap)) || (r = dalloc(c, &c->d_wd_len, cap)) ||
         (r = halloc(c, &c->h_wd_len, cap)) || (r = dalloc(c, &c->d_wd_out, wire_out_bytes(cap))) ||
-        (r = halloc(c, &c->h_wd_out, wire_out_bytes(cap))))
+        (r = halloc(c, &c->h_wd_out, wire_out_bytes(cap))) ||
+        (r = dalloc(c, &c->d_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))) ||
+        (r = halloc(c, &c->h_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))))
       return r;
     c->wd_cap = cap;
   }
@@ -1498,10 +1501,23 @@ int txv_decode_stage(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const
   memset(c->h_wd_wire + wire_bytes, 0, 128);
   memcpy(c->h_wd_off, msg_off, (size_t)n * 8);
   memcpy(c->h_wd_len, msg_len, (size_t)n * 4);
+  // per-chunk byte spans (the kernel stages a chunk into LDS when its span fits)
+  const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
+  c->pool->parallel_for(n_chunks, [&](uint32_t lo_c, uint32_t hi_c) {
+    for (uint32_t k = lo_c; k < hi_c; ++k) {
+      uint64_t lo = ~0ull, hi = 0;
+      for (uint32_t i = k * TXV_WIRE_BLOCK; i < std::min<uint32_t>(n, (k + 1) * TXV_WIRE_BLOCK); ++i)
+        if (msg_len[i]) { lo = std::min(lo, msg_off[i]); hi = std::max(hi, msg_off[i] + msg_len[i]); }
+      if (hi == 0) lo = 0;
+      c->h_wd_span[2 * k] = lo & ~15ull;
+      c->h_wd_span[2 * k + 1] = hi;
+    }
+  }, 64);
   HIP_TRY(c, hipMemcpyAsync(c->d_wd_wire, c->h_wd_wire, wire_bytes + 128, hipMemcpyHostToDevice, c->key_stream));
   if (n) {
     HIP_TRY(c, hipMemcpyAsync(c->d_wd_off, c->h_wd_off, (size_t)n * 8, hipMemcpyHostToDevice, c->key_stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_wd_len, c->h_wd_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_wd_span, c->h_wd_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, c->key_stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->key_stream));
   c->wd_n = n;
@@ -1521,9 +1537,13 @@ int txv_decode_run(txv_ctx* c, uint32_t max_msg_bytes, uint32_t reps, float* ker
   txvote_msg_disfix(&a.disamb, &a.prefix);
   a.wire = c->d_wd_wire; a.off = c->d_wd_off; a.len = c->d_wd_len;
   a.rec = reinterpret_cast<uint32_t*>(c->d_wd_out);
+  a.n_chunks = (a.n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
+  a.span = c->d_wd_span;
+  // persistent grid: 5 resident blocks per CU (LDS: 28.7 KB of staging per 128-message block)
+  const uint32_t grid = (uint32_t)c->n_cus * (getenv("TXV_WIRE_BPC") ? (uint32_t)atoi(getenv("TXV_WIRE_BPC")) : 5u);
   if (!reps) reps = 1;
   HIP_TRY(c, hipEventRecord(c->wd_ev[0], c->key_stream));
-  for (uint32_t k = 0; k < reps; ++k) HIP_TRY(c, txv_launch_decode_msgs(&a, c->key_stream));
+  for (uint32_t k = 0; k < reps; ++k) HIP_TRY(c, txv_launch_decode_msgs(&a, grid, c->key_stream));
   HIP_TRY(c, hipEventRecord(c->wd_ev[1], c->key_stream));
   HIP_TRY(c, hipEventSynchronize(c->wd_ev[1]));
   if (kernel_ms_avg) {

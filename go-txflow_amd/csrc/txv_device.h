@@ -73,8 +73,13 @@ struct SignArgs {
 //   9 sig_off | 10 sig_len | 11-18 TxKey | 19-23 address (first 20 bytes) | 24-39 signature (first 64)
 // offsets are absolute into `wire`; row bytes beyond a field's length are zero.
 #define TXV_WIRE_REC_WORDS 40
+#ifndef TXV_WIRE_BLOCK
+#define TXV_WIRE_BLOCK 128         // messages per chunk (one block iteration)
+#endif
 struct WireArgs {
   uint32_t n, max_msg_bytes;
+  uint32_t n_chunks, pad0;     // ceil(n / TXV_WIRE_BLOCK)
+  const uint64_t* span;        // [n_chunks][2]: 16-aligned start and end of the chunk's message bytes
   uint32_t disamb, prefix;     // amino disambiguation (3 bytes) / prefix (4 bytes), little-endian packed
   const uint8_t* wire;         // messages, padded by >= 128 bytes
   const uint64_t* off;         // [n]
@@ -83,7 +88,7 @@ struct WireArgs {
 };
 
 extern "C" {
-hipError_t txv_launch_decode_msgs(const WireArgs* args, hipStream_t st);
+hipError_t txv_launch_decode_msgs(const WireArgs* args, uint32_t grid, hipStream_t st);
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
