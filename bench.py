@@ -162,6 +162,16 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
               (d.sig[:n].reshape(-1) == b.sig).all() and (d.addr[:n].reshape(-1) == b.addr).all() and
               (d.txhash_len[:n] == b.txhash_len).all() and (d.sig_len[:n] == b.sig_len).all())
     alg = wb.nbytes + n * (12 + WIRE_OUT_BYTES)
+    traffic, pmc_src = None, None   # HBM bytes per launch from the committed PMC passes of this kernel
+    pmc = os.path.join(ROOT, "profiles", "pmc_wire.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pj = json.load(f)
+            if pj.get("msgs_per_launch") == n:
+                traffic, pmc_src = pj.get("traffic"), pj.get("source")
+        except Exception:
+            pass
     t0 = time.perf_counter()
     for _ in range(3):
         ctx.decode_msgs(wb)
@@ -170,7 +180,8 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
            "correct": ok, "msgs_per_s": round(n / (kms * 1e-3), 1), "kernel_ms": round(kms, 4),
            "roofline": {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": 8000.0,
                         "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / 8000.0, 4),
-                        "alg_bytes_per_launch": alg, "traffic": None},
+                        "alg_bytes_per_launch": alg, "traffic": traffic, "pmc_source": pmc_src,
+                        "kernel": "txv_k_decode_msgs"},
            "host_inclusive_msgs_per_s": round(n / host_s, 1)}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
