@@ -74,6 +74,7 @@ struct Slot {
   std::vector<int> lens;           // AddVote pack: SignBytes length (-1 amino error, -2 nil)
   std::vector<uint64_t> khash;     // AddVote pack: seeded hash of the TxHash bytes
   std::vector<uint32_t> vidx;      // AddVote pack: validator index or UINT32_MAX
+  std::vector<uint32_t> miss;      // AddVote pack: votes whose TxHash has no set yet
   // 0..2 kernel timing, 3 = the slot's uploads are done (copy stream), 4 = its results are in
   // the pinned buffers (compute stream)
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -522,14 +523,33 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   int r = ensure_slot(c, s, n, mw);
   if (r) return r;
   s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
-  // phase B (sequential, arrival order): TxHash -> set id, created on first sight
-  // (txflow/service.go:200-209, also for votes that then fail), touched-set list, the
-  // AddVote pre-checks (types/vote_set.go:92-105)
+  // phase B: TxHash -> set id, created on first sight in arrival order (txflow/service.go:200-209,
+  // also for votes that then fail), touched-set list, the AddVote pre-checks (types/vote_set.go:92-105).
+  // B1 (parallel): lookups of existing sets (read-only table) and the per-vote pre-checks;
+  // B2 (sequential, arrival order): the misses are interned -- new sets get their ids in
+  // first-seen order exactly as a sequential pass would assign them; B3: touched-set list.
   const uint32_t stage_id = ++c->stage_count;
   s.n_touched = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    s.h_flags[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0;
-    if (s.lens[i] == -2) { s.h_status[i] = TXV_ERR_NIL; continue; }
+  std::vector<uint32_t>& miss = s.miss;
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      s.h_flags[i] = 0; s.h_val[i] = 0;
+      if (s.lens[i] == -2) { s.h_status[i] = TXV_ERR_NIL; s.h_set[i] = UINT32_MAX - 1; continue; }
+      s.h_set[i] = c->tx_tab.find(v->txhash + v->txhash_off[i], v->txhash_len[i], s.khash[i]);
+      if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
+      const uint32_t vi = s.vidx[i];
+      if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
+      s.h_val[i] = vi;
+      // a SignBytes failure is only reached after the accepted-vote check (AddVote order), so
+      // the vote stays pending with BADMSG: it never verifies and the tally resolves it
+      s.h_status[i] = 0xFF;
+      s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
+    }
+  }, 4096);
+  miss.clear();
+  for (uint32_t i = 0; i < n; ++i)
+    if (s.h_set[i] == UINT32_MAX) miss.push_back(i);
+  for (const uint32_t i : miss) {
     bool created;
     const uint32_t sid = c->tx_tab.intern(v->txhash + v->txhash_off[i], v->txhash_len[i], s.khash[i], &created,
                                           c->cfg.max_txs);
@@ -538,19 +558,15 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_stage.push_back(0); c->set_tidx.push_back(0);
     }
     s.h_set[i] = sid;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t sid = s.h_set[i];
+    if (sid == UINT32_MAX - 1) { s.h_set[i] = 0; continue; }   // nil vote: no set
     if (c->seen_stage[sid] != stage_id) {
       c->seen_stage[sid] = stage_id;
       c->set_tidx[sid] = s.n_touched;
       s.h_touched[s.n_touched++] = sid;
     }
-    if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
-    const uint32_t vi = s.vidx[i];
-    if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
-    s.h_val[i] = vi;
-    // a SignBytes failure is only reached after the accepted-vote check (AddVote order), so
-    // the vote stays pending with BADMSG: it never verifies and the tally resolves it
-    s.h_status[i] = 0xFF;
-    s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
   }
   ht.mark("B");
   // phase C (parallel): column-major signature words and lengths; the SignBytes words are
