@@ -174,6 +174,7 @@ struct txv_pool {
   FlatIndex txs_map{&txs};                         // txsMap
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
+  std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -255,13 +256,26 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
+  // TxVote.Size() of every vote on the worker threads (order-independent)
+  p->sizes.resize(v->n);
+  {
+    const uint32_t n = v->n, nt = std::max(1u, std::min<uint32_t>(8, n / 8192));
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; ++t)
+      th.emplace_back([&, t] {
+        for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i)
+          p->sizes[i] = vote_size(v, i);
+      });
+    for (uint32_t i = 0; i < (uint32_t)((uint64_t)n / nt); ++i) p->sizes[i] = vote_size(v, i);
+    for (auto& x : th) x.join();
+  }
   constexpr uint32_t kAhead = 16;   // the loop is DRAM-latency bound: prefetch the hash slots ahead
   for (uint32_t i = 0; i < v->n; ++i) {
     if (i + kAhead < v->n) {
       if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
       p->txs_map.prefetch(keys[i + kAhead]);
     }
-    const uint32_t sz = vote_size(v, i);
+    const uint32_t sz = p->sizes[i];
     if (!sz) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
     if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
       status_out[i] = TXV_POOL_ERR_FULL;
