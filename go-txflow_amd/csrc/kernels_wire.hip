@@ -40,7 +40,7 @@ struct Prefetch {
 template <uint32_t K>
 __device__ __forceinline__ void load_vecs(u32x4 (&r)[kPer], const u32x4* src, uint32_t nv) {
   const uint32_t v = threadIdx.x + K * kWireBlock;
-  r[K] = src[v < nv ? v : nv - 1];
+  r[K] = __builtin_nontemporal_load(src + (v < nv ? v : nv - 1));   // streamed once: bypass-friendly
   if constexpr (K + 1 < kPer) load_vecs<K + 1>(r, src, nv);
 }
 template <uint32_t K>
@@ -155,10 +155,11 @@ __global__ void __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu
     const uint32_t i0 = c * kWireBlock;
     const uint32_t nb = a.n - i0 < kWireBlock ? a.n - i0 : kWireBlock;   // messages of this chunk
     constexpr uint32_t C = TXV_WIRE_REC_WORDS / 4;                        // 16-byte chunks per record
-    uint4* dst = reinterpret_cast<uint4*>(a.rec + (size_t)i0 * TXV_WIRE_REC_WORDS);
+    u32x4* dst = reinterpret_cast<u32x4*>(a.rec + (size_t)i0 * TXV_WIRE_REC_WORDS);
     for (uint32_t q = threadIdx.x; q < nb * C; q += kWireBlock) {
       const uint32_t* r = lds_w + (q / C) * R + 4 * (q % C);
-      dst[q] = make_uint4(r[0], r[1], r[2], r[3]);
+      const u32x4 val = {r[0], r[1], r[2], r[3]};
+      __builtin_nontemporal_store(val, dst + q);   // written once, read by the host copy
     }
   }
 }
