@@ -1095,6 +1095,22 @@ int txv_submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
 int txv_wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
                    uint32_t* n_ev) {
   if (!c) return TXV_EINVAL;
+  // wait for the batch's kernels without holding the context lock, so other threads' calls
+  // (pool ingest keys, decode) proceed meanwhile; the slot cannot be reused before this ticket
+  // is waited (submit refuses a slot whose ticket is set)
+  hipEvent_t done = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (ticket) {
+      const Slot& s = c->slots[(ticket - 1) % 2];
+      if (s.ticket == ticket && s.ran) done = s.ev[4];
+    }
+  }
+  if (done) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventSynchronize(done));
+  }
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   return wait_votes(c, ticket, status_out, ev, ev_cap, n_ev);
