@@ -77,6 +77,20 @@ struct FlatIndex {
       if (t[i].tag == tg && key_of(t[i].idx) == k) return t[i].idx;
     return -1;
   }
+  // one probe for "find, else insert": returns the existing index, or -1 after the caller's
+  // make_idx() result was inserted (capacity is ensured before probing)
+  template <typename F>
+  int32_t find_or_insert(const Key& k, F&& make_idx) {
+    if ((n + 1) * 2 > cap) grow();
+    const uint64_t hv = h(k);
+    const uint32_t tg = tag(hv);
+    size_t i = hv & mask;
+    for (; t[i].tag; i = (i + 1) & mask)
+      if (t[i].tag == tg && key_of(t[i].idx) == k) return t[i].idx;
+    t[i] = Slot{tg, make_idx()};
+    ++n;
+    return -1;
+  }
   void put(const Key& k, int32_t idx) {    // insert or overwrite
     if ((n + 1) * 2 > cap) grow();
     const uint64_t hv = h(k);
@@ -178,13 +192,17 @@ struct txv_pool {
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
-    const int32_t e = cache_map.find(k);
-    if (e >= 0) { cache.move_to_back(e); return false; }
-    if (cache.len >= cfg.cache_size && cache.head >= 0) {
+    if (cache.len >= cfg.cache_size && cache.head >= 0) {   // full: the eviction comes first
+      const int32_t e = cache_map.find(k);
+      if (e >= 0) { cache.move_to_back(e); return false; }
       cache_map.erase(cache.nodes[cache.head].k);   // before unlink: the index reads the node's key
       cache.unlink(cache.head);
+      cache_map.put(k, cache.push_back(k, 0));
+      return true;
     }
-    cache_map.put(k, cache.push_back(k, 0));
+    // not full: one probe finds the key or inserts it
+    const int32_t e = cache_map.find_or_insert(k, [&] { return cache.push_back(k, 0); });
+    if (e >= 0) { cache.move_to_back(e); return false; }
     return true;
   }
 };
