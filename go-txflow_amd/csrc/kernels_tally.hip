@@ -63,9 +63,16 @@ __device__ __forceinline__ bool sig_equals_vote(const TallyArgs& a, uint32_t i, 
   return d == 0;
 }
 
+// ADDED-vote list of a set kept in LDS when it has at most this many entries (every set of a
+// <= 256-validator registry): the crossing search reads it ~20 times
+constexpr uint32_t kListCap = 256;
+
 __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
+  __shared__ uint32_t l_vote[4][kListCap], l_val[4][kListCap];
+  __shared__ int64_t l_pow[4][kListCap];
   const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  const uint32_t wv = threadIdx.x >> 6;
   if (t >= a.n_touched) return;
   const uint32_t set = a.touched[t];
   const uint32_t beg = a.toff[t], end = a.toff[t + 1];
@@ -122,11 +129,13 @@ __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
       a.ent_vote[e] = i;
       a.ent_power[e] = pw;
       a.ent_val[e] = v;
+      if (e - beg < kListCap) { l_vote[wv][e - beg] = i; l_pow[wv][e - beg] = pw; l_val[wv][e - beg] = v; }
       batch += pw;
     }
     k += (uint32_t)__popcll(m);
   }
   __threadfence_block();   // the list written above is read back by other lanes of the wave
+  const bool in_lds = k <= kListCap;   // wave-uniform
 
   // pass 2: the commit crossing in arrival order
   const int64_t prior = a.set_sum[set];
@@ -145,8 +154,13 @@ __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
     for (int b = 31 - __builtin_clz(max(a.n, 2u) - 1u); b >= 0; --b) {
       const uint32_t cand = T | (1u << b);
       int64_t s = 0;
-      for (uint32_t c = lane; c < k; c += 64)
-        if (a.ent_vote[beg + c] < cand) s += a.ent_power[beg + c];
+      if (in_lds) {
+        for (uint32_t c = lane; c < k; c += 64)
+          if (l_vote[wv][c] < cand) s += l_pow[wv][c];
+      } else {
+        for (uint32_t c = lane; c < k; c += 64)
+          if (a.ent_vote[beg + c] < cand) s += a.ent_power[beg + c];
+      }
       if (wave_sum64(s) < need) T = cand;
     }
     cross = T;
@@ -154,10 +168,11 @@ __global__ void __launch_bounds__(256) txv_k_tally_sets(TallyArgs a) {
 
   // pass 3: ADDED statuses (+ fired bit) and the accepted-vote rows
   for (uint32_t e = lane; e < k; e += 64) {
-    const uint32_t ie = a.ent_vote[beg + e];
+    const uint32_t ie = in_lds ? l_vote[wv][e] : a.ent_vote[beg + e];
+    const uint32_t ve = in_lds ? l_val[wv][e] : a.ent_val[beg + e];
     const bool fire = cross != TXV_NO_CROSS && ie >= cross;
     a.status[ie] = TXV_ADDED_DEV | (fire ? 0x80u : 0u);
-    a.acc_slot[row + a.ent_val[beg + e]] = a.arena_base + ie + 1u;
+    a.acc_slot[row + ve] = a.arena_base + ie + 1u;
   }
   if (lane == 0) {
     a.set_sum[set] = total;
