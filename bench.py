@@ -229,7 +229,7 @@ def main():
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
     ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
                     help="base-point table window (0 = library default)")
-    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 2, 4, 8),
+    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the TxVoteMessage wire-decode leg")

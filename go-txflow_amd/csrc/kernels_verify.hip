@@ -12,6 +12,8 @@
 //
 // Launch geometry: 256-thread workgroups (4 waves), grid-stride over votes so each
 // workgroup stages the 55 KB B table into LDS once per launch, not once per 256 votes.
+#include <cstdlib>
+
 #include "ed25519_dev.h"
 #include "txv_device.h"
 
@@ -325,6 +327,106 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
   }
 }
 
+// Split mode (lane_votes = 1): the inversion leaves the scalar-multiply kernel.  Under SIMD a
+// wave pays the full inversion chain (254 S + 11 M wave instructions) however many of its
+// lanes' votes it covers, so its per-vote share only falls with more votes per LANE; inside
+// K1b that costs occupancy (V = 8 halves the waves of a 1M batch).  K1b-points therefore
+// stores R' = (X, Y, Z) per work entry, column-major by work index (coalesced, 96 B per vote),
+// and K1c gives each lane G entries: Montgomery's trick over G (3 multiplies per vote + one
+// inversion per G votes instead of per 4) followed by the canonical encoding and the compare
+// against the signature's R (x/crypto ed25519.Verify's final bytewise check).
+template <int BLOCK, int WB, int WA>
+__global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_points(VerifyArgs a) {
+  // XCD-aware split as in the multi kernel: the blocks of one XCD walk a contiguous eighth
+  const uint32_t n_grp = (a.n_work + 63u) & ~63u;
+  const uint32_t groups = gridDim.x >= 8 ? 8u : 1u;
+  const uint32_t grp = blockIdx.x % groups, blocks_in_grp = gridDim.x / groups + (grp < gridDim.x % groups);
+  const uint32_t chunk = ((n_grp + groups - 1) / groups + 63u) & ~63u;
+  const uint32_t lo = grp * chunk, hi = min(n_grp, lo + chunk);
+  const uint32_t stride = blocks_in_grp * BLOCK;
+  const size_t np = a.n_pad;
+#pragma unroll 1
+  for (uint32_t idx = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; idx < hi; idx += stride) {
+    if (idx >= a.n_work) continue;
+    const uint32_t i = a.order ? a.order[idx] : idx;
+    if (a.ok_out[i] != 2) continue;
+    uint32_t s[8], k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * np + i]; k[j] = a.kbuf[(size_t)j * np + i]; }
+    const ge_ext R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)a.val[i] * Tab<WA>::kWords, s, k, true);
+    uint32_t* o = a.rpts + idx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __builtin_nontemporal_store(R.X.v[j], o + (size_t)j * np);
+      __builtin_nontemporal_store(R.Y.v[j], o + (size_t)(8 + j) * np);
+      o[(size_t)(16 + j) * np] = R.Z.v[j];
+    }
+  }
+}
+
+// K1c: lane t takes the work entries (t & ~63) G + 64 h + (t & 63), h < G (a wave reads 64
+// consecutive entries per slot).  Pass 1 stores each active entry's exclusive prefix product
+// E_h = prod of the earlier active Z (words 24..31, skipped for the first); pass 2 walks back
+// from 1/P: 1/Z_h = E_h / (E_h Z_h), then 1/(E_h) = (1/(E_h Z_h)) Z_h.
+template <int G>
+__global__ void __launch_bounds__(64) txv_k_batch_encode(VerifyArgs a) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t base = (t & ~63u) * G + (t & 63u);
+  const size_t np = a.n_pad;
+  uint32_t act = 0;
+  fe P;
+#pragma unroll 1
+  for (int h = 0; h < G; ++h) {
+    const uint32_t idx = base + 64u * h;
+    if (idx >= a.n_work) break;
+    const uint32_t i = a.order ? a.order[idx] : idx;
+    if (a.ok_out[i] != 2) continue;
+    uint32_t* e = a.rpts + idx;
+    fe Z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Z.v[j] = e[(size_t)(16 + j) * np];
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[(size_t)(24 + j) * np] = P.v[j];
+      P = fe_mul(P, Z);
+    } else {
+      P = Z;
+    }
+    act |= 1u << h;
+  }
+  if (!act) return;
+  const int first = __builtin_ctz(act);
+  fe inv = fe_invert(P);
+#pragma unroll 1
+  for (int h = G - 1; h >= first; --h) {
+    if (!(act >> h & 1u)) continue;
+    const uint32_t idx = base + 64u * h;
+    const uint32_t i = a.order ? a.order[idx] : idx;
+    const uint32_t* e = a.rpts + idx;
+    fe X, Y, zi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      X.v[j] = __builtin_nontemporal_load(e + (size_t)j * np);
+      Y.v[j] = __builtin_nontemporal_load(e + (size_t)(8 + j) * np);
+    }
+    if (h > first) {
+      fe Z, E;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { Z.v[j] = e[(size_t)(16 + j) * np]; E.v[j] = e[(size_t)(24 + j) * np]; }
+      zi = fe_mul(inv, E);
+      inv = fe_mul(inv, Z);
+    } else {
+      zi = inv;
+    }
+    uint32_t enc[8];
+    ge_encode_zinv(enc, X, Y, zi);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * np + i];
+    a.ok_out[i] = diff == 0;
+  }
+}
+
 // ---------------------------------------------------------------- load generator
 // keygen: seed (32 B) -> expanded secret scalar a (mod L), prefix, public key encoding
 __global__ void __launch_bounds__(64) txv_k_keygen(const uint32_t* __restrict__ seeds_le, uint32_t n,
@@ -451,10 +553,42 @@ static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* t
                      tables, decode_ok, addr_words);
 }
 
-// V = 2: the LDS-parked pair kernel (WB = WA only); V = 4: parked in args->park
+// K1c's votes per lane: the largest G whose launch still gives every SIMD of the chip about
+// one wave (1024 SIMDs on MI355X), so the inversion's share per vote falls as the batch grows
+// without leaving SIMDs idle; TXV_K1C_G overrides it (experiments)
+static int k1c_votes_per_lane(uint32_t n_work) {
+  static const int forced = [] {
+    const char* e = getenv("TXV_K1C_G");
+    const int g = e ? atoi(e) : 0;
+    return (g == 4 || g == 8 || g == 16 || g == 32) ? g : 0;
+  }();
+  if (forced) return forced;
+  for (int g : {32, 16, 8})
+    if ((uint64_t)n_work >= (uint64_t)g * 64 * 1024) return g;
+  return 4;
+}
+
+static hipError_t launch_batch_encode(const VerifyArgs* args, hipStream_t st) {
+  const int g = k1c_votes_per_lane(args->n_work);
+  const uint32_t grid = (uint32_t)(((uint64_t)args->n_work + 64u * g - 1) / (64u * g));
+  switch (g) {
+    case 4: hipLaunchKernelGGL(txv_k_batch_encode<4>, dim3(grid), dim3(64), 0, st, *args); break;
+    case 8: hipLaunchKernelGGL(txv_k_batch_encode<8>, dim3(grid), dim3(64), 0, st, *args); break;
+    case 16: hipLaunchKernelGGL(txv_k_batch_encode<16>, dim3(grid), dim3(64), 0, st, *args); break;
+    default: hipLaunchKernelGGL(txv_k_batch_encode<32>, dim3(grid), dim3(64), 0, st, *args); break;
+  }
+  return hipSuccess;
+}
+
+// V = 2: the LDS-parked pair kernel (WB = WA only); V = 4: parked in args->park;
+// V = 1: split mode (points kernel, then K1c)
 template <int B, int WB, int WA>
 static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
-  if (args->lane_votes == 4) {
+  if (args->lane_votes == 1) {
+    if (!args->rpts) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((txv_k_scalarmult_points<B, WB, WA>), dim3(grid), dim3(B), 0, st, *args);
+    return launch_batch_encode(args, st);
+  } else if (args->lane_votes == 4) {
     hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 4>), dim3(grid), dim3(B), 0, st, *args);
   } else if (args->lane_votes == 8) {
     if constexpr (WB == 24) hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);

@@ -47,7 +47,7 @@ struct Slot {
   uint32_t* d_sig = nullptr; uint64_t* d_msg = nullptr; uint32_t* d_msg_len = nullptr;
   uint32_t* d_val = nullptr; uint32_t* d_set = nullptr; uint8_t* d_flags = nullptr;
   uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr; uint8_t* d_pre = nullptr;
-  uint32_t* d_kbuf = nullptr; uint32_t* d_order = nullptr; uint32_t* h_order = nullptr;
+  uint32_t* d_kbuf = nullptr; uint32_t* d_rpts = nullptr; uint32_t* d_order = nullptr; uint32_t* h_order = nullptr;
   uint32_t n_work = 0;
   // set-major tally order: pending votes grouped by (set, validator), arrival order inside
   uint32_t* d_toff = nullptr; uint32_t* h_toff = nullptr;
@@ -227,6 +227,7 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = dalloc(c, &s.d_msg_len, npad)) || (r = dalloc(c, &s.d_val, npad)) || (r = dalloc(c, &s.d_set, npad)) ||
         (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
         (r = dalloc(c, &s.d_pre, npad)) || (r = dalloc(c, &s.d_kbuf, 8 * npad)) ||
+        (c->lane_votes == 1 && (r = dalloc(c, &s.d_rpts, (size_t)TXV_RPTS_WORDS * npad))) ||
         (r = dalloc(c, &s.d_order, npad)) || (r = halloc(c, &s.h_order, npad)) ||
         (r = dalloc(c, &s.d_tvote, npad)) || (r = halloc(c, &s.h_tvote, npad)) ||
         (r = dalloc(c, &s.d_tval, npad)) || (r = halloc(c, &s.h_tval, npad)) ||
@@ -413,12 +414,14 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   a.order = by_val ? s.d_order : nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
   a.park = c->d_park;
+  a.rpts = s.d_rpts;
   a.lane_votes = c->lane_votes;
   return a;
 }
 
 // scratch for the V-1 parked results per K1b lane (the grid never exceeds verify_grid's cap)
 int ensure_park(txv_ctx* c) {
+  if (c->lane_votes == 1) return TXV_OK;   // split mode parks nothing
   const size_t words = (size_t)(c->lane_votes - 1) * TXV_PARK_WORDS * (size_t)c->n_cus * 2 * TXV_VERIFY_BLOCK;
   if (words <= c->park_words) return TXV_OK;
   int r;
@@ -679,7 +682,7 @@ int choose_window(const txv_ctx* c, uint32_t n) {
   if (c->cfg_w) return c->cfg_w;
   const uint64_t budget = (uint64_t)c->cfg.table_budget_mb << 20;
   for (int w : {20, 18, 16, 14, 12, 10, 8})
-    if ((w <= 16 || c->lane_votes >= 4) && (uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
+    if ((w <= 16 || c->lane_votes >= 4 || c->lane_votes == 1) && (uint64_t)std::max<uint32_t>(n, 1) * table_words(w) * 4 <= budget) return w;
   return 4;
 }
 
@@ -696,7 +699,7 @@ int select_window(txv_ctx* c, int w) {
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
   int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
-  if (c->lane_votes < 4 || !txv_verify_windows_supported(bw, w)) bw = w;
+  if ((c->lane_votes < 4 && c->lane_votes != 1) || !txv_verify_windows_supported(bw, w)) bw = w;
   if (bw != w) {
     if (c->btable_wide_w != bw) {
       dfree(c->d_btable_wide);
@@ -849,7 +852,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }
   if (TXV_CFG_LANE_VOTES(c->cfg.flags)) c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags);
-  if (c->lane_votes != 2 && c->lane_votes != 4 && c->lane_votes != 8) { delete c; return TXV_EINVAL; }
+  if (c->lane_votes != 1 && c->lane_votes != 2 && c->lane_votes != 4 && c->lane_votes != 8) { delete c; return TXV_EINVAL; }
   c->cfg_bw = (int)TXV_CFG_B_WINDOW(c->cfg.flags);
   if (c->cfg_bw && c->cfg_bw != 4 && !valid_window(c->cfg_bw) && c->cfg_bw != 20 && c->cfg_bw != 22 && c->cfg_bw != 24) {
     delete c;
@@ -892,7 +895,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->key_stream) (void)hipStreamSynchronize(c->key_stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
-    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_order); hfree(s.h_order);
+    dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_rpts); dfree(s.d_order); hfree(s.h_order);
     dfree(s.d_toff); hfree(s.h_toff); dfree(s.d_tvote); hfree(s.h_tvote); dfree(s.d_tval); hfree(s.h_tval);
     dfree(s.d_ent_vote); dfree(s.d_ent_power); dfree(s.d_ent_val); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);

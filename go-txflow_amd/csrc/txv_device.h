@@ -34,11 +34,15 @@ struct VerifyArgs {
   const uint32_t* btable;      // [kTableWords]
   uint8_t* ok_out;             // [n]
   uint32_t* park;              // [waves][V-1][32][64] parked points of the multi-vote K1b
-  uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2 or 4)
+  uint32_t lane_votes;         // V: votes per lane sharing one inversion at W >= 8 (2, 4, 8);
+                               // 1 = split: K1b stores R' per vote, K1c batch-inverts G per lane
+  uint32_t* rpts;              // split mode: [TXV_RPTS_WORDS][n_pad] per work entry: X, Y, Z of R',
+                               // then the exclusive prefix product of the lane's Z (K1b -> K1c)
 };
 
 #define TXV_PARK_WORDS 32          // X, Y, prefix product, Z of one parked vote
 #define TXV_MAX_LANE_VOTES 4
+#define TXV_RPTS_WORDS 32
 
 // TxVote.SignBytes on the device (kernels_signbytes.hip): fields in, msg words out
 struct SignBytesArgs {

@@ -376,8 +376,8 @@ class Context:
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
         if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20):
             raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16, 18, 20")
-        if lane_votes not in (0, 2, 4, 8):
-            raise ValueError("lane_votes must be 0 (default), 2, 4 or 8")
+        if lane_votes not in (0, 1, 2, 4, 8):
+            raise ValueError("lane_votes must be 0 (default), 1 (split K1b/K1c), 2, 4 or 8")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
                    (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16) | ((base_w & 0xFF) << 20),
                    table_budget_mb)

@@ -24,12 +24,14 @@ def main():
     ap.add_argument("--batches-per-epoch", type=int, default=4)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default="")
+    ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8))
     args = ap.parse_args()
     import oracle
     oracle.build()
     import txflow_amd as T
     import adversarial as A
-    ctx = T.Context(device=0, max_batch=args.batch + args.batch // 4, max_txs=1 << 17, max_validators=256)
+    ctx = T.Context(device=0, max_batch=args.batch + args.batch // 4, max_txs=1 << 17, max_validators=256,
+                    lane_votes=args.lane_votes)
     t0 = time.time()
     st = A.run_gate(ctx, args.votes, batch=args.batch, batches_per_epoch=args.batches_per_epoch,
                     threads=args.threads, log=lambda s: print(s, flush=True))
