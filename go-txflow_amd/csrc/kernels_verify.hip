@@ -15,9 +15,23 @@
 #include <cstdlib>
 
 #include "ed25519_dev.h"
+#include "fe_inv_var.h"
 #include "txv_device.h"
 
 using namespace txv;
+
+// K1b's shared inversion: the variable-time divstep inverse (fe_inv_var.h) or the Fermat
+// chain; the value is the same either way (encoding canonicalises)
+#ifndef TXV_INV_VAR
+#define TXV_INV_VAR 1
+#endif
+__device__ __forceinline__ fe verify_invert(const fe& z) {
+#if TXV_INV_VAR
+  return fe_invert_var(z);
+#else
+  return fe_invert(z);
+#endif
+}
 
 // ---------------------------------------------------------------- K0: tables
 // One lane per (point, position, chunk of 8 multiples): P_i = 2^(W i) A by W*i doublings,
@@ -137,7 +151,7 @@ __device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, 
     const uint32_t* ta = a.atables + (size_t)v * Tab<W>::kWords;
     ge_ext R = double_scalarmult_w<W>(btab, ta, s, k, true);
     uint32_t enc[8];
-    ge_encode(enc, R);
+    ge_encode_zinv(enc, R.X, R.Y, verify_invert(R.Z));
     uint32_t diff = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * a.n_pad + i];
@@ -214,7 +228,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
       Y0.v[j] = park[8 + j][threadIdx.x];
       Z0.v[j] = park[16 + j][threadIdx.x];
     }
-    const fe inv = fe_invert(fe_mul(Z0, R.Z));
+    const fe inv = verify_invert(fe_mul(Z0, R.Z));
     uint32_t enc[8];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -288,7 +302,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
         }
       }
     }
-    fe inv = fe_invert(P);
+    fe inv = verify_invert(P);
 #pragma unroll 1
     for (int h = V - 1; h >= 0; --h) {
       fe X, Y, Z, zi;
@@ -396,7 +410,7 @@ __global__ void __launch_bounds__(64) txv_k_batch_encode(VerifyArgs a) {
   }
   if (!act) return;
   const int first = __builtin_ctz(act);
-  fe inv = fe_invert(P);
+  fe inv = verify_invert(P);
 #pragma unroll 1
   for (int h = G - 1; h >= first; --h) {
     if (!(act >> h & 1u)) continue;

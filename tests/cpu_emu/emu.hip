@@ -4,6 +4,7 @@
 // ed25519_dev.h) for the host so logic errors in the kernel source can be localised on a
 // machine without a GPU.  It is not linked into libtxvote.so and the product never calls it.
 #include "../../go-txflow_amd/csrc/ed25519_dev.h"
+#include "../../go-txflow_amd/csrc/fe_inv_var.h"
 #include "../../go-txflow_amd/csrc/wire_dev.h"
 #include <cstring>
 #include <vector>
@@ -44,6 +45,7 @@ int emu_fe(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
     case 3: r = fe_sub(x, y); break;
     case 4: r = fe_canon(x); break;
     case 5: r = fe_invert(x); break;
+    case 7: r = fe_invert_var(x); break;
     default: {
       uint32_t t[16];
       for (int j = 0; j < 8; ++j) { t[j] = x.v[j]; t[8 + j] = y.v[j]; }
