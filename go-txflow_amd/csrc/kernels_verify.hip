@@ -250,6 +250,11 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 // 128 B per parked vote each way), so the register budget of the scalar multiply is
 // unchanged.  V = 4 saves 3/4 of an inversion (~190 squarings) per vote versus V = 1 and
 // fills 4 waves/SIMD in one round for a 1M-vote batch on 256 CUs.
+// TXV_PARK_LAST: the last vote's (X, Y, Z) is parked too, so only P is live in VGPRs across the
+// inversion (the divstep state needs ~40 VGPRs of the 128-VGPR / 4-wave budget)
+#ifndef TXV_PARK_LAST
+#define TXV_PARK_LAST 1
+#endif
 template <int BLOCK, int WB, int WA, int V>
 __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
   // lane group g = 64 w + l takes the work-list entries 64 V w + 64 h + l (h < V): the lanes of
@@ -267,7 +272,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
   // park layout: [wave][slot h][word][64 lanes]: a wave's stores of one word are one
   // contiguous 256-byte line and every offset is a compile-time immediate
   const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
-  uint32_t* park = a.park + (size_t)gwave * (V - 1) * TXV_PARK_WORDS * 64 + (threadIdx.x & 63);
+  uint32_t* park = a.park + (size_t)gwave * (V - 1 + TXV_PARK_LAST) * TXV_PARK_WORDS * 64 + (threadIdx.x & 63);
   for (uint32_t g = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; g < hi; g += stride) {
     uint32_t act = 0;
 #pragma unroll
@@ -291,7 +296,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
         R = ge_identity();
       }
       P = h ? fe_mul(P, R.Z) : R.Z;
-      if (h < V - 1) {
+      if (h < V - 1 || TXV_PARK_LAST) {
         uint32_t* slot = park + h * TXV_PARK_WORDS * 64;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -306,7 +311,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
 #pragma unroll 1
     for (int h = V - 1; h >= 0; --h) {
       fe X, Y, Z, zi;
-      if (h == V - 1) {
+      if (h == V - 1 && !TXV_PARK_LAST) {
         X = R.X; Y = R.Y; Z = R.Z;
       } else {
         const uint32_t* slot = park + h * TXV_PARK_WORDS * 64;

@@ -116,6 +116,7 @@ struct txv_ctx {
   uint32_t* d_btable_wide = nullptr;   // base-point table for b_w > tab_w (gigabytes at b_w >= 22)
   int btable_wide_w = 0;
   uint32_t lane_votes = 4;         // K1b votes per lane (one shared inversion)
+  bool lane_auto = true;           // no configured V: 8 for batches that still give >= 1.5 waves/SIMD
   uint32_t* d_park = nullptr;      // K1b parked points: [wave][V-1][32][64]
   size_t park_words = 0;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
@@ -419,10 +420,18 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   return a;
 }
 
-// scratch for the V-1 parked results per K1b lane (the grid never exceeds verify_grid's cap)
+// K1b votes per lane for a launch with base window wb.  V = 8 halves the inversions per vote
+// but also the waves; with the divstep inverse it wins once the batch still fills >= 1.5 waves
+// per SIMD (C2, 1M votes: 517 vs 503-512M votes/s, profiles/r01/inv_var, profiles/r01/park);
+// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 base table.
+uint32_t launch_lane_votes(const txv_ctx* c, int wb, uint32_t n_work) {
+  return (c->lane_auto && wb == 24 && n_work >= (3u << 18)) ? 8u : c->lane_votes;
+}
+
+// scratch for the parked results per K1b lane (V slots: the last one with TXV_PARK_LAST) (the grid never exceeds verify_grid's cap)
 int ensure_park(txv_ctx* c) {
   if (c->lane_votes == 1) return TXV_OK;   // split mode parks nothing
-  const size_t words = (size_t)(c->lane_votes - 1) * TXV_PARK_WORDS * (size_t)c->n_cus * 2 * TXV_VERIFY_BLOCK;
+  const size_t words = (size_t)(c->lane_auto ? 8u : c->lane_votes) * TXV_PARK_WORDS * (size_t)c->n_cus * 2 * TXV_VERIFY_BLOCK;
   if (words <= c->park_words) return TXV_OK;
   int r;
   if ((r = dalloc(c, &c->d_park, words))) return r;
@@ -615,6 +624,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
+  va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
   TallyArgs ta = tally_args(c, s, arena_base);
@@ -793,6 +803,7 @@ int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) 
   const bool reg_w = ks.w == c->tab_w;
   const int w_base = reg_w ? c->b_w : ks.w;
   va.btable = reg_w ? c->d_btable : (ks.w == 4 ? c->d_btable4 : c->d_btable8);
+  va.lane_votes = launch_lane_votes(c, w_base, va.n_work);
   HIP_TRY(c, txv_launch_verify(w_base, ks.w, &va, verify_grid(c, s.n), c->stream));
   ok.resize(s.n);
   if (s.n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, s.n, hipMemcpyDeviceToHost, c->stream));
@@ -851,7 +862,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }
-  if (TXV_CFG_LANE_VOTES(c->cfg.flags)) c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags);
+  if (TXV_CFG_LANE_VOTES(c->cfg.flags)) { c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags); c->lane_auto = false; }
   if (c->lane_votes != 1 && c->lane_votes != 2 && c->lane_votes != 4 && c->lane_votes != 8) { delete c; return TXV_EINVAL; }
   c->cfg_bw = (int)TXV_CFG_B_WINDOW(c->cfg.flags);
   if (c->cfg_bw && c->cfg_bw != 4 && !valid_window(c->cfg_bw) && c->cfg_bw != 20 && c->cfg_bw != 22 && c->cfg_bw != 24) {
