@@ -107,8 +107,10 @@ typedef struct {
  * 2 * ceil(256/W) = 128 / 64 / 52 */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
-/* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19
- * (2 or 4; 0 = default 4) */
+/* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19:
+ * 2, 4 or 8 (8 needs the radix-2^24 base table), 1 = split (scalar-multiply kernel stores R',
+ * a second kernel batch-inverts and encodes); 0 = auto: 8 when a launch's pending votes fill
+ * >= 1.5 waves per SIMD (>= 768K) with the radix-2^24 base table, else 4 */
 #define TXV_CFG_LANE_VOTES(flags) (((flags) >> 16) & 0xFu)
 #define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
 /* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 8.9 GB, over radix-2^16
