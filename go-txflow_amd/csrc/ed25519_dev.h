@@ -81,6 +81,42 @@ TXV_HD void sha512_prefixed(uint32_t digest_le[16], const uint64_t* pre, int pre
   }
 }
 
+// Same digest with the next block's message words loaded before the current block is
+// compressed, so a vote's HBM latency is exposed once instead of once per block (K1a: the
+// C2 SignBytes make 2 blocks).  Costs 16 u64 registers of look-ahead.
+TXV_HD void sha512_prefixed_pf(uint32_t digest_le[16], const uint64_t* pre, int pre_words, const MsgView& m) {
+  uint64_t st[8];
+  sha512_init(st);
+  const uint32_t total = 8u * (uint32_t)pre_words + m.len;
+  const uint32_t nblk = sha512_nblocks(total);
+  const uint32_t pad_word = total >> 3, pad_shift = 56u - 8u * (total & 7u);
+  const uint32_t last = 16u * nblk - 1u;
+  uint64_t nx[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) nx[t] = t < pre_words ? pre[t] : msg_word(m, (uint32_t)(t - pre_words));
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t gw = 16u * b + (uint32_t)t;
+      uint64_t v = nx[t];
+      if (gw == pad_word) v |= 0x80ull << pad_shift;
+      if (gw == last) v = (uint64_t)total * 8u;
+      w[t] = v;
+    }
+    if (b + 1 < nblk) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) nx[t] = msg_word(m, 16u * (b + 1) + (uint32_t)t - (uint32_t)pre_words);
+    }
+    sha512_block(st, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    digest_le[2 * k] = bswap32((uint32_t)(st[k] >> 32));
+    digest_le[2 * k + 1] = bswap32((uint32_t)st[k]);
+  }
+}
+
 // table entry fetch: T[pos][idx] from a flat word array
 template <int W, typename Ptr>
 TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {

@@ -20,6 +20,12 @@
 
 using namespace txv;
 
+// K1a's SHA-512 may load block b+1's message words before compressing block b (measured equal:
+// K1a 298 vs 299-306 us at 116 vs 99 VGPRs, profiles/r01/k1a_prefetch; off)
+#ifndef TXV_K1A_PREFETCH
+#define TXV_K1A_PREFETCH 0
+#endif
+
 // K1b's shared inversion: the variable-time divstep inverse (fe_inv_var.h) or the Fermat
 // chain; the value is the same either way (encoding canonicalises)
 #ifndef TXV_INV_VAR
@@ -117,7 +123,11 @@ __device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, 
   }
   MsgView m{a.msg + i, a.n_pad, a.msg_words, a.msg_len[i]};
   uint32_t dig[16];
+#if TXV_K1A_PREFETCH
+  sha512_prefixed_pf(dig, pre, 8, m);
+#else
   sha512_prefixed(dig, pre, 8, m);
+#endif
   sc k = sc_reduce512(dig);
 #pragma unroll
   for (int j = 0; j < 8; ++j) { k_out[j] = k.v[j]; s_out[j] = s[8 + j]; }
