@@ -5,6 +5,10 @@
 // (types/tx_vote.go:144-150) on the host threads -- runs for the whole batch first; then the
 // order-dependent part runs sequentially in arrival order exactly as CheckTxWithInfo does it
 // per vote (:187-261):
+//   0. txSize = TxVote.Size(), which is 0 when amino rejects the timestamp (types/tx_vote.go:144-150):
+//      such a vote goes through every step below with size 0 -- it is cached and admitted --
+//      unless a WAL is configured (TXV_POOL_WAL): then MustMarshalBinaryBare panics in the WAL
+//      write (:231-242) right after the cache push, reported as TXV_POOL_ERR_ENCODING
 //   1. Size() >= config.Size || txSize + TxsBytes() > config.MaxTxsBytes -> ErrMempoolIsFull
 //   2. txSize > MaxMsgBytes - aminoOverheadForTxMessage (8, reactor.go:27,379) -> ErrTxTooLarge
 //   3. cache.Push(key) false (key present: moved to the back) -> ErrTxInCache
@@ -293,8 +297,7 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
       if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
       p->txs_map.prefetch(keys[i + kAhead]);
     }
-    const uint32_t sz = p->sizes[i];
-    if (!sz) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
+    const uint32_t sz = p->sizes[i];   // 0: amino error (Size() swallows it)
     if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
       status_out[i] = TXV_POOL_ERR_FULL;
       continue;
@@ -303,6 +306,7 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     Key k;
     memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
     if (!p->cache_push(k)) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
+    if (!sz && (p->cfg.flags & TXV_POOL_WAL)) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
     p->txs_map.put(k, p->txs.push_back(k, sz));     // addTx (txsMap.Store overwrites)
     p->txs_bytes += sz;
     status_out[i] = TXV_POOL_OK;

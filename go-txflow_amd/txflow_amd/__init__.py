@@ -65,7 +65,7 @@ class _Votes(ctypes.Structure):
 
 class _PoolCfg(ctypes.Structure):
     _fields_ = [("size", ctypes.c_uint32), ("cache_size", ctypes.c_uint32), ("max_txs_bytes", ctypes.c_uint64),
-                ("max_msg_bytes", ctypes.c_uint32), ("pad0", ctypes.c_uint32)]
+                ("max_msg_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 class _WireVotes(ctypes.Structure):
@@ -640,6 +640,7 @@ def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):
 
 POOL_OK, POOL_ERR_FULL, POOL_ERR_TOO_LARGE, POOL_ERR_IN_CACHE, POOL_ERR_ENCODING = range(5)
 POOL_NO_CACHE = 0xFFFFFFFF
+POOL_WAL = 0x1      # TXV_POOL_WAL
 
 
 class TxVotePool:
@@ -649,9 +650,9 @@ class TxVotePool:
     cache_size POOL_NO_CACHE selects nopTxCache; 0 fields take tendermint's defaults."""
 
     def __init__(self, ctx: Context, size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
-                 max_msg_bytes: int = 0, height: int = 0):
+                 max_msg_bytes: int = 0, height: int = 0, wal: bool = False):
         self.ctx = ctx
-        cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes, 0)
+        cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes, POOL_WAL if wal else 0)
         h = ctypes.c_void_p()
         rc = lib().txv_pool_new(ctypes.byref(cfg), height, ctypes.byref(h))
         if rc != 0:

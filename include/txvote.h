@@ -264,8 +264,9 @@ typedef struct {
   uint32_t cache_size;      /* MempoolConfig.CacheSize: LRU entries; 0 -> 10000; TXV_POOL_NO_CACHE = nopTxCache */
   uint64_t max_txs_bytes;   /* MempoolConfig.MaxTxsBytes (0 -> 1 GiB) */
   uint32_t max_msg_bytes;   /* MempoolConfig.MaxMsgBytes (0 -> 1 MiB); max tx size = this - 8 (reactor.go:379) */
-  uint32_t pad0;
+  uint32_t flags;           /* TXV_POOL_WAL: the pool writes a WAL (InitWAL, node/node.go:805-807) */
 } txv_pool_config;
+#define TXV_POOL_WAL 0x1u
 #define TXV_POOL_NO_CACHE 0xFFFFFFFFu
 typedef struct txv_pool txv_pool;
 
@@ -274,7 +275,10 @@ typedef struct txv_pool txv_pool;
 #define TXV_POOL_ERR_FULL 1      /* mempool.ErrMempoolIsFull */
 #define TXV_POOL_ERR_TOO_LARGE 2 /* ErrTxTooLarge */
 #define TXV_POOL_ERR_IN_CACHE 3  /* mempool.ErrTxInCache */
-#define TXV_POOL_ERR_ENCODING 4  /* TxVote.Size(): amino rejects the timestamp (the reference panics) */
+#define TXV_POOL_ERR_ENCODING 4  /* only with TXV_POOL_WAL: amino rejects the timestamp, so the WAL write's
+                                    MustMarshalBinaryBare panics (txvotepool.go:231-242) after the
+                                    cache push.  Without a WAL such a vote is admitted with
+                                    TxVote.Size() == 0 (types/tx_vote.go:144-150) */
 
 int  txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out);
 void txv_pool_free(txv_pool* pool);

@@ -126,10 +126,12 @@ uint64_t orc_flow_num_verifies(orc_flow*);
 
 /* ---- TxVotePool (txvotepool/txvotepool.go) restatement ----
  * cache_size 0xFFFFFFFF = nopTxCache.  orc_pool_check returns 0 ok, 1 ErrMempoolIsFull,
- * 2 ErrTxTooLarge, 3 ErrTxInCache, 4 amino error in Size() (the reference panics). */
+ * 2 ErrTxTooLarge, 3 ErrTxInCache, 4 WAL panic: with `wal` set, a vote whose TxVote.Size() is 0
+ * (amino rejects its timestamp) panics in the WAL write after its cache push; without a WAL such
+ * a vote is admitted with size 0 (types/tx_vote.go:144-150, txvotepool.go:192-261). */
 typedef struct orc_pool orc_pool;
 orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_bytes, uint32_t max_msg_bytes,
-                       int64_t height);
+                       int64_t height, int wal);
 void orc_pool_free(orc_pool*);
 int orc_pool_check(orc_pool*, const orc_vote* v);
 void orc_pool_update(orc_pool*, int64_t height, const orc_vote* votes, uint32_t n);

@@ -54,7 +54,8 @@ def lib():
         L.orc_txvote_verify_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, c_u8p, ctypes.c_size_t, ctypes.c_int,
                                             ctypes.c_void_p]
         L.orc_pool_new.restype = ctypes.c_void_p
-        L.orc_pool_new.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64]
+        L.orc_pool_new.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64,
+                                   ctypes.c_int]
         L.orc_pool_free.argtypes = [ctypes.c_void_p]
         L.orc_pool_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
@@ -306,8 +307,9 @@ class Pool:
     """Sequential TxVotePool restatement (oracle/pool.c); votes as oracle-style dicts with the
     FULL signature bytes."""
 
-    def __init__(self, size=5000, cache_size=10000, max_txs_bytes=1 << 30, max_msg_bytes=1 << 20, height=0):
-        self._h = lib().orc_pool_new(size, cache_size, max_txs_bytes, max_msg_bytes, height)
+    def __init__(self, size=5000, cache_size=10000, max_txs_bytes=1 << 30, max_msg_bytes=1 << 20, height=0,
+                 wal=False):
+        self._h = lib().orc_pool_new(size, cache_size, max_txs_bytes, max_msg_bytes, height, int(bool(wal)))
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -2,7 +2,8 @@
  * pool.c — sequential restatement of TxVotePool.CheckTxWithInfo / Update / ReapMaxTxs / Flush
  * and mapTxCache (txvotepool/txvotepool.go).  TEST INFRASTRUCTURE ONLY (see oracle.h).
  *
- *   :187-261  CheckTxWithInfo: full (Size() >= config.Size || size + TxsBytes > MaxTxsBytes),
+ *   :187-261  CheckTxWithInfo: full (Size() >= config.Size || size + TxsBytes > MaxTxsBytes,
+ *             size = TxVote.Size() = 0 when amino rejects the timestamp),
  *             too large (size > MaxMsgBytes - 8, reactor.go:27,379), cache.Push false ->
  *             ErrTxInCache, else addTx (:265-270)
  *   :416-438  mapTxCache.Push: present -> MoveToBack, false; full -> remove Front; PushBack
@@ -36,6 +37,7 @@ struct orc_pool {
   uint32_t size, cache_size, max_msg_bytes;
   uint64_t max_txs_bytes;
   int cache_on;
+  int wal;                      /* InitWAL was called (node/node.go:805-807, config WalEnabled) */
   int64_t height, txs_bytes;
   plist cache, txs;
 };
@@ -82,8 +84,9 @@ static void pl_clear(plist* l) {
 static void pl_free(plist* l) { pl_clear(l); free(l->bucket); }
 
 orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_bytes, uint32_t max_msg_bytes,
-                       int64_t height) {
+                       int64_t height, int wal) {
   orc_pool* p = (orc_pool*)calloc(1, sizeof *p);
+  p->wal = wal;
   p->size = size; p->cache_size = cache_size; p->max_txs_bytes = max_txs_bytes; p->max_msg_bytes = max_msg_bytes;
   p->cache_on = cache_size != 0xFFFFFFFFu;
   p->height = height;
@@ -113,13 +116,16 @@ static int cache_push(orc_pool* p, const uint8_t* k) {
 static void vote_key(const orc_vote* v, uint8_t key[32]) { orc_sha256(v->sig, v->sig_len, key); }
 
 int orc_pool_check(orc_pool* p, const orc_vote* v) {
+  /* TxVote.Size() returns 0 when amino rejects the timestamp (types/tx_vote.go:144-150): such a
+   * vote passes the caps with size 0, is cached and admitted; only the WAL write
+   * (MustMarshalBinaryBare, :231-242, after the cache push) panics, when a WAL is configured */
   const int sz = orc_txvote_size(v->height, v->txhash_len, v->ts_sec, v->ts_nanos, v->addr_len, v->sig_len);
-  if (sz <= 0) return 4;                                   /* amino error: the reference panics */
   if ((int64_t)p->txs.len >= (int64_t)p->size || (int64_t)sz + p->txs_bytes > (int64_t)p->max_txs_bytes) return 1;
   if ((int64_t)sz > (int64_t)p->max_msg_bytes - 8) return 2;
   uint8_t k[32];
   vote_key(v, k);
   if (!cache_push(p, k)) return 3;
+  if (sz == 0 && p->wal) return 4;                        /* WAL MustMarshalBinaryBare panics */
   pl_push_back(&p->txs, k, (uint32_t)sz);
   p->txs_bytes += sz;
   return 0;

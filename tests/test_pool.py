@@ -115,6 +115,25 @@ def test_txs_bytes(oracle_lib):
     assert list(p.check([vote(b"\x04"), vote(b"\x05"), vote(b"\x06")])) == [OK, OK, FULL]
 
 
+def test_size_zero_vote_is_admitted(oracle_lib):
+    """TxVote.Size() returns 0 when amino rejects the timestamp (types/tx_vote.go:144-150), it
+    does not panic: CheckTxWithInfo (txvotepool.go:192-261) then passes the caps, caches
+    SHA-256(sig) and admits the vote with 0 bytes.  Only a configured WAL panics (its
+    MustMarshalBinaryBare, :231-242), after the cache push -- so a repeat is ErrTxInCache."""
+    bad_ts = (10 ** 13, 1)                              # year > 9999: amino time error
+    assert oracle_lib.txvote_size(1, 64, bad_ts[0], bad_ts[1], 20, 1) == 0
+    p = oracle_lib.Pool(max_txs_bytes=100)
+    st = p.check([vote(b"\x07", ts=bad_ts), vote(b"\x07", ts=bad_ts), vote(b"\x08")])
+    assert list(st) == [OK, IN_CACHE, FULL]             # vote 3 (~100 B) exceeds MaxTxsBytes
+    assert p.size() == 1 and p.txs_bytes() == 0
+    keys, sizes = p.reap()
+    assert [bytes(k) for k in keys] == [key(b"\x07")] and list(sizes) == [0]
+    w = oracle_lib.Pool(wal=True)
+    st = w.check([vote(b"\x07", ts=bad_ts), vote(b"\x07", ts=bad_ts), vote(b"\x08")])
+    assert list(st) == [ENCODING, IN_CACHE, OK]
+    assert w.size() == 1 and [bytes(k) for k in w.cache_keys()] == [key(b"\x07"), key(b"\x08")]
+
+
 # ------------------------------------------------------------------ GPU parity
 def _random_stream(rnd, n, n_sigs, long_frac=0.02):
     votes = []
@@ -150,8 +169,9 @@ def test_sig_keys_match_sha256(gpu_ctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [dict(size=700, cache_size=300), dict(size=2000, cache_size=0xFFFFFFFF),
-                                 dict(size=100000, cache_size=50, max_txs_bytes=60000, max_msg_bytes=300)],
-                         ids=["small-cache", "no-cache", "byte-limits"])
+                                 dict(size=100000, cache_size=50, max_txs_bytes=60000, max_msg_bytes=300),
+                                 dict(size=2000, cache_size=300, wal=True)],
+                         ids=["small-cache", "no-cache", "byte-limits", "wal"])
 def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
     """Random streams with repeated / empty / long (> 64 B) signatures, zero and out-of-range
     timestamps, long TxHashes: per-vote CheckTx results, Update, ReapMaxTxs order + sizes,
@@ -179,8 +199,9 @@ def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
                 assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
             assert np.array_equal(pool.cache_keys(), ref.cache_keys())
             seen |= set(int(x) for x in np.unique(exp))
-        want = {OK, ENCODING, FULL} | ({IN_CACHE} if cfg["cache_size"] != 0xFFFFFFFF else set()) | \
-            ({TOO_LARGE} if "max_msg_bytes" in cfg else set())
+        want = {OK, FULL} | ({IN_CACHE} if cfg["cache_size"] != 0xFFFFFFFF else set()) | \
+            ({TOO_LARGE} if "max_msg_bytes" in cfg else set()) | ({ENCODING} if cfg.get("wal") else set())
+        assert cfg.get("wal") or ENCODING not in seen      # without a WAL Size() == 0 votes are admitted
         assert seen >= want, (seen, want)
         pool.flush(); ref.flush()
         assert pool.Size() == 0 and pool.TxsBytes() == 0 and len(pool.cache_keys()) == 0
