@@ -1,12 +1,10 @@
 // host_pack.hpp — the host side of batch admission, built for 64k..1M-vote batches:
 //
-//   * WorkerPool: persistent threads + parallel_for over vote ranges (the pack of a batch
-//     is embarrassingly parallel except the TxHash routing, which stays sequential because
-//     set ids are assigned in first-seen order, txflow/service.go:200-209).
-//   * TxTable: TxHash bytes -> dense TxVoteSet id (open addressing, keys in one arena, seeded
-//     64-bit hash so crafted TxHash strings cannot force long probe chains).
+//   * WorkerPool: persistent threads + parallel_for over vote ranges (the staging copies of a
+//     batch into pinned memory, the verify-only packs).
 //   * AddrTable: 20-byte validator address -> validator index (ValidatorSet.GetByAddress,
-//     tendermint, called at types/vote_set.go:102), read-only during a pack.
+//     tendermint, called at types/vote_set.go:102); its slots are uploaded for the device
+//     lookup of the AddVote path (kernels_flow.hip) and used directly by the verify-only paths.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -23,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include "txv_hash.h"
+
 namespace txv_host {
 
 // ------------------------------------------------------------------ hashing
@@ -31,16 +31,13 @@ inline uint64_t mix64(uint64_t x) {
   x ^= x >> 32; x *= 0xd6e8feb86659fd93ULL; x ^= x >> 32; x *= 0xd6e8feb86659fd93ULL; x ^= x >> 32;
   return x;
 }
+// the same function the device uses for the set table and the validator address table
 inline uint64_t hash_bytes(const uint8_t* p, uint32_t n, uint64_t seed) {
-  uint64_t h = seed ^ (0x9e3779b97f4a7c15ULL * (n + 1));
-  uint32_t i = 0;
-  for (; i + 8 <= n; i += 8) h = mix64(h ^ load64(p + i)) + 0x9e3779b97f4a7c15ULL;
-  if (i < n) {
+  return txv_hash::hash_chunks(n, seed, [&](uint32_t i) {
     uint64_t t = 0;
-    memcpy(&t, p + i, n - i);
-    h = mix64(h ^ t ^ ((uint64_t)(n - i) << 56));
-  }
-  return mix64(h);
+    memcpy(&t, p + i, std::min<uint32_t>(8, n - i));
+    return t;
+  });
 }
 
 // ------------------------------------------------------------------ worker pool
@@ -173,71 +170,6 @@ uint32_t counting_sort(WorkerPool& pool, uint32_t n, uint32_t K, KeyF key, EmitF
   return run;
 }
 
-// ------------------------------------------------------------------ TxHash -> set id
-class TxTable {
- public:
-  explicit TxTable(uint64_t seed = 0x7478666c6f77ULL) : seed_(seed) { rehash(1024); }
-  uint64_t hash(const uint8_t* k, uint32_t n) const { return hash_bytes(k, n, seed_); }
-  // id of key (hash h = hash(k, n)), or UINT32_MAX
-  uint32_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
-    for (uint64_t i = h & mask_;; i = (i + 1) & mask_) {
-      const Slot& s = slots_[i];
-      if (!s.id1) return UINT32_MAX;
-      if (s.h == h && len_[s.id1 - 1] == n && !memcmp(arena_.data() + off_[s.id1 - 1], k, n)) return s.id1 - 1;
-    }
-  }
-  // id of key, inserting it with the next id when absent (*created = true); UINT32_MAX when
-  // absent and the table already holds `limit` keys
-  uint32_t intern(const uint8_t* k, uint32_t n, uint64_t h, bool* created, uint32_t limit = UINT32_MAX) {
-    uint64_t i = h & mask_;
-    for (;; i = (i + 1) & mask_) {
-      const Slot& s = slots_[i];
-      if (!s.id1) break;
-      if (s.h == h && len_[s.id1 - 1] == n && !memcmp(arena_.data() + off_[s.id1 - 1], k, n)) {
-        *created = false;
-        return s.id1 - 1;
-      }
-    }
-    *created = false;
-    if (off_.size() >= limit) return UINT32_MAX;
-    const uint32_t id = (uint32_t)off_.size();
-    off_.push_back(arena_.size());
-    len_.push_back(n);
-    arena_.insert(arena_.end(), k, k + n);
-    slots_[i] = Slot{h, id + 1};
-    *created = true;
-    if ((uint64_t)(id + 1) * 2 > mask_ + 1) rehash((mask_ + 1) * 2);
-    return id;
-  }
-  uint32_t size() const { return (uint32_t)off_.size(); }
-  void clear() {
-    off_.clear(); len_.clear(); arena_.clear();
-    slots_.clear();
-    rehash(1024);
-  }
-
- private:
-  struct Slot { uint64_t h; uint32_t id1; };
-  void rehash(uint64_t cap) {
-    std::vector<Slot> ns(cap, Slot{0, 0});
-    const uint64_t m = cap - 1;
-    for (const Slot& s : slots_) {
-      if (!s.id1) continue;
-      uint64_t i = s.h & m;
-      while (ns[i].id1) i = (i + 1) & m;
-      ns[i] = s;
-    }
-    slots_.swap(ns);
-    mask_ = m;
-  }
-  uint64_t seed_;
-  std::vector<Slot> slots_;
-  uint64_t mask_ = 0;
-  std::vector<uint64_t> off_;
-  std::vector<uint32_t> len_;
-  std::vector<uint8_t> arena_;
-};
-
 // ------------------------------------------------------------------ address -> validator
 class AddrTable {
  public:
@@ -255,6 +187,9 @@ class AddrTable {
       if (!dup) slots_[i] = v;   // first index wins for a repeated address
     }
   }
+  // the open-addressing slots (validator index or UINT32_MAX), mirrored on the device
+  const std::vector<uint32_t>& slots() const { return slots_; }
+  uint64_t mask() const { return mask_; }
   uint32_t find(const uint8_t* a) const {
     if (slots_.empty()) return UINT32_MAX;
     for (uint64_t i = hash_bytes(a, 20, kSeed) & mask_; slots_[i] != UINT32_MAX; i = (i + 1) & mask_)

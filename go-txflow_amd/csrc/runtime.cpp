@@ -1,16 +1,20 @@
 // runtime.cpp — host runtime behind include/txvote.h (libtxvote.so).
 //
-// Responsibilities (the parts of the reference path that stay on the host):
-//   * validator registry: address -> index (ValidatorSet.GetByAddress, ext, called at
-//     types/vote_set.go:102), powers, quorum = Total*2/3 + 1 (types/vote_set.go:158)
-//   * TxVoteSets routing: TxHash -> dense set id, created on first sight
-//     (txflow/service.go:200-209); host mirror of sum / maj23 for the readers
-//   * amino SignBytes encoding (amino.hpp) and the SoA pack into pinned buffers
-//   * device buffers, one HIP stream per context, launch order K1 verify -> K2 tally
+// Responsibilities of the host side:
+//   * validator registry: powers, quorum = Total*2/3 + 1 (types/vote_set.go:158) and the
+//     address table (ValidatorSet.GetByAddress, ext, called at types/vote_set.go:102), uploaded
+//   * the AddVote path (txv_submit_votes / txv_add_votes): copy the caller's raw TxVote columns
+//     into pinned memory (or DMA them straight from caller memory registered with
+//     txv_host_register) and queue the upload on the copy stream; every decision -- TxHash
+//     routing to TxVoteSets (txflow/service.go:200-209), the AddVote pre-checks, SignBytes, the
+//     verify, the tally -- is made by the kernel chain of run_slot on the compute stream
+//     (kernels_flow.hip, kernels_signbytes.hip, kernels_verify.hip)
+//   * the verify-only entry points (txv_verify_batch / txv_verify_bytes) and the signer pack
+//     their SignBytes on the host (amino.hpp) into pinned column-major buffers
 // Everything numeric about a vote's verdict runs on the GPU; there is no CPU verify path.
 #include "../../include/txvote.h"
 #include "txv_device.h"
-#include "txv_tally.h"
+#include "txv_flow.h"
 #include "amino.hpp"
 #include "host_pack.hpp"
 #include "sha2.h"
@@ -31,6 +35,8 @@
 #include <unordered_map>
 #include <vector>
 
+void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // SHA-256 on the host (below)
+
 namespace {
 
 // fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 24
@@ -41,43 +47,45 @@ constexpr uint32_t kSlots = 4;
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
-  uint32_t n_touched = 0, touched_cap = 0;
   bool staged = false, ran = false;
-  // device
+  // device: the verify kernels' columns (both paths)
   uint32_t* d_sig = nullptr; uint64_t* d_msg = nullptr; uint32_t* d_msg_len = nullptr;
   uint32_t* d_val = nullptr; uint32_t* d_set = nullptr; uint8_t* d_flags = nullptr;
   uint8_t* d_status = nullptr; uint8_t* d_ok = nullptr; uint8_t* d_pre = nullptr;
   uint32_t* d_kbuf = nullptr; uint32_t* d_rpts = nullptr; uint32_t* d_order = nullptr; uint32_t* h_order = nullptr;
   uint32_t n_work = 0;
-  // set-major tally order: pending votes grouped by (set, validator), arrival order inside
-  uint32_t* d_toff = nullptr; uint32_t* h_toff = nullptr;
-  uint32_t* d_tvote = nullptr; uint32_t* h_tvote = nullptr;
-  uint32_t* d_tval = nullptr; uint32_t* h_tval = nullptr;
-  uint32_t* d_ent_vote = nullptr; int64_t* d_ent_power = nullptr; uint32_t* d_ent_val = nullptr;
-  uint32_t* d_touched = nullptr; int64_t* d_tsum = nullptr; uint8_t* d_tmaj = nullptr; uint32_t* d_tcross = nullptr;
-  // pinned host
+  // pinned host (verify-only paths: host-packed columns)
   uint32_t* h_sig = nullptr; uint64_t* h_msg = nullptr; uint32_t* h_msg_len = nullptr;
   uint32_t* h_val = nullptr; uint32_t* h_set = nullptr; uint8_t* h_flags = nullptr; uint8_t* h_status = nullptr;
-  uint32_t* h_touched = nullptr; int64_t* h_tsum = nullptr; uint8_t* h_tmaj = nullptr; uint32_t* h_tcross = nullptr;
-  // results, written by the tally kernels straight into mapped host memory (m_* = device views)
-  uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
-  int64_t* m_tsum = nullptr; uint8_t* m_tmaj = nullptr; uint32_t* m_tcross = nullptr;
   std::vector<uint8_t> tmp_msg;   // SignBytes arena (verify-only paths)
   std::vector<size_t> tmp_off;
-  // device SignBytes inputs (kernels_signbytes.hip): pinned staging + device copies
+  // raw TxVote columns (the AddVote path uploads them as the caller passed them; the signer
+  // uses height .. TxHash arena for its device SignBytes): pinned staging + device copies
   int64_t *h_fh = nullptr, *h_fs = nullptr, *d_fh = nullptr, *d_fs = nullptr;     // height, ts_sec
   int32_t *h_fn = nullptr, *d_fn = nullptr;                                        // ts_nanos
   uint32_t *h_fo = nullptr, *h_fl = nullptr, *d_fo = nullptr, *d_fl = nullptr;     // txhash off / len
   uint8_t *h_arena = nullptr, *d_arena_th = nullptr;                               // TxHash arena
   size_t arena_cap = 0;
-  bool msg_on_device = false;      // this staging's SignBytes are built by txv_k_signbytes
-  std::vector<int> lens;           // AddVote pack: SignBytes length (-1 amino error, -2 nil)
-  std::vector<uint64_t> khash;     // AddVote pack: seeded hash of the TxHash bytes
-  std::vector<uint32_t> vidx;      // AddVote pack: validator index or UINT32_MAX
-  std::vector<uint32_t> miss;      // AddVote pack: votes whose TxHash has no set yet
-  // 0..2 kernel timing, 3 = the slot's uploads are done (copy stream), 4 = its results are in
-  // the pinned buffers (compute stream)
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t flow_cap = 0;           // capacity of the AddVote-only buffers below
+  uint8_t *h_addr = nullptr, *d_addr = nullptr;            // [n][20]
+  uint32_t *h_addr_len = nullptr, *d_addr_len = nullptr;
+  uint8_t *h_sigraw = nullptr, *d_sigraw = nullptr;        // [n][64]
+  uint32_t *h_sig_len = nullptr, *d_sig_len = nullptr;
+  uint8_t *h_nil = nullptr, *d_nil = nullptr;
+  uint8_t *h_txkey = nullptr, *d_txkey = nullptr;          // [n][32]
+  bool has_nil = false, has_txkey = false;
+  bool msg_on_device = false;      // the signer's SignBytes are built by txv_k_signbytes
+  uint64_t seq_base = 0;
+  // AddVote derived columns and scan scratch
+  uint32_t *d_entry = nullptr, *d_row = nullptr, *d_blk = nullptr;
+  uint8_t* d_ev_flag = nullptr;
+  // results, written by the kernels straight into mapped host memory (m_* = device views)
+  uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
+  FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
+  FlowSummary* h_sum = nullptr; FlowSummary* m_sum = nullptr;
+  // 0 start, 1 routed (+ SignBytes), 2 verified, 3 the slot's uploads are done (copy stream),
+  // 4 results are in host memory (compute stream), 5 tallied
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t ticket = 0;    // txv_submit_votes ticket in flight on this slot (0 = none)
 };
 
@@ -123,17 +131,27 @@ struct txv_ctx {
   uint32_t tmp_cap = 0;
   int tmp_w = 0;
   uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
-  // tally state
-  txv_host::TxTable tx_tab{std::random_device{}() * 0x9e3779b97f4a7c15ULL + 0x7478};   // TxHash -> set id
   std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
   bool profile_host = false;                    // TXV_PROFILE_HOST
-  std::vector<int64_t> h_sum;
-  std::vector<uint8_t> h_maj;
-  std::vector<uint32_t> seen_stage, set_tidx;   // per set: last staging that touched it, its index there
-  uint32_t stage_count = 0;
-  uint32_t* d_acc_slot = nullptr; uint32_t* d_arena = nullptr;
-  int64_t* d_set_sum = nullptr; uint32_t* d_bitmap = nullptr;
-  uint64_t arena_used = 0;          // arena rows reserved by the batches run since the last reset
+  // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
+  // accepted-vote arena, counters
+  SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
+  uint8_t* d_keys = nullptr; uint64_t keys_cap = 0;
+  uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_cnt = nullptr, *d_bitmap = nullptr;
+  int64_t* d_set_sum = nullptr;
+  uint32_t *d_acc = nullptr, *d_cand = nullptr, *d_touched = nullptr;
+  AccRow* d_arena = nullptr;
+  FlowCounters* d_ctr = nullptr;
+  uint32_t* d_addr_slots = nullptr; uint32_t addr_mask = 0;
+  uint32_t max_accepted = 0;        // accepted-vote rows (AccRow) of the arena
+  uint64_t hash_seed = 0;           // TxHash hash seed (random per context)
+  uint64_t seq_next = 0;            // sequence number of the next submitted vote
+  uint32_t n_sets_host = 0;         // TxVoteSets as of the last waited batch
+  uint32_t poisoned = 0;            // TXV_FERR_* seen: every AddVote call fails until txv_reset_flow
+  // caller memory registered with txv_host_register (DMA'd without a staging copy)
+  std::vector<std::pair<uintptr_t, uint64_t>> registered;
+  // reader scratch (lookups / gathers)
+  uint8_t* d_q = nullptr; uint64_t q_cap = 0;
   // signer slots (load generator)
   uint32_t n_signers = 0;
   uint32_t *d_sk_scal = nullptr, *d_sk_araw = nullptr, *d_sk_prefix = nullptr, *d_sk_pub = nullptr;
@@ -230,10 +248,6 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = dalloc(c, &s.d_pre, npad)) || (r = dalloc(c, &s.d_kbuf, 8 * npad)) ||
         (c->lane_votes == 1 && (r = dalloc(c, &s.d_rpts, (size_t)TXV_RPTS_WORDS * npad))) ||
         (r = dalloc(c, &s.d_order, npad)) || (r = halloc(c, &s.h_order, npad)) ||
-        (r = dalloc(c, &s.d_tvote, npad)) || (r = halloc(c, &s.h_tvote, npad)) ||
-        (r = dalloc(c, &s.d_tval, npad)) || (r = halloc(c, &s.h_tval, npad)) ||
-        (r = dalloc(c, &s.d_ent_vote, npad)) || (r = dalloc(c, &s.d_ent_power, npad)) ||
-        (r = dalloc(c, &s.d_ent_val, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
         (r = halloc(c, &s.h_flags, npad)) || (r = halloc(c, &s.h_status, npad)) ||
@@ -246,46 +260,95 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
     s.cap = cap;
     s.msg_cap_words = mw;
   }
-  if (s.touched_cap < need) {
-    int r;
-    if ((r = dalloc(c, &s.d_touched, need)) || (r = dalloc(c, &s.d_tsum, need)) || (r = dalloc(c, &s.d_tmaj, need)) ||
-        (r = dalloc(c, &s.d_toff, need + 1)) || (r = halloc(c, &s.h_toff, need + 1)) ||
-        (r = dalloc(c, &s.d_tcross, need)) || (r = halloc(c, &s.h_touched, need)) ||
-        (r = halloc_mapped(c, &s.h_tsum, &s.m_tsum, need)) || (r = halloc_mapped(c, &s.h_tmaj, &s.m_tmaj, need)) ||
-        (r = halloc_mapped(c, &s.h_tcross, &s.m_tcross, need)))
-      return r;
-    s.touched_cap = need;
-  }
   if (!s.ev[0])
     for (auto& e : s.ev) HIP_TRY(c, hipEventCreate(&e));
   return TXV_OK;
 }
 
-int alloc_tally(txv_ctx* c) {
-  const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
+// the AddVote path's raw columns, derived columns and mapped outputs for n votes
+int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
+  const uint32_t need = std::max<uint32_t>(n, 64);
+  if (s.flow_cap >= need) return TXV_OK;
+  const uint32_t cap = std::max(need, s.flow_cap);
+  const size_t npad = (cap + 63) / 64 * 64;
+  const size_t nblk = (npad + 1023) / 1024 + 1;
   int r;
-  if ((r = dalloc(c, &c->d_acc_slot, cells)) || (r = dalloc(c, &c->d_arena, (size_t)c->cfg.max_accepted * 16)) ||
-      (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) || (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)))
+  if ((r = halloc(c, &s.h_addr, 20 * npad)) || (r = dalloc(c, &s.d_addr, 20 * npad)) ||
+      (r = halloc(c, &s.h_addr_len, npad)) || (r = dalloc(c, &s.d_addr_len, npad)) ||
+      (r = halloc(c, &s.h_sigraw, 64 * npad)) || (r = dalloc(c, &s.d_sigraw, 64 * npad)) ||
+      (r = halloc(c, &s.h_sig_len, npad)) || (r = dalloc(c, &s.d_sig_len, npad)) ||
+      (r = halloc(c, &s.h_nil, npad)) || (r = dalloc(c, &s.d_nil, npad)) ||
+      (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
+      (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_row, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
+      (r = dalloc(c, &s.d_ev_flag, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
+      (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
     return r;
+  s.flow_cap = cap;
   return TXV_OK;
 }
 
-int reset_tally(txv_ctx* c, bool keep_ids = false) {
-  const size_t cells = (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
-  HIP_TRY(c, hipMemsetAsync(c->d_acc_slot, 0, cells * 4, c->stream));
+FlowState flow_state(const txv_ctx* c) {
+  FlowState f{};
+  f.tab = c->d_tab; f.tab_mask = c->tab_mask; f.max_txs = c->cfg.max_txs;
+  f.keys = c->d_keys; f.keys_cap = c->keys_cap;
+  f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_cnt = c->d_set_cnt;
+  f.bitmap = c->d_bitmap; f.acc = c->d_acc; f.cand = c->d_cand; f.arena = c->d_arena; f.touched = c->d_touched;
+  f.ctr = c->d_ctr; f.n_vals = c->n_vals; f.max_accepted = c->max_accepted; f.quorum = c->quorum;
+  f.power = c->d_power; f.val_addr = c->d_addr; f.addr_slots = c->d_addr_slots; f.addr_mask = c->addr_mask;
+  f.hash_seed = c->hash_seed;
+  return f;
+}
+
+// device TxFlow state sized for the registry: cells are max_txs x
+// n_vals, the accepted-vote arena holds max_accepted rows (default: one per cell, capped at
+// 2^26 rows = 8 GiB), the set table has >= 2 (max_txs + max_batch) slots
+int alloc_tally(txv_ctx* c) {
+  const uint64_t nv = std::max<uint32_t>(c->n_vals, 1);
+  const uint64_t cells = (uint64_t)c->cfg.max_txs * nv;
+  c->max_accepted = c->cfg.max_accepted ? c->cfg.max_accepted : (uint32_t)std::min<uint64_t>(cells, 1u << 26);
+  uint64_t tab = 1024;
+  while (tab < 2 * ((uint64_t)c->cfg.max_txs + c->cfg.max_batch)) tab *= 2;
+  c->tab_mask = (uint32_t)(tab - 1);
+  c->keys_cap = c->cfg.key_arena_bytes ? c->cfg.key_arena_bytes : (uint64_t)c->cfg.max_txs * 96 + (1u << 20);
+  int r;
+  if ((r = dalloc(c, &c->d_acc, cells)) || (r = dalloc(c, &c->d_cand, cells)) ||
+      (r = dalloc(c, &c->d_arena, c->max_accepted)) || (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_cnt, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_txkey, (size_t)c->cfg.max_txs * 8)) ||
+      (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_touched, c->cfg.max_batch)) ||
+      (r = dalloc(c, &c->d_tab, tab)) || (r = dalloc(c, &c->d_keys, c->keys_cap)) || (r = dalloc(c, &c->d_ctr, 1)))
+    return r;
+  HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_set_cnt, 0, (size_t)c->cfg.max_txs * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
-  c->arena_used = 0;
-  if (keep_ids) {
-    std::fill(c->h_sum.begin(), c->h_sum.end(), 0);
-    std::fill(c->h_maj.begin(), c->h_maj.end(), 0);
-    return TXV_OK;
+  HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, tab * sizeof(SetEntry), c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
+  c->seq_next = 0;
+  c->n_sets_host = 0;
+  c->poisoned = 0;
+  return TXV_OK;
+}
+
+// empty every TxVoteSet (keep_ids) or forget them (txv_reset_flow), on the compute stream
+// after every batch already submitted
+int reset_tally(txv_ctx* c, bool keep_ids = false) {
+  if (c->poisoned && !keep_ids) {   // a capacity overflow left partial state: clear everything
+    const uint64_t cells = (uint64_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
+    HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_set_cnt, 0, (size_t)c->cfg.max_txs * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, ((size_t)c->tab_mask + 1) * sizeof(SetEntry), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
+    c->poisoned = 0;
+  } else {
+    const FlowState fs = flow_state(c);
+    HIP_TRY(c, txv_flow_reset(&fs, keep_ids ? 1 : 0, c->stream));
+    if (keep_ids) c->poisoned &= ~TXV_FERR_ARENA;
   }
-  c->tx_tab.clear();
-  c->h_sum.clear();
-  c->h_maj.clear();
-  c->seen_stage.clear();
-  c->set_tidx.clear();
+  c->seq_next = 0;
+  if (!keep_ids) c->n_sets_host = 0;
   return TXV_OK;
 }
 
@@ -355,38 +418,14 @@ int upload_slot(txv_ctx* c, Slot& s) {
   HIP_TRY(c, hipMemcpyAsync(s.d_set, s.h_set, np * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_flags, s.h_flags, np, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, np, hipMemcpyHostToDevice, c->copy_stream));
-  if (s.n_touched)
-    HIP_TRY(c, hipMemcpyAsync(s.d_touched, s.h_touched, (size_t)s.n_touched * 4, hipMemcpyHostToDevice, c->copy_stream));
   if (s.n_work)
     HIP_TRY(c, hipMemcpyAsync(s.d_order, s.h_order, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // kernels on c->stream wait for it
   return TXV_OK;
 }
 
-// set-major tally order (AddVote path): stable counting sort of the validator-sorted pending
-// votes (h_order) by touched-set index gives (set, validator, arrival) order
-int build_set_order(txv_ctx* c, Slot& s) {
-  // stable by touched-set index over the validator-sorted pending votes
-  txv_host::counting_sort(*c->pool, s.n_work, s.n_touched,
-      [&](uint32_t q) { return c->set_tidx[s.h_set[s.h_order[q]]]; },
-      [&](uint32_t p, uint32_t q) {
-        const uint32_t i = s.h_order[q];
-        s.h_tvote[p] = i;
-        s.h_tval[p] = s.h_val[i] | ((s.h_flags[i] & TXV_FLAG_SIG64) ? 0x80000000u : 0u) |
-                      ((s.h_flags[i] & TXV_FLAG_BADMSG) ? 0x40000000u : 0u);
-      }, s.h_toff);
-  HIP_TRY(c, hipMemcpyAsync(s.d_toff, s.h_toff, (size_t)(s.n_touched + 1) * 4, hipMemcpyHostToDevice, c->copy_stream));
-  if (s.n_work) {
-    HIP_TRY(c, hipMemcpyAsync(s.d_tvote, s.h_tvote, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
-    HIP_TRY(c, hipMemcpyAsync(s.d_tval, s.h_tval, (size_t)s.n_work * 4, hipMemcpyHostToDevice, c->copy_stream));
-  }
-  HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
-  return TXV_OK;
-}
-
 // Counting sort of the pending votes by validator (keys = validator or caller-key index <
-// n_keys).  The tally's set-major order is built from it; K1b walks it only with the small
-// tables (verify_args).
+// n_keys), the verify-only paths' K1b work list with the small tables (verify_args).
 void build_order(txv_ctx* c, Slot& s, uint32_t n_keys) {
   s.n_work = txv_host::counting_sort(*c->pool, s.n, std::max<uint32_t>(n_keys, 1),
       [&](uint32_t i) { return (s.h_flags[i] & TXV_FLAG_PENDING) ? s.h_val[i] : UINT32_MAX; },
@@ -423,9 +462,12 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
 // K1b votes per lane for a launch with base window wb.  V = 8 halves the inversions per vote
 // but also the waves; with the divstep inverse it wins once the batch still fills >= 1.5 waves
 // per SIMD (C2, 1M votes: 517 vs 503-512M votes/s, profiles/r01/inv_var, profiles/r01/park);
-// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 base table.
+// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 base table
+// only, so a configured V = 8 runs V = 4 on any other base table (e.g. when the 8.9 GB wide
+// table could not be allocated, or for caller-key tables).
 uint32_t launch_lane_votes(const txv_ctx* c, int wb, uint32_t n_work) {
-  return (c->lane_auto && wb == 24 && n_work >= (3u << 18)) ? 8u : c->lane_votes;
+  if (wb != 24) return c->lane_votes == 8 ? 4u : c->lane_votes;
+  return (c->lane_auto && n_work >= (3u << 18)) ? 8u : c->lane_votes;
 }
 
 // scratch for the parked results per K1b lane (V slots: the last one with TXV_PARK_LAST) (the grid never exceeds verify_grid's cap)
@@ -439,21 +481,6 @@ int ensure_park(txv_ctx* c) {
   return TXV_OK;
 }
 
-TallyArgs tally_args(txv_ctx* c, Slot& s, uint32_t arena_base) {
-  TallyArgs a{};
-  a.n = s.n; a.n_pad = s.n_pad; a.n_vals = c->n_vals; a.n_touched = s.n_touched;
-  a.quorum = c->quorum; a.arena_base = arena_base;
-  a.sig = s.d_sig; a.ok = s.d_ok; a.pre = s.d_pre; a.status = s.d_status;
-  a.touched = s.d_touched; a.toff = s.d_toff; a.tvote = s.d_tvote; a.tval = s.d_tval;
-  a.ent_vote = s.d_ent_vote; a.ent_power = s.d_ent_power; a.ent_val = s.d_ent_val;
-  a.acc_slot = c->d_acc_slot; a.arena = c->d_arena;
-  a.power = c->d_power; a.set_sum = c->d_set_sum; a.commit_bitmap = c->d_bitmap;
-  a.t_sum = s.m_tsum; a.t_maj = s.m_tmaj; a.t_cross = s.m_tcross;   // mapped host memory
-  a.status_host = s.m_out;
-  return a;
-}
-
-// stage for the AddVote path: routing, pre-checks, SignBytes, pack, upload
 // Device SignBytes for slot s: stage the raw fields + the TxHash arena prefix
 // [0, arena_end) into pinned buffers (parallel), upload them on the copy stream and build the
 // column-major message words there with txv_k_signbytes.  s.h_msg_len must be set already.
@@ -502,143 +529,177 @@ int upload_chain(txv_ctx* c, const char* chain, uint32_t len, uint8_t** d, uint3
   return TXV_OK;
 }
 
+// Bound on the SignBytes length of any vote whose TxHash has at most max_hl bytes (the verify
+// kernels' message-column count): length prefix + Height (9) + TxHash field + TxKey (34) +
+// Timestamp field (<= 19) + ChainID field
+uint32_t signbytes_bound(uint32_t max_hl, uint32_t chain_len) {
+  const uint64_t body = 9 + (1 + txv_host::put_uvarint(nullptr, max_hl) + (uint64_t)max_hl) + 34 + 19 +
+                        (chain_len ? 1 + txv_host::put_uvarint(nullptr, chain_len) + chain_len : 0);
+  return (uint32_t)(txv_host::put_uvarint(nullptr, body) + body);
+}
+
+bool is_registered(const txv_ctx* c, const void* p, uint64_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto& r : c->registered)
+    if (a >= r.first && a + bytes <= r.first + r.second) return true;
+  return false;
+}
+
+// AddVote staging: the caller's raw columns go to the device as they are (txv_flow.h
+// FlowBatch); the only host pass reads TxHash offsets / lengths (arena extent, message-column
+// bound).  Registered columns are DMA'd straight from caller memory; the others are copied into
+// the slot's pinned buffers chunk by chunk on the pack threads, each chunk's DMA queued as soon
+// as it is copied, so copies and PCIe transfers overlap.
 int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
   Slot& s = c->slots[slot];
   const uint32_t n = v->n;
   const uint32_t chain_len = (uint32_t)c->chain.size();
   HostTimer ht(c->profile_host);
-  // phase A (parallel): SignBytes lengths, TxHash hashes, validator lookups
-  s.lens.resize(n); s.khash.resize(n); s.vidx.resize(n);
-  std::atomic<uint32_t> mx{0};
   std::atomic<uint64_t> arena_end{0};
+  std::atomic<uint32_t> max_hl{0};
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-    uint32_t m = 0;
     uint64_t ae = 0;
+    uint32_t mh = 0;
     for (uint32_t i = lo; i < hi; ++i) {
-      if (v->is_nil && v->is_nil[i]) { s.lens[i] = -2; continue; }
+      if (v->is_nil && v->is_nil[i]) continue;
       ae = std::max<uint64_t>(ae, (uint64_t)v->txhash_off[i] + v->txhash_len[i]);
-      const int L = txv_host::sign_bytes_len(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], chain_len);
-      s.lens[i] = L;
-      if (L > 0 && (uint32_t)L > m) m = (uint32_t)L;
-      s.khash[i] = c->tx_tab.hash(v->txhash + v->txhash_off[i], v->txhash_len[i]);
-      s.vidx[i] = v->addr_len[i] == 20 ? c->addr_tab.find(v->addr + (size_t)i * 20) : UINT32_MAX;
+      mh = std::max(mh, v->txhash_len[i]);
     }
-    uint32_t cur = mx.load();
-    while (m > cur && !mx.compare_exchange_weak(cur, m)) {}
     uint64_t ca = arena_end.load();
     while (ae > ca && !arena_end.compare_exchange_weak(ca, ae)) {}
-  });
-  const uint32_t mw = std::max<uint32_t>(1, (mx.load() + 7) / 8);
-  ht.mark("A");
-  int r = ensure_slot(c, s, n, mw);
-  if (r) return r;
+    uint32_t cm = max_hl.load();
+    while (mh > cm && !max_hl.compare_exchange_weak(cm, mh)) {}
+  }, 16384);
+  const uint64_t ae = arena_end.load();
+  if (ae >= (1ull << 32)) { c->err = "TxHash arena >= 4 GiB"; return TXV_EINVAL; }
+  const uint32_t mw = (signbytes_bound(max_hl.load(), chain_len) + 7) / 8;
+  int r;
+  if ((r = ensure_slot(c, s, n, mw)) || (r = ensure_flow_slot(c, s, n))) return r;
+  if (ae + 16 > s.arena_cap) {
+    const size_t cap = std::max<size_t>((size_t)ae + 16, s.arena_cap * 2);
+    if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
+    s.arena_cap = cap;
+  }
   s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
-  // phase B: TxHash -> set id, created on first sight in arrival order (txflow/service.go:200-209,
-  // also for votes that then fail), touched-set list, the AddVote pre-checks (types/vote_set.go:92-105).
-  // B1 (parallel): lookups of existing sets (read-only table) and the per-vote pre-checks;
-  // B2 (sequential, arrival order): the misses are interned -- new sets get their ids in
-  // first-seen order exactly as a sequential pass would assign them; B3: touched-set list.
-  const uint32_t stage_id = ++c->stage_count;
-  s.n_touched = 0;
-  std::vector<uint32_t>& miss = s.miss;
-  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) {
-      s.h_flags[i] = 0; s.h_val[i] = 0;
-      if (s.lens[i] == -2) { s.h_status[i] = TXV_ERR_NIL; s.h_set[i] = UINT32_MAX - 1; continue; }
-      s.h_set[i] = c->tx_tab.find(v->txhash + v->txhash_off[i], v->txhash_len[i], s.khash[i]);
-      if (v->addr_len[i] == 0) { s.h_status[i] = TXV_ERR_EMPTY_ADDR; continue; }
-      const uint32_t vi = s.vidx[i];
-      if (vi == UINT32_MAX) { s.h_status[i] = TXV_ERR_UNKNOWN_VALIDATOR; continue; }
-      s.h_val[i] = vi;
-      // a SignBytes failure is only reached after the accepted-vote check (AddVote order), so
-      // the vote stays pending with BADMSG: it never verifies and the tally resolves it
-      s.h_status[i] = 0xFF;
-      s.h_flags[i] = TXV_FLAG_PENDING | (v->sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (s.lens[i] < 0 ? TXV_FLAG_BADMSG : 0);
-    }
-  }, 4096);
-  miss.clear();
-  for (uint32_t i = 0; i < n; ++i)
-    if (s.h_set[i] == UINT32_MAX) miss.push_back(i);
-  for (const uint32_t i : miss) {
-    bool created;
-    const uint32_t sid = c->tx_tab.intern(v->txhash + v->txhash_off[i], v->txhash_len[i], s.khash[i], &created,
-                                          c->cfg.max_txs);
-    if (sid == UINT32_MAX) { c->err = "TxVoteSets exceed max_txs"; return TXV_ECAPACITY; }
-    if (created) {
-      c->h_sum.push_back(0); c->h_maj.push_back(0); c->seen_stage.push_back(0); c->set_tidx.push_back(0);
-    }
-    s.h_set[i] = sid;
+  s.has_nil = v->is_nil != nullptr;
+  s.has_txkey = v->txkey != nullptr;
+  s.seq_base = c->seq_next;
+  c->seq_next += n;
+  ht.mark("scan");
+  struct Col { const uint8_t* src; uint8_t* pin; uint8_t* dev; size_t elem; bool reg; };
+  Col cols[11];
+  int nc = 0;
+  auto add = [&](const void* src, void* pin, void* dev, size_t elem) {
+    if (!src) return;
+    cols[nc++] = Col{(const uint8_t*)src, (uint8_t*)pin, (uint8_t*)dev, elem, is_registered(c, src, (uint64_t)n * elem)};
+  };
+  add(v->height, s.h_fh, s.d_fh, 8);
+  add(v->ts_sec, s.h_fs, s.d_fs, 8);
+  add(v->ts_nanos, s.h_fn, s.d_fn, 4);
+  add(v->txhash_off, s.h_fo, s.d_fo, 4);
+  add(v->txhash_len, s.h_fl, s.d_fl, 4);
+  add(v->addr, s.h_addr, s.d_addr, 20);
+  add(v->addr_len, s.h_addr_len, s.d_addr_len, 4);
+  add(v->sig, s.h_sigraw, s.d_sigraw, 64);
+  add(v->sig_len, s.h_sig_len, s.d_sig_len, 4);
+  add(v->is_nil, s.h_nil, s.d_nil, 1);
+  add(v->txkey, s.h_txkey, s.d_txkey, 32);
+  for (int k = 0; k < nc; ++k)
+    if (cols[k].reg && n) HIP_TRY(c, hipMemcpyAsync(cols[k].dev, cols[k].src, (size_t)n * cols[k].elem, hipMemcpyHostToDevice, c->copy_stream));
+  // TxHash arena (+ 16 zero bytes: the device reads keys 8 bytes at a time)
+  const bool arena_reg = is_registered(c, v->txhash, ae);
+  if (arena_reg) {
+    if (ae) HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, v->txhash, (size_t)ae, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(c, hipMemsetAsync(s.d_arena_th + ae, 0, 16, c->copy_stream));
   }
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t sid = s.h_set[i];
-    if (sid == UINT32_MAX - 1) { s.h_set[i] = 0; continue; }   // nil vote: no set
-    if (c->seen_stage[sid] != stage_id) {
-      c->seen_stage[sid] = stage_id;
-      c->set_tidx[sid] = s.n_touched;
-      s.h_touched[s.n_touched++] = sid;
-    }
-  }
-  ht.mark("B");
-  // phase C (parallel): column-major signature words and lengths; the SignBytes words are
-  // built on the device (encode_signbytes_device)
-  const uint32_t np = s.n_pad;
-  c->pool->parallel_for(np, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) {
-      if (i >= n) {
-        for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = 0;
-        s.h_msg_len[i] = 0; s.h_val[i] = 0; s.h_set[i] = 0; s.h_flags[i] = 0; s.h_status[i] = TXV_ERR_NIL;
-        continue;
+  const uint32_t chunk = std::max<uint32_t>(65536, (n + 7) / 8);
+  const uint64_t achunk = std::max<uint64_t>(1u << 20, (ae + 7) / 8);
+  const uint32_t n_chunks = std::max<uint32_t>((n + chunk - 1) / chunk, arena_reg ? 0u : (uint32_t)((ae + achunk - 1) / achunk));
+  for (uint32_t k = 0; k < n_chunks; ++k) {
+    const uint32_t lo = std::min<uint64_t>((uint64_t)k * chunk, n), hi = std::min<uint64_t>((uint64_t)(k + 1) * chunk, n);
+    const uint64_t alo = arena_reg ? 0 : std::min<uint64_t>(k * achunk, ae), ahi = arena_reg ? 0 : std::min<uint64_t>((k + 1) * achunk, ae);
+    c->pool->parallel_for(hi - lo + (uint32_t)((ahi - alo + 4095) / 4096), [&](uint32_t a, uint32_t b) {
+      // items [0, hi - lo) are votes of this chunk, the rest 4 KiB pages of its arena slice
+      const uint32_t nv = hi - lo;
+      if (a < nv) {
+        const uint32_t va = lo + a, vb = lo + std::min(b, nv);
+        for (int q = 0; q < nc; ++q)
+          if (!cols[q].reg) memcpy(cols[q].pin + (size_t)va * cols[q].elem, cols[q].src + (size_t)va * cols[q].elem, (size_t)(vb - va) * cols[q].elem);
       }
-      uint8_t sg[64];
-      const uint32_t sl = v->sig_len[i] > 64 ? 64 : v->sig_len[i];
-      memset(sg, 0, 64);
-      memcpy(sg, v->sig + (size_t)i * 64, sl);
-      for (int j = 0; j < 16; ++j) s.h_sig[(size_t)j * np + i] = le32(sg + 4 * j);
-      s.h_msg_len[i] = s.lens[i] > 0 ? (uint32_t)s.lens[i] : 0;
-    }
-  }, 1024);
-  ht.mark("C");
-  build_order(c, s, c->n_vals);
-  ht.mark("order");
-  if ((r = encode_signbytes_device(c, s, v, c->d_chain, chain_len, arena_end.load()))) return r;
-  ht.mark("signbytes");
-  if ((r = upload_slot(c, s))) return r;
+      if (b > nv) {
+        const uint64_t pa = alo + (uint64_t)(std::max(a, nv) - nv) * 4096, pb = std::min<uint64_t>(alo + (uint64_t)(b - nv) * 4096, ahi);
+        if (pb > pa) memcpy(s.h_arena + pa, v->txhash + pa, pb - pa);
+      }
+    }, 4096);
+    for (int q = 0; q < nc; ++q)
+      if (!cols[q].reg && hi > lo)
+        HIP_TRY(c, hipMemcpyAsync(cols[q].dev + (size_t)lo * cols[q].elem, cols[q].pin + (size_t)lo * cols[q].elem,
+                                  (size_t)(hi - lo) * cols[q].elem, hipMemcpyHostToDevice, c->copy_stream));
+    if (ahi > alo)
+      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th + alo, s.h_arena + alo, ahi - alo, hipMemcpyHostToDevice, c->copy_stream));
+  }
+  if (!arena_reg) {
+    memset(s.h_arena + ae, 0, 16);
+    HIP_TRY(c, hipMemcpyAsync(s.d_arena_th + ae, s.h_arena + ae, 16, hipMemcpyHostToDevice, c->copy_stream));
+  }
+  HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
   ht.mark("upload");
-  if ((r = build_set_order(c, s))) return r;
-  ht.mark("set_order");
   s.staged = true; s.ran = false;
   return TXV_OK;
 }
 
+FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
+  FlowBatch b{};
+  b.n = s.n; b.n_pad = s.n_pad; b.msg_words = s.msg_words; b.chain_len = (uint32_t)c->chain.size();
+  b.seq_base = s.seq_base;
+  b.height = s.d_fh; b.ts_sec = s.d_fs; b.ts_nanos = s.d_fn; b.th_off = s.d_fo; b.th_len = s.d_fl; b.th = s.d_arena_th;
+  b.addr = s.d_addr; b.addr_len = s.d_addr_len; b.sig_raw = s.d_sigraw; b.sig_len = s.d_sig_len;
+  b.nil = s.has_nil ? s.d_nil : nullptr; b.txkey = s.has_txkey ? s.d_txkey : nullptr;
+  b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
+  b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status; b.row = s.d_row;
+  b.ev_flag = s.d_ev_flag; b.blk = s.d_blk;
+  b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
+  return b;
+}
+
+// the whole AddVote chain of a staged batch on the compute stream: route (keying, pre-checks,
+// set ids) -> SignBytes -> K1a/K1b verify -> tally -> results into mapped host memory
 int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   Slot& s = c->slots[slot];
   if (!s.staged) { c->err = "slot not staged"; return TXV_ESTATE; }
-  // arena rows [arena_used, arena_used + n) are this batch's (row = base + arrival index)
-  if (c->arena_used + s.n > c->cfg.max_accepted) { c->err = "accepted-signature arena full"; return TXV_ECAPACITY; }
-  const uint32_t arena_base = (uint32_t)c->arena_used;
-  c->arena_used += s.n;
+  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
   int r;
   if ((r = ensure_park(c))) return r;
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
+  const FlowState fs = flow_state(c);
+  const FlowBatch fb = flow_batch(c, s);
+  HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
+  SignBytesArgs sa{};
+  sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
+  sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
+  sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = s.d_msg_len; sa.msg = s.d_msg;
+  HIP_TRY(c, txv_launch_signbytes(&sa, c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
+  va.order = nullptr;          // arrival order; K1a marks the non-pending votes
+  va.n_work = s.n;
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
-  HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
-  TallyArgs ta = tally_args(c, s, arena_base);
-  HIP_TRY(c, txv_launch_tally(&ta, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
-  // the tally kernels wrote the statuses and per-set results into mapped host memory (no copy
-  // engine in the loop); fetch_slot only waits for the kernels
+  HIP_TRY(c, txv_flow_tally(&fs, &fb, c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[5], c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
   s.ran = true;
   if (ms) {
-    HIP_TRY(c, hipEventSynchronize(s.ev[2]));
+    HIP_TRY(c, hipEventSynchronize(s.ev[5]));
     HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
     HIP_TRY(c, hipEventElapsedTime(&ms[1], s.ev[1], s.ev[2]));
-    ms[2] = ms[0] + ms[1];
+    HIP_TRY(c, hipEventElapsedTime(&ms[2], s.ev[2], s.ev[5]));
+    HIP_TRY(c, hipEventElapsedTime(&ms[3], s.ev[0], s.ev[5]));
   }
   return TXV_OK;
 }
@@ -649,18 +710,21 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
   HostTimer ht(c->profile_host);
   HIP_TRY(c, hipEventSynchronize(s.ev[4]));
   ht.mark("fetch_sync");
-  if (status_out) memcpy(status_out, s.h_out, s.n);
-  ht.mark("fetch_copy");
-  uint32_t ne = 0;
-  for (uint32_t t = 0; t < s.n_touched; ++t) {
-    const uint32_t sid = s.h_touched[t];
-    c->h_sum[sid] = s.h_tsum[t];
-    c->h_maj[sid] = s.h_tmaj[t];
-    if (s.h_tcross[t] != TXV_NO_CROSS) {
-      if (ev && ne < ev_cap) ev[ne] = txv_commit_event{s.h_tcross[t], sid, s.h_tsum[t]};
-      ++ne;
-    }
+  FlowSummary sm;
+  memcpy(&sm, (const void*)s.h_sum, sizeof sm);   // written over PCIe by the last kernel
+  c->n_sets_host = sm.n_sets;
+  if (sm.err) {
+    c->poisoned |= sm.err;
+    c->err = std::string("TxFlow capacity exceeded:") + ((sm.err & TXV_FERR_SETS) ? " max_txs" : "") +
+             ((sm.err & TXV_FERR_TABLE) ? " set-table" : "") + ((sm.err & TXV_FERR_KEYS) ? " key_arena_bytes" : "") +
+             ((sm.err & TXV_FERR_ARENA) ? " max_accepted" : "") + " (txv_reset_flow to recover)";
+    return TXV_ECAPACITY;
   }
+  if (status_out && s.n) memcpy(status_out, s.h_out, s.n);
+  ht.mark("fetch_copy");
+  static_assert(sizeof(FlowEvent) == sizeof(txv_commit_event), "event layout");
+  const uint32_t ne = sm.n_events;
+  if (ev && ne) memcpy(ev, s.h_ev, (size_t)std::min(ne, ev_cap) * sizeof(FlowEvent));
   if (n_ev) *n_ev = ne;
   return TXV_OK;
 }
@@ -856,7 +920,8 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (!c->cfg.max_batch) c->cfg.max_batch = 1u << 20;
   if (!c->cfg.max_txs) c->cfg.max_txs = 1u << 20;
   if (!c->cfg.max_validators) c->cfg.max_validators = 1024;
-  if (!c->cfg.max_accepted) c->cfg.max_accepted = (uint32_t)std::min<uint64_t>((uint64_t)c->cfg.max_txs * 128, 1u << 28);
+  if (c->cfg.max_batch > (8u << 20)) { delete c; return TXV_EINVAL; }   // the device scans cover 8M votes
+  c->hash_seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x7478666c6f77ULL;
   if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
   if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 80u << 10;   // 80 GiB of the 288 GB HBM
   c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
@@ -907,17 +972,21 @@ void txv_destroy(txv_ctx* c) {
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
     dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_rpts); dfree(s.d_order); hfree(s.h_order);
-    dfree(s.d_toff); hfree(s.h_toff); dfree(s.d_tvote); hfree(s.h_tvote); dfree(s.d_tval); hfree(s.h_tval);
-    dfree(s.d_ent_vote); dfree(s.d_ent_power); dfree(s.d_ent_val); dfree(s.d_touched); dfree(s.d_tsum); dfree(s.d_tmaj); dfree(s.d_tcross);
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
-    hfree(s.h_status); hfree(s.h_touched); hfree(s.h_tsum); hfree(s.h_tmaj); hfree(s.h_tcross); hfree(s.h_out);
+    hfree(s.h_status); hfree(s.h_out);
+    hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
+    hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey);
+    dfree(s.d_entry); dfree(s.d_row); dfree(s.d_blk); dfree(s.d_ev_flag); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
-  dfree(c->d_acc_slot); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_bitmap);
+  dfree(c->d_acc); dfree(c->d_cand); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_set_cnt); dfree(c->d_bitmap);
+  dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_touched); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
+  dfree(c->d_addr_slots); dfree(c->d_q);
+  for (const auto& rg : c->registered) (void)hipHostUnregister((void*)rg.first);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
   dfree(c->d_chain); dfree(c->d_chain_sign);
   dfree(c->d_pk_sig); dfree(c->d_pk_len); dfree(c->d_pk_keys); hfree(c->h_pk_sig); hfree(c->h_pk_len); hfree(c->h_pk_keys);
@@ -978,8 +1047,14 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   c->addr_index.clear();
   for (uint32_t i = 0; i < n; ++i) c->addr_index.emplace(std::string((const char*)c->addrs.data() + 20 * i, 20), i);
   c->addr_tab.build(c->addrs.data(), n);
+  // the same open-addressing table on the device (the AddVote path's validator lookup)
+  c->addr_mask = (uint32_t)c->addr_tab.mask();
+  if ((r = dalloc(c, &c->d_addr_slots, c->addr_tab.slots().size()))) return r;
+  HIP_TRY(c, hipMemcpyAsync(c->d_addr_slots, c->addr_tab.slots().data(), c->addr_tab.slots().size() * 4,
+                            hipMemcpyHostToDevice, c->stream));
   if ((r = alloc_tally(c))) return r;
-  return reset_tally(c);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
 }
 
 int txv_get_validator_info(txv_ctx* c, uint8_t* addr20_out, uint8_t* decode_ok_out, uint32_t cap) {
@@ -1002,7 +1077,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
   int r = ensure_slot(c, s, v->n, mw);
   if (r) return r;
-  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw;
   KeySet ks = registry_keys(c);
   uint32_t n_keys = c->n_vals;
   if (pubs32) {
@@ -1070,7 +1145,7 @@ int txv_verify_bytes(txv_ctx* c, const uint8_t* pubs32, const uint8_t* msgs, con
   const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
   int r = ensure_slot(c, s, n, mw);
   if (r) return r;
-  s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0;
+  s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
   std::vector<uint32_t> kidx;
   KeySet ks;
   if ((r = prepare_keys(c, pubs32, n, kidx, nullptr, ks))) return r;
@@ -1130,14 +1205,135 @@ int txv_wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_
   return wait_votes(c, ticket, status_out, ev, ev_cap, n_ev);
 }
 
-int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23) {
-  if (!c) return TXV_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// Readers: set ids of n TxHashes (arena + off / len), looked up on the compute stream, i.e.
+// after every batch submitted so far.  Scratch layout in d_q: keys (16 B padded) | off | len | ids.
+int lookup_sets(txv_ctx* c, const uint8_t* arena, const uint32_t* off, const uint32_t* len, uint32_t n,
+                std::vector<uint32_t>& ids) {
+  ids.assign(n, TXV_NONE);
+  if (!n || !c->d_tab) return TXV_OK;
+  uint64_t kb = 0;
+  for (uint32_t q = 0; q < n; ++q) kb += len[q];
+  const uint64_t kpad = (kb + 16 + 15) / 16 * 16;
+  const uint64_t need = kpad + 12ull * n;
+  int r;
+  if (need > c->q_cap) {
+    if ((r = dalloc(c, &c->d_q, need))) return r;
+    c->q_cap = need;
+  }
+  std::vector<uint8_t> hk(kpad, 0);
+  std::vector<uint32_t> ho(n), hl(n);
+  uint64_t at = 0;
+  for (uint32_t q = 0; q < n; ++q) {
+    if (len[q]) memcpy(hk.data() + at, arena + off[q], len[q]);
+    ho[q] = (uint32_t)at;
+    hl[q] = len[q];
+    at += len[q];
+  }
+  uint32_t* d_off = reinterpret_cast<uint32_t*>(c->d_q + kpad);
+  uint32_t* d_len = d_off + n;
+  uint32_t* d_ids = d_len + n;
+  HIP_TRY(c, hipMemcpyAsync(c->d_q, hk.data(), kpad, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(d_off, ho.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(d_len, hl.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  const FlowState fs = flow_state(c);
+  HIP_TRY(c, txv_flow_lookup(&fs, c->d_q, d_off, d_len, n, d_ids, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(ids.data(), d_ids, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+// sums, TxKeys and (optionally) every validator's accepted vote of n set ids
+int read_sets(txv_ctx* c, const std::vector<uint32_t>& ids, std::vector<int64_t>* sums, std::vector<uint8_t>* txkeys,
+              std::vector<AccRow>* rows) {
+  const uint32_t n = (uint32_t)ids.size();
+  if (!n || !c->n_vals) return TXV_OK;
+  const size_t nv = c->n_vals;
+  uint32_t* d_ids = nullptr; int64_t* d_sum = nullptr; uint32_t* d_tk = nullptr; AccRow* d_rows = nullptr;
+  int r;
+  if ((r = dalloc(c, &d_ids, n)) || (r = dalloc(c, &d_sum, n)) || (r = dalloc(c, &d_tk, (size_t)n * 8)) ||
+      (rows && (r = dalloc(c, &d_rows, (size_t)n * nv)))) {
+    dfree(d_ids); dfree(d_sum); dfree(d_tk); dfree(d_rows);
+    return r;
+  }
+  const FlowState fs = flow_state(c);
+  hipError_t e = hipMemcpyAsync(d_ids, ids.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = txv_flow_gather(&fs, d_ids, n, d_sum, d_tk, d_rows, c->stream);
+  if (sums) sums->resize(n);
+  if (txkeys) txkeys->resize((size_t)n * 32);
+  if (rows) rows->resize((size_t)n * nv);
+  if (e == hipSuccess && sums) e = hipMemcpyAsync(sums->data(), d_sum, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && txkeys) e = hipMemcpyAsync(txkeys->data(), d_tk, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && rows)
+    e = hipMemcpyAsync(rows->data(), d_rows, (size_t)n * nv * sizeof(AccRow), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d_ids); dfree(d_sum); dfree(d_tk); dfree(d_rows);
+  HIP_TRY(c, e);
+  return TXV_OK;
+}
+
+// the accepted votes of one set in validator order, as the commit encodings need them
+int set_commit_votes(txv_ctx* c, uint32_t id, std::vector<AccRow>& rows, std::vector<txv_host::CommitVote>& out,
+                     uint8_t txkey[32], int64_t* sum) {
+  std::vector<int64_t> sums;
+  std::vector<uint8_t> tks;
+  int r = read_sets(c, std::vector<uint32_t>{id}, &sums, &tks, &rows);
+  if (r) return r;
+  memcpy(txkey, tks.data(), 32);
+  *sum = sums[0];
+  out.clear();
+  for (const AccRow& a : rows) {
+    if (a.val == TXV_NONE) continue;
+    out.push_back(txv_host::CommitVote{a.height, a.ts_sec, a.ts_nanos, reinterpret_cast<const uint8_t*>(a.txkey),
+                                       c->addrs.data() + (size_t)a.val * 20, reinterpret_cast<const uint8_t*>(a.sig)});
+  }
+  return TXV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int txv_query_txs(txv_ctx* c, const uint8_t* txhash, const uint32_t* off, const uint32_t* len, uint32_t n,
+                  uint8_t* exists_out, int64_t* sum_out, uint8_t* maj23_out, uint8_t* txkey_out) {
+  if (!c || (n && (!off || !len || (!txhash && n)))) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (!txhash && len) return TXV_EINVAL;
-  const uint32_t sid = c->tx_tab.find(txhash, len, c->tx_tab.hash(txhash, len));
-  if (sid == UINT32_MAX) return 0;
-  if (sum) *sum = c->h_sum[sid];
-  if (maj23) *maj23 = c->h_maj[sid];
+  HIP_TRY(c, hipSetDevice(c->device));
+  std::vector<uint32_t> ids;
+  int r = lookup_sets(c, txhash, off, len, n, ids);
+  if (r) return r;
+  std::vector<int64_t> sums;
+  std::vector<uint8_t> tks;
+  if ((r = read_sets(c, ids, &sums, txkey_out ? &tks : nullptr, nullptr))) return r;
+  for (uint32_t q = 0; q < n; ++q) {
+    const bool ex = ids[q] != TXV_NONE;
+    if (exists_out) exists_out[q] = ex ? 1 : 0;
+    const int64_t sm = ex && !sums.empty() ? sums[q] : 0;
+    if (sum_out) sum_out[q] = sm;
+    if (maj23_out) maj23_out[q] = ex && sm >= c->quorum ? 1 : 0;   // maj23 is sticky and sum only grows
+    if (txkey_out) {
+      if (ex && !tks.empty()) memcpy(txkey_out + (size_t)q * 32, tks.data() + (size_t)q * 32, 32);
+      else memset(txkey_out + (size_t)q * 32, 0, 32);
+    }
+  }
+  return TXV_OK;
+}
+
+int txv_query_tx(txv_ctx* c, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23) {
+  if (!c || (!txhash && len)) return TXV_EINVAL;
+  const uint32_t off = 0;
+  uint8_t ex = 0;
+  int64_t sm = 0;
+  uint8_t mj = 0;
+  const uint8_t dummy = 0;
+  int r = txv_query_txs(c, txhash ? txhash : &dummy, &off, &len, 1, &ex, &sm, &mj, nullptr);
+  if (r) return r;
+  if (!ex) return 0;
+  if (sum) *sum = sm;
+  if (maj23) *maj23 = mj;
   return 1;
 }
 
@@ -1147,27 +1343,21 @@ int txv_get_votes(txv_ctx* c, const uint8_t* txhash, uint32_t len, uint32_t* val
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   *n_out = 0;
-  const uint32_t sid = c->tx_tab.find(txhash, len, c->tx_tab.hash(txhash, len));
-  if (sid == UINT32_MAX || !c->n_vals) return TXV_OK;
-  uint32_t *d_rows = nullptr, *d_sigs = nullptr;
-  int r;
-  if ((r = dalloc(c, &d_rows, c->n_vals)) || (r = dalloc(c, &d_sigs, (size_t)c->n_vals * 16))) { dfree(d_rows); return r; }
-  std::vector<uint32_t> rows(c->n_vals), sigs((size_t)c->n_vals * 16);
-  // stream order: after every batch already submitted on this context
-  hipError_t e = txv_launch_set_votes(c->d_acc_slot + (size_t)sid * c->n_vals, c->n_vals, c->d_arena, d_rows, d_sigs,
-                                      c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d_rows, (size_t)c->n_vals * 4, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(sigs.data(), d_sigs, (size_t)c->n_vals * 64, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  dfree(d_rows); dfree(d_sigs);
-  HIP_TRY(c, e);
+  const uint32_t off = 0;
+  const uint8_t dummy = 0;
+  std::vector<uint32_t> ids;
+  int r = lookup_sets(c, txhash ? txhash : &dummy, &off, &len, 1, ids);
+  if (r) return r;
+  if (ids[0] == TXV_NONE || !c->n_vals) return TXV_OK;
+  std::vector<AccRow> rows;
+  if ((r = read_sets(c, ids, nullptr, nullptr, &rows))) return r;
   uint32_t k = 0;
-  for (uint32_t v = 0; v < c->n_vals; ++v) {
-    if (!rows[v]) continue;
+  for (const AccRow& a : rows) {
+    if (a.val == TXV_NONE) continue;
     if (k < cap) {
-      if (val_out) val_out[k] = v;
-      if (seq_out) seq_out[k] = rows[v] - 1;
-      if (sig_out) memcpy(sig_out + (size_t)k * 64, sigs.data() + (size_t)v * 16, 64);
+      if (val_out) val_out[k] = a.val;
+      if (seq_out) seq_out[k] = a.seq;
+      if (sig_out) memcpy(sig_out + (size_t)k * 64, a.sig, 64);
     }
     ++k;
   }
@@ -1175,7 +1365,63 @@ int txv_get_votes(txv_ctx* c, const uint8_t* txhash, uint32_t len, uint32_t* val
   return TXV_OK;
 }
 
-uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? c->tx_tab.size() : 0; }
+int txv_make_commit(txv_ctx* c, const uint8_t* txhash, uint32_t len, uint8_t* out, uint64_t cap, uint64_t* len_out) {
+  if (!c || (!txhash && len) || !len_out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t off = 0;
+  const uint8_t dummy = 0;
+  std::vector<uint32_t> ids;
+  int r = lookup_sets(c, txhash ? txhash : &dummy, &off, &len, 1, ids);
+  if (r) return r;
+  if (ids[0] == TXV_NONE) { c->err = "no TxVoteSet for this TxHash"; return TXV_ESTATE; }
+  std::vector<AccRow> rows;
+  std::vector<txv_host::CommitVote> votes;
+  uint8_t tk[32];
+  int64_t sum;
+  if ((r = set_commit_votes(c, ids[0], rows, votes, tk, &sum))) return r;
+  if (sum < c->quorum) { c->err = "MakeCommit without +2/3 (the reference panics)"; return TXV_ESTATE; }
+  const int64_t L = txv_host::commit_bytes(nullptr, txhash, len, votes.data(), (uint32_t)votes.size());
+  if (L < 0) { c->err = "amino time error in a commit vote"; return TXV_EINVAL; }
+  *len_out = (uint64_t)L;
+  if ((uint64_t)L > cap || !out) return TXV_ECAPACITY;
+  txv_host::commit_bytes(out, txhash, len, votes.data(), (uint32_t)votes.size());
+  return TXV_OK;
+}
+
+int txv_save_tx_bytes(txv_ctx* c, const uint8_t* txhash, uint32_t len, uint8_t* out, uint64_t cap, uint64_t lens_out[4]) {
+  if (!c || (!txhash && len) || !lens_out) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t off = 0;
+  const uint8_t dummy = 0;
+  std::vector<uint32_t> ids;
+  int r = lookup_sets(c, txhash ? txhash : &dummy, &off, &len, 1, ids);
+  if (r) return r;
+  if (ids[0] == TXV_NONE) { c->err = "no TxVoteSet for this TxHash"; return TXV_ESTATE; }
+  std::vector<AccRow> rows;
+  std::vector<txv_host::CommitVote> votes;
+  uint8_t tk[32];
+  int64_t sum;
+  if ((r = set_commit_votes(c, ids[0], rows, votes, tk, &sum))) return r;
+  if (sum < c->quorum) { c->err = "SaveTx -> MakeCommit without +2/3 (the reference panics)"; return TXV_ESTATE; }
+  const int64_t cl = txv_host::commit_bytes(nullptr, txhash, len, votes.data(), (uint32_t)votes.size());
+  if (cl < 0) { c->err = "amino time error in a commit vote"; return TXV_EINVAL; }
+  lens_out[0] = txv_host::store_key(nullptr, 'H', txhash, len);
+  lens_out[1] = txv_host::txvoteset_bytes(nullptr, txhash, len, tk);
+  lens_out[2] = txv_host::store_key(nullptr, 'C', txhash, len);
+  lens_out[3] = (uint64_t)cl;
+  const uint64_t total = lens_out[0] + lens_out[1] + lens_out[2] + lens_out[3];
+  if (total > cap || !out) return TXV_ECAPACITY;
+  uint8_t* p = out;
+  p += txv_host::store_key(p, 'H', txhash, len);
+  p += txv_host::txvoteset_bytes(p, txhash, len, tk);
+  p += txv_host::store_key(p, 'C', txhash, len);
+  txv_host::commit_bytes(p, txhash, len, votes.data(), (uint32_t)votes.size());
+  return TXV_OK;
+}
+
+uint32_t txv_num_tx_sets(txv_ctx* c) { return c ? c->n_sets_host : 0; }
 int64_t txv_total_power(txv_ctx* c) { return c ? c->total : 0; }
 
 int txv_signbytes(int64_t height, const uint8_t* txhash, uint32_t txhash_len, int64_t ts_sec, int32_t ts_nanos,
@@ -1233,7 +1479,7 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
   const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
   int r = ensure_slot(c, s, v->n, mw);
   if (r) return r;
-  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_touched = 0; s.n_work = 0;
+  s.n = v->n; s.n_pad = (v->n + 63) / 64 * 64; s.msg_words = mw; s.n_work = 0;
   for (uint32_t i = 0; i < s.n_pad; ++i) {
     const bool in = i < v->n;
     s.h_val[i] = in ? signer[i] : 0; s.h_flags[i] = 0; s.h_set[i] = 0; s.h_status[i] = 0;
@@ -1263,6 +1509,7 @@ int txv_stage(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!c || !v || slot >= kSlots - 2) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
+  if (c->slots[slot].ticket) { c->err = "slot holds a txv_submit_votes batch in flight"; return TXV_ESTATE; }
   int r = stage_add(c, slot, v);
   if (r) return r;
   HIP_TRY(c, hipStreamSynchronize(c->copy_stream));   // resident before any timed run
@@ -1273,6 +1520,7 @@ int txv_run_staged(txv_ctx* c, uint32_t slot, float* ms) {
   if (!c || slot >= kSlots - 2) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
+  if (c->slots[slot].ticket) { c->err = "slot holds a txv_submit_votes batch in flight"; return TXV_ESTATE; }
   return run_slot(c, slot, ms);
 }
 
@@ -1288,6 +1536,92 @@ int txv_commit_bitmap(txv_ctx* c, void** dev_ptr, uint64_t* bytes) {
   if (!c || !dev_ptr || !bytes) return TXV_EINVAL;
   *dev_ptr = c->d_bitmap;
   *bytes = (uint64_t)(c->cfg.max_txs + 31) / 32 * 4;
+  return TXV_OK;
+}
+
+int txv_host_register(txv_ctx* c, void* ptr, uint64_t bytes) {
+  if (!c || !ptr || !bytes) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  c->registered.emplace_back((uintptr_t)ptr, bytes);
+  return TXV_OK;
+}
+
+int txv_host_unregister(txv_ctx* c, void* ptr) {
+  if (!c || !ptr) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  for (size_t k = 0; k < c->registered.size(); ++k)
+    if (c->registered[k].first == (uintptr_t)ptr) {
+      // no DMA of an in-flight batch may still read it
+      HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
+      HIP_TRY(c, hipHostUnregister(ptr));
+      c->registered.erase(c->registered.begin() + (long)k);
+      return TXV_OK;
+    }
+  c->err = "pointer was not registered";
+  return TXV_EINVAL;
+}
+
+uint64_t txv_commit_state_bytes(uint32_t n_sets_cap) {
+  return 8ull + (uint64_t)(n_sets_cap + 31) / 32 * 4 + 8ull * n_sets_cap;
+}
+
+int txv_pack_commit_state(txv_ctx* c, void* dst_dev, uint32_t n_sets_cap) {
+  if (!c || !dst_dev) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->d_ctr) { c->err = "no validator set"; return TXV_ESTATE; }
+  const FlowState fs = flow_state(c);
+  HIP_TRY(c, txv_flow_pack(&fs, static_cast<uint32_t*>(dst_dev), (n_sets_cap + 31) / 32, n_sets_cap, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
+int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
+                               void* dst) {
+  if (!dst || n_sets > n_sets_cap || (n_sets && (!committed || !sums))) return TXV_EINVAL;
+  uint32_t* d = static_cast<uint32_t*>(dst);
+  const uint32_t bm = (n_sets_cap + 31) / 32;
+  memset(d, 0, txv_commit_state_bytes(n_sets_cap));
+  d[0] = n_sets;
+  for (uint32_t s = 0; s < n_sets; ++s) {
+    if (committed[s]) d[2 + s / 32] |= 1u << (s % 32);
+    memcpy(d + 2 + bm + 2 * s, &sums[s], 8);
+  }
+  return TXV_OK;
+}
+
+int txv_commit_state_unpack(const void* src, uint32_t n_sets_cap, uint32_t* n_sets, uint8_t* committed, int64_t* sums,
+                            uint32_t cap) {
+  if (!src || !n_sets) return TXV_EINVAL;
+  const uint32_t* d = static_cast<const uint32_t*>(src);
+  const uint32_t bm = (n_sets_cap + 31) / 32;
+  if (d[0] > n_sets_cap) return TXV_EINVAL;
+  *n_sets = d[0];
+  for (uint32_t s = 0; s < d[0] && s < cap; ++s) {
+    if (committed) committed[s] = (uint8_t)((d[2 + s / 32] >> (s % 32)) & 1u);
+    if (sums) memcpy(&sums[s], d + 2 + bm + 2 * s, 8);
+  }
+  return TXV_OK;
+}
+
+int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len, uint32_t n, uint32_t n_shards,
+                 uint32_t* shard_out) {
+  if (!n_shards || (n && (!txhash || !off || !len || !shard_out))) return TXV_EINVAL;
+  const uint32_t nt = std::max(1u, std::min<uint32_t>(16, n / 4096));
+  std::vector<std::thread> th;
+  auto work = [&](uint32_t t) {
+    for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i) {
+      uint8_t h[32];
+      txv_sha256_bytes(txhash + off[i], len[i], h);
+      shard_out[i] = h[0] % n_shards;
+    }
+  };
+  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
   return TXV_OK;
 }
 

@@ -1,0 +1,177 @@
+// txv_flow.h — device state and argument blocks of the TxFlow.addVote path on the GPU
+// (kernels_flow.hip): routing a batch of TxVotes to their TxVoteSets, the AddVote pre-checks
+// and the stake tally (txflow/service.go:192-234, types/vote_set.go:81-166).
+//
+// Persistent device state of one TxFlow (HBM, survives batches until txv_reset_flow):
+//   set table   SetEntry[tab_mask + 1]   TxHash -> dense TxVoteSet id, open addressing.  Ids are
+//               handed out in first-seen arrival order, exactly as the sequential
+//               `TxVoteSets[vote.TxHash]` creation would number them (service.go:200-209).
+//   key arena   u8[keys_cap]             TxHash bytes of every set (the table's keys)
+//   per set id  set_entry (table slot), set_txkey [8] u32 (TxKey of the first vote,
+//               service.go:201-207), set_sum i64, set_cnt (ADDED votes of the running batch),
+//               commit bitmap (1 bit per set)
+//   cells       acc [max_txs * n_vals] u32   0 or the accepted vote's arena row + 1 (the
+//                                            reference's `votes` map, vote_set.go:154)
+//               cand[max_txs * n_vals] u32   per batch: smallest arrival index of a verified
+//                                            vote of the (set, validator) cell; after the
+//                                            resolve step the row of set s holds the arrival
+//                                            indices of s's ADDED votes of the batch
+//   arena       AccRow[max_accepted]     every accepted vote in full (signature, height, time,
+//                                        TxKey, validator, sequence number): one row per ADDED
+//                                        vote, so a row is only spent on what the map stores
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#include "txv_hash.h"
+
+#define TXV_NO_CROSS 0xFFFFFFFFu
+#define TXV_NONE 0xFFFFFFFFu
+
+// per-vote status codes (device copies of include/txvote.h)
+#define TXV_S_ADDED 0u
+#define TXV_S_DUPLICATE 1u
+#define TXV_S_NIL 2u
+#define TXV_S_EMPTY_ADDR 3u
+#define TXV_S_UNKNOWN_VALIDATOR 4u
+#define TXV_S_NONDETERMINISTIC 5u
+#define TXV_S_INVALID_SIGNATURE 6u
+#define TXV_S_SIGNBYTES 8u
+#define TXV_S_PENDING 0xFFu
+#define TXV_S_FIRED 0x80u
+
+// FlowCounters.err bits: an infrastructure capacity was exceeded inside the batch (the
+// context is poisoned until txv_reset_flow: TXV_ECAPACITY)
+#define TXV_FERR_SETS 0x1u      // more TxVoteSets than max_txs
+#define TXV_FERR_TABLE 0x2u     // set table full (probe bound)
+#define TXV_FERR_KEYS 0x4u      // TxHash key arena full
+#define TXV_FERR_ARENA 0x8u     // accepted-vote arena full (max_accepted)
+
+// table entry states
+#define TXV_SE_EMPTY 0u
+#define TXV_SE_BUSY 1u          // being written by the lane that claimed it
+#define TXV_SE_BATCH 2u         // created by the running batch: key bytes in the batch's TxHash arena
+#define TXV_SE_KEPT 3u          // key bytes in the persistent key arena
+
+struct SetEntry {
+  uint64_t h;                   // seeded 64-bit hash of the TxHash bytes
+  uint32_t state;
+  uint32_t len;                 // TxHash length
+  uint64_t key_off;             // into the batch arena (BATCH) or the key arena (KEPT)
+  uint32_t first;               // BATCH: smallest arrival index of the key in the batch
+  uint32_t id;                  // dense set id (assigned after the batch's routing step)
+};
+
+// one accepted vote (128 B): what TxVoteSet.votes holds, for MakeCommit / GetVotes
+struct AccRow {
+  uint32_t sig[16];             // the 64 signature bytes (an accepted vote has exactly 64)
+  int64_t height;
+  int64_t ts_sec;
+  int32_t ts_nanos;
+  uint32_t val;                 // validator index (its ValidatorAddress is the registry's)
+  uint64_t seq;                 // sequence number of the vote since the last reset
+  uint32_t txkey[8];
+};
+
+struct FlowCounters {           // device-resident, updated by the kernels
+  uint32_t n_sets;              // TxVoteSets so far
+  uint32_t n_touched;           // sets with ADDED votes in the running batch
+  uint32_t arena_used;          // accepted-vote rows in use
+  uint32_t err;                 // TXV_FERR_*
+  uint64_t key_used;            // key arena bytes in use
+  uint32_t batch;               // batches run since the reset
+  uint32_t pad;
+};
+
+struct FlowSummary {            // written to mapped host memory by the last kernel of a batch
+  uint32_t n_sets, n_events, arena_used, err;
+  uint64_t key_used;
+};
+
+struct FlowEvent {              // txv_commit_event (include/txvote.h)
+  uint32_t vote_index, tx_index;
+  int64_t sum;
+};
+
+struct FlowState {
+  SetEntry* tab;
+  uint32_t tab_mask;
+  uint32_t max_txs;
+  uint8_t* keys;
+  uint64_t keys_cap;
+  uint32_t* set_entry;          // [max_txs]
+  uint32_t* set_txkey;          // [max_txs][8]
+  int64_t* set_sum;             // [max_txs]
+  uint32_t* set_cnt;            // [max_txs]
+  uint32_t* bitmap;             // [max_txs / 32]
+  uint32_t* acc;                // [max_txs * n_vals]
+  uint32_t* cand;               // [max_txs * n_vals]
+  AccRow* arena;                // [max_accepted]
+  uint32_t* touched;            // [max_batch] sets with ADDED votes in the running batch
+  FlowCounters* ctr;
+  uint32_t n_vals, max_accepted;
+  int64_t quorum;
+  const int64_t* power;         // [n_vals]
+  const uint32_t* val_addr;     // [n_vals][5] registry addresses (SHA-256(pub)[:20])
+  const uint32_t* addr_slots;   // [addr_mask + 1] validator index or TXV_NONE (AddrTable)
+  uint32_t addr_mask;
+  uint32_t pad0;
+  uint64_t hash_seed;           // TxHash hash seed (random per context)
+};
+
+// one batch (raw columns as the caller passed them, uploaded; derived columns)
+struct FlowBatch {
+  uint32_t n, n_pad, msg_words, chain_len;
+  uint64_t seq_base;            // sequence number of vote 0
+  const int64_t* height;
+  const int64_t* ts_sec;
+  const int32_t* ts_nanos;
+  const uint32_t* th_off;
+  const uint32_t* th_len;
+  const uint8_t* th;            // TxHash arena (>= 8 bytes of padding after the last key)
+  const uint8_t* addr;          // [n][20]
+  const uint32_t* addr_len;
+  const uint8_t* sig_raw;       // [n][64]
+  const uint32_t* sig_len;
+  const uint8_t* nil;           // [n] or null
+  const uint8_t* txkey;         // [n][32] or null (zero TxKey)
+  // derived
+  uint32_t* sig;                // [16][n_pad] column-major signature words (K1a / K1b / compares)
+  uint32_t* msg_len;            // [n] SignBytes length (0: nil / amino error)
+  uint32_t* val;                // [n] validator index
+  uint8_t* flags;               // [n] TXV_FLAG_*
+  uint8_t* pre;                 // [n] pre-check status or TXV_S_PENDING
+  uint32_t* entry;              // [n] set-table slot (TXV_NONE for nil)
+  uint32_t* set;                // [n] set id
+  const uint8_t* ok;            // [n] verify verdicts (1 = valid)
+  uint8_t* status;              // [n] tally status of pending votes
+  uint32_t* row;                // [n] arena row of an ADDED vote
+  uint8_t* ev_flag;             // [n] this vote's ADDED crossed 2/3 in the batch
+  uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
+  // outputs in mapped host memory
+  uint8_t* status_host;         // [n]
+  FlowEvent* ev_host;           // [n]
+  FlowSummary* summary_host;
+};
+
+extern "C" {
+// the whole AddVote chain of one batch except SignBytes and verify, split where the verify
+// kernels sit: route (pre-checks, set ids, signature transpose, SignBytes lengths) ...
+hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st);
+// ... then, after K1a/K1b wrote b->ok: tally, commit events, statuses to the host
+hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, hipStream_t st);
+// forget every TxVoteSet (keep_ids = 0) or empty them keeping their ids (keep_ids = 1)
+hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);
+// TxHash lookups for the readers: out_id[i] = set id or TXV_NONE
+hipError_t txv_flow_lookup(const FlowState* fs, const uint8_t* keys, const uint32_t* off, const uint32_t* len,
+                           uint32_t n, uint32_t* out_id, hipStream_t st);
+// per set id: sum, TxKey, and the accepted vote of every validator (AccRow, val = TXV_NONE
+// for none): out_rows[k * n_vals + v]
+hipError_t txv_flow_gather(const FlowState* fs, const uint32_t* ids, uint32_t n, int64_t* out_sum,
+                           uint32_t* out_txkey, AccRow* out_rows, hipStream_t st);
+// key bytes of set ids (for SaveTx / MakeCommit): out_off/out_len into the key arena
+hipError_t txv_flow_keys(const FlowState* fs, const uint32_t* ids, uint32_t n, uint64_t* out_off, uint32_t* out_len,
+                         hipStream_t st);
+// packed commit state of this shard: [n_sets u32][pad u32][bitmap words][sums i64]
+hipError_t txv_flow_pack(const FlowState* fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap, hipStream_t st);
+}

@@ -1,0 +1,35 @@
+// txv_hash.h — the seeded 64-bit byte-string hash of the TxHash -> TxVoteSet table, shared by
+// the device (kernels_flow.hip) and the host (reader lookups, host_pack.hpp's AddrTable), so
+// both sides place a key in the same slot.  Only the table's probe length depends on it: every
+// hit is confirmed by comparing the full key bytes.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define TXV_HASH_HD __host__ __device__ __forceinline__
+#else
+#define TXV_HASH_HD inline
+#endif
+
+namespace txv_hash {
+
+TXV_HASH_HD uint64_t mix64(uint64_t x) {
+  x ^= x >> 32; x *= 0xd6e8feb86659fd93ULL; x ^= x >> 32; x *= 0xd6e8feb86659fd93ULL; x ^= x >> 32;
+  return x;
+}
+
+// hash of n bytes whose little-endian 8-byte chunk at byte i (i % 8 == 0) is get(i); bytes
+// of the last chunk beyond n are masked off here
+template <class Get>
+TXV_HASH_HD uint64_t hash_chunks(uint32_t n, uint64_t seed, Get get) {
+  uint64_t h = seed ^ (0x9e3779b97f4a7c15ULL * (uint64_t)(n + 1));
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) h = mix64(h ^ get(i)) + 0x9e3779b97f4a7c15ULL;
+  if (i < n) {
+    const uint64_t t = get(i) & ((1ull << (8 * (n - i))) - 1ull);
+    h = mix64(h ^ t ^ ((uint64_t)(n - i) << 56));
+  }
+  return mix64(h) | 1ull;   // never 0
+}
+
+}  // namespace txv_hash

@@ -53,14 +53,15 @@ class _Cfg(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_batch", ctypes.c_uint32), ("max_txs", ctypes.c_uint32),
                 ("max_validators", ctypes.c_uint32), ("max_accepted", ctypes.c_uint32),
                 ("max_msg_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("table_budget_mb", ctypes.c_uint32)]
+                ("table_budget_mb", ctypes.c_uint32), ("key_arena_bytes", ctypes.c_uint64)]
 
 
 class _Votes(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("is_nil", ctypes.c_void_p), ("height", ctypes.c_void_p),
                 ("txhash", ctypes.c_void_p), ("txhash_off", ctypes.c_void_p), ("txhash_len", ctypes.c_void_p),
                 ("ts_sec", ctypes.c_void_p), ("ts_nanos", ctypes.c_void_p), ("addr", ctypes.c_void_p),
-                ("addr_len", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_void_p)]
+                ("addr_len", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_void_p),
+                ("txkey", ctypes.c_void_p)]
 
 
 class _PoolCfg(ctypes.Structure):
@@ -144,6 +145,17 @@ def lib():
             "txv_pool_receive": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp], ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
+            "txv_make_commit": ([vp, ctypes.c_char_p, u32, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)],
+                                ctypes.c_int),
+            "txv_save_tx_bytes": ([vp, ctypes.c_char_p, u32, vp, ctypes.c_uint64, vp], ctypes.c_int),
+            "txv_host_register": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
+            "txv_host_unregister": ([vp, vp], ctypes.c_int),
+            "txv_shard_of": ([vp, vp, vp, u32, u32, vp], ctypes.c_int),
+            "txv_commit_state_bytes": ([u32], ctypes.c_uint64),
+            "txv_pack_commit_state": ([vp, vp, u32], ctypes.c_int),
+            "txv_commit_state_pack_host": ([u32, vp, vp, u32, vp], ctypes.c_int),
+            "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -162,7 +174,10 @@ EXPORTED_SYMBOLS = [
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys",
-    "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs"]
+    "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
+    "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
+    "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_commit_state_pack_host",
+    "txv_commit_state_unpack"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -204,7 +219,7 @@ class VoteBatch:
     """Structure-of-arrays TxVote batch matching txv_votes (include/txvote.h)."""
 
     def __init__(self, n: int, *, height, txhash_arena, txhash_off, txhash_len, ts_sec, ts_nanos,
-                 addr, addr_len, sig, sig_len, is_nil=None):
+                 addr, addr_len, sig, sig_len, is_nil=None, txkey=None):
         self.n = int(n)
         c = np.ascontiguousarray
         self.height = c(height, dtype=np.int64)
@@ -221,7 +236,9 @@ class VoteBatch:
         self.sig = c(sig, dtype=np.uint8).reshape(-1)
         self.sig_len = c(sig_len, dtype=np.uint32)
         self.is_nil = None if is_nil is None else c(is_nil, dtype=np.uint8)
+        self.txkey = None if txkey is None else c(txkey, dtype=np.uint8).reshape(-1)
         assert self.addr.size == 20 * self.n and self.sig.size == 64 * self.n
+        assert self.txkey is None or self.txkey.size == 32 * self.n
 
     @classmethod
     def from_votes(cls, votes: Sequence[Optional[TxVote]]) -> "VoteBatch":
@@ -232,10 +249,12 @@ class VoteBatch:
         addr = np.zeros((n, 20), np.uint8); al = np.zeros(n, np.uint32)
         sig = np.zeros((n, 64), np.uint8); sl = np.zeros(n, np.uint32)
         nil = np.zeros(n, np.uint8)
+        tk = np.zeros((n, 32), np.uint8)
         for i, v in enumerate(votes):
             if v is None:
                 nil[i] = 1
                 continue
+            tk[i] = np.frombuffer(bytes(v.TxKey)[:32].ljust(32, b"\0"), np.uint8)
             th = v.TxHash.encode() if isinstance(v.TxHash, str) else v.TxHash
             off[i] = len(arena); ln[i] = len(th); arena += th
             h[i] = v.Height; ts[i], tn[i] = v.Timestamp
@@ -244,7 +263,7 @@ class VoteBatch:
             s = v.Signature or b""
             sl[i] = len(s); sig[i, :min(64, len(s))] = np.frombuffer(s[:64], np.uint8)
         return cls(n, height=h, txhash_arena=bytes(arena), txhash_off=off, txhash_len=ln, ts_sec=ts,
-                   ts_nanos=tn, addr=addr, addr_len=al, sig=sig, sig_len=sl, is_nil=nil)
+                   ts_nanos=tn, addr=addr, addr_len=al, sig=sig, sig_len=sl, is_nil=nil, txkey=tk)
 
     def c_struct(self) -> _Votes:
         v = _Votes()
@@ -260,6 +279,7 @@ class VoteBatch:
         v.addr_len = self.addr_len.ctypes.data
         v.sig = self.sig.ctypes.data
         v.sig_len = self.sig_len.ctypes.data
+        v.txkey = None if self.txkey is None else self.txkey.ctypes.data
         return v
 
     def txhash(self, i: int) -> bytes:
@@ -349,7 +369,8 @@ class DecodedMsgs:
         n = self.n
         return VoteBatch(n, height=self.height[:n], txhash_arena=self.wb.wire, txhash_off=self.txhash_off[:n],
                          txhash_len=self.txhash_len[:n], ts_sec=self.ts_sec[:n], ts_nanos=self.ts_nanos[:n],
-                         addr=self.addr[:n], addr_len=self.addr_len[:n], sig=self.sig[:n], sig_len=self.sig_len[:n])
+                         addr=self.addr[:n], addr_len=self.addr_len[:n], sig=self.sig[:n], sig_len=self.sig_len[:n],
+                         txkey=self.txkey[:n])
 
     def vote(self, i: int) -> Optional[TxVote]:
         if self.status[i] != WIRE_OK:
@@ -371,7 +392,7 @@ class Context:
     def __init__(self, device: int = -1, max_batch: int = 1 << 20, max_txs: int = 1 << 20,
                  max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
                  table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0,
-                 base_w: int = 0):
+                 base_w: int = 0, key_arena_bytes: int = 0):
         """table_w: fixed-base window (4, 8, 10, 12, 14, 16, 18, 20) or None = the largest whose
         per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
         if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20):
@@ -380,7 +401,7 @@ class Context:
             raise ValueError("lane_votes must be 0 (default), 1 (split K1b/K1c), 2, 4 or 8")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,
                    (((table_w or 0) & 0xFF) << 8) | ((lane_votes & 0xF) << 16) | ((base_w & 0xFF) << 20),
-                   table_budget_mb)
+                   table_budget_mb, key_arena_bytes)
         h = ctypes.c_void_p()
         rc = lib().txv_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
@@ -507,6 +528,53 @@ class Context:
         r = self._chk(lib().txv_query_tx(self._h, txhash, len(txhash), ctypes.byref(s), ctypes.byref(m)), "query")
         return (s.value, bool(m.value)) if r == 1 else None
 
+    def query_txs(self, hashes: Sequence[bytes]):
+        """batched readers: (exists [n] bool, sum [n] i64, maj23 [n] bool, TxKey [n, 32] u8)"""
+        n = len(hashes)
+        arena = np.frombuffer(b"".join(hashes) or b"\0", np.uint8)
+        ln = np.array([len(h) for h in hashes] or [0], np.uint32)
+        off = np.concatenate([[0], np.cumsum(ln[:-1], dtype=np.uint64)]).astype(np.uint32)
+        ex = np.zeros(max(n, 1), np.uint8); sm = np.zeros(max(n, 1), np.int64); mj = np.zeros(max(n, 1), np.uint8)
+        tk = np.zeros((max(n, 1), 32), np.uint8)
+        self._chk(lib().txv_query_txs(self._h, arena.ctypes.data, off.ctypes.data, ln.ctypes.data, n, ex.ctypes.data,
+                                      sm.ctypes.data, mj.ctypes.data, tk.ctypes.data), "txv_query_txs")
+        return ex[:n].astype(bool), sm[:n], mj[:n].astype(bool), tk[:n]
+
+    def make_commit(self, txhash: bytes) -> bytes:
+        """TxVoteSet.MakeCommit amino bytes (CommitSigs in validator order)"""
+        ln = ctypes.c_uint64()
+        rc = lib().txv_make_commit(self._h, txhash, len(txhash), None, 0, ctypes.byref(ln))
+        if rc not in (0, -28):
+            self._chk(rc, "txv_make_commit")
+        out = ctypes.create_string_buffer(max(ln.value, 1))
+        self._chk(lib().txv_make_commit(self._h, txhash, len(txhash), out, ln.value, ctypes.byref(ln)), "txv_make_commit")
+        return out.raw[:ln.value]
+
+    def save_tx_bytes(self, txhash: bytes):
+        """TxStore.SaveTx's two db.Set calls: (H-key, TxVoteSet bytes, C-key, Commit bytes)"""
+        lens = np.zeros(4, np.uint64)
+        rc = lib().txv_save_tx_bytes(self._h, txhash, len(txhash), None, 0, lens.ctypes.data)
+        if rc not in (0, -28):
+            self._chk(rc, "txv_save_tx_bytes")
+        out = ctypes.create_string_buffer(max(int(lens.sum()), 1))
+        self._chk(lib().txv_save_tx_bytes(self._h, txhash, len(txhash), out, int(lens.sum()), lens.ctypes.data),
+                  "txv_save_tx_bytes")
+        parts, at = [], 0
+        for L in lens.tolist():
+            parts.append(out.raw[at:at + int(L)])
+            at += int(L)
+        return tuple(parts)
+
+    def host_register(self, arr: np.ndarray):
+        """pin a host array so batch columns inside it are DMA'd without a staging copy"""
+        self._chk(lib().txv_host_register(self._h, arr.ctypes.data, arr.nbytes), "txv_host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        self._chk(lib().txv_host_unregister(self._h, arr.ctypes.data), "txv_host_unregister")
+
+    def pack_commit_state(self, dst_dev_ptr: int, n_sets_cap: int):
+        self._chk(lib().txv_pack_commit_state(self._h, ctypes.c_void_p(dst_dev_ptr), n_sets_cap), "pack state")
+
     def num_tx_sets(self) -> int:
         return lib().txv_num_tx_sets(self._h)
 
@@ -533,9 +601,10 @@ class Context:
         self._chk(lib().txv_stage(self._h, slot, ctypes.byref(vs)), "txv_stage")
 
     def run_staged(self, slot: int, timed: bool = False):
-        ms = (ctypes.c_float * 3)()
+        """timed: (route, verify, tally, total) device ms of this run"""
+        ms = (ctypes.c_float * 4)()
         self._chk(lib().txv_run_staged(self._h, slot, ms if timed else None), "txv_run_staged")
-        return (ms[0], ms[1], ms[2]) if timed else None
+        return (ms[0], ms[1], ms[2], ms[3]) if timed else None
 
     def fetch_staged(self, slot: int, n: int, ev_cap: int = 0, out: np.ndarray | None = None,
                      evs: np.ndarray | None = None):
@@ -621,6 +690,48 @@ class Context:
         out = np.zeros((n, 8), np.uint32)
         self._chk(lib().txv_fe_selftest(self._h, a.ctypes.data, b.ctypes.data, out.ctypes.data, n, op), "selftest")
         return out
+
+
+def shard_of(hashes: Sequence[bytes], n_shards: int) -> np.ndarray:
+    """SHA-256(TxHash)[0] mod n_shards per TxHash (txv_shard_of)"""
+    n = len(hashes)
+    arena = np.frombuffer(b"".join(hashes) or b"\0", np.uint8)
+    ln = np.array([len(h) for h in hashes] or [0], np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln[:-1], dtype=np.uint64)]).astype(np.uint32)
+    out = np.zeros(max(n, 1), np.uint32)
+    rc = lib().txv_shard_of(arena.ctypes.data, off.ctypes.data, ln.ctypes.data, n, n_shards, out.ctypes.data)
+    if rc:
+        raise TxvInfraError(f"txv_shard_of failed ({rc})")
+    return out[:n]
+
+
+def commit_state_bytes(n_sets_cap: int) -> int:
+    return int(lib().txv_commit_state_bytes(n_sets_cap))
+
+
+def commit_state_pack_host(committed: np.ndarray, sums: np.ndarray, n_sets_cap: int) -> np.ndarray:
+    """the packed per-shard commit state (txv_pack_commit_state's layout) from host arrays"""
+    committed = np.ascontiguousarray(committed, np.uint8)
+    sums = np.ascontiguousarray(sums, np.int64)
+    out = np.zeros(commit_state_bytes(n_sets_cap), np.uint8)
+    rc = lib().txv_commit_state_pack_host(len(sums), committed.ctypes.data if len(sums) else None,
+                                          sums.ctypes.data if len(sums) else None, n_sets_cap, out.ctypes.data)
+    if rc:
+        raise TxvInfraError(f"txv_commit_state_pack_host failed ({rc})")
+    return out
+
+
+def commit_state_unpack(buf: np.ndarray, n_sets_cap: int):
+    """(committed [n_sets] bool, sums [n_sets] i64) of one packed shard state"""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    ns = ctypes.c_uint32()
+    committed = np.zeros(max(n_sets_cap, 1), np.uint8)
+    sums = np.zeros(max(n_sets_cap, 1), np.int64)
+    rc = lib().txv_commit_state_unpack(buf.ctypes.data, n_sets_cap, ctypes.byref(ns), committed.ctypes.data,
+                                       sums.ctypes.data, n_sets_cap)
+    if rc:
+        raise TxvInfraError(f"txv_commit_state_unpack failed ({rc})")
+    return committed[:ns.value].astype(bool), sums[:ns.value]
 
 
 def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TXV_ABI_VERSION 1
+#define TXV_ABI_VERSION 2
 
 /* ---- return codes (infrastructure) ---- */
 #define TXV_OK 0
@@ -83,28 +83,40 @@ extern "C" {
 
 typedef struct txv_ctx txv_ctx;
 
+/* HBM footprint of a context (MI355X: 288 GB per GPU), all allocated up front:
+ *   validator tables   n_vals x table size of the window (see TXV_CFG_WINDOW): 654 MB each at the
+ *                      default radix-2^20 for <= 125 validators (65 GB for 100), within table_budget_mb
+ *   base-point table   8.9 GB (radix-2^24) per context, plus 0.4 MB / 55 KB for the small windows
+ *   TxFlow state       12 x max_txs x n_vals B of cells + 128 x max_accepted B of accepted votes +
+ *                      64 x 2 (max_txs + max_batch) B of set table + key_arena_bytes (1M sets x 100
+ *                      validators: 1.2 + 8.6 + 0.3 + 0.1 GB)
+ *   per batch slot     ~420 B x max_batch of device columns, ~170 B x max_batch pinned host memory
+ * txv_set_validators rebuilds the validator tables on the device (K0: 0.9 s for 100 validators at
+ * radix-2^20, once per validator set). */
 typedef struct {
   int32_t  device;          /* HIP device ordinal; -1 = current device */
-  uint32_t max_batch;       /* votes per call (default 1<<20) */
+  uint32_t max_batch;       /* votes per call (default 1<<20, at most 8<<20) */
   uint32_t max_txs;         /* TxVoteSets capacity (default 1<<20) */
   uint32_t max_validators;  /* default 1024 */
-  uint32_t max_accepted;    /* accepted-signature arena rows (default min(max_txs * 128, 2^28)); every
-                               txv_add_votes / txv_run_staged batch reserves one row per vote
-                               until txv_reset_tally (TXV_ECAPACITY when exhausted) */
-  uint32_t max_msg_bytes;   /* SignBytes capacity per vote (default 256) */
+  uint32_t max_accepted;    /* accepted votes held (TxVoteSet.votes rows, one per ADDED vote, at most
+                               one per (set, validator)); 0 = min(max_txs x n_vals, 2^26).  A batch that
+                               would exceed it fails with TXV_ECAPACITY (reset with txv_reset_flow) */
+  uint32_t max_msg_bytes;   /* unused since ABI 2 (SignBytes columns are sized per batch) */
   uint32_t flags;           /* TXV_CFG_* bits */
   uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 81920 =
                                80 GiB): the default window is the largest of 20/18/16/14/12/10/8
                                whose tables fit (100 validators: radix-2^20, 65 GB) */
+  uint64_t key_arena_bytes; /* device bytes for the TxHash strings of all TxVoteSets (each rounded up
+                               to 8); 0 = 96 x max_txs + 1 MiB */
 } txv_config;
-/* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the default
- * radix-256 tables (L2/MALL resident, 396 KB/validator, half the point additions) */
+/* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the wider
+ * L2/HBM-resident tables */
 #define TXV_CFG_TABLE_W4 0x1u
-/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18 or 20; 0 = auto by
- * table_budget_mb): per validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB / 189 MB /
- * 654 MB.  Windows >= 12 run against the 8.9 GB radix-2^24 base-point table: 11 + ceil(256/W)
- * point additions per verified vote (33 / 30 / 27 / 26 / 24 at W = 12..20); W = 4 / 8 / 10:
- * 2 * ceil(256/W) = 128 / 64 / 52 */
+/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18 or 20; 0 = auto: the
+ * largest whose n_vals tables fit table_budget_mb, radix-2^20 for <= 125 validators): per
+ * validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB / 189 MB / 654 MB.  Windows >= 12 run
+ * against the 8.9 GB radix-2^24 base-point table: 11 + ceil(256/W) point additions per verified
+ * vote (33 / 30 / 27 / 26 / 24 at W = 12..20); W = 4 / 8 / 10: 2 * ceil(256/W) = 128 / 64 / 52 */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19:
@@ -133,6 +145,9 @@ typedef struct {
   const uint32_t* addr_len;    /* [n] len(ValidatorAddress) (0 = empty) */
   const uint8_t*  sig;         /* [n][64] Signature bytes (first 64) */
   const uint32_t* sig_len;     /* [n] len(Signature) */
+  const uint8_t*  txkey;       /* [n][32] TxKey, or NULL (zero keys).  A new TxVoteSet takes its first
+                                  vote's TxKey (txflow/service.go:201-207); accepted votes keep theirs
+                                  (MakeCommit).  Not part of SignBytes (types/tx_vote.go:185-191) */
 } txv_votes;
 
 typedef struct {
@@ -171,17 +186,23 @@ int txv_verify_bytes(txv_ctx* ctx, const uint8_t* pubs32, const uint8_t* msgs, c
 
 /* TxFlow.TryAddVote for each vote in arrival order (votes[0] first).  Semantics are exactly
  * the sequential loop's; see SURVEY.md Appendix A.3.  ev_out (capacity ev_cap) receives one
- * event per tx whose 2/3 crossing happened in this batch; *n_ev its count. */
+ * event per tx whose 2/3 crossing happened in this batch, in arrival order of the crossing vote
+ * (the order the reference runs its commit side effects); *n_ev their count.  Every decision is
+ * made on the GPU: TxHash -> TxVoteSet routing (set ids in first-seen order), validator lookup,
+ * pre-checks, SignBytes, verify, the first-accepted resolution per (set, validator), stake sums
+ * and crossings; the host only moves the columns (registered memory: DMA only). */
 int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
                   txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev);
 
 /* txv_add_votes split for pipelining (north_star: pinned SoA batches uploaded on a side stream):
- * txv_submit_votes packs the batch on the host, queues its upload on the copy stream and its
- * verify + tally kernels and result copies on the compute stream, and returns a ticket without
- * waiting; txv_wait_votes(ticket) waits for those results and reports exactly what txv_add_votes
- * would have.  At most two batches may be in flight; tickets are waited in submission order.
- * The host pack of batch k+1 (and its upload) overlaps the kernels of batch k.  TxVoteSet
- * readers (txv_query_tx) reflect a batch once it has been waited for. */
+ * txv_submit_votes copies the batch's columns into pinned memory (registered columns: none),
+ * queues their upload on the copy stream and the kernel chain on the compute stream, and returns
+ * a ticket without waiting; txv_wait_votes(ticket) waits for the results and reports exactly what
+ * txv_add_votes would have.  At most two batches may be in flight; tickets are waited in
+ * submission order.  The staging of batch k+1 and its upload overlap the kernels of batch k.
+ * Registered columns (txv_host_register) are read by DMA until txv_wait_votes returns for the
+ * ticket; other caller buffers may be reused as soon as txv_submit_votes returns.  The TxVoteSet
+ * readers (txv_query_tx*, txv_get_votes, txv_make_commit, ...) run after every submitted batch. */
 int txv_submit_votes(txv_ctx* ctx, const txv_votes* votes, uint64_t* ticket);
 int txv_wait_votes(txv_ctx* ctx, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev_out, uint32_t ev_cap,
                    uint32_t* n_ev);
@@ -199,6 +220,22 @@ int txv_get_votes(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, uint32_t* v
 
 /* Tally readers for the TxVoteSet of txhash.  Returns 1 if the set exists, 0 if not. */
 int txv_query_tx(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, int64_t* sum, uint8_t* maj23);
+/* the same for n TxHashes (txhash + off[i], len[i] bytes); any output may be NULL; txkey_out
+ * [n][32] = TxVoteSet.TxKey (types/vote_set.go:24) */
+int txv_query_txs(txv_ctx* ctx, const uint8_t* txhash, const uint32_t* off, const uint32_t* len, uint32_t n,
+                  uint8_t* exists_out, int64_t* sum_out, uint8_t* maj23_out, uint8_t* txkey_out);
+
+/* ---- commit side effects (txflow/service.go:216-232) ----
+ * TxVoteSet.MakeCommit (types/vote_set.go:242-259): cdc.MustMarshalBinaryBare(Commit{TxHash,
+ * Commits}) with one CommitSig (= the accepted TxVote, types/tx_vote.go:154-159) per validator that
+ * has one, in validator-index order (the reference lists a Go map: any order; each CommitSig's
+ * bytes are exact).  TXV_ESTATE without +2/3 (the reference panics) or without the set;
+ * TXV_ECAPACITY (*len_out set) when cap is too small. */
+int txv_make_commit(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, uint8_t* out, uint64_t cap, uint64_t* len_out);
+/* TxStore.SaveTx (tx/store.go:83-107): out = calcTxKey ("H:%X") | MustMarshalBinaryBare(TxVoteSet)
+ * (TxHash, TxKey) | calcTxCommitKey ("C:%X") | MakeCommit bytes; lens_out = the four lengths. */
+int txv_save_tx_bytes(txv_ctx* ctx, const uint8_t* txhash, uint32_t len, uint8_t* out, uint64_t cap,
+                      uint64_t lens_out[4]);
 uint32_t txv_num_tx_sets(txv_ctx* ctx);
 int64_t  txv_total_power(txv_ctx* ctx);
 
@@ -216,14 +253,32 @@ int txv_sign_votes(txv_ctx* ctx, const txv_votes* votes, const uint32_t* signer,
                    uint32_t chain_len, uint8_t* sig_out);
 
 /* ---- device-resident batches (benchmark / pipelined ingest) ----
- * txv_stage: pack + upload a batch into device slot `slot` (host work + H2D, not timed).
- * txv_run_staged: run verify + tally on the staged batch entirely on device; results stay
- *   on device until txv_fetch_staged.  kernel_ms_out (optional, 3 entries): verify / tally /
- *   total device time of this run measured with HIP events on the stream the kernels run on. */
+ * txv_stage: upload a batch's raw columns into device slot `slot` (0 or 1; TXV_ESTATE while the
+ *   slot holds a txv_submit_votes batch).
+ * txv_run_staged: run the whole AddVote kernel chain on the staged batch; results land in host
+ *   memory for txv_fetch_staged.  kernel_ms_out (optional, 4 entries): route (TxHash keying,
+ *   pre-checks, SignBytes) / verify / tally / total device time of this run, measured with HIP
+ *   events on the stream the kernels run on. */
 int txv_stage(txv_ctx* ctx, uint32_t slot, const txv_votes* votes);
 int txv_run_staged(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
 int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commit_event* ev_out,
                      uint32_t ev_cap, uint32_t* n_ev);
+/* caller host memory the AddVote path may DMA from directly (hipHostRegister): columns of a
+ * txv_votes batch lying inside a registered range skip the staging copy */
+int txv_host_register(txv_ctx* ctx, void* ptr, uint64_t bytes);
+int txv_host_unregister(txv_ctx* ctx, void* ptr);
+/* ---- multi-GPU: votes shard by SHA-256(TxHash)[0] mod n_shards; each shard's
+ * commit state is packed as [n_sets u32][0 u32][bitmap: ceil(cap/32) u32][sums: cap i64] ---- */
+int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len, uint32_t n, uint32_t n_shards,
+                 uint32_t* shard_out);
+uint64_t txv_commit_state_bytes(uint32_t n_sets_cap);
+/* this context's state into caller device memory (e.g. an RCCL all-gather buffer) */
+int txv_pack_commit_state(txv_ctx* ctx, void* dst_dev, uint32_t n_sets_cap);
+/* host-side pack (from per-set committed flags and sums) and unpack of the same layout */
+int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
+                               void* dst);
+int txv_commit_state_unpack(const void* src, uint32_t n_sets_cap, uint32_t* n_sets, uint8_t* committed, int64_t* sums,
+                            uint32_t cap);
 /* device pointer + byte size of the per-set committed bitmap (1 bit per tx-set id) */
 int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 /* device-to-device copy of the commit bitmap into caller device memory (e.g. an RCCL buffer) */
@@ -233,12 +288,13 @@ int txv_copy_commit_bitmap(txv_ctx* ctx, void* dst_dev, uint64_t bytes);
 int txv_copy_set_sums(txv_ctx* ctx, void* dst_dev, uint32_t n_sets);
 /* measured integer-VALU issue rates of this device (lane-ops/s): v_add_u32 and v_mad_u64_u32 */
 int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
-/* fixed-base window of the current validator tables (4..16), 0 before txv_set_validators */
+/* fixed-base window of the current validator tables (4..20), 0 before txv_set_validators */
 int txv_table_window(txv_ctx* ctx);
 /* window of the base-point table the verify kernel uses (>= the validator window) */
 int txv_base_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids
- * already assigned stay assigned (their sets read as empty) */
+ * already assigned stay assigned (their sets read as empty).  Both resets run in stream order
+ * after every batch already submitted; vote sequence numbers restart at 0 */
 int txv_reset_tally(txv_ctx* ctx);
 /* a fresh TxFlow: forget every TxVoteSet and its tx id (TxVoteSets = make(map...) in NewTxFlow,
  * txflow/service.go:71), keeping the validator set and its tables */

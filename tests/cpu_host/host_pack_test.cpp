@@ -23,37 +23,25 @@ int main(int argc, char** argv) {
       for (uint32_t i = 0; i < n; ++i) if (hits[i] != 1) return fail("pool hit count", i, hits[i]);
     }
   }
-  // TxTable: ids in first-seen order, find after rehash, limit respected, clear
+  // hash_bytes (txv_hash.h, shared with the device set table): chunk-wise definition, tail bytes
+  // beyond the key never matter, never 0
   {
-    TxTable t(12345);
     std::mt19937_64 rng(7);
-    std::map<std::string, uint32_t> ref;
-    std::vector<std::string> keys;
-    for (int i = 0; i < 50000; ++i) {
-      std::string k;
-      const int len = (int)(rng() % 80);   // includes empty keys and non-multiple-of-8 lengths
-      for (int j = 0; j < len; ++j) k.push_back((char)(rng() % 16 + 'A'));
-      if (rng() % 3 == 0 && !keys.empty()) k = keys[rng() % keys.size()];
-      keys.push_back(k);
-      bool created;
-      const uint32_t id = t.intern((const uint8_t*)k.data(), (uint32_t)k.size(), t.hash((const uint8_t*)k.data(), (uint32_t)k.size()), &created);
-      auto it = ref.find(k);
-      if (it == ref.end()) {
-        if (!created || id != ref.size()) return fail("intern new id", id, (long)ref.size());
-        ref.emplace(k, id);
-      } else if (created || id != it->second) return fail("intern existing id", id, it->second);
+    for (int it = 0; it < 20000; ++it) {
+      const uint32_t len = (uint32_t)(rng() % 80);
+      std::vector<uint8_t> a(len + 16), b(len + 16);
+      for (auto& x : a) x = (uint8_t)rng();
+      b = a;
+      for (uint32_t j = len; j < len + 16; ++j) b[j] = (uint8_t)rng();   // different bytes after the key
+      const uint64_t seed = rng();
+      const uint64_t ha = hash_bytes(a.data(), len, seed), hb = hash_bytes(b.data(), len, seed);
+      if (ha != hb || !ha) return fail("hash tail", (long)len, 0);
+      uint64_t h = seed ^ (0x9e3779b97f4a7c15ULL * (uint64_t)(len + 1));
+      uint32_t i = 0;
+      for (; i + 8 <= len; i += 8) { uint64_t w; memcpy(&w, a.data() + i, 8); h = txv_hash::mix64(h ^ w) + 0x9e3779b97f4a7c15ULL; }
+      if (i < len) { uint64_t t = 0; memcpy(&t, a.data() + i, len - i); h = txv_hash::mix64(h ^ t ^ ((uint64_t)(len - i) << 56)); }
+      if ((txv_hash::mix64(h) | 1ull) != ha) return fail("hash def", (long)len, 1);
     }
-    for (auto& kv : ref) {
-      const uint32_t id = t.find((const uint8_t*)kv.first.data(), (uint32_t)kv.first.size(),
-                                 t.hash((const uint8_t*)kv.first.data(), (uint32_t)kv.first.size()));
-      if (id != kv.second) return fail("find", id, kv.second);
-    }
-    if (t.size() != ref.size()) return fail("size", t.size(), (long)ref.size());
-    bool created;
-    const uint8_t nk[3] = {1, 2, 3};
-    if (t.intern(nk, 3, t.hash(nk, 3), &created, t.size()) != UINT32_MAX || created) return fail("limit", 0, 1);
-    t.clear();
-    if (t.size() != 0 || t.find(nk, 3, t.hash(nk, 3)) != UINT32_MAX) return fail("clear", t.size(), 0);
   }
   // AddrTable: exact 20-byte match, first index wins on a repeated address, misses
   {
