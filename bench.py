@@ -2,20 +2,28 @@
 """bench.py — verified+tallied TxVotes/sec on MI355X (BASELINE.json metric).
 
 Workload: per GPU, 100 validators (power 1, quorum 67) x 10,000 txs
-= 1,000,000 ed25519-signed TxVotes in shuffled arrival order (config C2 at N=1; at N>1 each
-rank holds its shard = SHA-256(TxHash)[0] mod N of N x 10,000 txs, the C3 layout, weak
-scaling).  Signatures come from the device signer; inputs are staged in HBM before timing.
+= 1,000,000 ed25519-signed TxVotes in shuffled arrival order (config C2 at N=1).  At N>1 each
+rank holds its shard (SHA-256(TxHash)[0] mod N, txv_shard_of) of N x 20,000 txs: the C3 layout
+(16M votes at N = 8, ~2M per GPU), weak scaling.  Signatures come from the device signer.
 
-One step = one pass of the hot path over the resident batch: empty all TxVoteSets
-(device memsets), K1 verify every vote, K2 tally (first-accepted resolution, stake sums,
-2/3 crossings, commit bitmap), read back per-vote statuses; at N>1 also an RCCL all-gather
-of the per-shard commit bitmaps.  value = votes processed by all ranks / max-over-ranks time.
+One step = one pass of the hot path over the batch, inputs resident in HBM: a fresh TxFlow
+(txv_reset_flow), then the whole AddVote kernel chain of txv_run_staged -- TxHash routing to
+TxVoteSets (device hash table, first-seen ids), validator lookup and pre-checks, SignBytes,
+K1a/K1b verify, the first-accepted resolution, stake sums and 2/3 crossings -- and the per-vote
+statuses + commit events in host memory; at N>1 also the packed per-shard commit state
+all-gathered over RCCL.  value = votes processed by all ranks / max-over-ranks time.
+
+Beside it: the end-to-end rate from the caller's host SoA columns (txv_submit_votes /
+txv_wait_votes, two batches in flight: staging copy + PCIe upload + kernels + results), the
+CPU baseline (the oracle's C restatement on every allowed host core, and 1 thread), the
+TxVoteMessage wire-decode leg and the C5 streaming leg.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 """
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -26,62 +34,147 @@ sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
 
 import numpy as np  # noqa: E402
 
-W_ALG = 2.5e5   # int32 VALU lane-ops per verified vote, SURVEY.md §8d (Straus reference algorithm)
-TALLY_BYTES_PER_VOTE = 16.0   # SURVEY.md §8d algorithmic tally traffic
+# Roofline of the verify pair (K1a + K1b), integer VALU.  Peak = 256 CU x 4 SIMD x 32 lanes/clk x
+# 2.4 GHz (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle)").
+VALU_PEAK = 256 * 4 * 32 * 2.4e9
+# Algorithmic int32 lane-ops per verified vote of the algorithm that runs:
+#   SHA-512 of R||A||SignBytes, 2 blocks + ScReduce                      1.1e4
+#   [s]B + [k](-A) over fixed-base tables: 11 + 13 mixed additions x 7 FM   168 FM
+#   encode (2 FM), Montgomery batch inverse (3 FM / vote), divstep inverse / 8 (~8 FM-eq)  13 FM
+#   at 100 lane-ops per 255-bit field multiply (SURVEY.md §8d cost model)  -> 1.81e4
+W_ALG = 1.1e4 + (24 * 7 + 2 + 3 + 8) * 100.0
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cores() -> int:
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota if one is set"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(p))))
+    except Exception:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(wl, threads: int, serial_votes: int, parallel_votes: int):
-    """The oracle's C restatement of the reference path on this host (kind "port"):
-    serial = TxFlow.addVote loop with verification inside (1 goroutine, txflow/service.go:123-166);
-    parallel = verify on `threads` host threads + the sequential tally with those verdicts."""
+    """The oracle's C restatement of the reference path on this host (kind "port": the Go
+    reference cannot be built here): TxFlow.addVote over the same SoA batch -- SignBytes, ed25519
+    Verify on `threads` host threads, then the sequential tally (txflow/service.go:192-234) -- and
+    the 1-thread form (the reference's single checkMaj23Routine goroutine, service.go:123-166)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
-    n = wl.n
-    # serial: sequential AddVote with verification
-    idx = np.arange(min(serial_votes, n))
-    votes = [wl.vote(int(i)) for i in idx]
-    flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
-    flow.add_votes(votes)
-    ts = flow.last_seconds
-    serial_rate = len(votes) / ts
-    # parallel verify + sequential tally
-    m = min(parallel_votes, n)
-    msgs = [O.signbytes(1, wl.batch.txhash(i), int(wl.batch.ts_sec[i]), int(wl.batch.ts_nanos[i]), b"test_chain_id")
-            for i in range(m)]
-    arena = np.frombuffer(b"".join(msgs), np.uint8)
-    lens = np.array([len(x) for x in msgs], np.uint16)
-    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint32)
-    pubs = np.frombuffer(b"".join(wl.pubs), np.uint8)
-    tv, ok = O.verify_many(pubs, wl.val_of[:m], arena, offs, lens, wl.batch.sig[:64 * m], threads)
-    flow2 = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
-    pv = [wl.vote(i) for i in range(m)]
-    flow2.add_votes(pv, verdicts=ok)
-    tt = flow2.last_seconds
-    par_rate = m / (tv + tt)
-    assert ok.all()
-    return dict(value=round(par_rate, 1), unit="votes/s", cores=threads, kind="port",
-                sample=f"first {m} votes of the same workload: {threads}-thread oracle ed25519 verify "
-                       f"({tv:.2f}s) + sequential TxFlow.addVote tally ({tt:.2f}s); "
-                       f"serial 1-thread verify-inside-AddVote on {len(votes)} votes = {serial_rate:.1f} votes/s",
-                serial_value=round(serial_rate, 1), serial_cores=1)
+    out = {}
+    for name, m, th in (("parallel", min(parallel_votes, wl.n), threads), ("serial", min(serial_votes, wl.n), 1)):
+        flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        b = wl.head(m)
+        t0 = time.perf_counter()
+        st, _, _ = flow.add_batch(b, th)
+        secs = time.perf_counter() - t0
+        assert (st == 0).all(), "CPU baseline: a valid vote was not ADDED"
+        out[name] = (m, secs)
+    (mp, sp), (ms, ss) = out["parallel"], out["serial"]
+    return dict(value=round(mp / sp, 1), unit="votes/s", cores=threads, kind="port",
+                sample=f"first {mp} votes of the same workload through the oracle's TxFlow.addVote "
+                       f"(SignBytes + Verify on {threads} threads + sequential tally, {sp:.2f}s); "
+                       f"1 thread on the first {ms} votes = {ms / ss:.1f} votes/s",
+                serial_value=round(ms / ss, 1), serial_cores=1)
+
+
+def c1_leg(device: int, threads: int):
+    """C1 (BASELINE.json configs[0]): 4 validators, 10k signed TxVotes (2,500 txs x 4), the
+    reference's own CPU config: the oracle on 1 thread and on every core, and the same batch
+    end to end on the GPU (txv_add_votes: host SoA in, statuses and events out)."""
+    import txflow_amd as T
+    from txflow_amd.workload import Workload, SEEDS
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    ctx = T.Context(device=device, max_batch=16384, max_txs=4096, max_validators=8)
+    wl = Workload(ctx, 4, 2500, SEEDS["c1"])
+    res = {}
+    for name, th in (("serial", 1), ("parallel", threads)):
+        flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        t0 = time.perf_counter()
+        ost, _, ofired = flow.add_batch(wl.batch, th)
+        res[name] = wl.n / (time.perf_counter() - t0)
+    exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+    st, ev = ctx.add_votes(wl.batch)
+    ctx.reset_flow()
+    reps, t0 = 20, time.perf_counter()
+    for _ in range(reps):
+        st, ev = ctx.add_votes(wl.batch)
+        ctx.reset_flow()
+    gpu = wl.n * reps / (time.perf_counter() - t0)
+    ok = bool(np.array_equal(st, exp)) and len(ev) == wl.n_txs
+    ctx.close()
+    return {"workload": "C1: 4 validators x 2,500 txs = 10,000 signed TxVotes", "correct": ok,
+            "cpu_serial_votes_per_s": round(res["serial"], 1),
+            "cpu_parallel_votes_per_s": round(res["parallel"], 1), "cpu_cores": threads,
+            "gpu_end_to_end_votes_per_s": round(gpu, 1)}
+
+
+def end_to_end_leg(ctx, wl, steps: int, registered: bool):
+    """Host SoA -> statuses + commit events: txv_reset_flow + txv_submit_votes per step, two steps
+    in flight (step k+1's staging copy and upload overlap step k's kernels), txv_wait_votes."""
+    import txflow_amd as T
+    b = wl.batch
+    cols = [b.height, b.ts_sec, b.ts_nanos, b.txhash_off, b.txhash_len, b.addr, b.addr_len, b.sig, b.sig_len,
+            b.txhash_arena] + ([b.txkey] if b.txkey is not None else [])
+    if registered:
+        for a in cols:
+            ctx.host_register(a)
+    col_bytes = sum(a.nbytes for a in cols)
+    inflight, lat, ok = [], [], True
+    st_buf = None
+
+    def drain():
+        nonlocal ok
+        t_sub, tk = inflight.pop(0)
+        st, ev = ctx.wait_votes(tk, ev_cap=wl.n_txs + 1)
+        lat.append((time.perf_counter() - t_sub) * 1e3)
+        ok = ok and len(ev) == wl.n_txs and int(np.count_nonzero((st & 0x7F) == T.ADDED)) == wl.n
+
+    for _ in range(2):                      # warm-up: first touch of the staging buffers
+        ctx.reset_flow()
+        inflight.append((time.perf_counter(), ctx.submit_votes(b)))
+        drain()
+    lat.clear()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.reset_flow()
+        if len(inflight) == 2:
+            drain()
+        inflight.append((time.perf_counter(), ctx.submit_votes(b)))
+    while inflight:
+        drain()
+    el = time.perf_counter() - t0
+    if registered:
+        for a in cols:
+            ctx.host_unregister(a)
+    del st_buf
+    return {"votes_per_s": round(wl.n * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 3),
+            "p50_batch_ms": round(float(np.median(lat)), 3), "host_bytes_per_step": col_bytes,
+            "pcie_GBps": round(col_bytes * steps / el / 1e9, 2), "correct": ok}
 
 
 def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     """C5: 1000 weighted validators, the stream cut into `batch`-vote batches fed
     through the pool ingest (txv_pool_check: SHA-256(Signature) keys on the GPU, LRU + pool list on
-    the host) and txv_submit_votes / txv_wait_votes (host amino + routing + pack, H2D on the copy
-    stream, verify + tally kernels, statuses and commit events back), two batches in flight so the
-    host work of batch k+1 overlaps the kernels of batch k.  Latency-to-commit of a tx = return of the call that reported its commit
-    event - submission of the batch holding its first vote."""
+    the host) and txv_submit_votes / txv_wait_votes (columns staged + uploaded on the copy stream,
+    the whole AddVote chain on the GPU, statuses and commit events back), two batches in flight.
+    Latency-to-commit of a tx = return of the call that reported its commit event - submission of
+    the batch holding its first vote."""
     import txflow_amd as T
     from txflow_amd.workload import StreamWorkload, SEEDS
-    ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals,
-                    max_accepted=n_txs * n_vals + 4 * batch)
+    ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
     ctx.bind_host_numa()
     wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch)
     # Reactor.Receive -> TxVotePool.CheckTxWithInfo (GPU keys + host LRU) -> TxFlow.TryAddVote
@@ -109,7 +202,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
 
     # Reactor.Receive -> CheckTx runs on its own thread (the reference's per-peer Receive goroutines)
     # while the main thread drives TxFlow (checkMaj23Routine): batch k+1's pool check overlaps
-    # batch k's pack / kernels.  ctypes releases the GIL inside both calls.
+    # batch k's upload / kernels.  ctypes releases the GIL inside both calls.
     import queue
     import threading
     checked = queue.Queue(maxsize=2)
@@ -172,7 +265,7 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
     length per message read + a 160 B record written.  Also the host-inclusive rate (upload,
     decode, results copied into the caller's arrays) and the oracle's C decoder on one host thread."""
     import txflow_amd as T
-    wb = T.encode_msgs(wl.batch)
+    wb = T.encode_msgs(wl.batch, wl.batch.txkey)
     ctx.decode_stage(wb)
     ctx.decode_run(reps=2)
     kms = ctx.decode_run(reps=reps)
@@ -182,7 +275,8 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
     ok = bool((d.status[:n] == T.WIRE_OK).all() and (d.height[:n] == b.height).all() and
               (d.ts_sec[:n] == b.ts_sec).all() and (d.ts_nanos[:n] == b.ts_nanos).all() and
               (d.sig[:n].reshape(-1) == b.sig).all() and (d.addr[:n].reshape(-1) == b.addr).all() and
-              (d.txhash_len[:n] == b.txhash_len).all() and (d.sig_len[:n] == b.sig_len).all())
+              (d.txhash_len[:n] == b.txhash_len).all() and (d.sig_len[:n] == b.sig_len).all() and
+              (d.txkey[:n].reshape(-1) == b.txkey).all())
     alg = wb.nbytes + n * (12 + WIRE_OUT_BYTES)
     traffic, pmc_src = None, None   # HBM bytes per launch from the committed PMC passes of this kernel
     pmc = os.path.join(ROOT, "profiles", "pmc_wire.json")
@@ -190,7 +284,7 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
         try:
             with open(pmc) as f:
                 pj = json.load(f)
-            if pj.get("msgs_per_launch") == n:
+            if pj.get("msgs_per_launch") == n and pj.get("wire_bytes") in (None, wb.nbytes):
                 traffic, pmc_src = pj.get("traffic"), pj.get("source")
         except Exception:
             pass
@@ -216,15 +310,33 @@ def wire_decode_leg(ctx, wl, cpu: bool, reps: int = 20):
     return out
 
 
+def load_pmc(table_w: int, n_votes: int):
+    """executed VALU lane-slots / vote and HBM bytes / launch of the verify pair from the committed
+    PMC passes (profiles/pmc_verify.json), when they were taken on this kernel configuration"""
+    pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
+    if not os.path.exists(pmc):
+        return None, None, None
+    try:
+        with open(pmc) as f:
+            pj = json.load(f)
+    except Exception:
+        return None, None, None
+    if pj.get("table_window") != table_w:
+        return None, None, None
+    traffic = pj.get("hbm_bytes_per_launch") if pj.get("votes_per_launch", n_votes) == n_votes else None
+    return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--validators", type=int, default=100)
-    ap.add_argument("--txs-per-gpu", type=int, default=10_000)
+    ap.add_argument("--txs-per-gpu", type=int, default=0,
+                    help="0 = 10,000 at N=1 (C2) / 20,000 at N>1 (C3: 160k txs at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
     ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
     ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
@@ -232,19 +344,22 @@ def main():
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the TxVoteMessage wire-decode leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host SoA) leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (the measured path); gloo = CPU-side rehearsal of the N>1 "
                          "code path (with --same-gpu, several ranks on one GPU)")
     ap.add_argument("--same-gpu", action="store_true", help="every rank uses device 0 (rehearsal only)")
-    ap.add_argument("--cpu-serial-votes", type=int, default=150_000)
-    ap.add_argument("--cpu-parallel-votes", type=int, default=500_000)
+    ap.add_argument("--cpu-serial-votes", type=int, default=100_000)
+    ap.add_argument("--cpu-parallel-votes", type=int, default=1_000_000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    txs_per_gpu = args.txs_per_gpu or (10_000 if world == 1 else 20_000)
     dist = None
     gloo = args.dist_backend == "gloo"
     if world > 1:
@@ -256,12 +371,13 @@ def main():
     import txflow_amd as T
     from txflow_amd.workload import Workload, SEEDS
 
-    n_txs_global = args.txs_per_gpu * world
+    n_txs_global = txs_per_gpu * world
     t_setup = time.perf_counter()
-    max_txs = n_txs_global if world > 1 else args.txs_per_gpu
-    ctx = T.Context(device=local, max_batch=2 * args.txs_per_gpu * args.validators, max_txs=max_txs + 64,
-                    max_validators=max(args.validators, 1), table_w=args.table_w or None,
-                    lane_votes=args.lane_votes, base_w=args.base_w)
+    exp_votes = txs_per_gpu * args.validators
+    max_batch = exp_votes if world == 1 else int(exp_votes * 1.25) + 4096   # shards are ~equal
+    max_txs = (txs_per_gpu if world == 1 else int(txs_per_gpu * 1.25) + 64) + 64
+    ctx = T.Context(device=local, max_batch=max_batch, max_txs=max_txs, max_validators=max(args.validators, 1),
+                    table_w=args.table_w or None, lane_votes=args.lane_votes, base_w=args.base_w)
     numa = ctx.bind_host_numa()     # host threads + pinned buffers next to this GPU's PCIe root
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
@@ -269,22 +385,19 @@ def main():
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
         f"staged in {time.perf_counter() - t_setup:.1f}s")
 
-    # per-shard commit state all-gathered every step: the commit bitmap of the shard's
-    # set ids and their stake sums, packed in one buffer -> one RCCL all-gather over xGMI
-    bm_ptr, bm_bytes = ctx.commit_bitmap()
-    gathered = None
+    # per-shard commit state all-gathered every step: [n_sets][bitmap][sums] packed by
+    # txv_pack_commit_state into one device buffer -> one RCCL all-gather over xGMI
+    state = gathered = None
+    n_cap = max_txs
     if dist is not None:
         import torch
-        cap = 2 * args.txs_per_gpu                    # local set ids (shards are ~txs_per_gpu each)
-        bm_words = (cap + 31) // 32
-        state = torch.zeros(bm_words + 2 * cap, dtype=torch.int32, device=f"cuda:{local}")
-        gathered = torch.zeros(world * state.numel(), dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
+        words = T.commit_state_bytes(n_cap) // 4
+        state = torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}")
+        gathered = torch.zeros(world * words, dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
     red_dev = "cpu" if gloo else f"cuda:{local}"
 
-    def all_gather_bitmaps():
-        """per-shard commit bitmap + stake sums -> every rank (RCCL all-gather; gloo: host tensors)"""
-        ctx.copy_commit_bitmap(state.data_ptr(), 4 * bm_words)
-        ctx.copy_set_sums(state.data_ptr() + 4 * bm_words, cap)
+    def all_gather_state():
+        ctx.pack_commit_state(state.data_ptr(), n_cap)
         if gloo:
             torch.cuda.synchronize()
             dist.all_gather(list(gathered.chunk(world)), state.cpu())
@@ -292,54 +405,49 @@ def main():
             dist.all_gather_into_tensor(gathered, state)
             torch.cuda.synchronize()
 
-    step_ms, verify_ms, tally_ms = [], [], []
-
-    phases = {"reset": [], "run": [], "fetch": [], "gather": []}
+    step_ms, route_ms, verify_ms, tally_ms = [], [], [], []
     st_buf = np.zeros(wl.n, np.uint8)          # result buffers reused every step
     ev_buf = np.zeros(wl.n_txs + 1, T.EVENT_DTYPE)
 
     def step(record: bool):
         t0 = time.perf_counter()
-        ctx.reset_tally()
-        t1 = time.perf_counter()
-        ms = ctx.run_staged(0, timed=True)
-        t2 = time.perf_counter()
+        ctx.reset_flow()
+        ms = ctx.run_staged(0, timed=record)
         st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf, evs=ev_buf)
-        t3 = time.perf_counter()
         if dist is not None:
-            all_gather_bitmaps()
-        t4 = time.perf_counter()
+            all_gather_state()
         if record:
-            step_ms.append((t4 - t0) * 1e3)
-            verify_ms.append(ms[0])
-            tally_ms.append(ms[1])
-            for k, a_, b_ in (("reset", t0, t1), ("run", t1, t2), ("fetch", t2, t3), ("gather", t3, t4)):
-                phases[k].append((b_ - a_) * 1e3)
+            step_ms.append((time.perf_counter() - t0) * 1e3)
+            route_ms.append(ms[0]); verify_ms.append(ms[1]); tally_ms.append(ms[2])
         return st, ev
 
     for _ in range(args.warmup):
         st, ev = step(False)
-    # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once
+    # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once,
+    # with exactly n_vals - quorum + 1 fired votes per tx
     st, ev = step(False)
     n_added = int(np.count_nonzero((st & 0x7F) == T.ADDED))
     n_fired = int(np.count_nonzero(st & 0x80))
     quorum = ctx.total_power() * 2 // 3 + 1
     exp_fired = wl.n_txs * (args.validators - quorum + 1)
-    if n_added != wl.n or len(ev) != wl.n_txs or n_fired != exp_fired:
+    if n_added != wl.n or len(ev) != wl.n_txs or n_fired != exp_fired or ctx.num_tx_sets() != wl.n_txs:
         log(f"[rank {rank}] CORRECTNESS FAILURE: added {n_added}/{wl.n}, events {len(ev)}/{wl.n_txs}, "
-            f"fired {n_fired}/{exp_fired}")
+            f"fired {n_fired}/{exp_fired}, sets {ctx.num_tx_sets()}/{wl.n_txs}")
         sys.exit(2)
 
     if dist is not None:
-        # the gathered global state: every tx of every shard committed with the full stake
-        g = gathered.cpu().view(world, -1)
-        bits = int(sum(bin(int(w) & 0xFFFFFFFF).count("1") for w in g[:, :bm_words].flatten().tolist()))
-        sums = g[:, bm_words:].contiguous().view(torch.int64)
+        # the gathered global state (unpacked with the C-ABI's own layout): every tx of every shard
+        # committed with the full stake
+        g = gathered.cpu().numpy().view(np.uint8).reshape(world, -1)
+        bits = full = 0
+        for r in range(world):
+            com, sums = T.commit_state_unpack(g[r], n_cap)
+            bits += int(com.sum())
+            full += int((sums == ctx.total_power()).sum())
         nt = torch.tensor([wl.n_txs], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nt)
-        committed_sums = int((sums == ctx.total_power()).sum())
-        if bits != int(nt.item()) or committed_sums != bits:
-            log(f"[rank {rank}] GATHER CHECK FAILURE: {bits} commit bits / {committed_sums} full sums for {int(nt.item())} txs")
+        if bits != int(nt.item()) or full != bits:
+            log(f"[rank {rank}] GATHER CHECK FAILURE: {bits} commit bits / {full} full sums for {int(nt.item())} txs")
             sys.exit(3)
         dist.barrier()
         torch.cuda.synchronize()
@@ -363,35 +471,17 @@ def main():
         total_votes = wl.n
 
     value = total_votes * args.steps / elapsed
-    v_ms = statistics.median(verify_ms)
-    t_ms = statistics.median(tally_ms)
+    r_ms, v_ms, t_ms = statistics.median(route_ms), statistics.median(verify_ms), statistics.median(tally_ms)
     if rank == 0:
-        add_rate, mad_rate = ctx.valu_probe()
-        peak = add_rate / 1e12
-        # roofline.achieved = algorithmic work per launch / verify launch time: SURVEY.md §8d's
-        # W_alg = 2.5e5 int32 lane-ops per verified vote x votes per launch / (K1a+K1b) HIP-event
-        # time.  The executed work (rocprofv3 PMC pass of this kernel build, committed in
-        # profiles/pmc_verify.json: SQ_INSTS_VALU with 64-bit-class ops counted twice, in
-        # full-rate lane-op issue slots) is reported beside it as exec_*; traffic = HBM bytes
-        # per launch from FETCH_SIZE (x2 gfx950 correction) + WRITE_SIZE.
-        w_exec, traffic, pmc_src, pmc_w = None, None, None, None
-        pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as f:
-                    pj = json.load(f)
-                pmc_w = pj.get("table_window")
-                if pmc_w == ctx.table_w:
-                    w_exec = pj.get("verify_w_exec_lane_slots_per_vote")
-                    traffic = pj.get("hbm_bytes_per_launch")
-                    pmc_src = pj.get("source")
-            except Exception:
-                pass
-        achieved = wl.n * W_ALG / (v_ms * 1e-3) / 1e12
-        exec_rate = wl.n * w_exec / (v_ms * 1e-3) / 1e12 if w_exec else None
+        # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
+        # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
+        # (PMC SQ_INSTS_VALU pass of this build, profiles/pmc_verify.json) give exec_frac
+        w_exec, traffic, pmc_src = load_pmc(ctx.table_w, wl.n)
+        achieved = wl.n * W_ALG / (v_ms * 1e-3)
+        exec_rate = wl.n * w_exec / (v_ms * 1e-3) if w_exec else None
+        threads = args.cpu_threads or host_cores()
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(args.cpu_threads, os.cpu_count() or 1)
             cpu = cpu_baseline(wl, threads, args.cpu_serial_votes, args.cpu_parallel_votes)
         out = {
             "metric": "verified+tallied TxVotes/sec",
@@ -407,32 +497,41 @@ def main():
             "dtype": "u32",
             "data": "synthetic: device-signed ed25519 TxVotes (RFC 8032), SURVEY.md §8d seeds",
             "config": {"workload": ("C2: 100 validators x 10k txs = 1M votes on one MI355X" if world == 1 else
-                                    f"C3 layout: {world} x 10k txs sharded by SHA-256(TxHash)[0] mod {world}, "
-                                    f"100 validators, ~1M votes/GPU, RCCL all-gather of commit bitmaps + stake sums"),
-                       "validators": args.validators, "table_window": ctx.table_w, "base_window": ctx.base_w, "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs,
-                       "parallelism": f"shard{world}", "host_numa_bound": numa},
+                                    f"C3 layout: {n_txs_global} txs x {args.validators} validators = "
+                                    f"{n_txs_global * args.validators} votes sharded by SHA-256(TxHash)[0] mod {world} "
+                                    f"(~{exp_votes} per GPU), RCCL all-gather of the packed commit state"),
+                       "validators": args.validators, "table_window": ctx.table_w, "base_window": ctx.base_w,
+                       "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs, "parallelism": f"shard{world}",
+                       "host_numa_bound": numa,
+                       "step": "reset_flow + device TxHash routing/pre-checks/SignBytes + verify + tally + "
+                               "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "")},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
-            "step_phases_ms_p50": {k: round(statistics.median(v), 3) for k, v in phases.items() if v},
-            "verify_kernel_ms": round(v_ms, 3),
-            "tally_kernels_ms": round(t_ms, 3),
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 3),
-                         "unit": "Tlane-op/s (int32 VALU)", "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "kernel": "txv_k_challenge + txv_k_scalarmult (verify pair)",
-                         "alg_lane_ops_per_vote": W_ALG, "alg_source": "SURVEY.md §8d W_alg (Straus, w=8 NAF)",
+            "device_ms_p50": {"route": round(r_ms, 3), "verify": round(v_ms, 3), "tally": round(t_ms, 3)},
+            "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
+                         "unit": "Tlane-op/s (int32 VALU issue)", "frac": round(achieved / VALU_PEAK, 4),
+                         "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_multi (verify pair)",
+                         "alg_lane_ops_per_vote": W_ALG,
+                         "alg_source": "DESIGN.md §4: SHA-512 2 blocks + ScReduce + 181 field multiplies x 100",
                          "exec_lane_slots_per_vote": w_exec,
-                         "exec_achieved": None if exec_rate is None else round(exec_rate, 3),
-                         "exec_frac": None if exec_rate is None else round(exec_rate / peak, 4),
+                         "exec_achieved": None if exec_rate is None else round(exec_rate / 1e12, 3),
+                         "exec_frac": None if exec_rate is None else round(exec_rate / VALU_PEAK, 4),
                          "pmc_source": pmc_src,
-                         "peak_source": "live v_add_u32 issue-rate probe (txv_valu_probe)",
-                         "mad_u64_u32_peak": round(mad_rate / 1e12, 3),
-                         "tally_GBps": round(wl.n * TALLY_BYTES_PER_VOTE / (t_ms * 1e-3) / 1e9, 1)},
+                         "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"},
             "cpu_baseline": cpu,
         }
+        if world == 1 and not args.no_e2e:
+            out["end_to_end"] = {
+                "note": "host SoA columns -> statuses + commit events (staging copy, PCIe upload, kernels, "
+                        "results), txv_submit_votes/txv_wait_votes with two steps in flight",
+                "pageable": end_to_end_leg(ctx, wl, max(3, args.steps), registered=False),
+                "registered": end_to_end_leg(ctx, wl, max(3, args.steps), registered=True)}
         if world == 1 and not args.no_wire:
             out["wire_decode"] = wire_decode_leg(ctx, wl, not args.no_cpu_baseline)
         if world == 1 and not args.no_c5:
             ctx.close()
             out["c5_streaming"] = c5_streaming(local, 1000, args.c5_txs, 65536)
+        if world == 1 and not args.no_c1:
+            out["c1"] = c1_leg(local, threads)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

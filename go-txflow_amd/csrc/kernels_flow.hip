@@ -66,6 +66,74 @@ __device__ __forceinline__ bool key_eq(const uint8_t* a, const uint8_t* b, uint3
   return true;
 }
 
+// A key of at most 64 bytes in registers: 16 little-endian words (zero beyond the length),
+// fetched with <= 5 16-byte loads from p rounded down to 16 (the arenas carry >= 16 bytes of
+// padding) and realigned with v_alignbyte -- instead of 3 dword loads per 8 bytes
+constexpr uint32_t kKeyRegBytes = 64;
+struct KeyRegs {
+  uint32_t w[16];
+};
+__device__ __forceinline__ void load_key(const uint8_t* p, uint32_t n, KeyRegs& k) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint4* q = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  const uint32_t s = (uint32_t)(a & 15u);
+  uint32_t raw[20];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    const uint4 v = (16u * c < s + n) ? q[c] : make_uint4(0, 0, 0, 0);
+    raw[4 * c] = v.x; raw[4 * c + 1] = v.y; raw[4 * c + 2] = v.z; raw[4 * c + 3] = v.w;
+  }
+  const uint32_t sb = s & 3u;
+  // realign by whole words with a static copy per case (a computed index into raw[] would put
+  // it in scratch), then by bytes with v_alignbyte
+  uint32_t t[17];
+  switch (s >> 2) {
+#define TXV_SHIFT_CASE(W) \
+    case W: { _Pragma("unroll") for (int j = 0; j < 17; ++j) t[j] = raw[j + W]; } break;
+    TXV_SHIFT_CASE(0)
+    TXV_SHIFT_CASE(1)
+    TXV_SHIFT_CASE(2)
+    default: { _Pragma("unroll") for (int j = 0; j < 16; ++j) t[j] = raw[j + 3]; t[16] = raw[19]; } break;
+#undef TXV_SHIFT_CASE
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t x = __builtin_amdgcn_alignbyte(t[j + 1], t[j], sb);
+    const int valid = (int)n - 4 * j;
+    if (valid <= 0) x = 0;
+    else if (valid < 4) x &= 0xFFFFFFFFu >> (8 * (4 - valid));
+    k.w[j] = x;
+  }
+}
+__device__ __forceinline__ uint64_t key_chunk(const KeyRegs& k, uint32_t i) {   // i % 8 == 0, i < 64
+  uint64_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((uint32_t)j == i / 8) r = (uint64_t)k.w[2 * j] | ((uint64_t)k.w[2 * j + 1] << 32);
+  return r;
+}
+// txv_hash::hash_chunks over the key in registers (bit-identical: the words beyond n are zero)
+__device__ __forceinline__ uint64_t hash_regs(const KeyRegs& k, uint32_t n, uint64_t seed) {
+  uint64_t h = seed ^ (0x9e3779b97f4a7c15ULL * (uint64_t)(n + 1));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t i = 8u * j;
+    const uint64_t c = (uint64_t)k.w[2 * j] | ((uint64_t)k.w[2 * j + 1] << 32);
+    if (i + 8 <= n) h = txv_hash::mix64(h ^ c) + 0x9e3779b97f4a7c15ULL;
+    else if (i < n) h = txv_hash::mix64(h ^ c ^ ((uint64_t)(n - i) << 56));
+  }
+  return txv_hash::mix64(h) | 1ull;
+}
+
+__device__ __forceinline__ bool key_eq_regs(const KeyRegs& a, const uint8_t* p, uint32_t n) {
+  KeyRegs b;
+  load_key(p, n, b);
+  uint32_t d = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d |= a.w[j] ^ b.w[j];
+  return d == 0;
+}
+
 __device__ __forceinline__ uint32_t uvlen(uint64_t v) {
   uint32_t n = 1;
   while (v >= 0x80u) { v >>= 7; ++n; }
@@ -83,40 +151,72 @@ __device__ __forceinline__ int signbytes_len(int64_t height, uint32_t hl, int64_
   return (int)(uvlen(body) + body);
 }
 
-__device__ __forceinline__ uint32_t ld_state(const SetEntry* e) {
-  return __hip_atomic_load(&e->state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+// agent-coherent (sc1) 64-bit loads / stores of table words: the table is the one structure
+// written and read inside the same launch, by lanes on different XCDs (private L2s)
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t* w64(SetEntry* e, int k) { return reinterpret_cast<uint64_t*>(e) + k; }
+
+// Find-or-insert of one TxHash (linear probing).  A lane that claims an empty slot (CAS on the
+// state word) writes the entry's words through to the coherent level (sc1), waits for them
+// (s_waitcnt vmcnt(0)) and only then publishes the state.  Probing: a plain (cached) copy of
+// the entry is trusted for one conclusion only -- "this is my key" -- and only when it shows a
+// published entry (state set, key pointer set: key_off is stored + 1, so a copy fetched before
+// the entry was written reads 0) whose hash, length and key bytes all equal mine.  Every other
+// conclusion (empty -> claim, different key -> next slot) is drawn from sc1 loads of the coherent
+// copy: a stale or torn cached copy can then cost one extra coherent read, never a duplicate
+// entry.  A lane that meets a slot being written re-reads it in its next iteration: the writer
+// finished inside the iteration in which it claimed the slot, whether it is in the same wave or
+// not, so no lane waits on a lane that waits on it.
+template <bool kRegs>
+__device__ __forceinline__ bool key_matches(const uint8_t* stored, const uint8_t* kp, const KeyRegs& kr, uint32_t len) {
+  if constexpr (kRegs) return key_eq_regs(kr, stored, len);
+  else return key_eq(stored, kp, len);
 }
 
-__device__ __forceinline__ const uint8_t* entry_key(const FlowState& fs, const FlowBatch& b, const SetEntry& e,
-                                                     uint32_t state) {
-  return (state == TXV_SE_BATCH ? b.th : fs.keys) + e.key_off;
-}
-
-// Find-or-insert of one TxHash (linear probing).  A lane that claims an empty slot writes the
-// entry and publishes it with a release store in the same loop iteration; a lane that meets a
-// slot still being written re-reads it in its next iteration (the writer has finished by then,
-// whether it is in the same wave or not), so no lane ever waits on a lane that waits on it.
-__device__ uint32_t set_find_or_insert(const FlowState& fs, const FlowBatch& b, uint64_t h, const uint8_t* kp,
-                                       uint32_t len, uint64_t key_off, uint32_t i) {
+// kRegs: the key is in registers (keys of <= 64 bytes), else compared from memory
+template <bool kRegs>
+__device__ __forceinline__ uint32_t set_find_or_insert(const FlowState& fs, const FlowBatch& b, uint64_t h,
+                                                       const uint8_t* kp, const KeyRegs& kr, uint32_t len,
+                                                       uint64_t key_off, uint32_t i) {
   uint32_t slot = (uint32_t)h & fs.tab_mask;
   uint32_t probes = 0;
   for (;;) {
     SetEntry* e = fs.tab + slot;
-    const uint32_t st = ld_state(e);
-    if (st == TXV_SE_EMPTY) {
-      if (atomicCAS(&e->state, TXV_SE_EMPTY, TXV_SE_BUSY) == TXV_SE_EMPTY) {
-        e->h = h;
-        e->len = len;
-        e->key_off = key_off;
-        e->first = i;
-        e->id = TXV_NONE;
-        __hip_atomic_store(&e->state, TXV_SE_BATCH, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    {
+      // optimistic cached read: accept a match, decide nothing else
+      const uint4 lo = *reinterpret_cast<const uint4*>(e);        // h, (state, len)
+      const uint4 hi = *(reinterpret_cast<const uint4*>(e) + 1);  // key_off + 1, (first, id)
+      const uint32_t st = lo.z;
+      const uint64_t ek = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+      if ((st == TXV_SE_BATCH || st == TXV_SE_KEPT) && ek != 0 && lo.w == len &&
+          ((uint64_t)lo.x | ((uint64_t)lo.y << 32)) == h &&
+          key_matches<kRegs>((st == TXV_SE_BATCH ? b.th : fs.keys) + (ek - 1), kp, kr, len)) {
+        if (st == TXV_SE_BATCH && hi.z > i) atomicMin(&e->first, i);   // a stale first: one extra min
         return slot;
       }
-      // lost the claim: re-read the slot with acquire ordering in the next iteration
+    }
+    const uint64_t sl = ld_sc1(w64(e, 1));                     // (state, len), coherent
+    const uint32_t st = (uint32_t)sl;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     // keep the loads below after it
+    if (st == TXV_SE_EMPTY) {
+      if (atomicCAS(&e->state, TXV_SE_EMPTY, TXV_SE_BUSY) == TXV_SE_EMPTY) {
+        st_sc1(w64(e, 0), h);
+        st_sc1(w64(e, 2), key_off + 1);
+        st_sc1(w64(e, 3), (uint64_t)i | ((uint64_t)TXV_NONE << 32));   // first = i, id = none
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                 // entry words landed
+        st_sc1(w64(e, 1), (uint64_t)TXV_SE_BATCH | ((uint64_t)len << 32));
+        return slot;
+      }
+      // lost the claim: re-read the slot in the next iteration
     } else if (st != TXV_SE_BUSY) {
-      if (e->h == h && e->len == len && key_eq(entry_key(fs, b, *e, st), kp, len)) {
-        if (st == TXV_SE_BATCH) atomicMin(&e->first, i);
+      if ((uint32_t)(sl >> 32) == len && ld_sc1(w64(e, 0)) == h &&
+          key_matches<kRegs>((st == TXV_SE_BATCH ? b.th : fs.keys) + (ld_sc1(w64(e, 2)) - 1), kp, kr, len)) {
+        if (st == TXV_SE_BATCH && (uint32_t)ld_sc1(w64(e, 3)) > i) atomicMin(&e->first, i);
         return slot;
       }
       slot = (slot + 1) & fs.tab_mask;
@@ -175,8 +275,14 @@ __global__ void __launch_bounds__(256) txv_k_route(FlowState fs, FlowBatch b) {
   const uint32_t len = b.th_len[i];
   const uint32_t off = b.th_off[i];
   const uint8_t* kp = b.th + off;
-  const uint64_t h = txv_hash::hash_chunks(len, fs.hash_seed, [&](uint32_t k) { return ld64u(kp + k); });
-  b.entry[i] = set_find_or_insert(fs, b, h, kp, len, off, i);
+  KeyRegs kr;
+  if (len <= kKeyRegBytes) {
+    load_key(kp, len, kr);
+    b.entry[i] = set_find_or_insert<true>(fs, b, hash_regs(kr, len, fs.hash_seed), kp, kr, len, off, i);
+  } else {
+    const uint64_t h = txv_hash::hash_chunks(len, fs.hash_seed, [&](uint32_t k) { return ld64u(kp + k); });
+    b.entry[i] = set_find_or_insert<false>(fs, b, h, kp, kr, len, off, i);
+  }
   // AddVote pre-checks (types/vote_set.go:93-106)
   const uint32_t al = b.addr_len[i];
   uint32_t v = TXV_NONE;
@@ -223,12 +329,14 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t c, uint32_t* total)
   return before + x - c;
 }
 
+// A scan block covers items b*1024 + k*256 + t (round k < 4, thread t): consecutive lanes hold
+// consecutive items, so the predicate's and the action's column accesses coalesce per wave.
 template <class Pred>
 __global__ void __launch_bounds__(256) txv_k_scan_count(Pred p, uint32_t n, uint32_t* blk) {
-  const uint32_t base = blockIdx.x * kScanItems + threadIdx.x * 4;
+  const uint32_t base = blockIdx.x * kScanItems + threadIdx.x;
   uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) c += (base + k < n && p(base + k)) ? 1u : 0u;
+  for (int k = 0; k < 4; ++k) c += (base + 256u * k < n && p(base + 256u * k)) ? 1u : 0u;
   uint32_t total;
   (void)block_excl_scan(c, &total);
   if (threadIdx.x == 0) blk[blockIdx.x] = total;
@@ -271,19 +379,31 @@ __global__ void __launch_bounds__(1024) txv_k_scan_top(uint32_t* blk, uint32_t n
 
 template <class Pred, class Act>
 __global__ void __launch_bounds__(256) txv_k_scan_apply(Pred p, Act act, uint32_t n, const uint32_t* blk) {
-  const uint32_t base = blockIdx.x * kScanItems + threadIdx.x * 4;
+  __shared__ uint32_t cnt[4][4];     // [round][wave] flagged items
+  const uint32_t base = blockIdx.x * kScanItems + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   bool f[4];
-  uint32_t c = 0;
+  uint64_t m[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    f[k] = base + k < n && p(base + k);
-    c += f[k] ? 1u : 0u;
+    f[k] = base + 256u * k < n && p(base + 256u * k);
+    m[k] = __ballot(f[k]);
+    if (lane == 0) cnt[k][w] = (uint32_t)__popcll(m[k]);
   }
-  uint32_t total;
-  uint32_t rank = blk[blockIdx.x] + block_excl_scan(c, &total);
+  __syncthreads();
+  uint32_t rank = blk[blockIdx.x];
+  const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (f[k]) act(base + k, rank++);
+  for (int k = 0; k < 4; ++k) {
+    uint32_t before = 0, round = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      before += q < w ? cnt[k][q] : 0u;
+      round += cnt[k][q];
+    }
+    if (f[k]) act(base + 256u * k, rank + before + (uint32_t)__popcll(m[k] & below));
+    rank += round;
+  }
 }
 
 // ------------------------------------------------------------------ new set ids
@@ -299,7 +419,8 @@ struct NewSetPred {
 };
 
 // the vote that first carried a new TxHash: number its set (first-seen order), move the key
-// bytes into the persistent key arena, record the set's TxKey (service.go:201-207)
+// bytes into the set's key slot (or the overflow arena), record the set's TxKey
+// (service.go:201-207)
 struct NewSetAct {
   FlowState fs;
   FlowBatch b;
@@ -307,22 +428,28 @@ struct NewSetAct {
     const uint32_t slot = b.entry[i];
     SetEntry& e = fs.tab[slot];
     const uint32_t id = fs.ctr->n_sets + rank;
-    const uint32_t len = e.len, span = (len + 7u) & ~7u;
-    const unsigned long long ko = atomicAdd((unsigned long long*)&fs.ctr->key_used, (unsigned long long)span);
-    if (ko + span + 16 > fs.keys_cap) {
-      atomicOr(&fs.ctr->err, TXV_FERR_KEYS);
-    } else {
-      const uint8_t* src = b.th + e.key_off;
-      uint64_t* dst = reinterpret_cast<uint64_t*>(fs.keys + ko);
-      for (uint32_t k = 0; k < span; k += 8) dst[k / 8] = ld64u(src + k) & (k + 8 <= len ? ~0ull : ((1ull << (8 * (len - k))) - 1ull));
-      e.key_off = ko;
-    }
     e.state = TXV_SE_KEPT;
     if (id >= fs.max_txs) {
       atomicOr(&fs.ctr->err, TXV_FERR_SETS);
       e.id = TXV_NONE;
       return;
     }
+    const uint32_t len = e.len, span = (len + 7u) & ~7u;
+    uint64_t ko = (uint64_t)id * TXV_KEY_SLOT;
+    if (len > TXV_KEY_SLOT) {
+      const unsigned long long o = atomicAdd((unsigned long long*)&fs.ctr->key_used, (unsigned long long)span);
+      if (o + span + 16 > fs.keys_cap) {
+        atomicOr(&fs.ctr->err, TXV_FERR_KEYS);
+        e.id = TXV_NONE;
+        return;
+      }
+      ko = (uint64_t)fs.max_txs * TXV_KEY_SLOT + o;
+    }
+    const uint8_t* src = b.th + (e.key_off - 1);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(fs.keys + ko);
+    for (uint32_t k = 0; k < span; k += 8)
+      dst[k / 8] = ld64u(src + k) & (k + 8 <= len ? ~0ull : ((1ull << (8 * (len - k))) - 1ull));
+    e.key_off = ko + 1;
     e.id = id;
     fs.set_entry[id] = slot;
     uint32_t* tk = fs.set_txkey + (size_t)id * 8;
@@ -337,40 +464,42 @@ struct NewSetAct {
   }
 };
 
-// every vote's set id; pending votes clear their (set, validator) cell
-__global__ void __launch_bounds__(256) txv_k_set_ids(FlowState fs, FlowBatch b, uint32_t nb) {
+// ------------------------------------------------------------------ tally
+__device__ __forceinline__ uint64_t cand_key(uint32_t stamp, uint32_t i) {
+  return ((uint64_t)(0xFFFFFFFFu - stamp) << 32) | i;
+}
+// the cell's first verified vote of this batch, or TXV_NONE (stale stamp = an earlier batch's)
+__device__ __forceinline__ uint32_t cand_of(uint64_t c, uint32_t stamp) {
+  return (uint32_t)(c >> 32) == 0xFFFFFFFFu - stamp ? (uint32_t)c : TXV_NONE;
+}
+
+// every vote's set id (after the new-id step); each verified pending vote posts its arrival
+// index to its (set, validator) cell: the cell then holds the FIRST verified vote of the group
+// (cells that already hold an accepted vote skip: their votes are decided without verification)
+__global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b, uint32_t nb) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
     const uint32_t created = b.blk[nb];
     const uint32_t ns = fs.ctr->n_sets + created;
     fs.ctr->n_sets = ns > fs.max_txs ? fs.max_txs : ns;
-    fs.ctr->n_touched = 0;
-    fs.ctr->batch += 1;
   }
   if (i >= b.n) return;
   const uint32_t e = b.entry[i];
   const uint32_t s = e == TXV_NONE ? TXV_NONE : fs.tab[e].id;
   b.set[i] = s;
-  if (s != TXV_NONE && b.pre[i] == TXV_S_PENDING) fs.cand[(size_t)s * fs.n_vals + b.val[i]] = TXV_NONE;
+  if (s == TXV_NONE || b.pre[i] != TXV_S_PENDING || b.ok[i] != 1) return;
+  const size_t cell = (size_t)s * fs.n_vals + b.val[i];
+  if (fs.acc[cell] == 0) atomicMin((unsigned long long*)&fs.cand[cell], (unsigned long long)cand_key(b.stamp, i));
 }
 
-// ------------------------------------------------------------------ tally
 __device__ __forceinline__ bool pending_in_set(const FlowBatch& b, uint32_t i) {
   return b.pre[i] == TXV_S_PENDING && b.set[i] != TXV_NONE;
 }
 
-// the cell's first verified vote of the batch (votes of cells with an accepted vote skip)
-__global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= b.n || !pending_in_set(b, i) || b.ok[i] != 1) return;
-  const size_t cell = (size_t)b.set[i] * fs.n_vals + b.val[i];
-  if (fs.acc[cell] == 0) atomicMin(&fs.cand[cell], i);
-}
-
-__device__ __forceinline__ bool sig_eq_words(const FlowBatch& b, uint32_t i, const uint32_t* q) {
+__device__ __forceinline__ bool sig_eq_arena(const FlowState& fs, const FlowBatch& b, uint32_t i, uint32_t r) {
   uint32_t d = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) d |= b.sig[(size_t)j * b.n_pad + i] ^ q[j];
+  for (int j = 0; j < 16; ++j) d |= b.sig[(size_t)j * b.n_pad + i] ^ fs.arena_sig[(size_t)j * fs.max_accepted + r];
   return d == 0;
 }
 __device__ __forceinline__ bool sig_eq_votes(const FlowBatch& b, uint32_t i, uint32_t f) {
@@ -380,63 +509,76 @@ __device__ __forceinline__ bool sig_eq_votes(const FlowBatch& b, uint32_t i, uin
   return d == 0;
 }
 
+// each pending vote's code from its cell (types/vote_set.go:109-119)
 __global__ void __launch_bounds__(256) txv_k_tally_resolve(FlowState fs, FlowBatch b) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n || !pending_in_set(b, i)) return;
-  const uint32_t s = b.set[i], v = b.val[i];
+  const uint32_t s = b.set[i];
   const uint8_t fl = b.flags[i];
   const bool sig64 = (fl & TXV_FLAG_SIG64) != 0;
-  const size_t cell = (size_t)s * fs.n_vals + v;
+  const size_t cell = (size_t)s * fs.n_vals + b.val[i];
   const uint32_t acc = fs.acc[cell];
   uint8_t st;
   if (acc) {                                   // accepted in an earlier batch (vote_set.go:109-114)
-    st = sig64 && sig_eq_words(b, i, fs.arena[acc - 1].sig) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
+    st = sig64 && sig_eq_arena(fs, b, i, acc - 1) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
   } else {
-    const uint32_t f = fs.cand[cell];
-    if (f == i) {                              // ADDED: the reference stores the vote (vote_set.go:154)
-      st = TXV_S_ADDED;
-      const uint32_t r = atomicAdd(&fs.ctr->arena_used, 1u);
-      if (r < fs.max_accepted) {
-        AccRow* row = fs.arena + r;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) row->sig[j] = b.sig[(size_t)j * b.n_pad + i];
-        row->height = b.height[i];
-        row->ts_sec = b.ts_sec[i];
-        row->ts_nanos = b.ts_nanos[i];
-        row->val = v;
-        row->seq = b.seq_base + i;
-        if (b.txkey) {
-          const uint4* s4 = reinterpret_cast<const uint4*>(b.txkey + (size_t)i * 32);
-          const uint4 a = s4[0], c = s4[1];
-          row->txkey[0] = a.x; row->txkey[1] = a.y; row->txkey[2] = a.z; row->txkey[3] = a.w;
-          row->txkey[4] = c.x; row->txkey[5] = c.y; row->txkey[6] = c.z; row->txkey[7] = c.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) row->txkey[j] = 0;
-        }
-        b.row[i] = r;
-      } else {
-        atomicOr(&fs.ctr->err, TXV_FERR_ARENA);
-        b.row[i] = TXV_NONE;
-      }
-    } else if (f < i) {                        // an earlier vote of the batch was accepted
+    const uint32_t f = cand_of(fs.cand[cell], b.stamp);
+    if (f == i) st = TXV_S_ADDED;              // the reference stores it (vote_set.go:154)
+    else if (f != TXV_NONE && f < i)           // an earlier vote of the batch was accepted
       st = sig64 && sig_eq_votes(b, i, f) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
-    } else {                                   // no accepted vote before it and it did not verify
+    else                                       // no accepted vote before it and it did not verify
       st = (fl & TXV_FLAG_BADMSG) ? TXV_S_SIGNBYTES : TXV_S_INVALID_SIGNATURE;
-    }
   }
   b.status[i] = st;
 }
 
-// list the ADDED votes of each set in its cell row (at most one per validator)
-__global__ void __launch_bounds__(256) txv_k_tally_bucket(FlowState fs, FlowBatch b) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= b.n || !pending_in_set(b, i) || b.status[i] != TXV_S_ADDED) return;
-  const uint32_t s = b.set[i];
-  const uint32_t k = atomicAdd(&fs.set_cnt[s], 1u);
-  fs.cand[(size_t)s * fs.n_vals + k] = i;
-  if (k == 0) fs.touched[atomicAdd(&fs.ctr->n_touched, 1u)] = s;
-}
+// ADDED votes in arrival order -> consecutive arena rows (the accepted vote in full) and the
+// set's stamp (the cross step visits only stamped sets)
+struct AddedPred {
+  FlowBatch b;
+  __device__ bool operator()(uint32_t i) const { return b.pre[i] == TXV_S_PENDING && b.set[i] != TXV_NONE && b.status[i] == TXV_S_ADDED; }
+};
+struct AddedAct {
+  FlowState fs;
+  FlowBatch b;
+  __device__ void operator()(uint32_t i, uint32_t rank) const {
+    const uint32_t r = fs.ctr->arena_used + rank;
+    fs.set_stamp[b.set[i]] = b.stamp;
+    if (r >= fs.max_accepted) {
+      atomicOr(&fs.ctr->err, TXV_FERR_ARENA);
+      b.row[i] = TXV_NONE;
+      return;
+    }
+    b.row[i] = r;
+    const size_t M = fs.max_accepted;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) fs.arena_sig[j * M + r] = b.sig[(size_t)j * b.n_pad + i];
+    fs.arena_height[r] = b.height[i];
+    fs.arena_sec[r] = b.ts_sec[i];
+    fs.arena_nanos[r] = b.ts_nanos[i];
+    fs.arena_val[r] = b.val[i];
+    fs.arena_seq[r] = b.seq_base + i;
+    uint32_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (b.txkey) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(b.txkey + (size_t)i * 32);
+      const uint4 a = s4[0], c = s4[1];
+      tk[0] = a.x; tk[1] = a.y; tk[2] = a.z; tk[3] = a.w; tk[4] = c.x; tk[5] = c.y; tk[6] = c.z; tk[7] = c.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fs.arena_txkey[j * M + r] = tk[j];
+  }
+};
+
+// the sets stamped by this batch's ADDED votes, compacted (scan over the set ids)
+struct TouchedPred {
+  FlowState fs;
+  FlowBatch b;
+  __device__ bool operator()(uint32_t s) const { return s < fs.ctr->n_sets && fs.set_stamp[s] == b.stamp; }
+};
+struct TouchedAct {
+  FlowState fs;
+  __device__ void operator()(uint32_t s, uint32_t rank) const { fs.touched[rank] = s; }
+};
 
 __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 #pragma unroll
@@ -446,66 +588,86 @@ __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 
 constexpr uint32_t kListCap = 512;   // ADDED votes of a set kept in LDS (every set of a <= 512-validator registry)
 
-// one wave per set with ADDED votes (persistent waves over the device-side touched count)
-__global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b) {
+// One wave per set that ADDED votes in this batch (the compacted touched list; persistent
+// waves): its ADDED votes are the cells of its row whose candidate carries this batch's stamp
+// (and held no accepted vote); stake sum, and the arrival index at which the prefix (in arrival
+// order) of the stake first reaches quorum, by binary lifting over the index bits; ADDED votes at
+// or after it fire.
+__global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b, uint32_t nb, uint32_t nb_sets) {
   __shared__ uint32_t l_vote[4][kListCap];
   __shared__ int64_t l_pow[4][kListCap];
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t n_touched = fs.ctr->n_touched;
-  const uint32_t n_waves = gridDim.x * 4;
-  for (uint32_t t = blockIdx.x * 4 + wv; t < n_touched; t += n_waves) {
-    const uint32_t s = fs.touched[t];
-    const uint32_t k = fs.set_cnt[s];
-    const uint32_t* list = fs.cand + (size_t)s * fs.n_vals;
-    const bool in_lds = k <= kListCap;
-    int64_t part = 0;
-    for (uint32_t c = lane; c < k; c += 64) {
-      const uint32_t ie = list[c];
-      const int64_t pw = fs.power[b.val[ie]];
-      part += pw;
-      if (in_lds) { l_vote[wv][c] = ie; l_pow[wv][c] = pw; }
-    }
-    __threadfence_block();
-    const int64_t prior = fs.set_sum[s];
-    const int64_t total = prior + wave_sum64(part);
-    uint32_t cross = TXV_NO_CROSS;
-    if (prior >= fs.quorum) {
-      cross = 0;                                // already committed: every ADDED vote re-fires
-    } else if (total >= fs.quorum) {
-      // crossing = the arrival index T at which the stake prefix (in arrival order) first reaches
-      // quorum: with g(t) = stake of listed votes with arrival < t (monotone), T is the largest t
-      // with prior + g(t) < quorum, found bit by bit; each probe is one list pass + a wave sum
-      const int64_t need = fs.quorum - prior;
-      uint32_t T = 0;
-      for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
-        const uint32_t cand = T | (1u << bit);
-        int64_t sm = 0;
-        if (in_lds) {
-          for (uint32_t c = lane; c < k; c += 64)
-            if (l_vote[wv][c] < cand) sm += l_pow[wv][c];
-        } else {
-          for (uint32_t c = lane; c < k; c += 64) {
-            const uint32_t ie = list[c];
-            if (ie < cand) sm += fs.power[b.val[ie]];
-          }
+  const uint32_t n_touched = fs.touched_blk[nb_sets];
+  const uint32_t gw = blockIdx.x * 4 + wv, n_waves = gridDim.x * 4;
+  if (gw == 0 && lane == 0) {
+    const uint32_t au = fs.ctr->arena_used + b.blk[nb];
+    fs.ctr->arena_used = au > fs.max_accepted ? fs.max_accepted : au;
+  }
+  for (uint32_t t = gw; t < n_touched; t += n_waves) {
+    {
+      const uint32_t s = fs.touched[t];
+      const uint64_t* row = fs.cand + (size_t)s * fs.n_vals;
+      // list this set's ADDED votes (compacted in validator order)
+      uint32_t k = 0;
+      int64_t part = 0;
+      for (uint32_t v0 = 0; v0 < fs.n_vals; v0 += 64) {
+        const uint32_t v = v0 + lane;
+        const uint32_t f = v < fs.n_vals ? cand_of(row[v], b.stamp) : TXV_NONE;
+        const bool added = f != TXV_NONE && fs.acc[(size_t)s * fs.n_vals + v] == 0;
+        const uint64_t m = __ballot(added);
+        if (added) {
+          const uint32_t e = k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          const int64_t pw = fs.power[v];
+          if (e < kListCap) { l_vote[wv][e] = f; l_pow[wv][e] = pw; }
+          part += pw;
         }
-        if (wave_sum64(sm) < need) T = cand;
+        k += (uint32_t)__popcll(m);
       }
-      cross = T;
-    }
-    for (uint32_t c = lane; c < k; c += 64) {
-      const uint32_t ie = in_lds ? l_vote[wv][c] : list[c];
-      const bool fire = cross != TXV_NO_CROSS && ie >= cross;
-      b.status[ie] = (uint8_t)(TXV_S_ADDED | (fire ? TXV_S_FIRED : 0u));
-      const uint32_t r = b.row[ie];
-      fs.acc[(size_t)s * fs.n_vals + b.val[ie]] = r == TXV_NONE ? 0u : r + 1u;
-    }
-    if (lane == 0) {
-      fs.set_sum[s] = total;
-      fs.set_cnt[s] = 0;
-      if (total >= fs.quorum) atomicOr(&fs.bitmap[s >> 5], 1u << (s & 31));
-      if (prior < fs.quorum && total >= fs.quorum) b.ev_flag[cross] = 1;   // the commit event
+      __threadfence_block();
+      const bool in_lds = k <= kListCap;
+      const int64_t prior = fs.set_sum[s];
+      const int64_t total = prior + wave_sum64(part);
+      uint32_t cross = TXV_NO_CROSS;
+      if (prior >= fs.quorum) {
+        cross = 0;                              // already committed: every ADDED vote re-fires
+      } else if (total >= fs.quorum) {
+        // crossing = the arrival index T at which the stake prefix (in arrival order) first
+        // reaches quorum: with g(t) = stake of listed votes with arrival < t (monotone), T is
+        // the largest t with prior + g(t) < quorum, found bit by bit; each probe is one list
+        // pass + a wave sum
+        const int64_t need = fs.quorum - prior;
+        uint32_t T = 0;
+        for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
+          const uint32_t cand = T | (1u << bit);
+          int64_t sm = 0;
+          if (in_lds) {
+            for (uint32_t c = lane; c < k; c += 64)
+              if (l_vote[wv][c] < cand) sm += l_pow[wv][c];
+          } else {
+            for (uint32_t v = lane; v < fs.n_vals; v += 64) {
+              const uint32_t f = cand_of(row[v], b.stamp);
+              if (f != TXV_NONE && f < cand && fs.acc[(size_t)s * fs.n_vals + v] == 0) sm += fs.power[v];
+            }
+          }
+          if (wave_sum64(sm) < need) T = cand;
+        }
+        cross = T;
+      }
+      // ADDED statuses with the fired bit, and the accepted-vote cells
+      for (uint32_t v = lane; v < fs.n_vals; v += 64) {
+        const size_t cell = (size_t)s * fs.n_vals + v;
+        const uint32_t f = cand_of(row[v], b.stamp);
+        if (f == TXV_NONE || fs.acc[cell] != 0) continue;
+        const bool fire = cross != TXV_NO_CROSS && f >= cross;
+        b.status[f] = (uint8_t)(TXV_S_ADDED | (fire ? TXV_S_FIRED : 0u));
+        const uint32_t r = b.row[f];
+        fs.acc[cell] = r == TXV_NONE ? 0u : r + 1u;
+      }
+      if (lane == 0) {
+        fs.set_sum[s] = total;
+        if (prior < fs.quorum && total >= fs.quorum) b.ev_flag[cross] = 1;   // the commit event
+      }
     }
   }
 }
@@ -553,13 +715,11 @@ __global__ void __launch_bounds__(256) txv_k_reset_sets(FlowState fs, int keep_i
   for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += stride) fs.acc[c] = 0;
   for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < ns; s += stride) {
     fs.set_sum[s] = 0;
-    fs.set_cnt[s] = 0;
     if (!keep_ids) {
       SetEntry& e = fs.tab[fs.set_entry[s]];
       e.h = 0; e.len = 0; e.key_off = 0; e.first = 0; e.id = 0; e.state = TXV_SE_EMPTY;
     }
   }
-  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < ((uint64_t)ns + 31) / 32; w += stride) fs.bitmap[w] = 0;
 }
 
 __global__ void txv_k_reset_counters(FlowState fs, int keep_ids) {
@@ -571,8 +731,6 @@ __global__ void txv_k_reset_counters(FlowState fs, int keep_ids) {
     fs.ctr->err &= ~TXV_FERR_ARENA;
   }
   fs.ctr->arena_used = 0;
-  fs.ctr->n_touched = 0;
-  fs.ctr->batch = 0;
 }
 
 __global__ void __launch_bounds__(256) txv_k_lookup(FlowState fs, const uint8_t* keys, const uint32_t* off,
@@ -586,7 +744,7 @@ __global__ void __launch_bounds__(256) txv_k_lookup(FlowState fs, const uint8_t*
   for (uint32_t slot = (uint32_t)h & fs.tab_mask, probes = 0; probes <= fs.tab_mask; slot = (slot + 1) & fs.tab_mask, ++probes) {
     const SetEntry& e = fs.tab[slot];
     if (e.state == TXV_SE_EMPTY) break;
-    if (e.state == TXV_SE_KEPT && e.h == h && e.len == l && key_eq(fs.keys + e.key_off, kp, l)) {
+    if (e.state == TXV_SE_KEPT && e.h == h && e.len == l && key_eq(fs.keys + (e.key_off - 1), kp, l)) {
       id = e.id;
       break;
     }
@@ -607,13 +765,18 @@ __global__ void __launch_bounds__(256) txv_k_gather(FlowState fs, const uint32_t
       for (int j = 0; j < 8; ++j) out_txkey[(size_t)q * 8 + j] = ok ? fs.set_txkey[(size_t)id * 8 + j] : 0u;
   }
   if (!out_rows) return;
-  AccRow r;
+  AccRow r{};
+  r.val = TXV_NONE;
   const uint32_t a = ok ? fs.acc[(size_t)id * fs.n_vals + v] : 0u;
   if (a) {
-    r = fs.arena[a - 1];
-  } else {
-    r = AccRow{};
-    r.val = TXV_NONE;
+    const size_t M = fs.max_accepted, k = a - 1;
+    for (int j = 0; j < 16; ++j) r.sig[j] = fs.arena_sig[j * M + k];
+    for (int j = 0; j < 8; ++j) r.txkey[j] = fs.arena_txkey[j * M + k];
+    r.height = fs.arena_height[k];
+    r.ts_sec = fs.arena_sec[k];
+    r.ts_nanos = fs.arena_nanos[k];
+    r.val = fs.arena_val[k];
+    r.seq = fs.arena_seq[k];
   }
   out_rows[t] = r;
 }
@@ -625,20 +788,35 @@ __global__ void __launch_bounds__(256) txv_k_keys(FlowState fs, const uint32_t* 
   const uint32_t id = ids[q];
   if (id == TXV_NONE || id >= fs.max_txs) { out_off[q] = 0; out_len[q] = 0; return; }
   const SetEntry& e = fs.tab[fs.set_entry[id]];
-  out_off[q] = e.key_off;
+  out_off[q] = e.key_off - 1;
   out_len[q] = e.len;
+}
+
+// bit s of word t: TxVoteSet s has +2/3 (maj23 is sticky and the sum only grows)
+__device__ __forceinline__ uint32_t commit_word(const FlowState& fs, uint32_t t, uint32_t ns) {
+  uint32_t w = 0;
+  for (uint32_t j = 0; j < 32; ++j) {
+    const uint32_t s = t * 32 + j;
+    if (s < ns && fs.set_sum[s] >= fs.quorum) w |= 1u << j;
+  }
+  return w;
 }
 
 __global__ void __launch_bounds__(256) txv_k_pack(FlowState fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   const uint32_t ns = min(fs.ctr->n_sets, n_cap);
   if (t == 0) { dst[0] = ns; dst[1] = 0; }
-  if (t < bm_words) dst[2 + t] = (t * 32 < ns) ? fs.bitmap[t] & (t * 32 + 32 <= ns ? ~0u : ((1u << (ns & 31)) - 1u)) : 0u;
+  if (t < bm_words) dst[2 + t] = commit_word(fs, t, ns);
   if (t < n_cap) {
     const int64_t sm = t < ns ? fs.set_sum[t] : 0;
     dst[2 + bm_words + 2 * t] = (uint32_t)(uint64_t)sm;
     dst[2 + bm_words + 2 * t + 1] = (uint32_t)((uint64_t)sm >> 32);
   }
+}
+
+__global__ void __launch_bounds__(256) txv_k_bitmap(FlowState fs, uint32_t* dst, uint32_t bm_words) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t < bm_words) dst[t] = commit_word(fs, t, min(fs.ctr->n_sets, fs.max_txs));
 }
 
 template <class Pred, class Act>
@@ -656,28 +834,28 @@ extern "C" {
 
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
   if (((uint64_t)b->n + kScanItems - 1) / kScanItems > 8192) return hipErrorInvalidValue;
-  const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
   if (g) hipLaunchKernelGGL(txv_k_route, dim3(g), dim3(256), 0, st, *fs, *b);
-  hipError_t e = compact(NewSetPred{*fs, *b}, NewSetAct{*fs, *b}, b->n, b->blk, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(txv_k_set_ids, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
-  return hipGetLastError();
+  return compact(NewSetPred{*fs, *b}, NewSetAct{*fs, *b}, b->n, b->blk, st);
 }
 
-hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
+// sets_bound: an upper bound on the set ids in use after this batch (the host's count as of
+// the last waited batch + this batch's votes, at most max_txs): the touched-set scan covers it
+hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st) {
   const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
-  if (g) {
-    hipLaunchKernelGGL(txv_k_tally_min, dim3(g), dim3(256), 0, st, *fs, *b);
-    hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *fs, *b);
-    hipLaunchKernelGGL(txv_k_tally_bucket, dim3(g), dim3(256), 0, st, *fs, *b);
-    // persistent waves: enough to cover every set of a C2-sized batch in one round
-    const uint32_t sets_max = std::min<uint32_t>(b->n, fs->max_txs);
-    const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>((sets_max + 3) / 4, 4096));
-    hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b);
-  }
-  hipError_t e = compact(EventPred{*b}, EventAct{*fs, *b}, b->n, b->blk, st);
+  hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
+  if (g) hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *fs, *b);
+  hipError_t e = compact(AddedPred{*b}, AddedAct{*fs, *b}, b->n, b->blk, st);
+  if (e != hipSuccess) return e;
+  sets_bound = std::min(sets_bound, fs->max_txs);
+  const uint32_t nb_sets = (sets_bound + kScanItems - 1) / kScanItems;
+  e = compact(TouchedPred{*fs, *b}, TouchedAct{*fs}, sets_bound, fs->touched_blk, st);
+  if (e != hipSuccess) return e;
+  // persistent waves over the touched list: one wave per set (up to 8 waves per SIMD)
+  const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::min(sets_bound, b->n) + 3) / 4, 2048));
+  hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, nb, nb_sets);
+  e = compact(EventPred{*b}, EventAct{*fs, *b}, b->n, b->blk, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(txv_k_status_out, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
   return hipGetLastError();
@@ -715,6 +893,12 @@ hipError_t txv_flow_keys(const FlowState* fs, const uint32_t* ids, uint32_t n, u
 hipError_t txv_flow_pack(const FlowState* fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap, hipStream_t st) {
   const uint32_t t = std::max<uint32_t>(std::max(bm_words, n_cap), 1);
   hipLaunchKernelGGL(txv_k_pack, dim3((t + 255) / 256), dim3(256), 0, st, *fs, dst, bm_words, n_cap);
+  return hipGetLastError();
+}
+
+hipError_t txv_flow_bitmap(const FlowState* fs, uint32_t* dst, uint32_t bm_words, hipStream_t st) {
+  if (!bm_words) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_bitmap, dim3((bm_words + 255) / 256), dim3(256), 0, st, *fs, dst, bm_words);
   return hipGetLastError();
 }
 

@@ -11,39 +11,69 @@
 //       [0x22 uvarint(len) [0x08 uvarint(sec)] [0x10 uvarint(nanos)]]   (omitted at the Unix epoch)
 //       [0x2a uvarint(len) ChainID]                       (omitted when empty)
 //
-// The host keeps only what is order- or error-dependent: the length (which also decides the
-// amino time-range error, TXV_FLAG_BADMSG) is computed in its parallel phase A; the bytes are
-// produced here, one lane per vote, from the raw fields and the caller's TxHash arena, as
-// big-endian 64-bit words msg[w][n_pad] (zero beyond the length, so K1a needs no masking).
-// H2D per vote drops from ~148 B of message words to 28 B of fields (+ the shared TxHash arena).
+// The length (which also decides the amino time-range error, TXV_FLAG_BADMSG) comes from the
+// route kernel (kernels_flow.hip) or the signer's host pass; the bytes are produced here, one
+// lane per vote, from the raw fields and the TxHash arena, as big-endian 64-bit words
+// msg[w][n_pad] (zero beyond the length, so K1a needs no masking), 8 bytes per append step.
 #include "txv_device.h"
 
 namespace {
 
-// streaming big-endian word writer over one lane's column
+// little-endian 8 bytes at any byte address (reads up to 12 bytes from p rounded down to 4;
+// the TxHash arena and the chain id carry >= 16 bytes of padding)
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t s = (uint32_t)(a & 3u);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+  return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32) | __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+
+// Streaming big-endian word writer over one lane's column, appending up to 8 bytes per step:
+// acc holds the `fill` (< 8) pending bytes right-aligned, a full word goes out as soon as it
+// completes.  Byte strings are appended 8 bytes at a time (one unaligned load + bswap).
 struct WordSink {
   uint64_t* col;      // &msg[0][i]
   uint32_t stride;    // n_pad
   uint64_t acc = 0;
-  uint32_t fill = 0;  // bytes in acc
-  uint32_t word = 0;  // next word index
-  __device__ void put(uint32_t b) {
-    acc = (acc << 8) | (b & 0xFFu);
-    if (++fill == 8) {
-      col[(size_t)word * stride] = acc;
-      ++word; acc = 0; fill = 0;
+  uint32_t fill = 0;
+  uint32_t word = 0;
+  __device__ __forceinline__ void emit(uint64_t w) {
+    col[(size_t)word * stride] = w;
+    ++word;
+  }
+  // k (1..8) bytes, right-aligned big-endian in be (the first byte most significant)
+  __device__ __forceinline__ void put(uint64_t be, uint32_t k) {
+    const uint32_t total = fill + k;
+    if (total < 8) {
+      acc = (acc << (8 * k)) | be;
+      fill = total;
+      return;
+    }
+    const uint32_t rest = total - 8;
+    emit((fill ? acc << (8 * (8 - fill)) : 0ull) | (be >> (8 * rest)));
+    acc = rest ? be & ((1ull << (8 * rest)) - 1ull) : 0ull;
+    fill = rest;
+  }
+  __device__ __forceinline__ void uvarint(uint64_t v) {
+    uint64_t be = 0;
+    uint32_t k = 0;
+    while (v >= 0x80u) {
+      be = (be << 8) | ((v & 0x7Fu) | 0x80u);
+      v >>= 7;
+      if (++k == 8) { put(be, 8); be = 0; k = 0; }
+    }
+    put((be << 8) | v, k + 1);
+  }
+  __device__ __forceinline__ void bytes(const uint8_t* p, uint32_t n) {
+    for (uint32_t k = 0; k < n; k += 8) {
+      const uint32_t m = n - k < 8 ? n - k : 8;
+      put(__builtin_bswap64(ld64u(p + k)) >> (8 * (8 - m)), m);
     }
   }
-  __device__ void uvarint(uint64_t v) {
-    while (v >= 0x80u) { put((uint32_t)(v | 0x80u)); v >>= 7; }
-    put((uint32_t)v);
-  }
-  __device__ void finish(uint32_t words) {
-    if (fill) {
-      col[(size_t)word * stride] = acc << (8 * (8 - fill));
-      ++word;
-    }
-    for (; word < words; ++word) col[(size_t)word * stride] = 0;
+  __device__ __forceinline__ void finish(uint32_t words) {
+    if (fill) emit(acc << (8 * (8 - fill)));
+    for (; word < words;) emit(0);
   }
 };
 
@@ -65,7 +95,6 @@ __global__ void __launch_bounds__(256) txv_k_signbytes(SignBytesArgs a) {
     const int64_t sec = a.ts_sec[i];
     const int32_t nanos = a.ts_nanos[i];
     const uint32_t hl = a.txhash_len[i];
-    const uint8_t* th = a.txhash + a.txhash_off[i];
     const uint32_t tl = (sec != 0 ? 1u + uvarint_len((uint64_t)sec) : 0u) +
                         (nanos != 0 ? 1u + uvarint_len((uint64_t)(uint32_t)nanos) : 0u);
     const uint32_t body = (height != 0 ? 9u : 0u) + (hl ? 1u + uvarint_len(hl) + hl : 0u) + 34u +
@@ -73,26 +102,26 @@ __global__ void __launch_bounds__(256) txv_k_signbytes(SignBytesArgs a) {
                           (a.chain_len ? 1u + uvarint_len(a.chain_len) + a.chain_len : 0u);
     w.uvarint(body);
     if (height != 0) {
-      w.put(0x09);
-      for (int b = 0; b < 8; ++b) w.put((uint32_t)((uint64_t)height >> (8 * b)));
+      w.put(0x09, 1);
+      w.put(__builtin_bswap64((uint64_t)height), 8);
     }
     if (hl) {
-      w.put(0x12);
+      w.put(0x12, 1);
       w.uvarint(hl);
-      for (uint32_t b = 0; b < hl; ++b) w.put(th[b]);
+      w.bytes(a.txhash + a.txhash_off[i], hl);
     }
-    w.put(0x1a); w.put(0x20);
-    for (int b = 0; b < 32; ++b) w.put(0);
+    w.put(0x1a20, 2);                        // TxKey: never copied by CanonicalizeTxVote
+    w.put(0, 8); w.put(0, 8); w.put(0, 8); w.put(0, 8);
     if (tl) {
-      w.put(0x22);
+      w.put(0x22, 1);
       w.uvarint(tl);
-      if (sec != 0) { w.put(0x08); w.uvarint((uint64_t)sec); }
-      if (nanos != 0) { w.put(0x10); w.uvarint((uint64_t)(uint32_t)nanos); }
+      if (sec != 0) { w.put(0x08, 1); w.uvarint((uint64_t)sec); }
+      if (nanos != 0) { w.put(0x10, 1); w.uvarint((uint64_t)(uint32_t)nanos); }
     }
     if (a.chain_len) {
-      w.put(0x2a);
+      w.put(0x2a, 1);
       w.uvarint(a.chain_len);
-      for (uint32_t b = 0; b < a.chain_len; ++b) w.put(a.chain[b]);
+      w.bytes(a.chain, a.chain_len);
     }
   }
   w.finish(a.msg_words);

@@ -76,6 +76,8 @@ struct Slot {
   bool has_nil = false, has_txkey = false;
   bool msg_on_device = false;      // the signer's SignBytes are built by txv_k_signbytes
   uint64_t seq_base = 0;
+  uint32_t stamp = 0;              // batch stamp of the staged batch
+  bool counted = false;            // s.n is in txv_ctx::unfetched
   // AddVote derived columns and scan scratch
   uint32_t *d_entry = nullptr, *d_row = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
@@ -137,16 +139,22 @@ struct txv_ctx {
   // accepted-vote arena, counters
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
   uint8_t* d_keys = nullptr; uint64_t keys_cap = 0;
-  uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_cnt = nullptr, *d_bitmap = nullptr;
+  uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_stamp = nullptr, *d_bitmap = nullptr;
   int64_t* d_set_sum = nullptr;
-  uint32_t *d_acc = nullptr, *d_cand = nullptr, *d_touched = nullptr;
-  AccRow* d_arena = nullptr;
+  uint32_t* d_acc = nullptr;
+  uint64_t* d_cand = nullptr;
+  uint32_t *d_touched = nullptr, *d_touched_blk = nullptr;
+  uint32_t *d_arena_sig = nullptr, *d_arena_nanos = nullptr, *d_arena_val = nullptr, *d_arena_txkey = nullptr;
+  int64_t *d_arena_height = nullptr, *d_arena_sec = nullptr;
+  uint64_t* d_arena_seq = nullptr;
+  uint32_t stamp = 0;               // last batch stamp handed out (never reused by the context)
   FlowCounters* d_ctr = nullptr;
   uint32_t* d_addr_slots = nullptr; uint32_t addr_mask = 0;
   uint32_t max_accepted = 0;        // accepted-vote rows (AccRow) of the arena
   uint64_t hash_seed = 0;           // TxHash hash seed (random per context)
   uint64_t seq_next = 0;            // sequence number of the next submitted vote
   uint32_t n_sets_host = 0;         // TxVoteSets as of the last waited batch
+  uint64_t unfetched = 0;           // votes of batches run but not fetched yet (each may add sets)
   uint32_t poisoned = 0;            // TXV_FERR_* seen: every AddVote call fails until txv_reset_flow
   // caller memory registered with txv_host_register (DMA'd without a staging copy)
   std::vector<std::pair<uintptr_t, uint64_t>> registered;
@@ -291,8 +299,12 @@ FlowState flow_state(const txv_ctx* c) {
   FlowState f{};
   f.tab = c->d_tab; f.tab_mask = c->tab_mask; f.max_txs = c->cfg.max_txs;
   f.keys = c->d_keys; f.keys_cap = c->keys_cap;
-  f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_cnt = c->d_set_cnt;
-  f.bitmap = c->d_bitmap; f.acc = c->d_acc; f.cand = c->d_cand; f.arena = c->d_arena; f.touched = c->d_touched;
+  f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_stamp = c->d_set_stamp;
+  f.acc = c->d_acc; f.cand = c->d_cand;
+  f.arena_sig = c->d_arena_sig; f.arena_height = c->d_arena_height; f.arena_sec = c->d_arena_sec;
+  f.arena_nanos = reinterpret_cast<int32_t*>(c->d_arena_nanos); f.arena_val = c->d_arena_val;
+  f.arena_seq = c->d_arena_seq; f.arena_txkey = c->d_arena_txkey;
+  f.touched = c->d_touched; f.touched_blk = c->d_touched_blk;
   f.ctr = c->d_ctr; f.n_vals = c->n_vals; f.max_accepted = c->max_accepted; f.quorum = c->quorum;
   f.power = c->d_power; f.val_addr = c->d_addr; f.addr_slots = c->d_addr_slots; f.addr_mask = c->addr_mask;
   f.hash_seed = c->hash_seed;
@@ -309,20 +321,27 @@ int alloc_tally(txv_ctx* c) {
   uint64_t tab = 1024;
   while (tab < 2 * ((uint64_t)c->cfg.max_txs + c->cfg.max_batch)) tab *= 2;
   c->tab_mask = (uint32_t)(tab - 1);
-  c->keys_cap = c->cfg.key_arena_bytes ? c->cfg.key_arena_bytes : (uint64_t)c->cfg.max_txs * 96 + (1u << 20);
+  // key store: a 64-byte slot per set id, then the overflow arena for longer TxHashes
+  c->keys_cap = c->cfg.key_arena_bytes ? c->cfg.key_arena_bytes : std::max<uint64_t>((uint64_t)c->cfg.max_txs * 16, 1u << 20);
   int r;
+  const size_t M = c->max_accepted;
   if ((r = dalloc(c, &c->d_acc, cells)) || (r = dalloc(c, &c->d_cand, cells)) ||
-      (r = dalloc(c, &c->d_arena, c->max_accepted)) || (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
-      (r = dalloc(c, &c->d_set_cnt, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_arena_sig, 16 * M)) || (r = dalloc(c, &c->d_arena_height, M)) ||
+      (r = dalloc(c, &c->d_arena_sec, M)) || (r = dalloc(c, &c->d_arena_nanos, M)) || (r = dalloc(c, &c->d_arena_val, M)) ||
+      (r = dalloc(c, &c->d_arena_seq, M)) || (r = dalloc(c, &c->d_arena_txkey, 8 * M)) ||
+      (r = dalloc(c, &c->d_touched, c->cfg.max_txs)) || (r = dalloc(c, &c->d_touched_blk, (c->cfg.max_txs + 1023) / 1024 + 1)) ||
+      (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_stamp, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_set_txkey, (size_t)c->cfg.max_txs * 8)) ||
-      (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_touched, c->cfg.max_batch)) ||
-      (r = dalloc(c, &c->d_tab, tab)) || (r = dalloc(c, &c->d_keys, c->keys_cap)) || (r = dalloc(c, &c->d_ctr, 1)))
+      (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_tab, tab)) ||
+      (r = dalloc(c, &c->d_keys, (uint64_t)c->cfg.max_txs * TXV_KEY_SLOT + c->keys_cap)) || (r = dalloc(c, &c->d_ctr, 1)))
     return r;
   HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_cand, 0xFF, cells * 8, c->stream));   // stamp 0: no candidate
   HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_set_cnt, 0, (size_t)c->cfg.max_txs * 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_set_stamp, 0, (size_t)c->cfg.max_txs * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, tab * sizeof(SetEntry), c->stream));
+  c->stamp = 0;
   HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
   c->seq_next = 0;
   c->n_sets_host = 0;
@@ -337,8 +356,6 @@ int reset_tally(txv_ctx* c, bool keep_ids = false) {
     const uint64_t cells = (uint64_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
     HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->d_set_cnt, 0, (size_t)c->cfg.max_txs * 4, c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->d_bitmap, 0, (size_t)(c->cfg.max_txs + 31) / 32 * 4, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, ((size_t)c->tab_mask + 1) * sizeof(SetEntry), c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
     c->poisoned = 0;
@@ -487,9 +504,9 @@ int ensure_park(txv_ctx* c) {
 int encode_signbytes_device(txv_ctx* c, Slot& s, const txv_votes* v, const uint8_t* d_chain, uint32_t chain_len,
                             uint64_t arena_end) {
   const uint32_t n = s.n, np = s.n_pad;
-  if (arena_end + 1 > s.arena_cap) {
+  if (arena_end + 16 > s.arena_cap) {   // + 16 zero bytes: txv_k_signbytes reads 8 bytes at a time
     int r;
-    const size_t cap = std::max<size_t>((size_t)arena_end + 1, s.arena_cap * 2);
+    const size_t cap = std::max<size_t>((size_t)arena_end + 16, s.arena_cap * 2);
     if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
     s.arena_cap = cap;
   }
@@ -501,12 +518,13 @@ int encode_signbytes_device(txv_ctx* c, Slot& s, const txv_votes* v, const uint8
     memcpy(s.h_fl + lo, v->txhash_len + lo, (size_t)(hi - lo) * 4);
   }, 16384);
   if (arena_end) memcpy(s.h_arena, v->txhash, (size_t)arena_end);
+  memset(s.h_arena + arena_end, 0, 16);
   HIP_TRY(c, hipMemcpyAsync(s.d_fh, s.h_fh, (size_t)n * 8, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_fs, s.h_fs, (size_t)n * 8, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_fn, s.h_fn, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_fo, s.h_fo, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_fl, s.h_fl, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_stream));
-  if (arena_end) HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, (size_t)arena_end, hipMemcpyHostToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, (size_t)arena_end + 16, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipMemcpyAsync(s.d_msg_len, s.h_msg_len, (size_t)np * 4, hipMemcpyHostToDevice, c->copy_stream));
   SignBytesArgs a{};
   a.n = n; a.n_pad = np; a.msg_words = s.msg_words; a.chain_len = chain_len;
@@ -519,11 +537,12 @@ int encode_signbytes_device(txv_ctx* c, Slot& s, const txv_votes* v, const uint8
 
 // txv_set_validators / txv_sign_votes chain ids on the device
 int upload_chain(txv_ctx* c, const char* chain, uint32_t len, uint8_t** d, uint32_t* cap) {
-  if (len + 1 > *cap) {
+  if (len + 16 > *cap) {   // 16 bytes of zero padding: the SignBytes kernel reads 8 bytes at a time
     int r;
-    if ((r = dalloc(c, d, (size_t)len + 1))) return r;
-    *cap = len + 1;
+    if ((r = dalloc(c, d, (size_t)len + 16))) return r;
+    *cap = len + 16;
   }
+  HIP_TRY(c, hipMemsetAsync(*d, 0, *cap, c->copy_stream));
   if (len) HIP_TRY(c, hipMemcpyAsync(*d, chain, len, hipMemcpyHostToDevice, c->copy_stream));
   HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
   return TXV_OK;
@@ -655,6 +674,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   FlowBatch b{};
   b.n = s.n; b.n_pad = s.n_pad; b.msg_words = s.msg_words; b.chain_len = (uint32_t)c->chain.size();
   b.seq_base = s.seq_base;
+  b.stamp = s.stamp;
   b.height = s.d_fh; b.ts_sec = s.d_fs; b.ts_nanos = s.d_fn; b.th_off = s.d_fo; b.th_len = s.d_fl; b.th = s.d_arena_th;
   b.addr = s.d_addr; b.addr_len = s.d_addr_len; b.sig_raw = s.d_sigraw; b.sig_len = s.d_sig_len;
   b.nil = s.has_nil ? s.d_nil : nullptr; b.txkey = s.has_txkey ? s.d_txkey : nullptr;
@@ -673,6 +693,12 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
   int r;
   if ((r = ensure_park(c))) return r;
+  if (c->stamp == 0xFFFFFFFEu) {   // stamps are about to wrap: forget every candidate first
+    HIP_TRY(c, hipMemsetAsync(c->d_cand, 0xFF, (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1) * 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_set_stamp, 0, (size_t)c->cfg.max_txs * 4, c->stream));
+    c->stamp = 0;
+  }
+  s.stamp = ++c->stamp;            // every run of a batch gets a stamp of its own
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   const FlowState fs = flow_state(c);
@@ -690,7 +716,11 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
   HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
-  HIP_TRY(c, txv_flow_tally(&fs, &fb, c->stream));
+  // set ids in use after this batch: at most those known at the last fetch + one per vote of
+  // every batch run since (a bound for the touched-set scan)
+  if (!s.counted) { c->unfetched += s.n; s.counted = true; }
+  const uint32_t sets_bound = (uint32_t)std::min<uint64_t>((uint64_t)c->n_sets_host + c->unfetched, c->cfg.max_txs);
+  HIP_TRY(c, txv_flow_tally(&fs, &fb, sets_bound, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[5], c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
   s.ran = true;
@@ -713,6 +743,7 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
   FlowSummary sm;
   memcpy(&sm, (const void*)s.h_sum, sizeof sm);   // written over PCIe by the last kernel
   c->n_sets_host = sm.n_sets;
+  if (s.counted) { c->unfetched -= s.n; s.counted = false; }
   if (sm.err) {
     c->poisoned |= sm.err;
     c->err = std::string("TxFlow capacity exceeded:") + ((sm.err & TXV_FERR_SETS) ? " max_txs" : "") +
@@ -983,8 +1014,10 @@ void txv_destroy(txv_ctx* c) {
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
-  dfree(c->d_acc); dfree(c->d_cand); dfree(c->d_arena); dfree(c->d_set_sum); dfree(c->d_set_cnt); dfree(c->d_bitmap);
-  dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_touched); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
+  dfree(c->d_acc); dfree(c->d_cand); dfree(c->d_set_sum); dfree(c->d_touched); dfree(c->d_touched_blk);
+  dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
+  dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_bitmap);
+  dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
   dfree(c->d_addr_slots); dfree(c->d_q);
   for (const auto& rg : c->registered) (void)hipHostUnregister((void*)rg.first);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
@@ -1534,6 +1567,12 @@ int txv_fetch_staged(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_
 
 int txv_commit_bitmap(txv_ctx* c, void** dev_ptr, uint64_t* bytes) {
   if (!c || !dev_ptr || !bytes) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->d_ctr) { c->err = "no validator set"; return TXV_ESTATE; }
+  const FlowState fs = flow_state(c);   // derived from the stake sums after every submitted batch
+  HIP_TRY(c, txv_flow_bitmap(&fs, c->d_bitmap, (c->cfg.max_txs + 31) / 32, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   *dev_ptr = c->d_bitmap;
   *bytes = (uint64_t)(c->cfg.max_txs + 31) / 32 * 4;
   return TXV_OK;
@@ -1750,8 +1789,10 @@ int txv_copy_commit_bitmap(txv_ctx* c, void* dst_dev, uint64_t bytes) {
   if (!c || !dst_dev) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->d_ctr) { c->err = "no validator set"; return TXV_ESTATE; }
   const uint64_t have = (uint64_t)(c->cfg.max_txs + 31) / 32 * 4;
-  HIP_TRY(c, hipMemcpyAsync(dst_dev, c->d_bitmap, std::min(bytes, have), hipMemcpyDeviceToDevice, c->stream));
+  const FlowState fs = flow_state(c);
+  HIP_TRY(c, txv_flow_bitmap(&fs, static_cast<uint32_t*>(dst_dev), (uint32_t)(std::min(bytes, have) / 4), c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return TXV_OK;
 }

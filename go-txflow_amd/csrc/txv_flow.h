@@ -6,19 +6,28 @@
 //   set table   SetEntry[tab_mask + 1]   TxHash -> dense TxVoteSet id, open addressing.  Ids are
 //               handed out in first-seen arrival order, exactly as the sequential
 //               `TxVoteSets[vote.TxHash]` creation would number them (service.go:200-209).
-//   key arena   u8[keys_cap]             TxHash bytes of every set (the table's keys)
+//   key slots   u8[max_txs][64]          TxHash bytes of set id s at s * 64 (TxHashes of up to 64
+//               + overflow arena          bytes: every SHA-256 upper-hex TxHash); longer ones in
+//                                         the overflow arena (key_arena_bytes)
 //   per set id  set_entry (table slot), set_txkey [8] u32 (TxKey of the first vote,
-//               service.go:201-207), set_sum i64, set_cnt (ADDED votes of the running batch),
-//               commit bitmap (1 bit per set)
+//               service.go:201-207), set_sum i64, set_stamp (last batch that ADDED a vote)
 //   cells       acc [max_txs * n_vals] u32   0 or the accepted vote's arena row + 1 (the
 //                                            reference's `votes` map, vote_set.go:154)
-//               cand[max_txs * n_vals] u32   per batch: smallest arrival index of a verified
-//                                            vote of the (set, validator) cell; after the
-//                                            resolve step the row of set s holds the arrival
-//                                            indices of s's ADDED votes of the batch
-//   arena       AccRow[max_accepted]     every accepted vote in full (signature, height, time,
-//                                        TxKey, validator, sequence number): one row per ADDED
-//                                        vote, so a row is only spent on what the map stores
+//               cand[max_txs * n_vals] u64   (~stamp << 32 | arrival index) of the first
+//                                            verified vote of the (set, validator) cell in the
+//                                            batch with that stamp: one atomic min per verified
+//                                            vote, and a stale stamp reads as "none", so the
+//                                            cells are never cleared
+//   arena       [max_accepted] rows, column-major (sig [16][rows] u32, height, ts_sec, ts_nanos,
+//               val, seq, TxKey [8][rows]): every accepted vote in full, one row per ADDED vote,
+//               rows handed out by a compaction in arrival order (consecutive rows per wave, so
+//               each column store is one coalesced line per wave)
+// The commit bitmap is derived from set_sum on demand (txv_commit_bitmap, the packed state).
+//
+// gfx950 has 8 XCDs with private L2s: the only hand-off INSIDE a launch is the set-table insert
+// of the route kernel, done with write-through (sc1) stores, s_waitcnt vmcnt(0) and a relaxed
+// flag store by the creating lane, and sc1 loads by the probing lanes (cdna_hip_programming.md,
+// publish/consume recipe).  Every other producer -> consumer pair is separated by a launch.
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>
@@ -44,7 +53,7 @@
 // context is poisoned until txv_reset_flow: TXV_ECAPACITY)
 #define TXV_FERR_SETS 0x1u      // more TxVoteSets than max_txs
 #define TXV_FERR_TABLE 0x2u     // set table full (probe bound)
-#define TXV_FERR_KEYS 0x4u      // TxHash key arena full
+#define TXV_FERR_KEYS 0x4u      // TxHash overflow key arena full
 #define TXV_FERR_ARENA 0x8u     // accepted-vote arena full (max_accepted)
 
 // table entry states
@@ -53,14 +62,15 @@
 #define TXV_SE_BATCH 2u         // created by the running batch: key bytes in the batch's TxHash arena
 #define TXV_SE_KEPT 3u          // key bytes in the persistent key arena
 
-struct SetEntry {
+struct SetEntry {               // 32 B; (state, len) and (first, id) are loaded as one 64-bit word each
   uint64_t h;                   // seeded 64-bit hash of the TxHash bytes
   uint32_t state;
   uint32_t len;                 // TxHash length
-  uint64_t key_off;             // into the batch arena (BATCH) or the key arena (KEPT)
+  uint64_t key_off;             // 1 + offset into the batch arena (BATCH) or the key store (KEPT); 0 = unset
   uint32_t first;               // BATCH: smallest arrival index of the key in the batch
   uint32_t id;                  // dense set id (assigned after the batch's routing step)
 };
+#define TXV_KEY_SLOT 64u        // key store bytes per set id
 
 // one accepted vote (128 B): what TxVoteSet.votes holds, for MakeCommit / GetVotes
 struct AccRow {
@@ -75,12 +85,10 @@ struct AccRow {
 
 struct FlowCounters {           // device-resident, updated by the kernels
   uint32_t n_sets;              // TxVoteSets so far
-  uint32_t n_touched;           // sets with ADDED votes in the running batch
   uint32_t arena_used;          // accepted-vote rows in use
   uint32_t err;                 // TXV_FERR_*
-  uint64_t key_used;            // key arena bytes in use
-  uint32_t batch;               // batches run since the reset
   uint32_t pad;
+  uint64_t key_used;            // overflow key arena bytes in use
 };
 
 struct FlowSummary {            // written to mapped host memory by the last kernel of a batch
@@ -97,17 +105,23 @@ struct FlowState {
   SetEntry* tab;
   uint32_t tab_mask;
   uint32_t max_txs;
-  uint8_t* keys;
-  uint64_t keys_cap;
+  uint8_t* keys;                // [max_txs][TXV_KEY_SLOT] key slots, then the overflow arena
+  uint64_t keys_cap;            // overflow arena bytes
   uint32_t* set_entry;          // [max_txs]
   uint32_t* set_txkey;          // [max_txs][8]
   int64_t* set_sum;             // [max_txs]
-  uint32_t* set_cnt;            // [max_txs]
-  uint32_t* bitmap;             // [max_txs / 32]
+  uint32_t* set_stamp;          // [max_txs]
   uint32_t* acc;                // [max_txs * n_vals]
-  uint32_t* cand;               // [max_txs * n_vals]
-  AccRow* arena;                // [max_accepted]
-  uint32_t* touched;            // [max_batch] sets with ADDED votes in the running batch
+  uint64_t* cand;               // [max_txs * n_vals]
+  uint32_t* arena_sig;          // [16][max_accepted]
+  int64_t* arena_height;        // [max_accepted]
+  int64_t* arena_sec;
+  int32_t* arena_nanos;
+  uint32_t* arena_val;
+  uint64_t* arena_seq;
+  uint32_t* arena_txkey;        // [8][max_accepted]
+  uint32_t* touched;            // [max_txs] sets that ADDED votes in the running batch
+  uint32_t* touched_blk;        // scan scratch over set ids: [ceil(max_txs / 1024) + 1]
   FlowCounters* ctr;
   uint32_t n_vals, max_accepted;
   int64_t quorum;
@@ -123,6 +137,8 @@ struct FlowState {
 struct FlowBatch {
   uint32_t n, n_pad, msg_words, chain_len;
   uint64_t seq_base;            // sequence number of vote 0
+  uint32_t stamp;               // this batch's stamp (>= 1, never reused by the context)
+  uint32_t pad0;
   const int64_t* height;
   const int64_t* ts_sec;
   const int32_t* ts_nanos;
@@ -159,7 +175,7 @@ extern "C" {
 // kernels sit: route (pre-checks, set ids, signature transpose, SignBytes lengths) ...
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st);
 // ... then, after K1a/K1b wrote b->ok: tally, commit events, statuses to the host
-hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, hipStream_t st);
+hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st);
 // forget every TxVoteSet (keep_ids = 0) or empty them keeping their ids (keep_ids = 1)
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);
 // TxHash lookups for the readers: out_id[i] = set id or TXV_NONE
@@ -174,4 +190,6 @@ hipError_t txv_flow_keys(const FlowState* fs, const uint32_t* ids, uint32_t n, u
                          hipStream_t st);
 // packed commit state of this shard: [n_sets u32][pad u32][bitmap words][sums i64]
 hipError_t txv_flow_pack(const FlowState* fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap, hipStream_t st);
+// commit bitmap (bit s = set_sum[s] >= quorum) of the first bm_words * 32 set ids
+hipError_t txv_flow_bitmap(const FlowState* fs, uint32_t* dst, uint32_t bm_words, hipStream_t st);
 }

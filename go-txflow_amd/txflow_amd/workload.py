@@ -2,6 +2,7 @@
 
     chainID "test_chain_id", Height 1, Timestamp = 1.7e9 s + (i+1) ns (non-zero nanos),
     tx_j = le64(j) || 24 PRNG bytes, TxHash = upper-hex(SHA-256(tx_j))  (types/tx_vote.go:43-45),
+    TxKey = SHA-256(tx_j) (types/tx_vote.go:38-40; every vote of the tx carries it, reactor.go:113-118),
     validator seeds = SHA-512("txflow-val" || le32(i))[:32], keys derived on the GPU (RFC 8032).
 Signatures are produced by the device signer (txv_sign_votes, mirroring MockPV.SignTxVote,
 types/priv_validator.go:83-95).  The PRNG is numpy PCG64 seeded with the config seed.
@@ -33,6 +34,11 @@ def tx_hashes(n_txs: int, rng: np.random.Generator, first: int = 0) -> np.ndarra
     return out
 
 
+def tx_keys(hashes: np.ndarray) -> np.ndarray:
+    """[n_txs, 32] TxKey = SHA-256(tx): the bytes the upper-hex TxHash spells"""
+    return np.frombuffer(bytes.fromhex(hashes.tobytes().decode()), np.uint8).reshape(len(hashes), 32)
+
+
 class Workload:
     """Every validator votes every tx (C1/C2/C3 shape), arrival order shuffled."""
 
@@ -60,12 +66,13 @@ class Workload:
         perm = self.rng.permutation(n)
         self.tx_of, self.val_of = tx_of[perm], val_of[perm]
         self.n = n
+        self.txkeys = tx_keys(self.hashes)
         self.batch = VoteBatch(
             n, height=np.ones(n, np.int64), txhash_arena=self.hashes.reshape(-1),
             txhash_off=self.tx_of.astype(np.uint32) * 64, txhash_len=np.full(n, 64, np.uint32),
             ts_sec=np.full(n, 1_700_000_000, np.int64), ts_nanos=(np.arange(n, dtype=np.int64) % 999_999_999 + 1),
             addr=self.addrs[self.val_of], addr_len=np.full(n, 20, np.uint32),
-            sig=np.zeros((n, 64), np.uint8), sig_len=np.full(n, 64, np.uint32))
+            sig=np.zeros((n, 64), np.uint8), sig_len=np.full(n, 64, np.uint32), txkey=self.txkeys[self.tx_of])
         chunk = 1 << 18
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
@@ -75,6 +82,14 @@ class Workload:
                             addr=self.batch.addr[20 * s:20 * e], addr_len=self.batch.addr_len[s:e],
                             sig=self.batch.sig[64 * s:64 * e], sig_len=self.batch.sig_len[s:e])
             self.batch.sig[64 * s:64 * e] = ctx.sign_votes(sub, self.val_of[s:e], CHAIN_ID).reshape(-1)
+
+    def head(self, m: int) -> VoteBatch:
+        """the first m votes as a VoteBatch (views; the TxHash arena is shared)"""
+        b = self.batch
+        return VoteBatch(m, height=b.height[:m], txhash_arena=b.txhash_arena, txhash_off=b.txhash_off[:m],
+                         txhash_len=b.txhash_len[:m], ts_sec=b.ts_sec[:m], ts_nanos=b.ts_nanos[:m],
+                         addr=b.addr[:20 * m], addr_len=b.addr_len[:m], sig=b.sig[:64 * m], sig_len=b.sig_len[:m],
+                         txkey=None if b.txkey is None else b.txkey[:32 * m])
 
     def vote(self, i: int) -> dict:
         """oracle-style dict of vote i"""
@@ -99,6 +114,7 @@ class StreamWorkload:
         assert ok.all()
         self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(n_vals, 20)
         self.hashes = tx_hashes(n_txs, self.rng, 1 << 40)
+        self.txkeys = tx_keys(self.hashes)
         n = n_txs * n_vals
         tx_of = np.repeat(np.arange(n_txs, dtype=np.int64), n_vals)
         val_of = np.tile(np.arange(n_vals, dtype=np.int64), n_txs)
@@ -115,7 +131,7 @@ class StreamWorkload:
                           ts_sec=np.full(m, 1_700_000_000, np.int64),
                           ts_nanos=(np.arange(s, e, dtype=np.int64) % 999_999_999 + 1),
                           addr=self.addrs[self.val_of[s:e]], addr_len=np.full(m, 20, np.uint32),
-                          sig=sig[s:e], sig_len=np.full(m, 64, np.uint32))
+                          sig=sig[s:e], sig_len=np.full(m, 64, np.uint32), txkey=self.txkeys[self.tx_of[s:e]])
             b.sig = ctx.sign_votes(b, self.val_of[s:e].astype(np.uint32), CHAIN_ID).reshape(-1)
             self.batches.append(b)
         first = np.full(n_txs, -1, np.int64)

@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-prof}
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu-baseline --no-c5"
+B="python3 bench.py --no-cpu-baseline --no-c5 --no-c1 --no-wire --no-e2e"
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps 5 --warmup 1 > $OUT/bench_kt.json 2> $OUT/bench_kt.err || exit 1
