@@ -1618,6 +1618,24 @@ int txv_pack_commit_state(txv_ctx* c, void* dst_dev, uint32_t n_sets_cap) {
   return TXV_OK;
 }
 
+int txv_read_commit_state(txv_ctx* c, void* dst_host, uint32_t n_sets_cap) {
+  if (!c || !dst_host) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->d_ctr) { c->err = "no validator set"; return TXV_ESTATE; }
+  const uint64_t bytes = txv_commit_state_bytes(n_sets_cap);
+  if (bytes > c->q_cap) {
+    int r;
+    if ((r = dalloc(c, &c->d_q, bytes))) return r;
+    c->q_cap = bytes;
+  }
+  const FlowState fs = flow_state(c);
+  HIP_TRY(c, txv_flow_pack(&fs, reinterpret_cast<uint32_t*>(c->d_q), (n_sets_cap + 31) / 32, n_sets_cap, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(dst_host, c->d_q, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
 int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
                                void* dst) {
   if (!dst || n_sets > n_sets_cap || (n_sets && (!committed || !sums))) return TXV_EINVAL;

@@ -154,6 +154,7 @@ def lib():
             "txv_shard_of": ([vp, vp, vp, u32, u32, vp], ctypes.c_int),
             "txv_commit_state_bytes": ([u32], ctypes.c_uint64),
             "txv_pack_commit_state": ([vp, vp, u32], ctypes.c_int),
+            "txv_read_commit_state": ([vp, vp, u32], ctypes.c_int),
             "txv_commit_state_pack_host": ([u32, vp, vp, u32, vp], ctypes.c_int),
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
         }
@@ -176,7 +177,7 @@ EXPORTED_SYMBOLS = [
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
-    "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_commit_state_pack_host",
+    "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack"]
 
 
@@ -574,6 +575,12 @@ class Context:
 
     def pack_commit_state(self, dst_dev_ptr: int, n_sets_cap: int):
         self._chk(lib().txv_pack_commit_state(self._h, ctypes.c_void_p(dst_dev_ptr), n_sets_cap), "pack state")
+
+    def read_commit_state(self, n_sets_cap: int) -> np.ndarray:
+        """the device-packed commit state (txv_read_commit_state) as host bytes"""
+        out = np.zeros(commit_state_bytes(n_sets_cap), np.uint8)
+        self._chk(lib().txv_read_commit_state(self._h, out.ctypes.data, n_sets_cap), "read state")
+        return out
 
     def num_tx_sets(self) -> int:
         return lib().txv_num_tx_sets(self._h)

@@ -55,8 +55,9 @@ class Workload:
         self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(n_vals, 20)
         hashes = tx_hashes(n_txs, self.rng, tx_first)
         if n_shards > 1:
-            # shard = SHA-256(TxHash)[0] mod G
-            keep = np.array([hashlib.sha256(h.tobytes()).digest()[0] % n_shards == shard for h in hashes])
+            # shard = SHA-256(TxHash)[0] mod G (txv_shard_of)
+            from . import shard_of
+            keep = shard_of([h.tobytes() for h in hashes], n_shards) == shard
             hashes = hashes[keep]
         self.hashes = hashes
         self.n_txs = len(hashes)

@@ -274,6 +274,8 @@ int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len
 uint64_t txv_commit_state_bytes(uint32_t n_sets_cap);
 /* this context's state into caller device memory (e.g. an RCCL all-gather buffer) */
 int txv_pack_commit_state(txv_ctx* ctx, void* dst_dev, uint32_t n_sets_cap);
+/* the same packed by the device, copied into caller host memory (host-side gathers) */
+int txv_read_commit_state(txv_ctx* ctx, void* dst_host, uint32_t n_sets_cap);
 /* host-side pack (from per-set committed flags and sums) and unpack of the same layout */
 int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
                                void* dst);

@@ -156,6 +156,11 @@ typedef struct {
 } orc_wire_vote;
 int orc_wire_decode(const uint8_t* bz, size_t len, uint32_t max_msg_bytes, orc_wire_vote* out);
 /* cdc.MarshalBinaryBare(&TxVoteMessage{Tx: vote}); returns length, -1 on an amino time error or cap */
+/* cdc.MarshalBinaryBare(TxVote) (= a CommitSig's bytes, types/tx_vote.go:154-159, used by
+ * MakeCommit types/vote_set.go:242-259); out == 0: length only; -1 on an amino time error */
+int orc_txvote_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
+                      int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
+                      const uint8_t* sig, size_t sig_len, uint8_t* out);
 int orc_wire_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
                     int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
                     const uint8_t* sig, size_t sig_len, uint8_t* out, size_t cap);

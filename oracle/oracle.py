@@ -80,6 +80,8 @@ def lib():
         L.orc_verify_many.restype = ctypes.c_double
         L.orc_verify_many.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.orc_wire_decode.argtypes = [c_u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p]
+        L.orc_txvote_encode.argtypes = [ctypes.c_int64, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_int64, ctypes.c_int32,
+                                         c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t, ctypes.c_char_p]
         L.orc_wire_encode.argtypes = [ctypes.c_int64, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_int64, ctypes.c_int32,
                                       c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.orc_wire_prefix.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
@@ -375,6 +377,49 @@ def wire_encode(height, txhash: bytes, ts_sec, ts_nanos, addr: bytes, sig: bytes
     n = lib().orc_wire_encode(height, txhash, len(txhash), txkey, ts_sec, ts_nanos, addr, len(addr), sig, len(sig),
                               out, cap)
     return None if n < 0 else out.raw[:n]
+
+
+def txvote_bytes(height, txhash: bytes, ts_sec, ts_nanos, addr: bytes, sig: bytes, txkey: bytes = bytes(32)):
+    """cdc.MarshalBinaryBare(TxVote) -- a CommitSig's bytes (types/tx_vote.go:154-159)."""
+    n = lib().orc_txvote_encode(height, txhash, len(txhash), txkey, ts_sec, ts_nanos, addr, len(addr), sig, len(sig),
+                                None)
+    if n < 0:
+        return None
+    out = ctypes.create_string_buffer(max(n, 1))
+    lib().orc_txvote_encode(height, txhash, len(txhash), txkey, ts_sec, ts_nanos, addr, len(addr), sig, len(sig), out)
+    return out.raw[:n]
+
+
+def _uvarint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def commit_bytes(txhash: bytes, votes) -> bytes:
+    """cdc.MustMarshalBinaryBare(Commit{TxHash, Commits}) (types/vote_set.go:242-287, tx/store.go:92):
+    field 1 TxHash (omitted when empty), then field 2 once per CommitSig in the given order, each
+    length-prefixed with the accepted TxVote's bytes.  votes: dicts (height, ts_sec, ts_nanos, addr,
+    sig, txkey)."""
+    out = bytearray()
+    if txhash:
+        out += b"\x0a" + _uvarint(len(txhash)) + txhash
+    for v in votes:
+        body = txvote_bytes(v["height"], txhash, v["ts_sec"], v["ts_nanos"], v["addr"], v["sig"], v["txkey"])
+        out += b"\x12" + _uvarint(len(body)) + body
+    return bytes(out)
+
+
+def save_tx_bytes(txhash: bytes, txkey: bytes, votes):
+    """TxStore.SaveTx's two db.Set calls (tx/store.go:83-107): (calcTxKey = "H:%X", the TxVoteSet's
+    bytes -- only its exported TxHash (field 1) and TxKey (field 2) --, calcTxCommitKey = "C:%X",
+    the MakeCommit bytes)."""
+    hexkey = txhash.hex().upper().encode()
+    vs = (b"\x0a" + _uvarint(len(txhash)) + txhash if txhash else b"") + b"\x12\x20" + txkey
+    return b"H:" + hexkey, vs, b"C:" + hexkey, commit_bytes(txhash, votes)
 
 
 def wire_decode(bz: bytes, max_msg_bytes: int = 1 << 20):

@@ -287,10 +287,12 @@ static size_t put_bytes_field(uint8_t* out, uint8_t key, const uint8_t* b, size_
   return n + len;
 }
 
-int orc_wire_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
-                    int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
-                    const uint8_t* sig, size_t sig_len, uint8_t* out, size_t cap) {
-  /* TxVote body (MarshalBinaryBare field rules as TxVote.Size, types/tx_vote.go:144-150) */
+/* cdc.MarshalBinaryBare(TxVote) -- also a CommitSig's bytes (types/tx_vote.go:154-159) --
+ * field rules as TxVote.Size (types/tx_vote.go:144-150).  out == 0: length only; -1 when amino
+ * rejects the timestamp. */
+int orc_txvote_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
+                      int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
+                      const uint8_t* sig, size_t sig_len, uint8_t* w) {
   if (ts_sec != 0 && (ts_sec < MIN_SEC || ts_sec >= MAX_SEC)) return -1;
   if (ts_nanos < 0 || ts_nanos > 999999999) return -1;
   uint8_t tb[24];
@@ -298,33 +300,35 @@ int orc_wire_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, co
   if (ts_sec != 0) { tb[tl++] = 0x08; tl += put_uvarint(tb + tl, (uint64_t)ts_sec); }
   if (ts_nanos != 0) { tb[tl++] = 0x10; tl += put_uvarint(tb + tl, (uint64_t)ts_nanos); }
   static const uint8_t zero32[32];
-  size_t body = 0;
-  for (int pass = 0; pass < 2; ++pass) {
-    uint8_t* w = 0;
-    if (pass) {
-      uint8_t disamb[3], prefix[4];
-      orc_wire_prefix(disamb, prefix);
-      const size_t total = 4 + 1 + put_uvarint(0, body) + body;
-      if (total > cap) return -1;
-      memcpy(out, prefix, 4);
-      out[4] = 0x0a;
-      w = out + 5 + put_uvarint(out + 5, body);
-    }
-    size_t n = 0;
-    if (height != 0) {
-      if (w) w[n] = 0x08;
-      n += 1 + put_uvarint(w ? w + n + 1 : 0, (uint64_t)height);
-    }
-    n += put_bytes_field(w ? w + n : 0, 0x12, txhash, txhash_len);
-    if (w) { w[n] = 0x1a; w[n + 1] = 0x20; memcpy(w + n + 2, txkey ? txkey : zero32, 32); }
-    n += 34;
-    n += put_bytes_field(w ? w + n : 0, 0x22, tb, tl);
-    n += put_bytes_field(w ? w + n : 0, 0x2a, addr, addr_len);
-    n += put_bytes_field(w ? w + n : 0, 0x32, sig, sig_len);
-    if (!pass) body = n;
-    else return (int)((w + n) - out);
+  size_t n = 0;
+  if (height != 0) {
+    if (w) w[n] = 0x08;
+    n += 1 + put_uvarint(w ? w + n + 1 : 0, (uint64_t)height);
   }
-  return -1;
+  n += put_bytes_field(w ? w + n : 0, 0x12, txhash, txhash_len);
+  if (w) { w[n] = 0x1a; w[n + 1] = 0x20; memcpy(w + n + 2, txkey ? txkey : zero32, 32); }
+  n += 34;
+  n += put_bytes_field(w ? w + n : 0, 0x22, tb, tl);
+  n += put_bytes_field(w ? w + n : 0, 0x2a, addr, addr_len);
+  n += put_bytes_field(w ? w + n : 0, 0x32, sig, sig_len);
+  return (int)n;
+}
+
+int orc_wire_encode(int64_t height, const uint8_t* txhash, size_t txhash_len, const uint8_t* txkey,
+                    int64_t ts_sec, int32_t ts_nanos, const uint8_t* addr, size_t addr_len,
+                    const uint8_t* sig, size_t sig_len, uint8_t* out, size_t cap) {
+  /* 4 prefix bytes of the registered TxVoteMessage, field 1 = the TxVote body */
+  const int body = orc_txvote_encode(height, txhash, txhash_len, txkey, ts_sec, ts_nanos, addr, addr_len, sig, sig_len, 0);
+  if (body < 0) return -1;
+  uint8_t disamb[3], prefix[4];
+  orc_wire_prefix(disamb, prefix);
+  const size_t total = 4 + 1 + put_uvarint(0, (uint64_t)body) + (size_t)body;
+  if (total > cap) return -1;
+  memcpy(out, prefix, 4);
+  out[4] = 0x0a;
+  uint8_t* w = out + 5 + put_uvarint(out + 5, (uint64_t)body);
+  orc_txvote_encode(height, txhash, txhash_len, txkey, ts_sec, ts_nanos, addr, addr_len, sig, sig_len, w);
+  return (int)total;
 }
 
 /* CPU baseline: decode n messages in a loop on one thread; returns seconds */

@@ -1,7 +1,11 @@
-"""Multi-rank path on CPU (gloo, world_size 2): votes sharded by SHA-256(TxHash)[0] mod G,
-per-shard sequential tallies (oracle stands in for the per-GPU engine), one all-gather of the
-per-shard commit bitmaps; the merged committed set and per-tx stakes must equal a single
-global sequential run (the tally is shard-local, so sharding changes nothing)."""
+"""Multi-rank path on CPU (gloo, world_size 2): votes sharded by the C-ABI's rule
+(txv_shard_of: SHA-256(TxHash)[0] mod G), per-shard sequential tallies (the oracle stands in for
+the per-GPU engine: no GPU here), each shard's state packed with the C-ABI's layout
+(txv_commit_state_pack_host -- the same bytes txv_pack_commit_state writes on the GPU), ONE
+all-gather of the packed buffers, unpacked with txv_commit_state_unpack; the merged committed set
+and per-tx stakes must equal a single global sequential run (the tally is
+shard-local, so sharding changes nothing).  tests/test_configs.py checks on the GPU that the
+device pack equals the host pack of the same state."""
 import os
 import random
 import sys
@@ -39,6 +43,7 @@ def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+    import txflow_amd as T
     from txflow_amd import sharding
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -52,14 +57,15 @@ def _worker(rank, world, port, q):
     for v in mine:
         if v["txhash"] not in local_keys:
             local_keys.append(v["txhash"])
-    committed = [i for i, k in enumerate(local_keys) if flow.query(k)[1]]
-    bm = torch.from_numpy(sharding.pack_bitmap(committed, 64).view(np.int32).copy())
-    out = torch.zeros(world * bm.numel(), dtype=torch.int32)
-    dist.all_gather_into_tensor(out, bm)
+    cap = 64
+    committed = np.array([flow.query(k)[1] for k in local_keys], np.uint8)
+    sums = np.array([flow.query(k)[0] for k in local_keys], np.int64)
+    packed = torch.from_numpy(T.commit_state_pack_host(committed, sums, cap))
+    out = torch.zeros(world * packed.numel(), dtype=torch.uint8)
+    dist.all_gather_into_tensor(out, packed)
     keys_all = [None] * world
     dist.all_gather_object(keys_all, local_keys)
-    merged = sharding.merge_gathered(out.numpy().view(np.uint32), world, keys_all)
-    stakes = {k: flow.query(k)[0] for k in local_keys}
+    merged, stakes = sharding.merge_states(out.numpy(), world, cap, keys_all)
     q.put((rank, sorted(merged), stakes))
     dist.destroy_process_group()
 
@@ -79,11 +85,31 @@ def test_two_rank_sharded_tally_matches_global():
     flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
     flow.add_votes(votes)
     glob_commit = sorted(t for t in set(v["txhash"] for v in votes) if flow.query(t)[1])
-    for _, merged, _ in res:
+    for _, merged, stakes in res:
         assert merged == glob_commit
-    stakes = {}
-    for _, _, s in res:
-        stakes.update(s)
-    for t in set(v["txhash"] for v in votes):
-        assert stakes[t] == flow.query(t)[0]
+        for t in set(v["txhash"] for v in votes):     # every rank holds every tx's stake
+            assert stakes[t] == flow.query(t)[0]
     assert len(glob_commit) > 0
+
+
+def test_shard_rule_and_pack_layout():
+    """txv_shard_of = SHA-256(TxHash)[0] mod G; the packed state round-trips and has the
+    documented layout [n_sets u32][0 u32][bitmap][sums i64]."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+    import txflow_amd as T
+    rnd = random.Random(5)
+    hashes = [bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 1, 63, 64, 65, 200]))) for _ in range(500)]
+    for g in (1, 2, 3, 8):
+        assert list(T.shard_of(hashes, g)) == [hashlib.sha256(h).digest()[0] % g for h in hashes]
+    cap = 70
+    com = np.array([rnd.random() < 0.5 for _ in range(37)], np.uint8)
+    sums = np.array([rnd.randrange(-5, 1 << 40) for _ in range(37)], np.int64)
+    buf = T.commit_state_pack_host(com, sums, cap)
+    assert len(buf) == T.commit_state_bytes(cap) == 8 + 4 * ((cap + 31) // 32) + 8 * cap
+    w = buf.view(np.uint32)
+    assert w[0] == 37 and w[1] == 0
+    bits = np.unpackbits(buf[8:8 + 4 * ((cap + 31) // 32)], bitorder="little")[:37]
+    assert np.array_equal(bits, com)
+    c2, s2 = T.commit_state_unpack(buf, cap)
+    assert np.array_equal(c2, com.astype(bool)) and np.array_equal(s2, sums)
