@@ -6,14 +6,15 @@
 //   reject len(sig) != 64 | sig[63] & 0xE0 | undecodable A | s >= L,
 //   k = SHA-512(R || A || M) mod L, accept iff encode([s]B + [k](-A)) == R bytewise.
 // The double scalar multiplication is evaluated doubling-free over fixed-base radix-2^W
-// tables (ge.h Niels entries): T_P[i][j] = j * 2^(W i) * P for i < 256/W, j <= 2^(W-1)
+// tables (ge.h half-Niels entries): T_P[i][j] = j * 2^(W i) * P for i < 256/W, j <= 2^(W-1)
 // (j = 0 the identity), so [s]B + [k](-A) = sum_i T_B[i][s_i] - T_A[i][k_i] with signed
 // digits.  This is exact group arithmetic, hence the same point and encoding as x/crypto's
-// sliding-window GeDoubleScalarMultVartime.
-//   W = 4:  64 positions x    9 entries x 96 B =    55,296 B per point (B fits in LDS)
-//   W = 8:  32 positions x  129 entries x 96 B =   396,288 B per point (L2/MALL resident)
-//   W = 12: 22 positions x 2049 entries x 96 B = 4,327,488 B per point (MALL/HBM resident)
-// 2 * ceil(256/W) mixed additions per verification: 128 / 64 / 44.
+// sliding-window GeDoubleScalarMultVartime.  Entries are 128 B (one line):
+//   W = 4:  64 positions x    9 entries x 128 B =    73,728 B per point (B fits in LDS)
+//   W = 8:  32 positions x  129 entries x 128 B =   528,384 B per point (L2/MALL resident)
+//   W = 20: 13 positions x 2^19+1 entries x 128 B = 872 MB per point (HBM)
+// ceil(256/W_B) + ceil(256/W_A) table additions per verification, the first of them free
+// (the accumulator starts as the first B entry's point).
 #pragma once
 #include "fe.h"
 #include "sc.h"
@@ -21,8 +22,6 @@
 #include "ge.h"
 
 namespace txv {
-
-constexpr int kEntryWords = 24;        // y+x, y-x, 2dxy: 3 x 8 limbs
 
 template <int W>
 struct Tab {
@@ -117,25 +116,54 @@ TXV_HD void sha512_prefixed_pf(uint32_t digest_le[16], const uint64_t* pre, int 
   }
 }
 
-// table entry fetch: T[pos][idx] from a flat word array
+// table entry fetch: T[pos][idx] from a flat word array, (qp, qm) swapped for -Q (neg): the
+// swap is the choice of which 16-byte-aligned half of the line is loaded as which
 template <int W, typename Ptr>
-TXV_HD ge_niels load_entry_w(Ptr tab, int pos, int idx) {
+TXV_HD void load_entry_w(Ptr tab, int pos, int idx, bool neg, fe10& qp, fe10& qm, fe10& qd) {
 #if defined(TXV_EXP_L2_TABLES)   // experiment only: every lookup hits one entry (L1/L2 resident)
   const size_t base = (size_t)(1 + (idx & 1)) * kEntryWords;
 #else
   const size_t base = (size_t)(uint32_t)(pos * Tab<W>::kEntries + idx) * kEntryWords;
 #endif
-  ge_niels e;
+#ifndef TXV_ENTRY_LOADS
+#define TXV_ENTRY_LOADS 1
+#endif
+#if TXV_ENTRY_LOADS == 2
+  // the whole line as 8 x 16-byte loads, the sign swap as per-lane selects
+  const uint4* e4 = reinterpret_cast<const uint4*>(&tab[base]);
+  uint32_t w[32];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    e.ypx.v[i] = tab[base + i];
-    e.ymx.v[i] = tab[base + 8 + i];
-    e.xy2d.v[i] = tab[base + 16 + i];
+  for (int j = 0; j < 8; ++j) {
+    const uint4 x = e4[j];
+    w[4 * j] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
   }
-  return e;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    qd.v[i] = w[kEntryQd + i];
+    qm.v[i] = neg ? w[i] : w[kEntryQm + i];
+    qp.v[i] = neg ? w[kEntryQm + i] : w[i];
+  }
+#else
+  // in the order ge10_madd consumes them (qd, then qm, then qp), so each product can start as
+  // soon as its own operand has landed (vmcnt counts in issue order)
+  const uint32_t op = neg ? kEntryQm : 0u, om = neg ? 0u : kEntryQm;
+  const uint2* d2 = reinterpret_cast<const uint2*>(&tab[base + kEntryQd]);
+  const uint2 d0 = d2[0];
+  const uint4 d1 = reinterpret_cast<const uint4*>(d2 + 1)[0], d3 = reinterpret_cast<const uint4*>(d2 + 1)[1];
+  const uint4* m4 = reinterpret_cast<const uint4*>(&tab[base + om]);
+  const uint4 m0 = m4[0], m1 = m4[1];
+  const uint2 m2 = reinterpret_cast<const uint2*>(m4 + 2)[0];
+  const uint4* p4 = reinterpret_cast<const uint4*>(&tab[base + op]);
+  const uint4 p0 = p4[0], p1 = p4[1];
+  const uint2 p2 = reinterpret_cast<const uint2*>(p4 + 2)[0];
+  qp.v[0] = p0.x; qp.v[1] = p0.y; qp.v[2] = p0.z; qp.v[3] = p0.w;
+  qp.v[4] = p1.x; qp.v[5] = p1.y; qp.v[6] = p1.z; qp.v[7] = p1.w; qp.v[8] = p2.x; qp.v[9] = p2.y;
+  qm.v[0] = m0.x; qm.v[1] = m0.y; qm.v[2] = m0.z; qm.v[3] = m0.w;
+  qm.v[4] = m1.x; qm.v[5] = m1.y; qm.v[6] = m1.z; qm.v[7] = m1.w; qm.v[8] = m2.x; qm.v[9] = m2.y;
+  qd.v[0] = d0.x; qd.v[1] = d0.y; qd.v[2] = d1.x; qd.v[3] = d1.y;
+  qd.v[4] = d1.z; qd.v[5] = d1.w; qd.v[6] = d3.x; qd.v[7] = d3.y; qd.v[8] = d3.z; qd.v[9] = d3.w;
+#endif
 }
-template <typename Ptr>
-TXV_HD ge_niels load_entry(Ptr tab, int pos, int idx) { return load_entry_w<4>(tab, pos, idx); }
 
 // Streaming signed radix-2^W digit of a 256-bit scalar held in 8 words: returns the low
 // digit in [-2^(W-1), 2^(W-1)) (with the running carry) and shifts the scalar right by W.
@@ -154,25 +182,39 @@ TXV_HD int next_digit(uint32_t s[8], uint32_t& carry) {
 // sum_i T_B[i][s_i] + T_A[i][-k_i] over raw scalars s, k < 2^253 (digits of k negated,
 // giving [k](-A)); digits are produced on the fly, so any windows < 32 work.  The base
 // point's table may use a wider window WB than the validators' WA (one table serves every
-// vote, so it can take gigabytes of HBM): ceil(256/WB) + ceil(256/WA) mixed additions.
+// vote, so it can take gigabytes of HBM).  The walk runs in fe10 (ge10_madd); the result is
+// handed back in radix 2^32 (X, Y, Z; T is not produced).
 template <int WB, int WA, typename PtrB, typename PtrA>
 TXV_HD ge_ext double_scalarmult_w2(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {
   static_assert(WB >= WA, "B window must be at least the A window");
-  ge_ext P = ge_identity();
   uint32_t s[8], k[8], cs = 0, ck = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
+  fe10 qp, qm, qd;
+  ge10_ext P;
+  {
+    const int ds = next_digit<WB>(s, cs);
+    load_entry_w<WB>(tb, 0, ds < 0 ? -ds : ds, ds < 0, qp, qm, qd);
+    P = ge10_from_entry(qp, qm);
+  }
   for (int pos = 0; pos < Tab<WA>::kPositions; ++pos) {
-    if (pos < Tab<WB>::kPositions) {
+    if (pos > 0 && pos < Tab<WB>::kPositions) {
       const int ds = next_digit<WB>(s, cs);
-      P = ge_madd(P, load_entry_w<WB>(tb, pos, ds < 0 ? -ds : ds), ds < 0);
+      load_entry_w<WB>(tb, pos, ds < 0 ? -ds : ds, ds < 0, qp, qm, qd);
+      P = ge10_madd(P, qp, qm, qd, ds < 0);
     }
     if (use_a) {
       const int dk = next_digit<WA>(k, ck);
-      P = ge_madd(P, load_entry_w<WA>(ta, pos, dk < 0 ? -dk : dk), dk > 0);
+      load_entry_w<WA>(ta, pos, dk < 0 ? -dk : dk, dk > 0, qp, qm, qd);
+      P = ge10_madd(P, qp, qm, qd, dk > 0);
     }
   }
-  return P;
+  ge_ext R;
+  R.X = fe_from_fe10(P.X);
+  R.Y = fe_from_fe10(P.Y);
+  R.Z = fe_from_fe10(P.Z);
+  R.T = fe_zero();
+  return R;
 }
 template <int W, typename PtrB, typename PtrA>
 TXV_HD ge_ext double_scalarmult_w(PtrB tb, PtrA ta, const uint32_t s_in[8], const uint32_t k_in[8], bool use_a) {

@@ -6,10 +6,11 @@
 // so [s]B + [k](-A) comes out as the same group element x/crypto computes and its
 // canonical encoding is bit-identical (Appendix A.1 step 6).
 //
-// Precomputed table entries are "affine Niels" triples (y+x, y-x, 2d*x*y), canonical,
-// 96 bytes each; a mixed add costs 7 field multiplies.
+// Precomputed table entries are half-Niels triples ((y+x)/2, (y-x)/2, d*x*y) in fe10 limbs,
+// 128 bytes each (ge10_madd below); a mixed add costs 7 field multiplies.
 #pragma once
 #include "fe.h"
+#include "fe10.h"
 
 namespace txv {
 
@@ -20,31 +21,106 @@ TXV_HD ge_ext ge_identity() {
   ge_ext r; r.X = fe_zero(); r.Y = fe_one(); r.Z = fe_one(); r.T = fe_zero(); return r;
 }
 
-// P + s*Q where Q is an affine Niels point and s = -1 when neg (swap y+x/y-x, negate 2dxy)
-TXV_HD ge_ext ge_madd(const ge_ext& p, const ge_niels& q, bool neg) {
-  fe qp = fe_select(neg, q.ymx, q.ypx);
-  fe qm = fe_select(neg, q.ypx, q.ymx);
-  fe A = fe_mul(fe_sub(p.Y, p.X), qm);
+// ---------------------------------------------------------------- table walk (K1b)
+// The fixed-base tables hold each multiple Q = (x, y) as a HALF-Niels entry
+//   qp = (y + x) / 2, qm = (y - x) / 2, qd = d x y        (mod p, canonical, fe10 limbs)
+// With them the mixed addition below computes (E, H, G, F) = 1/2 of HWCD's
+// (B - A, B + A, 2Z + 2d T x y, 2Z - 2d T x y), so (X3, Y3, Z3, T3) = 1/4 of the HWCD sum: the
+// same projective point, and no doubling of Z -- which keeps every operand inside fe10_mul's
+// bounds without a carry pass.  7 multiplies, 6 carry-free adds/subs, one conditional negation.
+struct ge10_ext { fe10 X, Y, Z, T; };
+
+// P + Q or P - Q: the caller passes (qp, qm) already swapped for -Q (the swap is an address
+// choice when loading); neg negates qd's product
+TXV_HD ge10_ext ge10_madd(const ge10_ext& p, const fe10& qp, const fe10& qm, const fe10& qd, bool neg) {
+  // C first: T and qd die before the other products (register peak, 4 waves/SIMD at 128 VGPRs)
+  const fe10 C = fe10_cneg(fe10_mul(p.T, qd), neg);
   TXV_SCHED_FENCE();
-  fe B = fe_mul(fe_add(p.Y, p.X), qp);
+  const fe10 A = fe10_mul(fe10_sub(p.Y, p.X), qm);
   TXV_SCHED_FENCE();
-  fe E = fe_sub(B, A), H = fe_add(B, A);
-  fe C = fe_mul(p.T, q.xy2d);
+  const fe10 B = fe10_mul(fe10_add(p.Y, p.X), qp);
   TXV_SCHED_FENCE();
-  fe D = fe_dbl(p.Z);
-  fe Gp = fe_add(D, C), Fm = fe_sub(D, C);
-  fe G = fe_select(neg, Fm, Gp), F = fe_select(neg, Gp, Fm);
-  ge_ext r;
-  r.X = fe_mul(E, F);
+  const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
+  const fe10 G = fe10_add(p.Z, C), F = fe10_sub(p.Z, C);
+  ge10_ext r;
+  r.X = fe10_mul(E, F);
   TXV_SCHED_FENCE();
-  r.Y = fe_mul(G, H);
+  r.Y = fe10_mul(H, G);
   TXV_SCHED_FENCE();
-  r.Z = fe_mul(F, G);
+  r.Z = fe10_mul(F, G);
   TXV_SCHED_FENCE();
-  r.T = fe_mul(E, H);
+  r.T = fe10_mul(E, H);
   TXV_SCHED_FENCE();
   return r;
 }
+
+// the same addition with the entry read piecewise right before each use (rd(0) = qp, rd(1) = qm,
+// rd(2) = qd, already swapped for -Q): only one of them is live at a time, which keeps the
+// prefetching K1b walk inside 128 VGPRs; mid() runs once all three are read (the walk issues its
+// next prefetch there, into the buffer just read)
+template <class Rd, class Mid>
+TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {
+  const fe10 C = fe10_cneg(fe10_mul(p.T, rd(2)), neg);
+  TXV_SCHED_FENCE();
+  const fe10 A = fe10_mul(fe10_sub(p.Y, p.X), rd(1));
+  TXV_SCHED_FENCE();
+  const fe10 B = fe10_mul(fe10_add(p.Y, p.X), rd(0));
+  TXV_SCHED_FENCE();
+  mid();
+  const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
+  const fe10 G = fe10_add(p.Z, C), F = fe10_sub(p.Z, C);
+  ge10_ext r;
+  r.X = fe10_mul(E, F);
+  TXV_SCHED_FENCE();
+  r.Y = fe10_mul(H, G);
+  TXV_SCHED_FENCE();
+  r.Z = fe10_mul(F, G);
+  TXV_SCHED_FENCE();
+  r.T = fe10_mul(E, H);
+  TXV_SCHED_FENCE();
+  return r;
+}
+
+// the entry's own point (Z = 1): x = qp - qm, y = qp + qm, T = x y
+TXV_HD ge10_ext ge10_from_entry(const fe10& qp, const fe10& qm) {
+  ge10_ext r;
+  r.X = fe10_carry(fe10_sub(qp, qm));
+  r.Y = fe10_carry(fe10_add(qp, qm));
+  r.Z = fe10_one();
+  r.T = fe10_mul(r.X, r.Y);
+  return r;
+}
+
+// (p + 1) / 2
+TXV_HD fe fe_const_half() {
+  fe r; const uint32_t k[8] = {0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                               0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu};
+  for (int i = 0; i < 8; ++i) r.v[i] = k[i];
+  return r;
+}
+
+// table entry words: qp at 0..9, qm at 12..21 (both 16-byte aligned, so the sign swap is an
+// address offset), qd at 22..31; words 10, 11 zero.  32 words = one 128-byte line.
+constexpr int kEntryWords = 32;
+constexpr int kEntryQm = 12;
+constexpr int kEntryQd = 22;
+
+TXV_HD void entry_words(uint32_t e[kEntryWords], const fe& ypx, const fe& ymx, const fe& xy2d) {
+  const fe h = fe_const_half();
+  const fe10 qp = fe10_from_fe(fe_canon(fe_mul(ypx, h)));
+  const fe10 qm = fe10_from_fe(fe_canon(fe_mul(ymx, h)));
+  const fe10 qd = fe10_from_fe(fe_canon(fe_mul(xy2d, h)));
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    e[i] = qp.v[i];
+    e[kEntryQm + i] = qm.v[i];
+    e[kEntryQd + i] = qd.v[i];
+  }
+  e[10] = 0;
+  e[11] = 0;
+}
+// the identity's entry (y + x = y - x = 1, 2dxy = 0)
+TXV_HD void entry_identity(uint32_t e[kEntryWords]) { entry_words(e, fe_one(), fe_one(), fe_zero()); }
 
 // extended + extended (add-2008-hwcd-3), used by the table builder
 TXV_HD ge_ext ge_add(const ge_ext& p, const ge_ext& q) {

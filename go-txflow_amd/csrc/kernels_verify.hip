@@ -84,14 +84,9 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
     fe zi = j ? fe_mul(inv, pref[j - 1]) : inv;
     if (j) inv = fe_mul(inv, M[j].Z);
     ge_niels n = ge_to_niels(M[j], zi);
-    uint32_t* e = out + (8 * c + j + 1) * kEntryWords;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { e[i] = n.ypx.v[i]; e[8 + i] = n.ymx.v[i]; e[16 + i] = n.xy2d.v[i]; }
+    entry_words(out + (8 * c + j + 1) * kEntryWords, n.ypx, n.ymx, n.xy2d);
   }
-  if (c == 0) {
-#pragma unroll
-    for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;   // identity (1, 1, 0)
-  }
+  if (c == 0) entry_identity(out);
 }
 
 // ---------------------------------------------------------------- K1: verify
@@ -169,10 +164,10 @@ __device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, 
   }
 }
 
-// W = 4: the 55 KB B table is staged in LDS (8 waves per 512-thread block share it)
+// W = 4: the 74 KB B table is staged in LDS (8 waves per 512-thread block share it)
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_w4(VerifyArgs a) {
-  __shared__ uint32_t btab[Tab<4>::kWords];
+  __shared__ __attribute__((aligned(16))) uint32_t btab[Tab<4>::kWords];
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.btable);
     uint4* dst = reinterpret_cast<uint4*>(btab);
@@ -254,6 +249,111 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
   }
 }
 
+// ---------------------------------------------------------------- K1b table walk, prefetched
+// The walk's 24 table entries are random 128-byte lines in tens of GB of tables: every one is an
+// HBM miss, and per-lane loads of them cost the memory pipeline one line request per 16 bytes
+// (8 per entry; measured, tools/microbench/gather_calib.hip: 16M entries 2.00 ms as 8 x 16-byte
+// loads per lane, 0.78 ms loaded cooperatively).  So the wave loads its 64 entries together:
+// load i (i < 8) fetches entries 8i .. 8i+7, 8 lanes x 16 bytes per entry (one whole line per 8
+// lanes), global -> LDS (global_load_lds_dwordx4, no VGPRs; the entry's address comes from its
+// lane by ds_bpermute).  The LDS image is lane-linear (load i, lane l at i * 1 KiB + 16 l); lane
+// l loads piece ((l & 7) + e) & 7 of entry e = 8i + (l >> 3), which makes the pieces a reader
+// lane wants land in distinct banks (8 consecutive readers -> 8 distinct 16-byte slots of a
+// 256-byte row).  Entry t + 1 is issued once entry t has been read out, so it has a whole
+// addition (x the other waves) to arrive.  LDS per wave 8 KiB; 64 KiB per 512-thread block.
+// Schedule: B0 A0 B1 A1 ... (B positions first exhausted at W_B > W_A).
+#ifndef TXV_K1B_PREFETCH
+#define TXV_K1B_PREFETCH 1
+#endif
+
+// the wave's 64 entries (entry index e_l of lane l, 128-byte units from base) -> buf
+__device__ __forceinline__ void entries_to_lds(const uint32_t* base, uint32_t e_l, uint4* buf) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int src = 8 * i + (lane >> 3);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)e_l);
+    const uint32_t piece = (uint32_t)((lane & 7) + src) & 7u;
+    const uint32_t* g = base + (size_t)e * kEntryWords + piece * 4u;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)(buf + 64 * i), 16, 0, 0);
+  }
+}
+
+// piece j of this lane's entry in the image entries_to_lds wrote
+__device__ __forceinline__ const uint4* entry_piece(const uint4* buf, int j) {
+  const int e = threadIdx.x & 63;
+  return buf + 64 * (e >> 3) + 8 * (e & 7) + ((j - e) & 7);
+}
+
+// one field of the lane's entry; role 0 = qp, 1 = qm (swapped for -Q by the piece choice),
+// 2 = qd.  Words 0..9 = pieces 0, 1, 2.xy; 12..21 = pieces 3, 4, 5.xy; qd = 5.zw, 6, 7.
+__device__ __forceinline__ fe10 entry_field_lds(const uint4* buf, bool neg, int role) {
+  fe10 r;
+  if (role == 2) {
+    const uint2 d0 = reinterpret_cast<const uint2*>(entry_piece(buf, 5))[1];
+    const uint4 d1 = *entry_piece(buf, 6), d2 = *entry_piece(buf, 7);
+    r.v[0] = d0.x; r.v[1] = d0.y; r.v[2] = d1.x; r.v[3] = d1.y;
+    r.v[4] = d1.z; r.v[5] = d1.w; r.v[6] = d2.x; r.v[7] = d2.y; r.v[8] = d2.z; r.v[9] = d2.w;
+    return r;
+  }
+  const int j0 = (neg != (role == 1)) ? 3 : 0;
+  const uint4 p0 = *entry_piece(buf, j0), p1 = *entry_piece(buf, j0 + 1);
+  const uint2 p2 = *reinterpret_cast<const uint2*>(entry_piece(buf, j0 + 2));
+  r.v[0] = p0.x; r.v[1] = p0.y; r.v[2] = p0.z; r.v[3] = p0.w;
+  r.v[4] = p1.x; r.v[5] = p1.y; r.v[6] = p1.z; r.v[7] = p1.w; r.v[8] = p2.x; r.v[9] = p2.y;
+  return r;
+}
+
+// tb: the B table; ta: the validators' tables, va = this lane's validator (entries of validator v
+// start at entry v * positions * entries)
+template <int WB, int WA>
+__device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const uint32_t* ta, uint32_t va,
+                                                       const uint32_t s_in[8], const uint32_t k_in[8], uint4* buf) {
+  static_assert(WB >= WA, "B window must be at least the A window");
+  constexpr int nB = Tab<WB>::kPositions, nA = Tab<WA>::kPositions, nT = nB + nA;
+  uint32_t s[8], k[8], cs = 0, ck = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
+  // entry t of the schedule: its digit (consumed from s or k in order), table line -> LDS
+  auto issue = [&](int t) -> bool {
+    const bool isB = t < 2 * nB && !(t & 1);
+    const int pos = t < 2 * nB ? (t >> 1) : t - nB;
+    if (isB) {
+      const int d = next_digit<WB>(s, cs);
+      entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), buf);
+      return d < 0;
+    }
+    const int d = next_digit<WA>(k, ck);
+    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), buf);
+    return d > 0;                                   // [k](-A): a positive digit subtracts
+  };
+  ge10_ext P;
+  bool neg = issue(0);
+#pragma unroll 1
+  for (int t = 0; t < nT; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // entry t has landed in LDS
+    const bool neg_t = neg;
+    auto next = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // read out before the next DMA lands
+      if (t + 1 < nT) neg = issue(t + 1);
+    };
+    if (t) {
+      P = ge10_madd_rd(P, [&](int role) { return entry_field_lds(buf, neg_t, role); }, neg_t, next);
+    } else {
+      const fe10 qp = entry_field_lds(buf, neg_t, 0), qm = entry_field_lds(buf, neg_t, 1);
+      next();
+      P = ge10_from_entry(qp, qm);
+    }
+  }
+  ge_ext R;
+  R.X = fe_from_fe10(P.X);
+  R.Y = fe_from_fe10(P.Y);
+  R.Z = fe_from_fe10(P.Z);
+  R.T = fe_zero();
+  return R;
+}
+
 // W >= 8, V votes per lane sharing ONE field inversion (Montgomery's trick over the V
 // results: P_h = Z_0 ... Z_h; 1/Z_h = P_{h-1} / P_{V-1} walking back).  The first V-1
 // results wait in a global scratch buffer (wave-interleaved: coalesced, L2-resident,
@@ -265,8 +365,10 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 #ifndef TXV_PARK_LAST
 #define TXV_PARK_LAST 1
 #endif
+// V = 8 is launched for batches that give 2 waves per SIMD (launch_lane_votes), so its register
+// budget is 256 VGPRs (2 waves/SIMD); V = 4 keeps 128 (4 waves/SIMD)
 template <int BLOCK, int WB, int WA, int V>
-__global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
+__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
   // lane group g = 64 w + l takes the work-list entries 64 V w + 64 h + l (h < V): the lanes of
   // a wave read 64 consecutive entries per vote slot, so the vote-column reads (sig, kbuf) of an
   // arrival-ordered list are two lines per column per wave
@@ -283,6 +385,10 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
   // contiguous 256-byte line and every offset is a compile-time immediate
   const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
   uint32_t* park = a.park + (size_t)gwave * (V - 1 + TXV_PARK_LAST) * TXV_PARK_WORDS * 64 + (threadIdx.x & 63);
+#if TXV_K1B_PREFETCH
+  __shared__ uint4 pf[BLOCK / 64][8 * 64];
+  uint4* wbuf = pf[threadIdx.x >> 6];
+#endif
   for (uint32_t g = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; g < hi; g += stride) {
     uint32_t act = 0;
 #pragma unroll
@@ -290,11 +396,32 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
       const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
       if (idx < a.n_work && a.ok_out[a.order ? a.order[idx] : idx] == 2) act |= 1u << h;
     }
+#if TXV_K1B_PREFETCH
+    // the cooperative walk needs every lane of the wave (g < hi is wave-uniform: lo, hi and the
+    // wave's first g are multiples of 64): skip only when the whole wave is idle; idle lanes walk
+    // the digit-0 (identity) entries of validator 0
+    if (__builtin_amdgcn_ballot_w64(act != 0) == 0) continue;
+#else
     if (!act) continue;
+#endif
     ge_ext R;
     fe P;
 #pragma unroll 1
     for (int h = 0; h < V; ++h) {
+#if TXV_K1B_PREFETCH
+      {
+        const bool on = act >> h & 1u;
+        const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
+        const uint32_t i = on ? (a.order ? a.order[idx] : idx) : 0u;
+        uint32_t s[8], k[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
+          k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
+        }
+        R = double_scalarmult_pf<WB, WA>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+      }
+#else
       if (act >> h & 1u) {
         const uint32_t idx = (g & ~63u) * V + 64u * h + (g & 63u);
         const uint32_t i = a.order ? a.order[idx] : idx;
@@ -305,6 +432,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_multi
       } else {
         R = ge_identity();
       }
+#endif
       P = h ? fe_mul(P, R.Z) : R.Z;
       if (h < V - 1 || TXV_PARK_LAST) {
         uint32_t* slot = park + h * TXV_PARK_WORDS * 64;

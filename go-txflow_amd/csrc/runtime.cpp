@@ -39,9 +39,10 @@ void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // SHA-2
 
 namespace {
 
-// fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 24
-inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 24; }
-constexpr uint32_t kTableWords4 = 64 * 9 * 24;
+// fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 32
+// (one 128-byte half-Niels entry each, ge.h)
+inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32; }
+constexpr uint32_t kTableWords4 = 64 * 9 * 32;
 inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
 constexpr uint32_t kSlots = 4;
 
@@ -954,7 +955,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (c->cfg.max_batch > (8u << 20)) { delete c; return TXV_EINVAL; }   // the device scans cover 8M votes
   c->hash_seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x7478666c6f77ULL;
   if (!c->cfg.max_msg_bytes) c->cfg.max_msg_bytes = 256;
-  if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 80u << 10;   // 80 GiB of the 288 GB HBM
+  if (!c->cfg.table_budget_mb) c->cfg.table_budget_mb = 112u << 10;   // 112 GiB of the 288 GB HBM
   c->cfg_w = (c->cfg.flags & TXV_CFG_TABLE_W4) ? 4 : 0;
   if (TXV_CFG_WINDOW(c->cfg.flags)) c->cfg_w = (int)TXV_CFG_WINDOW(c->cfg.flags);
   if (c->cfg_w && !valid_window(c->cfg_w)) { delete c; return TXV_EINVAL; }

@@ -84,9 +84,9 @@ extern "C" {
 typedef struct txv_ctx txv_ctx;
 
 /* HBM footprint of a context (MI355X: 288 GB per GPU), all allocated up front:
- *   validator tables   n_vals x table size of the window (see TXV_CFG_WINDOW): 654 MB each at the
- *                      default radix-2^20 for <= 125 validators (65 GB for 100), within table_budget_mb
- *   base-point table   8.9 GB (radix-2^24) per context, plus 0.4 MB / 55 KB for the small windows
+ *   validator tables   n_vals x table size of the window (see TXV_CFG_WINDOW): 872 MB each at the
+ *                      default radix-2^20 for <= 137 validators (87 GB for 100), within table_budget_mb
+ *   base-point table   11.8 GB (radix-2^24) per context, plus 0.5 MB / 74 KB for the small windows
  *   TxFlow state       12 x max_txs x n_vals B of cells + 128 x max_accepted B of accepted votes +
  *                      64 x 2 (max_txs + max_batch) B of set table + key_arena_bytes (1M sets x 100
  *                      validators: 1.2 + 8.6 + 0.3 + 0.1 GB)
@@ -103,20 +103,21 @@ typedef struct {
                                would exceed it fails with TXV_ECAPACITY (reset with txv_reset_flow) */
   uint32_t max_msg_bytes;   /* unused since ABI 2 (SignBytes columns are sized per batch) */
   uint32_t flags;           /* TXV_CFG_* bits */
-  uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 81920 =
-                               80 GiB): the default window is the largest of 20/18/16/14/12/10/8
-                               whose tables fit (100 validators: radix-2^20, 65 GB) */
+  uint32_t table_budget_mb; /* HBM budget for the per-validator fixed-base tables (default 114688 =
+                               112 GiB): the default window is the largest of 20/18/16/14/12/10/8
+                               whose tables fit (100 validators: radix-2^20, 87 GB) */
   uint64_t key_arena_bytes; /* device bytes for the TxHash strings of all TxVoteSets (each rounded up
                                to 8); 0 = 96 x max_txs + 1 MiB */
 } txv_config;
-/* verify with radix-16 tables (B staged in LDS, 55 KB/validator) instead of the wider
+/* verify with radix-16 tables (B staged in LDS, 74 KB/validator) instead of the wider
  * L2/HBM-resident tables */
 #define TXV_CFG_TABLE_W4 0x1u
 /* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18 or 20; 0 = auto: the
- * largest whose n_vals tables fit table_budget_mb, radix-2^20 for <= 125 validators): per
- * validator 55 KB / 396 KB / 1.3 MB / 4.3 MB / 15 MB / 50 MB / 189 MB / 654 MB.  Windows >= 12 run
- * against the 8.9 GB radix-2^24 base-point table: 11 + ceil(256/W) point additions per verified
- * vote (33 / 30 / 27 / 26 / 24 at W = 12..20); W = 4 / 8 / 10: 2 * ceil(256/W) = 128 / 64 / 52 */
+ * largest whose n_vals tables fit table_budget_mb, radix-2^20 for <= 137 validators): per
+ * validator 74 KB / 0.5 MB / 1.7 MB / 5.8 MB / 20 MB / 67 MB / 252 MB / 872 MB (128-byte entries).
+ * Windows >= 12 run against the 11.8 GB radix-2^24 base-point table: 10 + ceil(256/W) point
+ * additions per verified vote (32 / 29 / 26 / 25 / 23 at W = 12..20; the first B entry is the
+ * starting point); W = 4 / 8 / 10: 2 * ceil(256/W) - 1 = 127 / 63 / 51 */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19:

@@ -26,10 +26,9 @@ static void build_table(std::vector<uint32_t>& tab, const uint32_t w[8], bool* o
     uint32_t* out = tab.data() + pos * kTabEntries * kEntryWords;
     for (int j = 0; j < 8; ++j) {
       ge_niels n = ge_to_niels(M[j], fe_invert(M[j].Z));
-      uint32_t* e = out + (j + 1) * kEntryWords;
-      for (int i = 0; i < 8; ++i) { e[i] = n.ypx.v[i]; e[8 + i] = n.ymx.v[i]; e[16 + i] = n.xy2d.v[i]; }
+      entry_words(out + (j + 1) * kEntryWords, n.ypx, n.ymx, n.xy2d);
     }
-    for (int i = 0; i < 24; ++i) out[i] = (i == 0 || i == 8) ? 1u : 0u;
+    entry_identity(out);
   }
 }
 
@@ -54,6 +53,54 @@ int emu_fe(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
     }
   }
   for (int j = 0; j < 8; ++j) out[j] = r.v[j];
+  return 0;
+}
+
+// fe10 primitives on raw limbs (op 0 mul, 1 add, 2 sub, 3 cneg, 4 carry, 5 strict, 6 from radix
+// 2^32 (8 words in), 7 to radix 2^32 (8 words out), 8 madd on (X,Y,Z,T) + entry words)
+int emu_fe10(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
+  fe10 x, y, r;
+  for (int j = 0; j < 10; ++j) { x.v[j] = a[j]; y.v[j] = b[j]; }
+  switch (op) {
+    case 0: r = fe10_mul(x, y); break;
+    case 1: r = fe10_add(x, y); break;
+    case 2: r = fe10_sub(x, y); break;
+    case 3: r = fe10_cneg(x, true); break;
+    case 4: r = fe10_carry(x); break;
+    case 5: r = fe10_strict(x); break;
+    case 6: {
+      fe f;
+      for (int j = 0; j < 8; ++j) f.v[j] = a[j];
+      r = fe10_from_fe(f);
+      break;
+    }
+    case 7: {
+      fe f = fe_from_fe10(x);
+      for (int j = 0; j < 8; ++j) out[j] = f.v[j];
+      return 0;
+    }
+    default: return -1;
+  }
+  for (int j = 0; j < 10; ++j) out[j] = r.v[j];
+  return 0;
+}
+// one table addition through ge10_madd: p = X,Y,Z,T (40 limbs), e = 32 entry words, out 40 limbs
+int emu_ge10_madd(const uint32_t* p, const uint32_t* e, int neg, uint32_t* out) {
+  ge10_ext P;
+  for (int j = 0; j < 10; ++j) { P.X.v[j] = p[j]; P.Y.v[j] = p[10 + j]; P.Z.v[j] = p[20 + j]; P.T.v[j] = p[30 + j]; }
+  fe10 qp, qm, qd;
+  load_entry_w<4>(e, 0, 0, neg != 0, qp, qm, qd);
+  P = ge10_madd(P, qp, qm, qd, neg != 0);
+  for (int j = 0; j < 10; ++j) { out[j] = P.X.v[j]; out[10 + j] = P.Y.v[j]; out[20 + j] = P.Z.v[j]; out[30 + j] = P.T.v[j]; }
+  return 0;
+}
+// entry words of the affine point (x, y) (radix 2^32 in, canonical)
+int emu_entry(const uint32_t* x, const uint32_t* y, uint32_t* e) {
+  fe X, Y;
+  for (int j = 0; j < 8; ++j) { X.v[j] = x[j]; Y.v[j] = y[j]; }
+  ge_ext P; P.X = X; P.Y = Y; P.Z = fe_one(); P.T = fe_mul(X, Y);
+  ge_niels n = ge_to_niels(P, fe_one());
+  entry_words(e, n.ypx, n.ymx, n.xy2d);
   return 0;
 }
 

@@ -21,13 +21,16 @@ L = 2 ** 252 + 27742317777372353535851937790883648493
 def emu():
     src = os.path.join(EMU_DIR, "emu.hip")
     deps = [src] + [os.path.join(HERE, "..", "go-txflow_amd", "csrc", f)
-                    for f in ("fe.h", "fe_inv_var.h", "sc.h", "sha2.h", "ge.h", "ed25519_dev.h", "wire_dev.h")]
+                    for f in ("fe.h", "fe10.h", "fe_inv_var.h", "sc.h", "sha2.h", "ge.h", "ed25519_dev.h", "wire_dev.h")]
     if not os.path.exists(EMU) or any(os.path.getmtime(d) > os.path.getmtime(EMU) for d in deps):
         os.makedirs(os.path.dirname(EMU), exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "-shared", src, "-o", EMU], check=True)
     E = ctypes.CDLL(EMU)
     E.emu_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
     E.emu_wire_fast_hits.restype = ctypes.c_uint64
+    E.emu_fe10.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    E.emu_ge10_madd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    E.emu_entry.argtypes = [ctypes.c_void_p] * 3
     E.emu_wire_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return E
@@ -57,6 +60,101 @@ def test_field_and_scalar_ops(emu):
             assert (v % P if op < 6 else v) == exp, (op, hex(x), hex(y))
             if op in (4, 7):   # canonical outputs (7: variable-time divstep inverse, K1b)
                 assert v == exp
+
+
+W10 = [26 if i % 2 == 0 else 25 for i in range(10)]
+O10 = [sum(W10[:i]) for i in range(10)]
+
+
+def v10(limbs):
+    return sum(int(x) << o for x, o in zip(limbs, O10))
+
+
+def l10(x):
+    return (ctypes.c_uint32 * 10)(*[(x >> o) & ((1 << w) - 1) for o, w in zip(O10, W10)])
+
+
+def carried(limbs):
+    return all(int(x) < (1 << w) for x, w in zip(limbs, W10)) or (
+        all(int(x) < (1 << w) for i, (x, w) in enumerate(zip(limbs, W10)) if i != 1) and limbs[1] < 2 ** 25 + 2 ** 18)
+
+
+def test_fe10_limb_arithmetic_at_its_bounds(emu):
+    """fe10 (radix 2^25.5, K1b's table walk): mul at the documented operand bounds (f < 4 2^w,
+    g < 3 2^w, incl. every limb at its maximum), add/sub/cneg/carry/strict and both conversions."""
+    rnd = random.Random(11)
+    out = (ctypes.c_uint32 * 10)()
+    maxf = [4 * (1 << w) - 1 for w in W10]
+    maxg = [3 * (1 << w) - 1 for w in W10]
+    cases = [(maxf, maxg), ([0] * 10, maxg), (maxf, [0] * 10)]
+    for _ in range(400):
+        cases.append(([rnd.randrange(4 << w) for w in W10], [rnd.randrange(3 << w) for w in W10]))
+        cases.append(([rnd.choice([0, (4 << w) - 1, rnd.randrange(4 << w)]) for w in W10],
+                      [rnd.choice([0, (3 << w) - 1, rnd.randrange(3 << w)]) for w in W10]))
+    for fa, ga in cases:
+        emu.emu_fe10((ctypes.c_uint32 * 10)(*fa), (ctypes.c_uint32 * 10)(*ga), out, 0)
+        assert v10(out) % P == v10(fa) * v10(ga) % P and carried(list(out)), (fa, ga)
+    for _ in range(300):
+        a, b = rnd.randrange(P), rnd.randrange(P)
+        for op, exp in ((1, a + b), (2, a - b), (3, -a)):
+            emu.emu_fe10(l10(a), l10(b), out, op)
+            assert v10(out) % P == exp % P, op
+            assert all(int(x) < (3 << w) for x, w in zip(out, W10))
+        big = [rnd.randrange(1 << 32 - 8) for _ in range(10)]
+        emu.emu_fe10((ctypes.c_uint32 * 10)(*big), l10(0), out, 4)
+        assert v10(out) % P == v10(big) % P and carried(list(out))
+        emu.emu_fe10((ctypes.c_uint32 * 10)(*big), l10(0), out, 5)
+        assert v10(out) % P == v10(big) % P and v10(out) < 2 ** 255
+        assert all(int(x) < (1 << w) for x, w in zip(out, W10))
+    o8 = (ctypes.c_uint32 * 8)()
+    for x in [0, 1, P - 1, P, 2 ** 255 - 1, 2 ** 255, 2 ** 256 - 1] + [rnd.getrandbits(256) for _ in range(200)]:
+        emu.emu_fe10(w(x), l10(0), out, 6)
+        assert v10(out) % P == x % P
+        emu.emu_fe10(out, l10(0), o8, 7)
+        assert f(o8) % P == x % P and f(o8) < 2 ** 255 + 19
+
+
+def _ed_add(p1, p2):
+    d = -121665 * pow(121666, P - 2, P) % P
+    (x1, y1), (x2, y2) = p1, p2
+    t = d * x1 * x2 * y1 * y2 % P
+    return ((x1 * y2 + y1 * x2) * pow(1 + t, P - 2, P) % P, (y1 * y2 + x1 * x2) * pow(1 - t, P - 2, P) % P)
+
+
+def test_ge10_madd_half_niels(emu):
+    """ge10_madd with the half-Niels entries ((y+x)/2, (y-x)/2, dxy) gives P + Q and P - Q as the
+    same projective point (x = X/Z, y = Y/Z, XY = ZT), including the identity entry and Q = P."""
+    by = 4 * pow(5, P - 2, P) % P
+    d = -121665 * pow(121666, P - 2, P) % P
+    u, v = (by * by - 1) % P, (d * by * by + 1) % P
+    bx = pow(u * pow(v, P - 2, P), (P + 3) // 8, P)
+    if (v * bx * bx - u) % P:
+        bx = bx * pow(2, (P - 1) // 4, P) % P
+    if bx & 1:
+        bx = P - bx
+    B = (bx, by)
+    pts = [B]
+    for _ in range(12):
+        pts.append(_ed_add(pts[-1], B if len(pts) % 2 else pts[-1]))
+    pts.append((0, 1))
+    rnd = random.Random(5)
+    e = (ctypes.c_uint32 * 32)()
+    out = (ctypes.c_uint32 * 40)()
+    for _ in range(60):
+        p1, q = rnd.choice(pts), rnd.choice(pts + [pts[0]])
+        z = rnd.randrange(1, P)
+        X, Y, Z = p1[0] * z % P, p1[1] * z % P, z
+        T = p1[0] * p1[1] * z % P
+        limbs = [int(x) for c in (X, Y, Z, T) for x in l10(c)]
+        emu.emu_entry(w(q[0]), w(q[1]), e)
+        assert e[10] == 0 and e[11] == 0
+        for neg in (0, 1):
+            emu.emu_ge10_madd((ctypes.c_uint32 * 40)(*limbs), e, neg, out)
+            X3, Y3, Z3, T3 = (v10(out[10 * i:10 * i + 10]) for i in range(4))
+            assert carried(list(out[:10])) and carried(list(out[30:]))
+            exp = _ed_add(p1, (P - q[0] if neg else q[0], q[1]))
+            zi = pow(Z3, P - 2, P)
+            assert (X3 * zi % P, Y3 * zi % P) == exp and (X3 * Y3 - Z3 * T3) % P == 0
 
 
 def test_verify_vectors_through_kernel_source(emu):

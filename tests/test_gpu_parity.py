@@ -224,17 +224,17 @@ def test_add_votes_matches_sequential_oracle(gpu_ctx, oracle_lib):
 
 
 def _table_mb(w: int) -> float:
-    return -(-256 // w) * ((1 << (w - 1)) + 1) * 24 * 4 / 2 ** 20
+    return -(-256 // w) * ((1 << (w - 1)) + 1) * 128 / 2 ** 20     # 128-byte entries
 
 
-@pytest.mark.parametrize("budget_mb,exp_w", [(1, 4), (100, 12), (1000, 16), (4000, 18), (0, 20)])
+@pytest.mark.parametrize("budget_mb,exp_w", [(1, 4), (100, 12), (1100, 16), (4100, 18), (0, 20)])
 def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
     """Auto window = largest of 20/18/16/14/12/10/8 whose per-validator tables fit the budget
-    (0 = 80 GiB default), else 4; every window verifies bit-exactly like the oracle, through
+    (0 = 112 GiB default), else 4; every window verifies bit-exactly like the oracle, through
     the registry and through caller-supplied keys on a context without a registry."""
     import txflow_amd as T
     n_vals = 16
-    exp_fit = max([w for w in (8, 10, 12, 14, 16, 18, 20) if n_vals * _table_mb(w) <= (budget_mb or 81920)], default=4)
+    exp_fit = max([w for w in (8, 10, 12, 14, 16, 18, 20) if n_vals * _table_mb(w) <= (budget_mb or 114688)], default=4)
     assert exp_fit == exp_w
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=64, table_budget_mb=budget_mb)
     try:

@@ -9,18 +9,19 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "go-txflo
 import txflow_amd as T  # noqa: E402
 from txflow_amd.workload import Workload, SEEDS  # noqa: E402
 
-for path in sys.argv[1:]:
+for arg in sys.argv[1:]:
+    path, _, w = arg.partition("@")          # lib.so@W: that validator-table window
     T._lib = None
     T.LIB_PATH = os.path.abspath(path)
-    ctx = T.Context(max_batch=2 * 1_000_000, max_txs=10_064, max_validators=100)
+    ctx = T.Context(max_batch=2 * 1_000_000, max_txs=10_064, max_validators=100, table_w=int(w) if w else None)
     wl = Workload(ctx, 100, 10_000, SEEDS["c2"])
     ctx.stage(0, wl.batch)
     v, t = [], []
     for rep in range(6):
-        ctx.reset_tally()
-        ms = ctx.run_staged(0, timed=True)
+        ctx.reset_flow()
+        ms = ctx.run_staged(0, timed=True)          # route, verify, tally, total (ms)
         ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1)
         if rep:
-            v.append(ms[0]); t.append(ms[1])
-    print(f"{os.path.basename(path)}: verify {statistics.median(v):.3f} ms  tally {statistics.median(t):.3f} ms", flush=True)
+            v.append(ms[1]); t.append(ms[2])
+    print(f"{arg} (W={ctx.table_w}/{ctx.base_w}): verify {statistics.median(v):.3f} ms  tally {statistics.median(t):.3f} ms", flush=True)
     ctx.close()

@@ -10,7 +10,7 @@
 //   96 96   (the verify tables today), 128 96 (entries padded to one line), 16 16 (one load).
 // Build: hipcc --offload-arch=gfx950 -O3 gather_calib.hip -o gather_calib
 // Run:   gather_calib STRIDE READ [TABLE_GIB]   (TABLE_GIB default 4; 64 probes the page-walk cost
-//        of a verify-sized table)
+//        of a verify-sized table) [MLANES]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -32,6 +32,32 @@ __global__ void gather(const uint4* __restrict__ table, const uint32_t* __restri
   out[i] = acc;
 }
 
+// cooperative: 8 lanes load one 128-byte entry (16 B each, one coalesced line per 8 lanes)
+__global__ void gather_coop(const uint4* __restrict__ table, const uint32_t* __restrict__ idx, uint32_t n,
+                            uint32_t stride_q, uint32_t* out) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if ((t >> 3) >= n) return;
+  const uint4 v = table[(size_t)idx[t >> 3] * stride_q + (t & 7)];
+  out[t >> 3] = v.x ^ v.y ^ v.z ^ v.w;
+}
+
+// the fe10 half-Niels entry's loads (ed25519_dev.h load_entry_w): (x4, x4, x2) at words 0 and 12
+// (swapped by a per-lane sign), x2 + x4 + x4 at word 22
+__global__ void gather_fe10(const uint32_t* __restrict__ table, const uint32_t* __restrict__ idx, uint32_t n,
+                            uint32_t stride_w, uint32_t* out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* e = table + (size_t)idx[i] * stride_w;
+  const bool neg = idx[i] & 1;
+  const uint4* p4 = reinterpret_cast<const uint4*>(e + (neg ? 12 : 0));
+  const uint4* m4 = reinterpret_cast<const uint4*>(e + (neg ? 0 : 12));
+  const uint2* d2 = reinterpret_cast<const uint2*>(e + 22);
+  const uint4 a = p4[0], b = p4[1], c = m4[0], d = m4[1], f = reinterpret_cast<const uint4*>(d2 + 1)[0],
+              g = reinterpret_cast<const uint4*>(d2 + 1)[1];
+  const uint2 h = reinterpret_cast<const uint2*>(p4 + 2)[0], k = reinterpret_cast<const uint2*>(m4 + 2)[0], l = d2[0];
+  out[i] = a.x ^ b.y ^ c.z ^ d.w ^ f.x ^ g.y ^ h.x ^ k.y ^ l.x ^ a.w ^ b.x ^ c.y ^ d.z ^ f.w ^ g.x;
+}
+
 static uint64_t distinct(const std::vector<uint32_t>& idx, uint64_t stride, uint64_t read, uint64_t g) {
   std::vector<uint64_t> s;
   s.reserve(idx.size() * (read / g + 2));
@@ -45,9 +71,11 @@ static uint64_t distinct(const std::vector<uint32_t>& idx, uint64_t stride, uint
 
 int main(int argc, char** argv) {
   const uint32_t stride = argc > 1 ? (uint32_t)atoi(argv[1]) : 96, read = argc > 2 ? (uint32_t)atoi(argv[2]) : 96;
-  if (stride % 16 || read % 16 || read > stride || (read != 16 && read != 96)) { fprintf(stderr, "bad shape\n"); return 2; }
+  // read 96: 6 x 16-byte loads; 128: 8 x 16-byte loads; 120: the fe10 entry's 9 loads
+  // read 8: the cooperative 128-byte gather (8 lanes per entry)
+  if (stride % 16 || read > stride || (read != 16 && read != 96 && read != 128 && read != 120 && read != 8)) { fprintf(stderr, "bad shape\n"); return 2; }
   const size_t bytes = (size_t)(argc > 3 ? atoi(argv[3]) : 4) << 30, entries = bytes / stride;
-  const uint32_t n = 1u << 20;
+  const uint32_t n = argc > 4 ? (uint32_t)atoi(argv[4]) << 20 : 1u << 20;
   uint4* table; uint32_t *didx, *out;
   CHK(hipMalloc(&table, bytes));
   CHK(hipMemset(table, 1, bytes));
@@ -66,6 +94,12 @@ int main(int argc, char** argv) {
     CHK(hipEventRecord(e0, 0));
     if (read == 96)
       hipLaunchKernelGGL(gather<6>, dim3((n + 255) / 256), dim3(256), 0, 0, table, didx, n, stride / 16, out);
+    else if (read == 128)
+      hipLaunchKernelGGL(gather<8>, dim3((n + 255) / 256), dim3(256), 0, 0, table, didx, n, stride / 16, out);
+    else if (read == 8)
+      hipLaunchKernelGGL(gather_coop, dim3((8 * n + 255) / 256), dim3(256), 0, 0, table, didx, n, stride / 16, out);
+    else if (read == 120)
+      hipLaunchKernelGGL(gather_fe10, dim3((n + 255) / 256), dim3(256), 0, 0, (const uint32_t*)table, didx, n, stride / 4, out);
     else
       hipLaunchKernelGGL(gather<1>, dim3((n + 255) / 256), dim3(256), 0, 0, table, didx, n, stride / 16, out);
     CHK(hipEventRecord(e1, 0));
