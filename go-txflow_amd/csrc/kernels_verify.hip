@@ -269,12 +269,16 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 // the wave's 64 entries (entry index e_l of lane l, 128-byte units from base) -> buf
 __device__ __forceinline__ void entries_to_lds(const uint32_t* base, uint32_t e_l, uint4* buf) {
   const int lane = threadIdx.x & 63;
+  // all 8 permutes first (one LDS round trip instead of one per load: the compiler waits for
+  // outstanding LDS operations before each LDS-DMA issue)
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * i + (lane >> 3)) << 2, (int)e_l);
+  TXV_SCHED_FENCE();
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int src = 8 * i + (lane >> 3);
-    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)e_l);
-    const uint32_t piece = (uint32_t)((lane & 7) + src) & 7u;
-    const uint32_t* g = base + (size_t)e * kEntryWords + piece * 4u;
+    const uint32_t piece = (uint32_t)((lane & 7) + 8 * i + (lane >> 3)) & 7u;
+    const uint32_t* g = base + (size_t)e[i] * kEntryWords + piece * 4u;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)(buf + 64 * i), 16, 0, 0);
   }
@@ -307,41 +311,53 @@ __device__ __forceinline__ fe10 entry_field_lds(const uint4* buf, bool neg, int 
 
 // tb: the B table; ta: the validators' tables, va = this lane's validator (entries of validator v
 // start at entry v * positions * entries)
-template <int WB, int WA>
+template <int WB, int WA, int PD>
 __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const uint32_t* ta, uint32_t va,
                                                        const uint32_t s_in[8], const uint32_t k_in[8], uint4* buf) {
   static_assert(WB >= WA, "B window must be at least the A window");
+  static_assert(PD == 1 || PD == 2, "prefetch depth");
   constexpr int nB = Tab<WB>::kPositions, nA = Tab<WA>::kPositions, nT = nB + nA;
   uint32_t s[8], k[8], cs = 0, ck = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
-  // entry t of the schedule: its digit (consumed from s or k in order), table line -> LDS
+  // entry t of the schedule: its digit (consumed from s or k in order), table lines -> LDS
+  // buffer t % PD
   auto issue = [&](int t) -> bool {
     const bool isB = t < 2 * nB && !(t & 1);
     const int pos = t < 2 * nB ? (t >> 1) : t - nB;
+    uint4* b = buf + (PD == 2 ? (t & 1) * 512 : 0);
     if (isB) {
       const int d = next_digit<WB>(s, cs);
-      entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), buf);
+      entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), b);
       return d < 0;
     }
     const int d = next_digit<WA>(k, ck);
-    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), buf);
+    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
     return d > 0;                                   // [k](-A): a positive digit subtracts
   };
   ge10_ext P;
-  bool neg = issue(0);
+  bool neg = issue(0), neg2 = false;
+  if (PD == 2) neg2 = issue(1);
 #pragma unroll 1
   for (int t = 0; t < nT; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // entry t has landed in LDS
+    // entry t has landed in LDS (with PD = 2 entry t + 1's 8 loads may stay in flight)
+    if (PD == 2 && t + 1 < nT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool neg_t = neg;
+    const uint4* bt = buf + (PD == 2 ? (t & 1) * 512 : 0);
     auto next = [&]() {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // read out before the next DMA lands
-      if (t + 1 < nT) neg = issue(t + 1);
+      if (PD == 2) {
+        neg = neg2;
+        if (t + 2 < nT) neg2 = issue(t + 2);
+      } else if (t + 1 < nT) {
+        neg = issue(t + 1);
+      }
     };
     if (t) {
-      P = ge10_madd_rd(P, [&](int role) { return entry_field_lds(buf, neg_t, role); }, neg_t, next);
+      P = ge10_madd_rd(P, [&](int role) { return entry_field_lds(bt, neg_t, role); }, neg_t, next);
     } else {
-      const fe10 qp = entry_field_lds(buf, neg_t, 0), qm = entry_field_lds(buf, neg_t, 1);
+      const fe10 qp = entry_field_lds(bt, neg_t, 0), qm = entry_field_lds(bt, neg_t, 1);
       next();
       P = ge10_from_entry(qp, qm);
     }
@@ -386,7 +402,10 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : 2 * BLOCK / 256) txv_k_sca
   const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
   uint32_t* park = a.park + (size_t)gwave * (V - 1 + TXV_PARK_LAST) * TXV_PARK_WORDS * 64 + (threadIdx.x & 63);
 #if TXV_K1B_PREFETCH
-  __shared__ uint4 pf[BLOCK / 64][8 * 64];
+  // V = 8 runs 2 waves/SIMD (one 512-thread block per CU): two 8 KiB entry buffers per wave
+  // (prefetch 2 additions ahead, 128 KiB); V = 4 runs two blocks per CU: one buffer (64 KiB)
+  constexpr int PD = V == 8 ? 2 : 1;
+  __shared__ uint4 pf[BLOCK / 64][PD * 8 * 64];
   uint4* wbuf = pf[threadIdx.x >> 6];
 #endif
   for (uint32_t g = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; g < hi; g += stride) {
@@ -419,7 +438,7 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : 2 * BLOCK / 256) txv_k_sca
           s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
           k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
         }
-        R = double_scalarmult_pf<WB, WA>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+        R = double_scalarmult_pf<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
       }
 #else
       if (act >> h & 1u) {

@@ -10,10 +10,12 @@ import txflow_amd as T  # noqa: E402
 from txflow_amd.workload import Workload, SEEDS  # noqa: E402
 
 for arg in sys.argv[1:]:
-    path, _, w = arg.partition("@")          # lib.so@W: that validator-table window
+    path, _, wv = arg.partition("@")         # lib.so@W[:V]: that validator-table window / lane_votes
+    w, _, v = wv.partition(":")
     T._lib = None
     T.LIB_PATH = os.path.abspath(path)
-    ctx = T.Context(max_batch=2 * 1_000_000, max_txs=10_064, max_validators=100, table_w=int(w) if w else None)
+    ctx = T.Context(max_batch=2 * 1_000_000, max_txs=10_064, max_validators=100, table_w=int(w) if w else None,
+                    lane_votes=int(v) if v else 0)
     wl = Workload(ctx, 100, 10_000, SEEDS["c2"])
     ctx.stage(0, wl.batch)
     v, t = [], []
