@@ -110,7 +110,8 @@ TXV_HD void s30_add_p_if(s30& a, int32_t mask) {
   s30_carry(a);
 }
 
-TXV_HD fe fe_invert_var(const fe& z) {
+// batches_out (host tests): the 30-divstep batches run, or -1 if g had not reached 0 at the cap
+TXV_HD fe fe_invert_var_n(const fe& z, int& batches_out) {
   const fe c = fe_canon(z);
   s30 f, g, d, e;
 #pragma unroll
@@ -128,6 +129,7 @@ TXV_HD fe fe_invert_var(const fe& z) {
   int32_t t[4];
   // <= 25 batches for 255-bit inputs (Bernstein–Yang bound: 724 divsteps); the cap only
   // guarantees termination
+  batches_out = -1;
 #pragma unroll 1
   for (int it = 0; it < 32; ++it) {
     eta = divsteps30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
@@ -136,7 +138,7 @@ TXV_HD fe fe_invert_var(const fe& z) {
     int32_t any = 0;
 #pragma unroll
     for (int j = 0; j < 9; ++j) any |= g.v[j];
-    if (!any) break;
+    if (!any) { batches_out = it + 1; break; }
   }
   // f = +-1: z^-1 = d * f, brought from (-2p, p) into [0, p)
   const int32_t neg = f.v[8] >> 31;
@@ -156,6 +158,10 @@ TXV_HD fe fe_invert_var(const fe& z) {
   }
   while (k < 8) { out.v[k++] = (uint32_t)acc; acc >>= 32; }
   return out;
+}
+TXV_HD fe fe_invert_var(const fe& z) {
+  int batches;
+  return fe_invert_var_n(z, batches);
 }
 
 }  // namespace txv

@@ -2,16 +2,19 @@
 //
 //   txv_k_build_tables  (K0)  per validator: address = SHA-256(pub)[:20] (tendermint
 //                              PubKeyEd25519.Address, called at types/tx_vote.go:111),
-//                              ref10 decode of A, radix-16 fixed-base Niels table of A.
-//                              Also run once on the base point B.
-//   txv_k_verify        (K1)  per vote: x/crypto ed25519.Verify (types/tx_vote.go:115)
-//                              with the B table staged in LDS and the validator's A table
-//                              gathered from HBM (L2/MALL-resident for small validator sets).
+//                              ref10 decode of A, radix-2^W fixed-base half-Niels table of A
+//                              (128-byte fe10 entries, ge.h).  Also run once on the base point B.
+//   txv_k_challenge     (K1a) per vote: x/crypto ed25519.Verify's scalar checks and
+//                              k = SHA-512(R || A || SignBytes) mod L (types/tx_vote.go:115)
+//   txv_k_scalarmult_multi (K1b) V votes per lane: [s]B + [k](-A) over the tables, gathered
+//                              cooperatively into LDS (one line per 8 lanes), one shared
+//                              inversion, canonical encoding compared with R
 //   txv_k_keygen / txv_k_sign  load generator mirroring MockPV.SignTxVote
 //                              (types/priv_validator.go:83-95): RFC 8032 signing on device.
 //
-// Launch geometry: 256-thread workgroups (4 waves), grid-stride over votes so each
-// workgroup stages the 55 KB B table into LDS once per launch, not once per 256 votes.
+// Launch geometry: 512-thread workgroups; K1b walks an XCD-contiguous eighth of the work list
+// per group of blocks (blocks b, b+8, ... share an XCD) and runs at 2 waves/SIMD with V = 8
+// (1M-vote batches) or 4 waves/SIMD with V = 4.
 #include <cstdlib>
 
 #include "ed25519_dev.h"

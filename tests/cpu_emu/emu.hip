@@ -56,6 +56,24 @@ int emu_fe(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
   return 0;
 }
 
+// divstep inverse with its batch count (-1: g had not reached 0 within the 32-batch cap)
+int emu_inv_var(const uint32_t* a, uint32_t* out) {
+  fe x;
+  for (int j = 0; j < 8; ++j) x.v[j] = a[j];
+  int batches;
+  const fe r = fe_invert_var_n(x, batches);
+  for (int j = 0; j < 8; ++j) out[j] = r.v[j];
+  return batches;
+}
+// batch counts of n inputs (32-byte little-endian each), for the search in the test
+void emu_inv_var_counts(const uint32_t* a, int n, int32_t* counts) {
+  for (int i = 0; i < n; ++i) {
+    fe x;
+    for (int j = 0; j < 8; ++j) x.v[j] = a[8 * i + j];
+    fe_invert_var_n(x, counts[i]);
+  }
+}
+
 // fe10 primitives on raw limbs (op 0 mul, 1 add, 2 sub, 3 cneg, 4 carry, 5 strict, 6 from radix
 // 2^32 (8 words in), 7 to radix 2^32 (8 words out), 8 madd on (X,Y,Z,T) + entry words)
 int emu_fe10(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {

@@ -31,6 +31,8 @@ def emu():
     E.emu_fe10.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
     E.emu_ge10_madd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     E.emu_entry.argtypes = [ctypes.c_void_p] * 3
+    E.emu_inv_var.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    E.emu_inv_var_counts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     E.emu_wire_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return E
@@ -60,6 +62,46 @@ def test_field_and_scalar_ops(emu):
             assert (v % P if op < 6 else v) == exp, (op, hex(x), hex(y))
             if op in (4, 7):   # canonical outputs (7: variable-time divstep inverse, K1b)
                 assert v == exp
+
+
+def test_divstep_inverse_near_its_bound(emu):
+    """fe_invert_var (K1b's shared inversion) on inputs chosen to need many divsteps: structured
+    ones (powers of two, p - 2^k, all-ones patterns, Fibonacci-ratio values) and the worst of a
+    hill-climbing search over the batch count; every result equals pow(z, p - 2, p) and g reaches
+    0 well before the 32-batch cap (Bernstein-Yang: <= 724 divsteps = 25 batches for 255 bits)."""
+    import numpy as np
+    rnd = random.Random(17)
+    out = (ctypes.c_uint32 * 8)()
+    fib = [0, 1]
+    while len(fib) < 400:
+        fib.append(fib[-1] + fib[-2])
+    cands = [1, 2, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 2 ** 254, 2 ** 255 - 20]
+    cands += [2 ** k % P for k in range(0, 255, 7)] + [(P - 2 ** k) % P for k in range(1, 255, 11)]
+    cands += [int("10" * 127, 2), int("110" * 84, 2) % P, int("1" * 254, 2)]
+    cands += [fib[k] % P for k in range(300, 400, 5)] + [fib[k] * pow(fib[k + 1], P - 2, P) % P for k in range(50, 380, 30)]
+
+    def counts(xs):
+        arr = np.array([[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)] for x in xs], np.uint32)
+        c = np.zeros(len(xs), np.int32)
+        emu.emu_inv_var_counts(arr.ctypes.data, len(xs), c.ctypes.data)
+        return c
+
+    pool = [rnd.randrange(1, P) for _ in range(2000)]
+    c = counts(pool)
+    best = [pool[i] for i in np.argsort(-c)[:32]]
+    for _ in range(40):                      # mutate the worst inputs, keep the worse
+        kids = [(x ^ (1 << rnd.randrange(255))) % P or 1 for x in best for _ in range(8)]
+        kc = counts(kids)
+        allx = best + kids
+        allc = np.concatenate([counts(best), kc])
+        best = [allx[i] for i in np.argsort(-allc)[:32]]
+    worst = int(counts(best).max())
+    for z in cands + best:
+        n = emu.emu_inv_var(w(z), out)
+        assert 0 < n <= 25, (hex(z), n)
+        assert f(out) == pow(z, P - 2, P), hex(z)
+    assert emu.emu_inv_var(w(0), out) in (-1, 0, 1) and f(out) == 0
+    assert worst >= 19                        # random inputs: 17-19 batches (mean 18.1 over 20k)
 
 
 W10 = [26 if i % 2 == 0 else 25 for i in range(10)]
