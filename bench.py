@@ -339,7 +339,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
     ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
-    ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24),
+    ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24, 26),
                     help="base-point table window (0 = library default)")
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")

@@ -770,7 +770,7 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
   } else if (args->lane_votes == 4) {
     hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 4>), dim3(grid), dim3(B), 0, st, *args);
   } else if (args->lane_votes == 8) {
-    if constexpr (WB == 24) hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+    if constexpr (WB >= 24) hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
     else return hipErrorInvalidValue;
   } else if (args->lane_votes == 2 && WB == WA) {
     hipLaunchKernelGGL((txv_k_scalarmult_pair<B, WA>), dim3(grid), dim3(B), 0, st, *args);
@@ -796,16 +796,19 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
     case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 26: launch_build<26>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 // (wb, wa): base-point and validator windows; supported pairs are (w, w) for every table
-// window and the wide base tables wb in {20, 22, 24} over wa = 16
+// window, the radix-2^24 base table over wa = 12..20, the radix-2^26 one (43 GB: 10 positions
+// instead of 11) over wa = 16..20, and wb in {20, 22} over wa = 16
 bool txv_verify_windows_supported(int wb, int wa) {
   if (wb == wa) return wa == 4 || wa == 8 || wa == 10 || wa == 12 || wa == 14 || wa == 16;
   if (wb == 24) return wa == 12 || wa == 14 || wa == 16 || wa == 18 || wa == 20;
+  if (wb == 26) return wa == 16 || wa == 18 || wa == 20;
   return wa == 16 && (wb == 20 || wb == 22);
 }
 
@@ -832,6 +835,9 @@ hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t gr
       case 2416: e = launch_multi<B, 24, 16>(args, grid, st); break;
       case 2418: e = launch_multi<B, 24, 18>(args, grid, st); break;
       case 2420: e = launch_multi<B, 24, 20>(args, grid, st); break;
+      case 2616: e = launch_multi<B, 26, 16>(args, grid, st); break;
+      case 2618: e = launch_multi<B, 26, 18>(args, grid, st); break;
+      case 2620: e = launch_multi<B, 26, 20>(args, grid, st); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

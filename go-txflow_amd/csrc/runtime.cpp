@@ -480,11 +480,11 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
 // K1b votes per lane for a launch with base window wb.  V = 8 halves the inversions per vote
 // but also the waves; with the divstep inverse it wins once the batch still fills >= 1.5 waves
 // per SIMD (C2, 1M votes: 517 vs 503-512M votes/s, profiles/r01/inv_var, profiles/r01/park);
-// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 base table
-// only, so a configured V = 8 runs V = 4 on any other base table (e.g. when the 8.9 GB wide
-// table could not be allocated, or for caller-key tables).
+// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 / 2^26 base
+// tables only, so a configured V = 8 runs V = 4 on any other base table (e.g. when no wide
+// table could be allocated, or for caller-key tables).
 uint32_t launch_lane_votes(const txv_ctx* c, int wb, uint32_t n_work) {
-  if (wb != 24) return c->lane_votes == 8 ? 4u : c->lane_votes;
+  if (wb != 24 && wb != 26) return c->lane_votes == 8 ? 4u : c->lane_votes;
   return (c->lane_auto && n_work >= (3u << 18)) ? 8u : c->lane_votes;
 }
 
@@ -793,38 +793,41 @@ int choose_window(const txv_ctx* c, uint32_t n) {
 }
 
 // make tab_w = w current: its B table exists; then the verify kernel's base-point window
-// b_w: the requested one if the kernels support (b_w, w), else by default the 8.9 GB
-// radix-2^24 table over radix-2^16 validator tables (11 instead of 16 additions for [s]B;
-// measured 2.06 vs 2.23 ms per 1M-vote verify, W_B = 22: 2.11), falling back to b_w = w
-// when the wide table cannot be allocated.  d_btable = table of b_w.
+// b_w: the requested one if the kernels support (b_w, w), else by default the 11.8 GB radix-2^24
+// table over radix-2^12..2^20 validator tables (11 instead of 16..22 additions for [s]B).  The
+// 43 GB radix-2^26 table (10 positions) is selectable (TXV_CFG_SET_B_WINDOW(26)) but not the
+// default: measured 1.42-1.44 vs 1.44-1.46 ms per 1M-vote verify (one addition of 23 saved, paid
+// back in TLB reach), for 31 GB more HBM.  A wide table that cannot be allocated falls back to
+// radix-2^24, then to b_w = w.  d_btable = table of b_w.
 int select_window(txv_ctx* c, int w) {
   int r;
-  // radix-2^18 / 2^20 validator tables only run against the radix-2^24 base table
+  // radix-2^18 / 2^20 validator tables only run against the wide base tables
   if (w != 4 && w <= 16 && (r = build_base_table(c, w))) return r;
   c->tab_w = w;
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
   int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
   if ((c->lane_votes < 4 && c->lane_votes != 1) || !txv_verify_windows_supported(bw, w)) bw = w;
-  if (bw != w) {
-    if (c->btable_wide_w != bw) {
-      dfree(c->d_btable_wide);
-      c->btable_wide_w = 0;
-      if (hipMalloc((void**)&c->d_btable_wide, table_words(bw) * 4) != hipSuccess) {
-        (void)hipGetLastError();
-        c->d_btable_wide = nullptr;
-        return TXV_OK;                       // no room: stay at b_w = w
-      }
-      uint32_t* d_b = nullptr;
-      if ((r = dalloc(c, &d_b, 8))) return r;
-      const uint32_t bwords[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                                  0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-      HIP_TRY(c, hipMemcpyAsync(d_b, bwords, 32, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(c, txv_launch_build_tables(bw, d_b, 1, c->d_btable_wide, nullptr, nullptr, c->stream));
-      HIP_TRY(c, hipStreamSynchronize(c->stream));
-      dfree(d_b);
-      c->btable_wide_w = bw;
+  while (bw != w && c->btable_wide_w != bw) {
+    dfree(c->d_btable_wide);
+    c->btable_wide_w = 0;
+    if (hipMalloc((void**)&c->d_btable_wide, table_words(bw) * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      c->d_btable_wide = nullptr;
+      bw = (bw == 26 && txv_verify_windows_supported(24, w)) ? 24 : w;   // no room: a narrower table
+      continue;
     }
+    uint32_t* d_b = nullptr;
+    if ((r = dalloc(c, &d_b, 8))) return r;
+    const uint32_t bwords[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                                0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+    HIP_TRY(c, hipMemcpyAsync(d_b, bwords, 32, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, txv_launch_build_tables(bw, d_b, 1, c->d_btable_wide, nullptr, nullptr, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    dfree(d_b);
+    c->btable_wide_w = bw;
+  }
+  if (bw != w) {
     c->b_w = bw;
     c->d_btable = c->d_btable_wide;
   }
@@ -962,7 +965,8 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (TXV_CFG_LANE_VOTES(c->cfg.flags)) { c->lane_votes = TXV_CFG_LANE_VOTES(c->cfg.flags); c->lane_auto = false; }
   if (c->lane_votes != 1 && c->lane_votes != 2 && c->lane_votes != 4 && c->lane_votes != 8) { delete c; return TXV_EINVAL; }
   c->cfg_bw = (int)TXV_CFG_B_WINDOW(c->cfg.flags);
-  if (c->cfg_bw && c->cfg_bw != 4 && !valid_window(c->cfg_bw) && c->cfg_bw != 20 && c->cfg_bw != 22 && c->cfg_bw != 24) {
+  if (c->cfg_bw && c->cfg_bw != 4 && !valid_window(c->cfg_bw) && c->cfg_bw != 20 && c->cfg_bw != 22 && c->cfg_bw != 24 &&
+      c->cfg_bw != 26) {
     delete c;
     return TXV_EINVAL;
   }

@@ -121,14 +121,15 @@ typedef struct {
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19:
- * 2, 4 or 8 (8 needs the radix-2^24 base table), 1 = split (scalar-multiply kernel stores R',
- * a second kernel batch-inverts and encodes); 0 = auto: 8 when a launch's pending votes fill
- * >= 1.5 waves per SIMD (>= 768K) with the radix-2^24 base table, else 4 */
+ * 2, 4 or 8 (8 needs the radix-2^24 or 2^26 base table), 1 = split (scalar-multiply kernel
+ * stores R', a second kernel batch-inverts and encodes); 0 = auto: 8 when a launch's pending votes
+ * fill >= 1.5 waves per SIMD (>= 768K) with a wide base table, else 4 */
 #define TXV_CFG_LANE_VOTES(flags) (((flags) >> 16) & 0xFu)
 #define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
-/* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 8.9 GB, over radix-2^16
- * validator tables; else the validator window), or 20 / 22 / 24 with window-16 validator
- * tables (0.65 / 2.4 / 8.9 GB, 13 / 12 / 11 additions for [s]B), or equal to the window */
+/* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 11.8 GB, over radix-2^12..2^20
+ * validator tables; else the validator window); 24 over windows 12..20; 26 (43 GB, 10 additions
+ * for [s]B instead of 11) over windows 16..20; 20 / 22 over window 16 (0.9 / 3.2 GB, 13 / 12
+ * additions); or equal to the window */
 #define TXV_CFG_B_WINDOW(flags) (((flags) >> 20) & 0xFFu)
 #define TXV_CFG_SET_B_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 20)
 

@@ -265,10 +265,11 @@ def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
         ctx2.close()
 
 
-@pytest.mark.parametrize("table_w,base_w", [(16, 20), (16, 24), (12, 24), (14, 24), (18, 24), (20, 24)])
+@pytest.mark.parametrize("table_w,base_w", [(16, 20), (16, 24), (12, 24), (14, 24), (18, 24), (20, 24), (16, 26),
+                                            (18, 26), (20, 26)])
 def test_wide_base_table_parity(oracle_lib, table_w, base_w):
-    """Radix-2^20 / 2^24 base-point tables (0.65 / 8.9 GB) over radix-2^12..2^20 validator
-    tables: the same verdicts as the oracle on valid and corrupted votes."""
+    """Radix-2^20 / 2^24 / 2^26 base-point tables (0.9 / 11.8 / 43 GB) over radix-2^12..2^20
+    validator tables: the same verdicts as the oracle on valid and corrupted votes."""
     import txflow_amd as T
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16, table_w=table_w, base_w=base_w)
     try:
