@@ -315,16 +315,18 @@ def load_pmc(table_w: int, n_votes: int):
     PMC passes (profiles/pmc_verify.json), when they were taken on this kernel configuration"""
     pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
     if not os.path.exists(pmc):
-        return None, None, None
+        return None, None, None, None
     try:
         with open(pmc) as f:
             pj = json.load(f)
     except Exception:
-        return None, None, None
+        return None, None, None, None
     if pj.get("table_window") != table_w:
-        return None, None, None
-    traffic = pj.get("hbm_bytes_per_launch") if pj.get("votes_per_launch", n_votes) == n_votes else None
-    return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source")
+        return None, None, None, None
+    same = pj.get("votes_per_launch", n_votes) == n_votes
+    traffic = pj.get("hbm_bytes_per_launch") if same else None
+    tally = pj.get("tally_hbm_bytes_per_launch") if same else None
+    return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source"), tally
 
 
 def main():
@@ -476,7 +478,7 @@ def main():
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
         # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
         # (PMC SQ_INSTS_VALU pass of this build, profiles/pmc_verify.json) give exec_frac
-        w_exec, traffic, pmc_src = load_pmc(ctx.table_w, wl.n)
+        w_exec, traffic, pmc_src, tally_bytes = load_pmc(ctx.table_w, wl.n)
         achieved = wl.n * W_ALG / (v_ms * 1e-3)
         exec_rate = wl.n * w_exec / (v_ms * 1e-3) if w_exec else None
         threads = args.cpu_threads or host_cores()
@@ -518,6 +520,13 @@ def main():
                          "pmc_source": pmc_src,
                          "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"},
             "cpu_baseline": cpu,
+            # the tally chain after verify (HBM-bound per BASELINE.md): bytes per launch from the same
+            # PMC passes (2 x FETCH_SIZE + WRITE_SIZE of its kernels) over this run's tally time
+            "tally": {"ms": round(t_ms, 3), "hbm_bytes_per_launch": tally_bytes,
+                      "GBps": None if not tally_bytes else round(tally_bytes / (t_ms * 1e-3) / 1e9, 1),
+                      "frac_of_8TBps": None if not tally_bytes else round(tally_bytes / (t_ms * 1e-3) / 8e12, 3),
+                      "note": "includes the accepted-vote arena rows (128 B per ADDED vote) MakeCommit reads; "
+                              "BASELINE.md's 16 B/vote counts the cell update alone"},
         }
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = {

@@ -836,6 +836,10 @@ hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t s
   if (((uint64_t)b->n + kScanItems - 1) / kScanItems > 8192) return hipErrorInvalidValue;
   const uint32_t g = (b->n + 255) / 256;
   if (g) hipLaunchKernelGGL(txv_k_route, dim3(g), dim3(256), 0, st, *fs, *b);
+  return hipGetLastError();
+}
+
+hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
   return compact(NewSetPred{*fs, *b}, NewSetAct{*fs, *b}, b->n, b->blk, st);
 }
 

@@ -88,7 +88,9 @@ struct Slot {
   FlowSummary* h_sum = nullptr; FlowSummary* m_sum = nullptr;
   // 0 start, 1 routed (+ SignBytes), 2 verified, 3 the slot's uploads are done (copy stream),
   // 4 results are in host memory (compute stream), 5 tallied
-  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // 0 start, 1 route+SignBytes done, 2 verify done, 3 upload done, 4/5 tally done,
+  // 6 route done (side stream starts), 7 new set ids done (tally waits)
+  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t ticket = 0;    // txv_submit_votes ticket in flight on this slot (0 = none)
 };
 
@@ -101,6 +103,7 @@ struct txv_ctx {
   hipStream_t stream = nullptr;        // compute: verify + tally kernels, result copies
   hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
   hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest) runs beside in-flight batches
+  hipStream_t side_stream = nullptr;   // a batch's new-set-id compaction, beside SignBytes + verify
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   std::string err;
   std::mutex mu;
@@ -705,6 +708,16 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
   HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
+  // the new set ids need only the route's output: their compaction runs on the side stream
+  // while SignBytes and K1a/K1b run here (joined before the tally)
+#ifndef TXV_SIDE_STREAM
+#define TXV_SIDE_STREAM 1
+#endif
+  hipStream_t ids_stream = TXV_SIDE_STREAM ? c->side_stream : c->stream;
+  HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
+  HIP_TRY(c, hipStreamWaitEvent(ids_stream, s.ev[6], 0));
+  HIP_TRY(c, txv_flow_new_ids(&fs, &fb, ids_stream));
+  HIP_TRY(c, hipEventRecord(s.ev[7], ids_stream));
   SignBytesArgs sa{};
   sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
@@ -721,6 +734,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   // every batch run since (a bound for the touched-set scan)
   if (!s.counted) { c->unfetched += s.n; s.counted = true; }
   const uint32_t sets_bound = (uint32_t)std::min<uint64_t>((uint64_t)c->n_sets_host + c->unfetched, c->cfg.max_txs);
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[7], 0));
   HIP_TRY(c, txv_flow_tally(&fs, &fb, sets_bound, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[5], c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
@@ -981,7 +995,8 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   c->device = dev;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TXV_EDEVICE;
   }
@@ -1005,6 +1020,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   if (c->key_stream) (void)hipStreamSynchronize(c->key_stream);
+  if (c->side_stream) (void)hipStreamSynchronize(c->side_stream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
     dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_rpts); dfree(s.d_order); hfree(s.h_order);
@@ -1034,6 +1050,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->key_stream) (void)hipStreamDestroy(c->key_stream);
+  if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
   delete c;
 }
 

@@ -172,9 +172,13 @@ struct FlowBatch {
 
 extern "C" {
 // the whole AddVote chain of one batch except SignBytes and verify, split where the verify
-// kernels sit: route (pre-checks, set ids, signature transpose, SignBytes lengths) ...
+// kernels sit: route (pre-checks, set-table find-or-insert, signature transpose, SignBytes
+// lengths) ...
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st);
-// ... then, after K1a/K1b wrote b->ok: tally, commit events, statuses to the host
+// ... new set ids (first-seen compaction; independent of verify: may run on a second stream
+// beside SignBytes and K1a/K1b, joined before the tally) ...
+hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t st);
+// ... then, after K1a/K1b wrote b->ok and the new ids exist: tally, commit events, statuses
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st);
 // forget every TxVoteSet (keep_ids = 0) or empty them keeping their ids (keep_ids = 1)
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);

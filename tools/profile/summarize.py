@@ -28,7 +28,11 @@ def rows(path_glob):
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").strip()
+    name = name.replace("(anonymous namespace)::", "")
+    base = name.split("(")[0].replace("void ", "").strip()
+    if "Pred" in base:   # the scan kernels by predicate: txv_k_scan_apply<AddedPred, AddedAct> -> <AddedPred>
+        base = base.split(",")[0].rstrip(">") + ">"
+    return base
 
 
 def main():
@@ -83,6 +87,15 @@ def main():
     if pair and all("hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d for d in pair):
         res["hbm_bytes_per_launch"] = sum(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"] for d in pair)
         res["hbm_bytes_per_launch_raw_fetch"] = sum(d["hbm_read_bytes_raw"] + d["hbm_write_bytes"] for d in pair)
+    # the tally chain after verify (kernels_flow.hip): HBM bytes per launch from the same passes
+    tally_names = ("txv_k_tally_min", "txv_k_tally_resolve", "txv_k_tally_cross", "txv_k_status_out",
+                   "txv_k_scan_count<AddedPred>", "txv_k_scan_apply<AddedPred>", "txv_k_scan_count<TouchedPred>",
+                   "txv_k_scan_apply<TouchedPred>", "txv_k_scan_count<EventPred>", "txv_k_scan_apply<EventPred>")
+    tk = [res["kernels"][k] for k in tally_names if k in res["kernels"]]
+    if tk and all("hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d for d in tk):
+        res["tally_hbm_bytes_per_launch"] = sum(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"] for d in tk)
+        res["tally_kernel_ns_per_launch"] = sum(d.get("avg_ns", 0.0) for d in tk)
+        res["tally_kernels"] = [k for k in tally_names if k in res["kernels"]]
     txt = json.dumps(res, indent=1, sort_keys=True)
     if a.out:
         with open(a.out, "w") as f:
