@@ -43,13 +43,13 @@ TXV_HD ge10_ext ge10_madd(const ge10_ext& p, const fe10& qp, const fe10& qm, con
   const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
   const fe10 G = fe10_add(p.Z, C), F = fe10_sub(p.Z, C);
   ge10_ext r;
-  r.X = fe10_mul(E, F);
+  r.X = fe10_mul(F, E);
   TXV_SCHED_FENCE();
   r.Y = fe10_mul(H, G);
   TXV_SCHED_FENCE();
   r.Z = fe10_mul(F, G);
   TXV_SCHED_FENCE();
-  r.T = fe10_mul(E, H);
+  r.T = fe10_mul(H, E);
   TXV_SCHED_FENCE();
   return r;
 }
@@ -58,7 +58,8 @@ TXV_HD ge10_ext ge10_madd(const ge10_ext& p, const fe10& qp, const fe10& qm, con
 // rd(2) = qd, already swapped for -Q): only one of them is live at a time, which keeps the
 // prefetching K1b walk inside 128 VGPRs; mid() runs once all three are read (the walk issues its
 // next prefetch there, into the buffer just read)
-template <class Rd, class Mid>
+// kT = false: the last addition of a walk (its T is never read)
+template <bool kT = true, class Rd, class Mid>
 TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {
   const fe10 C = fe10_cneg(fe10_mul(p.T, rd(2)), neg);
   TXV_SCHED_FENCE();
@@ -69,15 +70,21 @@ TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {
   mid();
   const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
   const fe10 G = fe10_add(p.Z, C), F = fe10_sub(p.Z, C);
+  // E and G are the g operands (the ones fe10_mul multiplies by 19) of two products each, so
+  // their 19x limbs are computed once
   ge10_ext r;
-  r.X = fe10_mul(E, F);
+  r.X = fe10_mul(F, E);
   TXV_SCHED_FENCE();
   r.Y = fe10_mul(H, G);
   TXV_SCHED_FENCE();
   r.Z = fe10_mul(F, G);
   TXV_SCHED_FENCE();
-  r.T = fe10_mul(E, H);
-  TXV_SCHED_FENCE();
+  if (kT) {
+    r.T = fe10_mul(H, E);
+    TXV_SCHED_FENCE();
+  } else {
+    r.T = fe10_zero();
+  }
   return r;
 }
 

@@ -342,7 +342,7 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
   bool neg = issue(0), neg2 = false;
   if (PD == 2) neg2 = issue(1);
 #pragma unroll 1
-  for (int t = 0; t < nT; ++t) {
+  for (int t = 0; t < nT - 1; ++t) {
     // entry t has landed in LDS (with PD = 2 entry t + 1's 8 loads may stay in flight)
     if (PD == 2 && t + 1 < nT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -364,6 +364,12 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
       next();
       P = ge10_from_entry(qp, qm);
     }
+  }
+  {   // the last addition: nothing left to prefetch, and its T is never read
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint4* bt = buf + (PD == 2 ? ((nT - 1) & 1) * 512 : 0);
+    const bool neg_t = neg;
+    P = ge10_madd_rd<false>(P, [&](int role) { return entry_field_lds(bt, neg_t, role); }, neg_t, [] {});
   }
   ge_ext R;
   R.X = fe_from_fe10(P.X);
