@@ -89,7 +89,9 @@ __global__ void __launch_bounds__(256) txv_k_signbytes(SignBytesArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n_pad) return;
   WordSink w{a.msg + i, a.n_pad};
-  const uint32_t len = i < a.n ? a.msg_len[i] : 0u;
+  // with no length column (the TxFlow path, beside the route kernel) every non-nil vote is
+  // encoded; K1a reads the words only for votes the route kernel left pending
+  const uint32_t len = i >= a.n ? 0u : (a.msg_len ? a.msg_len[i] : (a.nil && a.nil[i] ? 0u : 1u));
   if (len) {
     const int64_t height = a.height[i];
     const int64_t sec = a.ts_sec[i];

@@ -89,8 +89,8 @@ struct Slot {
   // 0 start, 1 routed (+ SignBytes), 2 verified, 3 the slot's uploads are done (copy stream),
   // 4 results are in host memory (compute stream), 5 tallied
   // 0 start, 1 route+SignBytes done, 2 verify done, 3 upload done, 4/5 tally done,
-  // 6 route done (side stream starts), 7 new set ids done (tally waits)
-  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // 6 route done (side stream starts), 7 new set ids done (tally waits), 8 SignBytes done
+  hipEvent_t ev[9] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t ticket = 0;    // txv_submit_votes ticket in flight on this slot (0 = none)
 };
 
@@ -707,22 +707,27 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
-  HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
-  // the new set ids need only the route's output: their compaction runs on the side stream
-  // while SignBytes and K1a/K1b run here (joined before the tally)
+  // SignBytes needs only the uploaded columns: it runs on the side stream beside the route
+  // kernel; then the new set ids (they need the route's output) run there beside K1a/K1b, and
+  // the tally waits for them
 #ifndef TXV_SIDE_STREAM
 #define TXV_SIDE_STREAM 1
 #endif
-  hipStream_t ids_stream = TXV_SIDE_STREAM ? c->side_stream : c->stream;
-  HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
-  HIP_TRY(c, hipStreamWaitEvent(ids_stream, s.ev[6], 0));
-  HIP_TRY(c, txv_flow_new_ids(&fs, &fb, ids_stream));
-  HIP_TRY(c, hipEventRecord(s.ev[7], ids_stream));
+  hipStream_t side = TXV_SIDE_STREAM ? c->side_stream : c->stream;
   SignBytesArgs sa{};
   sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
-  sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = s.d_msg_len; sa.msg = s.d_msg;
-  HIP_TRY(c, txv_launch_signbytes(&sa, c->stream));
+  sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = nullptr; sa.nil = s.has_nil ? s.d_nil : nullptr;
+  sa.msg = s.d_msg;
+  HIP_TRY(c, hipStreamWaitEvent(side, s.ev[0], 0));
+  HIP_TRY(c, txv_launch_signbytes(&sa, side));
+  HIP_TRY(c, hipEventRecord(s.ev[8], side));
+  HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
+  HIP_TRY(c, hipStreamWaitEvent(side, s.ev[6], 0));
+  HIP_TRY(c, txv_flow_new_ids(&fs, &fb, side));
+  HIP_TRY(c, hipEventRecord(s.ev[7], side));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[8], 0));
   HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
   va.order = nullptr;          // arrival order; K1a marks the non-pending votes

@@ -54,7 +54,8 @@ struct SignBytesArgs {
   const uint32_t* txhash_len;  // [n]
   const uint8_t* txhash;       // TxHash arena
   const uint8_t* chain;        // [chain_len]
-  const uint32_t* msg_len;     // [n] SignBytes length, 0 = none (nil / amino error)
+  const uint32_t* msg_len;     // [n] SignBytes length, 0 = none (nil / amino error); or null:
+  const uint8_t* nil;          // then every vote but the nil ones ([n] or null) is encoded
   uint64_t* msg;               // [msg_words][n_pad] out
 };
 
