@@ -11,7 +11,9 @@ One step = one pass of the hot path over the batch, inputs resident in HBM: a fr
 TxVoteSets (device hash table, first-seen ids), validator lookup and pre-checks, SignBytes,
 K1a/K1b verify, the first-accepted resolution, stake sums and 2/3 crossings -- and the per-vote
 statuses + commit events in host memory; at N>1 also the packed per-shard commit state
-all-gathered over RCCL.  value = votes processed by all ranks / max-over-ranks time.
+all-gathered over RCCL.  Steps run two in flight (slots 0 and 1 hold the same staged batch):
+step k+1's verify chain runs while step k's TxFlow chain tallies, as consecutive batches of a
+node do.  value = votes processed by all ranks / max-over-ranks time.
 
 Beside it: the end-to-end rate from the caller's host SoA columns (txv_submit_votes /
 txv_wait_votes, two batches in flight: staging copy + PCIe upload + kernels + results), the
@@ -383,48 +385,71 @@ def main():
     numa = ctx.bind_host_numa()     # host threads + pinned buffers next to this GPU's PCIe root
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
+    # the same batch in both device slots: step k runs in slot k % 2, so step k+1's verify chain
+    # overlaps step k's tally (txv_run_staged returns as soon as the chain is enqueued)
     ctx.stage(0, wl.batch)
+    ctx.stage(1, wl.batch)
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
         f"staged in {time.perf_counter() - t_setup:.1f}s")
 
     # per-shard commit state all-gathered every step: [n_sets][bitmap][sums] packed by
-    # txv_pack_commit_state into one device buffer -> one RCCL all-gather over xGMI
+    # the device at the end of each step's chain (txv_set_commit_sink, one buffer per slot) -> one
+    # RCCL all-gather over xGMI per step
     state = gathered = None
     n_cap = max_txs
     if dist is not None:
         import torch
         words = T.commit_state_bytes(n_cap) // 4
-        state = torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}")
+        state = [torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}") for _ in range(2)]
+        for sl in range(2):
+            ctx.set_commit_sink(sl, state[sl].data_ptr(), n_cap)
         gathered = torch.zeros(world * words, dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
     red_dev = "cpu" if gloo else f"cuda:{local}"
 
-    def all_gather_state():
-        ctx.pack_commit_state(state.data_ptr(), n_cap)
+    def all_gather_state(sl: int):
         if gloo:
-            torch.cuda.synchronize()
-            dist.all_gather(list(gathered.chunk(world)), state.cpu())
+            dist.all_gather(list(gathered.chunk(world)), state[sl].cpu())
         else:
-            dist.all_gather_into_tensor(gathered, state)
+            dist.all_gather_into_tensor(gathered, state[sl])
             torch.cuda.synchronize()
 
     step_ms, route_ms, verify_ms, tally_ms = [], [], [], []
-    st_buf = np.zeros(wl.n, np.uint8)          # result buffers reused every step
-    ev_buf = np.zeros(wl.n_txs + 1, T.EVENT_DTYPE)
+    st_buf = [np.zeros(wl.n, np.uint8) for _ in range(2)]          # result buffers reused every step
+    ev_buf = [np.zeros(wl.n_txs + 1, T.EVENT_DTYPE) for _ in range(2)]
+    t_launch = {}
 
-    def step(record: bool):
-        t0 = time.perf_counter()
+    def launch(k: int):
+        """enqueue step k: a fresh TxFlow (in stream order after step k-1's tally) + the chain"""
+        t_launch[k] = time.perf_counter()
         ctx.reset_flow()
-        ms = ctx.run_staged(0, timed=record)
-        st, ev = ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf, evs=ev_buf)
+        ctx.run_staged(k % 2)
+
+    def finish(k: int, record: bool):
+        sl = k % 2
+        st, ev = ctx.fetch_staged(sl, wl.n, ev_cap=wl.n_txs + 1, out=st_buf[sl], evs=ev_buf[sl])
         if dist is not None:
-            all_gather_state()
+            all_gather_state(sl)
         if record:
-            step_ms.append((time.perf_counter() - t0) * 1e3)
+            step_ms.append((time.perf_counter() - t_launch[k]) * 1e3)
+            ms = ctx.slot_kernel_ms(sl)
             route_ms.append(ms[0]); verify_ms.append(ms[1]); tally_ms.append(ms[2])
         return st, ev
 
-    for _ in range(args.warmup):
-        st, ev = step(False)
+    def run_steps(m: int, record: bool):
+        """m steps, two in flight: launch k+1 before waiting for k"""
+        out = None
+        if m <= 0:
+            return out
+        launch(0)
+        for k in range(1, m):
+            launch(k)
+            out = finish(k - 1, record)
+        return finish(m - 1, record)
+
+    def step(record: bool):
+        return run_steps(1, record)
+
+    run_steps(args.warmup, False)
     # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once,
     # with exactly n_vals - quorum + 1 fired votes per tx
     st, ev = step(False)
@@ -455,8 +480,7 @@ def main():
         torch.cuda.synchronize()
     ctx.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run_steps(args.steps, True)
     ctx.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -506,7 +530,8 @@ def main():
                        "votes_per_gpu": wl.n, "txs_per_gpu": wl.n_txs, "parallelism": f"shard{world}",
                        "host_numa_bound": numa,
                        "step": "reset_flow + device TxHash routing/pre-checks/SignBytes + verify + tally + "
-                               "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "")},
+                               "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "") +
+                               "; two steps in flight (step k+1's verify overlaps step k's tally)"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
             "device_ms_p50": {"route": round(r_ms, 3), "verify": round(v_ms, 3), "tally": round(t_ms, 3)},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),

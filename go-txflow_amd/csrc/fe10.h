@@ -155,6 +155,97 @@ TXV_HD fe10 fe10_mul(const fe10& f, const fe10& g) {
   return h;
 }
 
+// Two independent products with their column chains interleaved.  fe10_mul is ONE dependency
+// chain of 100 v_mad_u64_u32 (each column's carry is the next column's first addend), and a wave
+// issues it with nothing else to fill the mad's latency; two products in one asm block per column
+// (the mads of both chains alternating) give every mad an independent neighbour, at no extra
+// instruction (unlike splitting one column into two chains, which costs a 64-bit add per column).
+TXV_HD void fe10_col2(uint64_t c1, const uint32_t a[10], const uint32_t b[10], uint64_t c2, const uint32_t x[10],
+                      const uint32_t y[10], uint64_t& o1, uint64_t& o2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t p, q, cc;
+  asm("v_mad_u64_u32 %0, %2, %3, %13, %43\n\t"
+      "v_mad_u64_u32 %1, %2, %23, %33, %44\n\t"
+      "v_mad_u64_u32 %0, %2, %4, %14, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %24, %34, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %5, %15, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %25, %35, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %16, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %26, %36, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %7, %17, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %27, %37, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %8, %18, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %28, %38, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %9, %19, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %29, %39, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %10, %20, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %30, %40, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %11, %21, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %31, %41, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %12, %22, %0\n\t"
+      "v_mad_u64_u32 %1, %2, %32, %42, %1"
+      : "=&v"(p), "=&v"(q), "=&s"(cc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]),
+        "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(b[8]), "v"(b[9]),
+        "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]), "v"(x[9]),
+        "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]), "v"(y[6]), "v"(y[7]), "v"(y[8]), "v"(y[9]),
+        "v"(c1), "v"(c2));
+  o1 = p;
+  o2 = q;
+#else
+  uint64_t p = c1, q = c2;
+  for (int i = 0; i < 10; ++i) {
+    p += (uint64_t)a[i] * b[i];
+    q += (uint64_t)x[i] * y[i];
+  }
+  o1 = p;
+  o2 = q;
+#endif
+}
+
+// h1 = f1 * g1, h2 = f2 * g2 (mod p), carried: fe10_mul twice, same bounds, columns interleaved
+TXV_HD void fe10_mul2(const fe10& f1, const fe10& g1, const fe10& f2, const fe10& g2, fe10& h1, fe10& h2) {
+  uint32_t g19a[10], f2a[10], g19b[10], f2b[10];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) {
+    g19a[j] = 19u * g1.v[j];
+    g19b[j] = 19u * g2.v[j];
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    f2a[i] = (i & 1) ? f1.v[i] + f1.v[i] : f1.v[i];
+    f2b[i] = (i & 1) ? f2.v[i] + f2.v[i] : f2.v[i];
+  }
+  g19a[0] = g19b[0] = 0;
+  fe10 r1, r2;
+  uint64_t acc1 = 0, acc2 = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint32_t a[10], b[10], x[10], y[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const bool dbl = (i & 1) && !(k & 1);
+      a[i] = dbl ? f2a[i] : f1.v[i];
+      x[i] = dbl ? f2b[i] : f2.v[i];
+      b[i] = i <= k ? g1.v[k - i] : g19a[k + 10 - i];
+      y[i] = i <= k ? g2.v[k - i] : g19b[k + 10 - i];
+    }
+    fe10_col2(acc1, a, b, acc2, x, y, acc1, acc2);
+    r1.v[k] = (uint32_t)acc1 & TXV_M10(k);
+    r2.v[k] = (uint32_t)acc2 & TXV_M10(k);
+    acc1 >>= TXV_W10(k);
+    acc2 >>= TXV_W10(k);
+  }
+  const uint64_t t1 = (uint64_t)(uint32_t)acc1 * 19u + r1.v[0] + ((uint64_t)((uint32_t)(acc1 >> 32) * 19u) << 32);
+  const uint64_t t2 = (uint64_t)(uint32_t)acc2 * 19u + r2.v[0] + ((uint64_t)((uint32_t)(acc2 >> 32) * 19u) << 32);
+  r1.v[0] = (uint32_t)t1 & 0x3ffffffu;
+  r1.v[1] += (uint32_t)(t1 >> 26);
+  r2.v[0] = (uint32_t)t2 & 0x3ffffffu;
+  r2.v[1] += (uint32_t)(t2 >> 26);
+  h1 = r1;
+  h2 = r2;
+}
+
 // fully carried: every limb < 2^w(i), value < 2^255 (+ the value itself may still be >= p)
 TXV_HD fe10 fe10_strict(const fe10& a) {
   fe10 r = fe10_carry(a);

@@ -59,8 +59,35 @@ TXV_HD ge10_ext ge10_madd(const ge10_ext& p, const fe10& qp, const fe10& qm, con
 // prefetching K1b walk inside 128 VGPRs; mid() runs once all three are read (the walk issues its
 // next prefetch there, into the buffer just read)
 // kT = false: the last addition of a walk (its T is never read)
+#ifndef TXV_MUL_PAIRS
+#define TXV_MUL_PAIRS 1
+#endif
 template <bool kT = true, class Rd, class Mid>
 TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {
+#if TXV_MUL_PAIRS
+  // the 7 products as 3 interleaved pairs + 1 (fe10_mul2): (C, A), B, (X3, Y3), (Z3, T3)
+  fe10 Cm, A;
+  fe10_mul2(p.T, rd(2), fe10_sub(p.Y, p.X), rd(1), Cm, A);
+  const fe10 C = fe10_cneg(Cm, neg);
+  TXV_SCHED_FENCE();
+  const fe10 B = fe10_mul(fe10_add(p.Y, p.X), rd(0));
+  TXV_SCHED_FENCE();
+  mid();
+  const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
+  const fe10 G = fe10_add(p.Z, C), F = fe10_sub(p.Z, C);
+  ge10_ext r;
+  fe10_mul2(F, E, H, G, r.X, r.Y);
+  TXV_SCHED_FENCE();
+  if (kT) {
+    fe10_mul2(F, G, H, E, r.Z, r.T);
+    TXV_SCHED_FENCE();
+  } else {
+    r.Z = fe10_mul(F, G);
+    TXV_SCHED_FENCE();
+    r.T = fe10_zero();
+  }
+  return r;
+#else
   const fe10 C = fe10_cneg(fe10_mul(p.T, rd(2)), neg);
   TXV_SCHED_FENCE();
   const fe10 A = fe10_mul(fe10_sub(p.Y, p.X), rd(1));
@@ -86,6 +113,7 @@ TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {
     r.T = fe10_zero();
   }
   return r;
+#endif
 }
 
 // the entry's own point (Z = 1): x = qp - qm, y = qp + qm, T = x y

@@ -14,10 +14,11 @@
 //   txflow/service.go:215-216   commit side effects on every ADDED vote of a set with maj23
 //
 // The batch form (one launch chain per batch, everything keyed on the device):
-//   route    one lane per vote: validator lookup (address hash table), pre-checks, SignBytes
-//            length / amino time check, signature transpose into the column-major layout the
-//            verify kernels read, and find-or-insert of the TxHash into the set table; a key
-//            seen for the first time records the smallest arrival index that carries it
+//   prep     one lane per vote (verify stream): validator lookup (address hash table),
+//            pre-checks, SignBytes length / amino time check, signature transpose into the
+//            column-major layout the verify kernels read
+//   key      one lane per vote (flow stream): find-or-insert of the TxHash into the set table;
+//            a key seen for the first time records the smallest arrival index that carries it
 //   new ids  a stream compaction over the arrival order of "first occurrence of a new key"
 //            numbers the new sets exactly as the sequential loop would (first-seen order)
 //   set ids  every vote reads its set id; the (set, validator) cells of pending votes are
@@ -245,7 +246,13 @@ __device__ __forceinline__ uint32_t find_validator(const FlowState& fs, const ui
 }
 
 // ------------------------------------------------------------------ route
-__global__ void __launch_bounds__(256) txv_k_route(FlowState fs, FlowBatch b) {
+// Two kernels, so that the verify kernels never wait for the TxFlow state:
+//   prep  (verify stream) everything a vote's verification needs and nothing keyed by the
+//         TxFlow: signature transpose, nil / empty-address / unknown-validator pre-checks,
+//         validator lookup, SignBytes length and amino time check
+//   key   (flow stream, in batch order after the previous batch's tally) TxHash find-or-insert
+//         into the set table
+__global__ void __launch_bounds__(256) txv_k_route_prep(FlowState fs, FlowBatch b) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n) return;
   b.ev_flag[i] = 0;
@@ -267,21 +274,9 @@ __global__ void __launch_bounds__(256) txv_k_route(FlowState fs, FlowBatch b) {
       }
     }
   }
-  if (b.nil && b.nil[i]) {   // nil *TxVote: no set is created (AddVote's first check)
-    b.pre[i] = TXV_S_NIL; b.flags[i] = 0; b.entry[i] = TXV_NONE; b.msg_len[i] = 0; b.val[i] = 0;
+  if (b.nil && b.nil[i]) {   // nil *TxVote: AddVote's first check
+    b.pre[i] = TXV_S_NIL; b.flags[i] = 0; b.msg_len[i] = 0; b.val[i] = 0;
     return;
-  }
-  // TxVoteSets[vote.TxHash], created on first sight (txflow/service.go:200-209)
-  const uint32_t len = b.th_len[i];
-  const uint32_t off = b.th_off[i];
-  const uint8_t* kp = b.th + off;
-  KeyRegs kr;
-  if (len <= kKeyRegBytes) {
-    load_key(kp, len, kr);
-    b.entry[i] = set_find_or_insert<true>(fs, b, hash_regs(kr, len, fs.hash_seed), kp, kr, len, off, i);
-  } else {
-    const uint64_t h = txv_hash::hash_chunks(len, fs.hash_seed, [&](uint32_t k) { return ld64u(kp + k); });
-    b.entry[i] = set_find_or_insert<false>(fs, b, h, kp, kr, len, off, i);
   }
   // AddVote pre-checks (types/vote_set.go:93-106)
   const uint32_t al = b.addr_len[i];
@@ -297,12 +292,33 @@ __global__ void __launch_bounds__(256) txv_k_route(FlowState fs, FlowBatch b) {
   } else {
     pre = TXV_S_UNKNOWN_VALIDATOR;
   }
-  const int L = signbytes_len(b.height[i], len, b.ts_sec[i], b.ts_nanos[i], b.chain_len);
+  const int L = signbytes_len(b.height[i], b.th_len[i], b.ts_sec[i], b.ts_nanos[i], b.chain_len);
   b.pre[i] = pre;
   b.val[i] = v == TXV_NONE ? 0u : v;
   b.msg_len[i] = (pre == TXV_S_PENDING && L > 0) ? (uint32_t)L : 0u;
   b.flags[i] = pre != TXV_S_PENDING ? 0
                : (uint8_t)(TXV_FLAG_PENDING | (b.sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (L < 0 ? TXV_FLAG_BADMSG : 0));
+}
+
+// TxVoteSets[vote.TxHash], created on first sight for every non-nil vote (txflow/service.go:200-209)
+__global__ void __launch_bounds__(256) txv_k_route_key(FlowState fs, FlowBatch b) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= b.n) return;
+  if (b.nil && b.nil[i]) {
+    b.entry[i] = TXV_NONE;
+    return;
+  }
+  const uint32_t len = b.th_len[i];
+  const uint32_t off = b.th_off[i];
+  const uint8_t* kp = b.th + off;
+  KeyRegs kr;
+  if (len <= kKeyRegBytes) {
+    load_key(kp, len, kr);
+    b.entry[i] = set_find_or_insert<true>(fs, b, hash_regs(kr, len, fs.hash_seed), kp, kr, len, off, i);
+  } else {
+    const uint64_t h = txv_hash::hash_chunks(len, fs.hash_seed, [&](uint32_t k) { return ld64u(kp + k); });
+    b.entry[i] = set_find_or_insert<false>(fs, b, h, kp, kr, len, off, i);
+  }
 }
 
 // ------------------------------------------------------------------ block scan helpers
@@ -342,39 +358,23 @@ __global__ void __launch_bounds__(256) txv_k_scan_count(Pred p, uint32_t n, uint
   if (threadIdx.x == 0) blk[blockIdx.x] = total;
 }
 
-// exclusive offsets of nb block counts (nb <= 8192), blk[nb] = total
-__global__ void __launch_bounds__(1024) txv_k_scan_top(uint32_t* blk, uint32_t nb) {
-  __shared__ uint32_t wsum[16];
+// exclusive offsets of nb block counts (nb <= 8192), blk[nb] = total.  One 256-thread block
+// (4 waves): it runs beside K1b of the next batch, whose waves leave room for one wave per SIMD
+// but not for the 16 waves of a 1024-thread block (which then waited for K1b to drain).
+__global__ void __launch_bounds__(256) txv_k_scan_top(uint32_t* blk, uint32_t nb) {
   const uint32_t t = threadIdx.x;
-  uint32_t v[8], s = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t j = t * 8 + k;
-    v[k] = j < nb ? blk[j] : 0u;
-    s += v[k];
+  const uint32_t per = (nb + 255) / 256;          // consecutive counts per thread (<= 32)
+  const uint32_t lo = min(t * per, nb), hi = min(lo + per, nb);
+  uint32_t s = 0;
+  for (uint32_t j = lo; j < hi; ++j) s += blk[j];
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, &total);
+  for (uint32_t j = lo; j < hi; ++j) {
+    const uint32_t v = blk[j];
+    blk[j] = run;
+    run += v;
   }
-  const int lane = t & 63, w = t >> 6;
-  uint32_t x = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  uint32_t before = 0, all = 0;
-  for (int k = 0; k < 16; ++k) {
-    if (k < w) before += wsum[k];
-    all += wsum[k];
-  }
-  uint32_t run = before + x - s;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t j = t * 8 + k;
-    if (j < nb) blk[j] = run;
-    run += v[k];
-  }
-  if (t == 0) blk[nb] = all;
+  if (t == 0) blk[nb] = total;
 }
 
 template <class Pred, class Act>
@@ -823,7 +823,7 @@ template <class Pred, class Act>
 hipError_t compact(Pred p, Act act, uint32_t n, uint32_t* blk, hipStream_t st) {
   const uint32_t nb = (n + kScanItems - 1) / kScanItems;
   if (nb) hipLaunchKernelGGL((txv_k_scan_count<Pred>), dim3(nb), dim3(256), 0, st, p, n, blk);
-  hipLaunchKernelGGL(txv_k_scan_top, dim3(1), dim3(1024), 0, st, blk, nb);
+  hipLaunchKernelGGL(txv_k_scan_top, dim3(1), dim3(256), 0, st, blk, nb);
   if (nb) hipLaunchKernelGGL((txv_k_scan_apply<Pred, Act>), dim3(nb), dim3(256), 0, st, p, act, n, blk);
   return hipGetLastError();
 }
@@ -832,10 +832,17 @@ hipError_t compact(Pred p, Act act, uint32_t n, uint32_t* blk, hipStream_t st) {
 
 extern "C" {
 
+hipError_t txv_flow_prep(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
+  if (((uint64_t)b->n + kScanItems - 1) / kScanItems > 8192) return hipErrorInvalidValue;
+  const uint32_t g = (b->n + 255) / 256;
+  if (g) hipLaunchKernelGGL(txv_k_route_prep, dim3(g), dim3(256), 0, st, *fs, *b);
+  return hipGetLastError();
+}
+
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
   if (((uint64_t)b->n + kScanItems - 1) / kScanItems > 8192) return hipErrorInvalidValue;
   const uint32_t g = (b->n + 255) / 256;
-  if (g) hipLaunchKernelGGL(txv_k_route, dim3(g), dim3(256), 0, st, *fs, *b);
+  if (g) hipLaunchKernelGGL(txv_k_route_key, dim3(g), dim3(256), 0, st, *fs, *b);
   return hipGetLastError();
 }
 

@@ -391,9 +391,13 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
 #define TXV_PARK_LAST 1
 #endif
 // V = 8 is launched for batches that give 2 waves per SIMD (launch_lane_votes), so its register
-// budget is 256 VGPRs (2 waves/SIMD); V = 4 keeps 128 (4 waves/SIMD)
+// budget is 256 VGPRs (2 waves/SIMD); V = 4 keeps 128 (4 waves/SIMD) unless TXV_V4_WAVES says
+// otherwise
+#ifndef TXV_V4_WAVES
+#define TXV_V4_WAVES 4
+#endif
 template <int BLOCK, int WB, int WA, int V>
-__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : 2 * BLOCK / 256) txv_k_scalarmult_multi(VerifyArgs a) {
+__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) txv_k_scalarmult_multi(VerifyArgs a) {
   // lane group g = 64 w + l takes the work-list entries 64 V w + 64 h + l (h < V): the lanes of
   // a wave read 64 consecutive entries per vote slot, so the vote-column reads (sig, kbuf) of an
   // arrival-ordered list are two lines per column per wave

@@ -86,11 +86,13 @@ struct Slot {
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
   FlowSummary* h_sum = nullptr; FlowSummary* m_sum = nullptr;
-  // 0 start, 1 routed (+ SignBytes), 2 verified, 3 the slot's uploads are done (copy stream),
-  // 4 results are in host memory (compute stream), 5 tallied
-  // 0 start, 1 route+SignBytes done, 2 verify done, 3 upload done, 4/5 tally done,
-  // 6 route done (side stream starts), 7 new set ids done (tally waits), 8 SignBytes done
+  // copy stream: 3 upload done, 0 prep start, 1 prep + SignBytes done; verify stream: 7 K1a
+  // start, 2 verify done; flow stream: 4 results in host memory (+ commit sink), 5 tallied,
+  // 6 set keying done; 8 unused
   hipEvent_t ev[9] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool launched = false;           // a chain was enqueued on this slot (its ev[4] marks the end)
+  uint32_t* sink = nullptr;        // txv_set_commit_sink: packed commit state after each batch of this slot
+  uint32_t sink_cap = 0;
   uint64_t ticket = 0;    // txv_submit_votes ticket in flight on this slot (0 = none)
 };
 
@@ -100,10 +102,10 @@ struct txv_ctx {
   txv_config cfg{};
   int device = 0;
   int n_cus = 256;
-  hipStream_t stream = nullptr;        // compute: verify + tally kernels, result copies
+  hipStream_t stream = nullptr;        // flow: TxFlow keying + tally kernels, resets, readers (batch order)
+  hipStream_t vstream = nullptr;       // verify: prep + K1a/K1b (batch k+1 verifies while batch k tallies)
   hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
   hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest) runs beside in-flight batches
-  hipStream_t side_stream = nullptr;   // a batch's new-set-id compaction, beside SignBytes + verify
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   std::string err;
   std::mutex mu;
@@ -630,6 +632,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   add(v->sig_len, s.h_sig_len, s.d_sig_len, 4);
   add(v->is_nil, s.h_nil, s.d_nil, 1);
   add(v->txkey, s.h_txkey, s.d_txkey, 32);
+  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));   // its last chain has ended
   for (int k = 0; k < nc; ++k)
     if (cols[k].reg && n) HIP_TRY(c, hipMemcpyAsync(cols[k].dev, cols[k].src, (size_t)n * cols[k].elem, hipMemcpyHostToDevice, c->copy_stream));
   // TxHash arena (+ 16 zero bytes: the device reads keys 8 bytes at a time)
@@ -689,8 +692,18 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   return b;
 }
 
-// the whole AddVote chain of a staged batch on the compute stream: route (keying, pre-checks,
-// set ids) -> SignBytes -> K1a/K1b verify -> tally -> results into mapped host memory
+// device times of a slot's last run (its events have completed): prep (+ SignBytes), verify,
+// tally after verify, and the whole chain from the prep's start
+int slot_kernel_ms(txv_ctx* c, Slot& s, float* ms) {
+  HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
+  HIP_TRY(c, hipEventElapsedTime(&ms[1], s.ev[7], s.ev[2]));
+  HIP_TRY(c, hipEventElapsedTime(&ms[2], s.ev[2], s.ev[5]));
+  HIP_TRY(c, hipEventElapsedTime(&ms[3], s.ev[0], s.ev[5]));
+  return TXV_OK;
+}
+
+// the whole AddVote chain of a staged batch: prep + SignBytes -> K1a/K1b verify (verify
+// stream), set keying -> new ids -> tally -> results into mapped host memory (flow stream)
 int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   Slot& s = c->slots[slot];
   if (!s.staged) { c->err = "slot not staged"; return TXV_ESTATE; }
@@ -703,53 +716,56 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
     c->stamp = 0;
   }
   s.stamp = ++c->stamp;            // every run of a batch gets a stamp of its own
-  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
-  HIP_TRY(c, hipEventRecord(s.ev[0], c->stream));
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
-  // SignBytes needs only the uploaded columns: it runs on the side stream beside the route
-  // kernel; then the new set ids (they need the route's output) run there beside K1a/K1b, and
-  // the tally waits for them
-#ifndef TXV_SIDE_STREAM
-#define TXV_SIDE_STREAM 1
-#endif
-  hipStream_t side = TXV_SIDE_STREAM ? c->side_stream : c->stream;
+  // Three queues, so that batch k+1 verifies while batch k tallies and nothing but K1a/K1b sits
+  // on the verify stream:
+  //   copy stream  the uploads (stage_add), then prep (pre-checks, validator lookup, signature
+  //                transpose) and SignBytes: they read only the uploaded columns and run beside
+  //                the previous batch's K1b
+  //   vstream      K1a/K1b: reads nothing the TxFlow owns, so it never waits for an earlier
+  //                batch's tally
+  //   flow stream  set keying + new set ids, then -- after this batch's verify -- the tally:
+  //                every TxFlow access stays in batch order on this one stream
+  // (GPU_MAX_HW_QUEUES = 4: context, copy, key and verify streams each get a hardware queue; a
+  // further compute stream would share, i.e. serialise with, one of them)
+  // the slot's previous chain (its tally reads the derived columns prep rewrites) has ended
+  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
+  HIP_TRY(c, hipEventRecord(s.ev[0], c->copy_stream));
   SignBytesArgs sa{};
   sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
   sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = nullptr; sa.nil = s.has_nil ? s.d_nil : nullptr;
   sa.msg = s.d_msg;
-  HIP_TRY(c, hipStreamWaitEvent(side, s.ev[0], 0));
-  HIP_TRY(c, txv_launch_signbytes(&sa, side));
-  HIP_TRY(c, hipEventRecord(s.ev[8], side));
-  HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
-  HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
-  HIP_TRY(c, hipStreamWaitEvent(side, s.ev[6], 0));
-  HIP_TRY(c, txv_flow_new_ids(&fs, &fb, side));
-  HIP_TRY(c, hipEventRecord(s.ev[7], side));
-  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[8], 0));
-  HIP_TRY(c, hipEventRecord(s.ev[1], c->stream));
+  HIP_TRY(c, txv_flow_prep(&fs, &fb, c->copy_stream));
+  HIP_TRY(c, txv_launch_signbytes(&sa, c->copy_stream));
+  HIP_TRY(c, hipEventRecord(s.ev[1], c->copy_stream));
+  HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
+  HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
   va.order = nullptr;          // arrival order; K1a marks the non-pending votes
   va.n_work = s.n;
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
-  HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->stream));
-  HIP_TRY(c, hipEventRecord(s.ev[2], c->stream));
+  HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
+  HIP_TRY(c, hipEventRecord(s.ev[2], c->vstream));
+  HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
+  HIP_TRY(c, txv_flow_new_ids(&fs, &fb, c->stream));
+  HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
   // set ids in use after this batch: at most those known at the last fetch + one per vote of
   // every batch run since (a bound for the touched-set scan)
   if (!s.counted) { c->unfetched += s.n; s.counted = true; }
   const uint32_t sets_bound = (uint32_t)std::min<uint64_t>((uint64_t)c->n_sets_host + c->unfetched, c->cfg.max_txs);
-  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[7], 0));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[2], 0));
   HIP_TRY(c, txv_flow_tally(&fs, &fb, sets_bound, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[5], c->stream));
+  if (s.sink) HIP_TRY(c, txv_flow_pack(&fs, s.sink, (s.sink_cap + 31) / 32, s.sink_cap, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
   s.ran = true;
+  s.launched = true;
   if (ms) {
-    HIP_TRY(c, hipEventSynchronize(s.ev[5]));
-    HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
-    HIP_TRY(c, hipEventElapsedTime(&ms[1], s.ev[1], s.ev[2]));
-    HIP_TRY(c, hipEventElapsedTime(&ms[2], s.ev[2], s.ev[5]));
-    HIP_TRY(c, hipEventElapsedTime(&ms[3], s.ev[0], s.ev[5]));
+    HIP_TRY(c, hipEventSynchronize(s.ev[4]));
+    if ((r = slot_kernel_ms(c, s, ms))) return r;
   }
   return TXV_OK;
 }
@@ -916,16 +932,16 @@ int prepare_keys(txv_ctx* c, const uint8_t* pubs32, uint32_t n, std::vector<uint
 int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) {
   int r;
   if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
-  HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
+  HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[3], 0));
   VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables, ks.w);
   const bool reg_w = ks.w == c->tab_w;
   const int w_base = reg_w ? c->b_w : ks.w;
   va.btable = reg_w ? c->d_btable : (ks.w == 4 ? c->d_btable4 : c->d_btable8);
   va.lane_votes = launch_lane_votes(c, w_base, va.n_work);
-  HIP_TRY(c, txv_launch_verify(w_base, ks.w, &va, verify_grid(c, s.n), c->stream));
+  HIP_TRY(c, txv_launch_verify(w_base, ks.w, &va, verify_grid(c, s.n), c->vstream));
   ok.resize(s.n);
-  if (s.n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, s.n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (s.n) HIP_TRY(c, hipMemcpyAsync(ok.data(), s.d_ok, s.n, hipMemcpyDeviceToHost, c->vstream));
+  HIP_TRY(c, hipStreamSynchronize(c->vstream));
   return TXV_OK;
 }
 
@@ -1001,7 +1017,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TXV_EDEVICE;
   }
@@ -1025,7 +1041,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   if (c->key_stream) (void)hipStreamSynchronize(c->key_stream);
-  if (c->side_stream) (void)hipStreamSynchronize(c->side_stream);
+  if (c->vstream) (void)hipStreamSynchronize(c->vstream);
   for (auto& s : c->slots) {
     dfree(s.d_sig); dfree(s.d_msg); dfree(s.d_msg_len); dfree(s.d_val); dfree(s.d_set); dfree(s.d_flags);
     dfree(s.d_status); dfree(s.d_ok); dfree(s.d_pre); dfree(s.d_kbuf); dfree(s.d_rpts); dfree(s.d_order); hfree(s.h_order);
@@ -1055,7 +1071,7 @@ void txv_destroy(txv_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->key_stream) (void)hipStreamDestroy(c->key_stream);
-  if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
+  if (c->vstream) (void)hipStreamDestroy(c->vstream);
   delete c;
 }
 
@@ -1592,6 +1608,28 @@ int txv_fetch_staged(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_
   return fetch_slot(c, slot, status_out, ev, ev_cap, n_ev);
 }
 
+int txv_set_commit_sink(txv_ctx* c, uint32_t slot, void* dst_dev, uint32_t n_sets_cap) {
+  if (!c || slot >= 2 || (dst_dev && !n_sets_cap)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  Slot& s = c->slots[slot];
+  if (s.ticket) { c->err = "slot holds a txv_submit_votes batch in flight"; return TXV_ESTATE; }
+  if (s.launched) HIP_TRY(c, hipEventSynchronize(s.ev[4]));   // no pack into the old sink still pending
+  s.sink = static_cast<uint32_t*>(dst_dev);
+  s.sink_cap = dst_dev ? n_sets_cap : 0;
+  return TXV_OK;
+}
+
+int txv_slot_kernel_ms(txv_ctx* c, uint32_t slot, float* ms4) {
+  if (!c || !ms4 || slot >= kSlots - 2) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  Slot& s = c->slots[slot];
+  if (!s.launched) { c->err = "slot never ran"; return TXV_ESTATE; }
+  HIP_TRY(c, hipEventSynchronize(s.ev[4]));
+  return slot_kernel_ms(c, s, ms4);
+}
+
 int txv_commit_bitmap(txv_ctx* c, void** dev_ptr, uint64_t* bytes) {
   if (!c || !dev_ptr || !bytes) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1826,6 +1864,7 @@ int txv_reset_flow(txv_ctx* c) {
 
 int txv_sync(txv_ctx* c) {
   if (!c) return TXV_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->vstream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return TXV_OK;
 }

@@ -171,12 +171,14 @@ struct FlowBatch {
 };
 
 extern "C" {
-// the whole AddVote chain of one batch except SignBytes and verify, split where the verify
-// kernels sit: route (pre-checks, set-table find-or-insert, signature transpose, SignBytes
-// lengths) ...
+// the whole AddVote chain of one batch except SignBytes and verify, on two streams:
+// prep (pre-checks, validator lookup, signature transpose, SignBytes lengths: everything the
+// verify kernels read, nothing keyed by the TxFlow) runs on the verify stream ...
+hipError_t txv_flow_prep(const FlowState* fs, const FlowBatch* b, hipStream_t st);
+// ... the TxFlow part on the flow stream, in batch order after the previous batch's tally:
+// route (set-table find-or-insert of every TxHash) ...
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st);
-// ... new set ids (first-seen compaction; independent of verify: may run on a second stream
-// beside SignBytes and K1a/K1b, joined before the tally) ...
+// ... new set ids (first-seen compaction) ...
 hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t st);
 // ... then, after K1a/K1b wrote b->ok and the new ids exist: tally, commit events, statuses
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st);

@@ -154,6 +154,8 @@ def lib():
             "txv_shard_of": ([vp, vp, vp, u32, u32, vp], ctypes.c_int),
             "txv_commit_state_bytes": ([u32], ctypes.c_uint64),
             "txv_pack_commit_state": ([vp, vp, u32], ctypes.c_int),
+            "txv_set_commit_sink": ([vp, u32, vp, u32], ctypes.c_int),
+            "txv_slot_kernel_ms": ([vp, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "txv_read_commit_state": ([vp, vp, u32], ctypes.c_int),
             "txv_commit_state_pack_host": ([u32, vp, vp, u32, vp], ctypes.c_int),
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
@@ -178,7 +180,7 @@ EXPORTED_SYMBOLS = [
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
-    "txv_commit_state_unpack"]
+    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -575,6 +577,18 @@ class Context:
 
     def pack_commit_state(self, dst_dev_ptr: int, n_sets_cap: int):
         self._chk(lib().txv_pack_commit_state(self._h, ctypes.c_void_p(dst_dev_ptr), n_sets_cap), "pack state")
+
+    def set_commit_sink(self, slot: int, dst_dev_ptr: int | None, n_sets_cap: int = 0):
+        """txv_set_commit_sink: the packed commit state written into dst_dev_ptr (device memory)
+        at the end of every batch run in `slot` (staged slot / submit-ticket slot); None removes it"""
+        self._chk(lib().txv_set_commit_sink(self._h, slot, ctypes.c_void_p(dst_dev_ptr or 0), n_sets_cap if dst_dev_ptr else 0),
+                  "commit sink")
+
+    def slot_kernel_ms(self, slot: int):
+        """(prep + SignBytes, verify, tally after verify, total) device ms of the slot's last run"""
+        ms = (ctypes.c_float * 4)()
+        self._chk(lib().txv_slot_kernel_ms(self._h, slot, ms), "txv_slot_kernel_ms")
+        return (ms[0], ms[1], ms[2], ms[3])
 
     def read_commit_state(self, n_sets_cap: int) -> np.ndarray:
         """the device-packed commit state (txv_read_commit_state) as host bytes"""

@@ -255,16 +255,24 @@ int txv_sign_votes(txv_ctx* ctx, const txv_votes* votes, const uint32_t* signer,
                    uint32_t chain_len, uint8_t* sig_out);
 
 /* ---- device-resident batches (benchmark / pipelined ingest) ----
+ * Every AddVote batch (txv_add_votes, txv_submit_votes, txv_run_staged) runs on two device
+ * streams: its verify chain (pre-checks, validator lookup, SignBytes, K1a/K1b) reads nothing the
+ * TxFlow owns, so it starts as soon as its columns are uploaded, while the previous batch's
+ * tally still runs; its TxFlow chain (TxHash keying, new set ids, tally) follows the previous
+ * batch's on one stream, so results are those of the batches in submission order.
  * txv_stage: upload a batch's raw columns into device slot `slot` (0 or 1; TXV_ESTATE while the
  *   slot holds a txv_submit_votes batch).
- * txv_run_staged: run the whole AddVote kernel chain on the staged batch; results land in host
- *   memory for txv_fetch_staged.  kernel_ms_out (optional, 4 entries): route (TxHash keying,
- *   pre-checks, SignBytes) / verify / tally / total device time of this run, measured with HIP
- *   events on the stream the kernels run on. */
+ * txv_run_staged: enqueue the whole AddVote kernel chain on the staged batch and return (both
+ *   slots may be in flight: run slot 0, run slot 1, fetch slot 0, run slot 0, ...); results land
+ *   in host memory for txv_fetch_staged.  kernel_ms_out (optional, 4 entries; makes the call
+ *   wait): prep + SignBytes / verify (K1a + K1b) / tally after verify / total device time of
+ *   this run, measured with HIP events on the streams the kernels run on.
+ * txv_slot_kernel_ms: the same 4 times for the slot's last run, waiting for it if needed. */
 int txv_stage(txv_ctx* ctx, uint32_t slot, const txv_votes* votes);
 int txv_run_staged(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
 int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commit_event* ev_out,
                      uint32_t ev_cap, uint32_t* n_ev);
+int txv_slot_kernel_ms(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
 /* caller host memory the AddVote path may DMA from directly (hipHostRegister): columns of a
  * txv_votes batch lying inside a registered range skip the staging copy */
 int txv_host_register(txv_ctx* ctx, void* ptr, uint64_t bytes);
@@ -276,6 +284,13 @@ int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len
 uint64_t txv_commit_state_bytes(uint32_t n_sets_cap);
 /* this context's state into caller device memory (e.g. an RCCL all-gather buffer) */
 int txv_pack_commit_state(txv_ctx* ctx, void* dst_dev, uint32_t n_sets_cap);
+/* the same packed state written by the device at the end of every batch that runs in slot
+ * `slot` (0 or 1: staged slot, or the txv_submit_votes ticket t with (t - 1) % 2 == slot), in
+ * stream order before the batch's results are reported: once txv_fetch_staged / txv_wait_votes
+ * returns for the batch, dst_dev holds the state as of that batch, even when the next batch is
+ * already running.  dst_dev = NULL removes the sink.  For an all-gather per batch with two
+ * batches in flight (txvote's per-shard commit exchange). */
+int txv_set_commit_sink(txv_ctx* ctx, uint32_t slot, void* dst_dev, uint32_t n_sets_cap);
 /* the same packed by the device, copied into caller host memory (host-side gathers) */
 int txv_read_commit_state(txv_ctx* ctx, void* dst_host, uint32_t n_sets_cap);
 /* host-side pack (from per-set committed flags and sums) and unpack of the same layout */

@@ -97,6 +97,12 @@ int emu_fe10(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
       for (int j = 0; j < 8; ++j) out[j] = f.v[j];
       return 0;
     }
+    case 9: {   // fe10_mul2(x, y, y, x): both products, out[0..9] and out[10..19]
+      fe10 r2;
+      fe10_mul2(x, y, y, x, r, r2);
+      for (int j = 0; j < 10; ++j) out[10 + j] = r2.v[j];
+      break;
+    }
     default: return -1;
   }
   for (int j = 0; j < 10; ++j) out[j] = r.v[j];
@@ -109,6 +115,19 @@ int emu_ge10_madd(const uint32_t* p, const uint32_t* e, int neg, uint32_t* out) 
   fe10 qp, qm, qd;
   load_entry_w<4>(e, 0, 0, neg != 0, qp, qm, qd);
   P = ge10_madd(P, qp, qm, qd, neg != 0);
+  for (int j = 0; j < 10; ++j) { out[j] = P.X.v[j]; out[10 + j] = P.Y.v[j]; out[20 + j] = P.Z.v[j]; out[30 + j] = P.T.v[j]; }
+  return 0;
+}
+// the same addition through the walk's form (entry read piecewise, product pairs), kT = 0 for the
+// last addition of a walk (T not computed)
+int emu_ge10_madd_rd(const uint32_t* p, const uint32_t* e, int neg, uint32_t* out, int kT) {
+  ge10_ext P;
+  for (int j = 0; j < 10; ++j) { P.X.v[j] = p[j]; P.Y.v[j] = p[10 + j]; P.Z.v[j] = p[20 + j]; P.T.v[j] = p[30 + j]; }
+  fe10 q[3];
+  load_entry_w<4>(e, 0, 0, neg != 0, q[0], q[1], q[2]);
+  auto rd = [&](int role) { return q[role]; };
+  auto mid = [] {};
+  P = kT ? ge10_madd_rd<true>(P, rd, neg != 0, mid) : ge10_madd_rd<false>(P, rd, neg != 0, mid);
   for (int j = 0; j < 10; ++j) { out[j] = P.X.v[j]; out[10 + j] = P.Y.v[j]; out[20 + j] = P.Z.v[j]; out[30 + j] = P.T.v[j]; }
   return 0;
 }

@@ -329,3 +329,82 @@ def test_lane_votes_8_without_the_wide_base_table(oracle_lib):
             assert np.array_equal((st3 & 0x7F) == T.ADDED, exp)
         finally:
             ctx.close()
+
+
+def test_staged_two_in_flight_with_commit_sinks(oracle_lib):
+    """Two device-resident batches in flight (txv_run_staged returns at once; batch k+1's verify
+    chain runs beside batch k's tally): consecutive C5-shaped batches whose txs straddle the
+    batch boundary give the sequential oracle's per-vote codes and events, and each slot's commit
+    sink (txv_set_commit_sink, packed on the device at the end of its batch) holds the state as
+    of that batch although the next batch is already running.  Then the same with a fresh TxFlow
+    per batch (txv_reset_flow between launches), as bench.py replays its workload."""
+    import torch
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    n_vals, n_txs, batch, cap = 64, 700, 8192, 1024
+    ctx = T.Context(max_batch=batch, max_txs=cap, max_validators=n_vals)
+    try:
+        wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"] + 7, batch, window=96)
+        flow = oracle_lib.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        exp, events, states, committed, seen = [], [], [], set(), []
+        for b in wl.batches:
+            ost, _, ofired = flow.add_batch(b, _cores())
+            exp.append(_expected(ost, ofired))
+            events.append(_first_fired(b, ofired, committed))
+            for i in range(b.n):
+                h = b.txhash(i)
+                if h not in seen:
+                    seen.append(h)
+            q = [flow.query(h) for h in seen]
+            states.append(T.commit_state_pack_host(np.array([m for _, m in q], np.uint8),
+                                                   np.array([s for s, _ in q], np.int64), cap))
+        words = T.commit_state_bytes(cap) // 4
+        sinks = [torch.zeros(words, dtype=torch.int32, device="cuda:0") for _ in range(2)]
+        for sl in range(2):
+            ctx.set_commit_sink(sl, sinks[sl].data_ptr(), cap)
+
+        def check(k, st, ev, exp_state):
+            bad = np.nonzero(st != exp[k])[0]
+            assert len(bad) == 0, (k, [(int(i), int(st[i]), int(exp[k][i])) for i in bad[:10]])
+            assert sorted(int(x["vote_index"]) for x in ev) == events[k]
+            if exp_state is not None:
+                got = sinks[k % 2].cpu().numpy().view(np.uint8)
+                assert np.array_equal(got, exp_state), k
+
+        nb = len(wl.batches)
+        assert nb >= 4
+        ctx.stage(0, wl.batches[0])
+        ctx.run_staged(0)
+        ctx.stage(1, wl.batches[1])
+        ctx.run_staged(1)
+        # steady state: fetch k-1 while k runs, restage slot (k+1) % 2 after its fetch
+        st, ev = ctx.fetch_staged(0, wl.batches[0].n, ev_cap=batch)
+        check(0, st, ev, states[0])
+        for k in range(2, nb):
+            ctx.stage(k % 2, wl.batches[k])
+            ctx.run_staged(k % 2)
+            st, ev = ctx.fetch_staged((k - 1) % 2, wl.batches[k - 1].n, ev_cap=batch)
+            check(k - 1, st, ev, states[k - 1])
+        st, ev = ctx.fetch_staged((nb - 1) % 2, wl.batches[nb - 1].n, ev_cap=batch)
+        check(nb - 1, st, ev, states[nb - 1])
+        for h in wl.hashes:
+            assert ctx.query_tx(h.tobytes()) == flow.query(h.tobytes())
+        assert ctx.num_tx_sets() == n_txs
+        ms = ctx.slot_kernel_ms((nb - 1) % 2)
+        assert all(x >= 0 for x in ms) and ms[3] >= ms[1] > 0
+
+        # fresh TxFlow per launch, two in flight: every run of batch 0 gives batch 0's results
+        ctx.stage(0, wl.batches[0])
+        ctx.stage(1, wl.batches[0])
+        for k in range(6):
+            ctx.reset_flow()
+            ctx.run_staged(k % 2)
+            if k >= 1:
+                st, ev = ctx.fetch_staged((k - 1) % 2, wl.batches[0].n, ev_cap=batch)
+                check(0, st, ev, states[0])
+        st, ev = ctx.fetch_staged(1, wl.batches[0].n, ev_cap=batch)
+        check(0, st, ev, states[0])
+        for sl in range(2):
+            ctx.set_commit_sink(sl, None)
+    finally:
+        ctx.close()

@@ -30,6 +30,7 @@ def emu():
     E.emu_wire_fast_hits.restype = ctypes.c_uint64
     E.emu_fe10.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]
     E.emu_ge10_madd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    E.emu_ge10_madd_rd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     E.emu_entry.argtypes = [ctypes.c_void_p] * 3
     E.emu_inv_var.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     E.emu_inv_var_counts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
@@ -133,9 +134,16 @@ def test_fe10_limb_arithmetic_at_its_bounds(emu):
         cases.append(([rnd.randrange(4 << w) for w in W10], [rnd.randrange(3 << w) for w in W10]))
         cases.append(([rnd.choice([0, (4 << w) - 1, rnd.randrange(4 << w)]) for w in W10],
                       [rnd.choice([0, (3 << w) - 1, rnd.randrange(3 << w)]) for w in W10]))
+    out2 = (ctypes.c_uint32 * 20)()
     for fa, ga in cases:
         emu.emu_fe10((ctypes.c_uint32 * 10)(*fa), (ctypes.c_uint32 * 10)(*ga), out, 0)
         assert v10(out) % P == v10(fa) * v10(ga) % P and carried(list(out)), (fa, ga)
+        if max(fa[i] - (3 << w) for i, w in enumerate(W10)) < 0:
+            # fe10_mul2 (the walk's interleaved pair) = fe10_mul of each pair, limb for limb
+            emu.emu_fe10((ctypes.c_uint32 * 10)(*fa), (ctypes.c_uint32 * 10)(*ga), out2, 9)
+            assert list(out2[:10]) == list(out), (fa, ga)
+            emu.emu_fe10((ctypes.c_uint32 * 10)(*ga), (ctypes.c_uint32 * 10)(*fa), out, 0)
+            assert list(out2[10:]) == list(out), (fa, ga)
     for _ in range(300):
         a, b = rnd.randrange(P), rnd.randrange(P)
         for op, exp in ((1, a + b), (2, a - b), (3, -a)):
@@ -197,6 +205,12 @@ def test_ge10_madd_half_niels(emu):
             exp = _ed_add(p1, (P - q[0] if neg else q[0], q[1]))
             zi = pow(Z3, P - 2, P)
             assert (X3 * zi % P, Y3 * zi % P) == exp and (X3 * Y3 - Z3 * T3) % P == 0
+            # the walk's form (product pairs) gives the same limbs; without T for the last addition
+            out_rd = (ctypes.c_uint32 * 40)()
+            emu.emu_ge10_madd_rd((ctypes.c_uint32 * 40)(*limbs), e, neg, out_rd, 1)
+            assert list(out_rd) == list(out)
+            emu.emu_ge10_madd_rd((ctypes.c_uint32 * 40)(*limbs), e, neg, out_rd, 0)
+            assert list(out_rd[:30]) == list(out[:30])
 
 
 def test_verify_vectors_through_kernel_source(emu):
