@@ -11,9 +11,9 @@ One step = one pass of the hot path over the batch, inputs resident in HBM: a fr
 TxVoteSets (device hash table, first-seen ids), validator lookup and pre-checks, SignBytes,
 K1a/K1b verify, the first-accepted resolution, stake sums and 2/3 crossings -- and the per-vote
 statuses + commit events in host memory; at N>1 also the packed per-shard commit state
-all-gathered over RCCL.  Steps run two in flight (slots 0 and 1 hold the same staged batch):
-step k+1's verify chain runs while step k's TxFlow chain tallies, as consecutive batches of a
-node do.  value = votes processed by all ranks / max-over-ranks time.
+all-gathered over RCCL.  Steps run pipelined (slots 0-2 hold the same staged batch, up to three
+enqueued): step k+1's verify chain runs while step k's TxFlow chain tallies, as consecutive
+batches of a node do.  value = votes processed by all ranks / max-over-ranks time.
 
 Beside it: the end-to-end rate from the caller's host SoA columns (txv_submit_votes /
 txv_wait_votes, two batches in flight: staging copy + PCIe upload + kernels + results), the
@@ -385,10 +385,12 @@ def main():
     numa = ctx.bind_host_numa()     # host threads + pinned buffers next to this GPU's PCIe root
     wl = Workload(ctx, args.validators, n_txs_global, SEEDS["c3" if world > 1 else "c2"],
                   shard=rank, n_shards=world)
-    # the same batch in both device slots: step k runs in slot k % 2, so step k+1's verify chain
-    # overlaps step k's tally (txv_run_staged returns as soon as the chain is enqueued)
-    ctx.stage(0, wl.batch)
-    ctx.stage(1, wl.batch)
+    # the same batch in the three device slots: step k runs in slot k % 3 with up to three steps
+    # enqueued, so step k+1's prep runs beside step k's K1b and its K1a/K1b beside step k's tally
+    # (txv_run_staged returns as soon as the chain is enqueued)
+    DEPTH = 3
+    for sl in range(DEPTH):
+        ctx.stage(sl, wl.batch)
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
         f"staged in {time.perf_counter() - t_setup:.1f}s")
 
@@ -400,8 +402,8 @@ def main():
     if dist is not None:
         import torch
         words = T.commit_state_bytes(n_cap) // 4
-        state = [torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}") for _ in range(2)]
-        for sl in range(2):
+        state = [torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}") for _ in range(DEPTH)]
+        for sl in range(DEPTH):
             ctx.set_commit_sink(sl, state[sl].data_ptr(), n_cap)
         gathered = torch.zeros(world * words, dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
     red_dev = "cpu" if gloo else f"cuda:{local}"
@@ -414,18 +416,18 @@ def main():
             torch.cuda.synchronize()
 
     step_ms, route_ms, verify_ms, tally_ms = [], [], [], []
-    st_buf = [np.zeros(wl.n, np.uint8) for _ in range(2)]          # result buffers reused every step
-    ev_buf = [np.zeros(wl.n_txs + 1, T.EVENT_DTYPE) for _ in range(2)]
+    st_buf = [np.zeros(wl.n, np.uint8) for _ in range(DEPTH)]          # result buffers reused every step
+    ev_buf = [np.zeros(wl.n_txs + 1, T.EVENT_DTYPE) for _ in range(DEPTH)]
     t_launch = {}
 
     def launch(k: int):
         """enqueue step k: a fresh TxFlow (in stream order after step k-1's tally) + the chain"""
         t_launch[k] = time.perf_counter()
         ctx.reset_flow()
-        ctx.run_staged(k % 2)
+        ctx.run_staged(k % DEPTH)
 
     def finish(k: int, record: bool):
-        sl = k % 2
+        sl = k % DEPTH
         st, ev = ctx.fetch_staged(sl, wl.n, ev_cap=wl.n_txs + 1, out=st_buf[sl], evs=ev_buf[sl])
         if dist is not None:
             all_gather_state(sl)
@@ -436,15 +438,15 @@ def main():
         return st, ev
 
     def run_steps(m: int, record: bool):
-        """m steps, two in flight: launch k+1 before waiting for k"""
+        """m steps, up to DEPTH enqueued: launch k before waiting for k - DEPTH + 1"""
         out = None
-        if m <= 0:
-            return out
-        launch(0)
-        for k in range(1, m):
+        for k in range(m):
             launch(k)
-            out = finish(k - 1, record)
-        return finish(m - 1, record)
+            if k >= DEPTH - 1:
+                out = finish(k - DEPTH + 1, record)
+        for k in range(max(0, m - DEPTH + 1), m):
+            out = finish(k, record)
+        return out
 
     def step(record: bool):
         return run_steps(1, record)
@@ -498,6 +500,14 @@ def main():
 
     value = total_votes * args.steps / elapsed
     r_ms, v_ms, t_ms = statistics.median(route_ms), statistics.median(verify_ms), statistics.median(tally_ms)
+    # the same chain run alone (one step at a time, nothing beside it): per-stage device times
+    # without the pipeline's co-running kernels (the tally's HBM rate uses these)
+    solo = []
+    for _ in range(3):
+        ctx.reset_flow()
+        solo.append(ctx.run_staged(0, timed=True))
+        ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf[0], evs=ev_buf[0])
+    s_ms = [statistics.median(x[j] for x in solo) for j in range(4)]
     if rank == 0:
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
         # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
@@ -531,9 +541,14 @@ def main():
                        "host_numa_bound": numa,
                        "step": "reset_flow + device TxHash routing/pre-checks/SignBytes + verify + tally + "
                                "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "") +
-                               "; two steps in flight (step k+1's verify overlaps step k's tally)"},
+                               "; up to three steps enqueued (step k+1's verify overlaps step k's tally)"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
-            "device_ms_p50": {"route": round(r_ms, 3), "verify": round(v_ms, 3), "tally": round(t_ms, 3)},
+            "device_ms_p50": {"prep": round(r_ms, 3), "verify": round(v_ms, 3), "tally_after_verify": round(t_ms, 3),
+                              "note": "in the timed pipeline (HIP events on each stream): prep + SignBytes, K1a + K1b, "
+                                      "verify end -> tally end (includes waiting for the flow stream)"},
+            "device_ms_standalone": {"prep": round(s_ms[0], 3), "verify": round(s_ms[1], 3), "tally": round(s_ms[2], 3),
+                                     "chain": round(s_ms[3], 3),
+                                     "note": "one step alone after the timed region (no co-running kernels)"},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
                          "unit": "Tlane-op/s (int32 VALU issue)", "frac": round(achieved / VALU_PEAK, 4),
                          "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_multi (verify pair)",
@@ -546,10 +561,10 @@ def main():
                          "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"},
             "cpu_baseline": cpu,
             # the tally chain after verify (HBM-bound per BASELINE.md): bytes per launch from the same
-            # PMC passes (2 x FETCH_SIZE + WRITE_SIZE of its kernels) over this run's tally time
-            "tally": {"ms": round(t_ms, 3), "hbm_bytes_per_launch": tally_bytes,
-                      "GBps": None if not tally_bytes else round(tally_bytes / (t_ms * 1e-3) / 1e9, 1),
-                      "frac_of_8TBps": None if not tally_bytes else round(tally_bytes / (t_ms * 1e-3) / 8e12, 3),
+            # PMC passes (2 x FETCH_SIZE + WRITE_SIZE of its kernels) over the standalone tally time
+            "tally": {"ms": round(s_ms[2], 3), "hbm_bytes_per_launch": tally_bytes,
+                      "GBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 1e9, 1),
+                      "frac_of_8TBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 8e12, 3),
                       "note": "includes the accepted-vote arena rows (128 B per ADDED vote) MakeCommit reads; "
                               "BASELINE.md's 16 B/vote counts the cell update alone"},
         }

@@ -14,7 +14,8 @@
 //
 // Launch geometry: 512-thread workgroups; K1b walks an XCD-contiguous eighth of the work list
 // per group of blocks (blocks b, b+8, ... share an XCD) and runs at 2 waves/SIMD with V = 8
-// (1M-vote batches) or 4 waves/SIMD with V = 4.
+// (batches of >= 768K votes) or V = 4 (configured); smaller batches run one vote per lane
+// (txv_k_scalarmult_points + txv_k_batch_encode, 4 waves/SIMD).
 #include <cstdlib>
 
 #include "ed25519_dev.h"
@@ -391,10 +392,10 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
 #define TXV_PARK_LAST 1
 #endif
 // V = 8 is launched for batches that give 2 waves per SIMD (launch_lane_votes), so its register
-// budget is 256 VGPRs (2 waves/SIMD); V = 4 keeps 128 (4 waves/SIMD) unless TXV_V4_WAVES says
-// otherwise
+// budget is 256 VGPRs (2 waves/SIMD); V = 4 too (at 128 VGPRs / 4 waves it spilled ~138 VGPRs:
+// 1.57 vs 0.60 ms for a 65k-vote batch, profiles/r02/small_batch)
 #ifndef TXV_V4_WAVES
-#define TXV_V4_WAVES 4
+#define TXV_V4_WAVES 2
 #endif
 template <int BLOCK, int WB, int WA, int V>
 __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) txv_k_scalarmult_multi(VerifyArgs a) {

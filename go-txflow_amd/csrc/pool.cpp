@@ -29,6 +29,7 @@
 #include <mutex>
 #include <thread>
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <vector>
 
@@ -193,6 +194,7 @@ struct txv_pool {
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
+  std::vector<uint32_t> admitted;                  // batch scratch: admitted votes in order
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -291,26 +293,59 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     for (uint32_t i = 0; i < (uint32_t)((uint64_t)n / nt); ++i) p->sizes[i] = vote_size(v, i);
     for (auto& x : th) x.join();
   }
-  constexpr uint32_t kAhead = 16;   // the loop is DRAM-latency bound: prefetch the hash slots ahead
-  for (uint32_t i = 0; i < v->n; ++i) {
-    if (i + kAhead < v->n) {
-      if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
-      p->txs_map.prefetch(keys[i + kAhead]);
+  // The sequential CheckTx loop, split over two threads.  The decision for vote i needs only the
+  // pool's running Size()/TxsBytes (counters of the votes admitted before it) and the cache, so
+  // this thread decides every vote and drives mapTxCache; a second thread replays the admitted
+  // votes into txs / txsMap in the same order (addTx), a few entries behind.  Both loops are
+  // DRAM-latency bound on their hash tables and prefetch ahead.
+  constexpr uint32_t kAhead = 16;
+  const uint32_t n = v->n;
+  std::vector<uint32_t>& adm = p->admitted;
+  adm.resize(n);
+  std::atomic<uint32_t> published{0};
+  std::atomic<bool> decided{false};
+  auto add_txs = [&] {
+    uint32_t j = 0;
+    for (;;) {
+      const uint32_t m = published.load(std::memory_order_acquire);
+      if (j == m) {
+        if (decided.load(std::memory_order_acquire) && j == published.load(std::memory_order_acquire)) break;
+        std::this_thread::yield();
+        continue;
+      }
+      for (; j < m; ++j) {
+        if (j + kAhead < m) p->txs_map.prefetch(keys[adm[j + kAhead]]);
+        const uint32_t i = adm[j];
+        p->txs_map.put(keys[i], p->txs.push_back(keys[i], p->sizes[i]));   // addTx (txsMap.Store overwrites)
+      }
     }
+  };
+  const bool two = n >= 4096;
+  std::thread tb;
+  if (two) tb = std::thread(add_txs);
+  int64_t len_run = (int64_t)p->txs.len, bytes_run = p->txs_bytes;
+  uint32_t na = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (i + kAhead < n && p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
     const uint32_t sz = p->sizes[i];   // 0: amino error (Size() swallows it)
-    if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
+    if (len_run >= (int64_t)p->cfg.size || (int64_t)sz + bytes_run > (int64_t)p->cfg.max_txs_bytes) {
       status_out[i] = TXV_POOL_ERR_FULL;
       continue;
     }
     if ((int64_t)sz > max_tx) { status_out[i] = TXV_POOL_ERR_TOO_LARGE; continue; }
-    Key k;
-    memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
-    if (!p->cache_push(k)) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
+    if (!p->cache_push(keys[i])) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
     if (!sz && (p->cfg.flags & TXV_POOL_WAL)) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
-    p->txs_map.put(k, p->txs.push_back(k, sz));     // addTx (txsMap.Store overwrites)
-    p->txs_bytes += sz;
+    ++len_run;
+    bytes_run += sz;
     status_out[i] = TXV_POOL_OK;
+    adm[na++] = i;
+    if (two && (na & 63) == 0) published.store(na, std::memory_order_release);
   }
+  published.store(na, std::memory_order_release);
+  decided.store(true, std::memory_order_release);
+  if (two) tb.join();
+  else add_txs();
+  p->txs_bytes = bytes_run;
   if (getenv("TXV_PROFILE_HOST")) {
     const auto t2 = std::chrono::steady_clock::now();
     fprintf(stderr, "[txv pool] keys=%.3fms lru=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),

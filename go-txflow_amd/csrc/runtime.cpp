@@ -44,7 +44,7 @@ namespace {
 inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32; }
 constexpr uint32_t kTableWords4 = 64 * 9 * 32;
 inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
-constexpr uint32_t kSlots = 4;
+constexpr uint32_t kSlots = 5;   // 0-2 staged (0, 1 also the submit ring), 3 signer, 4 verify-only
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
@@ -86,8 +86,8 @@ struct Slot {
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
   FlowSummary* h_sum = nullptr; FlowSummary* m_sum = nullptr;
-  // copy stream: 3 upload done, 0 prep start, 1 prep + SignBytes done; verify stream: 7 K1a
-  // start, 2 verify done; flow stream: 4 results in host memory (+ commit sink), 5 tallied,
+  // copy stream: 3 upload done; key stream: 0 prep start, 1 prep + SignBytes done; verify
+  // stream: 7 K1a start, 2 verify done; flow stream: 4 results in host memory (+ commit sink), 5 tallied,
   // 6 set keying done; 8 unused
   hipEvent_t ev[9] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool launched = false;           // a chain was enqueued on this slot (its ev[4] marks the end)
@@ -105,7 +105,7 @@ struct txv_ctx {
   hipStream_t stream = nullptr;        // flow: TxFlow keying + tally kernels, resets, readers (batch order)
   hipStream_t vstream = nullptr;       // verify: prep + K1a/K1b (batch k+1 verifies while batch k tallies)
   hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
-  hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest) runs beside in-flight batches
+  hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest), wire decode, and each batch's prep + SignBytes
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   std::string err;
   std::mutex mu;
@@ -260,7 +260,7 @@ int ensure_slot(txv_ctx* c, Slot& s, uint32_t n, uint32_t msg_words) {
         (r = dalloc(c, &s.d_msg_len, npad)) || (r = dalloc(c, &s.d_val, npad)) || (r = dalloc(c, &s.d_set, npad)) ||
         (r = dalloc(c, &s.d_flags, npad)) || (r = dalloc(c, &s.d_status, npad)) || (r = dalloc(c, &s.d_ok, npad)) ||
         (r = dalloc(c, &s.d_pre, npad)) || (r = dalloc(c, &s.d_kbuf, 8 * npad)) ||
-        (c->lane_votes == 1 && (r = dalloc(c, &s.d_rpts, (size_t)TXV_RPTS_WORDS * npad))) ||
+        ((c->lane_votes == 1 || c->lane_auto) && (r = dalloc(c, &s.d_rpts, (size_t)TXV_RPTS_WORDS * npad))) ||
         (r = dalloc(c, &s.d_order, npad)) || (r = halloc(c, &s.h_order, npad)) ||
         (r = halloc(c, &s.h_sig, 16 * npad)) || (r = halloc(c, &s.h_msg, (size_t)mw * npad)) ||
         (r = halloc(c, &s.h_msg_len, npad)) || (r = halloc(c, &s.h_val, npad)) || (r = halloc(c, &s.h_set, npad)) ||
@@ -485,12 +485,16 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
 // K1b votes per lane for a launch with base window wb.  V = 8 halves the inversions per vote
 // but also the waves; with the divstep inverse it wins once the batch still fills >= 1.5 waves
 // per SIMD (C2, 1M votes: 517 vs 503-512M votes/s, profiles/r01/inv_var, profiles/r01/park);
-// smaller batches (C5's 64k) keep V = 4.  V = 8 kernels exist for the radix-2^24 / 2^26 base
+// smaller batches run one vote per lane (split mode: the points kernel + K1c's batched
+// inversion), which gives them the most waves (C5's 65k votes: 0.52 ms vs 0.60 at V = 4,
+// profiles/r02/small_batch).  V = 8 kernels exist for the radix-2^24 / 2^26 base
 // tables only, so a configured V = 8 runs V = 4 on any other base table (e.g. when no wide
 // table could be allocated, or for caller-key tables).
 uint32_t launch_lane_votes(const txv_ctx* c, int wb, uint32_t n_work) {
-  if (wb != 24 && wb != 26) return c->lane_votes == 8 ? 4u : c->lane_votes;
-  return (c->lane_auto && n_work >= (3u << 18)) ? 8u : c->lane_votes;
+  const bool wide = wb == 24 || wb == 26;
+  if (c->lane_auto) return wide && n_work >= (3u << 18) ? 8u : 1u;
+  if (!wide) return c->lane_votes == 8 ? 4u : c->lane_votes;
+  return c->lane_votes;
 }
 
 // scratch for the parked results per K1b lane (V slots: the last one with TXV_PARK_LAST) (the grid never exceeds verify_grid's cap)
@@ -718,29 +722,32 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   s.stamp = ++c->stamp;            // every run of a batch gets a stamp of its own
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
-  // Three queues, so that batch k+1 verifies while batch k tallies and nothing but K1a/K1b sits
-  // on the verify stream:
-  //   copy stream  the uploads (stage_add), then prep (pre-checks, validator lookup, signature
-  //                transpose) and SignBytes: they read only the uploaded columns and run beside
-  //                the previous batch's K1b
+  // Three compute queues, so that batch k+1 verifies while batch k tallies and nothing but
+  // K1a/K1b sits on the verify stream:
+  //   key stream   (after the uploads on the copy stream) prep (pre-checks, validator lookup,
+  //                signature transpose) and SignBytes: they read only the uploaded columns and
+  //                run beside the previous batch's K1b; the copy stream stays pure DMA, so batch
+  //                k+2's upload never queues behind them
   //   vstream      K1a/K1b: reads nothing the TxFlow owns, so it never waits for an earlier
   //                batch's tally
   //   flow stream  set keying + new set ids, then -- after this batch's verify -- the tally:
   //                every TxFlow access stays in batch order on this one stream
-  // (GPU_MAX_HW_QUEUES = 4: context, copy, key and verify streams each get a hardware queue; a
-  // further compute stream would share, i.e. serialise with, one of them)
+  // (GPU_MAX_HW_QUEUES = 4: flow, copy, key and verify streams each get a hardware queue; a
+  // further stream would share, i.e. serialise with, one of them)
   // the slot's previous chain (its tally reads the derived columns prep rewrites) has ended
-  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));
+  hipStream_t ps = c->key_stream;
+  HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[3], 0));
+  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[4], 0));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
-  HIP_TRY(c, hipEventRecord(s.ev[0], c->copy_stream));
+  HIP_TRY(c, hipEventRecord(s.ev[0], ps));
   SignBytesArgs sa{};
   sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
   sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = nullptr; sa.nil = s.has_nil ? s.d_nil : nullptr;
   sa.msg = s.d_msg;
-  HIP_TRY(c, txv_flow_prep(&fs, &fb, c->copy_stream));
-  HIP_TRY(c, txv_launch_signbytes(&sa, c->copy_stream));
-  HIP_TRY(c, hipEventRecord(s.ev[1], c->copy_stream));
+  HIP_TRY(c, txv_flow_prep(&fs, &fb, ps));
+  HIP_TRY(c, txv_launch_signbytes(&sa, ps));
+  HIP_TRY(c, hipEventRecord(s.ev[1], ps));
   HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
   HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
@@ -975,7 +982,40 @@ int wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_even
   return fetch_slot(c, (uint32_t)((ticket - 1) % 2), status_out, ev, ev_cap, n_ev);
 }
 
+// The context's four streams.  Experiment knobs (environment, read once per context):
+// TXV_VSTREAM_PRIO=1 creates the verify stream at the device's highest priority; TXV_FLOW_CUS=N
+// restricts the flow and key streams to N CUs spread over the XCDs (hipExtStreamCreateWithCUMask),
+// so their latency-bound kernels stay off the CUs K1b runs on.
+hipError_t create_streams(txv_ctx* c) {
+  hipError_t e;
+  const char* fc = getenv("TXV_FLOW_CUS");
+  const int flow_cus = fc ? atoi(fc) : 0;
+  int ncu = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
+  if (flow_cus > 0 && flow_cus < ncu) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    const int stride = ncu / flow_cus;
+    for (int i = 0, k = 0; i < ncu && k < flow_cus; i += stride, ++k) mask[i / 32] |= 1u << (i % 32);
+    if ((e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask.size(), mask.data())) != hipSuccess) return e;
+    if ((e = hipExtStreamCreateWithCUMask(&c->key_stream, (uint32_t)mask.size(), mask.data())) != hipSuccess) return e;
+  } else {
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking)) != hipSuccess) return e;
+  }
+  if ((e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) return e;
+  const char* vp = getenv("TXV_VSTREAM_PRIO");
+  if (vp && atoi(vp) > 0) {
+    int lo = 0, hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return e;
+    return hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, hi);
+  }
+  return hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking);
+}
+
 }  // namespace
+
+// ==================================================================== C ABI}  // namespace
 
 // ==================================================================== C ABI
 extern "C" {
@@ -1014,10 +1054,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
   if (dev < 0) { if (hipGetDevice(&dev) != hipSuccess) dev = 0; }
   if (dev >= ndev) { delete c; return TXV_EINVAL; }
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->vstream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || create_streams(c) != hipSuccess) {
     delete c;
     return TXV_EDEVICE;
   }
@@ -1609,7 +1646,7 @@ int txv_fetch_staged(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_
 }
 
 int txv_set_commit_sink(txv_ctx* c, uint32_t slot, void* dst_dev, uint32_t n_sets_cap) {
-  if (!c || slot >= 2 || (dst_dev && !n_sets_cap)) return TXV_EINVAL;
+  if (!c || slot >= kSlots - 2 || (dst_dev && !n_sets_cap)) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   Slot& s = c->slots[slot];

@@ -337,7 +337,8 @@ def test_staged_two_in_flight_with_commit_sinks(oracle_lib):
     batch boundary give the sequential oracle's per-vote codes and events, and each slot's commit
     sink (txv_set_commit_sink, packed on the device at the end of its batch) holds the state as
     of that batch although the next batch is already running.  Then the same with a fresh TxFlow
-    per batch (txv_reset_flow between launches), as bench.py replays its workload."""
+    per batch (txv_reset_flow between launches) and all three staged slots enqueued, as bench.py
+    replays its workload."""
     import torch
     import txflow_amd as T
     from txflow_amd.workload import StreamWorkload, SEEDS
@@ -393,18 +394,24 @@ def test_staged_two_in_flight_with_commit_sinks(oracle_lib):
         ms = ctx.slot_kernel_ms((nb - 1) % 2)
         assert all(x >= 0 for x in ms) and ms[3] >= ms[1] > 0
 
-        # fresh TxFlow per launch, two in flight: every run of batch 0 gives batch 0's results
-        ctx.stage(0, wl.batches[0])
-        ctx.stage(1, wl.batches[0])
-        for k in range(6):
+        # fresh TxFlow per launch, three slots enqueued (as bench.py runs): every run of batch 0
+        # gives batch 0's results and its sink batch 0's state
+        sinks.append(torch.zeros(words, dtype=torch.int32, device="cuda:0"))
+        ctx.set_commit_sink(2, sinks[2].data_ptr(), cap)
+        for sl in range(3):
+            ctx.stage(sl, wl.batches[0])
+        for k in range(8):
             ctx.reset_flow()
-            ctx.run_staged(k % 2)
-            if k >= 1:
-                st, ev = ctx.fetch_staged((k - 1) % 2, wl.batches[0].n, ev_cap=batch)
-                check(0, st, ev, states[0])
-        st, ev = ctx.fetch_staged(1, wl.batches[0].n, ev_cap=batch)
-        check(0, st, ev, states[0])
-        for sl in range(2):
+            ctx.run_staged(k % 3)
+            if k >= 2:
+                st, ev = ctx.fetch_staged((k - 2) % 3, wl.batches[0].n, ev_cap=batch)
+                check(0, st, ev, None)
+                assert np.array_equal(sinks[(k - 2) % 3].cpu().numpy().view(np.uint8), states[0])
+        for k in (6, 7):
+            st, ev = ctx.fetch_staged(k % 3, wl.batches[0].n, ev_cap=batch)
+            check(0, st, ev, None)
+            assert np.array_equal(sinks[k % 3].cpu().numpy().view(np.uint8), states[0])
+        for sl in range(3):
             ctx.set_commit_sink(sl, None)
     finally:
         ctx.close()
