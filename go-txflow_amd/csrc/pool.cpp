@@ -187,10 +187,13 @@ struct txv_pool {
   bool cache_on = true;
   int64_t height = 0;
   std::mutex mu;                                   // proxyMtx
-  KeyList cache;                                   // mapTxCache.list
-  FlatIndex cache_map{&cache};                     // mapTxCache.map_
-  KeyList txs;                                     // txs (clist of MempoolTxVote)
-  FlatIndex txs_map{&txs};                         // txsMap
+  // the cache and the pool list are driven by different threads inside txv_pool_check: each on
+  // cache lines of its own
+  alignas(64) KeyList cache;                       // mapTxCache.list
+  alignas(64) FlatIndex cache_map{&cache};         // mapTxCache.map_
+  alignas(64) KeyList txs;                         // txs (clist of MempoolTxVote)
+  alignas(64) FlatIndex txs_map{&txs};             // txsMap
+  alignas(64) char pad_[1] = {0};
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
@@ -320,7 +323,8 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
       }
     }
   };
-  const bool two = n >= 4096;
+  const bool one_thread = getenv("TXV_POOL_ONE_THREAD") != nullptr;   // A/B knob
+  const bool two = n >= 4096 && !one_thread;
   std::thread tb;
   if (two) tb = std::thread(add_txs);
   int64_t len_run = (int64_t)p->txs.len, bytes_run = p->txs_bytes;

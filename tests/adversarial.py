@@ -103,6 +103,7 @@ class C4Stream:
         base_frac = 1.0 - 0.05 - 0.05 - 0.02 - 0.005 - 0.0025 - 0.001
         self.epoch_txs = max(1, int(batch * batches_per_epoch * base_frac) // N_HONEST)
         self.epoch = -1
+        self.generated = 0
         self.stats = dict(votes=0, batches=0, epochs=0, mismatches=0, verify_checked=0, events=0,
                           txs_checked=0, by_status={})
 
@@ -133,8 +134,10 @@ class C4Stream:
         return R + s.to_bytes(32, "little")
 
     def next_batch(self):
-        if self.epoch < 0 or (self.stats["batches"] % self.bpe) == 0:
+        # epochs by batches generated (a pipelined driver generates batch k+1 before checking k)
+        if self.epoch < 0 or (self.generated % self.bpe) == 0:
             self._new_epoch()
+        self.generated += 1
         import txflow_amd as T
         rng, n = self.rng, self.batch
         n_rep, n_conf = int(n * 0.05), int(n * 0.05)
@@ -288,10 +291,15 @@ class C4Stream:
 
     # ---------------------------------------------------------------- the gate
     def run_batch(self):
-        import txflow_amd as T
-        O = self.O
         batch, f = self.next_batch()
         st, ev = self.ctx.add_votes(batch, ev_cap=batch.n)
+        return self.check_batch(batch, f, st, ev)
+
+    def check_batch(self, batch, f, st, ev):
+        """the device's results of one batch (statuses + fire bits, events) against the oracle's
+        sequential run of the same batch (batches must be checked in submission order)"""
+        import txflow_amd as T
+        O = self.O
         ost, osum, ofired = self.flow.add_batch(batch, self.threads)
         exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
         bad = np.nonzero(st != exp)[0]
@@ -353,16 +361,38 @@ class C4Stream:
 
 
 def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int = 4, threads: int = 16,
-             log=print, seed: int = 0x7478763034):
-    """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0)."""
+             log=print, seed: int = 0x7478763034, pipelined: bool = True):
+    """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0).
+    pipelined: batches go through txv_submit_votes / txv_wait_votes with two in flight (batch
+    k+1 verifies on the device while batch k tallies and is checked against the oracle); the
+    pipeline drains at each epoch end, before the per-set check reads the device state."""
     s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads)
     t0 = time.time()
-    while s.stats["votes"] < total_votes:
-        r = s.run_batch()
+
+    def report(r):
         log(f"[c4] batch {s.stats['batches']} epoch {s.epoch}: {r['n']} votes, status mismatches "
             f"{r['status_mismatches']}, events ok {r['events_ok']}, verify mismatches {r['verify_mismatches']}; "
             f"total {s.stats['votes']} votes, {s.stats['mismatches']} mismatches, {time.time() - t0:.0f}s"
             + (f" first_bad={r['first_bad']}" if r["first_bad"] else ""))
+
+    inflight = []
+    submitted = sub_votes = 0
+    while (s.stats["votes"] if not pipelined else sub_votes) < total_votes or inflight:
+        if not pipelined:
+            report(s.run_batch())
+            continue
+        # the batch that closes an epoch is checked with nothing behind it in flight
+        epoch_end = (submitted % s.bpe) == 0 and submitted > 0
+        if sub_votes < total_votes and not (epoch_end and inflight) and len(inflight) < 2:
+            b, f = s.next_batch()
+            inflight.append((b, f, ctx.submit_votes(b)))
+            submitted += 1
+            sub_votes += b.n
+            if len(inflight) < 2 and (submitted % s.bpe) != 0 and sub_votes < total_votes:
+                continue
+        b, f, tk = inflight.pop(0)
+        st, ev = ctx.wait_votes(tk, ev_cap=b.n)
+        report(s.check_batch(b, f, st, ev))
     if s.stats["batches"] % s.bpe:
         s.stats["mismatches"] += s.check_sets()
     s.stats["seconds"] = round(time.time() - t0, 1)
