@@ -1015,8 +1015,6 @@ hipError_t create_streams(txv_ctx* c) {
 
 }  // namespace
 
-// ==================================================================== C ABI}  // namespace
-
 // ==================================================================== C ABI
 extern "C" {
 

@@ -38,13 +38,15 @@ double orc_verify_many(const uint8_t* pubs32, const uint32_t* val_idx,
   if (threads > 256) threads = 256;
   job jobs[256];
   pthread_t th[256];
+  int started[256];
   double t0 = now_s();
   for (int t = 0; t < threads; ++t) {
     jobs[t] = (job){pubs32, msg_arena, sigs64, val_idx, msg_off, msg_len, out_ok,
                     (uint32_t)((uint64_t)n * t / threads), (uint32_t)((uint64_t)n * (t + 1) / threads)};
-    if (threads == 1) run(&jobs[0]);
-    else pthread_create(&th[t], 0, run, &jobs[t]);
+    started[t] = threads > 1 && pthread_create(&th[t], 0, run, &jobs[t]) == 0;   /* else inline */
+    if (!started[t]) run(&jobs[t]);
   }
-  if (threads > 1) for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  for (int t = 0; t < threads; ++t)
+    if (started[t]) pthread_join(th[t], 0);
   return now_s() - t0;
 }

@@ -279,12 +279,15 @@ void orc_flow_add_votes_soa(orc_flow* f, const orc_soa* b, int threads, uint8_t*
   uint8_t* code = (uint8_t*)malloc(b->n ? b->n : 1);
   soa_job jobs[256];
   pthread_t th[256];
+  int started[256];
   for (int t = 0; t < threads; ++t) {
     jobs[t] = (soa_job){f, b, code, (uint32_t)((uint64_t)b->n * t / threads), (uint32_t)((uint64_t)b->n * (t + 1) / threads)};
-    if (threads == 1) soa_verify(&jobs[0]);
-    else pthread_create(&th[t], 0, soa_verify, &jobs[t]);
+    /* a thread that cannot be created runs its range inline: never a range left unverified */
+    started[t] = threads > 1 && pthread_create(&th[t], 0, soa_verify, &jobs[t]) == 0;
+    if (!started[t]) soa_verify(&jobs[t]);
   }
-  if (threads > 1) for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  for (int t = 0; t < threads; ++t)
+    if (started[t]) pthread_join(th[t], 0);
   for (uint32_t i = 0; i < b->n; ++i) {
     orc_vote v = soa_vote(b, i);
     status[i] = flow_add_one(f, &v, code[i] == 0xFF ? -1 : code[i], sum_after ? sum_after + i : 0, fired ? fired + i : 0);
@@ -315,13 +318,15 @@ void orc_txvote_verify_soa(const orc_soa* b, const uint8_t* pubs32, const uint8_
   if (threads > 256) threads = 256;
   verify_job jobs[256];
   pthread_t th[256];
+  int started[256];
   for (int t = 0; t < threads; ++t) {
     jobs[t] = (verify_job){b, pubs32, chain_id, chain_len, out, (uint32_t)((uint64_t)b->n * t / threads),
                            (uint32_t)((uint64_t)b->n * (t + 1) / threads)};
-    if (threads == 1) soa_txvote_verify(&jobs[0]);
-    else pthread_create(&th[t], 0, soa_txvote_verify, &jobs[t]);
+    started[t] = threads > 1 && pthread_create(&th[t], 0, soa_txvote_verify, &jobs[t]) == 0;
+    if (!started[t]) soa_txvote_verify(&jobs[t]);
   }
-  if (threads > 1) for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  for (int t = 0; t < threads; ++t)
+    if (started[t]) pthread_join(th[t], 0);
 }
 
 int orc_flow_query(orc_flow* f, const uint8_t* txhash, uint32_t len, int64_t* sum, int32_t* maj23) {

@@ -60,7 +60,16 @@ def test_c2_full_size_matches_oracle(oracle_lib):
         ost, _, ofired = flow.add_batch(wl.batch, _cores())
         exp = _expected(ost, ofired)
         bad = np.nonzero(st != exp)[0]
-        assert len(bad) == 0, [(int(i), int(st[i]), int(exp[i])) for i in bad[:10]]
+        if len(bad):
+            # which side moved: the oracle again on one thread over the first 2,000 votes, and the
+            # device's own verdicts on them through txv_verify_batch with the registry keys
+            head = wl.head(2000)
+            o1, _, _ = oracle_lib.Flow(wl.pubs, wl.powers, b"test_chain_id").add_batch(head, 1)
+            pubs = np.frombuffer(b"".join(wl.pubs), np.uint8).reshape(-1, 32)[wl.val_of[:2000]]
+            dv = ctx.verify_batch(head, pubs)
+            raise AssertionError(f"{len(bad)} mismatches {[(int(i), int(st[i]), int(exp[i])) for i in bad[:10]]}; "
+                                 f"oracle 1-thread ADDED {int((o1 == 0).sum())}/2000, device verify ok "
+                                 f"{int((dv == 0).sum())}/2000, cores {_cores()}")
         assert sorted(int(e["vote_index"]) for e in ev) == _first_fired(wl.batch, ofired, set())
         hashes = [h.tobytes() for h in wl.hashes]
         ex, sums, maj, txkeys = ctx.query_txs(hashes)
