@@ -59,8 +59,11 @@ TXV_HD ge10_ext ge10_madd(const ge10_ext& p, const fe10& qp, const fe10& qm, con
 // prefetching K1b walk inside 128 VGPRs; mid() runs once all three are read (the walk issues its
 // next prefetch there, into the buffer just read)
 // kT = false: the last addition of a walk (its T is never read)
+// TXV_MUL_PAIRS=1: the 7 products as interleaved pairs (fe10_mul2).  Measured equal (589 vs 592M
+// votes/s, profiles/r02) and 20 VGPRs more (218 vs 198), which leaves no room for a K1a wave
+// beside two K1b waves on a SIMD: off by default
 #ifndef TXV_MUL_PAIRS
-#define TXV_MUL_PAIRS 1
+#define TXV_MUL_PAIRS 0
 #endif
 template <bool kT = true, class Rd, class Mid>
 TXV_HD ge10_ext ge10_madd_rd(const ge10_ext& p, Rd rd, bool neg, Mid mid) {

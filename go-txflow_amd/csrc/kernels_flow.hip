@@ -31,8 +31,8 @@
 //            first verified earlier -> signature compare with it; none -> invalid signature
 //   bucket   the ADDED votes of each set (<= one per validator) are listed in the set's cell row
 //   cross    one wave per set with ADDED votes: stake sum, and the arrival index at which the
-//            prefix (in arrival order) of the stake first reaches quorum, by binary lifting
-//            over the index bits; ADDED votes at or after it carry the fired bit
+//            prefix (in arrival order) of the stake first reaches quorum (per-lane prefix sums
+//            over the set's list in LDS, one wave min); ADDED votes at or after it fire
 //   events   compaction of the crossing votes in arrival order -> commit events
 //   out      final statuses (pre-check or tally) into mapped host memory
 #include <algorithm>
@@ -179,6 +179,15 @@ __device__ __forceinline__ bool key_matches(const uint8_t* stored, const uint8_t
   else return key_eq(stored, kp, len);
 }
 
+#ifndef TXV_ROUTE_SLEEP
+#define TXV_ROUTE_SLEEP 2
+#endif
+#if TXV_ROUTE_SLEEP
+#define TXV_ROUTE_BACKOFF() __builtin_amdgcn_s_sleep(TXV_ROUTE_SLEEP)
+#else
+#define TXV_ROUTE_BACKOFF() ((void)0)
+#endif
+
 // kRegs: the key is in registers (keys of <= 64 bytes), else compared from memory
 template <bool kRegs>
 __device__ __forceinline__ uint32_t set_find_or_insert(const FlowState& fs, const FlowBatch& b, uint64_t h,
@@ -214,7 +223,12 @@ __device__ __forceinline__ uint32_t set_find_or_insert(const FlowState& fs, cons
         return slot;
       }
       // lost the claim: re-read the slot in the next iteration
-    } else if (st != TXV_SE_BUSY) {
+      TXV_ROUTE_BACKOFF();
+    } else if (st == TXV_SE_BUSY) {
+      // another lane is writing this entry: give the SIMD's issue slots to it (and to K1b,
+      // which this kernel runs beside) instead of re-reading at once
+      TXV_ROUTE_BACKOFF();
+    } else {
       if ((uint32_t)(sl >> 32) == len && ld_sc1(w64(e, 0)) == h &&
           key_matches<kRegs>((st == TXV_SE_BATCH ? b.th : fs.keys) + (ld_sc1(w64(e, 2)) - 1), kp, kr, len)) {
         if (st == TXV_SE_BATCH && (uint32_t)ld_sc1(w64(e, 3)) > i) atomicMin(&e->first, i);
@@ -591,11 +605,11 @@ constexpr uint32_t kListCap = 512;   // ADDED votes of a set kept in LDS (every 
 // One wave per set that ADDED votes in this batch (the compacted touched list; persistent
 // waves): its ADDED votes are the cells of its row whose candidate carries this batch's stamp
 // (and held no accepted vote); stake sum, and the arrival index at which the prefix (in arrival
-// order) of the stake first reaches quorum, by binary lifting over the index bits; ADDED votes at
-// or after it fire.
+// order) of the stake first reaches quorum (per-lane prefix sums over the LDS list, one wave
+// min); ADDED votes at or after it fire.
 __global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b, uint32_t nb, uint32_t nb_sets) {
-  __shared__ uint32_t l_vote[4][kListCap];
-  __shared__ int64_t l_pow[4][kListCap];
+  __shared__ __attribute__((aligned(16))) uint32_t l_vote[4][kListCap + 4];
+  __shared__ __attribute__((aligned(16))) int64_t l_pow[4][kListCap + 4];
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t n_touched = fs.touched_blk[nb_sets];
@@ -637,22 +651,49 @@ __global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch
         // the largest t with prior + g(t) < quorum, found bit by bit; each probe is one list
         // pass + a wave sum
         const int64_t need = fs.quorum - prior;
-        uint32_t T = 0;
-        for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
-          const uint32_t cand = T | (1u << bit);
-          int64_t sm = 0;
-          if (in_lds) {
-            for (uint32_t c = lane; c < k; c += 64)
-              if (l_vote[wv][c] < cand) sm += l_pow[wv][c];
-          } else {
+        if (in_lds) {
+          // T = the smallest listed arrival index f_c whose prefix stake (every listed vote with
+          // f_j <= f_c) reaches need: each lane sums the prefix of its own entries with one pass
+          // over the list (LDS broadcast reads, independent iterations), then one wave min --
+          // no chain of dependent wave reductions (the kernel runs beside K1b, at a small share
+          // of the SIMDs' issue slots)
+          uint32_t T = TXV_NONE;
+          const uint32_t k4 = (k + 3u) & ~3u;        // the list padded to 4 with (never, 0)
+          if (lane < k4 - k) { l_vote[wv][k + lane] = 0xFFFFFFFFu; l_pow[wv][k + lane] = 0; }
+          __threadfence_block();
+          for (uint32_t c0 = 0; c0 < k; c0 += 128) {   // two entries per lane per pass
+            const uint32_t ca = c0 + lane, cb = c0 + 64 + lane;
+            const uint32_t fa = ca < k ? l_vote[wv][ca] : 0xFFFFFFFFu, fb = cb < k ? l_vote[wv][cb] : 0xFFFFFFFFu;
+            int64_t pa = 0, pb = 0;
+            const uint4* vq = reinterpret_cast<const uint4*>(l_vote[wv]);
+            const longlong2* pq = reinterpret_cast<const longlong2*>(l_pow[wv]);
+            for (uint32_t j = 0; j < k4; j += 4) {
+              const uint4 f4 = vq[j / 4];
+              const longlong2 p01 = pq[j / 2], p23 = pq[j / 2 + 1];
+              pa += (f4.x <= fa ? p01.x : 0) + (f4.y <= fa ? p01.y : 0) + (f4.z <= fa ? p23.x : 0) + (f4.w <= fa ? p23.y : 0);
+              pb += (f4.x <= fb ? p01.x : 0) + (f4.y <= fb ? p01.y : 0) + (f4.z <= fb ? p23.x : 0) + (f4.w <= fb ? p23.y : 0);
+            }
+            if (ca < k && pa >= need && fa < T) T = fa;
+            if (cb < k && pb >= need && fb < T) T = fb;
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) T = min(T, (uint32_t)__shfl_xor((int)T, o, 64));
+          cross = T;
+        } else {
+          // more ADDED votes than the LDS list holds: binary lifting over the arrival-index bits,
+          // one pass over the set's row per probe
+          uint32_t T = 0;
+          for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
+            const uint32_t cand = T | (1u << bit);
+            int64_t sm = 0;
             for (uint32_t v = lane; v < fs.n_vals; v += 64) {
               const uint32_t f = cand_of(row[v], b.stamp);
               if (f != TXV_NONE && f < cand && fs.acc[(size_t)s * fs.n_vals + v] == 0) sm += fs.power[v];
             }
+            if (wave_sum64(sm) < need) T = cand;
           }
-          if (wave_sum64(sm) < need) T = cand;
+          cross = T;
         }
-        cross = T;
       }
       // ADDED statuses with the fired bit, and the accepted-vote cells
       for (uint32_t v = lane; v < fs.n_vals; v += 64) {

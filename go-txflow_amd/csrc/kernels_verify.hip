@@ -137,7 +137,12 @@ __device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, 
 #ifndef TXV_K1A_WAVES
 #define TXV_K1A_WAVES 4
 #endif
-__global__ void __launch_bounds__(256, TXV_K1A_WAVES) txv_k_challenge(VerifyArgs a) {
+#ifdef TXV_K1A_VGPRS
+#define TXV_K1A_VGPR_ATTR __attribute__((amdgpu_num_vgpr(TXV_K1A_VGPRS)))
+#else
+#define TXV_K1A_VGPR_ATTR
+#endif
+__global__ void __launch_bounds__(256, TXV_K1A_WAVES) TXV_K1A_VGPR_ATTR txv_k_challenge(VerifyArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
   if (!(a.flags[i] & TXV_FLAG_PENDING)) { a.ok_out[i] = 0; return; }   // K1b may walk every vote
@@ -397,8 +402,13 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
 #ifndef TXV_V4_WAVES
 #define TXV_V4_WAVES 2
 #endif
+#ifdef TXV_K1B_VGPRS
+#define TXV_K1B_VGPR_ATTR __attribute__((amdgpu_num_vgpr(TXV_K1B_VGPRS)))
+#else
+#define TXV_K1B_VGPR_ATTR
+#endif
 template <int BLOCK, int WB, int WA, int V>
-__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) txv_k_scalarmult_multi(VerifyArgs a) {
+__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) TXV_K1B_VGPR_ATTR txv_k_scalarmult_multi(VerifyArgs a) {
   // lane group g = 64 w + l takes the work-list entries 64 V w + 64 h + l (h < V): the lanes of
   // a wave read 64 consecutive entries per vote slot, so the vote-column reads (sig, kbuf) of an
   // arrival-ordered list are two lines per column per wave
@@ -823,12 +833,28 @@ bool txv_verify_windows_supported(int wb, int wa) {
   return wa == 16 && (wb == 20 || wb == 22);
 }
 
+// K1a alone (the AddVote pipeline runs it on another stream than K1b, beside the previous
+// batch's K1b: K1b leaves ~116 VGPRs per SIMD free, room for one K1a wave)
+hipError_t txv_launch_challenge(const VerifyArgs* args, hipStream_t st) {
+  if (!args->n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
+  return hipGetLastError();
+}
+
 hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (!args->n) return hipSuccess;
   if (!txv_verify_windows_supported(wb, wa)) return hipErrorInvalidValue;
   // K1a stays a separate launch: fused into the 4-vote kernel (128-VGPR budget) the SHA-512
   // phase spilled and every wave hit its memory stalls at the same time (2.29 vs 2.12 ms)
-  hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
+  hipError_t e0 = txv_launch_challenge(args, st);
+  if (e0 != hipSuccess) return e0;
+  return txv_launch_scalarmult(wb, wa, args, grid, st);
+}
+
+// K1b (+ K1c in split mode) alone, after K1a wrote kbuf and the verdict flags
+hipError_t txv_launch_scalarmult(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st) {
+  if (!args->n) return hipSuccess;
+  if (!txv_verify_windows_supported(wb, wa)) return hipErrorInvalidValue;
   if (args->n_work) {
     constexpr int B = TXV_VERIFY_BLOCK;
     hipError_t e = hipSuccess;

@@ -187,17 +187,13 @@ struct txv_pool {
   bool cache_on = true;
   int64_t height = 0;
   std::mutex mu;                                   // proxyMtx
-  // the cache and the pool list are driven by different threads inside txv_pool_check: each on
-  // cache lines of its own
-  alignas(64) KeyList cache;                       // mapTxCache.list
-  alignas(64) FlatIndex cache_map{&cache};         // mapTxCache.map_
-  alignas(64) KeyList txs;                         // txs (clist of MempoolTxVote)
-  alignas(64) FlatIndex txs_map{&txs};             // txsMap
-  alignas(64) char pad_[1] = {0};
+  KeyList cache;                                   // mapTxCache.list
+  FlatIndex cache_map{&cache};                     // mapTxCache.map_
+  KeyList txs;                                     // txs (clist of MempoolTxVote)
+  FlatIndex txs_map{&txs};                         // txsMap
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
-  std::vector<uint32_t> admitted;                  // batch scratch: admitted votes in order
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -296,60 +292,29 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     for (uint32_t i = 0; i < (uint32_t)((uint64_t)n / nt); ++i) p->sizes[i] = vote_size(v, i);
     for (auto& x : th) x.join();
   }
-  // The sequential CheckTx loop, split over two threads.  The decision for vote i needs only the
-  // pool's running Size()/TxsBytes (counters of the votes admitted before it) and the cache, so
-  // this thread decides every vote and drives mapTxCache; a second thread replays the admitted
-  // votes into txs / txsMap in the same order (addTx), a few entries behind.  Both loops are
-  // DRAM-latency bound on their hash tables and prefetch ahead.
+  // The sequential CheckTx loop (DRAM-latency bound on the two hash tables: prefetched ahead).
+  // A two-thread split (decisions + cache on one thread, the admitted votes replayed into
+  // txs / txsMap on another) measured slower: 3.0 vs 2.4 ms per 64k votes
+  // (tools/debug/pool_ab.py, profiles/r02/pool_ab.log).
   constexpr uint32_t kAhead = 16;
   const uint32_t n = v->n;
-  std::vector<uint32_t>& adm = p->admitted;
-  adm.resize(n);
-  std::atomic<uint32_t> published{0};
-  std::atomic<bool> decided{false};
-  auto add_txs = [&] {
-    uint32_t j = 0;
-    for (;;) {
-      const uint32_t m = published.load(std::memory_order_acquire);
-      if (j == m) {
-        if (decided.load(std::memory_order_acquire) && j == published.load(std::memory_order_acquire)) break;
-        std::this_thread::yield();
-        continue;
-      }
-      for (; j < m; ++j) {
-        if (j + kAhead < m) p->txs_map.prefetch(keys[adm[j + kAhead]]);
-        const uint32_t i = adm[j];
-        p->txs_map.put(keys[i], p->txs.push_back(keys[i], p->sizes[i]));   // addTx (txsMap.Store overwrites)
-      }
-    }
-  };
-  const bool one_thread = getenv("TXV_POOL_ONE_THREAD") != nullptr;   // A/B knob
-  const bool two = n >= 4096 && !one_thread;
-  std::thread tb;
-  if (two) tb = std::thread(add_txs);
-  int64_t len_run = (int64_t)p->txs.len, bytes_run = p->txs_bytes;
-  uint32_t na = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    if (i + kAhead < n && p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
+    if (i + kAhead < n) {
+      if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);
+      p->txs_map.prefetch(keys[i + kAhead]);
+    }
     const uint32_t sz = p->sizes[i];   // 0: amino error (Size() swallows it)
-    if (len_run >= (int64_t)p->cfg.size || (int64_t)sz + bytes_run > (int64_t)p->cfg.max_txs_bytes) {
+    if ((int64_t)p->txs.len >= (int64_t)p->cfg.size || (int64_t)sz + p->txs_bytes > (int64_t)p->cfg.max_txs_bytes) {
       status_out[i] = TXV_POOL_ERR_FULL;
       continue;
     }
     if ((int64_t)sz > max_tx) { status_out[i] = TXV_POOL_ERR_TOO_LARGE; continue; }
     if (!p->cache_push(keys[i])) { status_out[i] = TXV_POOL_ERR_IN_CACHE; continue; }
     if (!sz && (p->cfg.flags & TXV_POOL_WAL)) { status_out[i] = TXV_POOL_ERR_ENCODING; continue; }
-    ++len_run;
-    bytes_run += sz;
+    p->txs_map.put(keys[i], p->txs.push_back(keys[i], sz));     // addTx (txsMap.Store overwrites)
+    p->txs_bytes += sz;
     status_out[i] = TXV_POOL_OK;
-    adm[na++] = i;
-    if (two && (na & 63) == 0) published.store(na, std::memory_order_release);
   }
-  published.store(na, std::memory_order_release);
-  decided.store(true, std::memory_order_release);
-  if (two) tb.join();
-  else add_txs();
-  p->txs_bytes = bytes_run;
   if (getenv("TXV_PROFILE_HOST")) {
     const auto t2 = std::chrono::steady_clock::now();
     fprintf(stderr, "[txv pool] keys=%.3fms lru=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),

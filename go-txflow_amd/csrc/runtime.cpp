@@ -44,6 +44,10 @@ namespace {
 inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32; }
 constexpr uint32_t kTableWords4 = 64 * 9 * 32;
 inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
+// K1a runs on the key stream (beside the previous batch's K1b) unless built with 0
+#ifndef TXV_K1A_ON_KEY_STREAM
+#define TXV_K1A_ON_KEY_STREAM 1
+#endif
 constexpr uint32_t kSlots = 5;   // 0-2 staged (0, 1 also the submit ring), 3 signer, 4 verify-only
 
 struct Slot {
@@ -86,9 +90,9 @@ struct Slot {
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
   FlowSummary* h_sum = nullptr; FlowSummary* m_sum = nullptr;
-  // copy stream: 3 upload done; key stream: 0 prep start, 1 prep + SignBytes done; verify
-  // stream: 7 K1a start, 2 verify done; flow stream: 4 results in host memory (+ commit sink), 5 tallied,
-  // 6 set keying done; 8 unused
+  // copy stream: 3 upload done; key stream: 0 prep start, 8 prep + SignBytes done (K1a starts),
+  // 1 K1a done; verify stream: 7 K1b start, 2 verify done; flow stream: 4 results in host memory
+  // (+ commit sink), 5 tallied, 6 set keying done
   hipEvent_t ev[9] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool launched = false;           // a chain was enqueued on this slot (its ev[4] marks the end)
   uint32_t* sink = nullptr;        // txv_set_commit_sink: packed commit state after each batch of this slot
@@ -699,8 +703,16 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
 // device times of a slot's last run (its events have completed): prep (+ SignBytes), verify,
 // tally after verify, and the whole chain from the prep's start
 int slot_kernel_ms(txv_ctx* c, Slot& s, float* ms) {
-  HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
-  HIP_TRY(c, hipEventElapsedTime(&ms[1], s.ev[7], s.ev[2]));
+  // prep + SignBytes; K1a + K1b (each on its own stream: their durations added)
+  float k1a = 0.f, k1b = 0.f;
+  if (TXV_K1A_ON_KEY_STREAM) {
+    HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[8]));
+    HIP_TRY(c, hipEventElapsedTime(&k1a, s.ev[8], s.ev[1]));
+  } else {
+    HIP_TRY(c, hipEventElapsedTime(&ms[0], s.ev[0], s.ev[1]));
+  }
+  HIP_TRY(c, hipEventElapsedTime(&k1b, s.ev[7], s.ev[2]));
+  ms[1] = k1a + k1b;
   HIP_TRY(c, hipEventElapsedTime(&ms[2], s.ev[2], s.ev[5]));
   HIP_TRY(c, hipEventElapsedTime(&ms[3], s.ev[0], s.ev[5]));
   return TXV_OK;
@@ -745,16 +757,24 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
   sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = nullptr; sa.nil = s.has_nil ? s.d_nil : nullptr;
   sa.msg = s.d_msg;
-  HIP_TRY(c, txv_flow_prep(&fs, &fb, ps));
-  HIP_TRY(c, txv_launch_signbytes(&sa, ps));
-  HIP_TRY(c, hipEventRecord(s.ev[1], ps));
-  HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
-  HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
   VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
   va.order = nullptr;          // arrival order; K1a marks the non-pending votes
   va.n_work = s.n;
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
-  HIP_TRY(c, txv_launch_verify(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
+  if (!txv_verify_windows_supported(c->b_w, c->tab_w)) { c->err = "verify windows"; return TXV_EDEVICE; }
+  HIP_TRY(c, txv_flow_prep(&fs, &fb, ps));
+  HIP_TRY(c, txv_launch_signbytes(&sa, ps));
+  // K1a on the key stream too: it runs beside the previous batch's K1b (one K1a wave fits in the
+  // VGPRs two K1b waves leave on a SIMD and fills K1b's idle issue cycles)
+  if (TXV_K1A_ON_KEY_STREAM) {
+    HIP_TRY(c, hipEventRecord(s.ev[8], ps));
+    HIP_TRY(c, txv_launch_challenge(&va, ps));
+  }
+  HIP_TRY(c, hipEventRecord(s.ev[1], ps));
+  HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
+  HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
+  if (!TXV_K1A_ON_KEY_STREAM) HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
+  HIP_TRY(c, txv_launch_scalarmult(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->vstream));
   HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
   HIP_TRY(c, txv_flow_new_ids(&fs, &fb, c->stream));

@@ -99,6 +99,9 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
 bool txv_verify_windows_supported(int wb, int wa);
 hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st);
+// the two halves of txv_launch_verify: K1a (challenge), then K1b (+ K1c in split mode)
+hipError_t txv_launch_challenge(const VerifyArgs* args, hipStream_t st);
+hipError_t txv_launch_scalarmult(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st);
 hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_t* btable, uint32_t* scal,
                              uint32_t* araw, uint32_t* prefix, uint32_t* pub, hipStream_t st);
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
