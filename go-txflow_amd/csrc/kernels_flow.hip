@@ -314,7 +314,13 @@ __global__ void __launch_bounds__(256) txv_k_route_prep(FlowState fs, FlowBatch 
                : (uint8_t)(TXV_FLAG_PENDING | (b.sig_len[i] == 64 ? TXV_FLAG_SIG64 : 0) | (L < 0 ? TXV_FLAG_BADMSG : 0));
 }
 
-// TxVoteSets[vote.TxHash], created on first sight for every non-nil vote (txflow/service.go:200-209)
+// TxVoteSets[vote.TxHash], created on first sight for every non-nil vote (txflow/service.go:200-209).
+// TXV_ROUTE_KEY_REGS=0 compares keys from memory (36 instead of 86 VGPRs), so that two route
+// waves fit beside K1b's on a SIMD; measured slower (573-604 vs 605-615M votes/s): the
+// co-resident waves cost K1b more than the route gains, so the key stays in registers
+#ifndef TXV_ROUTE_KEY_REGS
+#define TXV_ROUTE_KEY_REGS 1
+#endif
 __global__ void __launch_bounds__(256) txv_k_route_key(FlowState fs, FlowBatch b) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n) return;
@@ -326,7 +332,7 @@ __global__ void __launch_bounds__(256) txv_k_route_key(FlowState fs, FlowBatch b
   const uint32_t off = b.th_off[i];
   const uint8_t* kp = b.th + off;
   KeyRegs kr;
-  if (len <= kKeyRegBytes) {
+  if (TXV_ROUTE_KEY_REGS && len <= kKeyRegBytes) {
     load_key(kp, len, kr);
     b.entry[i] = set_find_or_insert<true>(fs, b, hash_regs(kr, len, fs.hash_seed), kp, kr, len, off, i);
   } else {
