@@ -568,6 +568,11 @@ def main():
                          "exec_achieved": None if exec_rate is None else round(exec_rate / 1e12, 3),
                          "exec_frac": None if exec_rate is None else round(exec_rate / VALU_PEAK, 4),
                          "pmc_source": pmc_src,
+                         "standalone": {"verify_ms": round(s_ms[1], 3),
+                                        "achieved": round(wl.n * W_ALG / (s_ms[1] * 1e-3) / 1e12, 3),
+                                        "frac": round(wl.n * W_ALG / (s_ms[1] * 1e-3) / VALU_PEAK, 4),
+                                        "note": "the same pair run alone after the timed region (no co-running "
+                                                "flow kernels)"},
                          "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"},
             "cpu_baseline": cpu,
             # the tally chain after verify (HBM-bound per BASELINE.md): bytes per launch from the same

@@ -44,9 +44,12 @@ namespace {
 inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32; }
 constexpr uint32_t kTableWords4 = 64 * 9 * 32;
 inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
-// K1a runs on the key stream (beside the previous batch's K1b) unless built with 0
+// TXV_K1A_ON_KEY_STREAM=1 runs K1a on the key stream, beside the previous batch's K1b (its 99
+// VGPRs do not fit beside two K1b waves, so it mostly fills K1b's tail): measured 614-621 vs
+// 608M votes/s (within box noise, profiles/r02/ab), while the two kernels' overlapping durations
+// no longer add up to the verify time; off: K1a then K1b on the verify stream
 #ifndef TXV_K1A_ON_KEY_STREAM
-#define TXV_K1A_ON_KEY_STREAM 1
+#define TXV_K1A_ON_KEY_STREAM 0
 #endif
 constexpr uint32_t kSlots = 5;   // 0-2 staged (0, 1 also the submit ring), 3 signer, 4 verify-only
 
@@ -764,8 +767,6 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   if (!txv_verify_windows_supported(c->b_w, c->tab_w)) { c->err = "verify windows"; return TXV_EDEVICE; }
   HIP_TRY(c, txv_flow_prep(&fs, &fb, ps));
   HIP_TRY(c, txv_launch_signbytes(&sa, ps));
-  // K1a on the key stream too: it runs beside the previous batch's K1b (one K1a wave fits in the
-  // VGPRs two K1b waves leave on a SIMD and fills K1b's idle issue cycles)
   if (TXV_K1A_ON_KEY_STREAM) {
     HIP_TRY(c, hipEventRecord(s.ev[8], ps));
     HIP_TRY(c, txv_launch_challenge(&va, ps));
