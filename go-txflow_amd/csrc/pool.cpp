@@ -296,7 +296,10 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   // A two-thread split (decisions + cache on one thread, the admitted votes replayed into
   // txs / txsMap on another) measured slower: 3.0 vs 2.4 ms per 64k votes
   // (tools/debug/pool_ab.py, profiles/r02/pool_ab.log).
-  constexpr uint32_t kAhead = 16;
+#ifndef TXV_POOL_AHEAD
+#define TXV_POOL_AHEAD 16
+#endif
+  constexpr uint32_t kAhead = TXV_POOL_AHEAD;
   const uint32_t n = v->n;
   for (uint32_t i = 0; i < n; ++i) {
     if (i + kAhead < n) {
