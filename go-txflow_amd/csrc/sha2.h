@@ -33,6 +33,37 @@ TXV_HD uint64_t shr64(uint64_t x, int n) {
   return x >> n;
 #endif
 }
+// three-input XOR and majority of 64-bit words: one v_bitop3_b32 per half on gfx950 (truth
+// tables 0x96 / 0xE8; symmetric in their inputs) instead of two v_xor_b32 / a bfi + xor
+#ifndef TXV_SHA_BITOP3
+#define TXV_SHA_BITOP3 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && TXV_SHA_BITOP3
+// (lo, hi) words as one 64-bit register pair (an OR of shifted halves lowers to v_lshl_add_u64)
+__device__ __forceinline__ uint64_t pair64(uint32_t lo, uint32_t hi) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 v;
+  v.x = lo;
+  v.y = hi;
+  return __builtin_bit_cast(uint64_t, v);
+}
+#endif
+TXV_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && TXV_SHA_BITOP3
+  return pair64(__builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96),
+                __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96));
+#else
+  return a ^ b ^ c;
+#endif
+}
+TXV_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && TXV_SHA_BITOP3
+  return pair64(__builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8),
+                __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8));
+#else
+  return (a & b) | (c & (a | b));
+#endif
+}
 TXV_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 TXV_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -82,18 +113,18 @@ TXV_HD void sha512_init(uint64_t st[8]) {
     uint64_t wi;                                                                           \
     if (SCHED) {                                                                           \
       const uint64_t w15 = w[((J) + 1) & 15], w2 = w[((J) + 14) & 15];                      \
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);                 \
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);                  \
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));           \
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));            \
       wi = w[(J) & 15] + s0 + w[((J) + 9) & 15] + s1;                                      \
       w[(J) & 15] = wi;                                                                    \
     } else {                                                                               \
       wi = w[J];                                                                           \
     }                                                                                      \
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);                     \
+    const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));              \
     const uint64_t ch = g ^ (e & (f ^ g));                                                 \
     const uint64_t t1 = h + S1 + ch + sha512_k(I) + wi;                                     \
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);                     \
-    const uint64_t mj = (a & b) | (c & (a | b));                                           \
+    const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));              \
+    const uint64_t mj = maj64(a, b, c);                                                    \
     const uint64_t t2 = S0 + mj;                                                           \
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;                    \
   }
