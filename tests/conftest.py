@@ -26,10 +26,11 @@ def oracle_lib():
                 ids=["wauto", "w4", "w8v2", "w12v4", "wauto_split", "w12_split", "wauto_v8"])
 def gpu_ctx(request):
     """One context per verify-table window: auto (radix-2^16 for the small test registries,
-    4 votes per lane, radix-2^24 base table), radix-16 LDS-resident B table, radix-256 with
-    the LDS-parked pair kernel, radix-4096 with 4 votes per lane, and the split K1b/K1c
-    path (points kernel + batched-inversion encode) over the auto and radix-4096 tables, and 8
-    votes per lane (the kernel the library picks by itself for batches of >= 768K votes)."""
+    radix-2^24 base table, and for these small batches the split K1b/K1c path the library picks
+    below 768K votes), radix-16 LDS-resident B table, radix-256 with the LDS-parked pair kernel,
+    radix-4096 with 4 votes per lane, the split path configured explicitly over the auto and
+    radix-4096 tables, and 8 votes per lane (the kernel the library picks by itself for batches
+    of >= 768K votes)."""
     import txflow_amd as T
     w, lv = request.param
     ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256, table_w=w, lane_votes=lv)
