@@ -39,6 +39,11 @@ import numpy as np  # noqa: E402
 # Roofline of the verify pair (K1a + K1b), integer VALU.  Peak = 256 CU x 4 SIMD x 32 lanes/clk x
 # 2.4 GHz (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle)").
 VALU_PEAK = 256 * 4 * 32 * 2.4e9
+# Algorithmic HBM bytes per verified vote of the verify pair: 23 table entries of
+# 128 B (11 base-point + 13 validator positions - 1 starting entry), the signature (64 B), the
+# SignBytes words (2 SHA-512 blocks' worth of message, 128 B), k written and read (2 x 32 B), the
+# parked points of V = 8 (7/8 of a vote parks 128 B, written and read back), the verdict (1 B)
+VERIFY_ALG_BYTES = 23 * 128 + 64 + 128 + 2 * 32 + 7 / 8 * 2 * 128 + 1
 # Algorithmic int32 lane-ops per verified vote of the algorithm that runs:
 #   SHA-512 of R||A||SignBytes, 2 blocks + ScReduce                      1.1e4
 #   [s]B + [k](-A) over fixed-base tables: 11 + 13 mixed additions x 7 FM   168 FM
@@ -398,7 +403,7 @@ def main():
     # the same batch in the three device slots: step k runs in slot k % 3 with up to three steps
     # enqueued, so step k+1's prep runs beside step k's K1b and its K1a/K1b beside step k's tally
     # (txv_run_staged returns as soon as the chain is enqueued)
-    DEPTH = 3
+    DEPTH = int(os.environ.get("TXV_BENCH_DEPTH", "3"))   # 2..4 staged slots
     for sl in range(DEPTH):
         ctx.stage(sl, wl.batch)
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
@@ -562,6 +567,8 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
                          "unit": "Tlane-op/s (int32 VALU issue)", "frac": round(achieved / VALU_PEAK, 4),
                          "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_multi (verify pair)",
+                         "alg_bytes_per_launch": round(wl.n * VERIFY_ALG_BYTES),
+                         "traffic_over_alg_bytes": None if not traffic else round(traffic / (wl.n * VERIFY_ALG_BYTES), 3),
                          "alg_lane_ops_per_vote": W_ALG,
                          "alg_source": "DESIGN.md §4: SHA-512 2 blocks + ScReduce + 181 field multiplies x 100",
                          "exec_lane_slots_per_vote": w_exec,

@@ -51,7 +51,7 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #ifndef TXV_K1A_ON_KEY_STREAM
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
-constexpr uint32_t kSlots = 5;   // 0-2 staged (0, 1 also the submit ring), 3 signer, 4 verify-only
+constexpr uint32_t kSlots = 6;   // 0-3 staged (0, 1 also the submit ring), 4 signer, 5 verify-only
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;

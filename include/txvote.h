@@ -260,10 +260,10 @@ int txv_sign_votes(txv_ctx* ctx, const txv_votes* votes, const uint32_t* signer,
  * TxFlow owns, so it starts as soon as its columns are uploaded, while the previous batch's
  * tally still runs; its TxFlow chain (TxHash keying, new set ids, tally) follows the previous
  * batch's on one stream, so results are those of the batches in submission order.
- * txv_stage: upload a batch's raw columns into device slot `slot` (0, 1 or 2; TXV_ESTATE while
- *   the slot holds a txv_submit_votes batch: the submit ring uses slots 0 and 1).
+ * txv_stage: upload a batch's raw columns into device slot `slot` (0-3; TXV_ESTATE while the
+ *   slot holds a txv_submit_votes batch: the submit ring uses slots 0 and 1).
  * txv_run_staged: enqueue the whole AddVote kernel chain on the staged batch and return (all
- *   three slots may be in flight: run 0, run 1, run 2, fetch 0, run 0, fetch 1, ...; a slot's
+ *   four slots may be in flight: run 0, run 1, run 2, fetch 0, run 0, fetch 1, ...; a slot's
  *   next chain waits on the device for its previous one); results land in host memory for
  *   txv_fetch_staged.  kernel_ms_out (optional, 4 entries; makes the call
  *   wait): prep + SignBytes / verify (K1a + K1b) / tally after verify / total device time of
@@ -286,7 +286,7 @@ uint64_t txv_commit_state_bytes(uint32_t n_sets_cap);
 /* this context's state into caller device memory (e.g. an RCCL all-gather buffer) */
 int txv_pack_commit_state(txv_ctx* ctx, void* dst_dev, uint32_t n_sets_cap);
 /* the same packed state written by the device at the end of every batch that runs in slot
- * `slot` (0-2: staged slot, or the txv_submit_votes ticket t with (t - 1) % 2 == slot), in
+ * `slot` (0-3: staged slot, or the txv_submit_votes ticket t with (t - 1) % 2 == slot), in
  * stream order before the batch's results are reported: once txv_fetch_staged / txv_wait_votes
  * returns for the batch, dst_dev holds the state as of that batch, even when the next batch is
  * already running.  dst_dev = NULL removes the sink.  For an all-gather per batch with two
