@@ -18,6 +18,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -44,7 +45,15 @@ inline uint64_t hash_bytes(const uint8_t* p, uint32_t n, uint64_t seed) {
 class WorkerPool {
  public:
   explicit WorkerPool(unsigned n) {
-    for (unsigned t = 1; t < n; ++t) th_.emplace_back([this] { loop(); });
+    // a thread that cannot be created (EAGAIN under a process/thread limit) leaves a smaller
+    // pool; parallel_for runs inline with none
+    for (unsigned t = 1; t < n; ++t) {
+      try {
+        th_.emplace_back([this] { loop(); });
+      } catch (const std::system_error&) {
+        break;
+      }
+    }
   }
   ~WorkerPool() {
     {

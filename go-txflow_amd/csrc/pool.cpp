@@ -27,6 +27,7 @@
 #include <cstring>
 #include <sys/mman.h>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <algorithm>
 #include <atomic>
@@ -284,11 +285,17 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   {
     const uint32_t n = v->n, nt = std::max(1u, std::min<uint32_t>(8, n / 8192));
     std::vector<std::thread> th;
-    for (uint32_t t = 1; t < nt; ++t)
-      th.emplace_back([&, t] {
+    for (uint32_t t = 1; t < nt; ++t) {
+      auto part = [&, t] {
         for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i)
           p->sizes[i] = vote_size(v, i);
-      });
+      };
+      try {
+        th.emplace_back(part);
+      } catch (const std::system_error&) {
+        part();   // no thread to spare: the range runs here
+      }
+    }
     for (uint32_t i = 0; i < (uint32_t)((uint64_t)n / nt); ++i) p->sizes[i] = vote_size(v, i);
     for (auto& x : th) x.join();
   }
@@ -436,15 +443,21 @@ int txv_encode_msgs(const txv_votes* v, const uint8_t* txkey, const uint8_t* sig
   const uint32_t n = v->n;
   const uint32_t nt = std::max(1u, std::min<uint32_t>(16, n / 16384));
   std::vector<std::thread> th;
-  for (uint32_t t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
+  for (uint32_t t = 0; t < nt; ++t) {
+    auto part = [&, t] {
       for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i) {
         const uint8_t* sig = v->sig_len[i] > 64 ? sig_full + sig_full_off[i] : v->sig + (size_t)i * 64;
         txv_host::txvote_msg(out + off_out[i], prefix, v->height[i], v->txhash + v->txhash_off[i], v->txhash_len[i],
                              txkey ? txkey + (size_t)i * 32 : nullptr, v->ts_sec[i], v->ts_nanos[i],
                              v->addr + (size_t)i * 20, v->addr_len[i], sig, v->sig_len[i]);
       }
-    });
+    };
+    try {
+      th.emplace_back(part);
+    } catch (const std::system_error&) {
+      part();
+    }
+  }
   for (auto& x : th) x.join();
   return TXV_OK;
 }

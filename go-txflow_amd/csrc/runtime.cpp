@@ -30,6 +30,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <system_error>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -1797,7 +1798,13 @@ int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len
       shard_out[i] = h[0] % n_shards;
     }
   };
-  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work, t);
+  for (uint32_t t = 1; t < nt; ++t) {
+    try {
+      th.emplace_back(work, t);
+    } catch (const std::system_error&) {
+      work(t);   // no thread to spare: the range runs here
+    }
+  }
   work(0);
   for (auto& x : th) x.join();
   return TXV_OK;
