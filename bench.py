@@ -349,8 +349,10 @@ def load_pmc(table_w: int, n_votes: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # 30 steps by default: the timed region starts from an empty pipeline and ends drained, and
+    # that fill / drain (about one batch's latency) is amortised over the steps (48 ms in all)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--validators", type=int, default=100)
     ap.add_argument("--txs-per-gpu", type=int, default=0,
                     help="0 = 10,000 at N=1 (C2) / 20,000 at N>1 (C3: 160k txs at N=8)")
