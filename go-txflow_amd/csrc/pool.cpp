@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <sys/mman.h>
+#include <functional>
 #include <mutex>
 #include <system_error>
 #include <thread>
@@ -223,6 +224,7 @@ int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig
 }  // namespace
 
 void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // runtime.cpp
+void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn);   // runtime.cpp
 
 namespace {
 
@@ -284,20 +286,10 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   p->sizes.resize(v->n);
   {
     const uint32_t n = v->n, nt = std::max(1u, std::min<uint32_t>(8, n / 8192));
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < nt; ++t) {
-      auto part = [&, t] {
-        for (uint32_t i = (uint32_t)((uint64_t)n * t / nt); i < (uint32_t)((uint64_t)n * (t + 1) / nt); ++i)
-          p->sizes[i] = vote_size(v, i);
-      };
-      try {
-        th.emplace_back(part);
-      } catch (const std::system_error&) {
-        part();   // no thread to spare: the range runs here
-      }
-    }
-    for (uint32_t i = 0; i < (uint32_t)((uint64_t)n / nt); ++i) p->sizes[i] = vote_size(v, i);
-    for (auto& x : th) x.join();
+    (void)nt;
+    txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
+    });
   }
   // The sequential CheckTx loop (DRAM-latency bound on the two hash tables: prefetched ahead).
   // A two-thread split (decisions + cache on one thread, the admitted votes replayed into

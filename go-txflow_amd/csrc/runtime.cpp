@@ -1844,6 +1844,13 @@ static void sha256_host(const uint8_t* p, uint64_t n, uint8_t out[32]) {
 // internal (pool.cpp): SHA-256 on the host
 void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]) { sha256_host(p, n, out); }
 
+// the context's persistent host workers for pool.cpp's order-independent passes (no thread
+// creation per call)
+void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn) {
+  if (c && c->pool) c->pool->parallel_for(n, fn, 4096);
+  else if (n) fn(0, n);
+}
+
 extern "C" {
 
 int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
