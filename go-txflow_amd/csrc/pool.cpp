@@ -27,6 +27,7 @@
 #include <cstring>
 #include <sys/mman.h>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <system_error>
 #include <thread>
@@ -182,6 +183,28 @@ struct KeyList {
 
 inline const Key& FlatIndex::key_of(int32_t idx) const { return owner->nodes[idx].k; }
 
+// kParts independent FlatIndex tables, chosen by hash bits the in-table slot does not use: the
+// same sequential API, and a batch can be inserted by several threads, each owning whole
+// partitions (txv_pool_check's fast path)
+constexpr uint32_t kParts = 16;
+struct PartIndex {
+  std::vector<std::unique_ptr<FlatIndex>> p;
+  explicit PartIndex(const KeyList* o) {
+    for (uint32_t i = 0; i < kParts; ++i) p.emplace_back(new FlatIndex(o));
+  }
+  static uint32_t part(const Key& k) { return (uint32_t)(FlatIndex::h(k) >> 40) & (kParts - 1); }
+  FlatIndex& of(const Key& k) { return *p[part(k)]; }
+  const FlatIndex& of(const Key& k) const { return *p[part(k)]; }
+  void prefetch(const Key& k) const { of(k).prefetch(k); }
+  int32_t find(const Key& k) const { return of(k).find(k); }
+  template <typename F>
+  int32_t find_or_insert(const Key& k, F&& make_idx) { return of(k).find_or_insert(k, make_idx); }
+  void put(const Key& k, int32_t idx) { of(k).put(k, idx); }
+  bool erase(const Key& k) { return of(k).erase(k); }
+  void clear() { for (auto& f : p) f->clear(); }
+  void reserve(size_t m) { for (auto& f : p) f->reserve(m / kParts + m / (4 * kParts) + 64); }
+};
+
 }  // namespace
 
 struct txv_pool {
@@ -190,12 +213,13 @@ struct txv_pool {
   int64_t height = 0;
   std::mutex mu;                                   // proxyMtx
   KeyList cache;                                   // mapTxCache.list
-  FlatIndex cache_map{&cache};                     // mapTxCache.map_
+  PartIndex cache_map{&cache};                     // mapTxCache.map_
   KeyList txs;                                     // txs (clist of MempoolTxVote)
-  FlatIndex txs_map{&txs};                         // txsMap
+  PartIndex txs_map{&txs};                         // txsMap
   int64_t txs_bytes = 0;
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
+  std::vector<int32_t> idx_c, idx_t;               // batch scratch: node indices (fast path)
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -224,7 +248,38 @@ int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig
 }  // namespace
 
 void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // runtime.cpp
-void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn);   // runtime.cpp
+void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn,
+                           uint32_t min_chunk = 4096);   // runtime.cpp (the context's host workers)
+
+namespace {
+
+// node indices a KeyList hands out to its next n push_backs (free list from the back first)
+void next_indices(const KeyList& L, uint32_t n, std::vector<int32_t>& idx) {
+  idx.resize(n);
+  const size_t nf = L.free_.size();
+  for (uint32_t i = 0; i < n; ++i)
+    idx[i] = i < nf ? L.free_[nf - 1 - i] : (int32_t)(L.nodes.size() + (i - nf));
+}
+
+// the n nodes at idx (keys already written) appended in order: links (on the host workers),
+// head / tail, free list
+void link_appended(txv_ctx* ctx, KeyList& L, const std::vector<int32_t>& idx, uint32_t n) {
+  const int32_t tail = L.tail;
+  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      KeyList::Node& nd = L.nodes[idx[i]];
+      nd.prev = i ? idx[i - 1] : tail;
+      nd.next = i + 1 < n ? idx[i + 1] : -1;
+    }
+  });
+  if (L.tail >= 0) L.nodes[L.tail].next = idx[0]; else L.head = idx[0];
+  L.tail = idx[n - 1];
+  L.len += n;
+  const size_t nf = L.free_.size();
+  L.free_.resize(nf - std::min<size_t>(nf, n));
+}
+
+}  // namespace
 
 namespace {
 
@@ -245,6 +300,92 @@ void txvote_msg_disfix(uint8_t disamb[3], uint8_t prefix[4]) {
 inline uint32_t vote_size(const txv_votes* v, uint32_t i) {
   return (uint32_t)txv_host::txvote_size(v->height[i], v->txhash_len[i], v->ts_sec[i], v->ts_nanos[i], v->addr_len[i],
                                          v->sig_len[i]);
+}
+
+}  // namespace
+
+namespace {
+
+bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, int64_t max_tx, uint8_t* status_out) {
+  // the caps no vote may reach (txvotepool.go:192-261 in order: full, too large, cache, WAL)
+  std::atomic<uint64_t> sum_a{0};
+  std::atomic<bool> capped{false};
+  std::vector<uint8_t> part(n);
+  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+    uint64_t sm = 0;
+    bool cp = false;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t sz = p->sizes[i];
+      cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
+      sm += sz;
+      part[i] = (uint8_t)PartIndex::part(keys[i]);
+    }
+    sum_a += sm;
+    if (cp) capped = true;
+  });
+  if (capped) return false;
+  const uint64_t sum = sum_a.load();
+  if ((int64_t)p->txs.len + (int64_t)n > (int64_t)p->cfg.size) return false;
+  if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;
+  if (p->cache_on && (uint64_t)p->cache.len + n > (uint64_t)p->cfg.cache_size) return false;
+  // batch order per partition
+  std::vector<uint32_t> cnt(kParts + 1, 0), order(n);
+  for (uint32_t i = 0; i < n; ++i) ++cnt[part[i] + 1];
+  for (uint32_t q = 0; q < kParts; ++q) cnt[q + 1] += cnt[q];
+  {
+    std::vector<uint32_t> at(cnt.begin(), cnt.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) order[at[part[i]]++] = i;
+  }
+  auto per_part = [&](const std::function<void(uint32_t)>& fn) {
+    txv_host_parallel_for(ctx, kParts, [&](uint32_t lo, uint32_t hi) { for (uint32_t q = lo; q < hi; ++q) fn(q); }, 1);
+  };
+  // node keys first (the indices compare keys through the nodes), links only once admitted
+  const size_t old_c = p->cache.nodes.size(), old_t = p->txs.nodes.size();
+  next_indices(p->cache, n, p->idx_c);
+  next_indices(p->txs, n, p->idx_t);
+  // the last index is the highest new one whenever the free list runs out
+  if (p->cache_on) p->cache.nodes.resize(std::max<size_t>(old_c, (size_t)p->idx_c[n - 1] + 1));
+  p->txs.nodes.resize(std::max<size_t>(old_t, (size_t)p->idx_t[n - 1] + 1));
+  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      if (p->cache_on) { KeyList::Node& c = p->cache.nodes[p->idx_c[i]]; c.k = keys[i]; c.size = 0; }
+      KeyList::Node& t = p->txs.nodes[p->idx_t[i]]; t.k = keys[i]; t.size = p->sizes[i];
+    }
+  });
+  if (p->cache_on) {
+    std::atomic<bool> clash{false};
+    per_part([&](uint32_t q) {   // mapTxCache.Push of every key: all must be new
+      FlatIndex& f = *p->cache_map.p[q];
+      for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
+        const uint32_t i = order[j];
+        if (f.find_or_insert(keys[i], [&] { return p->idx_c[i]; }) >= 0) { clash = true; return; }
+      }
+    });
+    if (clash) {   // undo: erase the keys this batch inserted, drop the new nodes
+      per_part([&](uint32_t q) {
+        FlatIndex& f = *p->cache_map.p[q];
+        for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
+          const uint32_t i = order[j];
+          if (f.find(keys[i]) == p->idx_c[i]) f.erase(keys[i]);
+        }
+      });
+      p->cache.nodes.resize(old_c);
+      p->txs.nodes.resize(old_t);
+      return false;
+    }
+    link_appended(ctx, p->cache, p->idx_c, n);
+  }
+  per_part([&](uint32_t q) {     // addTx: txsMap.Store of every key
+    FlatIndex& f = *p->txs_map.p[q];
+    for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
+      const uint32_t i = order[j];
+      f.put(keys[i], p->idx_t[i]);
+    }
+  });
+  link_appended(ctx, p->txs, p->idx_t, n);
+  p->txs_bytes += (int64_t)sum;
+  memset(status_out, TXV_POOL_OK, n);
+  return true;
 }
 
 }  // namespace
@@ -284,12 +425,23 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
   // TxVote.Size() of every vote on the worker threads (order-independent)
   p->sizes.resize(v->n);
-  {
-    const uint32_t n = v->n, nt = std::max(1u, std::min<uint32_t>(8, n / 8192));
-    (void)nt;
-    txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
-    });
+  const uint32_t n = v->n;
+  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
+  });
+  // Fast path: when no vote of the batch can hit a size cap, a cache eviction or the WAL rule,
+  // the sequential loop would admit every vote whose key is new -- so if every key is new (in
+  // the cache and within the batch) the result is "all admitted, in order".  The keys go into
+  // the partitioned cache and pool indices on the context's host workers (one worker per
+  // partition, batch order within it); a key found present undoes the batch's inserts and the
+  // sequential loop below decides instead.
+  if (n >= 4096 && try_batch_admit(p, ctx, keys, n, max_tx, status_out)) {
+    if (getenv("TXV_PROFILE_HOST")) {
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr, "[txv pool] keys=%.3fms batch-admit=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(), v->n);
+    }
+    return TXV_OK;
   }
   // The sequential CheckTx loop (DRAM-latency bound on the two hash tables: prefetched ahead).
   // A two-thread split (decisions + cache on one thread, the admitted votes replayed into
@@ -299,7 +451,6 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
 #define TXV_POOL_AHEAD 16
 #endif
   constexpr uint32_t kAhead = TXV_POOL_AHEAD;
-  const uint32_t n = v->n;
   for (uint32_t i = 0; i < n; ++i) {
     if (i + kAhead < n) {
       if (p->cache_on) p->cache_map.prefetch(keys[i + kAhead]);

@@ -1846,8 +1846,9 @@ void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]) { sha256_ho
 
 // the context's persistent host workers for pool.cpp's order-independent passes (no thread
 // creation per call)
-void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn) {
-  if (c && c->pool) c->pool->parallel_for(n, fn, 4096);
+void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn,
+                           uint32_t min_chunk) {
+  if (c && c->pool) c->pool->parallel_for(n, fn, min_chunk);
   else if (n) fn(0, n);
 }
 

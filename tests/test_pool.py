@@ -207,3 +207,56 @@ def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
         assert pool.Size() == 0 and pool.TxsBytes() == 0 and len(pool.cache_keys()) == 0
     finally:
         pool.close()
+
+
+@pytest.mark.gpu
+def test_pool_batch_admit_matches_oracle(oracle_lib):
+    """Batches of >= 4096 votes take txv_pool_check's batch-admit path (every key new, no cap
+    reachable: keys inserted into the partitioned indices on the host workers); a key already
+    cached, a key repeated inside the batch, or a batch that would evict from the cache falls
+    back to the sequential loop after undoing the inserts.  Every outcome, Size, TxsBytes,
+    ReapMaxTxs order and the LRU order equal the oracle's, including node reuse after Update."""
+    import txflow_amd as T
+    rnd = random.Random(77)
+    ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
+    cfg = dict(size=100000, cache_size=30000)
+    pool = T.TxVotePool(ctx, **cfg)
+    ref = oracle_lib.Pool(**cfg)
+
+    def fresh(n):
+        return [vote(bytes(rnd.getrandbits(8) for _ in range(64)), ts=(1_700_000_000, 1 + i)) for i in range(n)]
+
+    def check(votes):
+        b, long_sigs = _batch(T, votes)
+        st = pool.check_batch(b, long_sigs)
+        exp = ref.check(votes)
+        assert np.array_equal(st, exp), np.nonzero(st != exp)[0][:10]
+        assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+        for m in (-1, 0, 33):
+            gk, gs = pool.reap(m)
+            ok, os_ = ref.reap(m)
+            assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+        assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+        return st
+
+    try:
+        first = fresh(6000)
+        assert (check(first) == OK).all()                       # batch-admit
+        committed = rnd.sample(first, 1500)                      # Update: pool nodes to the free list
+        cb, clong = _batch(T, committed)
+        pool.update(1, cb, clong)
+        ref.update(1, committed)
+        assert (check(fresh(5000)) == OK).all()                  # batch-admit reusing freed nodes
+        again = fresh(5000)
+        again[2500] = dict(first[10])                            # an already cached key
+        st = check(again)
+        assert st[2500] == IN_CACHE and (np.delete(st, 2500) == OK).all()
+        dup = fresh(5000)
+        dup[4000] = dict(dup[7])                                 # a key repeated inside the batch
+        st = check(dup)
+        assert st[4000] == IN_CACHE and (np.delete(st, 4000) == OK).all()
+        st = check(fresh(12000))                                 # the cache (30000) would evict
+        assert (st == OK).all() and len(pool.cache_keys()) == 30000
+    finally:
+        pool.close()
+        ctx.close()
