@@ -220,6 +220,7 @@ struct txv_pool {
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
   std::vector<int32_t> idx_c, idx_t;               // batch scratch: node indices (fast path)
+  std::vector<uint8_t> part;                       // batch scratch: index partition per key (fast path)
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -306,25 +307,15 @@ inline uint32_t vote_size(const txv_votes* v, uint32_t i) {
 
 namespace {
 
-bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, int64_t max_tx, uint8_t* status_out) {
+// slots prefetched ahead in the per-partition insert loops (DRAM-latency bound, as the sequential loop)
+constexpr uint32_t kAdmitAhead = 16;
+
+// sum = the batch's summed sizes; capped = some vote is too large or hits the WAL rule; part[i] =
+// vote i's index partition (all from the sizes pass in txv_pool_check)
+bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint64_t sum, bool capped,
+                     const uint8_t* part, uint8_t* status_out) {
   // the caps no vote may reach (txvotepool.go:192-261 in order: full, too large, cache, WAL)
-  std::atomic<uint64_t> sum_a{0};
-  std::atomic<bool> capped{false};
-  std::vector<uint8_t> part(n);
-  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-    uint64_t sm = 0;
-    bool cp = false;
-    for (uint32_t i = lo; i < hi; ++i) {
-      const uint32_t sz = p->sizes[i];
-      cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
-      sm += sz;
-      part[i] = (uint8_t)PartIndex::part(keys[i]);
-    }
-    sum_a += sm;
-    if (cp) capped = true;
-  });
   if (capped) return false;
-  const uint64_t sum = sum_a.load();
   if ((int64_t)p->txs.len + (int64_t)n > (int64_t)p->cfg.size) return false;
   if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;
   if (p->cache_on && (uint64_t)p->cache.len + n > (uint64_t)p->cfg.cache_size) return false;
@@ -357,6 +348,7 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, int
     per_part([&](uint32_t q) {   // mapTxCache.Push of every key: all must be new
       FlatIndex& f = *p->cache_map.p[q];
       for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
+        if (j + kAdmitAhead < cnt[q + 1]) f.prefetch(keys[order[j + kAdmitAhead]]);
         const uint32_t i = order[j];
         if (f.find_or_insert(keys[i], [&] { return p->idx_c[i]; }) >= 0) { clash = true; return; }
       }
@@ -378,6 +370,7 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, int
   per_part([&](uint32_t q) {     // addTx: txsMap.Store of every key
     FlatIndex& f = *p->txs_map.p[q];
     for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
+      if (j + kAdmitAhead < cnt[q + 1]) f.prefetch(keys[order[j + kAdmitAhead]]);
       const uint32_t i = order[j];
       f.put(keys[i], p->idx_t[i]);
     }
@@ -424,10 +417,27 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
   // TxVote.Size() of every vote on the worker threads (order-independent)
+  // (and for the fast path: the summed sizes, the too-large / WAL caps, each key's partition)
   p->sizes.resize(v->n);
   const uint32_t n = v->n;
+  const bool fast = n >= 4096;
+  if (fast) p->part.resize(n);
+  std::atomic<uint64_t> sum_a{0};
+  std::atomic<bool> capped{false};
   txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
+    uint64_t sm = 0;
+    bool cp = false;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t sz = vote_size(v, i);
+      p->sizes[i] = sz;
+      if (!fast) continue;
+      cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
+      sm += sz;
+      p->part[i] = (uint8_t)PartIndex::part(keys[i]);
+    }
+    if (!fast) return;
+    sum_a += sm;
+    if (cp) capped = true;
   });
   // Fast path: when no vote of the batch can hit a size cap, a cache eviction or the WAL rule,
   // the sequential loop would admit every vote whose key is new -- so if every key is new (in
@@ -435,7 +445,7 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   // the partitioned cache and pool indices on the context's host workers (one worker per
   // partition, batch order within it); a key found present undoes the batch's inserts and the
   // sequential loop below decides instead.
-  if (n >= 4096 && try_batch_admit(p, ctx, keys, n, max_tx, status_out)) {
+  if (fast && try_batch_admit(p, ctx, keys, n, sum_a.load(), capped.load(), p->part.data(), status_out)) {
     if (getenv("TXV_PROFILE_HOST")) {
       const auto t2 = std::chrono::steady_clock::now();
       fprintf(stderr, "[txv pool] keys=%.3fms batch-admit=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),

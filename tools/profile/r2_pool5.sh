@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r2_pool5
+O=gpurun_out/${1:-r2_pool5}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_pool.py tests/test_configs.py -m gpu -x -q --timeout 200 --timeout-method thread -k "pool or c5" > $O/pool_tests.log 2>&1 || { echo POOLTESTFAIL; tail -40 $O/pool_tests.log; exit 1; }
 tail -1 $O/pool_tests.log
