@@ -260,3 +260,38 @@ def test_pool_batch_admit_matches_oracle(oracle_lib):
     finally:
         pool.close()
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
+    """The batch-admit path without a cache (a key repeated inside the batch is admitted twice,
+    txsMap.Store keeping the later node), and batches the size / byte caps cut off (sequential
+    loop: ErrMempoolIsFull from the cap on): outcomes, Size, TxsBytes and ReapMaxTxs equal the
+    oracle's."""
+    import txflow_amd as T
+    rnd = random.Random(78)
+    ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
+
+    def fresh(n):
+        return [vote(bytes(rnd.getrandbits(8) for _ in range(64)), ts=(1_700_000_000, 1 + i)) for i in range(n)]
+
+    for cfg in (dict(size=20000, cache_size=0xFFFFFFFF), dict(size=9000, cache_size=50000),
+                dict(size=100000, cache_size=50000, max_txs_bytes=1_000_000)):
+        pool = T.TxVotePool(ctx, **cfg)
+        ref = oracle_lib.Pool(**cfg)
+        try:
+            for votes in (fresh(6000), fresh(6000), fresh(5000)):
+                if cfg["cache_size"] == 0xFFFFFFFF:
+                    votes[3000] = dict(votes[11])
+                b, long_sigs = _batch(T, votes)
+                st = pool.check_batch(b, long_sigs)
+                exp = ref.check(votes)
+                assert np.array_equal(st, exp), (cfg, np.nonzero(st != exp)[0][:10])
+                assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+                gk, gs = pool.reap(-1)
+                ok, os_ = ref.reap(-1)
+                assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+            assert pool.Size() < 17000 or cfg["cache_size"] == 0xFFFFFFFF   # the caps were reached
+        finally:
+            pool.close()
+    ctx.close()
