@@ -59,7 +59,6 @@ class WorkerPool {
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
-      ++gen_;
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -72,8 +71,9 @@ class WorkerPool {
     return ok;
   }
   // fn(lo, hi) over [0, n) in chunks; the caller thread takes part.  Small n runs inline.
-  // Each call is its own Job: a worker still draining an earlier job only sees that job's
-  // (exhausted) counters, never the new one's.
+  // Each call is its own Job and several threads may call at once (e.g. the pool's CheckTx
+  // beside txv_submit_votes' staging): idle workers take chunks of any job that has some left,
+  // and every caller drains its own job, so no call waits on another's.
   void parallel_for(uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn, uint32_t min_chunk = 2048) {
     const uint32_t parts = std::min<uint32_t>(size() * 4, std::max<uint32_t>(1, n / min_chunk));
     if (parts <= 1 || th_.empty()) { if (n) fn(0, n); return; }
@@ -81,14 +81,14 @@ class WorkerPool {
     job->fn = &fn; job->n = n; job->parts = parts;
     {
       std::lock_guard<std::mutex> g(m_);
-      job_ = job;
-      ++gen_;
+      jobs_.push_back(job);
     }
     cv_.notify_all();
     work(*job);
     std::unique_lock<std::mutex> lk(m_);
     done_cv_.wait(lk, [&] { return job->done.load() == job->parts; });
-    job_.reset();
+    for (size_t i = 0; i < jobs_.size(); ++i)
+      if (jobs_[i] == job) { jobs_.erase(jobs_.begin() + (ptrdiff_t)i); break; }
   }
 
  private:
@@ -109,25 +109,27 @@ class WorkerPool {
       }
     }
   }
+  // a job with chunks left (under m_)
+  std::shared_ptr<Job> pick() const {
+    for (const auto& j : jobs_)
+      if (j->next.load() < j->parts) return j;
+    return nullptr;
+  }
   void loop() {
-    uint64_t seen = 0;
     for (;;) {
       std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
+        cv_.wait(lk, [&] { return stop_ || (j = pick()) != nullptr; });
         if (stop_) return;
-        j = job_;
       }
-      if (j) work(*j);
+      work(*j);
     }
   }
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
-  std::shared_ptr<Job> job_;
-  uint64_t gen_ = 0;
+  std::vector<std::shared_ptr<Job>> jobs_;   // jobs whose callers have not returned yet
   bool stop_ = false;
 };
 
