@@ -319,6 +319,11 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uin
   if ((int64_t)p->txs.len + (int64_t)n > (int64_t)p->cfg.size) return false;
   if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;
   if (p->cache_on && (uint64_t)p->cache.len + n > (uint64_t)p->cfg.cache_size) return false;
+  static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
+  std::chrono::steady_clock::time_point tp[6];
+  int ntp = 0;
+  auto mark = [&] { if (prof) tp[ntp++] = std::chrono::steady_clock::now(); };
+  mark();
   // batch order per partition
   std::vector<uint32_t> cnt(kParts + 1, 0), order(n);
   for (uint32_t i = 0; i < n; ++i) ++cnt[part[i] + 1];
@@ -332,6 +337,7 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uin
   };
   // node keys first (the indices compare keys through the nodes), links only once admitted
   const size_t old_c = p->cache.nodes.size(), old_t = p->txs.nodes.size();
+  mark();
   next_indices(p->cache, n, p->idx_c);
   next_indices(p->txs, n, p->idx_t);
   // the last index is the highest new one whenever the free list runs out
@@ -343,6 +349,7 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uin
       KeyList::Node& t = p->txs.nodes[p->idx_t[i]]; t.k = keys[i]; t.size = p->sizes[i];
     }
   });
+  mark();
   if (p->cache_on) {
     std::atomic<bool> clash{false};
     per_part([&](uint32_t q) {   // mapTxCache.Push of every key: all must be new
@@ -365,6 +372,7 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uin
       p->txs.nodes.resize(old_t);
       return false;
     }
+    mark();
     link_appended(ctx, p->cache, p->idx_c, n);
   }
   per_part([&](uint32_t q) {     // addTx: txsMap.Store of every key
@@ -376,6 +384,11 @@ bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uin
     }
   });
   link_appended(ctx, p->txs, p->idx_t, n);
+  mark();
+  if (prof && ntp == 5) {
+    auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
+    fprintf(stderr, "[txv pool] admit: order=%.3f nodes=%.3f cache=%.3f txs+links=%.3f ms\n", ms(0), ms(1), ms(2), ms(3));
+  }
   p->txs_bytes += (int64_t)sum;
   memset(status_out, TXV_POOL_OK, n);
   return true;

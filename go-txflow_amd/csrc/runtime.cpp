@@ -180,6 +180,7 @@ struct txv_ctx {
   Slot slots[kSlots];
   // txv_sig_keys scratch: signatures [n][16] u32, lengths, keys [n][8] u32
   uint32_t pk_cap = 0;
+  std::mutex pk_mu;                  // txv_sig_keys' buffers (not c->mu: CheckTx's keys run beside txv_submit_votes)
   uint32_t *d_pk_sig = nullptr, *d_pk_len = nullptr, *d_pk_keys = nullptr;
   uint32_t *h_pk_sig = nullptr, *h_pk_len = nullptr, *h_pk_keys = nullptr;
   // txv_decode_* (TxVoteMessage wire decode): staged messages, packed outputs (one D2H copy)
@@ -1860,7 +1861,10 @@ int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const 
   const uint32_t n = v->n;
   for (uint32_t i = 0; i < n; ++i)
     if (v->sig_len[i] > 64 && (!sig_full || !sig_full_off)) { c->err = "signature > 64 bytes without sig_full"; return TXV_EINVAL; }
-  std::lock_guard<std::mutex> g(c->mu);
+  // its own lock: the pool's keys (TxVotePool.CheckTx on the ingest thread) must not wait for a
+  // txv_submit_votes staging on another thread, nor hold it up over the key stream's round trip;
+  // the key stream takes both threads' work in enqueue order, the worker pool both threads' passes
+  std::lock_guard<std::mutex> g(c->pk_mu);
   HIP_TRY(c, hipSetDevice(c->device));
   if (!n) return TXV_OK;
   if (n > c->pk_cap) {
