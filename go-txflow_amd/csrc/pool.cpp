@@ -147,7 +147,11 @@ struct FlatIndex {
 
 // doubly linked list in a vector (stable indices)
 struct KeyList {
-  struct Node { Key k; uint32_t size; int32_t prev, next; };
+  struct Node {
+    Key k; uint32_t size; int32_t prev, next;
+    Node() {}   // left unset: a batch grows the array by 64k nodes whose every field is written after
+    Node(const Key& k_, uint32_t s, int32_t p, int32_t n) : k(k_), size(s), prev(p), next(n) {}
+  };
   std::vector<Node> nodes;
   std::vector<int32_t> free_;
   int32_t head = -1, tail = -1;
