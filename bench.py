@@ -192,82 +192,94 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             ctx.add_votes(b, ev_cap=b.n)
         ctx.reset_flow()
         pool.flush()
-    submit, done, commit_t, pool_ms = [], [], {}, []
-    added = [0]
+    # three timed passes over the same stream (reset between): the 2M-vote pass lasts ~45 ms, so
+    # a single host stall moves it; the median pass is reported, all three beside it
+    runs = []
+    for rep in range(3):
+        submit, done, commit_t, pool_ms = [], [], {}, []
+        added = [0]
 
-    # Three threads, as a node's goroutines: Reactor.Receive -> CheckTx (ingest), the
-    # checkMaj23Routine submitting each checked batch (main), and a drain thread waiting each
-    # ticket in order as soon as it is submitted (commit events reported when the device is
-    # done, not when a third batch arrives).  At most two batches in flight (txv_submit_votes);
-    # ctypes releases the GIL inside every call.
-    import queue
-    import threading
-    checked = queue.Queue(maxsize=2)
-    tickets = queue.Queue()
-    slots = threading.Semaphore(2)
-    pool_err = []
+        # Three threads, as a node's goroutines: Reactor.Receive -> CheckTx (ingest), the
+        # checkMaj23Routine submitting each checked batch (main), and a drain thread waiting each
+        # ticket in order as soon as it is submitted (commit events reported when the device is
+        # done, not when a third batch arrives).  At most two batches in flight (txv_submit_votes);
+        # ctypes releases the GIL inside every call.
+        import queue
+        import threading
+        checked = queue.Queue(maxsize=2)
+        tickets = queue.Queue()
+        slots = threading.Semaphore(2)
+        pool_err = []
 
-    def ingest():
-        for k, b in enumerate(wl.batches):
-            ts = time.perf_counter()
-            ps = pool.check_batch(b)
-            tp = time.perf_counter()
-            if not (ps == T.POOL_OK).all():
-                pool_err.append(k)
-            checked.put((k, ts, tp))
-        checked.put(None)
+        def ingest():
+            for k, b in enumerate(wl.batches):
+                ts = time.perf_counter()
+                ps = pool.check_batch(b)
+                tp = time.perf_counter()
+                if not (ps == T.POOL_OK).all():
+                    pool_err.append(k)
+                checked.put((k, ts, tp))
+            checked.put(None)
 
-    def drain():
+        def drain():
+            while True:
+                item = tickets.get()
+                if item is None:
+                    return
+                k, tk = item
+                st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
+                te = time.perf_counter()
+                slots.release()
+                done.append(te)
+                added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
+                for e in ev:
+                    tx = int(wl.tx_of[k * batch + int(e["vote_index"])])
+                    assert tx not in commit_t, "tx committed twice"
+                    commit_t[tx] = te
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=ingest, daemon=True)
+        td = threading.Thread(target=drain, daemon=True)
+        th.start()
+        td.start()
         while True:
-            item = tickets.get()
+            item = checked.get()
             if item is None:
-                return
-            k, tk = item
-            st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
-            te = time.perf_counter()
-            slots.release()
-            done.append(te)
-            added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
-            for e in ev:
-                tx = int(wl.tx_of[k * batch + int(e["vote_index"])])
-                assert tx not in commit_t, "tx committed twice"
-                commit_t[tx] = te
-
-    t0 = time.perf_counter()
-    th = threading.Thread(target=ingest, daemon=True)
-    td = threading.Thread(target=drain, daemon=True)
-    th.start()
-    td.start()
-    while True:
-        item = checked.get()
-        if item is None:
-            break
-        k, ts, tp = item
-        slots.acquire()
-        submit.append(ts)
-        tickets.put((k, ctx.submit_votes(wl.batches[k])))
-        pool_ms.append((tp - ts) * 1e3)
-    th.join()
-    tickets.put(None)
-    td.join()
-    if pool_err:
-        raise RuntimeError("C5: pool rejected a unique vote")
-    added = added[0]
-    total = time.perf_counter() - t0
-    ok = added == wl.n and len(commit_t) == wl.n_txs
-    lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
-    bl = (np.array(done) - np.array(submit)) * 1e3
-    ok = ok and pool.Size() == wl.n
+                break
+            k, ts, tp = item
+            slots.acquire()
+            submit.append(ts)
+            tickets.put((k, ctx.submit_votes(wl.batches[k])))
+            pool_ms.append((tp - ts) * 1e3)
+        th.join()
+        tickets.put(None)
+        td.join()
+        if pool_err:
+            raise RuntimeError("C5: pool rejected a unique vote")
+        added = added[0]
+        total = time.perf_counter() - t0
+        ok = added == wl.n and len(commit_t) == wl.n_txs
+        lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
+        bl = (np.array(done) - np.array(submit)) * 1e3
+        ok = ok and pool.Size() == wl.n
+        out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n} votes in {batch}-vote batches "
+                           f"through txv_pool_check (TxVotePool.CheckTx, on an ingest thread) + txv_submit_votes/txv_wait_votes "
+                           f"(TxFlow.TryAddVote, two batches in flight, each waited by a drain thread as soon as submitted)",
+               "correct": ok, "votes_per_s": round(wl.n / total, 1),
+               "p50_pool_check_ms": round(float(np.median(pool_ms)), 3),
+               "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
+               "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
+               "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
+               "table_window": ctx.table_w, "base_window": ctx.base_w}
+        runs.append(out)
+        ctx.reset_flow()
+        pool.flush()
     pool.close()
-    out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n} votes in {batch}-vote batches "
-                       f"through txv_pool_check (TxVotePool.CheckTx, on an ingest thread) + txv_submit_votes/txv_wait_votes "
-                       f"(TxFlow.TryAddVote, two batches in flight, each waited by a drain thread as soon as submitted)",
-           "correct": ok, "votes_per_s": round(wl.n / total, 1),
-           "p50_pool_check_ms": round(float(np.median(pool_ms)), 3),
-           "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
-           "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
-           "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
-           "table_window": ctx.table_w, "base_window": ctx.base_w}
+    runs.sort(key=lambda r: r["votes_per_s"])
+    out = dict(runs[1])
+    out["passes"] = 3
+    out["votes_per_s_passes"] = [r["votes_per_s"] for r in runs]
+    out["correct"] = all(r["correct"] for r in runs)
     ctx.close()
     return out
 
