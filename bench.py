@@ -416,74 +416,37 @@ def main():
                   shard=rank, n_shards=world)
     # the same batch in the three device slots: step k runs in slot k % 3 with up to three steps
     # enqueued, so step k+1's prep runs beside step k's K1b and its K1a/K1b beside step k's tally
-    # (txv_run_staged returns as soon as the chain is enqueued)
+    # (txv_run_staged returns as soon as the chain is enqueued).  At N>1 each step's packed
+    # per-shard commit state ([n_sets][bitmap][sums], written by the device into the
+    # slot's commit sink) is all-gathered over RCCL on the context's flow stream right behind the
+    # step's chain (txflow_amd/pipeline.py): no host thread waits for the exchange.
+    from txflow_amd.pipeline import PipelinedSteps
     DEPTH = int(os.environ.get("TXV_BENCH_DEPTH", "3"))   # 2..4 staged slots
-    for sl in range(DEPTH):
-        ctx.stage(sl, wl.batch)
+    n_cap = max_txs
+    steps_rt = PipelinedSteps(ctx, [wl.batch], depth=DEPTH, fresh_flow=True, dist=dist, n_sets_cap=n_cap,
+                              device=local, ev_cap=wl.n_txs + 1)
     log(f"[rank {rank}] {ctx.device_name()}: {wl.n} votes ({wl.n_txs} txs x {args.validators} validators) "
         f"staged in {time.perf_counter() - t_setup:.1f}s")
-
-    # per-shard commit state all-gathered every step: [n_sets][bitmap][sums] packed by
-    # the device at the end of each step's chain (txv_set_commit_sink, one buffer per slot) -> one
-    # RCCL all-gather over xGMI per step
-    state = gathered = None
-    n_cap = max_txs
-    if dist is not None:
-        import torch
-        words = T.commit_state_bytes(n_cap) // 4
-        state = [torch.zeros(words, dtype=torch.int32, device=f"cuda:{local}") for _ in range(DEPTH)]
-        for sl in range(DEPTH):
-            ctx.set_commit_sink(sl, state[sl].data_ptr(), n_cap)
-        gathered = torch.zeros(world * words, dtype=torch.int32, device="cpu" if gloo else f"cuda:{local}")
     red_dev = "cpu" if gloo else f"cuda:{local}"
 
-    def all_gather_state(sl: int):
-        if gloo:
-            dist.all_gather(list(gathered.chunk(world)), state[sl].cpu())
-        else:
-            dist.all_gather_into_tensor(gathered, state[sl])
-            torch.cuda.synchronize()
-
     step_ms, route_ms, verify_ms, tally_ms = [], [], [], []
-    st_buf = [np.zeros(wl.n, np.uint8) for _ in range(DEPTH)]          # result buffers reused every step
-    ev_buf = [np.zeros(wl.n_txs + 1, T.EVENT_DTYPE) for _ in range(DEPTH)]
     t_launch = {}
+    launch0 = steps_rt.launch
 
     def launch(k: int):
-        """enqueue step k: a fresh TxFlow (in stream order after step k-1's tally) + the chain"""
         t_launch[k] = time.perf_counter()
-        ctx.reset_flow()
-        ctx.run_staged(k % DEPTH)
+        launch0(k)
+    steps_rt.launch = launch
 
-    def finish(k: int, record: bool):
-        sl = k % DEPTH
-        st, ev = ctx.fetch_staged(sl, wl.n, ev_cap=wl.n_txs + 1, out=st_buf[sl], evs=ev_buf[sl])
-        if dist is not None:
-            all_gather_state(sl)
-        if record:
-            step_ms.append((time.perf_counter() - t_launch[k]) * 1e3)
-            ms = ctx.slot_kernel_ms(sl)
-            route_ms.append(ms[0]); verify_ms.append(ms[1]); tally_ms.append(ms[2])
-        return st, ev
+    def record(k, st, ev):
+        step_ms.append((time.perf_counter() - t_launch[k]) * 1e3)
+        ms = ctx.slot_kernel_ms(k % DEPTH)
+        route_ms.append(ms[0]); verify_ms.append(ms[1]); tally_ms.append(ms[2])
 
-    def run_steps(m: int, record: bool):
-        """m steps, up to DEPTH enqueued: launch k before waiting for k - DEPTH + 1"""
-        out = None
-        for k in range(m):
-            launch(k)
-            if k >= DEPTH - 1:
-                out = finish(k - DEPTH + 1, record)
-        for k in range(max(0, m - DEPTH + 1), m):
-            out = finish(k, record)
-        return out
-
-    def step(record: bool):
-        return run_steps(1, record)
-
-    run_steps(args.warmup, False)
+    steps_rt.run(args.warmup)
     # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once,
     # with exactly n_vals - quorum + 1 fired votes per tx
-    st, ev = step(False)
+    st, ev = steps_rt.run(1)
     n_added = int(np.count_nonzero((st & 0x7F) == T.ADDED))
     n_fired = int(np.count_nonzero(st & 0x80))
     quorum = ctx.total_power() * 2 // 3 + 1
@@ -494,12 +457,11 @@ def main():
         sys.exit(2)
 
     if dist is not None:
+        import torch
         # the gathered global state (unpacked with the C-ABI's own layout): every tx of every shard
         # committed with the full stake
-        g = gathered.cpu().numpy().view(np.uint8).reshape(world, -1)
         bits = full = 0
-        for r in range(world):
-            com, sums = T.commit_state_unpack(g[r], n_cap)
+        for com, sums in steps_rt.gathered_states():
             bits += int(com.sum())
             full += int((sums == ctx.total_power()).sum())
         nt = torch.tensor([wl.n_txs], dtype=torch.int64, device=red_dev)
@@ -511,7 +473,7 @@ def main():
         torch.cuda.synchronize()
     ctx.sync()
     t0 = time.perf_counter()
-    run_steps(args.steps, True)
+    steps_rt.run(args.steps, record)
     ctx.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -535,7 +497,7 @@ def main():
     for _ in range(3):
         ctx.reset_flow()
         solo.append(ctx.run_staged(0, timed=True))
-        ctx.fetch_staged(0, wl.n, ev_cap=wl.n_txs + 1, out=st_buf[0], evs=ev_buf[0])
+        steps_rt.finish(0)
     s_ms = [statistics.median(x[j] for x in solo) for j in range(4)]
     if rank == 0:
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
@@ -618,6 +580,7 @@ def main():
         if world == 1 and not args.no_c1:
             out["c1"] = c1_leg(local, threads)
         print(json.dumps(out), flush=True)
+    steps_rt.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

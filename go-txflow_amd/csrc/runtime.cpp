@@ -86,7 +86,8 @@ struct Slot {
   bool msg_on_device = false;      // the signer's SignBytes are built by txv_k_signbytes
   uint64_t seq_base = 0;
   uint32_t stamp = 0;              // batch stamp of the staged batch
-  bool counted = false;            // s.n is in txv_ctx::unfetched
+  uint64_t run_seq = 0;            // txv_ctx::run_seq of the slot's last run (orders its summary)
+  uint64_t counted = 0;            // votes of this slot's unfetched runs, included in txv_ctx::unfetched
   // AddVote derived columns and scan scratch
   uint32_t *d_entry = nullptr, *d_row = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
@@ -106,6 +107,25 @@ struct Slot {
 
 }  // namespace
 
+// The last error message.  Threads holding c->mu (submit / wait, decode) and txv_sig_keys (its
+// own pk_mu) may fail at the same time, so the string has a lock of its own; txv_last_error
+// hands out a per-thread copy.
+struct ErrMsg {
+  std::mutex m;
+  std::string s;
+  ErrMsg& operator=(std::string v) {
+    std::lock_guard<std::mutex> g(m);
+    s = std::move(v);
+    return *this;
+  }
+  const char* copy() {
+    thread_local std::string t;
+    std::lock_guard<std::mutex> g(m);
+    t = s;
+    return t.c_str();
+  }
+};
+
 struct txv_ctx {
   txv_config cfg{};
   int device = 0;
@@ -115,7 +135,7 @@ struct txv_ctx {
   hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
   hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest), wire decode, and each batch's prep + SignBytes
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
-  std::string err;
+  ErrMsg err;
   std::mutex mu;
   // validator registry
   uint32_t n_vals = 0;
@@ -167,7 +187,9 @@ struct txv_ctx {
   uint32_t max_accepted = 0;        // accepted-vote rows (AccRow) of the arena
   uint64_t hash_seed = 0;           // TxHash hash seed (random per context)
   uint64_t seq_next = 0;            // sequence number of the next submitted vote
-  uint32_t n_sets_host = 0;         // TxVoteSets as of the last waited batch
+  uint32_t n_sets_host = 0;         // TxVoteSets as of the newest run whose results were fetched
+  uint64_t run_seq = 0;             // runs handed out (run_slot), in flow-stream order
+  uint64_t sets_seq = 0;            // run_seq n_sets_host belongs to (older summaries are not applied)
   uint64_t unfetched = 0;           // votes of batches run but not fetched yet (each may add sets)
   uint32_t poisoned = 0;            // TXV_FERR_* seen: every AddVote call fails until txv_reset_flow
   // caller memory registered with txv_host_register (DMA'd without a staging copy)
@@ -360,6 +382,7 @@ int alloc_tally(txv_ctx* c) {
   HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
   c->seq_next = 0;
   c->n_sets_host = 0;
+  c->sets_seq = c->run_seq;   // summaries of earlier runs describe the old state
   c->poisoned = 0;
   return TXV_OK;
 }
@@ -380,7 +403,10 @@ int reset_tally(txv_ctx* c, bool keep_ids = false) {
     if (keep_ids) c->poisoned &= ~TXV_FERR_ARENA;
   }
   c->seq_next = 0;
-  if (!keep_ids) c->n_sets_host = 0;
+  if (!keep_ids) {
+    c->n_sets_host = 0;
+    c->sets_seq = c->run_seq;   // a summary of a run enqueued before the reset is stale
+  }
   return TXV_OK;
 }
 
@@ -737,6 +763,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
     c->stamp = 0;
   }
   s.stamp = ++c->stamp;            // every run of a batch gets a stamp of its own
+  s.run_seq = ++c->run_seq;
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
   // Three compute queues, so that batch k+1 verifies while batch k tallies and nothing but
@@ -782,9 +809,12 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
   HIP_TRY(c, txv_flow_new_ids(&fs, &fb, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
-  // set ids in use after this batch: at most those known at the last fetch + one per vote of
-  // every batch run since (a bound for the touched-set scan)
-  if (!s.counted) { c->unfetched += s.n; s.counted = true; }
+  // set ids in use after this batch: at most those known at the newest fetched run + one per
+  // vote of every run not fetched yet (a bound for the touched-set scan).  A slot run again
+  // before it was fetched keeps its earlier run's votes counted too: that run's sets only show
+  // in a later summary.
+  c->unfetched += s.n;
+  s.counted += s.n;
   const uint32_t sets_bound = (uint32_t)std::min<uint64_t>((uint64_t)c->n_sets_host + c->unfetched, c->cfg.max_txs);
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[2], 0));
   HIP_TRY(c, txv_flow_tally(&fs, &fb, sets_bound, c->stream));
@@ -808,8 +838,14 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
   ht.mark("fetch_sync");
   FlowSummary sm;
   memcpy(&sm, (const void*)s.h_sum, sizeof sm);   // written over PCIe by the last kernel
-  c->n_sets_host = sm.n_sets;
-  if (s.counted) { c->unfetched -= s.n; s.counted = false; }
+  // only a summary newer than the one applied last moves the set count (slots may be fetched out
+  // of run order, e.g. staged slots beside the submit ring); an older one is covered by it
+  if (s.run_seq > c->sets_seq) {
+    c->n_sets_host = sm.n_sets;
+    c->sets_seq = s.run_seq;
+  }
+  c->unfetched -= s.counted;
+  s.counted = 0;
   if (sm.err) {
     c->poisoned |= sm.err;
     c->err = std::string("TxFlow capacity exceeded:") + ((sm.err & TXV_FERR_SETS) ? " max_txs" : "") +
@@ -1133,7 +1169,7 @@ void txv_destroy(txv_ctx* c) {
   delete c;
 }
 
-const char* txv_last_error(txv_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* txv_last_error(txv_ctx* c) { return c ? c->err.copy() : "null context"; }
 
 int txv_device_name(txv_ctx* c, char* buf, uint32_t cap) {
   if (!c || !buf || !cap) return TXV_EINVAL;
@@ -1936,6 +1972,8 @@ int txv_reset_flow(txv_ctx* c) {
   if (!c->n_vals) return TXV_OK;
   return reset_tally(c, false);
 }
+
+void* txv_flow_stream(txv_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int txv_sync(txv_ctx* c) {
   if (!c) return TXV_EINVAL;

@@ -117,6 +117,7 @@ def lib():
             "txv_reset_tally": ([vp], ctypes.c_int),
             "txv_reset_flow": ([vp], ctypes.c_int),
             "txv_sync": ([vp], ctypes.c_int),
+            "txv_flow_stream": ([vp], vp),
             "txv_fe_selftest": ([vp, vp, vp, vp, u32, ctypes.c_int], ctypes.c_int),
             "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -180,7 +181,7 @@ EXPORTED_SYMBOLS = [
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
-    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms"]
+    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_flow_stream"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -678,6 +679,10 @@ class Context:
     def reset_flow(self):
         """forget every TxVoteSet (a fresh TxFlow, txflow/service.go:71); validators stay"""
         self._chk(lib().txv_reset_flow(self._h), "txv_reset_flow")
+
+    def flow_stream(self) -> int:
+        """hipStream_t of the context's flow stream (txv_flow_stream), for torch.cuda.ExternalStream"""
+        return lib().txv_flow_stream(self._h)
 
     def sync(self):
         self._chk(lib().txv_sync(self._h), "txv_sync")

@@ -292,6 +292,12 @@ int txv_pack_commit_state(txv_ctx* ctx, void* dst_dev, uint32_t n_sets_cap);
  * already running.  dst_dev = NULL removes the sink.  For an all-gather per batch with two
  * batches in flight (txvote's per-shard commit exchange). */
 int txv_set_commit_sink(txv_ctx* ctx, uint32_t slot, void* dst_dev, uint32_t n_sets_cap);
+/* the context's flow stream (hipStream_t): every batch's TxFlow chain (keying, tally, commit
+ * sink pack) runs on it in submission order.  A collective enqueued on it right after
+ * txv_run_staged / txv_submit_votes (e.g. the per-batch RCCL all-gather of the commit sink)
+ * reads the sink after that batch's pack and the next batch's TxFlow chain queues behind it, so
+ * no host thread has to wait for the exchange.  Valid until txv_destroy. */
+void* txv_flow_stream(txv_ctx* ctx);
 /* the same packed by the device, copied into caller host memory (host-side gathers) */
 int txv_read_commit_state(txv_ctx* ctx, void* dst_host, uint32_t n_sets_cap);
 /* host-side pack (from per-set committed flags and sums) and unpack of the same layout */

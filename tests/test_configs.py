@@ -424,3 +424,144 @@ def test_staged_two_in_flight_with_commit_sinks(oracle_lib):
             ctx.set_commit_sink(sl, None)
     finally:
         ctx.close()
+
+
+def _signed_votes(ctx, T, addrs, hashes, n_vals, rnd, ts0=1):
+    """every validator votes every tx of `hashes` (arrival order shuffled), device-signed"""
+    votes, signer = [], []
+    for h in hashes:
+        for v in range(n_vals):
+            votes.append(T.TxVote(Height=1, TxHash=h, Timestamp=(1_700_000_000, ts0 + len(votes)),
+                                  ValidatorAddress=addrs[v]))
+            signer.append(v)
+    order = list(range(len(votes)))
+    rnd.shuffle(order)
+    votes = [votes[i] for i in order]
+    signer = np.array([signer[i] for i in order], np.uint32)
+    sigs = ctx.sign_votes(T.VoteBatch.from_votes(votes), signer, "test_chain_id")
+    for v, s in zip(votes, sigs):
+        v.Signature = s.tobytes()
+    return votes
+
+
+def _odicts(votes):
+    return [dict(height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0], ts_nanos=v.Timestamp[1],
+                 addr=v.ValidatorAddress, sig=v.Signature) for v in votes]
+
+
+def test_fetch_out_of_run_order_keeps_every_set_tallied(oracle_lib):
+    """a staged slot fetched after a later txv_submit_votes batch was waited (an older
+    summary arriving last), and a slot re-staged and run again before its results were fetched,
+    must not shrink the touched-set bound of later batches: every new TxVoteSet of the following
+    batches is still tallied, its commit event reported and its stake summed, as the sequential
+    TxFlow.addVote does (txflow/service.go:192-234)."""
+    import txflow_amd as T
+    rnd = random.Random(77)
+    n_vals = 16
+    ctx = T.Context(max_batch=1 << 14, max_txs=2048, max_validators=n_vals)
+    try:
+        seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(n_vals)]
+        pubs = ctx.keygen(seeds)
+        ctx.set_validators(pubs, [1] * n_vals, "test_chain_id")
+        addrs, _ = ctx.validator_info()
+        flow = oracle_lib.Flow(pubs, [1] * n_vals, b"test_chain_id")
+        hx = lambda k: ["%064X" % rnd.getrandbits(256) for _ in range(k)]
+        b0 = _signed_votes(ctx, T, addrs, hx(100), n_vals, rnd, 1)       # slot 2, staged
+        b1 = _signed_votes(ctx, T, addrs, hx(200), n_vals, rnd, 10 ** 6)  # submit ring (slot 0)
+        b2 = _signed_votes(ctx, T, addrs, hx(1), n_vals, rnd, 2 * 10 ** 6)
+        b3 = _signed_votes(ctx, T, addrs, hx(1), n_vals, rnd, 3 * 10 ** 6)    # slot 3, never fetched
+        b4 = _signed_votes(ctx, T, addrs, hx(40), n_vals, rnd, 4 * 10 ** 6)   # slot 3 again
+        b5 = _signed_votes(ctx, T, addrs, hx(1), n_vals, rnd, 5 * 10 ** 6)
+
+        def expect(votes):
+            ost, _, ofired = flow.add_votes(_odicts(votes))
+            return _expected(ost, ofired)
+
+        e0, e1, e2, _, e4, e5 = (expect(b) for b in (b0, b1, b2, b3, b4, b5))
+        ctx.stage(2, T.VoteBatch.from_votes(b0))
+        ctx.run_staged(2)
+        t = ctx.submit_votes(T.VoteBatch.from_votes(b1))
+        st1, ev1 = ctx.wait_votes(t, ev_cap=len(b1))
+        st0, ev0 = ctx.fetch_staged(2, len(b0), ev_cap=len(b0))       # the older summary, fetched last
+        assert np.array_equal(st0, e0) and np.array_equal(st1, e1) and len(ev0) == 100 and len(ev1) == 200
+        assert ctx.num_tx_sets() == 300
+        st2, ev2 = ctx.add_votes(T.VoteBatch.from_votes(b2))
+        assert np.array_equal(st2, e2) and len(ev2) == 1
+        ctx.stage(3, T.VoteBatch.from_votes(b3))
+        ctx.run_staged(3)
+        ctx.stage(3, T.VoteBatch.from_votes(b4))                      # re-staged before its fetch
+        ctx.run_staged(3)
+        st4, ev4 = ctx.fetch_staged(3, len(b4), ev_cap=len(b4))
+        assert np.array_equal(st4, e4) and len(ev4) == 40
+        st5, ev5 = ctx.add_votes(T.VoteBatch.from_votes(b5))
+        assert np.array_equal(st5, e5) and len(ev5) == 1
+        for v in b0[:1] + b1[:1] + b2[:1] + b3[:1] + b4[:1] + b5[:1]:
+            assert ctx.query_tx(v.TxHash.encode()) == flow.query(v.TxHash.encode())
+        assert ctx.num_tx_sets() == flow.num_sets() == 343
+    finally:
+        ctx.close()
+
+
+def test_c1_full_config_matches_oracle(oracle_lib):
+    """C1 (BASELINE.json configs[0]) at its own size: 4 validators x 2,500 txs = 10,000 signed
+    TxVotes, shuffled, through txv_add_votes and again through the pipelined submit / wait path;
+    every per-vote status + fired bit, every commit event and every TxVoteSet's (sum, maj23) equal
+    the sequential oracle's (verify on every host core)."""
+    import txflow_amd as T
+    from txflow_amd.workload import Workload, SEEDS
+    ctx = T.Context(max_batch=16384, max_txs=4096, max_validators=8)
+    try:
+        wl = Workload(ctx, 4, 2500, SEEDS["c1"])
+        assert wl.n == 10_000
+        flow = oracle_lib.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        ost, _, ofired = flow.add_batch(wl.batch, _cores())
+        exp = _expected(ost, ofired)
+        st, ev = ctx.add_votes(wl.batch, ev_cap=wl.n_txs + 1)
+        assert np.array_equal(st, exp)
+        assert sorted(int(e["vote_index"]) for e in ev) == _first_fired(wl.batch, ofired, set())
+        # quorum of 4 x power 1 = 3: the 3rd and 4th vote of every tx fire
+        assert int(np.count_nonzero(st & 0x80)) == 2 * wl.n_txs
+        hashes = [h.tobytes() for h in wl.hashes]
+        ex, sums, maj, _ = ctx.query_txs(hashes)
+        assert ex.all() and all((int(sums[j]), bool(maj[j])) == flow.query(h) for j, h in enumerate(hashes))
+        ctx.reset_flow()
+        t = ctx.submit_votes(wl.batch)
+        st2, ev2 = ctx.wait_votes(t, ev_cap=wl.n_txs + 1)
+        assert np.array_equal(st2, exp) and len(ev2) == len(ev)
+    finally:
+        ctx.close()
+
+
+def test_c3_one_rank_full_shard_matches_oracle(oracle_lib):
+    """C3 (BASELINE.json configs[2]) at one rank's real size: the full C3 workload (160,000 txs x
+    100 validators = 16M votes) sharded by SHA-256(TxHash)[0] mod 8, shard 3 (~20k txs, ~2M
+    votes) on one context, as bench.py's rank 3 of 8 holds it: every per-vote status + fired bit
+    and commit event equals the oracle's, and the packed commit state written by the device
+    equals the host pack of the oracle's per-set state."""
+    import txflow_amd as T
+    from txflow_amd.workload import Workload, SEEDS
+    world, rank = 8, 3
+    cap = 22_000
+    ctx = T.Context(max_batch=(cap + 64) * 100, max_txs=cap + 64, max_validators=100)
+    try:
+        wl = Workload(ctx, 100, 160_000, SEEDS["c3"], shard=rank, n_shards=world)
+        assert 19_000 < wl.n_txs < cap and wl.n == wl.n_txs * 100
+        st, ev = ctx.add_votes(wl.batch, ev_cap=wl.n_txs + 1)
+        flow = oracle_lib.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        ost, _, ofired = flow.add_batch(wl.batch, _cores())
+        bad = np.nonzero(st != _expected(ost, ofired))[0]
+        assert len(bad) == 0, [(int(i), int(st[i])) for i in bad[:10]]
+        assert sorted(int(e["vote_index"]) for e in ev) == _first_fired(wl.batch, ofired, set())
+        keys, seen = [], set()
+        for i in range(wl.n):
+            h = wl.batch.txhash(i)
+            if h not in seen:
+                seen.add(h)
+                keys.append(h)
+        q = [flow.query(k) for k in keys]
+        host = T.commit_state_pack_host(np.array([m for _, m in q], np.uint8), np.array([s for s, _ in q], np.int64),
+                                        cap)
+        assert np.array_equal(ctx.read_commit_state(cap), host)
+        assert ctx.num_tx_sets() == flow.num_sets() == wl.n_txs
+    finally:
+        ctx.close()

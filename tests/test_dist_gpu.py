@@ -1,0 +1,146 @@
+"""The product's multi-rank step path on the GPU, in fresh child processes:
+
+  two ranks (gloo, both on cuda:0, each with its own txv_ctx): the C3 layout -- the workload's
+  TxHashes sharded by SHA-256(TxHash)[0] mod 2 (txv_shard_of) -- run through bench.py's step
+  path (txflow_amd/pipeline.py: staged slots, up to two steps enqueued, each step's packed commit
+  state written by the device into the slot's commit sink and all-gathered after the step);
+  steps alternate the shard's votes with a batch of replays, conflicting signatures, corrupted
+  signatures and new txs, on one TxFlow.  Every step's per-vote statuses + fired bits equal the
+  sequential oracle's over the shard, and every rank's row of the gathered state equals the host
+  pack of the owning rank's oracle state (so every rank holds the global committed set + stakes);
+  one rank (nccl = RCCL): the same path with the all-gather enqueued on the context's flow stream
+  through torch.cuda.ExternalStream (the bench's N>1 exchange), the gathered state equal to the
+  oracle's after every step.
+"""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _adversarial(T, wl, ctx, rnd):
+    """replays / conflicts / corrupted signatures of the shard's votes + votes for new txs"""
+    b = wl.batch
+    n = b.n
+    pick = np.array(sorted(rnd.sample(range(n), n // 5)), np.int64)
+    sig = b.sig.reshape(n, 64)[pick].copy()
+    kind = np.array(rnd.choices([0, 1, 2], weights=[45, 45, 10], k=len(pick)))
+    sig[kind == 1, 5] ^= 0x10            # same validator + tx, other signature: NONDETERMINISTIC
+    m = len(pick)
+    nb = T.VoteBatch(m, height=b.height[pick], txhash_arena=b.txhash_arena, txhash_off=b.txhash_off[pick],
+                     txhash_len=b.txhash_len[pick], ts_sec=b.ts_sec[pick], ts_nanos=b.ts_nanos[pick],
+                     addr=b.addr.reshape(n, 20)[pick], addr_len=b.addr_len[pick], sig=sig,
+                     sig_len=b.sig_len[pick], txkey=b.txkey.reshape(n, 32)[pick])
+    # kind 2 on a tx of its own: a TxHash nobody else uses, corrupted signature -> INVALID
+    arena = np.concatenate([b.txhash_arena, np.frombuffer(b"F" * 64 * int((kind == 2).sum()), np.uint8)])
+    base = len(b.txhash_arena)
+    off = nb.txhash_off.copy()
+    off[kind == 2] = base + 64 * np.arange(int((kind == 2).sum()), dtype=np.uint32)
+    for j, i in enumerate(np.nonzero(kind == 2)[0]):
+        arena[off[i]:off[i] + 2] = np.frombuffer(b"%02X" % (j % 256), np.uint8)
+        arena[off[i] + 2:off[i] + 6] = np.frombuffer(b"%04X" % (j // 256), np.uint8)
+    nb = T.VoteBatch(m, height=nb.height, txhash_arena=arena, txhash_off=off, txhash_len=nb.txhash_len,
+                     ts_sec=nb.ts_sec, ts_nanos=nb.ts_nanos, addr=nb.addr, addr_len=nb.addr_len, sig=nb.sig,
+                     sig_len=nb.sig_len, txkey=nb.txkey)
+    return nb
+
+
+def _worker(rank, world, port, backend, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        for p in (os.path.join(ROOT, "go-txflow_amd"), os.path.join(ROOT, "oracle")):
+            sys.path.insert(0, p)
+        import oracle as O
+        import txflow_amd as T
+        from txflow_amd.pipeline import PipelinedSteps
+        from txflow_amd.workload import Workload, SEEDS
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend, rank=rank, world_size=world)
+        cap = 4096
+        ctx = T.Context(device=0, max_batch=1 << 17, max_txs=cap, max_validators=100, table_w=16)
+        wl = Workload(ctx, 100, 1200, SEEDS["c3"], shard=rank, n_shards=2)
+        adv = _adversarial(T, wl, ctx, random.Random(100 + rank))
+        flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
+        runner = PipelinedSteps(ctx, [wl.batch, adv], depth=2, fresh_flow=False, dist=dist, n_sets_cap=cap,
+                                device=0, ev_cap=1 << 17)
+        keys, seen = [], set()
+        errors = []
+        for k in range(4):
+            b = runner.batches[k % 2]
+            ost, _, ofired = flow.add_batch(b, 8)
+            exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+            for i in range(b.n):
+                h = b.txhash(i)
+                if h not in seen:
+                    seen.add(h)
+                    keys.append(h)
+            runner.launch(k)
+            st, ev = runner.finish(k)
+            if not np.array_equal(st, exp):
+                bad = np.nonzero(st != exp)[0]
+                errors.append(f"rank {rank} step {k}: {len(bad)} status mismatches "
+                              f"{[(int(i), int(st[i]), int(exp[i])) for i in bad[:5]]}")
+            qv = [flow.query(h) for h in keys]
+            mine = T.commit_state_pack_host(np.array([m for _, m in qv], np.uint8),
+                                            np.array([s for s, _ in qv], np.int64), cap)
+            rows = [None] * world
+            dist.all_gather_object(rows, mine)
+            got = runner.gathered_states()
+            for r in range(world):
+                ec, es = T.commit_state_unpack(rows[r], cap)
+                gc, gs = got[r]
+                if not (np.array_equal(gc, ec) and np.array_equal(gs, es)):
+                    errors.append(f"rank {rank} step {k}: gathered state of rank {r} differs")
+        by = np.bincount(st & 0x7F, minlength=8)
+        runner.close()
+        ctx.close()
+        dist.destroy_process_group()
+        q.put((rank, errors, len(keys), by.tolist()))
+    except Exception as e:   # report instead of hanging the parent
+        import traceback
+        q.put((rank, [f"rank {rank} raised {e!r}\n{traceback.format_exc()}"], 0, []))
+
+
+def _run(world, backend):
+    port = 29500 + random.Random().randrange(2000)
+    c = mp.get_context("spawn")
+    q = c.Queue()
+    procs = [c.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:          # a rank stuck in a collective after its peer failed
+            if p.is_alive():
+                p.kill()
+    return res, [p.exitcode for p in procs]
+
+
+def test_two_ranks_one_gpu_sharded_steps_match_oracle():
+    res, codes = _run(2, "gloo")
+    errs = [e for _, es, _, _ in res for e in es]
+    assert not errs, "\n".join(errs)
+    assert codes == [0, 0]
+    assert sum(n for _, _, n, _ in res) > 1200        # the shards' txs + the adversarial new txs
+    for _, _, _, by in res:                           # the last (adversarial) step had every outcome
+        assert by[1] > 0 and by[5] > 0 and by[6] > 0, by
+
+
+def test_one_rank_rccl_exchange_on_flow_stream():
+    res, codes = _run(1, "nccl")
+    errs = [e for _, es, _, _ in res for e in es]
+    assert not errs, "\n".join(errs)
+    assert codes == [0]
