@@ -134,6 +134,8 @@ orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_byte
                        int64_t height, int wal);
 void orc_pool_free(orc_pool*);
 int orc_pool_check(orc_pool*, const orc_vote* v);
+void orc_pool_check_soa(orc_pool*, const orc_soa* b, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                        uint8_t* out);
 void orc_pool_update(orc_pool*, int64_t height, const orc_vote* votes, uint32_t n);
 uint64_t orc_pool_reap(orc_pool*, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap);
 void orc_pool_flush(orc_pool*);

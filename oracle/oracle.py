@@ -58,6 +58,8 @@ def lib():
                                    ctypes.c_int]
         L.orc_pool_free.argtypes = [ctypes.c_void_p]
         L.orc_pool_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_pool_check_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]
         L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
         L.orc_pool_reap.restype = ctypes.c_uint64
         L.orc_pool_reap.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
@@ -322,6 +324,26 @@ class Pool:
         import numpy as np
         keep = []
         return np.array([lib().orc_pool_check(self._h, ctypes.byref(_orc_vote(v, keep))) for v in votes], np.uint8)
+
+    def check_batch(self, b, long_sigs=None):
+        """orc_pool_check over a VoteBatch-shaped object in arrival order; long_sigs: {index: full
+        signature bytes} for votes whose sig_len exceeds 64"""
+        import numpy as np
+        soa = _soa(b)
+        full = off = None
+        if long_sigs:
+            arena = b"".join(long_sigs[i] for i in sorted(long_sigs))
+            full = ctypes.create_string_buffer(arena, max(len(arena), 1))
+            offs = np.zeros(max(b.n, 1), np.uint64)
+            o = 0
+            for i in sorted(long_sigs):
+                offs[i] = o
+                o += len(long_sigs[i])
+            off = offs
+        out = np.zeros(max(b.n, 1), np.uint8)
+        lib().orc_pool_check_soa(self._h, ctypes.addressof(soa), full, None if off is None else off.ctypes.data,
+                                 out.ctypes.data)
+        return out[:b.n]
 
     def update(self, height, votes):
         keep = []

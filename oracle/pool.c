@@ -131,6 +131,26 @@ int orc_pool_check(orc_pool* p, const orc_vote* v) {
   return 0;
 }
 
+/* orc_pool_check over an SoA batch in arrival order (the gate's pool stage).  Signatures longer
+ * than 64 bytes are read from sig_full + sig_full_off[i] (NULL: none in the batch). */
+void orc_pool_check_soa(orc_pool* p, const orc_soa* b, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                        uint8_t* out) {
+  for (uint32_t i = 0; i < b->n; ++i) {
+    orc_vote v;
+    v.is_nil = b->is_nil ? b->is_nil[i] : 0;
+    v.height = b->height[i];
+    v.txhash = b->txhash + b->txhash_off[i];
+    v.txhash_len = b->txhash_len[i];
+    v.ts_sec = b->ts_sec[i];
+    v.ts_nanos = b->ts_nanos[i];
+    v.addr = b->addr + (size_t)i * 20;
+    v.addr_len = b->addr_len[i];
+    v.sig = (b->sig_len[i] > 64 && sig_full) ? sig_full + sig_full_off[i] : b->sig + (size_t)i * 64;
+    v.sig_len = b->sig_len[i];
+    out[i] = (uint8_t)orc_pool_check(p, &v);
+  }
+}
+
 void orc_pool_update(orc_pool* p, int64_t height, const orc_vote* votes, uint32_t n) {
   p->height = height;
   for (uint32_t i = 0; i < n; ++i) {

@@ -17,6 +17,17 @@ re-signed votes (same validator + tx, new timestamp), sourced from this batch or
 (cross-batch state).  Crafted validators: identity (canonical, y+p, x=0 with sign bit), order 2,
 order 4 (both roots, y+p encoding), order 8, mixed-order A+T4 / A+T8, and an undecodable key.
 Forgeries: R = [r]B, s = r + k*a (a = 0 for pure torsion keys), valid exactly when [k]T = 0.
+
+Pool stage (pool_stage=True; Appendix C "ErrTxInCache when the pool stage is enabled"): every
+generated batch first goes through TxVotePool.CheckTx in arrival order -- the device pool
+(txv_pool_check: SHA-256(Signature) keys on the GPU, LRU cache + pool list on the host) and the
+oracle's sequential restatement (oracle/pool.c) -- whose per-vote outcomes must agree; only the
+admitted votes continue to TxFlow.addVote, as Reactor.Receive -> CheckTxWithInfo -> the pool's
+list -> checkMaj23Routine -> TryAddVote do (txvotepool/reactor.go:170-190, txvotepool.go:187-261,
+txflow/service.go:123-188).  Exact replays whose key is still cached stop there as ErrTxInCache;
+replays whose key the bounded LRU has evicted reach the tally as DUPLICATE.  Nil votes cannot be
+gossiped (CheckTx takes the vote by value) and go to TryAddVote directly.  Both pools are flushed
+at each epoch end (a fresh node).
 """
 from __future__ import annotations
 
@@ -77,7 +88,8 @@ class C4Stream:
     over `epoch_txs` transactions; each epoch is `batches_per_epoch` batches of `batch` votes."""
 
     def __init__(self, ctx, seed: int = 0x7478763034, batch: int = 1 << 20, batches_per_epoch: int = 4,
-                 oracle_threads: int = 16, verify_slice: int = 4096):
+                 oracle_threads: int = 16, verify_slice: int = 4096, pool_stage: bool = False,
+                 pool_cache: int = 1 << 20):
         import oracle as O
         from txflow_amd.workload import validator_seeds
         self.ctx, self.O = ctx, O
@@ -106,6 +118,13 @@ class C4Stream:
         self.generated = 0
         self.stats = dict(votes=0, batches=0, epochs=0, mismatches=0, verify_checked=0, events=0,
                           txs_checked=0, by_status={})
+        self.pool = self.opool = None
+        if pool_stage:
+            import txflow_amd as T
+            big = (1 << 31) - 1
+            self.pool = T.TxVotePool(ctx, size=big, cache_size=pool_cache, max_txs_bytes=1 << 40)
+            self.opool = O.Pool(size=big, cache_size=pool_cache, max_txs_bytes=1 << 40)
+            self.stats.update(pool_votes=0, pool_mismatches=0, pool_by_status={}, pool_cache=pool_cache)
 
     # ---------------------------------------------------------------- epoch state
     def _new_epoch(self):
@@ -123,6 +142,9 @@ class C4Stream:
         self.nanos = 1
         self.committed = set()
         self.stats["epochs"] += 1
+        if self.pool is not None:
+            self.pool.flush()
+            self.opool.flush()
 
     # ---------------------------------------------------------------- batch construction
     def _forge(self, vi: int, msg: bytes, pick: int):
@@ -289,9 +311,50 @@ class C4Stream:
                             is_nil=f["is_nil"])
         return batch, f
 
+    def next_admitted(self):
+        """next_batch, then (pool stage) TxVotePool.CheckTx on the device and in the oracle: the
+        per-vote pool outcomes are compared, and the admitted votes (+ nil votes) are returned in
+        arrival order as the batch for TxFlow"""
+        batch, f = self.next_batch()
+        if self.pool is None:
+            return batch, f
+        import txflow_amd as T
+        gossip = np.nonzero(f["is_nil"] == 0)[0]
+        m = len(gossip)
+        sub = T.VoteBatch(m, height=f["height"][gossip], txhash_arena=batch.txhash_arena,
+                          txhash_off=f["txoff"][gossip], txhash_len=np.full(m, 64, np.uint32),
+                          ts_sec=np.full(m, 1_700_000_000, np.int64), ts_nanos=f["ts_nanos"][gossip],
+                          addr=f["addr"][gossip], addr_len=f["addr_len"][gossip], sig=f["sig"][gossip],
+                          sig_len=f["sig_len"][gossip])
+        # signatures longer than 64 bytes: the 64 held bytes + zero bytes (the key hashes them all)
+        long_sigs = {int(q): sub.sig[64 * q:64 * q + 64].tobytes() + bytes(int(sub.sig_len[q]) - 64)
+                     for q in np.nonzero(sub.sig_len > 64)[0]}
+        ps = self.pool.check_batch(sub, long_sigs)
+        ops = self.opool.check_batch(sub, long_sigs)
+        pm = int(np.count_nonzero(ps != ops))
+        self.stats["pool_mismatches"] += pm
+        self.stats["mismatches"] += pm
+        self.stats["pool_votes"] += m
+        names = {T.POOL_OK: "OK", T.POOL_ERR_FULL: "ErrMempoolIsFull", T.POOL_ERR_TOO_LARGE: "ErrTxTooLarge",
+                 T.POOL_ERR_IN_CACHE: "ErrTxInCache", T.POOL_ERR_ENCODING: "ErrWAL"}
+        for code, cnt in zip(*np.unique(ops, return_counts=True)):
+            nm = names.get(int(code), str(code))
+            self.stats["pool_by_status"][nm] = self.stats["pool_by_status"].get(nm, 0) + int(cnt)
+        keep = np.ones(f["n"], bool)
+        keep[gossip[ops != T.POOL_OK]] = False
+        idx = np.nonzero(keep)[0]
+        g = {k: (v[idx] if isinstance(v, np.ndarray) else v) for k, v in f.items()}
+        g["n"] = len(idx)
+        out = T.VoteBatch(len(idx), height=g["height"], txhash_arena=batch.txhash_arena, txhash_off=g["txoff"],
+                          txhash_len=np.full(len(idx), 64, np.uint32),
+                          ts_sec=np.full(len(idx), 1_700_000_000, np.int64), ts_nanos=g["ts_nanos"],
+                          addr=g["addr"], addr_len=g["addr_len"], sig=g["sig"], sig_len=g["sig_len"],
+                          is_nil=g["is_nil"])
+        return out, g
+
     # ---------------------------------------------------------------- the gate
     def run_batch(self):
-        batch, f = self.next_batch()
+        batch, f = self.next_admitted()
         st, ev = self.ctx.add_votes(batch, ev_cap=batch.n)
         return self.check_batch(batch, f, st, ev)
 
@@ -361,18 +424,22 @@ class C4Stream:
 
 
 def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int = 4, threads: int = 16,
-             log=print, seed: int = 0x7478763034, pipelined: bool = True):
+             log=print, seed: int = 0x7478763034, pipelined: bool = True, pool_stage: bool = False,
+             pool_cache: int = 1 << 20):
     """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0).
     pipelined: batches go through txv_submit_votes / txv_wait_votes with two in flight (batch
     k+1 verifies on the device while batch k tallies and is checked against the oracle); the
     pipeline drains at each epoch end, before the per-set check reads the device state."""
-    s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads)
+    s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads,
+                 pool_stage=pool_stage, pool_cache=pool_cache)
     t0 = time.time()
 
     def report(r):
         log(f"[c4] batch {s.stats['batches']} epoch {s.epoch}: {r['n']} votes, status mismatches "
             f"{r['status_mismatches']}, events ok {r['events_ok']}, verify mismatches {r['verify_mismatches']}; "
             f"total {s.stats['votes']} votes, {s.stats['mismatches']} mismatches, {time.time() - t0:.0f}s"
+            + (f", pool {s.stats['pool_votes']} checked / {s.stats['pool_mismatches']} mismatches "
+               f"{s.stats['pool_by_status']}" if s.pool is not None else "")
             + (f" first_bad={r['first_bad']}" if r["first_bad"] else ""))
 
     inflight = []
@@ -384,7 +451,7 @@ def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int
         # the batch that closes an epoch is checked with nothing behind it in flight
         epoch_end = (submitted % s.bpe) == 0 and submitted > 0
         if sub_votes < total_votes and not (epoch_end and inflight) and len(inflight) < 2:
-            b, f = s.next_batch()
+            b, f = s.next_admitted()
             inflight.append((b, f, ctx.submit_votes(b)))
             submitted += 1
             sub_votes += b.n
@@ -396,4 +463,6 @@ def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int
     if s.stats["batches"] % s.bpe:
         s.stats["mismatches"] += s.check_sets()
     s.stats["seconds"] = round(time.time() - t0, 1)
+    if s.pool is not None:
+        s.pool.close()
     return s.stats

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """C4 bit-exact gate (BASELINE.json config 4): stream N adversarial TxVotes
 through libtxvote.so on cuda:0 and through the sequential CPU oracle; every per-vote status,
-commit-fire bit, commit event, direct-Verify verdict (slice) and per-tx (sum, maj23) must agree.
+commit-fire bit, commit event, direct-Verify verdict (slice) and per-tx (sum, maj23) must agree.  By default every
+batch first passes TxVotePool.CheckTx (device txv_pool_check vs the oracle pool, outcomes compared
+per vote; replays still cached -> ErrTxInCache) and only the admitted votes reach TxFlow.
 
     python tools/gate/c4_gate.py --votes 100000000 --out gpurun_out/c4/gate.json
 
@@ -25,6 +27,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default="")
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8))
+    ap.add_argument("--no-pool", action="store_true", help="feed txv_add_votes directly (no TxVotePool stage)")
+    ap.add_argument("--pool-cache", type=int, default=1 << 20, help="TxVotePool CacheSize (LRU entries)")
     args = ap.parse_args()
     import oracle
     oracle.build()
@@ -34,8 +38,14 @@ def main():
                     lane_votes=args.lane_votes)
     t0 = time.time()
     st = A.run_gate(ctx, args.votes, batch=args.batch, batches_per_epoch=args.batches_per_epoch,
-                    threads=args.threads, log=lambda s: print(s, flush=True))
-    st.update(device=ctx.device_name(), table_window=ctx.table_w, base_window=ctx.base_w,
+                    threads=args.threads, log=lambda s: print(s, flush=True), pool_stage=not args.no_pool,
+                    pool_cache=args.pool_cache)
+    import subprocess
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except Exception:
+        head = ""
+    st.update(head=head or os.environ.get("TXV_HEAD", ""), device=ctx.device_name(), table_window=ctx.table_w, base_window=ctx.base_w,
               validators=len(A.crafted_keys()) + A.N_HONEST, wall_s=round(time.time() - t0, 1),
               oracle_threads=args.threads, batch=args.batch, batches_per_epoch=args.batches_per_epoch)
     print(json.dumps(st), flush=True)
