@@ -44,12 +44,15 @@ VALU_PEAK = 256 * 4 * 32 * 2.4e9
 # SignBytes words (2 SHA-512 blocks' worth of message, 128 B), k written and read (2 x 32 B), the
 # parked points of V = 8 (7/8 of a vote parks 128 B, written and read back), the verdict (1 B)
 VERIFY_ALG_BYTES = 23 * 128 + 64 + 128 + 2 * 32 + 7 / 8 * 2 * 128 + 1
-# Algorithmic int32 lane-ops per verified vote of the algorithm that runs:
-#   SHA-512 of R||A||SignBytes, 2 blocks + ScReduce                      1.1e4
-#   [s]B + [k](-A) over fixed-base tables: 11 + 13 mixed additions x 7 FM   168 FM
-#   encode (2 FM), Montgomery batch inverse (3 FM / vote), divstep inverse / 8 (~8 FM-eq)  13 FM
-#   at 100 lane-ops per 255-bit field multiply (SURVEY.md §8d cost model)  -> 1.81e4
-W_ALG = 1.1e4 + (24 * 7 + 2 + 3 + 8) * 100.0
+# Algorithmic int32 lane-ops per verified vote of the algorithm that runs (the
+# one roofline definition, also BASELINE.md "Roofline as measured"):
+#   SHA-512 of R||A||SignBytes, 2 blocks + ScReduce                                1.1e4
+#   [s]B + [k](-A) over fixed-base tables: 11 + 13 = 24 entries -> the first is the
+#   starting point (1 FM for its T), then 23 mixed additions x 7 FM, the last without T (6)  161 FM
+#   encode (2 FM), Montgomery batch inverse (3 FM / vote), divstep inverse / 8 (~8 FM-eq)     13 FM
+#   at 100 lane-ops per 255-bit field multiply (SURVEY.md §8d cost model)  -> 1.74e4
+W_FM = 1 + 22 * 7 + 6 + 2 + 3 + 8
+W_ALG = 1.1e4 + W_FM * 100.0
 
 
 def log(*a):
@@ -344,18 +347,18 @@ def load_pmc(table_w: int, n_votes: int):
     PMC passes (profiles/pmc_verify.json), when they were taken on this kernel configuration"""
     pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
     if not os.path.exists(pmc):
-        return None, None, None, None
+        return None, None, None, None, None
     try:
         with open(pmc) as f:
             pj = json.load(f)
     except Exception:
-        return None, None, None, None
+        return None, None, None, None, None
     if pj.get("table_window") != table_w:
-        return None, None, None, None
+        return None, None, None, None, None
     same = pj.get("votes_per_launch", n_votes) == n_votes
     traffic = pj.get("hbm_bytes_per_launch") if same else None
     tally = pj.get("tally_hbm_bytes_per_launch") if same else None
-    return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source"), tally
+    return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source"), tally, pj.get("k1b_valu_issue_busy")
 
 
 def main():
@@ -503,7 +506,7 @@ def main():
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
         # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
         # (PMC SQ_INSTS_VALU pass of this build, profiles/pmc_verify.json) give exec_frac
-        w_exec, traffic, pmc_src, tally_bytes = load_pmc(ctx.table_w, wl.n)
+        w_exec, traffic, pmc_src, tally_bytes, k1b_busy = load_pmc(ctx.table_w, wl.n)
         achieved = wl.n * W_ALG / (v_ms * 1e-3)
         exec_rate = wl.n * w_exec / (v_ms * 1e-3) if w_exec else None
         threads = args.cpu_threads or host_cores()
@@ -546,7 +549,12 @@ def main():
                          "alg_bytes_per_launch": round(wl.n * VERIFY_ALG_BYTES),
                          "traffic_over_alg_bytes": None if not traffic else round(traffic / (wl.n * VERIFY_ALG_BYTES), 3),
                          "alg_lane_ops_per_vote": W_ALG,
-                         "alg_source": "DESIGN.md §4: SHA-512 2 blocks + ScReduce + 181 field multiplies x 100",
+                         "alg_source": f"DESIGN.md §4: SHA-512 2 blocks + ScReduce + {W_FM} field multiplies x 100",
+                         "k1b_valu_issue_busy": None if k1b_busy is None else round(k1b_busy, 3),
+                         "valu_busy_note": "K1b wave-instructions x issue cycles (64-bit class 4, others 2) / SIMD-cycles "
+                                           "of the dispatch (GRBM_GUI_ACTIVE), from the committed PMC pass; "
+                                           "SQ_ACTIVE_INST_VALU / SQ_THREAD_CYCLES_VALU count instructions on this "
+                                           "stack; the pure-VALU issue probe reads 0.81-0.85 on the same metric",
                          "exec_lane_slots_per_vote": w_exec,
                          "exec_achieved": None if exec_rate is None else round(exec_rate / 1e12, 3),
                          "exec_frac": None if exec_rate is None else round(exec_rate / VALU_PEAK, 4),

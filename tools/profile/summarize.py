@@ -70,8 +70,23 @@ def main():
             d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
-        if "SQ_ACTIVE_INST_VALU" in d and "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
-            d["valu_active_frac_of_wave_cycles"] = d["SQ_ACTIVE_INST_VALU"] / d["SQ_WAVE_CYCLES"]
+        # On this stack (ROCm 7.2, gfx950) SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU and
+        # SQ_THREAD_CYCLES_VALU equals 64 x SQ_INSTS_VALU for every kernel, including the issue-rate
+        # probe whose v_mad_u64_u32 takes twice a v_add_u32's time (profiles/r03/prof_head/
+        # probe_*): they count instructions, not cycles.  VALU issue-busy is therefore derived:
+        # wave-instructions x their issue cycles on a SIMD-32 (64-bit class 4, others 2;
+        # MI355X_MICROARCH.md) over the SIMD-cycles of the dispatch (GRBM_GUI_ACTIVE summed over
+        # the 8 XCDs = 8 x the dispatch's cycles; 1024 SIMDs).  The probe itself reads 0.81 (adds)
+        # and 0.85 (mads): loop SALU and launch / drain are the rest.
+        if all(c in d for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT64", "GRBM_GUI_ACTIVE")) and d["GRBM_GUI_ACTIVE"]:
+            cyc = 4.0 * d["SQ_INSTS_VALU_INT64"] + 2.0 * (d["SQ_INSTS_VALU"] - d["SQ_INSTS_VALU_INT64"])
+            d["valu_issue_busy"] = cyc / (1024.0 * d["GRBM_GUI_ACTIVE"] / 8.0)
+            d["dispatch_cycles"] = d["GRBM_GUI_ACTIVE"] / 8.0
+        if all(c in d for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")) and d["SQ_WAVE_CYCLES"]:
+            d["wave_frac_active"] = d["SQ_ACTIVE_INST_ANY"] / d["SQ_WAVE_CYCLES"]
+            d["wave_frac_wait_issue"] = d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"]
+            if "SQ_WAIT_ANY" in d:
+                d["wave_frac_wait_mem"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
         if "SQ_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
             d["note"] = "SQ_* cycle counters are per-SE sums in quad-cycles (MI355X_MICROARCH.md)"
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and (d["TCC_HIT_sum"] + d["TCC_MISS_sum"]):
@@ -84,6 +99,9 @@ def main():
         slots = sum((d["SQ_INSTS_VALU"] + d["SQ_INSTS_VALU_INT64"]) * 64 for d in pair)
         res["verify_w_exec_lane_slots_per_vote"] = slots / a.votes
         res["verify_valu_lane_insts_per_vote"] = sum(d["SQ_INSTS_VALU"] * 64 for d in pair) / a.votes
+    k1b = [d for k, d in res["kernels"].items() if k.startswith("txv_k_scalarmult")]
+    if k1b and "valu_issue_busy" in k1b[0]:
+        res["k1b_valu_issue_busy"] = k1b[0]["valu_issue_busy"]
     if pair and all("hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d for d in pair):
         res["hbm_bytes_per_launch"] = sum(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"] for d in pair)
         res["hbm_bytes_per_launch_raw_fetch"] = sum(d["hbm_read_bytes_raw"] + d["hbm_write_bytes"] for d in pair)
