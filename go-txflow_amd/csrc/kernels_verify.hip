@@ -275,8 +275,14 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
 #define TXV_K1B_PREFETCH 1
 #endif
 
+// TXV_K1B_NO_GATHER=1 (experiment builds only, tools/microbench/walk_rate): issue no gathers, the
+// walk reads whatever the LDS buffers hold -- the walk's time without its table traffic
+#ifndef TXV_K1B_NO_GATHER
+#define TXV_K1B_NO_GATHER 0
+#endif
 // the wave's 64 entries (entry index e_l of lane l, 128-byte units from base) -> buf
 __device__ __forceinline__ void entries_to_lds(const uint32_t* base, uint32_t e_l, uint4* buf) {
+  if (TXV_K1B_NO_GATHER) return;
   const int lane = threadIdx.x & 63;
   // all 8 permutes first (one LDS round trip instead of one per load: the compiler waits for
   // outstanding LDS operations before each LDS-DMA issue)
@@ -385,6 +391,108 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
   return R;
 }
 
+// The same walk with the entry fields staged in VGPRs (TXV_K1B_REGSTAGE, the default): addition
+// t starts with entry t's three fields already in registers; entry t+1's are read out of LDS
+// right after addition t's first three products consumed entry t's (the registers are free
+// then), so the LDS read latency hides behind the last four products instead of stalling in
+// front of each field's first use; once they are read the buffer takes entry t+3's gather.
+// Two LDS buffers per wave as in double_scalarmult_pf<.., .., 2>: entry t+1 lands during
+// addition t-1, t+2 during addition t.
+template <int WB, int WA>
+__device__ __forceinline__ ge_ext double_scalarmult_rs(const uint32_t* tb, const uint32_t* ta, uint32_t va,
+                                                       const uint32_t s_in[8], const uint32_t k_in[8], uint4* buf) {
+  static_assert(WB >= WA, "B window must be at least the A window");
+  constexpr int nB = Tab<WB>::kPositions, nA = Tab<WA>::kPositions, nT = nB + nA;
+  static_assert(nT >= 4, "schedule too short");
+  uint32_t s[8], k[8], cs = 0, ck = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = s_in[i]; k[i] = k_in[i]; }
+  auto issue = [&](int t) -> bool {           // entry t's digit and gather into buffer t % 2
+    const bool isB = t < 2 * nB && !(t & 1);
+    const int pos = t < 2 * nB ? (t >> 1) : t - nB;
+    uint4* b = buf + (t & 1) * 512;
+    if (isB) {
+      const int d = next_digit<WB>(s, cs);
+      entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), b);
+      return d < 0;
+    }
+    const int d = next_digit<WA>(k, ck);
+    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
+    return d > 0;                                   // [k](-A): a positive digit subtracts
+  };
+  const bool n0 = issue(0), n1a = issue(1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // entry 0 landed
+  fe10 qp = entry_field_lds(buf, n0, 0), qm = entry_field_lds(buf, n0, 1), qd;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bool nq2 = issue(2);
+  ge10_ext P = ge10_from_entry(qp, qm);
+  TXV_SCHED_FENCE();
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // entry 1 landed
+  qp = entry_field_lds(buf + 512, n1a, 0);
+  qm = entry_field_lds(buf + 512, n1a, 1);
+  qd = entry_field_lds(buf + 512, n1a, 2);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bool ncur = n1a, nq1 = nq2;
+  nq2 = issue(3);
+  TXV_SCHED_FENCE();
+#pragma unroll 1
+  for (int t = 1; t < nT; ++t) {
+    // VGPRs: entry t; LDS: entry t+1 (buffer (t+1) % 2) and t+2 (buffer t % 2), both gathers
+    // possibly in flight
+    const bool more = t + 1 < nT;
+    const fe10 C = fe10_cneg(fe10_mul(P.T, qd), ncur);
+    TXV_SCHED_FENCE();
+    const fe10 A = fe10_mul(fe10_sub(P.Y, P.X), qm);
+    TXV_SCHED_FENCE();
+    const fe10 B = fe10_mul(fe10_add(P.Y, P.X), qp);
+    TXV_SCHED_FENCE();
+    if (more) {
+      if (t + 2 < nT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // entry t+1 landed
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint4* bn = buf + ((t + 1) & 1) * 512;
+      qp = entry_field_lds(bn, nq1, 0);
+      qm = entry_field_lds(bn, nq1, 1);
+      qd = entry_field_lds(bn, nq1, 2);
+    }
+    TXV_SCHED_FENCE();
+    const fe10 E = fe10_sub(B, A), H = fe10_add(B, A);
+    const fe10 G = fe10_add(P.Z, C), F = fe10_sub(P.Z, C);
+    ge10_ext r;
+    r.X = fe10_mul(F, E);
+    TXV_SCHED_FENCE();
+    if (more) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // entry t+1 read out of its buffer
+      ncur = nq1;
+      nq1 = nq2;
+      if (t + 3 < nT) nq2 = issue(t + 3);
+    }
+    TXV_SCHED_FENCE();
+    r.Y = fe10_mul(H, G);
+    TXV_SCHED_FENCE();
+    r.Z = fe10_mul(F, G);
+    TXV_SCHED_FENCE();
+    r.T = more ? fe10_mul(H, E) : fe10_zero();           // the last addition's T is never read
+    TXV_SCHED_FENCE();
+    P = r;
+  }
+  ge_ext R;
+  R.X = fe_from_fe10(P.X);
+  R.Y = fe_from_fe10(P.Y);
+  R.Z = fe_from_fe10(P.Z);
+  R.T = fe_zero();
+  return R;
+}
+
+#ifndef TXV_K1B_REGSTAGE
+#define TXV_K1B_REGSTAGE 1
+#endif
+template <int WB, int WA, int PD>
+__device__ __forceinline__ ge_ext k1b_walk(const uint32_t* tb, const uint32_t* ta, uint32_t va, const uint32_t s[8],
+                                           const uint32_t k[8], uint4* buf) {
+  if constexpr (TXV_K1B_REGSTAGE && PD == 2) return double_scalarmult_rs<WB, WA>(tb, ta, va, s, k, buf);
+  else return double_scalarmult_pf<WB, WA, PD>(tb, ta, va, s, k, buf);
+}
+
 // W >= 8, V votes per lane sharing ONE field inversion (Montgomery's trick over the V
 // results: P_h = Z_0 ... Z_h; 1/Z_h = P_{h-1} / P_{V-1} walking back).  The first V-1
 // results wait in a global scratch buffer (wave-interleaved: coalesced, L2-resident,
@@ -462,7 +570,7 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
           s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
           k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
         }
-        R = double_scalarmult_pf<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+        R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
       }
 #else
       if (act >> h & 1u) {
