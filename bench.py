@@ -287,6 +287,59 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     return out
 
 
+def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
+    """C5 from received wire bytes (SURVEY.md §8f.3 + §8a a15): the C5 stream as TxVoteMessage
+    bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) through txv_ingest_msgs per
+    64k-message batch -- Reactor.Receive / decodeMsg on the GPU, CheckTxWithInfo (keys and sizes
+    computed on the GPU from the decoded records, LRU on the host), TryAddVote for the admitted
+    votes built on the device from the same records: the wire bytes cross PCIe once.
+    Latency-to-commit of a tx = return of the call that reported its commit event - the call's
+    start for the batch holding its first vote (one batch at a time)."""
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
+    ctx.bind_host_numa()
+    wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch)
+    wbs = [T.encode_msgs(b, b.txkey) for b in wl.batches]
+    wire_bytes = sum(w.nbytes for w in wbs)
+    pool = T.TxVotePool(ctx, size=wl.n + 1, cache_size=wl.n + 1, max_txs_bytes=1 << 40)
+    for w in wbs:                                   # warm-up pass
+        pool.ingest(w)
+    ctx.reset_flow()
+    pool.flush()
+    runs = []
+    for rep in range(3):
+        start, commit_t, added, ok = [], {}, 0, True
+        t0 = time.perf_counter()
+        for k, w in enumerate(wbs):
+            ts = time.perf_counter()
+            start.append(ts)
+            ws, ps, fs, ev = pool.ingest(w)
+            te = time.perf_counter()
+            ok = ok and bool((ws == T.WIRE_OK).all() and (ps == T.POOL_OK).all())
+            added += int(np.count_nonzero((fs & 0x7F) == T.ADDED))
+            for e in ev:
+                commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
+        total = time.perf_counter() - t0
+        lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
+        bl = np.diff(np.array(start + [t0 + total])) * 1e3
+        runs.append({"votes_per_s": round(wl.n / total, 1), "correct": ok and added == wl.n and len(commit_t) == wl.n_txs,
+                     "p50_batch_ms": round(float(np.median(bl)), 3),
+                     "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
+                     "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None})
+        ctx.reset_flow()
+        pool.flush()
+    pool.close()
+    ctx.close()
+    runs.sort(key=lambda r: r["votes_per_s"])
+    out = dict(runs[1])
+    out.update(workload=f"C5 as wire bytes: {n_vals} validators, {wl.n} TxVoteMessages ({wire_bytes / wl.n:.1f} B avg) in "
+                        f"{batch}-message batches through txv_ingest_msgs (decode -> pool -> TxFlow, device-resident)",
+               passes=3, votes_per_s_passes=[r["votes_per_s"] for r in runs], correct=all(r["correct"] for r in runs),
+               pcie_bytes_per_vote_up=round(wire_bytes / wl.n + 16, 1), pcie_bytes_per_vote_down=38)
+    return out
+
+
 WIRE_OUT_BYTES = 160   # per decoded message: one record (status, height, ts, offsets, lengths, TxKey, addr, sig)
 
 
@@ -585,6 +638,7 @@ def main():
         if world == 1 and not args.no_c5:
             ctx.close()
             out["c5_streaming"] = c5_streaming(local, 1000, args.c5_txs, 65536)
+            out["c5_wire"] = c5_wire_leg(local, 1000, args.c5_txs, 65536)
         if world == 1 and not args.no_c1:
             out["c1"] = c1_leg(local, threads)
         print(json.dumps(out), flush=True)

@@ -14,12 +14,19 @@
 #include <stdint.h>
 #include <string.h>
 
+// the size rules also run on the device (kernels_wire.hip: TxVote.Size() of decoded messages)
+#if defined(__HIPCC__)
+#define TXV_AHD __host__ __device__ inline
+#else
+#define TXV_AHD inline
+#endif
+
 namespace txv_host {
 
 constexpr int64_t kAminoMinSec = -62135596800LL;   // 0001-01-01T00:00:00Z
 constexpr int64_t kAminoMaxSec = 253402300800LL;   // 10000-01-01T00:00:00Z (exclusive)
 
-inline uint32_t put_uvarint(uint8_t* out, uint64_t v) {
+TXV_AHD uint32_t put_uvarint(uint8_t* out, uint64_t v) {
   uint32_t n = 0;
   while (v >= 0x80) { if (out) out[n] = (uint8_t)(v | 0x80); ++n; v >>= 7; }
   if (out) out[n] = (uint8_t)v;
@@ -27,7 +34,7 @@ inline uint32_t put_uvarint(uint8_t* out, uint64_t v) {
 }
 
 // time body length (or -1 when amino rejects the time)
-inline int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
+TXV_AHD int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
   uint32_t n = 0;
   if (sec != 0) {
     if (sec < kAminoMinSec || sec >= kAminoMaxSec) return -1;
@@ -45,7 +52,7 @@ inline int time_body(uint8_t* out, int64_t sec, int32_t nanos) {
 }
 
 // SignBytes length (or -1 when amino rejects the time), without encoding
-inline int sign_bytes_len(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t chain_len) {
+TXV_AHD int sign_bytes_len(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t chain_len) {
   const int tl = time_body(nullptr, sec, nanos);
   if (tl < 0) return -1;
   uint64_t body = 0;
@@ -99,7 +106,7 @@ inline int sign_bytes(uint8_t* out, uint32_t cap, int64_t height, const uint8_t*
   return (int)(p - out);
 }
 
-inline int txvote_size(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t addr_len,
+TXV_AHD int txvote_size(int64_t height, uint32_t txhash_len, int64_t sec, int32_t nanos, uint32_t addr_len,
                        uint32_t sig_len) {
   const int tl = time_body(nullptr, sec, nanos);
   if (tl < 0) return 0;

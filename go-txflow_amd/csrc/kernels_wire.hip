@@ -15,6 +15,8 @@
 // memory.  The 32-byte TxKey, 20-byte address and 64-byte signature are copied into their output
 // rows dword by dword with alignbit (unaligned source), zero beyond the field length; TxHash bytes
 // and long signatures are not copied: the outputs carry their offsets into the wire buffer.
+#include "amino.hpp"
+#include "sha2.h"
 #include "txv_device.h"
 #include "wire_dev.h"
 
@@ -162,6 +164,121 @@ __global__ void __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu
       __builtin_nontemporal_store(val, dst + q);   // written once, read by the host copy
     }
   }
+}
+
+// ------------------------------------------------------------------ device-resident ingest
+// (txv_ingest_msgs: Reactor.Receive -> TxVotePool.CheckTxWithInfo -> TxFlow.TryAddVote without
+// the decoded records leaving HBM)
+
+namespace {
+
+// SHA-256 of n bytes at p (any alignment; the wire buffer is padded behind its last message)
+__device__ void sha256_bytes(const uint8_t* p, uint32_t n, uint32_t st[8]) {
+  txv::sha256_init(st);
+  const uint32_t nblk = (n + 9 + 63) / 64;       // message + 0x80 + 8-byte length
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t k = 64u * b + 4u * (uint32_t)t + (uint32_t)q;   // byte index in the padded message
+        uint32_t byte = 0;
+        if (k < n) byte = p[k];
+        else if (k == n) byte = 0x80u;
+        v = (v << 8) | byte;
+      }
+      w[t] = v;
+    }
+    if (b == nblk - 1) { w[14] = (uint32_t)((uint64_t)n >> 29); w[15] = n << 3; }
+    txv::sha256_block(st, w);
+  }
+}
+
+}  // namespace
+
+// Per decoded message (records of txv_k_decode_msgs): its wire status, and for the decoded ones
+// txVoteKey = SHA-256(Signature) (txvotepool/txvotepool.go:467-469: the first 64 bytes come from
+// the record, longer signatures are hashed from the wire buffer) and TxVote.Size()
+// (types/tx_vote.go:144-150: 0 when amino rejects the time) -- everything the pool's
+// order-dependent admission needs; the longest TxHash goes to max_hl (SignBytes column bound).
+__global__ void __launch_bounds__(256) txv_k_rec_keys(const uint32_t* __restrict__ rec, const uint8_t* __restrict__ wire,
+                                                      uint32_t n, uint8_t* __restrict__ status,
+                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ sizes,
+                                                      uint32_t* max_hl) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* r = rec + (size_t)i * TXV_WIRE_REC_WORDS;
+  const uint32_t stt = r[0];
+  status[i] = (uint8_t)stt;
+  if (stt != 0) return;
+  const int64_t height = (int64_t)((uint64_t)r[1] | ((uint64_t)r[2] << 32));
+  const int64_t sec = (int64_t)((uint64_t)r[3] | ((uint64_t)r[4] << 32));
+  const uint32_t hl = r[7], al = r[8], sl = r[10];
+  sizes[i] = (uint32_t)txv_host::txvote_size(height, hl, sec, (int32_t)r[5], al, sl);
+  if (hl) atomicMax(max_hl, hl);
+  uint32_t st[8];
+  if (sl <= 64) {   // the record's signature words (little-endian, zero beyond sig_len)
+    uint32_t w[16];
+    txv::sha256_init(st);
+    const uint32_t nblk = sl <= 55 ? 1u : 2u;
+    for (uint32_t b = 0; b < nblk; ++b) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const uint32_t gw = 16u * b + (uint32_t)t;
+        uint32_t v = gw < 16 ? txv::bswap32(r[24 + gw]) : 0u;
+        if (gw == sl / 4) v |= 0x80000000u >> (8 * (sl & 3));
+        if (gw == 16u * nblk - 1u) v = sl * 8u;
+        w[t] = v;
+      }
+      txv::sha256_block(st, w);
+    }
+  } else {
+    sha256_bytes(wire + r[9], sl, st);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) keys[(size_t)i * 8 + j] = txv::bswap32(st[j]);
+}
+
+// The admitted messages (pool OK, arrival order) -> the flow slot's raw TxVote columns, the
+// layout txv_add_votes uploads (txv_flow.h FlowBatch): the TxHash offsets stay offsets into the
+// wire buffer, which is the batch's TxHash arena.
+__global__ void __launch_bounds__(256) txv_k_rec_to_flow(const uint32_t* __restrict__ rec,
+                                                         const uint32_t* __restrict__ list, uint32_t n, FlowCols c) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t* r = rec + (size_t)list[j] * TXV_WIRE_REC_WORDS;
+  c.height[j] = (int64_t)((uint64_t)r[1] | ((uint64_t)r[2] << 32));
+  c.ts_sec[j] = (int64_t)((uint64_t)r[3] | ((uint64_t)r[4] << 32));
+  c.ts_nanos[j] = (int32_t)r[5];
+  c.th_off[j] = r[6];
+  c.th_len[j] = r[7];
+  c.addr_len[j] = r[8];
+  c.sig_len[j] = r[10];
+  uint32_t* a = reinterpret_cast<uint32_t*>(c.addr + (size_t)j * 20);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) a[q] = r[19 + q];
+  uint4* sg = reinterpret_cast<uint4*>(c.sig + (size_t)j * 64);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sg[q] = make_uint4(r[24 + 4 * q], r[25 + 4 * q], r[26 + 4 * q], r[27 + 4 * q]);
+  uint4* tk = reinterpret_cast<uint4*>(c.txkey + (size_t)j * 32);
+  tk[0] = make_uint4(r[11], r[12], r[13], r[14]);
+  tk[1] = make_uint4(r[15], r[16], r[17], r[18]);
+}
+
+extern "C" hipError_t txv_launch_rec_keys(const uint32_t* rec, const uint8_t* wire, uint32_t n, uint8_t* status,
+                                          uint32_t* keys, uint32_t* sizes, uint32_t* max_hl, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_rec_keys, dim3((n + 255) / 256), dim3(256), 0, st, rec, wire, n, status, keys, sizes, max_hl);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t txv_launch_rec_to_flow(const uint32_t* rec, const uint32_t* list, uint32_t n, const FlowCols* c,
+                                             hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_rec_to_flow, dim3((n + 255) / 256), dim3(256), 0, st, rec, list, n, *c);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t txv_launch_decode_msgs(const WireArgs* a, uint32_t grid, hipStream_t st) {

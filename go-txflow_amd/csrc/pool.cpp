@@ -423,39 +423,34 @@ int txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out) {
 
 void txv_pool_free(txv_pool* p) { delete p; }
 
-int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
-                   const uint64_t* sig_full_off, uint8_t* status_out) {
-  if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
-  std::lock_guard<std::mutex> g(p->mu);
-  const auto t0 = std::chrono::steady_clock::now();
-  int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
-  if (r) return r;
+}  // extern "C"
+
+namespace {
+
+// CheckTxWithInfo for n votes in arrival order whose keys (keys) and TxVote.Size() values
+// (p->sizes) are known: the order-dependent part (caps, cache, pool list).  p->mu is held.
+int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
   const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
-  const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
-  // TxVote.Size() of every vote on the worker threads (order-independent)
-  // (and for the fast path: the summed sizes, the too-large / WAL caps, each key's partition)
-  p->sizes.resize(v->n);
-  const uint32_t n = v->n;
+  // for the fast path: the summed sizes, the too-large / WAL caps, each key's partition
   const bool fast = n >= 4096;
-  if (fast) p->part.resize(n);
   std::atomic<uint64_t> sum_a{0};
   std::atomic<bool> capped{false};
-  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-    uint64_t sm = 0;
-    bool cp = false;
-    for (uint32_t i = lo; i < hi; ++i) {
-      const uint32_t sz = vote_size(v, i);
-      p->sizes[i] = sz;
-      if (!fast) continue;
-      cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
-      sm += sz;
-      p->part[i] = (uint8_t)PartIndex::part(keys[i]);
-    }
-    if (!fast) return;
-    sum_a += sm;
-    if (cp) capped = true;
-  });
+  if (fast) {
+    p->part.resize(n);
+    txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+      uint64_t sm = 0;
+      bool cp = false;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t sz = p->sizes[i];
+        cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
+        sm += sz;
+        p->part[i] = (uint8_t)PartIndex::part(keys[i]);
+      }
+      sum_a += sm;
+      if (cp) capped = true;
+    });
+  }
   // Fast path: when no vote of the batch can hit a size cap, a cache eviction or the WAL rule,
   // the sequential loop would admit every vote whose key is new -- so if every key is new (in
   // the cache and within the batch) the result is "all admitted, in order".  The keys go into
@@ -465,8 +460,7 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   if (fast && try_batch_admit(p, ctx, keys, n, sum_a.load(), capped.load(), p->part.data(), status_out)) {
     if (getenv("TXV_PROFILE_HOST")) {
       const auto t2 = std::chrono::steady_clock::now();
-      fprintf(stderr, "[txv pool] keys=%.3fms batch-admit=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
-              std::chrono::duration<double, std::milli>(t2 - t1).count(), v->n);
+      fprintf(stderr, "[txv pool] batch-admit=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t2 - t1).count(), n);
     }
     return TXV_OK;
   }
@@ -497,10 +491,48 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   }
   if (getenv("TXV_PROFILE_HOST")) {
     const auto t2 = std::chrono::steady_clock::now();
-    fprintf(stderr, "[txv pool] keys=%.3fms lru=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t2 - t1).count(), v->n);
+    fprintf(stderr, "[txv pool] lru=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t2 - t1).count(), n);
   }
   return TXV_OK;
+}
+
+}  // namespace
+
+// the pool's MaxMsgBytes (Reactor.Receive's decodeMsg cap, reactor.go:278-284)
+uint32_t txv_pool_max_msg_bytes(txv_pool* p) {
+  std::lock_guard<std::mutex> g(p->mu);
+  return p->cfg.max_msg_bytes;
+}
+
+// CheckTxWithInfo for n votes whose keys (n x 32 bytes) and Size() values were computed on the
+// device from decoded wire records (runtime.cpp txv_ingest_msgs)
+int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
+                        uint8_t* status_out) {
+  if (!p || !ctx || (n && (!keys32 || !sizes || !status_out))) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->sizes.assign(sizes, sizes + n);
+  return pool_admit(p, ctx, reinterpret_cast<const Key*>(keys32), n, status_out);
+}
+
+extern "C" {
+
+int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
+                   const uint64_t* sig_full_off, uint8_t* status_out) {
+  if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  const auto t0 = std::chrono::steady_clock::now();
+  int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
+  if (r) return r;
+  const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
+  // TxVote.Size() of every vote on the worker threads (order-independent)
+  p->sizes.resize(v->n);
+  txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
+  });
+  if (getenv("TXV_PROFILE_HOST"))
+    fprintf(stderr, "[txv pool] keys+sizes=%.3fms n=%u\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
+  return pool_admit(p, ctx, keys, v->n, status_out);
 }
 
 int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,

@@ -52,7 +52,9 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #ifndef TXV_K1A_ON_KEY_STREAM
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
-constexpr uint32_t kSlots = 6;   // 0-3 staged (0, 1 also the submit ring), 4 signer, 5 verify-only
+constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0, 1 also the submit ring)
+constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest
+constexpr uint32_t kSlots = 7;
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
@@ -215,6 +217,12 @@ struct txv_ctx {
   uint8_t *d_wd_out = nullptr, *h_wd_out = nullptr;
   uint64_t *d_wd_span = nullptr, *h_wd_span = nullptr;   // [chunks][2] byte span of each 128-message chunk
   hipEvent_t wd_ev[2] = {nullptr, nullptr};
+  // txv_ingest_msgs (wire bytes -> pool -> TxFlow, device-resident): per-message status, keys,
+  // sizes and the longest TxHash (device + pinned host), the admitted messages' indices
+  uint32_t ing_cap = 0;
+  uint8_t *d_ing_status = nullptr, *h_ing_status = nullptr;
+  uint32_t *d_ing_keys = nullptr, *h_ing_keys = nullptr, *d_ing_sizes = nullptr, *h_ing_sizes = nullptr;
+  uint32_t *d_ing_list = nullptr, *h_ing_list = nullptr, *d_ing_max = nullptr, *h_ing_max = nullptr;
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -1241,7 +1249,7 @@ int txv_verify_batch(txv_ctx* c, const txv_votes* v, const uint8_t* pubs32, uint
   HIP_TRY(c, hipSetDevice(c->device));
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
   if (!pubs32 && !c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
-  Slot& s = c->slots[kSlots - 1];
+  Slot& s = c->slots[kVerifySlot];
   std::vector<int> lens;
   const uint32_t mx = encode_all(c, s, v, c->chain.data(), (uint32_t)c->chain.size(), lens);
   const uint32_t mw = std::max<uint32_t>(1, (mx + 7) / 8);
@@ -1299,7 +1307,7 @@ int txv_verify_bytes(txv_ctx* c, const uint8_t* pubs32, const uint8_t* msgs, con
   HIP_TRY(c, hipSetDevice(c->device));
   if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
   if (!n) return TXV_OK;
-  Slot& s = c->slots[kSlots - 1];
+  Slot& s = c->slots[kVerifySlot];
   // the messages go to the device as they are (SHA-512 input R || A || msg)
   std::vector<int> lens(n);
   s.tmp_msg.clear();
@@ -1635,7 +1643,7 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
   HIP_TRY(c, hipSetDevice(c->device));
   for (uint32_t i = 0; i < v->n; ++i)
     if (signer[i] >= c->n_signers) { c->err = "signer index out of range"; return TXV_EINVAL; }
-  Slot& s = c->slots[kSlots - 2];
+  Slot& s = c->slots[kSignerSlot];
   // SignBytes are built on the device (txv_k_signbytes), the same encoder the AddVote path uses
   std::vector<int> lens(v->n);
   uint32_t mx = 0;
@@ -1676,7 +1684,7 @@ int txv_sign_votes(txv_ctx* c, const txv_votes* v, const uint32_t* signer, const
 }
 
 int txv_stage(txv_ctx* c, uint32_t slot, const txv_votes* v) {
-  if (!c || !v || slot >= kSlots - 2) return TXV_EINVAL;
+  if (!c || !v || slot >= kStagedSlots) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->slots[slot].ticket) { c->err = "slot holds a txv_submit_votes batch in flight"; return TXV_ESTATE; }
@@ -1687,7 +1695,7 @@ int txv_stage(txv_ctx* c, uint32_t slot, const txv_votes* v) {
 }
 
 int txv_run_staged(txv_ctx* c, uint32_t slot, float* ms) {
-  if (!c || slot >= kSlots - 2) return TXV_EINVAL;
+  if (!c || slot >= kStagedSlots) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->slots[slot].ticket) { c->err = "slot holds a txv_submit_votes batch in flight"; return TXV_ESTATE; }
@@ -1696,14 +1704,14 @@ int txv_run_staged(txv_ctx* c, uint32_t slot, float* ms) {
 
 int txv_fetch_staged(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
                      uint32_t* n_ev) {
-  if (!c || slot >= kSlots - 2) return TXV_EINVAL;
+  if (!c || slot >= kStagedSlots) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   return fetch_slot(c, slot, status_out, ev, ev_cap, n_ev);
 }
 
 int txv_set_commit_sink(txv_ctx* c, uint32_t slot, void* dst_dev, uint32_t n_sets_cap) {
-  if (!c || slot >= kSlots - 2 || (dst_dev && !n_sets_cap)) return TXV_EINVAL;
+  if (!c || slot >= kStagedSlots || (dst_dev && !n_sets_cap)) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   Slot& s = c->slots[slot];
@@ -1715,7 +1723,7 @@ int txv_set_commit_sink(txv_ctx* c, uint32_t slot, void* dst_dev, uint32_t n_set
 }
 
 int txv_slot_kernel_ms(txv_ctx* c, uint32_t slot, float* ms4) {
-  if (!c || !ms4 || slot >= kSlots - 2) return TXV_EINVAL;
+  if (!c || !ms4 || slot >= kStagedSlots) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   Slot& s = c->slots[slot];
@@ -2210,6 +2218,177 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
   if (!r) r = txv_decode_run(c, max_msg_bytes, 1, nullptr);
   if (!r) r = txv_decode_fetch(c, out);
   return r;
+}
+
+}  // extern "C"
+
+int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
+                        uint8_t* status_out);   // pool.cpp
+uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
+
+namespace {
+
+// Reactor.Receive -> CheckTxWithInfo -> TryAddVote for one batch of received messages, with the
+// decoded votes kept in HBM (txv_ingest_msgs): c->mu is held.
+int ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint8_t* flow_status,
+                txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev) {
+  if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+  if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+  if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
+  for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernels trust these
+    if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
+      c->err = "message " + std::to_string(i) + " outside the wire buffer";
+      return TXV_EINVAL;
+    }
+  if (n_ev) *n_ev = 0;
+  if (!n) return TXV_OK;
+  HostTimer ht(c->profile_host);
+  Slot& s = c->slots[kIngestSlot];
+  int r;
+  // buffers: decode records / offsets (shared with txv_decode_*), the per-message outputs
+  if (n > c->wd_cap) {
+    const uint32_t cap = std::max<uint32_t>(n, 1024);
+    if ((r = dalloc(c, &c->d_wd_off, cap)) || (r = halloc(c, &c->h_wd_off, cap)) || (r = dalloc(c, &c->d_wd_len, cap)) ||
+        (r = halloc(c, &c->h_wd_len, cap)) || (r = dalloc(c, &c->d_wd_out, wire_out_bytes(cap))) ||
+        (r = halloc(c, &c->h_wd_out, wire_out_bytes(cap))) ||
+        (r = dalloc(c, &c->d_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))) ||
+        (r = halloc(c, &c->h_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))))
+      return r;
+    c->wd_cap = cap;
+  }
+  if (n > c->ing_cap) {
+    const uint32_t cap = std::max<uint32_t>(n, 1024);
+    if ((r = dalloc(c, &c->d_ing_status, cap)) || (r = halloc(c, &c->h_ing_status, cap)) ||
+        (r = dalloc(c, &c->d_ing_keys, (size_t)cap * 8)) || (r = halloc(c, &c->h_ing_keys, (size_t)cap * 8)) ||
+        (r = dalloc(c, &c->d_ing_sizes, cap)) || (r = halloc(c, &c->h_ing_sizes, cap)) ||
+        (r = dalloc(c, &c->d_ing_list, cap)) || (r = halloc(c, &c->h_ing_list, cap)) ||
+        (r = dalloc(c, &c->d_ing_max, 1)) || (r = halloc(c, &c->h_ing_max, 1)))
+      return r;
+    c->ing_cap = cap;
+  }
+  // the wire bytes go straight into the slot's TxHash arena: the decoded TxHash offsets index it
+  if (wire_bytes + 128 > s.arena_cap) {
+    const size_t cap = std::max<size_t>((size_t)wire_bytes + 128, s.arena_cap * 2);
+    if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
+    s.arena_cap = cap;
+  }
+  if ((r = ensure_flow_slot(c, s, n))) return r;
+  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->key_stream, s.ev[4], 0));   // the slot's last chain ended
+  c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
+    const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
+    memcpy(s.h_arena + a, wire + a, b - a);
+  }, 16);
+  memset(s.h_arena + wire_bytes, 0, 128);
+  memcpy(c->h_wd_off, msg_off, (size_t)n * 8);
+  memcpy(c->h_wd_len, msg_len, (size_t)n * 4);
+  const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
+  c->pool->parallel_for(n_chunks, [&](uint32_t lo_c, uint32_t hi_c) {
+    for (uint32_t k = lo_c; k < hi_c; ++k) {
+      uint64_t lo = ~0ull, hi = 0;
+      for (uint32_t i = k * TXV_WIRE_BLOCK; i < std::min<uint32_t>(n, (k + 1) * TXV_WIRE_BLOCK); ++i)
+        if (msg_len[i]) { lo = std::min(lo, msg_off[i]); hi = std::max(hi, msg_off[i] + msg_len[i]); }
+      if (hi == 0) lo = 0;
+      c->h_wd_span[2 * k] = lo & ~15ull;
+      c->h_wd_span[2 * k + 1] = hi;
+    }
+  }, 64);
+  *c->h_ing_max = 0;
+  hipStream_t ks = c->key_stream;
+  HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->d_wd_off, c->h_wd_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->d_wd_len, c->h_wd_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->d_wd_span, c->h_wd_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->d_ing_max, c->h_ing_max, 4, hipMemcpyHostToDevice, ks));
+  ht.mark("upload");
+  // decodeMsg (kernels_wire.hip) into records in HBM, then per decoded message its pool key and
+  // TxVote.Size(); only statuses, keys and sizes cross PCIe
+  WireArgs a{};
+  a.n = n;
+  a.max_msg_bytes = txv_pool_max_msg_bytes(p);
+  txvote_msg_disfix(&a.disamb, &a.prefix);
+  a.wire = s.d_arena_th; a.off = c->d_wd_off; a.len = c->d_wd_len;
+  a.rec = reinterpret_cast<uint32_t*>(c->d_wd_out);
+  a.n_chunks = n_chunks;
+  a.span = c->d_wd_span;
+  HIP_TRY(c, txv_launch_decode_msgs(&a, (uint32_t)c->n_cus * 5u, ks));
+  HIP_TRY(c, txv_launch_rec_keys(a.rec, s.d_arena_th, n, c->d_ing_status, c->d_ing_keys, c->d_ing_sizes, c->d_ing_max, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ing_status, c->d_ing_status, n, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ing_keys, c->d_ing_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ing_sizes, c->d_ing_sizes, (size_t)n * 4, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ing_max, c->d_ing_max, 4, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipStreamSynchronize(ks));
+  ht.mark("decode_keys");
+  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it)
+  std::vector<uint32_t> ok;
+  ok.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (wire_status) wire_status[i] = c->h_ing_status[i];
+    if (pool_status) pool_status[i] = TXV_POOL_NOT_CHECKED;
+    if (flow_status) flow_status[i] = TXV_FLOW_NOT_ADDED;
+    if (c->h_ing_status[i] == TXV_WIRE_OK) ok.push_back(i);
+  }
+  const uint32_t m = (uint32_t)ok.size();
+  std::vector<uint8_t> keys((size_t)m * 32), pst(m);
+  std::vector<uint32_t> sizes(m);
+  c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t j = lo; j < hi; ++j) {
+      memcpy(keys.data() + (size_t)j * 32, c->h_ing_keys + (size_t)ok[j] * 8, 32);
+      sizes[j] = c->h_ing_sizes[ok[j]];
+    }
+  }, 8192);
+  if ((r = txv_pool_check_keys(p, c, keys.data(), sizes.data(), m, pst.data()))) return r;
+  uint32_t n_adm = 0;
+  for (uint32_t j = 0; j < m; ++j) {
+    if (pool_status) pool_status[ok[j]] = pst[j];
+    if (pst[j] == TXV_POOL_OK) c->h_ing_list[n_adm++] = ok[j];
+  }
+  ht.mark("pool");
+  if (!n_adm) return TXV_OK;
+  // the admitted votes -> the slot's TxVote columns on the device, then the AddVote chain
+  const uint32_t chain_len = (uint32_t)c->chain.size();
+  const uint32_t mw = (signbytes_bound(*c->h_ing_max, chain_len) + 7) / 8;
+  if ((r = ensure_slot(c, s, n_adm, mw))) return r;
+  HIP_TRY(c, hipMemcpyAsync(c->d_ing_list, c->h_ing_list, (size_t)n_adm * 4, hipMemcpyHostToDevice, ks));
+  FlowCols fc{s.d_fh, s.d_fs, s.d_fn, s.d_fo, s.d_fl, s.d_addr, s.d_addr_len, s.d_sigraw, s.d_sig_len, s.d_txkey};
+  HIP_TRY(c, txv_launch_rec_to_flow(a.rec, c->d_ing_list, n_adm, &fc, ks));
+  HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's kernels wait for this
+  s.n = n_adm; s.n_pad = (n_adm + 63) / 64 * 64; s.msg_words = mw;
+  s.has_nil = false;
+  s.has_txkey = true;
+  s.seq_base = c->seq_next;
+  c->seq_next += n_adm;
+  s.staged = true; s.ran = false;
+  if ((r = run_slot(c, kIngestSlot, nullptr))) return r;
+  std::vector<uint8_t> fst(n_adm);
+  std::vector<txv_commit_event> evs(ev_out ? std::min(ev_cap, n_adm) : 0);
+  uint32_t ne = 0;
+  if ((r = fetch_slot(c, kIngestSlot, fst.data(), evs.data(), (uint32_t)evs.size(), &ne))) return r;
+  ht.mark("flow");
+  if (flow_status)
+    for (uint32_t j = 0; j < n_adm; ++j) flow_status[c->h_ing_list[j]] = fst[j];
+  for (uint32_t e = 0; e < std::min<uint32_t>(ne, (uint32_t)evs.size()); ++e) {   // batch index -> message index
+    txv_commit_event x = evs[e];
+    x.vote_index = c->h_ing_list[x.vote_index];
+    ev_out[e] = x;
+  }
+  if (n_ev) *n_ev = ne;
+  return TXV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                    const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status,
+                    uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev) {
+  if (!c || !p || (n && (!wire || !msg_off || !msg_len))) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  return ingest_msgs(c, p, wire, wire_bytes, msg_off, msg_len, n, wire_status, pool_status, flow_status, ev_out,
+                     ev_cap, n_ev);
 }
 
 }  // extern "C"

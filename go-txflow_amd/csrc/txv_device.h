@@ -92,8 +92,21 @@ struct WireArgs {
   uint32_t* rec;               // [n][TXV_WIRE_REC_WORDS]
 };
 
+// the raw TxVote columns of a flow slot, written on the device from decoded wire records
+struct FlowCols {
+  int64_t* height; int64_t* ts_sec; int32_t* ts_nanos;
+  uint32_t* th_off; uint32_t* th_len;
+  uint8_t* addr; uint32_t* addr_len;    // [n][20]
+  uint8_t* sig; uint32_t* sig_len;      // [n][64]
+  uint8_t* txkey;                       // [n][32]
+};
+
 extern "C" {
 hipError_t txv_launch_decode_msgs(const WireArgs* args, uint32_t grid, hipStream_t st);
+hipError_t txv_launch_rec_keys(const uint32_t* rec, const uint8_t* wire, uint32_t n, uint8_t* status, uint32_t* keys,
+                               uint32_t* sizes, uint32_t* max_hl, hipStream_t st);
+hipError_t txv_launch_rec_to_flow(const uint32_t* rec, const uint32_t* list, uint32_t n, const FlowCols* c,
+                                  hipStream_t st);
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);

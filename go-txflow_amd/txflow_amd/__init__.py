@@ -144,6 +144,8 @@ def lib():
             "txv_decode_run": ([vp, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "txv_decode_fetch": ([vp, ctypes.POINTER(_WireVotes)], ctypes.c_int),
             "txv_pool_receive": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp], ctypes.c_int),
+            "txv_ingest_msgs": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp, vp, vp, u32, ctypes.POINTER(u32)],
+                                ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
@@ -181,7 +183,7 @@ EXPORTED_SYMBOLS = [
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
-    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_flow_stream"]
+    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_flow_stream", "txv_ingest_msgs"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -776,6 +778,7 @@ def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):
 
 
 POOL_OK, POOL_ERR_FULL, POOL_ERR_TOO_LARGE, POOL_ERR_IN_CACHE, POOL_ERR_ENCODING = range(5)
+FLOW_NOT_ADDED = 0xFE   # TXV_FLOW_NOT_ADDED: a message the pool did not admit (txv_ingest_msgs)
 POOL_NO_CACHE = 0xFFFFFFFF
 POOL_WAL = 0x1      # TXV_POOL_WAL
 
@@ -821,6 +824,22 @@ class TxVotePool:
                                              wb.len.ctypes.data, wb.n, ws.ctypes.data, ps.ctypes.data),
                       "txv_pool_receive")
         return ws[:wb.n], ps[:wb.n]
+
+    def ingest(self, wb: WireBatch, ev_cap: int = 0):
+        """txv_ingest_msgs: Reactor.Receive -> CheckTxWithInfo -> TxFlow.TryAddVote for a batch of
+        received messages with the decoded votes kept on the device.  Returns (wire status, pool
+        status, flow status (FLOW_NOT_ADDED unless admitted), commit events by message index)."""
+        n = wb.n
+        ws = np.zeros(max(n, 1), np.uint8)
+        ps = np.zeros(max(n, 1), np.uint8)
+        fs = np.zeros(max(n, 1), np.uint8)
+        ev_cap = ev_cap or max(n, 1)
+        evs = np.zeros(ev_cap, EVENT_DTYPE)
+        nev = ctypes.c_uint32()
+        self.ctx._chk(lib().txv_ingest_msgs(self.ctx._h, self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                            wb.len.ctypes.data, n, ws.ctypes.data, ps.ctypes.data, fs.ctypes.data,
+                                            evs.ctypes.data, ev_cap, ctypes.byref(nev)), "txv_ingest_msgs")
+        return ws[:n], ps[:n], fs[:n], evs[:min(nev.value, ev_cap)]
 
     def update(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
         full, off = _long_sig_arena(batch, long_sigs)

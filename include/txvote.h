@@ -432,6 +432,24 @@ int txv_encode_msgs(const txv_votes* votes, const uint8_t* txkey, const uint8_t*
 int txv_pool_receive(txv_pool* pool, txv_ctx* ctx, const uint8_t* wire, uint64_t wire_bytes,
                      const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status_out,
                      uint8_t* pool_status_out);
+/* The whole ingest chain for n received messages in arrival order, device-resident:
+ *   Reactor.Receive / decodeMsg (txvotepool/reactor.go:170-190, 278-284)
+ *   -> TxVotePool.CheckTxWithInfo (txvotepool/txvotepool.go:187-261) for every decoded vote
+ *   -> TxFlow.TryAddVote (txflow/service.go:169-234) for every vote the pool admitted, in order
+ * (the order the reference's checkMaj23Routine walks the pool's list, service.go:123-166).
+ * The wire bytes are uploaded once; the decoded votes stay in HBM: the pool's keys
+ * (SHA-256(Signature)) and TxVote.Size() are computed on the device and only they cross back
+ * for the order-dependent LRU admission; the admitted votes' TxVote columns are built on the
+ * device from the decoded records and run through the AddVote chain of txv_add_votes.
+ * wire_status[i] = TXV_WIRE_*; pool_status[i] = TXV_POOL_* (TXV_POOL_NOT_CHECKED when not
+ * decoded); flow_status[i] = txv_add_votes' status (| TXV_STATUS_FIRED) for admitted votes,
+ * TXV_FLOW_NOT_ADDED otherwise; commit events (up to ev_cap; *n_ev = total) carry the MESSAGE
+ * index as vote_index.  Any output pointer may be NULL. */
+#define TXV_FLOW_NOT_ADDED 0xFE
+int txv_ingest_msgs(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
+                    const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status,
+                    uint8_t* pool_status, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
+                    uint32_t* n_ev);
 
 /* ---- self-test hook: field/scalar ops on device (tests only) ---- */
 int txv_fe_selftest(txv_ctx* ctx, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op);

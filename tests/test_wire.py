@@ -311,3 +311,104 @@ def test_host_encoder_matches_oracle():
         assert wb.msg(i) == exp, i
     with pytest.raises(T.TxvInfraError):   # amino rejects the time: MustMarshalBinaryBare panics
         T.encode_msgs(T.VoteBatch.from_votes([T.TxVote(Height=1, TxHash="A", Timestamp=(1 << 40, 0))]))
+
+
+@pytest.mark.gpu
+def test_gpu_ingest_chain_matches_oracle():
+    """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
+    kept in HBM) over three batches of received messages against the oracle's decoder, pool and
+    sequential TxFlow: signed votes, exact replays of earlier messages (ErrTxInCache while the
+    bounded LRU still holds their key, DUPLICATE once it evicted it), conflicting signatures,
+    corrupted ones, a 65-byte signature (its key hashes all 65 bytes), non-canonical framings and
+    undecodable / oversize messages.  Per message: wire status, pool status, flow status + fired
+    bit; commit events by message index; the pool and TxFlow state at the end."""
+    import txflow_amd as T
+    rng = random.Random(31)
+    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16)
+    try:
+        seeds = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(7)]
+        powers = [1, 2, 3, 1, 1, 2, 1]
+        pubs = ctx.keygen(seeds)
+        ctx.set_validators(pubs, powers, "test_chain_id")
+        addrs, _ = ctx.validator_info()
+        votes, signer = [], []
+        for t in range(60):
+            h = hashlib.sha256(b"ingest%d" % t).hexdigest().upper()
+            tk = hashlib.sha256(b"key%d" % t).digest()
+            for v in range(7):
+                votes.append(T.TxVote(Height=1 + (t % 3 == 0), TxHash=h, TxKey=tk,
+                                      Timestamp=(1_700_000_000, 1 + len(votes)), ValidatorAddress=addrs[v]))
+                signer.append(v)
+        sigs = ctx.sign_votes(T.VoteBatch.from_votes(votes), np.array(signer, np.uint32), "test_chain_id")
+        for v, s in zip(votes, sigs):
+            v.Signature = s.tobytes()
+
+        def wire_of(v):
+            return O.wire_encode(v.Height, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], v.ValidatorAddress,
+                                 v.Signature, v.TxKey)
+
+        order = list(range(len(votes)))
+        rng.shuffle(order)
+        stream = []
+        for j in order:
+            v = votes[j]
+            stream.append(wire_of(v))
+            r = rng.random()
+            if r < 0.08:                                  # a replay of an earlier message
+                stream.append(stream[rng.randrange(len(stream))])
+            elif r < 0.14:                                # same validator + tx, another signature
+                c = T.TxVote(Height=v.Height, TxHash=v.TxHash, TxKey=v.TxKey, Timestamp=v.Timestamp,
+                             ValidatorAddress=v.ValidatorAddress, Signature=bytes([v.Signature[0] ^ 4]) + v.Signature[1:])
+                stream.append(wire_of(c))
+            elif r < 0.17:                                # a 65-byte signature
+                c = T.TxVote(Height=v.Height, TxHash=v.TxHash, TxKey=v.TxKey, Timestamp=v.Timestamp,
+                             ValidatorAddress=v.ValidatorAddress, Signature=v.Signature + b"\x07")
+                stream.append(wire_of(c))
+        junk = G.messages(120, seed=5, p_noncanon=0.3, p_mutate=0.5) + [b"", b"\x01" * 5000]
+        for m in junk:
+            stream.insert(rng.randrange(len(stream) + 1), m)
+        max_msg = 4096
+        pool = T.TxVotePool(ctx, size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
+        opool = O.Pool(size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
+        flow = O.Flow(pubs, powers, b"test_chain_id")
+        committed, cuts = set(), [0, len(stream) // 3, 2 * len(stream) // 3, len(stream)]
+        seen = {"cache": 0, "dup": 0, "fired": 0, "undecoded": 0, "nondet": 0, "invalid": 0}
+        for b in range(3):
+            part = stream[cuts[b]:cuts[b + 1]]
+            ws, ps, fs, ev = pool.ingest(T.WireBatch(part))
+            exp_fired = []
+            for i, m in enumerate(part):
+                st, f = O.wire_decode(m, max_msg)
+                assert ws[i] == st, (b, i)
+                if st != O.WIRE_OK:
+                    seen["undecoded"] += 1
+                    assert ps[i] == T.POOL_NOT_CHECKED and fs[i] == T.FLOW_NOT_ADDED, (b, i)
+                    continue
+                ov = dict(height=f["height"], txhash=f["txhash"], ts_sec=f["ts_sec"], ts_nanos=f["ts_nanos"],
+                          addr=f["addr"], sig=f["sig"])
+                op = opool.check([ov])[0]
+                assert ps[i] == op, (b, i, int(ps[i]), int(op))
+                if op != T.POOL_OK:
+                    seen["cache"] += op == T.POOL_ERR_IN_CACHE
+                    assert fs[i] == T.FLOW_NOT_ADDED, (b, i)
+                    continue
+                ost, _, ofired = flow.add_votes([ov])
+                exp = int(ost[0]) | (int(ofired[0]) << 7)
+                assert fs[i] == exp, (b, i, int(fs[i]), exp)
+                seen["dup"] += ost[0] == T.DUPLICATE
+                seen["nondet"] += ost[0] == 5
+                seen["invalid"] += ost[0] == 6
+                if ofired[0] and f["txhash"] not in committed:
+                    committed.add(f["txhash"])
+                    exp_fired.append(i)
+                seen["fired"] += int(ofired[0])
+            assert sorted(int(e["vote_index"]) for e in ev) == exp_fired, b
+        assert pool.Size() == opool.size() and pool.TxsBytes() == opool.txs_bytes()
+        assert np.array_equal(pool.cache_keys(), opool.cache_keys())      # the LRU order too
+        for t in range(60):
+            h = hashlib.sha256(b"ingest%d" % t).hexdigest().upper().encode()
+            assert ctx.query_tx(h) == flow.query(h)
+        assert all(seen[k] > 0 for k in seen), seen
+        pool.close()
+    finally:
+        ctx.close()
