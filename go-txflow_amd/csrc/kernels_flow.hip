@@ -919,6 +919,19 @@ hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets
   return hipGetLastError();
 }
 
+// a column every element of which is the same value (the host saw a uniform column and did not
+// upload it: txv_submit_votes' staging)
+__global__ void __launch_bounds__(256) txv_k_fill64(uint64_t* dst, uint64_t v, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = v;
+}
+
+hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_fill64, dim3((n + 255) / 256), dim3(256), 0, st, dst, v, n);
+  return hipGetLastError();
+}
+
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st) {
   hipLaunchKernelGGL(txv_k_reset_sets, dim3(1024), dim3(256), 0, st, *fs, keep_ids);
   hipLaunchKernelGGL(txv_k_reset_counters, dim3(1), dim3(1), 0, st, *fs, keep_ids);

@@ -171,6 +171,7 @@ struct txv_ctx {
   uint32_t* d_tmp_pubs = nullptr; uint8_t* d_tmp_ok = nullptr; uint32_t* d_tmp_tables = nullptr; uint32_t* d_tmp_addr = nullptr;
   std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
   bool profile_host = false;                    // TXV_PROFILE_HOST
+  bool uniform_cols = true;                     // uniform columns filled on the device (TXV_UNIFORM_COLS=0: off)
   // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
   // accepted-vote arena, counters
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
@@ -632,19 +633,34 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   HostTimer ht(c->profile_host);
   std::atomic<uint64_t> arena_end{0};
   std::atomic<uint32_t> max_hl{0};
+  // columns whose every element equals the first are not uploaded but filled on the device
+  // (height, seconds and the three length columns: 28 of a vote's 152 bytes when uniform)
+  enum { kUH, kUS, kUHL, kUAL, kUSL, kU };
+  std::atomic<uint32_t> varying{0};
+  const bool check_uniform = n > 0 && c->uniform_cols && v->height && v->ts_sec && v->txhash_len && v->addr_len &&
+                             v->sig_len;
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     uint64_t ae = 0;
-    uint32_t mh = 0;
+    uint32_t mh = 0, var = 0;
     for (uint32_t i = lo; i < hi; ++i) {
       if (v->is_nil && v->is_nil[i]) continue;
       ae = std::max<uint64_t>(ae, (uint64_t)v->txhash_off[i] + v->txhash_len[i]);
       mh = std::max(mh, v->txhash_len[i]);
+    }
+    if (check_uniform) {
+      for (uint32_t i = lo; i < hi; ++i) {
+        var |= (uint32_t)(v->height[i] != v->height[0]) << kUH | (uint32_t)(v->ts_sec[i] != v->ts_sec[0]) << kUS |
+               (uint32_t)(v->txhash_len[i] != v->txhash_len[0]) << kUHL |
+               (uint32_t)(v->addr_len[i] != v->addr_len[0]) << kUAL | (uint32_t)(v->sig_len[i] != v->sig_len[0]) << kUSL;
+      }
+      if (var) varying.fetch_or(var);
     }
     uint64_t ca = arena_end.load();
     while (ae > ca && !arena_end.compare_exchange_weak(ca, ae)) {}
     uint32_t cm = max_hl.load();
     while (mh > cm && !max_hl.compare_exchange_weak(cm, mh)) {}
   }, 16384);
+  const uint32_t uniform = check_uniform ? ~varying.load() & ((1u << kU) - 1u) : 0u;
   const uint64_t ae = arena_end.load();
   if (ae >= (1ull << 32)) { c->err = "TxHash arena >= 4 GiB"; return TXV_EINVAL; }
   const uint32_t mw = (signbytes_bound(max_hl.load(), chain_len) + 7) / 8;
@@ -668,18 +684,23 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     if (!src) return;
     cols[nc++] = Col{(const uint8_t*)src, (uint8_t*)pin, (uint8_t*)dev, elem, is_registered(c, src, (uint64_t)n * elem)};
   };
-  add(v->height, s.h_fh, s.d_fh, 8);
-  add(v->ts_sec, s.h_fs, s.d_fs, 8);
+  add((uniform >> kUH & 1) ? nullptr : v->height, s.h_fh, s.d_fh, 8);
+  add((uniform >> kUS & 1) ? nullptr : v->ts_sec, s.h_fs, s.d_fs, 8);
   add(v->ts_nanos, s.h_fn, s.d_fn, 4);
   add(v->txhash_off, s.h_fo, s.d_fo, 4);
-  add(v->txhash_len, s.h_fl, s.d_fl, 4);
+  add((uniform >> kUHL & 1) ? nullptr : v->txhash_len, s.h_fl, s.d_fl, 4);
   add(v->addr, s.h_addr, s.d_addr, 20);
-  add(v->addr_len, s.h_addr_len, s.d_addr_len, 4);
+  add((uniform >> kUAL & 1) ? nullptr : v->addr_len, s.h_addr_len, s.d_addr_len, 4);
   add(v->sig, s.h_sigraw, s.d_sigraw, 64);
-  add(v->sig_len, s.h_sig_len, s.d_sig_len, 4);
+  add((uniform >> kUSL & 1) ? nullptr : v->sig_len, s.h_sig_len, s.d_sig_len, 4);
   add(v->is_nil, s.h_nil, s.d_nil, 1);
   add(v->txkey, s.h_txkey, s.d_txkey, 32);
   if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));   // its last chain has ended
+  if (uniform >> kUH & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fh), (uint64_t)v->height[0], n, c->copy_stream));
+  if (uniform >> kUS & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fs), (uint64_t)v->ts_sec[0], n, c->copy_stream));
+  if (uniform >> kUHL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_fl), (int)v->txhash_len[0], n, c->copy_stream));
+  if (uniform >> kUAL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_addr_len), (int)v->addr_len[0], n, c->copy_stream));
+  if (uniform >> kUSL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_sig_len), (int)v->sig_len[0], n, c->copy_stream));
   for (int k = 0; k < nc; ++k)
     if (cols[k].reg && n) HIP_TRY(c, hipMemcpyAsync(cols[k].dev, cols[k].src, (size_t)n * cols[k].elem, hipMemcpyHostToDevice, c->copy_stream));
   // TxHash arena (+ 16 zero bytes: the device reads keys 8 bytes at a time)
@@ -1132,6 +1153,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     if (const char* e = getenv("TXV_HOST_THREADS")) nt = (unsigned)std::max(1, std::min(256, atoi(e)));
     c->pool.reset(new txv_host::WorkerPool(nt));
     c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
+    c->uniform_cols = !(getenv("TXV_UNIFORM_COLS") && atoi(getenv("TXV_UNIFORM_COLS")) == 0);
   }
   *out = c;
   return TXV_OK;

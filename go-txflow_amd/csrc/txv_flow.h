@@ -184,6 +184,7 @@ hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st);
 // forget every TxVoteSet (keep_ids = 0) or empty them keeping their ids (keep_ids = 1)
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);
+hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st);
 // TxHash lookups for the readers: out_id[i] = set id or TXV_NONE
 hipError_t txv_flow_lookup(const FlowState* fs, const uint8_t* keys, const uint32_t* off, const uint32_t* len,
                            uint32_t n, uint32_t* out_id, hipStream_t st);

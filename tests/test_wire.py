@@ -352,6 +352,10 @@ def test_gpu_ingest_chain_matches_oracle():
         stream = []
         for j in order:
             v = votes[j]
+            if rng.random() < 0.05:                       # a corrupted copy ahead of the vote itself
+                c = T.TxVote(Height=v.Height, TxHash=v.TxHash, TxKey=v.TxKey, Timestamp=v.Timestamp,
+                             ValidatorAddress=v.ValidatorAddress, Signature=v.Signature[:40] + bytes([v.Signature[40] ^ 1]) + v.Signature[41:])
+                stream.append(wire_of(c))
             stream.append(wire_of(v))
             r = rng.random()
             if r < 0.08:                                  # a replay of an earlier message
