@@ -173,6 +173,21 @@ struct KeyList {
     free_.push_back(i);
     --len;
   }
+  void detach(int32_t i) {                        // unlink without freeing the node
+    Node& n = nodes[i];
+    if (n.prev >= 0) nodes[n.prev].next = n.next; else head = n.next;
+    if (n.next >= 0) nodes[n.next].prev = n.prev; else tail = n.prev;
+    --len;
+  }
+  void append_linked(const std::vector<int32_t>& idx) {   // detached / fresh nodes, in order
+    for (int32_t i : idx) {
+      nodes[i].prev = tail;
+      nodes[i].next = -1;
+      if (tail >= 0) nodes[tail].next = i; else head = i;
+      tail = i;
+    }
+    len += idx.size();
+  }
   void move_to_back(int32_t i) {
     if (i == tail) return;
     Node& n = nodes[i];
@@ -209,6 +224,14 @@ struct PartIndex {
   void reserve(size_t m) { for (auto& f : p) f->reserve(m / kParts + m / (4 * kParts) + 64); }
 };
 
+// batch_check's per-call arrays, kept across calls
+struct BatchScratch {
+  std::vector<uint32_t> cnt, order, aidx;
+  std::vector<int32_t> prevb, nextb, firstb, cnode, qpos;
+  std::vector<uint8_t> dec;                 // 0 not a push (too large), 1 miss, 2 hit, 3 far
+  std::vector<int32_t> qtouched;
+};
+
 }  // namespace
 
 struct txv_pool {
@@ -224,7 +247,8 @@ struct txv_pool {
   std::vector<uint8_t> keys;                       // batch scratch
   std::vector<uint32_t> sizes;                     // batch scratch: TxVote.Size() per vote
   std::vector<int32_t> idx_c, idx_t;               // batch scratch: node indices (fast path)
-  std::vector<uint8_t> part;                       // batch scratch: index partition per key (fast path)
+  std::vector<uint8_t> part;                       // batch scratch: index partition per key (batch path)
+  BatchScratch bs;                                 // batch scratch (batch path)
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -311,90 +335,256 @@ inline uint32_t vote_size(const txv_votes* v, uint32_t i) {
 
 namespace {
 
-// slots prefetched ahead in the per-partition insert loops (DRAM-latency bound, as the sequential loop)
+// slots prefetched ahead in the per-partition loops (DRAM-latency bound, as the sequential loop)
 constexpr uint32_t kAdmitAhead = 16;
 
-// sum = the batch's summed sizes; capped = some vote is too large or hits the WAL rule; part[i] =
-// vote i's index partition (all from the sizes pass in txv_pool_check)
-bool try_batch_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint64_t sum, bool capped,
-                     const uint8_t* part, uint8_t* status_out) {
-  // the caps no vote may reach (txvotepool.go:192-261 in order: full, too large, cache, WAL)
-  if (capped) return false;
-  if ((int64_t)p->txs.len + (int64_t)n > (int64_t)p->cfg.size) return false;
-  if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;
-  if (p->cache_on && (uint64_t)p->cache.len + n > (uint64_t)p->cfg.cache_size) return false;
+// Batch CheckTxWithInfo (txvotepool.go:187-261) without the sequential loop, exact for any mix of
+// new keys, in-batch repeats, cached replays and LRU evictions.
+//
+// The cache (mapTxCache, :416-438) is an LRU of capacity C over the keys of the votes that reach
+// cache.Push -- every vote that is neither rejected as full nor too large -- whether the push hits
+// (move to back) or misses (push back, evicting the front when full).  So with S = the cache's
+// entries front to back followed by the batch's pushes, a push of key k at position e hits iff k
+// occurs earlier in S (last at p) and the number of DISTINCT keys in S(p, e) is below C: LRU's
+// stack-distance property.  That count is (e - p - 1) minus the pairs (i, next(i)) of consecutive
+// occurrences of one key nested inside (p, e), so every decision is independent of the others:
+//   - k neither cached nor earlier in the batch: miss;
+//   - L0 + pushes <= C (nothing can be evicted), or e - p - 1 < C: hit;
+//   - a cached key beyond the first min(L0, pushes) entries from the front cannot be evicted by
+//     this batch's pushes: hit;
+//   - otherwise count the nested pairs (offline sweep over a Fenwick tree; only these "far"
+//     repeats pay for it).
+// The pool's Size cap cuts the batch at the first vote that finds the pool full: every later vote
+// is ErrMempoolIsFull and pushes nothing, so the decisions before the cut stand.  When the
+// MaxTxsBytes cap could bind (it is not monotone in the batch), the sequential loop runs instead.
+// The state is then written directly: the new LRU = the C most recent distinct keys, the pool list
+// = the admitted votes appended in order (txsMap.Store overwriting, as addTx does).
+
+uint64_t batch_tab_hash(const Key& k) { uint64_t v; memcpy(&v, k.b + 16, 8); return v ^ (v >> 31); }
+
+bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, uint32_t n, uint64_t sum,
+                 const uint8_t* part, uint8_t* status_out) {
+  if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;   // the bytes cap could bind
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
-  std::chrono::steady_clock::time_point tp[6];
+  std::chrono::steady_clock::time_point tp[8];
   int ntp = 0;
   auto mark = [&] { if (prof) tp[ntp++] = std::chrono::steady_clock::now(); };
   mark();
+  const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+  const bool wal = (p->cfg.flags & TXV_POOL_WAL) != 0, cache_on = p->cache_on;
+  const uint64_t C = p->cfg.cache_size, L0 = cache_on ? p->cache.len : 0;
+  const uint32_t* sizes = p->sizes.data();
+  // pushes: the votes that reach cache.Push (the Size cap aside); position L0 + aidx[i] in S
+  S.aidx.resize(n);
+  uint32_t na = 0;
+  for (uint32_t i = 0; i < n; ++i) { S.aidx[i] = na; na += (int64_t)sizes[i] <= max_tx; }
+  const bool evict = cache_on && L0 + na > C;
   // batch order per partition
-  std::vector<uint32_t> cnt(kParts + 1, 0), order(n);
-  for (uint32_t i = 0; i < n; ++i) ++cnt[part[i] + 1];
-  for (uint32_t q = 0; q < kParts; ++q) cnt[q + 1] += cnt[q];
+  S.cnt.assign(kParts + 1, 0);
+  S.order.resize(n);
+  for (uint32_t i = 0; i < n; ++i) ++S.cnt[part[i] + 1];
+  for (uint32_t q = 0; q < kParts; ++q) S.cnt[q + 1] += S.cnt[q];
   {
-    std::vector<uint32_t> at(cnt.begin(), cnt.end() - 1);
-    for (uint32_t i = 0; i < n; ++i) order[at[part[i]]++] = i;
+    std::vector<uint32_t> at(S.cnt.begin(), S.cnt.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) S.order[at[part[i]]++] = i;
   }
   auto per_part = [&](const std::function<void(uint32_t)>& fn) {
     txv_host_parallel_for(ctx, kParts, [&](uint32_t lo, uint32_t hi) { for (uint32_t q = lo; q < hi; ++q) fn(q); }, 1);
   };
-  // node keys first (the indices compare keys through the nodes), links only once admitted
-  const size_t old_c = p->cache.nodes.size(), old_t = p->txs.nodes.size();
+  S.prevb.resize(n); S.firstb.resize(n); S.cnode.resize(n); S.nextb.assign(n, -1); S.dec.resize(n);
   mark();
-  next_indices(p->cache, n, p->idx_c);
-  next_indices(p->txs, n, p->idx_t);
-  // the last index is the highest new one whenever the free list runs out
-  if (p->cache_on) p->cache.nodes.resize(std::max<size_t>(old_c, (size_t)p->idx_c[n - 1] + 1));
-  p->txs.nodes.resize(std::max<size_t>(old_t, (size_t)p->idx_t[n - 1] + 1));
-  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) {
-      if (p->cache_on) { KeyList::Node& c = p->cache.nodes[p->idx_c[i]]; c.k = keys[i]; c.size = 0; }
-      KeyList::Node& t = p->txs.nodes[p->idx_t[i]]; t.k = keys[i]; t.size = p->sizes[i];
+  // 1. per partition, in batch order: the previous push of the same key in the batch, the first
+  //    one, and the cache node of a first push whose key is cached
+  per_part([&](uint32_t q) {
+    const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
+    uint32_t cap = 16;
+    while (cap < 2 * (hi - lo)) cap *= 2;
+    std::vector<uint32_t> tab(cap, 0);            // batch index + 1 of the key's last push
+    const FlatIndex& cf = *p->cache_map.p[q];
+    for (uint32_t j = lo; j < hi; ++j) {
+      if (cache_on && j + kAdmitAhead < hi) cf.prefetch(keys[S.order[j + kAdmitAhead]]);
+      const uint32_t i = S.order[j];
+      S.cnode[i] = -1;
+      if ((int64_t)sizes[i] > max_tx) { S.prevb[i] = -2; S.firstb[i] = (int32_t)i; continue; }
+      size_t s = batch_tab_hash(keys[i]) & (cap - 1);
+      while (tab[s] && !(keys[tab[s] - 1] == keys[i])) s = (s + 1) & (cap - 1);
+      if (tab[s]) {
+        const uint32_t pv = tab[s] - 1;
+        S.prevb[i] = (int32_t)pv;
+        S.firstb[i] = S.firstb[pv];
+        S.nextb[pv] = (int32_t)i;
+      } else {
+        S.prevb[i] = -1;
+        S.firstb[i] = (int32_t)i;
+        if (cache_on) S.cnode[i] = cf.find(keys[i]);
+      }
+      tab[s] = i + 1;
     }
   });
   mark();
-  if (p->cache_on) {
-    std::atomic<bool> clash{false};
-    per_part([&](uint32_t q) {   // mapTxCache.Push of every key: all must be new
+  // 2. front ranks: only the first min(L0, pushes) cache entries can be evicted by this batch
+  if (evict) {
+    if (S.qpos.size() < p->cache.nodes.size()) S.qpos.resize(p->cache.nodes.size(), -1);
+    const uint64_t F = std::min<uint64_t>(L0, na);
+    S.qtouched.clear();
+    int32_t e = p->cache.head;
+    for (uint64_t r = 0; r < F && e >= 0; ++r, e = p->cache.nodes[e].next) {
+      S.qpos[e] = (int32_t)r;
+      S.qtouched.push_back(e);
+    }
+  }
+  mark();
+  // 3. decisions
+  std::vector<uint32_t> far;
+  std::mutex far_mu;
+  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
+    std::vector<uint32_t> mine;
+    for (uint32_t i = lo; i < hi; ++i) {
+      uint8_t d;
+      if (S.prevb[i] == -2) d = 0;
+      else if (!cache_on) d = 1;
+      else if (S.prevb[i] >= 0) d = (!evict || S.aidx[i] - S.aidx[S.prevb[i]] - 1 < C) ? 2 : 3;
+      else if (S.cnode[i] >= 0) {
+        const int32_t r = evict ? S.qpos[S.cnode[i]] : -1;
+        d = (r < 0 || L0 + S.aidx[i] - (uint64_t)r - 1 < C) ? 2 : 3;
+      } else d = 1;
+      S.dec[i] = d;
+      if (d == 3) mine.push_back(i);
+    }
+    if (!mine.empty()) {
+      std::lock_guard<std::mutex> g(far_mu);
+      far.insert(far.end(), mine.begin(), mine.end());
+    }
+  });
+  mark();
+  if (!far.empty()) {
+    // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
+    auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
+    auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
+    std::vector<std::pair<uint64_t, uint64_t>> pairs;      // (next occurrence, occurrence)
+    for (uint32_t i = 0; i < n; ++i) {
+      if (S.prevb[i] >= 0) pairs.emplace_back(pos2(i), pos2((uint32_t)S.prevb[i]));
+      else if (S.prevb[i] == -1 && S.cnode[i] >= 0) pairs.emplace_back(pos2(i), init2(S.cnode[i]));
+    }
+    std::sort(pairs.begin(), pairs.end());
+    std::sort(far.begin(), far.end());                     // by position = batch order
+    const uint64_t M = 2 * (L0 + na) + 2;
+    std::vector<uint32_t> fen(M + 1, 0);
+    uint32_t added = 0;
+    size_t pi = 0;
+    for (uint32_t i : far) {
+      const uint64_t e = pos2(i);
+      for (; pi < pairs.size() && pairs[pi].first < e; ++pi, ++added)
+        for (uint64_t x = pairs[pi].second + 1; x <= M; x += x & (~x + 1)) ++fen[x];
+      const uint64_t p2 = S.prevb[i] >= 0 ? pos2((uint32_t)S.prevb[i]) : init2(S.cnode[i]);
+      uint32_t upto = 0;                                   // pairs starting at or before p
+      for (uint64_t x = p2 + 1; x > 0; x -= x & (~x + 1)) upto += fen[x];
+      const uint64_t nested = added - upto;
+      const uint64_t window = (e - p2) / 2 - 1;           // pushes strictly between (p is exact here)
+      S.dec[i] = window - nested < C ? 2 : 1;
+    }
+  }
+  if (evict)
+    for (int32_t e : S.qtouched) S.qpos[e] = -1;
+  mark();
+  // 4. statuses in arrival order, the Size cap's cut
+  uint32_t m = n;
+  uint64_t admitted = 0, admitted_bytes = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if ((int64_t)p->txs.len + (int64_t)admitted >= (int64_t)p->cfg.size) { m = i; break; }
+    const uint8_t d = S.dec[i];
+    if (d == 0) status_out[i] = TXV_POOL_ERR_TOO_LARGE;
+    else if (d == 2) status_out[i] = TXV_POOL_ERR_IN_CACHE;
+    else if (!sizes[i] && wal) status_out[i] = TXV_POOL_ERR_ENCODING;
+    else { status_out[i] = TXV_POOL_OK; ++admitted; admitted_bytes += sizes[i]; }
+  }
+  if (m < n) memset(status_out + m, TXV_POOL_ERR_FULL, n - m);
+  // 5. the cache: the C most recent distinct keys of S up to the cut, in recency order
+  if (cache_on) {
+    std::vector<uint32_t> last;                            // pushes that are their key's last before m
+    for (uint32_t i = 0; i < m; ++i)
+      if (S.dec[i] && (S.nextb[i] < 0 || (uint32_t)S.nextb[i] >= m)) last.push_back(i);
+    const size_t U = last.size(), keepU = std::min<uint64_t>(U, C);
+    // cached keys pushed again leave their place (their node moves, or goes when too old)
+    for (uint32_t i = 0; i < m; ++i)
+      if (S.prevb[i] == -1 && S.cnode[i] >= 0) p->cache.detach(S.cnode[i]);
+    while (p->cache.len > C - keepU) {                     // evictions from the front
+      const int32_t h = p->cache.head;
+      p->cache_map.erase(p->cache.nodes[h].k);
+      p->cache.unlink(h);
+    }
+    std::vector<int32_t> fin(keepU);
+    uint32_t n_new = 0;
+    for (size_t u = 0; u < U; ++u) {
+      const uint32_t i = last[u];
+      const int32_t cn = S.cnode[S.firstb[i]];
+      if (u < U - keepU) {                                 // pushed, then evicted inside the batch
+        if (cn >= 0) { p->cache_map.erase(keys[i]); p->cache.free_.push_back(cn); }
+      } else {
+        fin[u - (U - keepU)] = cn;
+        n_new += cn < 0;
+      }
+    }
+    next_indices(p->cache, n_new, p->idx_c);
+    if (n_new) {
+      const size_t old = p->cache.nodes.size();
+      p->cache.nodes.resize(std::max<size_t>(old, (size_t)p->idx_c[n_new - 1] + 1));
+      const size_t nf = p->cache.free_.size();
+      p->cache.free_.resize(nf - std::min<size_t>(nf, n_new));
+    }
+    for (size_t u = 0, k = 0; u < keepU; ++u)
+      if (fin[u] < 0) {
+        fin[u] = p->idx_c[k++];
+        p->cache.nodes[fin[u]] = KeyList::Node{keys[last[U - keepU + u]], 0, -1, -1};
+      }
+    std::vector<std::vector<std::pair<uint32_t, int32_t>>> ins(kParts);
+    for (size_t u = 0; u < keepU; ++u) {
+      const uint32_t i = last[U - keepU + u];
+      if (S.cnode[S.firstb[i]] < 0) ins[part[i]].emplace_back(i, fin[u]);
+    }
+    per_part([&](uint32_t q) {                             // index the new nodes
       FlatIndex& f = *p->cache_map.p[q];
-      for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
-        if (j + kAdmitAhead < cnt[q + 1]) f.prefetch(keys[order[j + kAdmitAhead]]);
-        const uint32_t i = order[j];
-        if (f.find_or_insert(keys[i], [&] { return p->idx_c[i]; }) >= 0) { clash = true; return; }
+      const auto& L = ins[q];
+      for (size_t j = 0; j < L.size(); ++j) {
+        if (j + kAdmitAhead < L.size()) f.prefetch(keys[L[j + kAdmitAhead].first]);
+        f.put(keys[L[j].first], L[j].second);
       }
     });
-    if (clash) {   // undo: erase the keys this batch inserted, drop the new nodes
-      per_part([&](uint32_t q) {
-        FlatIndex& f = *p->cache_map.p[q];
-        for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
-          const uint32_t i = order[j];
-          if (f.find(keys[i]) == p->idx_c[i]) f.erase(keys[i]);
-        }
-      });
-      p->cache.nodes.resize(old_c);
-      p->txs.nodes.resize(old_t);
-      return false;
-    }
-    mark();
-    link_appended(ctx, p->cache, p->idx_c, n);
+    p->cache.append_linked(fin);
   }
-  per_part([&](uint32_t q) {     // addTx: txsMap.Store of every key
-    FlatIndex& f = *p->txs_map.p[q];
-    for (uint32_t j = cnt[q]; j < cnt[q + 1]; ++j) {
-      if (j + kAdmitAhead < cnt[q + 1]) f.prefetch(keys[order[j + kAdmitAhead]]);
-      const uint32_t i = order[j];
-      f.put(keys[i], p->idx_t[i]);
-    }
-  });
-  link_appended(ctx, p->txs, p->idx_t, n);
   mark();
-  if (prof && ntp == 5) {
-    auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    fprintf(stderr, "[txv pool] admit: order=%.3f nodes=%.3f cache=%.3f txs+links=%.3f ms\n", ms(0), ms(1), ms(2), ms(3));
+  // 6. addTx for the admitted votes in arrival order (txsMap.Store overwrites)
+  if (admitted) {
+    std::vector<uint32_t> adm;
+    adm.reserve(admitted);
+    for (uint32_t i = 0; i < m; ++i)
+      if (status_out[i] == TXV_POOL_OK) adm.push_back(i);
+    const uint32_t A = (uint32_t)adm.size();
+    next_indices(p->txs, A, p->idx_t);
+    p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
+    txv_host_parallel_for(ctx, A, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t a = lo; a < hi; ++a) p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[adm[a]], sizes[adm[a]], -1, -1};
+    });
+    std::vector<int32_t> slot_of(n, -1);
+    for (uint32_t a = 0; a < A; ++a) slot_of[adm[a]] = p->idx_t[a];
+    per_part([&](uint32_t q) {
+      FlatIndex& f = *p->txs_map.p[q];
+      const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
+      for (uint32_t j = lo; j < hi; ++j) {
+        if (j + kAdmitAhead < hi) f.prefetch(keys[S.order[j + kAdmitAhead]]);
+        const uint32_t i = S.order[j];
+        if (slot_of[i] >= 0) f.put(keys[i], slot_of[i]);
+      }
+    });
+    link_appended(ctx, p->txs, p->idx_t, A);
+    p->txs_bytes += (int64_t)admitted_bytes;
   }
-  p->txs_bytes += (int64_t)sum;
-  memset(status_out, TXV_POOL_OK, n);
+  mark();
+  if (prof) {
+    auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
+    fprintf(stderr, "[txv pool] batch: order=%.3f scan=%.3f front=%.3f decide=%.3f far(%zu)=%.3f cache=%.3f txs=%.3f ms\n",
+            ms(0), ms(1), ms(2), ms(3), far.size(), ms(4), ms(5), ms(6));
+  }
   return true;
 }
 
@@ -432,35 +622,24 @@ namespace {
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
   const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
-  // for the fast path: the summed sizes, the too-large / WAL caps, each key's partition
+  // for the batch path: the summed sizes and each key's index partition
   const bool fast = n >= 4096;
   std::atomic<uint64_t> sum_a{0};
-  std::atomic<bool> capped{false};
   if (fast) {
     p->part.resize(n);
     txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
       uint64_t sm = 0;
-      bool cp = false;
       for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t sz = p->sizes[i];
-        cp |= (int64_t)sz > max_tx || (!sz && (p->cfg.flags & TXV_POOL_WAL));
-        sm += sz;
+        sm += p->sizes[i];
         p->part[i] = (uint8_t)PartIndex::part(keys[i]);
       }
       sum_a += sm;
-      if (cp) capped = true;
     });
   }
-  // Fast path: when no vote of the batch can hit a size cap, a cache eviction or the WAL rule,
-  // the sequential loop would admit every vote whose key is new -- so if every key is new (in
-  // the cache and within the batch) the result is "all admitted, in order".  The keys go into
-  // the partitioned cache and pool indices on the context's host workers (one worker per
-  // partition, batch order within it); a key found present undoes the batch's inserts and the
-  // sequential loop below decides instead.
-  if (fast && try_batch_admit(p, ctx, keys, n, sum_a.load(), capped.load(), p->part.data(), status_out)) {
+  if (fast && batch_check(p, ctx, p->bs, keys, n, sum_a.load(), p->part.data(), status_out)) {
     if (getenv("TXV_PROFILE_HOST")) {
       const auto t2 = std::chrono::steady_clock::now();
-      fprintf(stderr, "[txv pool] batch-admit=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t2 - t1).count(), n);
+      fprintf(stderr, "[txv pool] batch-check=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t2 - t1).count(), n);
     }
     return TXV_OK;
   }
@@ -504,17 +683,18 @@ uint32_t txv_pool_max_msg_bytes(txv_pool* p) {
   return p->cfg.max_msg_bytes;
 }
 
-// CheckTxWithInfo for n votes whose keys (n x 32 bytes) and Size() values were computed on the
-// device from decoded wire records (runtime.cpp txv_ingest_msgs)
+extern "C" {
+
+// CheckTxWithInfo for n votes whose keys (n x 32 bytes) and Size() values are known (computed on
+// the device from decoded wire records by txv_ingest_msgs, or by the caller); ctx may be NULL
+// (the batch passes then run on the calling thread)
 int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
                         uint8_t* status_out) {
-  if (!p || !ctx || (n && (!keys32 || !sizes || !status_out))) return TXV_EINVAL;
+  if (!p || (n && (!keys32 || !sizes || !status_out))) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   p->sizes.assign(sizes, sizes + n);
   return pool_admit(p, ctx, reinterpret_cast<const Key*>(keys32), n, status_out);
 }
-
-extern "C" {
 
 int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
                    const uint64_t* sig_full_off, uint8_t* status_out) {

@@ -2244,8 +2244,6 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
 
 }  // extern "C"
 
-int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
-                        uint8_t* status_out);   // pool.cpp
 uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
 
 namespace {

@@ -132,6 +132,7 @@ def lib():
             "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
             "txv_pool_free": ([vp], None),
             "txv_pool_check": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
+            "txv_pool_check_keys": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_pool_update": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
             "txv_pool_reap": ([vp, i64, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_pool_flush": ([vp], ctypes.c_int),
@@ -178,7 +179,7 @@ EXPORTED_SYMBOLS = [
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
-    "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
+    "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
@@ -789,7 +790,7 @@ class TxVotePool:
     Update (:329-359), ReapMaxTxs (:310-324), Flush (:146-159), Size (:136), TxsBytes (:141).
     cache_size POOL_NO_CACHE selects nopTxCache; 0 fields take tendermint's defaults."""
 
-    def __init__(self, ctx: Context, size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
+    def __init__(self, ctx: Optional[Context], size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
                  max_msg_bytes: int = 0, height: int = 0, wal: bool = False):
         self.ctx = ctx
         cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes, POOL_WAL if wal else 0)
@@ -814,6 +815,19 @@ class TxVotePool:
         self.ctx._chk(lib().txv_pool_check(self._h, self.ctx._h, ctypes.byref(vs), full, off, out.ctypes.data),
                       "txv_pool_check")
         return out[:batch.n]
+
+    def check_keys(self, keys: np.ndarray, sizes: np.ndarray) -> np.ndarray:
+        """CheckTxWithInfo over (txVoteKey [n, 32] u8, TxVote.Size() [n] u32) pairs in arrival order
+        (txv_pool_check_keys); needs no GPU when the pool was made with ctx=None"""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        sizes = np.ascontiguousarray(sizes, np.uint32)
+        n = len(sizes)
+        out = np.zeros(max(n, 1), np.uint8)
+        rc = lib().txv_pool_check_keys(self._h, self.ctx._h if self.ctx is not None else None, keys.ctypes.data,
+                                       sizes.ctypes.data, n, out.ctypes.data)
+        if rc != 0:
+            raise TxvInfraError(f"txv_pool_check_keys failed ({rc})")
+        return out[:n]
 
     def receive(self, wb: WireBatch):
         """Reactor.Receive (txvotepool/reactor.go:170-190) for a batch of messages in arrival order:

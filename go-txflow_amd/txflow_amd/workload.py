@@ -102,9 +102,16 @@ class Workload:
 class StreamWorkload:
     """C5: `n_vals` validators with power 1 + (rand mod 10^6), every validator
     votes every tx, arrival order = tx index + U(0, window) so a tx's votes straddle a few
-    consecutive `batch`-vote batches; the stream is cut into batches in arrival order."""
+    consecutive `batch`-vote batches; the stream is cut into batches in arrival order.
 
-    def __init__(self, ctx: Context, n_vals: int, n_txs: int, seed: int, batch: int = 65536, window: int = 128):
+    replay > 0 adds SURVEY.md Appendix C's exact replays (gossip re-deliveries): after each vote,
+    with probability `replay`, a byte-identical copy of an earlier vote -- half of them from the
+    last `near` votes, half from anywhere before -- so a replay meets TxVotePool's LRU while its
+    key is still cached (ErrTxInCache) or after it was evicted (admitted again; TxFlow then says
+    DUPLICATE).  n = stream length, n_unique = distinct votes."""
+
+    def __init__(self, ctx: Context, n_vals: int, n_txs: int, seed: int, batch: int = 65536, window: int = 128,
+                 replay: float = 0.0, near: int = 4096):
         self.rng = np.random.default_rng(seed)
         self.n_vals, self.n_txs, self.batch_size = n_vals, n_txs, batch
         self.seeds = validator_seeds(n_vals)
@@ -116,25 +123,51 @@ class StreamWorkload:
         self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(n_vals, 20)
         self.hashes = tx_hashes(n_txs, self.rng, 1 << 40)
         self.txkeys = tx_keys(self.hashes)
-        n = n_txs * n_vals
+        nu = n_txs * n_vals
         tx_of = np.repeat(np.arange(n_txs, dtype=np.int64), n_vals)
         val_of = np.tile(np.arange(n_vals, dtype=np.int64), n_txs)
-        order = np.argsort(tx_of + self.rng.random(n) * window, kind="stable")
-        self.tx_of, self.val_of = tx_of[order], val_of[order]
-        self.n = n
-        sig = np.zeros((n, 64), np.uint8)
-        self.batches = []
-        for s in range(0, n, batch):
-            e = min(n, s + batch)
+        order = np.argsort(tx_of + self.rng.random(nu) * window, kind="stable")
+        utx, uval = tx_of[order], val_of[order]
+        unanos = np.arange(nu, dtype=np.int64) % 999_999_999 + 1
+        # the distinct votes, signed in chunks (arrival order)
+        usig = np.zeros((nu, 64), np.uint8)
+        for s in range(0, nu, batch):
+            e = min(nu, s + batch)
             m = e - s
             b = VoteBatch(m, height=np.ones(m, np.int64), txhash_arena=self.hashes.reshape(-1),
-                          txhash_off=(self.tx_of[s:e] * 64).astype(np.uint32), txhash_len=np.full(m, 64, np.uint32),
-                          ts_sec=np.full(m, 1_700_000_000, np.int64),
-                          ts_nanos=(np.arange(s, e, dtype=np.int64) % 999_999_999 + 1),
-                          addr=self.addrs[self.val_of[s:e]], addr_len=np.full(m, 20, np.uint32),
-                          sig=sig[s:e], sig_len=np.full(m, 64, np.uint32), txkey=self.txkeys[self.tx_of[s:e]])
-            b.sig = ctx.sign_votes(b, self.val_of[s:e].astype(np.uint32), CHAIN_ID).reshape(-1)
+                          txhash_off=(utx[s:e] * 64).astype(np.uint32), txhash_len=np.full(m, 64, np.uint32),
+                          ts_sec=np.full(m, 1_700_000_000, np.int64), ts_nanos=unanos[s:e],
+                          addr=self.addrs[uval[s:e]], addr_len=np.full(m, 20, np.uint32),
+                          sig=usig[s:e], sig_len=np.full(m, 64, np.uint32))
+            usig[s:e] = ctx.sign_votes(b, uval[s:e].astype(np.uint32), CHAIN_ID).reshape(m, 64)
+        # the stream: stream slot -> distinct vote
+        if replay > 0:
+            flag = self.rng.random(nu) < replay
+            i = np.arange(nu, dtype=np.int64)
+            near_src = np.maximum(0, i - self.rng.integers(0, near, nu))
+            far_src = (self.rng.random(nu) * (i + 1)).astype(np.int64)
+            rsrc = np.where(self.rng.random(nu) < 0.5, near_src, far_src)
+            at = i + np.cumsum(flag) - flag               # stream slot of distinct vote i
+            src = np.empty(nu + int(flag.sum()), np.int64)
+            src[at] = i
+            src[at[flag] + 1] = rsrc[flag]
+        else:
+            src = np.arange(nu, dtype=np.int64)
+        self.src = src
+        self.tx_of, self.val_of = utx[src], uval[src]
+        self.n, self.n_unique = len(src), nu
+        self.batches = []
+        for s in range(0, self.n, batch):
+            e = min(self.n, s + batch)
+            m = e - s
+            q = src[s:e]
+            b = VoteBatch(m, height=np.ones(m, np.int64), txhash_arena=self.hashes.reshape(-1),
+                          txhash_off=(utx[q] * 64).astype(np.uint32), txhash_len=np.full(m, 64, np.uint32),
+                          ts_sec=np.full(m, 1_700_000_000, np.int64), ts_nanos=unanos[q],
+                          addr=self.addrs[uval[q]], addr_len=np.full(m, 20, np.uint32),
+                          sig=usig[q], sig_len=np.full(m, 64, np.uint32), txkey=self.txkeys[utx[q]])
             self.batches.append(b)
+        n = self.n
         first = np.full(n_txs, -1, np.int64)
         bidx = np.arange(n) // batch
         # batch index of each tx's first vote

@@ -367,6 +367,12 @@ void txv_pool_free(txv_pool* pool);
 /* CheckTxWithInfo for each vote in arrival order (keys on ctx's GPU); status_out[i] = TXV_POOL_*. */
 int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
                    const uint64_t* sig_full_off, uint8_t* status_out);
+/* CheckTxWithInfo for n votes given as (txVoteKey, TxVote.Size()) pairs in arrival order: keys32
+ * n x 32 bytes (SHA-256(Signature), txvotepool.go:467-469), sizes[i] = Size() (0 when amino
+ * rejects the timestamp); status_out[i] = TXV_POOL_*.  ctx (optional) lends its host workers;
+ * NULL runs every pass on the calling thread.  txvotepool.go:187-261 */
+int txv_pool_check_keys(txv_pool* pool, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
+                        uint8_t* status_out);
 /* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
  * leaves the pool if its key is there. */
 int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,

@@ -134,6 +134,8 @@ orc_pool* orc_pool_new(uint32_t size, uint32_t cache_size, uint64_t max_txs_byte
                        int64_t height, int wal);
 void orc_pool_free(orc_pool*);
 int orc_pool_check(orc_pool*, const orc_vote* v);
+/* the same check for n votes given as (txVoteKey 32 B, TxVote.Size()) pairs */
+void orc_pool_check_keys(orc_pool*, const uint8_t* keys32, const uint32_t* sizes, uint32_t n, uint8_t* out);
 void orc_pool_check_soa(orc_pool*, const orc_soa* b, const uint8_t* sig_full, const uint64_t* sig_full_off,
                         uint8_t* out);
 void orc_pool_update(orc_pool*, int64_t height, const orc_vote* votes, uint32_t n);

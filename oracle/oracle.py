@@ -58,6 +58,7 @@ def lib():
                                    ctypes.c_int]
         L.orc_pool_free.argtypes = [ctypes.c_void_p]
         L.orc_pool_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_pool_check_keys.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         L.orc_pool_check_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]
         L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
@@ -344,6 +345,16 @@ class Pool:
         lib().orc_pool_check_soa(self._h, ctypes.addressof(soa), full, None if off is None else off.ctypes.data,
                                  out.ctypes.data)
         return out[:b.n]
+
+    def check_keys(self, keys, sizes):
+        """orc_pool_check over (txVoteKey, Size()) pairs: keys [n, 32] u8, sizes [n] u32"""
+        import numpy as np
+        keys = np.ascontiguousarray(keys, np.uint8)
+        sizes = np.ascontiguousarray(sizes, np.uint32)
+        n = len(sizes)
+        out = np.zeros(max(n, 1), np.uint8)
+        lib().orc_pool_check_keys(self._h, keys.ctypes.data, sizes.ctypes.data, n, out.ctypes.data)
+        return out[:n]
 
     def update(self, height, votes):
         keep = []

@@ -115,20 +115,30 @@ static int cache_push(orc_pool* p, const uint8_t* k) {
 
 static void vote_key(const orc_vote* v, uint8_t key[32]) { orc_sha256(v->sig, v->sig_len, key); }
 
-int orc_pool_check(orc_pool* p, const orc_vote* v) {
-  /* TxVote.Size() returns 0 when amino rejects the timestamp (types/tx_vote.go:144-150): such a
-   * vote passes the caps with size 0, is cached and admitted; only the WAL write
-   * (MustMarshalBinaryBare, :231-242, after the cache push) panics, when a WAL is configured */
-  const int sz = orc_txvote_size(v->height, v->txhash_len, v->ts_sec, v->ts_nanos, v->addr_len, v->sig_len);
+/* CheckTxWithInfo (txvotepool.go:187-261) for a vote whose txVoteKey k and Size() sz are known */
+static int pool_check_key(orc_pool* p, const uint8_t* k, int sz) {
   if ((int64_t)p->txs.len >= (int64_t)p->size || (int64_t)sz + p->txs_bytes > (int64_t)p->max_txs_bytes) return 1;
   if ((int64_t)sz > (int64_t)p->max_msg_bytes - 8) return 2;
-  uint8_t k[32];
-  vote_key(v, k);
   if (!cache_push(p, k)) return 3;
   if (sz == 0 && p->wal) return 4;                        /* WAL MustMarshalBinaryBare panics */
   pl_push_back(&p->txs, k, (uint32_t)sz);
   p->txs_bytes += sz;
   return 0;
+}
+
+int orc_pool_check(orc_pool* p, const orc_vote* v) {
+  /* TxVote.Size() returns 0 when amino rejects the timestamp (types/tx_vote.go:144-150): such a
+   * vote passes the caps with size 0, is cached and admitted; only the WAL write
+   * (MustMarshalBinaryBare, :231-242, after the cache push) panics, when a WAL is configured */
+  const int sz = orc_txvote_size(v->height, v->txhash_len, v->ts_sec, v->ts_nanos, v->addr_len, v->sig_len);
+  uint8_t k[32];
+  vote_key(v, k);
+  return pool_check_key(p, k, sz);
+}
+
+/* orc_pool_check over n votes given as (txVoteKey, Size()) pairs, in arrival order */
+void orc_pool_check_keys(orc_pool* p, const uint8_t* keys32, const uint32_t* sizes, uint32_t n, uint8_t* out) {
+  for (uint32_t i = 0; i < n; ++i) out[i] = (uint8_t)pool_check_key(p, keys32 + (size_t)i * 32, (int)sizes[i]);
 }
 
 /* orc_pool_check over an SoA batch in arrival order (the gate's pool stage).  Signatures longer

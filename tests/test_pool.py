@@ -211,10 +211,9 @@ def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
 
 @pytest.mark.gpu
 def test_pool_batch_admit_matches_oracle(oracle_lib):
-    """Batches of >= 4096 votes take txv_pool_check's batch-admit path (every key new, no cap
-    reachable: keys inserted into the partitioned indices on the host workers); a key already
-    cached, a key repeated inside the batch, or a batch that would evict from the cache falls
-    back to the sequential loop after undoing the inserts.  Every outcome, Size, TxsBytes,
+    """Batches of >= 4096 votes take txv_pool_check's batch path (pool.cpp batch_check: LRU
+    decisions by stack distance, state written once): all-new keys, a key already cached, a key
+    repeated inside the batch, a batch that evicts from the cache.  Every outcome, Size, TxsBytes,
     ReapMaxTxs order and the LRU order equal the oracle's, including node reuse after Update."""
     import txflow_amd as T
     rnd = random.Random(77)
@@ -264,10 +263,10 @@ def test_pool_batch_admit_matches_oracle(oracle_lib):
 
 @pytest.mark.gpu
 def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
-    """The batch-admit path without a cache (a key repeated inside the batch is admitted twice,
-    txsMap.Store keeping the later node), and batches the size / byte caps cut off (sequential
-    loop: ErrMempoolIsFull from the cap on): outcomes, Size, TxsBytes and ReapMaxTxs equal the
-    oracle's."""
+    """The batch path without a cache (a key repeated inside the batch is admitted twice,
+    txsMap.Store keeping the later node), a batch the Size cap cuts (ErrMempoolIsFull from the
+    cut on) and one the byte cap could cut (sequential loop): outcomes, Size, TxsBytes and
+    ReapMaxTxs equal the oracle's."""
     import txflow_amd as T
     rnd = random.Random(78)
     ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
@@ -295,3 +294,41 @@ def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
         finally:
             pool.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_pool_replay_stream_bounded_cache(oracle_lib):
+    """Appendix C's exact replays (near: within the last 4096 votes; far: any earlier vote) in
+    32k-vote batches through txv_pool_check with tendermint's default CacheSize (10000): replays
+    still cached -> ErrTxInCache, replays of evicted keys admitted again (second pool element);
+    every outcome, the LRU order and the pool order equal the oracle's after each batch."""
+    import txflow_amd as T
+    rnd = random.Random(79)
+    ctx = T.Context(max_batch=1 << 16, max_txs=1024, max_validators=8)
+    pool = T.TxVotePool(ctx, size=1 << 20, cache_size=0)
+    ref = oracle_lib.Pool(size=1 << 20, cache_size=10000)
+    hist = []
+    try:
+        for b in range(4):
+            votes = []
+            for i in range(32768):
+                if hist and rnd.random() < 0.05:
+                    j = rnd.randrange(len(hist)) if rnd.random() < 0.5 else max(0, len(hist) - 1 - rnd.randrange(4096))
+                    votes.append(dict(hist[j]))
+                else:
+                    votes.append(vote(rnd.randbytes(64), ts=(1_700_000_000, 1 + len(hist))))
+                hist.append(votes[-1])
+            bt, long_sigs = _batch(T, votes)
+            st = pool.check_batch(bt, long_sigs)
+            exp = ref.check(votes)
+            assert np.array_equal(st, exp), (b, np.nonzero(st != exp)[0][:10])
+            assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+            assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+            gk, gs = pool.reap(-1)
+            ok, os_ = ref.reap(-1)
+            assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+            if b:
+                assert (st == IN_CACHE).any() and (st == OK).sum() > 30000
+    finally:
+        pool.close()
+        ctx.close()

@@ -1,0 +1,111 @@
+"""TxVotePool.CheckTx batch path (pool.cpp batch_check) vs the sequential oracle pool, on the host:
+txv_pool_check_keys with precomputed (txVoteKey, Size()) pairs and no GPU context.
+
+Reference: txvotepool/txvotepool.go:187-261 (CheckTxWithInfo: full -> too large -> cache.Push ->
+WAL -> addTx), :416-438 (mapTxCache.Push: hit moves to back, miss evicts the front when full),
+:265-270 (addTx: txsMap.Store overwrites).  The streams mix new keys, near and far in-batch
+repeats, replays of earlier batches (cached or already evicted), too-large votes, Size()==0 votes
+with and without a WAL, and pools that fill up mid-batch; after every batch the per-vote statuses,
+the LRU order (cache_keys), the pool order (reap), Size and TxsBytes must equal the oracle's."""
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+import txflow_amd as T
+
+
+def _stream(rng, n_batches, batch, replay=0.05, far_frac=0.5, big_frac=0.0, zero_frac=0.0, max_msg=1 << 20):
+    """batches of (keys [n,32], sizes [n]): fresh keys, replays of any earlier key (near: within the
+    last 64 votes; far: anywhere before)"""
+    hist = []
+    out = []
+    for _ in range(n_batches):
+        keys = rng.integers(0, 256, size=(batch, 32), dtype=np.uint8)
+        sizes = rng.integers(100, 200, size=batch).astype(np.uint32)
+        for i in range(batch):
+            if (hist or i) and rng.random() < replay:
+                total = len(hist) + i
+                if rng.random() < far_frac:
+                    j = int(rng.integers(0, total))
+                else:
+                    j = max(0, total - 1 - int(rng.integers(0, 64)))
+                keys[i] = hist[j] if j < len(hist) else keys[j - len(hist)]
+            if rng.random() < big_frac:
+                sizes[i] = max_msg  # > MaxMsgBytes - 8: ErrTxTooLarge
+            elif rng.random() < zero_frac:
+                sizes[i] = 0
+        hist.extend(list(keys))
+        out.append((keys, sizes))
+    return out
+
+
+def _check_equal(pool, opool, st, ost, where):
+    assert np.array_equal(st, ost), f"{where}: {int(np.count_nonzero(st != ost))} status mismatches, first at " \
+                                    f"{int(np.flatnonzero(st != ost)[0])}: {st[st != ost][:5]} vs {ost[st != ost][:5]}"
+    assert pool.Size() == opool.size(), where
+    assert pool.TxsBytes() == opool.txs_bytes(), where
+    ck, ock = pool.cache_keys(), opool.cache_keys()
+    assert ck.shape == ock.shape and np.array_equal(ck, ock), f"{where}: LRU order differs"
+    rk, rs = pool.reap(-1)
+    ork, ors = opool.reap(-1)
+    assert np.array_equal(rk, ork) and np.array_equal(rs, ors), f"{where}: pool order differs"
+
+
+CASES = [
+    # name, cache_size, pool size, max_txs_bytes, wal, replay, far, big, zero, batches, batch
+    ("unbounded_no_repeats", 1 << 20, 1 << 20, 1 << 40, False, 0.0, 0.5, 0.0, 0.0, 3, 8192),
+    ("unbounded_replays", 1 << 20, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 3, 8192),
+    ("cache10k_replays", 10000, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 4, 8192),
+    ("cache10k_near_only", 10000, 1 << 20, 1 << 40, False, 0.10, 0.0, 0.0, 0.0, 3, 8192),
+    ("cache1000_heavy", 1000, 1 << 20, 1 << 40, False, 0.30, 0.7, 0.0, 0.0, 3, 6000),
+    ("cache7", 7, 1 << 20, 1 << 40, False, 0.30, 0.0, 0.0, 0.0, 2, 5000),
+    ("cache1", 1, 1 << 20, 1 << 40, False, 0.30, 0.0, 0.0, 0.0, 2, 5000),
+    ("pool_fills_mid_batch", 10000, 11000, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 3, 8192),
+    ("too_large_and_wal", 5000, 1 << 20, 1 << 40, True, 0.05, 0.5, 0.02, 0.02, 3, 8192),
+    ("size0_no_wal", 5000, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.01, 0.02, 3, 8192),
+    ("bytes_cap_binds", 10000, 1 << 20, 3_000_000, False, 0.05, 0.5, 0.0, 0.0, 3, 8192),
+    ("no_cache", T.POOL_NO_CACHE, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.01, 0.0, 3, 8192),
+    ("small_batches", 3000, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 6, 1500),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_pool_batch_matches_oracle(case):
+    name, cache, size, max_bytes, wal, replay, far, big, zero, nb, batch = case
+    O.build()
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    pool = T.TxVotePool(None, size=size, cache_size=cache, max_txs_bytes=max_bytes, wal=wal)
+    opool = O.Pool(size=size, cache_size=cache, max_txs_bytes=max_bytes, wal=wal)
+    try:
+        for b, (keys, sizes) in enumerate(_stream(rng, nb, batch, replay, far, big, zero)):
+            st = pool.check_keys(keys, sizes)
+            ost = opool.check_keys(keys, sizes)
+            _check_equal(pool, opool, st, ost, f"{name} batch {b}")
+    finally:
+        pool.close()
+
+
+def test_pool_batch_replays_of_evicted_keys():
+    """a key evicted from a 4096-entry cache by later pushes is admitted again (a second pool
+    element, txsMap pointing at the newer one), one still cached is ErrTxInCache"""
+    O.build()
+    rng = np.random.default_rng(7)
+    base = rng.integers(0, 256, size=(20000, 32), dtype=np.uint8)
+    pool = T.TxVotePool(None, size=1 << 20, cache_size=4096, max_txs_bytes=1 << 40)
+    opool = O.Pool(size=1 << 20, cache_size=4096, max_txs_bytes=1 << 40)
+    try:
+        sizes = np.full(10000, 150, np.uint32)
+        st = pool.check_keys(base[:10000], sizes)
+        _check_equal(pool, opool, st, opool.check_keys(base[:10000], sizes), "first")
+        # replay every 3rd key of the first batch (the older ones were evicted), interleaved with new ones
+        keys = np.concatenate([base[:10000:3], base[10000:16000]])
+        keys = keys[rng.permutation(len(keys))]
+        sizes = np.full(len(keys), 150, np.uint32)
+        st = pool.check_keys(keys, sizes)
+        ost = opool.check_keys(keys, sizes)
+        _check_equal(pool, opool, st, ost, "replays")
+        assert (st == T.POOL_ERR_IN_CACHE).any() and (st == T.POOL_OK).sum() > 6000
+    finally:
+        pool.close()
