@@ -875,6 +875,20 @@ hipError_t compact(Pred p, Act act, uint32_t n, uint32_t* blk, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Experiment builds only (tools/profile/build_variant_flow.sh -DTXV_EXP_SKIP): TXV_EXP_SKIP=<mask>
+// leaves flow kernels out of every chain (wrong results; for attributing co-running costs):
+// 1 tally_min, 2 resolve, 4 ADDED compaction, 8 touched compaction, 16 cross, 32 events + status,
+// 64 route_key, 128 new-id compaction
+#ifdef TXV_EXP_SKIP
+uint32_t exp_skip() {
+  static const uint32_t m = getenv("TXV_EXP_SKIP") ? (uint32_t)strtoul(getenv("TXV_EXP_SKIP"), nullptr, 0) : 0u;
+  return m;
+}
+#define TXV_SKIP(bit) (exp_skip() & (bit))
+#else
+#define TXV_SKIP(bit) false
+#endif
+
 }  // namespace
 
 extern "C" {
@@ -889,11 +903,12 @@ hipError_t txv_flow_prep(const FlowState* fs, const FlowBatch* b, hipStream_t st
 hipError_t txv_flow_route(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
   if (((uint64_t)b->n + kScanItems - 1) / kScanItems > 8192) return hipErrorInvalidValue;
   const uint32_t g = (b->n + 255) / 256;
-  if (g) hipLaunchKernelGGL(txv_k_route_key, dim3(g), dim3(256), 0, st, *fs, *b);
+  if (g && !TXV_SKIP(64)) hipLaunchKernelGGL(txv_k_route_key, dim3(g), dim3(256), 0, st, *fs, *b);
   return hipGetLastError();
 }
 
 hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t st) {
+  if (TXV_SKIP(128)) return hipSuccess;
   return compact(NewSetPred{*fs, *b}, NewSetAct{*fs, *b}, b->n, b->blk, st);
 }
 
@@ -902,17 +917,18 @@ hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st) {
   const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
-  hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
-  if (g) hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *fs, *b);
-  hipError_t e = compact(AddedPred{*b}, AddedAct{*fs, *b}, b->n, b->blk, st);
+  if (!TXV_SKIP(1)) hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
+  if (g && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *fs, *b);
+  hipError_t e = TXV_SKIP(4) ? hipSuccess : compact(AddedPred{*b}, AddedAct{*fs, *b}, b->n, b->blk, st);
   if (e != hipSuccess) return e;
   sets_bound = std::min(sets_bound, fs->max_txs);
   const uint32_t nb_sets = (sets_bound + kScanItems - 1) / kScanItems;
-  e = compact(TouchedPred{*fs, *b}, TouchedAct{*fs}, sets_bound, fs->touched_blk, st);
+  e = TXV_SKIP(8) ? hipSuccess : compact(TouchedPred{*fs, *b}, TouchedAct{*fs}, sets_bound, fs->touched_blk, st);
   if (e != hipSuccess) return e;
   // persistent waves over the touched list: one wave per set (up to 8 waves per SIMD)
   const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::min(sets_bound, b->n) + 3) / 4, 2048));
-  hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, nb, nb_sets);
+  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, nb, nb_sets);
+  if (TXV_SKIP(32)) return hipGetLastError();
   e = compact(EventPred{*b}, EventAct{*fs, *b}, b->n, b->blk, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(txv_k_status_out, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);

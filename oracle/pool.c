@@ -53,7 +53,22 @@ static pnode* pl_find(const plist* l, const uint8_t* k) {   /* the mapped node w
     if (n->mapped && !memcmp(n->key, k, 32)) return n;
   return 0;
 }
+/* chains stay short: the bucket array doubles when the list outgrows it (the gate's pool holds
+ * ~10^8 entries) */
+static void pl_rehash(plist* l) {
+  const size_t nb = l->nb * 2 + 1;
+  pnode** b = (pnode**)calloc(nb, sizeof(pnode*));
+  free(l->bucket);
+  l->bucket = b;
+  l->nb = nb;
+  for (pnode* n = l->head; n; n = n->next) {
+    const size_t i = bidx(l, n->key);
+    n->hnext = b[i];
+    b[i] = n;
+  }
+}
 static pnode* pl_push_back(plist* l, const uint8_t* k, uint32_t size) {
+  if (l->len >= 2 * l->nb) pl_rehash(l);
   pnode* old = pl_find(l, k);
   if (old) old->mapped = 0;     /* txsMap.Store / cache map assignment replaces the entry */
   pnode* n = (pnode*)calloc(1, sizeof *n);
