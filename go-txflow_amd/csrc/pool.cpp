@@ -224,11 +224,13 @@ struct PartIndex {
   void reserve(size_t m) { for (auto& f : p) f->reserve(m / kParts + m / (4 * kParts) + 64); }
 };
 
-// batch_check's per-call arrays, kept across calls
+// batch_check's per-call arrays, kept across calls.  Per-vote arrays are indexed by arrival
+// index i; per-partition ones by position j in the partition order (order[j] = i, pos[i] = j), so
+// the threads of the per-partition passes write disjoint contiguous ranges
 struct BatchScratch {
-  std::vector<uint32_t> cnt, order, aidx;
-  std::vector<int32_t> prevb, nextb, firstb, cnode, qpos;
-  std::vector<uint8_t> dec;                 // 0 not a push (too large), 1 miss, 2 hit, 3 far
+  std::vector<uint32_t> cnt, order, pos, aidx, hist;
+  std::vector<int32_t> prevj, nextj, firstj, cnodej, qpos, adm;
+  std::vector<uint8_t> decj, dec;           // 0 not a push (too large), 1 miss, 2 hit, 3 far
   std::vector<int32_t> qtouched;
 };
 
@@ -366,7 +368,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
                  const uint8_t* part, uint8_t* status_out) {
   if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;   // the bytes cap could bind
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
-  std::chrono::steady_clock::time_point tp[8];
+  std::chrono::steady_clock::time_point tp[10];
   int ntp = 0;
   auto mark = [&] { if (prof) tp[ntp++] = std::chrono::steady_clock::now(); };
   mark();
@@ -374,51 +376,97 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   const bool wal = (p->cfg.flags & TXV_POOL_WAL) != 0, cache_on = p->cache_on;
   const uint64_t C = p->cfg.cache_size, L0 = cache_on ? p->cache.len : 0;
   const uint32_t* sizes = p->sizes.data();
-  // pushes: the votes that reach cache.Push (the Size cap aside); position L0 + aidx[i] in S
-  S.aidx.resize(n);
-  uint32_t na = 0;
-  for (uint32_t i = 0; i < n; ++i) { S.aidx[i] = na; na += (int64_t)sizes[i] <= max_tx; }
-  const bool evict = cache_on && L0 + na > C;
-  // batch order per partition
+  auto is_push = [&](uint32_t i) { return (int64_t)sizes[i] <= max_tx; };
+  // 0. partition order (stable) and the push index aidx[i] (position L0 + aidx[i] in S), from
+  //    per-chunk histograms
+  const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
+  S.hist.assign((size_t)P * (kParts + 1), 0);
+  S.order.resize(n); S.pos.resize(n); S.aidx.resize(n);
+  auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
+  };
+  txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      uint32_t lo, hi, pushes = 0;
+      chunk(c, lo, hi);
+      uint32_t* h = S.hist.data() + (size_t)c * (kParts + 1);
+      for (uint32_t i = lo; i < hi; ++i) { ++h[part[i]]; pushes += is_push(i); }
+      h[kParts] = pushes;
+    }
+  }, 1);
   S.cnt.assign(kParts + 1, 0);
-  S.order.resize(n);
-  for (uint32_t i = 0; i < n; ++i) ++S.cnt[part[i] + 1];
-  for (uint32_t q = 0; q < kParts; ++q) S.cnt[q + 1] += S.cnt[q];
+  uint32_t na = 0;
   {
-    std::vector<uint32_t> at(S.cnt.begin(), S.cnt.end() - 1);
-    for (uint32_t i = 0; i < n; ++i) S.order[at[part[i]]++] = i;
+    uint32_t run = 0;
+    for (uint32_t q = 0; q < kParts; ++q) {
+      S.cnt[q] = run;
+      for (uint32_t c = 0; c < P; ++c) {
+        uint32_t& h = S.hist[(size_t)c * (kParts + 1) + q];
+        const uint32_t t = h;
+        h = run;
+        run += t;
+      }
+    }
+    S.cnt[kParts] = run;
+    for (uint32_t c = 0; c < P; ++c) {
+      uint32_t& h = S.hist[(size_t)c * (kParts + 1) + kParts];
+      const uint32_t t = h;
+      h = na;
+      na += t;
+    }
   }
+  txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      uint32_t lo, hi;
+      chunk(c, lo, hi);
+      uint32_t* h = S.hist.data() + (size_t)c * (kParts + 1);
+      uint32_t a = h[kParts];
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t j = h[part[i]]++;
+        S.order[j] = i;
+        S.pos[i] = j;
+        S.aidx[i] = a;
+        a += is_push(i);
+      }
+    }
+  }, 1);
+  const bool evict = cache_on && L0 + na > C;
   auto per_part = [&](const std::function<void(uint32_t)>& fn) {
     txv_host_parallel_for(ctx, kParts, [&](uint32_t lo, uint32_t hi) { for (uint32_t q = lo; q < hi; ++q) fn(q); }, 1);
   };
-  S.prevb.resize(n); S.firstb.resize(n); S.cnode.resize(n); S.nextb.assign(n, -1); S.dec.resize(n);
+  S.prevj.resize(n); S.firstj.resize(n); S.cnodej.resize(n); S.nextj.resize(n); S.decj.resize(n);
   mark();
   // 1. per partition, in batch order: the previous push of the same key in the batch, the first
-  //    one, and the cache node of a first push whose key is cached
+  //    one, and the cache node of a first push whose key is cached (a hash tag beside each slot:
+  //    keys are compared only on a tag match)
   per_part([&](uint32_t q) {
     const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
     uint32_t cap = 16;
     while (cap < 2 * (hi - lo)) cap *= 2;
-    std::vector<uint32_t> tab(cap, 0);            // batch index + 1 of the key's last push
+    std::vector<uint64_t> tab(cap, 0);            // (tag << 32) | (j + 1) of the key's last push
     const FlatIndex& cf = *p->cache_map.p[q];
     for (uint32_t j = lo; j < hi; ++j) {
       if (cache_on && j + kAdmitAhead < hi) cf.prefetch(keys[S.order[j + kAdmitAhead]]);
       const uint32_t i = S.order[j];
-      S.cnode[i] = -1;
-      if ((int64_t)sizes[i] > max_tx) { S.prevb[i] = -2; S.firstb[i] = (int32_t)i; continue; }
-      size_t s = batch_tab_hash(keys[i]) & (cap - 1);
-      while (tab[s] && !(keys[tab[s] - 1] == keys[i])) s = (s + 1) & (cap - 1);
-      if (tab[s]) {
-        const uint32_t pv = tab[s] - 1;
-        S.prevb[i] = (int32_t)pv;
-        S.firstb[i] = S.firstb[pv];
-        S.nextb[pv] = (int32_t)i;
+      S.cnodej[j] = -1;
+      S.nextj[j] = -1;
+      if (!is_push(i)) { S.prevj[j] = -2; S.firstj[j] = (int32_t)j; continue; }
+      const uint64_t hv = batch_tab_hash(keys[i]);
+      const uint64_t tag = (hv >> 32) | 1u;
+      size_t sl = hv & (cap - 1);
+      for (; tab[sl]; sl = (sl + 1) & (cap - 1))
+        if ((tab[sl] >> 32) == tag && keys[S.order[(uint32_t)tab[sl] - 1]] == keys[i]) break;
+      if (tab[sl]) {
+        const uint32_t pj = (uint32_t)tab[sl] - 1;
+        S.prevj[j] = (int32_t)pj;
+        S.firstj[j] = S.firstj[pj];
+        S.nextj[pj] = (int32_t)j;
       } else {
-        S.prevb[i] = -1;
-        S.firstb[i] = (int32_t)i;
-        if (cache_on) S.cnode[i] = cf.find(keys[i]);
+        S.prevj[j] = -1;
+        S.firstj[j] = (int32_t)j;
+        if (cache_on) S.cnodej[j] = cf.find(keys[i]);
       }
-      tab[s] = i + 1;
+      tab[sl] = (tag << 32) | (j + 1);
     }
   });
   mark();
@@ -434,21 +482,22 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     }
   }
   mark();
-  // 3. decisions
-  std::vector<uint32_t> far;
+  // 3. decisions, per partition position
+  std::vector<uint32_t> far;                      // arrival indices
   std::mutex far_mu;
   txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
     std::vector<uint32_t> mine;
-    for (uint32_t i = lo; i < hi; ++i) {
+    for (uint32_t j = lo; j < hi; ++j) {
+      const uint32_t i = S.order[j];
       uint8_t d;
-      if (S.prevb[i] == -2) d = 0;
+      if (S.prevj[j] == -2) d = 0;
       else if (!cache_on) d = 1;
-      else if (S.prevb[i] >= 0) d = (!evict || S.aidx[i] - S.aidx[S.prevb[i]] - 1 < C) ? 2 : 3;
-      else if (S.cnode[i] >= 0) {
-        const int32_t r = evict ? S.qpos[S.cnode[i]] : -1;
+      else if (S.prevj[j] >= 0) d = (!evict || S.aidx[i] - S.aidx[S.order[S.prevj[j]]] - 1 < C) ? 2 : 3;
+      else if (S.cnodej[j] >= 0) {
+        const int32_t r = evict ? S.qpos[S.cnodej[j]] : -1;
         d = (r < 0 || L0 + S.aidx[i] - (uint64_t)r - 1 < C) ? 2 : 3;
       } else d = 1;
-      S.dec[i] = d;
+      S.decj[j] = d;
       if (d == 3) mine.push_back(i);
     }
     if (!mine.empty()) {
@@ -462,9 +511,10 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
     auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
     std::vector<std::pair<uint64_t, uint64_t>> pairs;      // (next occurrence, occurrence)
-    for (uint32_t i = 0; i < n; ++i) {
-      if (S.prevb[i] >= 0) pairs.emplace_back(pos2(i), pos2((uint32_t)S.prevb[i]));
-      else if (S.prevb[i] == -1 && S.cnode[i] >= 0) pairs.emplace_back(pos2(i), init2(S.cnode[i]));
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t i = S.order[j];
+      if (S.prevj[j] >= 0) pairs.emplace_back(pos2(i), pos2(S.order[S.prevj[j]]));
+      else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) pairs.emplace_back(pos2(i), init2(S.cnodej[j]));
     }
     std::sort(pairs.begin(), pairs.end());
     std::sort(far.begin(), far.end());                     // by position = batch order
@@ -473,107 +523,175 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     uint32_t added = 0;
     size_t pi = 0;
     for (uint32_t i : far) {
+      const uint32_t j = S.pos[i];
       const uint64_t e = pos2(i);
       for (; pi < pairs.size() && pairs[pi].first < e; ++pi, ++added)
         for (uint64_t x = pairs[pi].second + 1; x <= M; x += x & (~x + 1)) ++fen[x];
-      const uint64_t p2 = S.prevb[i] >= 0 ? pos2((uint32_t)S.prevb[i]) : init2(S.cnode[i]);
+      const uint64_t p2 = S.prevj[j] >= 0 ? pos2(S.order[S.prevj[j]]) : init2(S.cnodej[j]);
       uint32_t upto = 0;                                   // pairs starting at or before p
       for (uint64_t x = p2 + 1; x > 0; x -= x & (~x + 1)) upto += fen[x];
       const uint64_t nested = added - upto;
       const uint64_t window = (e - p2) / 2 - 1;           // pushes strictly between (p is exact here)
-      S.dec[i] = window - nested < C ? 2 : 1;
+      S.decj[j] = window - nested < C ? 2 : 1;
     }
   }
   if (evict)
     for (int32_t e : S.qtouched) S.qpos[e] = -1;
   mark();
-  // 4. statuses in arrival order, the Size cap's cut
+  // 4. statuses in arrival order, the Size cap's cut (only when the batch could reach it)
+  S.dec.resize(n); S.adm.resize(n);
   uint32_t m = n;
   uint64_t admitted = 0, admitted_bytes = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    if ((int64_t)p->txs.len + (int64_t)admitted >= (int64_t)p->cfg.size) { m = i; break; }
-    const uint8_t d = S.dec[i];
-    if (d == 0) status_out[i] = TXV_POOL_ERR_TOO_LARGE;
-    else if (d == 2) status_out[i] = TXV_POOL_ERR_IN_CACHE;
-    else if (!sizes[i] && wal) status_out[i] = TXV_POOL_ERR_ENCODING;
-    else { status_out[i] = TXV_POOL_OK; ++admitted; admitted_bytes += sizes[i]; }
+  auto status_of = [&](uint32_t i, uint8_t d) -> uint8_t {
+    if (d == 0) return TXV_POOL_ERR_TOO_LARGE;
+    if (d == 2) return TXV_POOL_ERR_IN_CACHE;
+    return (!sizes[i] && wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
+  };
+  if ((int64_t)p->txs.len + (int64_t)na < (int64_t)p->cfg.size) {
+    std::vector<uint64_t> cnt_c(P, 0), bytes_c(P, 0);
+    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+      for (uint32_t c = c0; c < c1; ++c) {
+        uint32_t lo, hi;
+        chunk(c, lo, hi);
+        uint64_t k = 0, b = 0;
+        for (uint32_t i = lo; i < hi; ++i) {
+          const uint8_t d = S.decj[S.pos[i]];
+          S.dec[i] = d;
+          const uint8_t st = status_of(i, d);
+          status_out[i] = st;
+          if (st == TXV_POOL_OK) { ++k; b += sizes[i]; }
+        }
+        cnt_c[c] = k;
+        bytes_c[c] = b;
+      }
+    }, 1);
+    std::vector<uint64_t> base_c(P, 0);
+    for (uint32_t c = 0; c < P; ++c) { base_c[c] = admitted; admitted += cnt_c[c]; admitted_bytes += bytes_c[c]; }
+    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+      for (uint32_t c = c0; c < c1; ++c) {
+        uint32_t lo, hi;
+        chunk(c, lo, hi);
+        int32_t a = (int32_t)base_c[c];
+        for (uint32_t i = lo; i < hi; ++i) S.adm[i] = status_out[i] == TXV_POOL_OK ? a++ : -1;
+      }
+    }, 1);
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      if ((int64_t)p->txs.len + (int64_t)admitted >= (int64_t)p->cfg.size) { m = i; break; }
+      const uint8_t d = S.decj[S.pos[i]];
+      S.dec[i] = d;
+      const uint8_t st = status_of(i, d);
+      status_out[i] = st;
+      S.adm[i] = -1;
+      if (st == TXV_POOL_OK) { S.adm[i] = (int32_t)admitted++; admitted_bytes += sizes[i]; }
+    }
+    if (m < n) {
+      memset(status_out + m, TXV_POOL_ERR_FULL, n - m);
+      for (uint32_t i = m; i < n; ++i) { S.dec[i] = 0; S.adm[i] = -1; }
+    }
   }
-  if (m < n) memset(status_out + m, TXV_POOL_ERR_FULL, n - m);
+  mark();
   // 5. the cache: the C most recent distinct keys of S up to the cut, in recency order
   if (cache_on) {
     std::vector<uint32_t> last;                            // pushes that are their key's last before m
-    for (uint32_t i = 0; i < m; ++i)
-      if (S.dec[i] && (S.nextb[i] < 0 || (uint32_t)S.nextb[i] >= m)) last.push_back(i);
+    last.reserve(na);
+    for (uint32_t i = 0; i < m; ++i) {
+      if (!S.dec[i]) continue;
+      const int32_t nj = S.nextj[S.pos[i]];
+      if (nj < 0 || S.order[nj] >= m) last.push_back(i);
+    }
     const size_t U = last.size(), keepU = std::min<uint64_t>(U, C);
-    // cached keys pushed again leave their place (their node moves, or goes when too old)
+    auto cnode_of = [&](uint32_t i) { return S.cnodej[S.firstj[S.pos[i]]]; };
+    // cached keys pushed again leave their place
+    uint64_t detached = 0;
     for (uint32_t i = 0; i < m; ++i)
-      if (S.prevb[i] == -1 && S.cnode[i] >= 0) p->cache.detach(S.cnode[i]);
-    while (p->cache.len > C - keepU) {                     // evictions from the front
-      const int32_t h = p->cache.head;
-      p->cache_map.erase(p->cache.nodes[h].k);
-      p->cache.unlink(h);
-    }
-    std::vector<int32_t> fin(keepU);
-    uint32_t n_new = 0;
-    for (size_t u = 0; u < U; ++u) {
-      const uint32_t i = last[u];
-      const int32_t cn = S.cnode[S.firstb[i]];
-      if (u < U - keepU) {                                 // pushed, then evicted inside the batch
-        if (cn >= 0) { p->cache_map.erase(keys[i]); p->cache.free_.push_back(cn); }
-      } else {
-        fin[u - (U - keepU)] = cn;
-        n_new += cn < 0;
+      if (S.dec[i] && S.prevj[S.pos[i]] == -1 && S.cnodej[S.pos[i]] >= 0) { p->cache.detach(S.cnodej[S.pos[i]]); ++detached; }
+    const uint64_t keep_old = std::min<uint64_t>(p->cache.len, C - keepU), evicted = p->cache.len - keep_old;
+    if (keep_old < evicted + detached) {
+      // most of the old LRU goes: rebuild list and index from the survivors + this batch's keys
+      std::vector<Key> fin_keys;
+      fin_keys.reserve(keep_old + keepU);
+      {
+        int32_t e = p->cache.head;
+        for (uint64_t r = 0; r < evicted; ++r) e = p->cache.nodes[e].next;
+        for (; e >= 0; e = p->cache.nodes[e].next) fin_keys.push_back(p->cache.nodes[e].k);
       }
-    }
-    next_indices(p->cache, n_new, p->idx_c);
-    if (n_new) {
-      const size_t old = p->cache.nodes.size();
-      p->cache.nodes.resize(std::max<size_t>(old, (size_t)p->idx_c[n_new - 1] + 1));
-      const size_t nf = p->cache.free_.size();
-      p->cache.free_.resize(nf - std::min<size_t>(nf, n_new));
-    }
-    for (size_t u = 0, k = 0; u < keepU; ++u)
-      if (fin[u] < 0) {
-        fin[u] = p->idx_c[k++];
-        p->cache.nodes[fin[u]] = KeyList::Node{keys[last[U - keepU + u]], 0, -1, -1};
+      for (size_t u = U - keepU; u < U; ++u) fin_keys.push_back(keys[last[u]]);
+      const uint32_t L = (uint32_t)fin_keys.size();
+      p->cache.clear();
+      p->cache.nodes.resize(L);
+      for (uint32_t k = 0; k < L; ++k)
+        p->cache.nodes[k] = KeyList::Node{fin_keys[k], 0, (int32_t)k - 1, k + 1 < L ? (int32_t)k + 1 : -1};
+      p->cache.head = L ? 0 : -1;
+      p->cache.tail = (int32_t)L - 1;
+      p->cache.len = L;
+      per_part([&](uint32_t q) {
+        FlatIndex& f = *p->cache_map.p[q];
+        f.clear();
+        for (uint32_t k = 0; k < L; ++k)
+          if (PartIndex::part(fin_keys[k]) == q) f.put(fin_keys[k], (int32_t)k);
+      });
+    } else {
+      for (uint64_t r = 0; r < evicted; ++r) {             // evictions from the front
+        const int32_t h = p->cache.head;
+        p->cache_map.erase(p->cache.nodes[h].k);
+        p->cache.unlink(h);
       }
-    std::vector<std::vector<std::pair<uint32_t, int32_t>>> ins(kParts);
-    for (size_t u = 0; u < keepU; ++u) {
-      const uint32_t i = last[U - keepU + u];
-      if (S.cnode[S.firstb[i]] < 0) ins[part[i]].emplace_back(i, fin[u]);
-    }
-    per_part([&](uint32_t q) {                             // index the new nodes
-      FlatIndex& f = *p->cache_map.p[q];
-      const auto& L = ins[q];
-      for (size_t j = 0; j < L.size(); ++j) {
-        if (j + kAdmitAhead < L.size()) f.prefetch(keys[L[j + kAdmitAhead].first]);
-        f.put(keys[L[j].first], L[j].second);
+      std::vector<int32_t> fin(keepU);
+      uint32_t n_new = 0;
+      for (size_t u = 0; u < U; ++u) {
+        const uint32_t i = last[u];
+        const int32_t cn = cnode_of(i);
+        if (u < U - keepU) {                               // pushed, then evicted inside the batch
+          if (cn >= 0) { p->cache_map.erase(keys[i]); p->cache.free_.push_back(cn); }
+        } else {
+          fin[u - (U - keepU)] = cn;
+          n_new += cn < 0;
+        }
       }
-    });
-    p->cache.append_linked(fin);
+      next_indices(p->cache, n_new, p->idx_c);
+      if (n_new) {
+        const size_t old = p->cache.nodes.size();
+        p->cache.nodes.resize(std::max<size_t>(old, (size_t)p->idx_c[n_new - 1] + 1));
+        const size_t nf = p->cache.free_.size();
+        p->cache.free_.resize(nf - std::min<size_t>(nf, n_new));
+      }
+      std::vector<std::vector<std::pair<uint32_t, int32_t>>> ins(kParts);
+      for (size_t u = 0, k = 0; u < keepU; ++u)
+        if (fin[u] < 0) {
+          const uint32_t i = last[U - keepU + u];
+          fin[u] = p->idx_c[k++];
+          p->cache.nodes[fin[u]] = KeyList::Node{keys[i], 0, -1, -1};
+          ins[part[i]].emplace_back(i, fin[u]);
+        }
+      per_part([&](uint32_t q) {                           // index the new nodes
+        FlatIndex& f = *p->cache_map.p[q];
+        const auto& L = ins[q];
+        for (size_t j = 0; j < L.size(); ++j) {
+          if (j + kAdmitAhead < L.size()) f.prefetch(keys[L[j + kAdmitAhead].first]);
+          f.put(keys[L[j].first], L[j].second);
+        }
+      });
+      p->cache.append_linked(fin);
+    }
   }
   mark();
   // 6. addTx for the admitted votes in arrival order (txsMap.Store overwrites)
   if (admitted) {
-    std::vector<uint32_t> adm;
-    adm.reserve(admitted);
-    for (uint32_t i = 0; i < m; ++i)
-      if (status_out[i] == TXV_POOL_OK) adm.push_back(i);
-    const uint32_t A = (uint32_t)adm.size();
+    const uint32_t A = (uint32_t)admitted;
     next_indices(p->txs, A, p->idx_t);
     p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
-    txv_host_parallel_for(ctx, A, [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t a = lo; a < hi; ++a) p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[adm[a]], sizes[adm[a]], -1, -1};
+    txv_host_parallel_for(ctx, m, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; ++i)
+        if (S.adm[i] >= 0) p->txs.nodes[p->idx_t[S.adm[i]]] = KeyList::Node{keys[i], sizes[i], -1, -1};
     });
-    std::vector<int32_t> slot_of(n, -1);
-    for (uint32_t a = 0; a < A; ++a) slot_of[adm[a]] = p->idx_t[a];
     per_part([&](uint32_t q) {
       FlatIndex& f = *p->txs_map.p[q];
       const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
       for (uint32_t j = lo; j < hi; ++j) {
         if (j + kAdmitAhead < hi) f.prefetch(keys[S.order[j + kAdmitAhead]]);
         const uint32_t i = S.order[j];
-        if (slot_of[i] >= 0) f.put(keys[i], slot_of[i]);
+        if (S.adm[i] >= 0) f.put(keys[i], p->idx_t[S.adm[i]]);
       }
     });
     link_appended(ctx, p->txs, p->idx_t, A);
@@ -582,8 +700,8 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   mark();
   if (prof) {
     auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    fprintf(stderr, "[txv pool] batch: order=%.3f scan=%.3f front=%.3f decide=%.3f far(%zu)=%.3f cache=%.3f txs=%.3f ms\n",
-            ms(0), ms(1), ms(2), ms(3), far.size(), ms(4), ms(5), ms(6));
+    fprintf(stderr, "[txv pool] batch: order=%.3f scan=%.3f front=%.3f decide=%.3f far(%zu)=%.3f status=%.3f cache=%.3f txs=%.3f ms\n",
+            ms(0), ms(1), ms(2), ms(3), far.size(), ms(4), ms(5), ms(6), ms(7));
   }
   return true;
 }
