@@ -441,6 +441,10 @@ def load_pmc(table_w: int, n_votes: int):
     return pj.get("verify_w_exec_lane_slots_per_vote"), traffic, pj.get("source"), tally, pj.get("k1b_valu_issue_busy")
 
 
+TALLY_ALG_VOTE = 16       # B per vote the tally must move
+TALLY_ALG_ADDED = 244     # B per ADDED vote: 128-byte accepted row written + 116 source bytes read
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -648,11 +652,19 @@ def main():
             "cpu_baseline": cpu,
             # the tally chain after verify (HBM-bound per BASELINE.md): bytes per launch from the same
             # PMC passes (2 x FETCH_SIZE + WRITE_SIZE of its kernels) over the standalone tally time
+            # algorithmic bytes: 16 B per vote (set id, validator, verdict, pre-check,
+            # status, cell) + 244 B per ADDED vote (its 128-byte accepted-vote row written, the 116
+            # bytes of signature / height / time / TxKey it is made of read); every C2 vote is ADDED
             "tally": {"ms": round(s_ms[2], 3), "hbm_bytes_per_launch": tally_bytes,
+                      "alg_bytes_per_launch": TALLY_ALG_VOTE * wl.n + TALLY_ALG_ADDED * wl.n,
+                      "alg_GBps": round((TALLY_ALG_VOTE + TALLY_ALG_ADDED) * wl.n / (s_ms[2] * 1e-3) / 1e9, 1),
+                      "alg_frac_of_8TBps": round((TALLY_ALG_VOTE + TALLY_ALG_ADDED) * wl.n / (s_ms[2] * 1e-3) / 8e12, 3),
+                      "traffic_over_alg": None if not tally_bytes else
+                      round(tally_bytes / ((TALLY_ALG_VOTE + TALLY_ALG_ADDED) * wl.n), 3),
                       "GBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 1e9, 1),
                       "frac_of_8TBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 8e12, 3),
-                      "note": "includes the accepted-vote arena rows (128 B per ADDED vote) MakeCommit reads; "
-                              "BASELINE.md's 16 B/vote counts the cell update alone"},
+                      "note": "hbm_bytes_per_launch from the committed PMC passes (2 x FETCH_SIZE + WRITE_SIZE of "
+                              "the tally kernels); alg = 16 B/vote + 244 B per ADDED vote (BASELINE.md)"},
         }
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = {

@@ -27,14 +27,17 @@
 //   min      every verified pending vote posts its arrival index to its cell (atomic min):
 //            the cell then holds the FIRST verified vote of the (set, validator) group
 //   resolve  each pending vote decides its code from its cell: earlier accepted vote ->
-//            signature compare; first verified == itself -> ADDED (an arena row is taken);
-//            first verified earlier -> signature compare with it; none -> invalid signature
-//   bucket   the ADDED votes of each set (<= one per validator) are listed in the set's cell row
-//   cross    one wave per set with ADDED votes: stake sum, and the arrival index at which the
-//            prefix (in arrival order) of the stake first reaches quorum (per-lane prefix sums
-//            over the set's list in LDS, one wave min); ADDED votes at or after it fire
-//   events   compaction of the crossing votes in arrival order -> commit events
-//   out      final statuses (pre-check or tally) into mapped host memory
+//            signature compare; first verified == itself -> ADDED (an arena row is taken by a
+//            wave-aggregated atomic and written right there); first verified earlier ->
+//            signature compare with it; none -> invalid signature
+//   cross    one wave per set the batch ADDED votes to (persistent waves over the set ids,
+//            stamp check): its ADDED votes are the stamped cells of its row; stake sum, and the
+//            arrival index at which the prefix (in arrival order) of the stake first reaches
+//            quorum (per-lane prefix sums over the set's list in LDS, one wave min); the cells'
+//            accepted rows
+//   out      final statuses (pre-check or tally; an ADDED vote at or after its set's crossing
+//            fires) into mapped host memory, and the per-block counts of commit events
+//   events   compaction of the crossing votes in arrival order -> commit events + batch summary
 #include <algorithm>
 
 #include "txv_device.h"
@@ -508,8 +511,8 @@ __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b
   const uint32_t s = e == TXV_NONE ? TXV_NONE : fs.tab[e].id;
   b.set[i] = s;
   if (s == TXV_NONE || b.pre[i] != TXV_S_PENDING || b.ok[i] != 1) return;
-  const size_t cell = (size_t)s * fs.n_vals + b.val[i];
-  if (fs.acc[cell] == 0) atomicMin((unsigned long long*)&fs.cand[cell], (unsigned long long)cand_key(b.stamp, i));
+  TallyCell& c = fs.cell[(size_t)s * fs.n_vals + b.val[i]];
+  if (c.acc == 0) atomicMin((unsigned long long*)&c.cand, (unsigned long long)cand_key(b.stamp, i));
 }
 
 __device__ __forceinline__ bool pending_in_set(const FlowBatch& b, uint32_t i) {
@@ -529,76 +532,75 @@ __device__ __forceinline__ bool sig_eq_votes(const FlowBatch& b, uint32_t i, uin
   return d == 0;
 }
 
-// each pending vote's code from its cell (types/vote_set.go:109-119)
-__global__ void __launch_bounds__(256) txv_k_tally_resolve(FlowState fs, FlowBatch b) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= b.n || !pending_in_set(b, i)) return;
-  const uint32_t s = b.set[i];
-  const uint8_t fl = b.flags[i];
-  const bool sig64 = (fl & TXV_FLAG_SIG64) != 0;
-  const size_t cell = (size_t)s * fs.n_vals + b.val[i];
-  const uint32_t acc = fs.acc[cell];
-  uint8_t st;
-  if (acc) {                                   // accepted in an earlier batch (vote_set.go:109-114)
-    st = sig64 && sig_eq_arena(fs, b, i, acc - 1) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
-  } else {
-    const uint32_t f = cand_of(fs.cand[cell], b.stamp);
-    if (f == i) st = TXV_S_ADDED;              // the reference stores it (vote_set.go:154)
-    else if (f != TXV_NONE && f < i)           // an earlier vote of the batch was accepted
-      st = sig64 && sig_eq_votes(b, i, f) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
-    else                                       // no accepted vote before it and it did not verify
-      st = (fl & TXV_FLAG_BADMSG) ? TXV_S_SIGNBYTES : TXV_S_INVALID_SIGNATURE;
+// each pending vote's code from its cell (types/vote_set.go:109-119); an ADDED vote takes an
+// arena row (one atomic per 1024-vote block for the block's ADDED votes) and stores the accepted vote in full
+// (the reference's votes[addr] = vote, vote_set.go:154); the cell keeps the row for the crossing
+// step, which publishes it as the cell's accepted vote once no vote of the batch reads acc
+__global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBatch b) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base_s;
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bool added = false;
+  uint32_t s = TXV_NONE;
+  TallyCell* cell = nullptr;
+  if (i < b.n && pending_in_set(b, i)) {
+    s = b.set[i];
+    const uint8_t fl = b.flags[i];
+    const bool sig64 = (fl & TXV_FLAG_SIG64) != 0;
+    cell = fs.cell + (size_t)s * fs.n_vals + b.val[i];
+    const uint32_t acc = cell->acc;
+    uint8_t st;
+    if (acc) {                                   // accepted in an earlier batch (vote_set.go:109-114)
+      st = sig64 && sig_eq_arena(fs, b, i, acc - 1) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
+    } else {
+      const uint32_t f = cand_of(cell->cand, b.stamp);
+      if (f == i) { st = TXV_S_ADDED; added = true; }   // the reference stores it (vote_set.go:154)
+      else if (f != TXV_NONE && f < i)           // an earlier vote of the batch was accepted
+        st = sig64 && sig_eq_votes(b, i, f) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
+      else                                       // no accepted vote before it and it did not verify
+        st = (fl & TXV_FLAG_BADMSG) ? TXV_S_SIGNBYTES : TXV_S_INVALID_SIGNATURE;
+    }
+    b.status[i] = st;
   }
-  b.status[i] = st;
+  // the block's ADDED votes take consecutive arena rows: one atomic per 1024 votes (a hot
+  // counter serialises at ~10k atomics per 50 us)
+  const uint64_t m = __ballot(added);
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < 16; ++k) t += wsum[k];
+    base_s = t ? atomicAdd(&fs.ctr->arena_used, t) : 0u;
+  }
+  __syncthreads();
+  if (!added) return;
+  uint32_t r = base_s + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  for (int k = 0; k < w; ++k) r += wsum[k];
+  fs.set_stamp[s] = b.stamp;
+  if (r >= fs.max_accepted) {
+    atomicOr(&fs.ctr->err, TXV_FERR_ARENA);
+    cell->row = 0;
+    return;
+  }
+  cell->row = r + 1;
+  const size_t M = fs.max_accepted;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) fs.arena_sig[j * M + r] = b.sig[(size_t)j * b.n_pad + i];
+  fs.arena_height[r] = b.height[i];
+  fs.arena_sec[r] = b.ts_sec[i];
+  fs.arena_nanos[r] = b.ts_nanos[i];
+  fs.arena_val[r] = b.val[i];
+  fs.arena_seq[r] = b.seq_base + i;
+  uint32_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (b.txkey) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(b.txkey + (size_t)i * 32);
+    const uint4 x = s4[0], y = s4[1];
+    tk[0] = x.x; tk[1] = x.y; tk[2] = x.z; tk[3] = x.w; tk[4] = y.x; tk[5] = y.y; tk[6] = y.z; tk[7] = y.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fs.arena_txkey[j * M + r] = tk[j];
 }
-
-// ADDED votes in arrival order -> consecutive arena rows (the accepted vote in full) and the
-// set's stamp (the cross step visits only stamped sets)
-struct AddedPred {
-  FlowBatch b;
-  __device__ bool operator()(uint32_t i) const { return b.pre[i] == TXV_S_PENDING && b.set[i] != TXV_NONE && b.status[i] == TXV_S_ADDED; }
-};
-struct AddedAct {
-  FlowState fs;
-  FlowBatch b;
-  __device__ void operator()(uint32_t i, uint32_t rank) const {
-    const uint32_t r = fs.ctr->arena_used + rank;
-    fs.set_stamp[b.set[i]] = b.stamp;
-    if (r >= fs.max_accepted) {
-      atomicOr(&fs.ctr->err, TXV_FERR_ARENA);
-      b.row[i] = TXV_NONE;
-      return;
-    }
-    b.row[i] = r;
-    const size_t M = fs.max_accepted;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) fs.arena_sig[j * M + r] = b.sig[(size_t)j * b.n_pad + i];
-    fs.arena_height[r] = b.height[i];
-    fs.arena_sec[r] = b.ts_sec[i];
-    fs.arena_nanos[r] = b.ts_nanos[i];
-    fs.arena_val[r] = b.val[i];
-    fs.arena_seq[r] = b.seq_base + i;
-    uint32_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (b.txkey) {
-      const uint4* s4 = reinterpret_cast<const uint4*>(b.txkey + (size_t)i * 32);
-      const uint4 a = s4[0], c = s4[1];
-      tk[0] = a.x; tk[1] = a.y; tk[2] = a.z; tk[3] = a.w; tk[4] = c.x; tk[5] = c.y; tk[6] = c.z; tk[7] = c.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fs.arena_txkey[j * M + r] = tk[j];
-  }
-};
-
-// the sets stamped by this batch's ADDED votes, compacted (scan over the set ids)
-struct TouchedPred {
-  FlowState fs;
-  FlowBatch b;
-  __device__ bool operator()(uint32_t s) const { return s < fs.ctr->n_sets && fs.set_stamp[s] == b.stamp; }
-};
-struct TouchedAct {
-  FlowState fs;
-  __device__ void operator()(uint32_t s, uint32_t rank) const { fs.touched[rank] = s; }
-};
 
 __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 #pragma unroll
@@ -608,113 +610,105 @@ __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
 
 constexpr uint32_t kListCap = 512;   // ADDED votes of a set kept in LDS (every set of a <= 512-validator registry)
 
-// One wave per set that ADDED votes in this batch (the compacted touched list; persistent
-// waves): its ADDED votes are the cells of its row whose candidate carries this batch's stamp
-// (and held no accepted vote); stake sum, and the arrival index at which the prefix (in arrival
-// order) of the stake first reaches quorum (per-lane prefix sums over the LDS list, one wave
-// min); ADDED votes at or after it fire.
-__global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b, uint32_t nb, uint32_t nb_sets) {
+// One wave per set that ADDED votes in this batch (persistent waves over the set ids; a set
+// whose stamp is not this batch's is skipped): its ADDED votes are the cells of its row whose
+// candidate carries this batch's stamp and that held no accepted vote; stake sum, and the arrival
+// index at which the prefix (in arrival order) of the stake first reaches quorum (per-lane prefix
+// sums over the LDS list, one wave min): set_cross[s], read by the status pass (ADDED votes at or
+// after it fire); the cells' accepted rows are published here.
+__global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b, uint32_t sets_bound) {
   __shared__ __attribute__((aligned(16))) uint32_t l_vote[4][kListCap + 4];
   __shared__ __attribute__((aligned(16))) int64_t l_pow[4][kListCap + 4];
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t n_touched = fs.touched_blk[nb_sets];
   const uint32_t gw = blockIdx.x * 4 + wv, n_waves = gridDim.x * 4;
-  if (gw == 0 && lane == 0) {
-    const uint32_t au = fs.ctr->arena_used + b.blk[nb];
-    fs.ctr->arena_used = au > fs.max_accepted ? fs.max_accepted : au;
-  }
-  for (uint32_t t = gw; t < n_touched; t += n_waves) {
-    {
-      const uint32_t s = fs.touched[t];
-      const uint64_t* row = fs.cand + (size_t)s * fs.n_vals;
-      // list this set's ADDED votes (compacted in validator order)
-      uint32_t k = 0;
-      int64_t part = 0;
-      for (uint32_t v0 = 0; v0 < fs.n_vals; v0 += 64) {
-        const uint32_t v = v0 + lane;
-        const uint32_t f = v < fs.n_vals ? cand_of(row[v], b.stamp) : TXV_NONE;
-        const bool added = f != TXV_NONE && fs.acc[(size_t)s * fs.n_vals + v] == 0;
-        const uint64_t m = __ballot(added);
-        if (added) {
-          const uint32_t e = k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          const int64_t pw = fs.power[v];
-          if (e < kListCap) { l_vote[wv][e] = f; l_pow[wv][e] = pw; }
-          part += pw;
-        }
-        k += (uint32_t)__popcll(m);
+  const uint32_t n_sets = min(fs.ctr->n_sets, sets_bound);
+  for (uint32_t s = gw; s < n_sets; s += n_waves) {
+    if (fs.set_stamp[s] != b.stamp) continue;
+    TallyCell* row = fs.cell + (size_t)s * fs.n_vals;
+    // list this set's ADDED votes (compacted in validator order)
+    uint32_t k = 0;
+    int64_t part = 0;
+    for (uint32_t v0 = 0; v0 < fs.n_vals; v0 += 64) {
+      const uint32_t v = v0 + lane;
+      uint32_t f = TXV_NONE;
+      if (v < fs.n_vals) {
+        const TallyCell c = row[v];
+        if (c.acc == 0) f = cand_of(c.cand, b.stamp);
       }
-      __threadfence_block();
-      const bool in_lds = k <= kListCap;
-      const int64_t prior = fs.set_sum[s];
-      const int64_t total = prior + wave_sum64(part);
-      uint32_t cross = TXV_NO_CROSS;
-      if (prior >= fs.quorum) {
-        cross = 0;                              // already committed: every ADDED vote re-fires
-      } else if (total >= fs.quorum) {
-        // crossing = the arrival index T at which the stake prefix (in arrival order) first
-        // reaches quorum: with g(t) = stake of listed votes with arrival < t (monotone), T is
-        // the largest t with prior + g(t) < quorum, found bit by bit; each probe is one list
-        // pass + a wave sum
-        const int64_t need = fs.quorum - prior;
-        if (in_lds) {
-          // T = the smallest listed arrival index f_c whose prefix stake (every listed vote with
-          // f_j <= f_c) reaches need: each lane sums the prefix of its own entries with one pass
-          // over the list (LDS broadcast reads, independent iterations), then one wave min --
-          // no chain of dependent wave reductions (the kernel runs beside K1b, at a small share
-          // of the SIMDs' issue slots)
-          uint32_t T = TXV_NONE;
-          const uint32_t k4 = (k + 3u) & ~3u;        // the list padded to 4 with (never, 0)
-          if (lane < k4 - k) { l_vote[wv][k + lane] = 0xFFFFFFFFu; l_pow[wv][k + lane] = 0; }
-          __threadfence_block();
-          for (uint32_t c0 = 0; c0 < k; c0 += 128) {   // two entries per lane per pass
-            const uint32_t ca = c0 + lane, cb = c0 + 64 + lane;
-            const uint32_t fa = ca < k ? l_vote[wv][ca] : 0xFFFFFFFFu, fb = cb < k ? l_vote[wv][cb] : 0xFFFFFFFFu;
-            int64_t pa = 0, pb = 0;
-            const uint4* vq = reinterpret_cast<const uint4*>(l_vote[wv]);
-            const longlong2* pq = reinterpret_cast<const longlong2*>(l_pow[wv]);
-            for (uint32_t j = 0; j < k4; j += 4) {
-              const uint4 f4 = vq[j / 4];
-              const longlong2 p01 = pq[j / 2], p23 = pq[j / 2 + 1];
-              pa += (f4.x <= fa ? p01.x : 0) + (f4.y <= fa ? p01.y : 0) + (f4.z <= fa ? p23.x : 0) + (f4.w <= fa ? p23.y : 0);
-              pb += (f4.x <= fb ? p01.x : 0) + (f4.y <= fb ? p01.y : 0) + (f4.z <= fb ? p23.x : 0) + (f4.w <= fb ? p23.y : 0);
-            }
-            if (ca < k && pa >= need && fa < T) T = fa;
-            if (cb < k && pb >= need && fb < T) T = fb;
+      const bool added = f != TXV_NONE;
+      const uint64_t m = __ballot(added);
+      if (added) {
+        const uint32_t e = k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const int64_t pw = fs.power[v];
+        if (e < kListCap) { l_vote[wv][e] = f; l_pow[wv][e] = pw; }
+        part += pw;
+      }
+      k += (uint32_t)__popcll(m);
+    }
+    __threadfence_block();
+    const bool in_lds = k <= kListCap;
+    const int64_t prior = fs.set_sum[s];
+    const int64_t total = prior + wave_sum64(part);
+    uint32_t cross = TXV_NO_CROSS;
+    if (prior >= fs.quorum) {
+      cross = 0;                              // already committed: every ADDED vote re-fires
+    } else if (total >= fs.quorum) {
+      const int64_t need = fs.quorum - prior;
+      if (in_lds) {
+        // T = the smallest listed arrival index f_c whose prefix stake (every listed vote with
+        // f_j <= f_c) reaches need: each lane sums the prefix of its own entries with one pass
+        // over the list (LDS broadcast reads, independent iterations), then one wave min --
+        // no chain of dependent wave reductions (the kernel runs beside K1b, at a small share
+        // of the SIMDs' issue slots)
+        uint32_t T = TXV_NONE;
+        const uint32_t k4 = (k + 3u) & ~3u;        // the list padded to 4 with (never, 0)
+        if (lane < k4 - k) { l_vote[wv][k + lane] = 0xFFFFFFFFu; l_pow[wv][k + lane] = 0; }
+        __threadfence_block();
+        for (uint32_t c0 = 0; c0 < k; c0 += 128) {   // two entries per lane per pass
+          const uint32_t ca = c0 + lane, cb = c0 + 64 + lane;
+          const uint32_t fa = ca < k ? l_vote[wv][ca] : 0xFFFFFFFFu, fb = cb < k ? l_vote[wv][cb] : 0xFFFFFFFFu;
+          int64_t pa = 0, pb = 0;
+          const uint4* vq = reinterpret_cast<const uint4*>(l_vote[wv]);
+          const longlong2* pq = reinterpret_cast<const longlong2*>(l_pow[wv]);
+          for (uint32_t j = 0; j < k4; j += 4) {
+            const uint4 f4 = vq[j / 4];
+            const longlong2 p01 = pq[j / 2], p23 = pq[j / 2 + 1];
+            pa += (f4.x <= fa ? p01.x : 0) + (f4.y <= fa ? p01.y : 0) + (f4.z <= fa ? p23.x : 0) + (f4.w <= fa ? p23.y : 0);
+            pb += (f4.x <= fb ? p01.x : 0) + (f4.y <= fb ? p01.y : 0) + (f4.z <= fb ? p23.x : 0) + (f4.w <= fb ? p23.y : 0);
           }
+          if (ca < k && pa >= need && fa < T) T = fa;
+          if (cb < k && pb >= need && fb < T) T = fb;
+        }
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) T = min(T, (uint32_t)__shfl_xor((int)T, o, 64));
-          cross = T;
-        } else {
-          // more ADDED votes than the LDS list holds: binary lifting over the arrival-index bits,
-          // one pass over the set's row per probe
-          uint32_t T = 0;
-          for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
-            const uint32_t cand = T | (1u << bit);
-            int64_t sm = 0;
-            for (uint32_t v = lane; v < fs.n_vals; v += 64) {
-              const uint32_t f = cand_of(row[v], b.stamp);
-              if (f != TXV_NONE && f < cand && fs.acc[(size_t)s * fs.n_vals + v] == 0) sm += fs.power[v];
-            }
-            if (wave_sum64(sm) < need) T = cand;
+        for (int o = 32; o > 0; o >>= 1) T = min(T, (uint32_t)__shfl_xor((int)T, o, 64));
+        cross = T;
+      } else {
+        // more ADDED votes than the LDS list holds: binary lifting over the arrival-index bits,
+        // one pass over the set's row per probe
+        uint32_t T = 0;
+        for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
+          const uint32_t cand = T | (1u << bit);
+          int64_t sm = 0;
+          for (uint32_t v = lane; v < fs.n_vals; v += 64) {
+            const TallyCell c = row[v];
+            const uint32_t f = c.acc == 0 ? cand_of(c.cand, b.stamp) : TXV_NONE;
+            if (f != TXV_NONE && f < cand) sm += fs.power[v];
           }
-          cross = T;
+          if (wave_sum64(sm) < need) T = cand;
         }
+        cross = T;
       }
-      // ADDED statuses with the fired bit, and the accepted-vote cells
-      for (uint32_t v = lane; v < fs.n_vals; v += 64) {
-        const size_t cell = (size_t)s * fs.n_vals + v;
-        const uint32_t f = cand_of(row[v], b.stamp);
-        if (f == TXV_NONE || fs.acc[cell] != 0) continue;
-        const bool fire = cross != TXV_NO_CROSS && f >= cross;
-        b.status[f] = (uint8_t)(TXV_S_ADDED | (fire ? TXV_S_FIRED : 0u));
-        const uint32_t r = b.row[f];
-        fs.acc[cell] = r == TXV_NONE ? 0u : r + 1u;
-      }
-      if (lane == 0) {
-        fs.set_sum[s] = total;
-        if (prior < fs.quorum && total >= fs.quorum) b.ev_flag[cross] = 1;   // the commit event
-      }
+    }
+    // the accepted-vote cells (after every vote of the batch read acc in the resolve step)
+    for (uint32_t v = lane; v < fs.n_vals; v += 64) {
+      TallyCell& c = row[v];
+      if (c.acc == 0 && cand_of(c.cand, b.stamp) != TXV_NONE) c.acc = c.row;
+    }
+    if (lane == 0) {
+      fs.set_sum[s] = total;
+      fs.set_cross[s] = cross;
+      if (prior < fs.quorum && total >= fs.quorum) b.ev_flag[cross] = 1;   // the commit event
     }
   }
 }
@@ -736,21 +730,61 @@ struct EventAct {
   }
 };
 
-// final statuses into mapped host memory (coalesced), then the batch summary
-__global__ void __launch_bounds__(256) txv_k_status_out(FlowState fs, FlowBatch b, uint32_t nb) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < b.n) {
+// final statuses into mapped host memory (an ADDED vote at or after its set's crossing index
+// fires), and the number of commit events per scan block (items b*1024 + k*256 + t, as
+// txv_k_scan_count) for the event compaction
+__global__ void __launch_bounds__(256) txv_k_status_out(FlowState fs, FlowBatch b) {
+  const uint32_t base = blockIdx.x * kScanItems + threadIdx.x;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = base + 256u * k;
+    if (i >= b.n) continue;
     const uint8_t p = b.pre[i];
-    b.status_host[i] = p == TXV_S_PENDING ? (b.set[i] == TXV_NONE ? (uint8_t)TXV_S_INVALID_SIGNATURE : b.status[i]) : p;
+    uint8_t st = p;
+    if (p == TXV_S_PENDING) {
+      const uint32_t s = b.set[i];
+      if (s == TXV_NONE) {
+        st = TXV_S_INVALID_SIGNATURE;
+      } else {
+        st = b.status[i];
+        if (st == TXV_S_ADDED) {
+          const uint32_t x = fs.set_cross[s];
+          if (x != TXV_NO_CROSS && i >= x) st |= TXV_S_FIRED;
+        }
+      }
+    }
+    b.status_host[i] = st;
+    c += b.ev_flag[i] != 0;
   }
-  if (i == 0) {
-    FlowSummary s;
-    s.n_sets = fs.ctr->n_sets;
-    s.n_events = b.blk[nb];
-    s.arena_used = fs.ctr->arena_used;
-    s.err = fs.ctr->err;
-    s.key_used = fs.ctr->key_used;
-    *b.summary_host = s;
+  uint32_t total;
+  (void)block_excl_scan(c, &total);
+  if (threadIdx.x == 0) b.blk[blockIdx.x] = total;
+}
+
+// the event compaction's scan top, then the batch summary into mapped host memory
+__global__ void __launch_bounds__(256) txv_k_event_top(FlowState fs, FlowBatch b, uint32_t nb) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nb + 255) / 256;
+  const uint32_t lo = min(t * per, nb), hi = min(lo + per, nb);
+  uint32_t s = 0;
+  for (uint32_t j = lo; j < hi; ++j) s += b.blk[j];
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, &total);
+  for (uint32_t j = lo; j < hi; ++j) {
+    const uint32_t v = b.blk[j];
+    b.blk[j] = run;
+    run += v;
+  }
+  if (t == 0) {
+    b.blk[nb] = total;
+    FlowSummary sm;
+    sm.n_sets = fs.ctr->n_sets;
+    sm.n_events = total;
+    sm.arena_used = min(fs.ctr->arena_used, fs.max_accepted);
+    sm.err = fs.ctr->err;
+    sm.key_used = fs.ctr->key_used;
+    *b.summary_host = sm;
   }
 }
 
@@ -759,13 +793,22 @@ __global__ void __launch_bounds__(256) txv_k_reset_sets(FlowState fs, int keep_i
   const uint32_t ns = fs.ctr->n_sets;
   const uint64_t cells = (uint64_t)ns * fs.n_vals;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += stride) fs.acc[c] = 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += stride)
+    *reinterpret_cast<uint64_t*>(&fs.cell[c].acc) = 0;   // acc and row
   for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < ns; s += stride) {
     fs.set_sum[s] = 0;
     if (!keep_ids) {
       SetEntry& e = fs.tab[fs.set_entry[s]];
       e.h = 0; e.len = 0; e.key_off = 0; e.first = 0; e.id = 0; e.state = TXV_SE_EMPTY;
     }
+  }
+}
+
+__global__ void __launch_bounds__(256) txv_k_init_cells(FlowState fs, uint64_t cells, int clear_acc) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += stride) {
+    fs.cell[c].cand = ~0ull;                          // stamp 0: no candidate
+    if (clear_acc) *reinterpret_cast<uint64_t*>(&fs.cell[c].acc) = 0;
   }
 }
 
@@ -814,7 +857,7 @@ __global__ void __launch_bounds__(256) txv_k_gather(FlowState fs, const uint32_t
   if (!out_rows) return;
   AccRow r{};
   r.val = TXV_NONE;
-  const uint32_t a = ok ? fs.acc[(size_t)id * fs.n_vals + v] : 0u;
+  const uint32_t a = ok ? fs.cell[(size_t)id * fs.n_vals + v].acc : 0u;
   if (a) {
     const size_t M = fs.max_accepted, k = a - 1;
     for (int j = 0; j < 16; ++j) r.sig[j] = fs.arena_sig[j * M + k];
@@ -877,7 +920,7 @@ hipError_t compact(Pred p, Act act, uint32_t n, uint32_t* blk, hipStream_t st) {
 
 // Experiment builds only (tools/profile/build_variant_flow.sh -DTXV_EXP_SKIP): TXV_EXP_SKIP=<mask>
 // leaves flow kernels out of every chain (wrong results; for attributing co-running costs):
-// 1 tally_min, 2 resolve, 4 ADDED compaction, 8 touched compaction, 16 cross, 32 events + status,
+// 1 tally_min, 2 resolve, 16 cross, 32 status + events,
 // 64 route_key, 128 new-id compaction
 #ifdef TXV_EXP_SKIP
 uint32_t exp_skip() {
@@ -913,25 +956,21 @@ hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t
 }
 
 // sets_bound: an upper bound on the set ids in use after this batch (the host's count as of
-// the last waited batch + this batch's votes, at most max_txs): the touched-set scan covers it
+// the last waited batch + this batch's votes, at most max_txs): the crossing step covers it
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st) {
   const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
   if (!TXV_SKIP(1)) hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
-  if (g && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3(g), dim3(256), 0, st, *fs, *b);
-  hipError_t e = TXV_SKIP(4) ? hipSuccess : compact(AddedPred{*b}, AddedAct{*fs, *b}, b->n, b->blk, st);
-  if (e != hipSuccess) return e;
+  if (b->n && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3((b->n + 1023) / 1024), dim3(1024), 0, st, *fs, *b);
   sets_bound = std::min(sets_bound, fs->max_txs);
-  const uint32_t nb_sets = (sets_bound + kScanItems - 1) / kScanItems;
-  e = TXV_SKIP(8) ? hipSuccess : compact(TouchedPred{*fs, *b}, TouchedAct{*fs}, sets_bound, fs->touched_blk, st);
-  if (e != hipSuccess) return e;
-  // persistent waves over the touched list: one wave per set (up to 8 waves per SIMD)
+  // persistent waves over the set ids: one wave per set (up to 8 waves per SIMD)
   const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::min(sets_bound, b->n) + 3) / 4, 2048));
-  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, nb, nb_sets);
+  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, sets_bound);
   if (TXV_SKIP(32)) return hipGetLastError();
-  e = compact(EventPred{*b}, EventAct{*fs, *b}, b->n, b->blk, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(txv_k_status_out, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
+  hipLaunchKernelGGL(txv_k_status_out, dim3(nb ? nb : 1), dim3(256), 0, st, *fs, *b);
+  hipLaunchKernelGGL(txv_k_event_top, dim3(1), dim3(256), 0, st, *fs, *b, nb);
+  if (nb) hipLaunchKernelGGL((txv_k_scan_apply<EventPred, EventAct>), dim3(nb), dim3(256), 0, st, EventPred{*b},
+                             EventAct{*fs, *b}, b->n, b->blk);
   return hipGetLastError();
 }
 
@@ -951,6 +990,13 @@ hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st) {
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st) {
   hipLaunchKernelGGL(txv_k_reset_sets, dim3(1024), dim3(256), 0, st, *fs, keep_ids);
   hipLaunchKernelGGL(txv_k_reset_counters, dim3(1), dim3(1), 0, st, *fs, keep_ids);
+  return hipGetLastError();
+}
+
+hipError_t txv_flow_init_cells(const FlowState* fs, uint64_t cells, int clear_acc, hipStream_t st) {
+  if (!cells) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_init_cells, dim3((uint32_t)std::min<uint64_t>((cells + 255) / 256, 8192)), dim3(256), 0, st,
+                     *fs, cells, clear_acc);
   return hipGetLastError();
 }
 

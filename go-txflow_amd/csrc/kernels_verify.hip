@@ -510,6 +510,15 @@ __device__ __forceinline__ ge_ext k1b_walk(const uint32_t* tb, const uint32_t* t
 #ifndef TXV_V4_WAVES
 #define TXV_V4_WAVES 2
 #endif
+// Experiment builds only (time attribution inside K1b; wrong verdicts): TXV_EXP_NO_TAIL=1 skips
+// the shared inversion and the encodings (the walks' results still go to the park buffer),
+// TXV_EXP_NO_WALK=1 replaces each walk by a point made of the scalar words (the tail alone)
+#ifndef TXV_EXP_NO_TAIL
+#define TXV_EXP_NO_TAIL 0
+#endif
+#ifndef TXV_EXP_NO_WALK
+#define TXV_EXP_NO_WALK 0
+#endif
 #ifdef TXV_K1B_VGPRS
 #define TXV_K1B_VGPR_ATTR __attribute__((amdgpu_num_vgpr(TXV_K1B_VGPRS)))
 #else
@@ -570,7 +579,13 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
           s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
           k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
         }
+#if TXV_EXP_NO_WALK
+        (void)wbuf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { R.X.v[j] = s[j] | 1u; R.Y.v[j] = k[j] | 2u; R.Z.v[j] = s[j] ^ k[j] ^ 5u; R.T.v[j] = 0; }
+#else
         R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+#endif
       }
 #else
       if (act >> h & 1u) {
@@ -596,6 +611,10 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
         }
       }
     }
+#if TXV_EXP_NO_TAIL
+    if (act & 1u) a.ok_out[(g & ~63u) * V + (g & 63u)] = P.v[0] == 0x12345u;
+    continue;
+#endif
     fe inv = verify_invert(P);
 #pragma unroll 1
     for (int h = V - 1; h >= 0; --h) {

@@ -269,11 +269,15 @@ struct txv_pool {
   }
 };
 
+int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                         uint8_t* keys_out, const std::function<void()>& overlap);   // runtime.cpp
+
 namespace {
 
-int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off) {
+int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
+               const std::function<void()>& overlap = nullptr) {
   p->keys.resize((size_t)v->n * 32 + 32);
-  return txv_sig_keys(ctx, v, sig_full, sig_full_off, p->keys.data());
+  return txv_sig_keys_overlap(ctx, v, sig_full, sig_full_off, p->keys.data(), overlap);
 }
 
 }  // namespace
@@ -510,26 +514,38 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
     auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
     auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
-    std::vector<std::pair<uint64_t, uint64_t>> pairs;      // (next occurrence, occurrence)
-    for (uint32_t j = 0; j < n; ++j) {
-      const uint32_t i = S.order[j];
-      if (S.prevj[j] >= 0) pairs.emplace_back(pos2(i), pos2(S.order[S.prevj[j]]));
-      else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) pairs.emplace_back(pos2(i), init2(S.cnodej[j]));
-    }
-    std::sort(pairs.begin(), pairs.end());
-    std::sort(far.begin(), far.end());                     // by position = batch order
-    const uint64_t M = 2 * (L0 + na) + 2;
+    // pairs (next occurrence, occurrence) of consecutive pushes of one key, per partition
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> pp(kParts);
+    per_part([&](uint32_t q) {
+      for (uint32_t j = S.cnt[q]; j < S.cnt[q + 1]; ++j) {
+        const uint32_t i = S.order[j];
+        if (S.prevj[j] >= 0) pp[q].emplace_back(pos2(i), pos2(S.order[S.prevj[j]]));
+        else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) pp[q].emplace_back(pos2(i), init2(S.cnodej[j]));
+      }
+    });
+    std::vector<std::pair<uint64_t, uint64_t>> pairs;
+    for (auto& v : pp) pairs.insert(pairs.end(), v.begin(), v.end());
+    std::sort(pairs.begin(), pairs.end());                 // by next occurrence: the sweep order
+    std::vector<uint64_t> starts(pairs.size());            // Fenwick tree over the distinct starts
+    for (size_t k = 0; k < pairs.size(); ++k) starts[k] = pairs[k].second;
+    std::sort(starts.begin(), starts.end());
+    starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+    const size_t M = starts.size();
     std::vector<uint32_t> fen(M + 1, 0);
+    std::sort(far.begin(), far.end());                     // by position = batch order
     uint32_t added = 0;
     size_t pi = 0;
     for (uint32_t i : far) {
       const uint32_t j = S.pos[i];
       const uint64_t e = pos2(i);
-      for (; pi < pairs.size() && pairs[pi].first < e; ++pi, ++added)
-        for (uint64_t x = pairs[pi].second + 1; x <= M; x += x & (~x + 1)) ++fen[x];
+      for (; pi < pairs.size() && pairs[pi].first < e; ++pi, ++added) {
+        const size_t x0 = std::lower_bound(starts.begin(), starts.end(), pairs[pi].second) - starts.begin() + 1;
+        for (size_t x = x0; x <= M; x += x & (~x + 1)) ++fen[x];
+      }
       const uint64_t p2 = S.prevj[j] >= 0 ? pos2(S.order[S.prevj[j]]) : init2(S.cnodej[j]);
       uint32_t upto = 0;                                   // pairs starting at or before p
-      for (uint64_t x = p2 + 1; x > 0; x -= x & (~x + 1)) upto += fen[x];
+      for (size_t x = std::upper_bound(starts.begin(), starts.end(), p2) - starts.begin(); x > 0; x -= x & (~x + 1))
+        upto += fen[x];
       const uint64_t nested = added - upto;
       const uint64_t window = (e - p2) / 2 - 1;           // pushes strictly between (p is exact here)
       S.decj[j] = window - nested < C ? 2 : 1;
@@ -819,14 +835,15 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   const auto t0 = std::chrono::steady_clock::now();
-  int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
+  // TxVote.Size() of every vote on the worker threads (order-independent) while the GPU hashes
+  p->sizes.resize(v->n);
+  int r = batch_keys(p, ctx, v, sig_full, sig_full_off, [&] {
+    txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
+    });
+  });
   if (r) return r;
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
-  // TxVote.Size() of every vote on the worker threads (order-independent)
-  p->sizes.resize(v->n);
-  txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
-  });
   if (getenv("TXV_PROFILE_HOST"))
     fprintf(stderr, "[txv pool] keys+sizes=%.3fms n=%u\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);

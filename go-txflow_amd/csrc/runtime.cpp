@@ -91,7 +91,7 @@ struct Slot {
   uint64_t run_seq = 0;            // txv_ctx::run_seq of the slot's last run (orders its summary)
   uint64_t counted = 0;            // votes of this slot's unfetched runs, included in txv_ctx::unfetched
   // AddVote derived columns and scan scratch
-  uint32_t *d_entry = nullptr, *d_row = nullptr, *d_blk = nullptr;
+  uint32_t *d_entry = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
@@ -176,11 +176,9 @@ struct txv_ctx {
   // accepted-vote arena, counters
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
   uint8_t* d_keys = nullptr; uint64_t keys_cap = 0;
-  uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_stamp = nullptr, *d_bitmap = nullptr;
+  uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_stamp = nullptr, *d_set_cross = nullptr, *d_bitmap = nullptr;
   int64_t* d_set_sum = nullptr;
-  uint32_t* d_acc = nullptr;
-  uint64_t* d_cand = nullptr;
-  uint32_t *d_touched = nullptr, *d_touched_blk = nullptr;
+  TallyCell* d_cells = nullptr;
   uint32_t *d_arena_sig = nullptr, *d_arena_nanos = nullptr, *d_arena_val = nullptr, *d_arena_txkey = nullptr;
   int64_t *d_arena_height = nullptr, *d_arena_sec = nullptr;
   uint64_t* d_arena_seq = nullptr;
@@ -333,7 +331,7 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_sig_len, npad)) || (r = dalloc(c, &s.d_sig_len, npad)) ||
       (r = halloc(c, &s.h_nil, npad)) || (r = dalloc(c, &s.d_nil, npad)) ||
       (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
-      (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_row, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
+      (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
       (r = dalloc(c, &s.d_ev_flag, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
     return r;
@@ -346,11 +344,10 @@ FlowState flow_state(const txv_ctx* c) {
   f.tab = c->d_tab; f.tab_mask = c->tab_mask; f.max_txs = c->cfg.max_txs;
   f.keys = c->d_keys; f.keys_cap = c->keys_cap;
   f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_stamp = c->d_set_stamp;
-  f.acc = c->d_acc; f.cand = c->d_cand;
+  f.cell = c->d_cells; f.set_cross = c->d_set_cross;
   f.arena_sig = c->d_arena_sig; f.arena_height = c->d_arena_height; f.arena_sec = c->d_arena_sec;
   f.arena_nanos = reinterpret_cast<int32_t*>(c->d_arena_nanos); f.arena_val = c->d_arena_val;
   f.arena_seq = c->d_arena_seq; f.arena_txkey = c->d_arena_txkey;
-  f.touched = c->d_touched; f.touched_blk = c->d_touched_blk;
   f.ctr = c->d_ctr; f.n_vals = c->n_vals; f.max_accepted = c->max_accepted; f.quorum = c->quorum;
   f.power = c->d_power; f.val_addr = c->d_addr; f.addr_slots = c->d_addr_slots; f.addr_mask = c->addr_mask;
   f.hash_seed = c->hash_seed;
@@ -371,19 +368,20 @@ int alloc_tally(txv_ctx* c) {
   c->keys_cap = c->cfg.key_arena_bytes ? c->cfg.key_arena_bytes : std::max<uint64_t>((uint64_t)c->cfg.max_txs * 16, 1u << 20);
   int r;
   const size_t M = c->max_accepted;
-  if ((r = dalloc(c, &c->d_acc, cells)) || (r = dalloc(c, &c->d_cand, cells)) ||
+  if ((r = dalloc(c, &c->d_cells, cells)) || (r = dalloc(c, &c->d_set_cross, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_arena_sig, 16 * M)) || (r = dalloc(c, &c->d_arena_height, M)) ||
       (r = dalloc(c, &c->d_arena_sec, M)) || (r = dalloc(c, &c->d_arena_nanos, M)) || (r = dalloc(c, &c->d_arena_val, M)) ||
       (r = dalloc(c, &c->d_arena_seq, M)) || (r = dalloc(c, &c->d_arena_txkey, 8 * M)) ||
-      (r = dalloc(c, &c->d_touched, c->cfg.max_txs)) || (r = dalloc(c, &c->d_touched_blk, (c->cfg.max_txs + 1023) / 1024 + 1)) ||
       (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_set_stamp, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_set_txkey, (size_t)c->cfg.max_txs * 8)) ||
       (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_tab, tab)) ||
       (r = dalloc(c, &c->d_keys, (uint64_t)c->cfg.max_txs * TXV_KEY_SLOT + c->keys_cap)) || (r = dalloc(c, &c->d_ctr, 1)))
     return r;
-  HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->d_cand, 0xFF, cells * 8, c->stream));   // stamp 0: no candidate
+  {
+    const FlowState fs = flow_state(c);
+    HIP_TRY(c, txv_flow_init_cells(&fs, cells, 1, c->stream));   // no candidate, no accepted vote
+  }
   HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_set_stamp, 0, (size_t)c->cfg.max_txs * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, tab * sizeof(SetEntry), c->stream));
@@ -401,7 +399,10 @@ int alloc_tally(txv_ctx* c) {
 int reset_tally(txv_ctx* c, bool keep_ids = false) {
   if (c->poisoned && !keep_ids) {   // a capacity overflow left partial state: clear everything
     const uint64_t cells = (uint64_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1);
-    HIP_TRY(c, hipMemsetAsync(c->d_acc, 0, cells * 4, c->stream));
+    {
+      const FlowState fs = flow_state(c);
+      HIP_TRY(c, txv_flow_init_cells(&fs, cells, 1, c->stream));
+    }
     HIP_TRY(c, hipMemsetAsync(c->d_set_sum, 0, (size_t)c->cfg.max_txs * 8, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_tab, 0, ((size_t)c->tab_mask + 1) * sizeof(SetEntry), c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_ctr, 0, sizeof(FlowCounters), c->stream));
@@ -754,7 +755,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.addr = s.d_addr; b.addr_len = s.d_addr_len; b.sig_raw = s.d_sigraw; b.sig_len = s.d_sig_len;
   b.nil = s.has_nil ? s.d_nil : nullptr; b.txkey = s.has_txkey ? s.d_txkey : nullptr;
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
-  b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status; b.row = s.d_row;
+  b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
   b.ev_flag = s.d_ev_flag; b.blk = s.d_blk;
   b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
   return b;
@@ -787,7 +788,8 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   int r;
   if ((r = ensure_park(c))) return r;
   if (c->stamp == 0xFFFFFFFEu) {   // stamps are about to wrap: forget every candidate first
-    HIP_TRY(c, hipMemsetAsync(c->d_cand, 0xFF, (size_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1) * 8, c->stream));
+    const FlowState fs0 = flow_state(c);
+    HIP_TRY(c, txv_flow_init_cells(&fs0, (uint64_t)c->cfg.max_txs * std::max<uint32_t>(c->n_vals, 1), 0, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_set_stamp, 0, (size_t)c->cfg.max_txs * 4, c->stream));
     c->stamp = 0;
   }
@@ -1173,14 +1175,14 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
     hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey);
-    dfree(s.d_entry); dfree(s.d_row); dfree(s.d_blk); dfree(s.d_ev_flag); hfree(s.h_ev); hfree(s.h_sum);
+    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
-  dfree(c->d_acc); dfree(c->d_cand); dfree(c->d_set_sum); dfree(c->d_touched); dfree(c->d_touched_blk);
+  dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
   dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_bitmap);
   dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
@@ -1921,8 +1923,22 @@ void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint
 
 extern "C" {
 
+}  // extern "C"
+int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                         uint8_t* keys_out, const std::function<void()>& overlap);
+extern "C" {
+
 int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
                  uint8_t* keys_out) {
+  return txv_sig_keys_overlap(c, v, sig_full, sig_full_off, keys_out, nullptr);
+}
+
+}  // extern "C"
+
+// txv_sig_keys, running `overlap` (host work of the caller's, e.g. the pool's TxVote.Size pass)
+// while the key stream hashes
+int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
+                         uint8_t* keys_out, const std::function<void()>& overlap) {
   if (!c || !v || (v->n && (!v->sig || !v->sig_len || !keys_out))) return TXV_EINVAL;
   const uint32_t n = v->n;
   for (uint32_t i = 0; i < n; ++i)
@@ -1949,6 +1965,7 @@ int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const 
   HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
   HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->key_stream));
   HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->key_stream));
+  if (overlap) overlap();
   HIP_TRY(c, hipStreamSynchronize(c->key_stream));
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
@@ -1957,6 +1974,8 @@ int txv_sig_keys(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const 
   }, 8192);
   return TXV_OK;
 }
+
+extern "C" {
 
 // CPUs of the NUMA node the GPU hangs off (sysfs local_cpulist of its PCI function)
 static bool gpu_local_cpuset(int dev, cpu_set_t* out) {

@@ -11,17 +11,20 @@
 //                                         the overflow arena (key_arena_bytes)
 //   per set id  set_entry (table slot), set_txkey [8] u32 (TxKey of the first vote,
 //               service.go:201-207), set_sum i64, set_stamp (last batch that ADDED a vote)
-//   cells       acc [max_txs * n_vals] u32   0 or the accepted vote's arena row + 1 (the
-//                                            reference's `votes` map, vote_set.go:154)
-//               cand[max_txs * n_vals] u64   (~stamp << 32 | arrival index) of the first
-//                                            verified vote of the (set, validator) cell in the
-//                                            batch with that stamp: one atomic min per verified
-//                                            vote, and a stale stamp reads as "none", so the
-//                                            cells are never cleared
+//   cells       TallyCell [max_txs * n_vals], 16 B (one line touch per cell access):
+//                 cand  (~stamp << 32 | arrival index) of the first verified vote of the (set,
+//                       validator) cell in the batch with that stamp: one atomic min per verified
+//                       vote, and a stale stamp reads as "none", so it is never cleared
+//                 acc   0 or the accepted vote's arena row + 1 (the reference's `votes` map,
+//                       vote_set.go:154), written once the batch's crossing step ran
+//                 row   the arena row + 1 the running batch's ADDED vote of the cell took
 //   arena       [max_accepted] rows, column-major (sig [16][rows] u32, height, ts_sec, ts_nanos,
 //               val, seq, TxKey [8][rows]): every accepted vote in full, one row per ADDED vote,
-//               rows handed out by a compaction in arrival order (consecutive rows per wave, so
-//               each column store is one coalesced line per wave)
+//               rows taken by wave-aggregated atomics as the votes are resolved (the rows of a
+//               wave are consecutive, so each column store is one coalesced line per wave; row
+//               order carries no meaning -- the readers order by validator)
+//   set_cross   [max_txs] arrival index at which the set's stake crossed 2/3 in the batch that
+//               last touched it (TXV_NO_CROSS: none): the fired bit of each ADDED vote
 // The commit bitmap is derived from set_sum on demand (txv_commit_bitmap, the packed state).
 //
 // gfx950 has 8 XCDs with private L2s: the only hand-off INSIDE a launch is the set-table insert
@@ -55,6 +58,12 @@
 #define TXV_FERR_TABLE 0x2u     // set table full (probe bound)
 #define TXV_FERR_KEYS 0x4u      // TxHash overflow key arena full
 #define TXV_FERR_ARENA 0x8u     // accepted-vote arena full (max_accepted)
+
+struct TallyCell {              // 16 B, see the header comment
+  uint64_t cand;
+  uint32_t acc;
+  uint32_t row;
+};
 
 // table entry states
 #define TXV_SE_EMPTY 0u
@@ -111,8 +120,8 @@ struct FlowState {
   uint32_t* set_txkey;          // [max_txs][8]
   int64_t* set_sum;             // [max_txs]
   uint32_t* set_stamp;          // [max_txs]
-  uint32_t* acc;                // [max_txs * n_vals]
-  uint64_t* cand;               // [max_txs * n_vals]
+  uint32_t* set_cross;          // [max_txs]
+  TallyCell* cell;              // [max_txs * n_vals]
   uint32_t* arena_sig;          // [16][max_accepted]
   int64_t* arena_height;        // [max_accepted]
   int64_t* arena_sec;
@@ -120,8 +129,6 @@ struct FlowState {
   uint32_t* arena_val;
   uint64_t* arena_seq;
   uint32_t* arena_txkey;        // [8][max_accepted]
-  uint32_t* touched;            // [max_txs] sets that ADDED votes in the running batch
-  uint32_t* touched_blk;        // scan scratch over set ids: [ceil(max_txs / 1024) + 1]
   FlowCounters* ctr;
   uint32_t n_vals, max_accepted;
   int64_t quorum;
@@ -161,7 +168,6 @@ struct FlowBatch {
   uint32_t* set;                // [n] set id
   const uint8_t* ok;            // [n] verify verdicts (1 = valid)
   uint8_t* status;              // [n] tally status of pending votes
-  uint32_t* row;                // [n] arena row of an ADDED vote
   uint8_t* ev_flag;             // [n] this vote's ADDED crossed 2/3 in the batch
   uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
   // outputs in mapped host memory
@@ -184,6 +190,9 @@ hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st);
 // forget every TxVoteSet (keep_ids = 0) or empty them keeping their ids (keep_ids = 1)
 hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);
+// cells of the first `cells` (set, validator) pairs: every candidate forgotten (cand = ~0), and
+// with clear_acc the accepted votes too
+hipError_t txv_flow_init_cells(const FlowState* fs, uint64_t cells, int clear_acc, hipStream_t st);
 hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st);
 // TxHash lookups for the readers: out_id[i] = set id or TXV_NONE
 hipError_t txv_flow_lookup(const FlowState* fs, const uint8_t* keys, const uint32_t* off, const uint32_t* len,

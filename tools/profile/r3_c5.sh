@@ -11,3 +11,6 @@ TXV_PROFILE_HOST=1 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 --n
   > $O/bench.json 2> $O/bench.err || { echo BENCHFAIL; tail $O/bench.err; exit 3; }
 python3 -c "import json;b=json.load(open('$O/bench.json'));print(b['c5_streaming']);print(b['c5_wire'])"
 grep "batch:" $O/bench.err | tail -4
+bash tools/profile/r3_corun.sh ${1:-r3_c5}/corun 255 0 255 || exit 4
+CORUN_LIB=build_exp/notail CORUN_TAG=notail bash tools/profile/r3_corun.sh ${1:-r3_c5}/corun 0 || exit 5
+CORUN_LIB=build_exp/nowalk CORUN_TAG=nowalk bash tools/profile/r3_corun.sh ${1:-r3_c5}/corun 0 || exit 6

@@ -6,7 +6,7 @@ TAG=$1; shift
 O=gpurun_out/$TAG
 mkdir -p $O
 for m in "$@"; do
-  TXV_LIB_PATH=$PWD/build_exp/skip/libtxvote.so TXV_EXP_SKIP=$m timeout -k 10 200 python3 -u tools/debug/corun_exp.py \
-    >> $O/corun.jsonl 2> $O/corun_$m.err || { echo "FAIL $m"; tail -5 $O/corun_$m.err; exit 1; }
+  TXV_LIB_PATH=$PWD/${CORUN_LIB:-build_exp/skip}/libtxvote.so TXV_EXP_SKIP=$m timeout -k 10 200 python3 -u tools/debug/corun_exp.py \
+    >> $O/corun.jsonl 2> $O/corun_${CORUN_TAG:-}$m.err || { echo "FAIL $m"; tail -5 $O/corun_$m.err; exit 1; }
   tail -1 $O/corun.jsonl
 done
