@@ -22,7 +22,7 @@
 // Scheduling fence: keeps the compiler from interleaving independent field multiplies,
 // which buys ILP at the cost of registers; with >= 4 waves per SIMD latency is hidden by
 // the other waves instead (DESIGN.md §K1 register budget).
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TXV_SCHED_FENCE_OFF)   // _OFF: experiment builds
 #define TXV_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define TXV_SCHED_FENCE() ((void)0)

@@ -368,9 +368,7 @@ constexpr uint32_t kAdmitAhead = 16;
 
 uint64_t batch_tab_hash(const Key& k) { uint64_t v; memcpy(&v, k.b + 16, 8); return v ^ (v >> 31); }
 
-bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, uint32_t n, uint64_t sum,
-                 const uint8_t* part, uint8_t* status_out) {
-  if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;   // the bytes cap could bind
+bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, uint32_t n, uint8_t* status_out) {
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
   std::chrono::steady_clock::time_point tp[10];
   int ntp = 0;
@@ -381,10 +379,15 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   const uint64_t C = p->cfg.cache_size, L0 = cache_on ? p->cache.len : 0;
   const uint32_t* sizes = p->sizes.data();
   auto is_push = [&](uint32_t i) { return (int64_t)sizes[i] <= max_tx; };
-  // 0. partition order (stable) and the push index aidx[i] (position L0 + aidx[i] in S), from
-  //    per-chunk histograms
+  p->part.resize(n);
+  uint8_t* part = p->part.data();
+  // 0. per chunk of arrival order: each key's index partition, the summed sizes, per-partition
+  //    counts and pushes; then the stable partition order and the push index aidx[i] (position
+  //    L0 + aidx[i] in S)
   const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
-  S.hist.assign((size_t)P * (kParts + 1), 0);
+  const uint32_t HW = kParts + 2;                          // per chunk: kParts counts, pushes, -
+  S.hist.assign((size_t)P * HW, 0);
+  std::vector<uint64_t> sum_c(P, 0);
   S.order.resize(n); S.pos.resize(n); S.aidx.resize(n);
   auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
@@ -392,12 +395,23 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
     for (uint32_t c = c0; c < c1; ++c) {
       uint32_t lo, hi, pushes = 0;
+      uint64_t sm = 0;
       chunk(c, lo, hi);
-      uint32_t* h = S.hist.data() + (size_t)c * (kParts + 1);
-      for (uint32_t i = lo; i < hi; ++i) { ++h[part[i]]; pushes += is_push(i); }
+      uint32_t* h = S.hist.data() + (size_t)c * HW;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint8_t q = (uint8_t)PartIndex::part(keys[i]);
+        part[i] = q;
+        ++h[q];
+        pushes += is_push(i);
+        sm += sizes[i];
+      }
       h[kParts] = pushes;
+      sum_c[c] = sm;
     }
   }, 1);
+  uint64_t sum = 0;
+  for (uint32_t c = 0; c < P; ++c) sum += sum_c[c];
+  if (p->txs_bytes + (int64_t)sum > (int64_t)p->cfg.max_txs_bytes) return false;   // the bytes cap could bind
   S.cnt.assign(kParts + 1, 0);
   uint32_t na = 0;
   {
@@ -405,7 +419,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     for (uint32_t q = 0; q < kParts; ++q) {
       S.cnt[q] = run;
       for (uint32_t c = 0; c < P; ++c) {
-        uint32_t& h = S.hist[(size_t)c * (kParts + 1) + q];
+        uint32_t& h = S.hist[(size_t)c * HW + q];
         const uint32_t t = h;
         h = run;
         run += t;
@@ -413,7 +427,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     }
     S.cnt[kParts] = run;
     for (uint32_t c = 0; c < P; ++c) {
-      uint32_t& h = S.hist[(size_t)c * (kParts + 1) + kParts];
+      uint32_t& h = S.hist[(size_t)c * HW + kParts];
       const uint32_t t = h;
       h = na;
       na += t;
@@ -423,7 +437,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     for (uint32_t c = c0; c < c1; ++c) {
       uint32_t lo, hi;
       chunk(c, lo, hi);
-      uint32_t* h = S.hist.data() + (size_t)c * (kParts + 1);
+      uint32_t* h = S.hist.data() + (size_t)c * HW;
       uint32_t a = h[kParts];
       for (uint32_t i = lo; i < hi; ++i) {
         const uint32_t j = h[part[i]]++;
@@ -440,41 +454,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   };
   S.prevj.resize(n); S.firstj.resize(n); S.cnodej.resize(n); S.nextj.resize(n); S.decj.resize(n);
   mark();
-  // 1. per partition, in batch order: the previous push of the same key in the batch, the first
-  //    one, and the cache node of a first push whose key is cached (a hash tag beside each slot:
-  //    keys are compared only on a tag match)
-  per_part([&](uint32_t q) {
-    const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
-    uint32_t cap = 16;
-    while (cap < 2 * (hi - lo)) cap *= 2;
-    std::vector<uint64_t> tab(cap, 0);            // (tag << 32) | (j + 1) of the key's last push
-    const FlatIndex& cf = *p->cache_map.p[q];
-    for (uint32_t j = lo; j < hi; ++j) {
-      if (cache_on && j + kAdmitAhead < hi) cf.prefetch(keys[S.order[j + kAdmitAhead]]);
-      const uint32_t i = S.order[j];
-      S.cnodej[j] = -1;
-      S.nextj[j] = -1;
-      if (!is_push(i)) { S.prevj[j] = -2; S.firstj[j] = (int32_t)j; continue; }
-      const uint64_t hv = batch_tab_hash(keys[i]);
-      const uint64_t tag = (hv >> 32) | 1u;
-      size_t sl = hv & (cap - 1);
-      for (; tab[sl]; sl = (sl + 1) & (cap - 1))
-        if ((tab[sl] >> 32) == tag && keys[S.order[(uint32_t)tab[sl] - 1]] == keys[i]) break;
-      if (tab[sl]) {
-        const uint32_t pj = (uint32_t)tab[sl] - 1;
-        S.prevj[j] = (int32_t)pj;
-        S.firstj[j] = S.firstj[pj];
-        S.nextj[pj] = (int32_t)j;
-      } else {
-        S.prevj[j] = -1;
-        S.firstj[j] = (int32_t)j;
-        if (cache_on) S.cnodej[j] = cf.find(keys[i]);
-      }
-      tab[sl] = (tag << 32) | (j + 1);
-    }
-  });
-  mark();
-  // 2. front ranks: only the first min(L0, pushes) cache entries can be evicted by this batch
+  // 1. front ranks: only the first min(L0, pushes) cache entries can be evicted by this batch
   if (evict) {
     if (S.qpos.size() < p->cache.nodes.size()) S.qpos.resize(p->cache.nodes.size(), -1);
     const uint64_t F = std::min<uint64_t>(L0, na);
@@ -486,29 +466,54 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     }
   }
   mark();
-  // 3. decisions, per partition position
-  std::vector<uint32_t> far;                      // arrival indices
-  std::mutex far_mu;
-  txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-    std::vector<uint32_t> mine;
+  // 2. per partition, in batch order: the previous push of the same key in the batch, the first
+  //    one, the cache node of a first push whose key is cached (a hash tag beside each slot: keys
+  //    are compared only on a tag match), and the decision (1 miss, 2 hit, 3 far: counted below)
+  std::vector<std::vector<uint32_t>> far_q(kParts);
+  per_part([&](uint32_t q) {
+    const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
+    uint32_t cap = 16;
+    while (cap < 2 * (hi - lo)) cap *= 2;
+    std::vector<uint64_t> tab(cap, 0);            // (tag << 32) | (j + 1) of the key's last push
+    const FlatIndex& cf = *p->cache_map.p[q];
     for (uint32_t j = lo; j < hi; ++j) {
+      if (cache_on && j + kAdmitAhead < hi) cf.prefetch(keys[S.order[j + kAdmitAhead]]);
       const uint32_t i = S.order[j];
+      S.cnodej[j] = -1;
+      S.nextj[j] = -1;
+      if (!is_push(i)) { S.prevj[j] = -2; S.firstj[j] = (int32_t)j; S.decj[j] = 0; continue; }
+      const uint64_t hv = batch_tab_hash(keys[i]);
+      const uint64_t tag = (hv >> 32) | 1u;
+      size_t sl = hv & (cap - 1);
+      for (; tab[sl]; sl = (sl + 1) & (cap - 1))
+        if ((tab[sl] >> 32) == tag && keys[S.order[(uint32_t)tab[sl] - 1]] == keys[i]) break;
       uint8_t d;
-      if (S.prevj[j] == -2) d = 0;
-      else if (!cache_on) d = 1;
-      else if (S.prevj[j] >= 0) d = (!evict || S.aidx[i] - S.aidx[S.order[S.prevj[j]]] - 1 < C) ? 2 : 3;
-      else if (S.cnodej[j] >= 0) {
-        const int32_t r = evict ? S.qpos[S.cnodej[j]] : -1;
-        d = (r < 0 || L0 + S.aidx[i] - (uint64_t)r - 1 < C) ? 2 : 3;
-      } else d = 1;
+      if (tab[sl]) {
+        const uint32_t pj = (uint32_t)tab[sl] - 1;
+        S.prevj[j] = (int32_t)pj;
+        S.firstj[j] = S.firstj[pj];
+        S.nextj[pj] = (int32_t)j;
+        d = !cache_on ? 1 : ((!evict || S.aidx[i] - S.aidx[S.order[pj]] - 1 < C) ? 2 : 3);
+      } else {
+        S.prevj[j] = -1;
+        S.firstj[j] = (int32_t)j;
+        d = 1;
+        if (cache_on) {
+          const int32_t cn = cf.find(keys[i]);
+          S.cnodej[j] = cn;
+          if (cn >= 0) {
+            const int32_t r = evict ? S.qpos[cn] : -1;
+            d = (r < 0 || L0 + S.aidx[i] - (uint64_t)r - 1 < C) ? 2 : 3;
+          }
+        }
+      }
+      tab[sl] = (tag << 32) | (j + 1);
       S.decj[j] = d;
-      if (d == 3) mine.push_back(i);
-    }
-    if (!mine.empty()) {
-      std::lock_guard<std::mutex> g(far_mu);
-      far.insert(far.end(), mine.begin(), mine.end());
+      if (d == 3) far_q[q].push_back(i);
     }
   });
+  std::vector<uint32_t> far;
+  for (auto& v : far_q) far.insert(far.end(), v.begin(), v.end());
   mark();
   if (!far.empty()) {
     // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
@@ -554,7 +559,8 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   if (evict)
     for (int32_t e : S.qtouched) S.qpos[e] = -1;
   mark();
-  // 4. statuses in arrival order, the Size cap's cut (only when the batch could reach it)
+  // 3. statuses in arrival order, the Size cap's cut (only when the batch could reach it); the
+  //    admitted votes' pool nodes written and linked in the same passes
   S.dec.resize(n); S.adm.resize(n);
   uint32_t m = n;
   uint64_t admitted = 0, admitted_bytes = 0;
@@ -563,7 +569,9 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     if (d == 2) return TXV_POOL_ERR_IN_CACHE;
     return (!sizes[i] && wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
   };
-  if ((int64_t)p->txs.len + (int64_t)na < (int64_t)p->cfg.size) {
+  std::vector<uint64_t> base_c(P, 0);
+  const bool may_cut = (int64_t)p->txs.len + (int64_t)na >= (int64_t)p->cfg.size;
+  if (!may_cut) {
     std::vector<uint64_t> cnt_c(P, 0), bytes_c(P, 0);
     txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
       for (uint32_t c = c0; c < c1; ++c) {
@@ -581,16 +589,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
         bytes_c[c] = b;
       }
     }, 1);
-    std::vector<uint64_t> base_c(P, 0);
     for (uint32_t c = 0; c < P; ++c) { base_c[c] = admitted; admitted += cnt_c[c]; admitted_bytes += bytes_c[c]; }
-    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
-      for (uint32_t c = c0; c < c1; ++c) {
-        uint32_t lo, hi;
-        chunk(c, lo, hi);
-        int32_t a = (int32_t)base_c[c];
-        for (uint32_t i = lo; i < hi; ++i) S.adm[i] = status_out[i] == TXV_POOL_OK ? a++ : -1;
-      }
-    }, 1);
   } else {
     for (uint32_t i = 0; i < n; ++i) {
       if ((int64_t)p->txs.len + (int64_t)admitted >= (int64_t)p->cfg.size) { m = i; break; }
@@ -606,8 +605,41 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       for (uint32_t i = m; i < n; ++i) { S.dec[i] = 0; S.adm[i] = -1; }
     }
   }
+  const uint32_t A = (uint32_t)admitted;
+  const int32_t old_tail = p->txs.tail;
+  if (A) {
+    next_indices(p->txs, A, p->idx_t);
+    p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
+  }
+  auto write_node = [&](uint32_t i, uint32_t a) {
+    p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[i], sizes[i], a ? p->idx_t[a - 1] : old_tail,
+                                              a + 1 < A ? p->idx_t[a + 1] : -1};
+  };
+  if (!may_cut) {
+    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+      for (uint32_t c = c0; c < c1; ++c) {
+        uint32_t lo, hi;
+        chunk(c, lo, hi);
+        uint32_t a = (uint32_t)base_c[c];
+        for (uint32_t i = lo; i < hi; ++i) {
+          if (status_out[i] == TXV_POOL_OK) { S.adm[i] = (int32_t)a; write_node(i, a); ++a; }
+          else S.adm[i] = -1;
+        }
+      }
+    }, 1);
+  } else {
+    for (uint32_t i = 0; i < m; ++i)
+      if (S.adm[i] >= 0) write_node(i, (uint32_t)S.adm[i]);
+  }
+  if (A) {                                                 // addTx: txs.PushBack in arrival order
+    if (old_tail >= 0) p->txs.nodes[old_tail].next = p->idx_t[0]; else p->txs.head = p->idx_t[0];
+    p->txs.tail = p->idx_t[A - 1];
+    p->txs.len += A;
+    const size_t nf = p->txs.free_.size();
+    p->txs.free_.resize(nf - std::min<size_t>(nf, A));
+  }
   mark();
-  // 5. the cache: the C most recent distinct keys of S up to the cut, in recency order
+  // 4. the cache: the C most recent distinct keys of S up to the cut, in recency order
   if (cache_on) {
     std::vector<uint32_t> last;                            // pushes that are their key's last before m
     last.reserve(na);
@@ -692,15 +724,9 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     }
   }
   mark();
-  // 6. addTx for the admitted votes in arrival order (txsMap.Store overwrites)
-  if (admitted) {
-    const uint32_t A = (uint32_t)admitted;
-    next_indices(p->txs, A, p->idx_t);
-    p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
-    txv_host_parallel_for(ctx, m, [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t i = lo; i < hi; ++i)
-        if (S.adm[i] >= 0) p->txs.nodes[p->idx_t[S.adm[i]]] = KeyList::Node{keys[i], sizes[i], -1, -1};
-    });
+  // 5. txsMap.Store of the admitted votes (batch order within each partition: a key admitted
+  //    twice keeps its later node, as the sequential Store does)
+  if (A) {
     per_part([&](uint32_t q) {
       FlatIndex& f = *p->txs_map.p[q];
       const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
@@ -710,14 +736,13 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
         if (S.adm[i] >= 0) f.put(keys[i], p->idx_t[S.adm[i]]);
       }
     });
-    link_appended(ctx, p->txs, p->idx_t, A);
     p->txs_bytes += (int64_t)admitted_bytes;
   }
   mark();
   if (prof) {
     auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    fprintf(stderr, "[txv pool] batch: order=%.3f scan=%.3f front=%.3f decide=%.3f far(%zu)=%.3f status=%.3f cache=%.3f txs=%.3f ms\n",
-            ms(0), ms(1), ms(2), ms(3), far.size(), ms(4), ms(5), ms(6), ms(7));
+    fprintf(stderr, "[txv pool] batch: order=%.3f front=%.3f scan+decide=%.3f far(%zu)=%.3f status+nodes=%.3f cache=%.3f txs=%.3f ms\n",
+            ms(0), ms(1), ms(2), far.size(), ms(3), ms(4), ms(5), ms(6));
   }
   return true;
 }
@@ -756,21 +781,7 @@ namespace {
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
   const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
-  // for the batch path: the summed sizes and each key's index partition
-  const bool fast = n >= 4096;
-  std::atomic<uint64_t> sum_a{0};
-  if (fast) {
-    p->part.resize(n);
-    txv_host_parallel_for(ctx, n, [&](uint32_t lo, uint32_t hi) {
-      uint64_t sm = 0;
-      for (uint32_t i = lo; i < hi; ++i) {
-        sm += p->sizes[i];
-        p->part[i] = (uint8_t)PartIndex::part(keys[i]);
-      }
-      sum_a += sm;
-    });
-  }
-  if (fast && batch_check(p, ctx, p->bs, keys, n, sum_a.load(), p->part.data(), status_out)) {
+  if (n >= 4096 && batch_check(p, ctx, p->bs, keys, n, status_out)) {
     if (getenv("TXV_PROFILE_HOST")) {
       const auto t2 = std::chrono::steady_clock::now();
       fprintf(stderr, "[txv pool] batch-check=%.3fms n=%u\n", std::chrono::duration<double, std::milli>(t2 - t1).count(), n);

@@ -165,6 +165,8 @@ def lib():
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
+            if os.environ.get("TXV_LIB_PATH") and not hasattr(L, name):
+                continue            # an experiment build of an older ABI (A/B runs of tools/)
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
