@@ -547,7 +547,8 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
   // (prefetch 2 additions ahead, 128 KiB); V = 4 runs two blocks per CU: one buffer (64 KiB)
   constexpr int PD = V == 8 ? 2 : 1;
   __shared__ uint4 pf[BLOCK / 64][PD * 8 * 64];
-  uint4* wbuf = pf[threadIdx.x >> 6];
+  // the wave's buffer from a wave-uniform (scalar) index: the LDS-DMA destination goes to M0
+  uint4* wbuf = pf[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
 #endif
   for (uint32_t g = lo + (blockIdx.x / groups) * BLOCK + threadIdx.x; g < hi; g += stride) {
     uint32_t act = 0;

@@ -23,7 +23,8 @@ constexpr int kBlock = 512, kWalks = 8, kNScal = 1 << 16;
 __global__ void __launch_bounds__(kBlock, 2) k_pfwalk(const uint32_t* tb, const uint32_t* ta, uint32_t n_val,
                                                       const uint32_t* scal, uint32_t* out, uint32_t group) {
   __shared__ uint4 pf[kBlock / 64][2 * 8 * 64];
-  uint4* wbuf = pf[threadIdx.x >> 6];
+  // the wave's buffer from a wave-uniform (scalar) index: the LDS-DMA destination goes to M0
+  uint4* wbuf = pf[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
   const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
   uint32_t acc = 0;
 #pragma unroll 1

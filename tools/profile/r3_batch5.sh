@@ -6,6 +6,8 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-r3_batch5}
 mkdir -p $O
 timeout -k 10 120 tools/microbench/walk_rate > $O/walk_rate.json 2>&1 || { echo WALKFAIL; exit 1; }
+timeout -k 10 120 tools/microbench/walk_rate_sgpr > $O/walk_rate_sgpr.json 2>&1 || { echo WALKFAIL; exit 1; }
+cat $O/walk_rate_sgpr.json | tr "\n" " "; echo
 cat $O/walk_rate.json | tr '\n' ' '; echo
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_pool.py tests/test_wire.py \
   > $O/tests.log 2>&1 || { echo TESTFAIL; tail -40 $O/tests.log; exit 2; }
