@@ -655,6 +655,110 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
   }
 }
 
+// The same multi-vote K1b with dynamic work (TXV_K1B_DYNAMIC, the default at V = 8): K1b is ONE
+// round of waves (2 per SIMD for a 1M-vote batch), so with a static split its time is that of the
+// slowest CU -- a CU whose block was dispatched late (a TxFlow kernel of the neighbouring batch
+// still held its slots) or that shares its issue slots with one finishes last.  Here every wave
+// takes its work in chunks of 64 work entries (one vote slot per lane) from the counter of its
+// XCD's eighth of the work list, and from the other eighths once its own is drained: up to V
+// chunks share one inversion, and a wave keeps taking chunks (further inversions) while any are
+// left.  Each slot parks its lane's vote index beside the point (park word 32).
+#ifndef TXV_K1B_DYNAMIC
+#define TXV_K1B_DYNAMIC 1
+#endif
+template <int BLOCK, int WB, int WA, int V>
+__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t n_chunks = (a.n_work + 63u) / 64u;
+  const uint32_t xg = gridDim.x >= 8 ? 8u : 1u, myx = blockIdx.x % xg;
+  const uint32_t per = (n_chunks + xg - 1u) / xg;
+  const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  uint32_t* park = a.park + (size_t)gwave * V * TXV_PARK_WORDS * 64 + lane;
+  constexpr int PD = V == 8 ? 2 : 1;
+  __shared__ uint4 pf[BLOCK / 64][PD * 8 * 64];
+  uint4* wbuf = pf[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  uint32_t src = 0;                      // ranges tried: (myx + src) % xg
+  // the next chunk for this wave (wave-uniform), or 0xFFFFFFFFu when every range is drained
+  auto next_chunk = [&]() -> uint32_t {
+    while (src < xg) {
+      const uint32_t x = (myx + src) % xg;
+      const uint32_t end = min(n_chunks, (x + 1u) * per);
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(a.wctr + 16u * x, 1u);
+      c = x * per + __builtin_amdgcn_readfirstlane(c);
+      if (c < end) return c;
+      ++src;
+    }
+    return 0xFFFFFFFFu;
+  };
+  for (;;) {
+    ge_ext R;
+    fe P;
+    uint32_t h = 0;
+#pragma unroll 1
+    for (; h < (uint32_t)V; ++h) {
+      const uint32_t c = next_chunk();
+      if (c == 0xFFFFFFFFu) break;
+      const uint32_t idx = 64u * c + lane;
+      const uint32_t i = idx < a.n_work ? (a.order ? a.order[idx] : idx) : 0u;
+      const bool on = idx < a.n_work && a.ok_out[i] == 2;
+      uint32_t s[8], k[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
+        k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
+      }
+      // idle lanes walk the digit-0 (identity) entries of validator 0: the cooperative gathers
+      // need every lane of the wave
+      R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+      P = h ? fe_mul(P, R.Z) : R.Z;
+      uint32_t* slot = park + h * TXV_PARK_WORDS * 64;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        slot[j * 64] = R.X.v[j];
+        slot[(8 + j) * 64] = R.Y.v[j];
+        slot[(16 + j) * 64] = P.v[j];
+        slot[(24 + j) * 64] = R.Z.v[j];
+      }
+      slot[32 * 64] = on ? i + 1u : 0u;
+    }
+    if (h == 0) break;
+    fe inv = verify_invert(P);
+#pragma unroll 1
+    for (int hh = (int)h - 1; hh >= 0; --hh) {
+      const uint32_t* slot = park + hh * TXV_PARK_WORDS * 64;
+      fe X, Y, Z, zi;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        X.v[j] = slot[j * 64];
+        Y.v[j] = slot[(8 + j) * 64];
+        Z.v[j] = slot[(24 + j) * 64];
+      }
+      const uint32_t i1 = slot[32 * 64];
+      if (hh) {
+        const uint32_t* prev = park + (hh - 1) * TXV_PARK_WORDS * 64;
+        fe Pp;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Pp.v[j] = prev[(16 + j) * 64];
+        zi = fe_mul(inv, Pp);          // 1/Z_h = P_{h-1} / P_h
+        inv = fe_mul(inv, Z);          // 1/P_{h-1}
+      } else {
+        zi = inv;
+      }
+      if (i1) {
+        const uint32_t i = i1 - 1u;
+        uint32_t enc[8];
+        ge_encode_zinv(enc, X, Y, zi);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) diff |= enc[j] ^ a.sig[(size_t)j * a.n_pad + i];
+        a.ok_out[i] = diff == 0;
+      }
+    }
+    if (h < (uint32_t)V) break;
+  }
+}
+
 // Split mode (lane_votes = 1): the inversion leaves the scalar-multiply kernel.  Under SIMD a
 // wave pays the full inversion chain (254 S + 11 M wave instructions) however many of its
 // lanes' votes it covers, so its per-vote share only falls with more votes per LANE; inside
@@ -919,8 +1023,17 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
   } else if (args->lane_votes == 4) {
     hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 4>), dim3(grid), dim3(B), 0, st, *args);
   } else if (args->lane_votes == 8) {
-    if constexpr (WB >= 24) hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
-    else return hipErrorInvalidValue;
+    if constexpr (WB >= 24) {
+      if (TXV_K1B_DYNAMIC && args->wctr) {
+        const hipError_t e = hipMemsetAsync(args->wctr, 0, 8 * 16 * sizeof(uint32_t), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+      } else {
+        hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+      }
+    } else {
+      return hipErrorInvalidValue;
+    }
   } else if (args->lane_votes == 2 && WB == WA) {
     hipLaunchKernelGGL((txv_k_scalarmult_pair<B, WA>), dim3(grid), dim3(B), 0, st, *args);
   } else {

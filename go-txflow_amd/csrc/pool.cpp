@@ -519,6 +519,37 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
     auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
     auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
+    std::sort(far.begin(), far.end());                     // by position = batch order
+    const size_t F = far.size();
+    std::vector<uint64_t> fe(F), fp(F);                    // each far push's window (p, e)
+    for (size_t f = 0; f < F; ++f) {
+      const uint32_t i = far[f], j = S.pos[i];
+      fe[f] = pos2(i);
+      fp[f] = S.prevj[j] >= 0 ? pos2(S.order[S.prevj[j]]) : init2(S.cnodej[j]);
+    }
+    auto decide_far = [&](size_t f, uint64_t nested) {
+      const uint64_t window = (fe[f] - fp[f]) / 2 - 1;     // pushes strictly between (p is exact here)
+      S.decj[S.pos[far[f]]] = window - nested < C ? 2 : 1;
+    };
+    if (F <= 64) {
+      // few far repeats: every partition counts its nested pairs for each of them directly
+      std::vector<uint32_t> cnt_qf(kParts * F, 0);
+      per_part([&](uint32_t q) {
+        uint32_t* cf = cnt_qf.data() + (size_t)q * F;
+        for (uint32_t j = S.cnt[q]; j < S.cnt[q + 1]; ++j) {
+          uint64_t a, b;                                   // pair (start, next occurrence)
+          if (S.prevj[j] >= 0) { a = pos2(S.order[S.prevj[j]]); b = pos2(S.order[j]); }
+          else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) { a = init2(S.cnodej[j]); b = pos2(S.order[j]); }
+          else continue;
+          for (size_t f = 0; f < F; ++f) cf[f] += (uint32_t)(a > fp[f]) & (uint32_t)(b < fe[f]);
+        }
+      });
+      for (size_t f = 0; f < F; ++f) {
+        uint64_t nested = 0;
+        for (uint32_t q = 0; q < kParts; ++q) nested += cnt_qf[(size_t)q * F + f];
+        decide_far(f, nested);
+      }
+    } else {
     // pairs (next occurrence, occurrence) of consecutive pushes of one key, per partition
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> pp(kParts);
     per_part([&](uint32_t q) {
@@ -537,23 +568,18 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
     starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
     const size_t M = starts.size();
     std::vector<uint32_t> fen(M + 1, 0);
-    std::sort(far.begin(), far.end());                     // by position = batch order
     uint32_t added = 0;
     size_t pi = 0;
-    for (uint32_t i : far) {
-      const uint32_t j = S.pos[i];
-      const uint64_t e = pos2(i);
-      for (; pi < pairs.size() && pairs[pi].first < e; ++pi, ++added) {
+    for (size_t f = 0; f < F; ++f) {
+      for (; pi < pairs.size() && pairs[pi].first < fe[f]; ++pi, ++added) {
         const size_t x0 = std::lower_bound(starts.begin(), starts.end(), pairs[pi].second) - starts.begin() + 1;
         for (size_t x = x0; x <= M; x += x & (~x + 1)) ++fen[x];
       }
-      const uint64_t p2 = S.prevj[j] >= 0 ? pos2(S.order[S.prevj[j]]) : init2(S.cnodej[j]);
       uint32_t upto = 0;                                   // pairs starting at or before p
-      for (size_t x = std::upper_bound(starts.begin(), starts.end(), p2) - starts.begin(); x > 0; x -= x & (~x + 1))
+      for (size_t x = std::upper_bound(starts.begin(), starts.end(), fp[f]) - starts.begin(); x > 0; x -= x & (~x + 1))
         upto += fen[x];
-      const uint64_t nested = added - upto;
-      const uint64_t window = (e - p2) / 2 - 1;           // pushes strictly between (p is exact here)
-      S.decj[j] = window - nested < C ? 2 : 1;
+      decide_far(f, added - upto);
+    }
     }
   }
   if (evict)
@@ -641,19 +667,19 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   mark();
   // 4. the cache: the C most recent distinct keys of S up to the cut, in recency order
   if (cache_on) {
-    std::vector<uint32_t> last;                            // pushes that are their key's last before m
+    // pushes that are their key's last before m; cached keys pushed again leave their place
+    std::vector<uint32_t> last;
     last.reserve(na);
+    uint64_t detached = 0;
     for (uint32_t i = 0; i < m; ++i) {
       if (!S.dec[i]) continue;
-      const int32_t nj = S.nextj[S.pos[i]];
+      const uint32_t j = S.pos[i];
+      const int32_t nj = S.nextj[j];
       if (nj < 0 || S.order[nj] >= m) last.push_back(i);
+      if (S.prevj[j] == -1 && S.cnodej[j] >= 0) { p->cache.detach(S.cnodej[j]); ++detached; }
     }
     const size_t U = last.size(), keepU = std::min<uint64_t>(U, C);
     auto cnode_of = [&](uint32_t i) { return S.cnodej[S.firstj[S.pos[i]]]; };
-    // cached keys pushed again leave their place
-    uint64_t detached = 0;
-    for (uint32_t i = 0; i < m; ++i)
-      if (S.dec[i] && S.prevj[S.pos[i]] == -1 && S.cnodej[S.pos[i]] >= 0) { p->cache.detach(S.cnodej[S.pos[i]]); ++detached; }
     const uint64_t keep_old = std::min<uint64_t>(p->cache.len, C - keepU), evicted = p->cache.len - keep_old;
     if (keep_old < evicted + detached) {
       // most of the old LRU goes: rebuild list and index from the survivors + this batch's keys

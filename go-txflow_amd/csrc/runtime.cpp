@@ -163,7 +163,8 @@ struct txv_ctx {
   int btable_wide_w = 0;
   uint32_t lane_votes = 4;         // K1b votes per lane (one shared inversion)
   bool lane_auto = true;           // no configured V: 8 for batches that still give >= 1.5 waves/SIMD
-  uint32_t* d_park = nullptr;      // K1b parked points: [wave][V-1][32][64]
+  uint32_t* d_park = nullptr;      // K1b parked points: [wave][V][33][64]
+  uint32_t* d_wctr = nullptr;      // chunk counters of the work-stealing K1b
   size_t park_words = 0;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;
@@ -522,6 +523,7 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   a.order = by_val ? s.d_order : nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
   a.park = c->d_park;
+  a.wctr = c->d_wctr;
   a.rpts = s.d_rpts;
   a.lane_votes = c->lane_votes;
   return a;
@@ -546,8 +548,9 @@ uint32_t launch_lane_votes(const txv_ctx* c, int wb, uint32_t n_work) {
 int ensure_park(txv_ctx* c) {
   if (c->lane_votes == 1) return TXV_OK;   // split mode parks nothing
   const size_t words = (size_t)(c->lane_auto ? 8u : c->lane_votes) * TXV_PARK_WORDS * (size_t)c->n_cus * 2 * TXV_VERIFY_BLOCK;
-  if (words <= c->park_words) return TXV_OK;
   int r;
+  if (!c->d_wctr && (r = dalloc(c, &c->d_wctr, 8 * 16))) return r;
+  if (words <= c->park_words) return TXV_OK;
   if ((r = dalloc(c, &c->d_park, words))) return r;
   c->park_words = words;
   return TXV_OK;
@@ -1181,7 +1184,7 @@ void txv_destroy(txv_ctx* c) {
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
-  dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
+  dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
   dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_bitmap);

@@ -38,9 +38,11 @@ struct VerifyArgs {
                                // 1 = split: K1b stores R' per vote, K1c batch-inverts G per lane
   uint32_t* rpts;              // split mode: [TXV_RPTS_WORDS][n_pad] per work entry: X, Y, Z of R',
                                // then the exclusive prefix product of the lane's Z (K1b -> K1c)
+  uint32_t* wctr;              // [8 * 16] chunk counters of the work-stealing K1b (one per XCD
+                               // range, 64 B apart), zeroed before each launch
 };
 
-#define TXV_PARK_WORDS 32          // X, Y, prefix product, Z of one parked vote
+#define TXV_PARK_WORDS 33          // X, Y, prefix product, Z of one parked vote; its vote index + 1
 #define TXV_MAX_LANE_VOTES 4
 #define TXV_RPTS_WORDS 32
 
