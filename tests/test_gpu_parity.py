@@ -416,3 +416,40 @@ def test_device_signbytes_edge_fields(gpu_ctx, oracle_lib, chain):
         assert not np.any(ok == T.ERR_INVALID_SIGNATURE)
     finally:
         ctx.close()
+
+
+def test_set_validators_same_keys_new_powers(oracle_lib):
+    """txv_set_validators with the keys of the current registry (same order) keeps the validator
+    tables (no K0 rebuild) but takes the new powers and resets the TxFlow: the tally then follows
+    the new powers exactly (oracle with those powers), and a changed key set rebuilds."""
+    import time
+    import txflow_amd as T
+    rnd = random.Random(35)
+    ctx = T.Context(max_batch=1 << 14, max_txs=256, max_validators=16)
+    try:
+        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 8, 600, rnd, n_txs=20)
+        b = T.VoteBatch.from_votes(votes)
+        od = [dict(height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0], ts_nanos=v.Timestamp[1],
+                   addr=v.ValidatorAddress, sig=v.Signature) for v in votes]
+        times = []
+        for powers in ([1] * 8, [9, 1, 1, 1, 1, 1, 1, 1], [1, 2, 3, 4, 5, 6, 7, 8]):
+            t0 = time.perf_counter()
+            ctx.set_validators(pubs, powers, "test_chain_id")
+            times.append(time.perf_counter() - t0)
+            st, ev = ctx.add_votes(b)
+            flow = oracle_lib.Flow(pubs, powers, b"test_chain_id")
+            ost, osum, ofired = flow.add_votes(od)
+            exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+            assert np.array_equal(st, exp), powers
+            for v in votes:
+                assert ctx.query_tx(v.TxHash.encode()) == flow.query(v.TxHash.encode())
+        assert ctx.total_power() == sum([1, 2, 3, 4, 5, 6, 7, 8])
+        # a different key order is a different registry: tables rebuilt, verdicts follow it
+        ctx.set_validators(list(reversed(pubs)), [1] * 8, "test_chain_id")
+        st, _ = ctx.add_votes(b)
+        flow = oracle_lib.Flow(list(reversed(pubs)), [1] * 8, b"test_chain_id")
+        ost, _, ofired = flow.add_votes(od)
+        assert np.array_equal(st, ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7))
+        print("set_validators seconds:", [round(t, 4) for t in times])
+    finally:
+        ctx.close()
