@@ -666,15 +666,20 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
 #ifndef TXV_K1B_DYNAMIC
 #define TXV_K1B_DYNAMIC 1
 #endif
-template <int BLOCK, int WB, int WA, int V>
-__global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
+// TXV_K1B_DYN_WAVES (experiment): waves per SIMD of the work-stealing K1b; 3 needs <= 168 VGPRs and
+// one 8 KiB entry buffer per wave (prefetch one addition ahead) to fit the 160 KiB of LDS
+#ifndef TXV_K1B_DYN_WAVES
+#define TXV_K1B_DYN_WAVES 2
+#endif
+template <int BLOCK, int WB, int WA, int V, int WAVES = 2>
+__global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n_chunks = (a.n_work + 63u) / 64u;
   const uint32_t xg = gridDim.x >= 8 ? 8u : 1u, myx = blockIdx.x % xg;
   const uint32_t per = (n_chunks + xg - 1u) / xg;
   const uint32_t gwave = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
   uint32_t* park = a.park + (size_t)gwave * V * TXV_PARK_WORDS * 64 + lane;
-  constexpr int PD = V == 8 ? 2 : 1;
+  constexpr int PD = WAVES >= 3 ? 1 : 2;
   __shared__ uint4 pf[BLOCK / 64][PD * 8 * 64];
   uint4* wbuf = pf[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
   uint32_t src = 0;                      // ranges tried: (myx + src) % xg
@@ -1027,7 +1032,15 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
       if (TXV_K1B_DYNAMIC && args->wctr) {
         const hipError_t e = hipMemsetAsync(args->wctr, 0, 8 * 16 * sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+        if constexpr (TXV_K1B_DYN_WAVES >= 3) {
+          // persistent: every resident slot (256-thread blocks, TXV_K1B_DYN_WAVES per SIMD)
+          static int cus = 0;
+          if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+          hipLaunchKernelGGL((txv_k_scalarmult_dyn<256, WB, WA, 8, TXV_K1B_DYN_WAVES>),
+                             dim3((uint32_t)cus * TXV_K1B_DYN_WAVES), dim3(256), 0, st, *args);
+        } else {
+          hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
+        }
       } else {
         hipLaunchKernelGGL((txv_k_scalarmult_multi<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
       }
