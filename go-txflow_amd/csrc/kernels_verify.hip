@@ -1034,10 +1034,13 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
         if (e != hipSuccess) return e;
         if constexpr (TXV_K1B_DYN_WAVES >= 3) {
           // persistent: every resident slot (256-thread blocks, TXV_K1B_DYN_WAVES per SIMD)
-          static int cus = 0;
+          // TXV_K1B_DYN_BLOCKS = blocks per CU x 100 (default: every slot); fewer leave SIMDs with
+          // room for the neighbouring batches' TxFlow kernels
+          static int cus = 0, per100 = 0;
           if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+          if (!per100) per100 = getenv("TXV_K1B_DYN_BLOCKS") ? atoi(getenv("TXV_K1B_DYN_BLOCKS")) : 100 * TXV_K1B_DYN_WAVES;
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<256, WB, WA, 8, TXV_K1B_DYN_WAVES>),
-                             dim3((uint32_t)cus * TXV_K1B_DYN_WAVES), dim3(256), 0, st, *args);
+                             dim3(std::max<uint32_t>(8, (uint32_t)cus * (uint32_t)per100 / 100u)), dim3(256), 0, st, *args);
         } else {
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
         }
