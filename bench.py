@@ -187,6 +187,7 @@ C5_CACHE = 10000        # TxVotePool CacheSize: tendermint's default (config.Def
 
 def c5_expected_pool(wl, cache_size: int):
     """the oracle pool's CheckTx verdicts for the stream, batch by batch (checker, untimed)"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
     op = O.Pool(size=wl.n + 1, cache_size=cache_size, max_txs_bytes=1 << 40)

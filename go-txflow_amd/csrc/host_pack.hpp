@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -42,6 +44,12 @@ inline uint64_t hash_bytes(const uint8_t* p, uint32_t n, uint64_t seed) {
 }
 
 // ------------------------------------------------------------------ worker pool
+// Persistent threads; a parallel_for posts its chunks in one of kSlots job slots and the caller
+// takes part.  Claiming a chunk is one CAS on the slot's (sequence, next chunk) word -- no mutex on
+// the hot path: with a mutex the 15 woken workers of every pass queued on it one futex hand-off
+// after another (tens of microseconds per pass, ~8 passes per CheckTx batch).  A worker that runs
+// out of chunks spins for TXV_HOST_SPIN_US (default 200 us: the passes of one CheckTx batch or one
+// staging follow each other within microseconds), then sleeps on a condition variable.
 class WorkerPool {
  public:
   explicit WorkerPool(unsigned n) {
@@ -56,9 +64,10 @@ class WorkerPool {
     }
   }
   ~WorkerPool() {
+    stop_.store(true);
     {
       std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -71,66 +80,109 @@ class WorkerPool {
     return ok;
   }
   // fn(lo, hi) over [0, n) in chunks; the caller thread takes part.  Small n runs inline.
-  // Each call is its own Job and several threads may call at once (e.g. the pool's CheckTx
-  // beside txv_submit_votes' staging): idle workers take chunks of any job that has some left,
-  // and every caller drains its own job, so no call waits on another's.
+  // Several threads may call at once (e.g. the pool's CheckTx beside txv_submit_votes' staging):
+  // each call has its own slot, idle workers take chunks of any slot, and every caller drains its
+  // own job, so no call waits on another's.  With every slot taken the call runs inline.
   void parallel_for(uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn, uint32_t min_chunk = 2048) {
     const uint32_t parts = std::min<uint32_t>(size() * 4, std::max<uint32_t>(1, n / min_chunk));
     if (parts <= 1 || th_.empty()) { if (n) fn(0, n); return; }
-    auto job = std::make_shared<Job>();
-    job->fn = &fn; job->n = n; job->parts = parts;
-    {
-      std::lock_guard<std::mutex> g(m_);
-      jobs_.push_back(job);
+    Slot* s = nullptr;
+    for (auto& c : slots_) {
+      bool f = false;
+      if (c.owned.compare_exchange_strong(f, true)) { s = &c; break; }
     }
-    cv_.notify_all();
-    work(*job);
-    std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [&] { return job->done.load() == job->parts; });
-    for (size_t i = 0; i < jobs_.size(); ++i)
-      if (jobs_[i] == job) { jobs_.erase(jobs_.begin() + (ptrdiff_t)i); break; }
+    if (!s) { fn(0, n); return; }
+    s->fn = &fn; s->n = n; s->parts.store(parts, std::memory_order_relaxed);
+    s->done.store(0, std::memory_order_relaxed);
+    const uint64_t seq = (s->state.load(std::memory_order_relaxed) >> 32) + 1;
+    s->state.store(seq << 32, std::memory_order_release);      // published: chunk 0 is next
+    gen_.fetch_add(1);
+    if (sleepers_.load()) {
+      std::lock_guard<std::mutex> g(m_);
+      cv_.notify_all();
+    }
+    while (claim_run(*s)) {}
+    // the other threads' chunks are usually a few microseconds behind: spin before sleeping
+    for (auto t0 = std::chrono::steady_clock::now(); s->done.load(std::memory_order_acquire) != parts;) {
+      cpu_relax();
+      if (std::chrono::steady_clock::now() - t0 > spin_) {
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return s->done.load() == parts; });
+        break;
+      }
+    }
+    s->owned.store(false, std::memory_order_release);
   }
 
  private:
-  struct Job {
+  static constexpr int kSlots = 8;
+  struct Slot {
+    std::atomic<uint64_t> state{0};            // (sequence << 32) | next chunk
+    std::atomic<uint32_t> done{0};
+    std::atomic<bool> owned{false};            // a caller is using the slot
     const std::function<void(uint32_t, uint32_t)>* fn = nullptr;
-    uint32_t n = 0, parts = 0;
-    std::atomic<uint32_t> next{0}, done{0};
+    uint32_t n = 0;
+    std::atomic<uint32_t> parts{0};            // read before the CAS, possibly of a finished job
   };
-  void work(Job& j) {
+  // claim the slot's next chunk and run it; false when none is left.  A claimed chunk keeps the
+  // job alive (its caller waits for done == parts), so fn / n / parts are read after the CAS.
+  bool claim_run(Slot& s) {
+    uint64_t v = s.state.load(std::memory_order_acquire);
     for (;;) {
-      const uint32_t p = j.next.fetch_add(1);
-      if (p >= j.parts) return;
-      const uint32_t lo = (uint32_t)((uint64_t)j.n * p / j.parts), hi = (uint32_t)((uint64_t)j.n * (p + 1) / j.parts);
-      (*j.fn)(lo, hi);
-      if (j.done.fetch_add(1) + 1 == j.parts) {
-        std::lock_guard<std::mutex> g(m_);
-        done_cv_.notify_all();
+      const uint32_t nx = (uint32_t)v, parts = s.parts.load(std::memory_order_relaxed);
+      if (nx >= parts || (v >> 32) == 0) return false;
+      if (s.state.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) {
+        const uint32_t n = s.n;
+        const uint32_t lo = (uint32_t)((uint64_t)n * nx / parts), hi = (uint32_t)((uint64_t)n * (nx + 1) / parts);
+        (*s.fn)(lo, hi);
+        if (s.done.fetch_add(1, std::memory_order_acq_rel) + 1 == parts) {
+          std::lock_guard<std::mutex> g(m_);
+          done_cv_.notify_all();
+        }
+        return true;
       }
     }
   }
-  // a job with chunks left (under m_)
-  std::shared_ptr<Job> pick() const {
-    for (const auto& j : jobs_)
-      if (j->next.load() < j->parts) return j;
-    return nullptr;
+  bool run_any() {
+    bool any = false;
+    for (auto& s : slots_)
+      while (claim_run(s)) any = true;
+    return any;
+  }
+  static void cpu_relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
   }
   void loop() {
     for (;;) {
-      std::shared_ptr<Job> j;
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return stop_ || (j = pick()) != nullptr; });
-        if (stop_) return;
+      const uint64_t g0 = gen_.load();
+      if (run_any()) continue;
+      for (auto t0 = std::chrono::steady_clock::now(); gen_.load(std::memory_order_acquire) == g0;) {
+        cpu_relax();
+        if (std::chrono::steady_clock::now() - t0 > spin_) {
+          std::unique_lock<std::mutex> lk(m_);
+          sleepers_.fetch_add(1);
+          cv_.wait(lk, [&] { return stop_.load() || gen_.load() != g0; });
+          sleepers_.fetch_sub(1);
+          break;
+        }
       }
-      work(*j);
+      if (stop_.load()) return;
     }
   }
   std::vector<std::thread> th_;
+  Slot slots_[kSlots];
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
-  std::vector<std::shared_ptr<Job>> jobs_;   // jobs whose callers have not returned yet
-  bool stop_ = false;
+  std::atomic<bool> stop_{false};
+  std::atomic<unsigned> sleepers_{0};        // workers waiting on cv_
+  std::atomic<uint64_t> gen_{0};             // jobs posted so far
+  std::chrono::microseconds spin_{spin_us()};
+  static unsigned spin_us() {                // TXV_HOST_SPIN_US (default 200, 0 = sleep at once)
+    const char* e = getenv("TXV_HOST_SPIN_US");
+    return e ? (unsigned)std::max(0, atoi(e)) : 200u;
+  }
 };
 
 // ------------------------------------------------------------------ parallel stable counting sort

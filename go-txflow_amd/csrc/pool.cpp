@@ -232,6 +232,12 @@ struct BatchScratch {
   std::vector<int32_t> prevj, nextj, firstj, cnodej, qpos, adm;
   std::vector<uint8_t> decj, dec;           // 0 not a push (too large), 1 miss, 2 hit, 3 far
   std::vector<int32_t> qtouched;
+  // per partition, filled by the scan: pairs (start, next occurrence) of consecutive pushes of one
+  // key in doubled S positions (only while evicting), distinct keys pushed, cached keys pushed
+  std::vector<std::pair<uint64_t, uint64_t>> pairs[16];
+  uint32_t firsts[16];
+  std::vector<int32_t> cached_firsts[16];
+  std::vector<uint8_t> dmark;               // per cache node: pushed again by this batch
 };
 
 }  // namespace
@@ -251,6 +257,7 @@ struct txv_pool {
   std::vector<int32_t> idx_c, idx_t;               // batch scratch: node indices (fast path)
   std::vector<uint8_t> part;                       // batch scratch: index partition per key (batch path)
   BatchScratch bs;                                 // batch scratch (batch path)
+  std::shared_ptr<void> workers;                   // batch passes of calls without a context
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -285,6 +292,22 @@ int batch_keys(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig
 void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // runtime.cpp
 void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn,
                            uint32_t min_chunk = 4096);   // runtime.cpp (the context's host workers)
+
+std::shared_ptr<void> txv_host_workers_new();   // runtime.cpp: a standalone worker pool
+void txv_host_workers_for(void* w, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn, uint32_t min_chunk);
+
+namespace {
+
+// the batch passes' worker threads: the context's when there is one, else the pool's own
+// (created on the first batch-path call without a context: TXV_HOST_THREADS, else min(16, cores))
+void pool_parallel_for(txv_pool* p, txv_ctx* ctx, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn,
+                       uint32_t min_chunk = 4096) {
+  if (ctx) { txv_host_parallel_for(ctx, n, fn, min_chunk); return; }
+  if (!p->workers) p->workers = txv_host_workers_new();
+  txv_host_workers_for(p->workers.get(), n, fn, min_chunk);
+}
+
+}  // namespace
 
 namespace {
 
@@ -370,7 +393,7 @@ uint64_t batch_tab_hash(const Key& k) { uint64_t v; memcpy(&v, k.b + 16, 8); ret
 
 bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, uint32_t n, uint8_t* status_out) {
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
-  std::chrono::steady_clock::time_point tp[10];
+  std::chrono::steady_clock::time_point tp[16];
   int ntp = 0;
   auto mark = [&] { if (prof) tp[ntp++] = std::chrono::steady_clock::now(); };
   mark();
@@ -392,7 +415,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
   };
-  txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
     for (uint32_t c = c0; c < c1; ++c) {
       uint32_t lo, hi, pushes = 0;
       uint64_t sm = 0;
@@ -433,7 +456,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       na += t;
     }
   }
-  txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
     for (uint32_t c = c0; c < c1; ++c) {
       uint32_t lo, hi;
       chunk(c, lo, hi);
@@ -450,7 +473,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   }, 1);
   const bool evict = cache_on && L0 + na > C;
   auto per_part = [&](const std::function<void(uint32_t)>& fn) {
-    txv_host_parallel_for(ctx, kParts, [&](uint32_t lo, uint32_t hi) { for (uint32_t q = lo; q < hi; ++q) fn(q); }, 1);
+    pool_parallel_for(p, ctx, kParts, [&](uint32_t lo, uint32_t hi) { for (uint32_t q = lo; q < hi; ++q) fn(q); }, 1);
   };
   S.prevj.resize(n); S.firstj.resize(n); S.cnodej.resize(n); S.nextj.resize(n); S.decj.resize(n);
   mark();
@@ -470,13 +493,22 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   //    one, the cache node of a first push whose key is cached (a hash tag beside each slot: keys
   //    are compared only on a tag match), and the decision (1 miss, 2 hit, 3 far: counted below)
   std::vector<std::vector<uint32_t>> far_q(kParts);
+  // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
+  auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
+  auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
   per_part([&](uint32_t q) {
     const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
+    auto& pairs = S.pairs[q];
+    auto& cfirst = S.cached_firsts[q];
+    pairs.clear();
+    cfirst.clear();
+    uint32_t firsts = 0;
     uint32_t cap = 16;
     while (cap < 2 * (hi - lo)) cap *= 2;
     std::vector<uint64_t> tab(cap, 0);            // (tag << 32) | (j + 1) of the key's last push
     const FlatIndex& cf = *p->cache_map.p[q];
     for (uint32_t j = lo; j < hi; ++j) {
+      if (j + 2 * kAdmitAhead < hi) __builtin_prefetch(&keys[S.order[j + 2 * kAdmitAhead]]);   // the key, then its slot
       if (cache_on && j + kAdmitAhead < hi) cf.prefetch(keys[S.order[j + kAdmitAhead]]);
       const uint32_t i = S.order[j];
       S.cnodej[j] = -1;
@@ -494,9 +526,11 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
         S.firstj[j] = S.firstj[pj];
         S.nextj[pj] = (int32_t)j;
         d = !cache_on ? 1 : ((!evict || S.aidx[i] - S.aidx[S.order[pj]] - 1 < C) ? 2 : 3);
+        if (evict) pairs.emplace_back(pos2(S.order[pj]), pos2(i));
       } else {
         S.prevj[j] = -1;
         S.firstj[j] = (int32_t)j;
+        ++firsts;
         d = 1;
         if (cache_on) {
           const int32_t cn = cf.find(keys[i]);
@@ -504,6 +538,8 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
           if (cn >= 0) {
             const int32_t r = evict ? S.qpos[cn] : -1;
             d = (r < 0 || L0 + S.aidx[i] - (uint64_t)r - 1 < C) ? 2 : 3;
+            cfirst.push_back(cn);
+            if (evict) pairs.emplace_back(init2(cn), pos2(i));
           }
         }
       }
@@ -511,14 +547,12 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       S.decj[j] = d;
       if (d == 3) far_q[q].push_back(i);
     }
+    S.firsts[q] = firsts;
   });
   std::vector<uint32_t> far;
   for (auto& v : far_q) far.insert(far.end(), v.begin(), v.end());
   mark();
   if (!far.empty()) {
-    // doubled positions: front entry r -> 2r, an entry beyond the front -> 2 L0 - 1, push i -> 2 (L0 + aidx)
-    auto pos2 = [&](uint32_t i) -> uint64_t { return 2 * (L0 + S.aidx[i]); };
-    auto init2 = [&](int32_t node) -> uint64_t { const int32_t r = S.qpos[node]; return r >= 0 ? 2 * (uint64_t)r : 2 * L0 - 1; };
     std::sort(far.begin(), far.end());                     // by position = batch order
     const size_t F = far.size();
     std::vector<uint64_t> fe(F), fp(F);                    // each far push's window (p, e)
@@ -531,18 +565,15 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       const uint64_t window = (fe[f] - fp[f]) / 2 - 1;     // pushes strictly between (p is exact here)
       S.decj[S.pos[far[f]]] = window - nested < C ? 2 : 1;
     };
-    if (F <= 64) {
+    size_t npairs = 0;
+    for (uint32_t q = 0; q < kParts; ++q) npairs += S.pairs[q].size();
+    if (F <= 64 || F * npairs <= (size_t)1 << 21) {
       // few far repeats: every partition counts its nested pairs for each of them directly
       std::vector<uint32_t> cnt_qf(kParts * F, 0);
       per_part([&](uint32_t q) {
         uint32_t* cf = cnt_qf.data() + (size_t)q * F;
-        for (uint32_t j = S.cnt[q]; j < S.cnt[q + 1]; ++j) {
-          uint64_t a, b;                                   // pair (start, next occurrence)
-          if (S.prevj[j] >= 0) { a = pos2(S.order[S.prevj[j]]); b = pos2(S.order[j]); }
-          else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) { a = init2(S.cnodej[j]); b = pos2(S.order[j]); }
-          else continue;
-          for (size_t f = 0; f < F; ++f) cf[f] += (uint32_t)(a > fp[f]) & (uint32_t)(b < fe[f]);
-        }
+        for (const auto& ab : S.pairs[q])                  // pair (start, next occurrence)
+          for (size_t f = 0; f < F; ++f) cf[f] += (uint32_t)(ab.first > fp[f]) & (uint32_t)(ab.second < fe[f]);
       });
       for (size_t f = 0; f < F; ++f) {
         uint64_t nested = 0;
@@ -550,17 +581,10 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
         decide_far(f, nested);
       }
     } else {
-    // pairs (next occurrence, occurrence) of consecutive pushes of one key, per partition
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> pp(kParts);
-    per_part([&](uint32_t q) {
-      for (uint32_t j = S.cnt[q]; j < S.cnt[q + 1]; ++j) {
-        const uint32_t i = S.order[j];
-        if (S.prevj[j] >= 0) pp[q].emplace_back(pos2(i), pos2(S.order[S.prevj[j]]));
-        else if (S.prevj[j] == -1 && S.cnodej[j] >= 0) pp[q].emplace_back(pos2(i), init2(S.cnodej[j]));
-      }
-    });
+    // pairs (next occurrence, occurrence) of consecutive pushes of one key
     std::vector<std::pair<uint64_t, uint64_t>> pairs;
-    for (auto& v : pp) pairs.insert(pairs.end(), v.begin(), v.end());
+    for (uint32_t q = 0; q < kParts; ++q)
+      for (const auto& ab : S.pairs[q]) pairs.emplace_back(ab.second, ab.first);
     std::sort(pairs.begin(), pairs.end());                 // by next occurrence: the sweep order
     std::vector<uint64_t> starts(pairs.size());            // Fenwick tree over the distinct starts
     for (size_t k = 0; k < pairs.size(); ++k) starts[k] = pairs[k].second;
@@ -599,7 +623,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   const bool may_cut = (int64_t)p->txs.len + (int64_t)na >= (int64_t)p->cfg.size;
   if (!may_cut) {
     std::vector<uint64_t> cnt_c(P, 0), bytes_c(P, 0);
-    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+    pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
       for (uint32_t c = c0; c < c1; ++c) {
         uint32_t lo, hi;
         chunk(c, lo, hi);
@@ -642,7 +666,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
                                               a + 1 < A ? p->idx_t[a + 1] : -1};
   };
   if (!may_cut) {
-    txv_host_parallel_for(ctx, P, [&](uint32_t c0, uint32_t c1) {
+    pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
       for (uint32_t c = c0; c < c1; ++c) {
         uint32_t lo, hi;
         chunk(c, lo, hi);
@@ -667,30 +691,58 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   mark();
   // 4. the cache: the C most recent distinct keys of S up to the cut, in recency order
   if (cache_on) {
-    // pushes that are their key's last before m; cached keys pushed again leave their place
+    // U = distinct keys pushed before m (each one's last push is kept in recency order), detached
+    // = cached keys pushed again (they leave their place in the old list)
     std::vector<uint32_t> last;
-    last.reserve(na);
-    uint64_t detached = 0;
-    for (uint32_t i = 0; i < m; ++i) {
-      if (!S.dec[i]) continue;
-      const uint32_t j = S.pos[i];
-      const int32_t nj = S.nextj[j];
-      if (nj < 0 || S.order[nj] >= m) last.push_back(i);
-      if (S.prevj[j] == -1 && S.cnodej[j] >= 0) { p->cache.detach(S.cnodej[j]); ++detached; }
+    uint64_t U = 0, detached = 0;
+    const bool whole = m == n;                             // no cut: the scan's counts hold
+    if (whole)
+      for (uint32_t q = 0; q < kParts; ++q) { U += S.firsts[q]; detached += S.cached_firsts[q].size(); }
+    else {
+      last.reserve(na);
+      for (uint32_t i = 0; i < m; ++i) {
+        if (!S.dec[i]) continue;
+        const uint32_t j = S.pos[i];
+        const int32_t nj = S.nextj[j];
+        if (nj < 0 || S.order[nj] >= m) last.push_back(i);
+        if (S.prevj[j] == -1 && S.cnodej[j] >= 0) ++detached;
+      }
+      U = last.size();
     }
-    const size_t U = last.size(), keepU = std::min<uint64_t>(U, C);
+    const uint64_t keepU = std::min<uint64_t>(U, C), L1 = p->cache.len - detached;
     auto cnode_of = [&](uint32_t i) { return S.cnodej[S.firstj[S.pos[i]]]; };
-    const uint64_t keep_old = std::min<uint64_t>(p->cache.len, C - keepU), evicted = p->cache.len - keep_old;
+    const uint64_t keep_old = std::min<uint64_t>(L1, C - keepU), evicted = L1 - keep_old;
     if (keep_old < evicted + detached) {
       // most of the old LRU goes: rebuild list and index from the survivors + this batch's keys
-      std::vector<Key> fin_keys;
-      fin_keys.reserve(keep_old + keepU);
-      {
-        int32_t e = p->cache.head;
-        for (uint64_t r = 0; r < evicted; ++r) e = p->cache.nodes[e].next;
-        for (; e >= 0; e = p->cache.nodes[e].next) fin_keys.push_back(p->cache.nodes[e].k);
+      std::vector<Key> fin_keys(keep_old + keepU);
+      if (keep_old) {                                      // the last keep_old entries not pushed again
+        if (S.dmark.size() < p->cache.nodes.size()) S.dmark.resize(p->cache.nodes.size(), 0);
+        auto mark_pushed = [&](uint8_t v) {
+          if (whole) {
+            for (uint32_t q = 0; q < kParts; ++q)
+              for (int32_t e : S.cached_firsts[q]) S.dmark[e] = v;
+          } else {
+            for (uint32_t i = 0; i < m; ++i) {
+              const uint32_t j = S.pos[i];
+              if (S.dec[i] && S.prevj[j] == -1 && S.cnodej[j] >= 0) S.dmark[S.cnodej[j]] = v;
+            }
+          }
+        };
+        mark_pushed(1);
+        uint64_t r = keep_old;
+        for (int32_t e = p->cache.tail; r && e >= 0; e = p->cache.nodes[e].prev)
+          if (!S.dmark[e]) fin_keys[--r] = p->cache.nodes[e].k;
+        mark_pushed(0);
       }
-      for (size_t u = U - keepU; u < U; ++u) fin_keys.push_back(keys[last[u]]);
+      // the last push of each of the keepU most recent distinct keys, from the end of the batch back
+      uint64_t kf = keep_old + keepU;
+      if (whole) {
+        for (uint32_t i = m; i-- > 0 && kf > keep_old;)
+          if (S.dec[i] && S.nextj[S.pos[i]] < 0) fin_keys[--kf] = keys[i];
+      } else {
+        for (size_t u = U; u-- > U - keepU;) fin_keys[--kf] = keys[last[u]];
+      }
+      mark();
       const uint32_t L = (uint32_t)fin_keys.size();
       p->cache.clear();
       p->cache.nodes.resize(L);
@@ -699,13 +751,31 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       p->cache.head = L ? 0 : -1;
       p->cache.tail = (int32_t)L - 1;
       p->cache.len = L;
+      mark();
+      std::vector<uint8_t> kpart(L);
+      pool_parallel_for(p, ctx, L, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t k = lo; k < hi; ++k) kpart[k] = (uint8_t)PartIndex::part(fin_keys[k]);
+      });
+      mark();
       per_part([&](uint32_t q) {
         FlatIndex& f = *p->cache_map.p[q];
         f.clear();
         for (uint32_t k = 0; k < L; ++k)
-          if (PartIndex::part(fin_keys[k]) == q) f.put(fin_keys[k], (int32_t)k);
+          if (kpart[k] == q) f.put(fin_keys[k], (int32_t)k);
       });
     } else {
+      if (whole) {                                         // every push's key, in order, for the lists below
+        last.reserve(U);
+        for (uint32_t i = 0; i < m; ++i)
+          if (S.dec[i] && S.nextj[S.pos[i]] < 0) last.push_back(i);
+      }
+      for (uint32_t q = 0; q < kParts && whole; ++q)       // cached keys pushed again leave their place
+        for (int32_t e : S.cached_firsts[q]) p->cache.detach(e);
+      if (!whole)
+        for (uint32_t i = 0; i < m; ++i) {
+          const uint32_t j = S.pos[i];
+          if (S.dec[i] && S.prevj[j] == -1 && S.cnodej[j] >= 0) p->cache.detach(S.cnodej[j]);
+        }
       for (uint64_t r = 0; r < evicted; ++r) {             // evictions from the front
         const int32_t h = p->cache.head;
         p->cache_map.erase(p->cache.nodes[h].k);
@@ -757,6 +827,7 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
       FlatIndex& f = *p->txs_map.p[q];
       const uint32_t lo = S.cnt[q], hi = S.cnt[q + 1];
       for (uint32_t j = lo; j < hi; ++j) {
+        if (j + 2 * kAdmitAhead < hi) __builtin_prefetch(&keys[S.order[j + 2 * kAdmitAhead]]);
         if (j + kAdmitAhead < hi) f.prefetch(keys[S.order[j + kAdmitAhead]]);
         const uint32_t i = S.order[j];
         if (S.adm[i] >= 0) f.put(keys[i], p->idx_t[S.adm[i]]);
@@ -767,8 +838,13 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
   mark();
   if (prof) {
     auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    fprintf(stderr, "[txv pool] batch: order=%.3f front=%.3f scan+decide=%.3f far(%zu)=%.3f status+nodes=%.3f cache=%.3f txs=%.3f ms\n",
-            ms(0), ms(1), ms(2), far.size(), ms(3), ms(4), ms(5), ms(6));
+    if (ntp == 8)
+      fprintf(stderr, "[txv pool] batch: order=%.3f front=%.3f scan+decide=%.3f far(%zu)=%.3f status+nodes=%.3f cache=%.3f txs=%.3f ms\n",
+              ms(0), ms(1), ms(2), far.size(), ms(3), ms(4), ms(5), ms(6));
+    else if (ntp == 11)   // the cache rebuilt: survivors + last pushes, list, partitions, index
+      fprintf(stderr, "[txv pool] batch: order=%.3f front=%.3f scan+decide=%.3f far(%zu)=%.3f status+nodes=%.3f "
+              "cache=%.3f (keys %.3f list %.3f part %.3f index %.3f) txs=%.3f ms\n", ms(0), ms(1), ms(2), far.size(), ms(3),
+              ms(4), std::chrono::duration<double, std::milli>(tp[9] - tp[5]).count(), ms(5), ms(6), ms(7), ms(8), ms(9));
   }
   return true;
 }

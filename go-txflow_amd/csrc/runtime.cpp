@@ -1941,9 +1941,19 @@ void txv_host_parallel_for(txv_ctx* c, uint32_t n, const std::function<void(uint
   else if (n) fn(0, n);
 }
 
-extern "C" {
+// a worker pool of its own for a TxVotePool used without a context (TXV_HOST_THREADS, else
+// min(16, hardware threads)), created on its first batch-path call
+std::shared_ptr<void> txv_host_workers_new() {
+  unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (const char* e = getenv("TXV_HOST_THREADS")) nt = (unsigned)std::max(1, std::min(256, atoi(e)));
+  return std::shared_ptr<void>(new txv_host::WorkerPool(nt),
+                               [](void* w) { delete static_cast<txv_host::WorkerPool*>(w); });
+}
+void txv_host_workers_for(void* w, uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn,
+                          uint32_t min_chunk) {
+  static_cast<txv_host::WorkerPool*>(w)->parallel_for(n, fn, min_chunk);
+}
 
-}  // extern "C"
 int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off,
                          uint8_t* keys_out, const std::function<void()>& overlap);
 extern "C" {

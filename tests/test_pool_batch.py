@@ -68,6 +68,12 @@ CASES = [
     ("bytes_cap_binds", 10000, 1 << 20, 3_000_000, False, 0.05, 0.5, 0.0, 0.0, 3, 8192),
     ("no_cache", T.POOL_NO_CACHE, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.01, 0.0, 3, 8192),
     ("small_batches", 3000, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 6, 1500),
+    # the cache kept in place (most of the old LRU survives a batch), evicting from the front
+    ("cache30k_incremental", 30000, 1 << 20, 1 << 40, False, 0.05, 0.5, 0.0, 0.0, 6, 8192),
+    ("cache30k_incremental_cut", 30000, 20000, 1 << 40, False, 0.10, 0.5, 0.0, 0.0, 4, 8192),
+    ("cache2500_rebuild_cut", 2500, 15000, 1 << 40, False, 0.20, 0.5, 0.0, 0.0, 3, 8192),
+    # thousands of far repeats x thousands of nested pairs: the Fenwick sweep, not the direct count
+    ("far_heavy_fenwick", 1000, 1 << 20, 1 << 40, False, 0.5, 0.9, 0.0, 0.0, 2, 20000),
 ]
 
 
