@@ -84,7 +84,7 @@ class WorkerPool {
   // each call has its own slot, idle workers take chunks of any slot, and every caller drains its
   // own job, so no call waits on another's.  With every slot taken the call runs inline.
   void parallel_for(uint32_t n, const std::function<void(uint32_t, uint32_t)>& fn, uint32_t min_chunk = 2048) {
-    const uint32_t parts = std::min<uint32_t>(size() * 4, std::max<uint32_t>(1, n / min_chunk));
+    const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(size() * 4, 0xffff), std::max<uint32_t>(1, n / min_chunk));
     if (parts <= 1 || th_.empty()) { if (n) fn(0, n); return; }
     Slot* s = nullptr;
     for (auto& c : slots_) {
@@ -92,10 +92,10 @@ class WorkerPool {
       if (c.owned.compare_exchange_strong(f, true)) { s = &c; break; }
     }
     if (!s) { fn(0, n); return; }
-    s->fn = &fn; s->n = n; s->parts.store(parts, std::memory_order_relaxed);
+    s->fn = &fn; s->n = n;
     s->done.store(0, std::memory_order_relaxed);
     const uint64_t seq = (s->state.load(std::memory_order_relaxed) >> 32) + 1;
-    s->state.store(seq << 32, std::memory_order_release);      // published: chunk 0 is next
+    s->state.store(seq << 32 | (uint64_t)parts << 16, std::memory_order_release);   // published: chunk 0 is next
     gen_.fetch_add(1);
     if (sleepers_.load()) {
       std::lock_guard<std::mutex> g(m_);
@@ -117,19 +117,20 @@ class WorkerPool {
  private:
   static constexpr int kSlots = 8;
   struct Slot {
-    std::atomic<uint64_t> state{0};            // (sequence << 32) | next chunk
+    // (sequence << 32) | (parts << 16) | next chunk: the CAS that claims a chunk checks all three
+    // (a separate parts word could be the next job's while this word still names the last one)
+    std::atomic<uint64_t> state{0};
     std::atomic<uint32_t> done{0};
     std::atomic<bool> owned{false};            // a caller is using the slot
     const std::function<void(uint32_t, uint32_t)>* fn = nullptr;
     uint32_t n = 0;
-    std::atomic<uint32_t> parts{0};            // read before the CAS, possibly of a finished job
   };
   // claim the slot's next chunk and run it; false when none is left.  A claimed chunk keeps the
   // job alive (its caller waits for done == parts), so fn / n / parts are read after the CAS.
   bool claim_run(Slot& s) {
     uint64_t v = s.state.load(std::memory_order_acquire);
     for (;;) {
-      const uint32_t nx = (uint32_t)v, parts = s.parts.load(std::memory_order_relaxed);
+      const uint32_t nx = (uint32_t)(v & 0xffff), parts = (uint32_t)(v >> 16) & 0xffff;
       if (nx >= parts || (v >> 32) == 0) return false;
       if (s.state.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) {
         const uint32_t n = s.n;
