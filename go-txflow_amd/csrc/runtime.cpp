@@ -1987,21 +1987,32 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
       return r;
     c->pk_cap = n;
   }
+  static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
+  std::chrono::steady_clock::time_point tp[5];
+  if (prof) tp[0] = std::chrono::steady_clock::now();
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
     memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
   }, 8192);
+  if (prof) tp[1] = std::chrono::steady_clock::now();
   HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig, c->h_pk_sig, (size_t)n * 64, hipMemcpyHostToDevice, c->key_stream));
   HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
   HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->key_stream));
   HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->key_stream));
   if (overlap) overlap();
+  if (prof) tp[2] = std::chrono::steady_clock::now();
   HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+  if (prof) tp[3] = std::chrono::steady_clock::now();
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
     for (uint32_t i = lo; i < hi; ++i)
       if (v->sig_len[i] > 64) sha256_host(sig_full + sig_full_off[i], v->sig_len[i], keys_out + (size_t)i * 32);
   }, 8192);
+  if (prof) {
+    tp[4] = std::chrono::steady_clock::now();
+    auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
+    fprintf(stderr, "[txv keys] stage=%.3f enqueue+overlap=%.3f sync=%.3f copy_out=%.3f ms\n", ms(0), ms(1), ms(2), ms(3));
+  }
   return TXV_OK;
 }
 
