@@ -444,6 +444,10 @@ def load_pmc(table_w: int, n_votes: int):
 
 TALLY_ALG_VOTE = 16       # B per vote the tally must move
 TALLY_ALG_ADDED = 244     # B per ADDED vote: 128-byte accepted row written + 116 source bytes read
+# B per vote when its 16-byte (set, validator) cell costs the whole 128-byte line a random access
+# moves (tools/microbench/tally_calib.hip: 103 B of line traffic per random 16-B cell load,
+# profiles/r03/tally_calib) + the 16 algorithmic bytes
+TALLY_LINE_VOTE = 128 + 16
 
 
 def main():
@@ -662,10 +666,16 @@ def main():
                       "alg_frac_of_8TBps": round((TALLY_ALG_VOTE + TALLY_ALG_ADDED) * wl.n / (s_ms[2] * 1e-3) / 8e12, 3),
                       "traffic_over_alg": None if not tally_bytes else
                       round(tally_bytes / ((TALLY_ALG_VOTE + TALLY_ALG_ADDED) * wl.n), 3),
+                      "line_bound_bytes_per_launch": (TALLY_LINE_VOTE + TALLY_ALG_ADDED) * wl.n,
+                      "traffic_over_line_bound": None if not tally_bytes else
+                      round(tally_bytes / ((TALLY_LINE_VOTE + TALLY_ALG_ADDED) * wl.n), 3),
                       "GBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 1e9, 1),
                       "frac_of_8TBps": None if not tally_bytes else round(tally_bytes / (s_ms[2] * 1e-3) / 8e12, 3),
                       "note": "hbm_bytes_per_launch from the committed PMC passes (2 x FETCH_SIZE + WRITE_SIZE of "
-                              "the tally kernels); alg = 16 B/vote + 244 B per ADDED vote (BASELINE.md)"},
+                              "the tally kernels; the x2 holds for its 1- to 16-byte column reads and its random "
+                              "cell accesses too: profiles/r03/tally_calib); alg = 16 B/vote + 244 B per ADDED vote "
+                              "(BASELINE.md); line bound = the same with the vote's (set, validator) cell moved as "
+                              "the 128-B line a random access costs (C2's arrival order is shuffled)"},
         }
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = {
