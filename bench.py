@@ -634,7 +634,7 @@ def main():
                                      "note": "one step alone after the timed region (no co-running kernels)"},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
                          "unit": "Tlane-op/s (int32 VALU issue)", "frac": round(achieved / VALU_PEAK, 4),
-                         "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_multi (verify pair)",
+                         "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_dyn (verify pair; txv_k_scalarmult_multi when TXV_K1B_DYNAMIC=0)",
                          "alg_bytes_per_launch": round(wl.n * VERIFY_ALG_BYTES),
                          "traffic_over_alg_bytes": None if not traffic else round(traffic / (wl.n * VERIFY_ALG_BYTES), 3),
                          "alg_lane_ops_per_vote": W_ALG,

@@ -273,6 +273,7 @@ __global__ void __launch_bounds__(256) txv_k_route_prep(FlowState fs, FlowBatch 
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n) return;
   b.ev_flag[i] = 0;
+  b.mark[i] = 0;
   // signature: [n][64] bytes -> [16][n_pad] words, zero beyond min(len, 64)
   {
     const uint32_t sl = b.sig_len[i];
@@ -498,7 +499,14 @@ __device__ __forceinline__ uint32_t cand_of(uint64_t c, uint32_t stamp) {
 
 // every vote's set id (after the new-id step); each verified pending vote posts its arrival
 // index to its (set, validator) cell: the cell then holds the FIRST verified vote of the group
-// (cells that already hold an accepted vote skip: their votes are decided without verification)
+// (cells that already hold an accepted vote skip: their votes are decided without verification).
+// The atomic's old value tells each vote whether it can be ADDED without tally_resolve reading
+// the cell again: status[i] (scratch until resolve) = 1 when the cell must be read (accepted
+// earlier, not verified, or a smaller arrival index was already there), and a vote that takes
+// the cell from a larger index k marks k.  A vote with status 0 and no mark is its cell's first
+// verified vote: ADDED.  With shuffled arrival order every cell access is a random 128-byte line
+// (profiles/r03/tally_calib), so resolve's re-read was a line per vote.
+constexpr uint8_t kReadCell = 1;
 __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b, uint32_t nb) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
@@ -510,9 +518,16 @@ __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b
   const uint32_t e = b.entry[i];
   const uint32_t s = e == TXV_NONE ? TXV_NONE : fs.tab[e].id;
   b.set[i] = s;
-  if (s == TXV_NONE || b.pre[i] != TXV_S_PENDING || b.ok[i] != 1) return;
+  if (s == TXV_NONE || b.pre[i] != TXV_S_PENDING) return;
+  if (b.ok[i] != 1) { b.status[i] = kReadCell; return; }
   TallyCell& c = fs.cell[(size_t)s * fs.n_vals + b.val[i]];
-  if (c.acc == 0) atomicMin((unsigned long long*)&c.cand, (unsigned long long)cand_key(b.stamp, i));
+  if (c.acc != 0) { b.status[i] = kReadCell; return; }
+  const uint64_t key = cand_key(b.stamp, i);
+  const uint64_t old = atomicMin((unsigned long long*)&c.cand, (unsigned long long)key);
+  uint8_t tf = 0;
+  if (old < key) tf = kReadCell;                           // an earlier vote of the batch holds it
+  else if (cand_of(old, b.stamp) != TXV_NONE) b.mark[(uint32_t)old] = 1;   // took it from a later one
+  b.status[i] = tf;
 }
 
 __device__ __forceinline__ bool pending_in_set(const FlowBatch& b, uint32_t i) {
@@ -549,9 +564,13 @@ __global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBa
     const uint8_t fl = b.flags[i];
     const bool sig64 = (fl & TXV_FLAG_SIG64) != 0;
     cell = fs.cell + (size_t)s * fs.n_vals + b.val[i];
-    const uint32_t acc = cell->acc;
+    const bool first = b.status[i] == 0 && b.mark[i] == 0;   // tally_min: its cell's first verified vote
+    const uint32_t acc = first ? 0u : cell->acc;
     uint8_t st;
-    if (acc) {                                   // accepted in an earlier batch (vote_set.go:109-114)
+    if (first) {
+      st = TXV_S_ADDED;
+      added = true;
+    } else if (acc) {                                   // accepted in an earlier batch (vote_set.go:109-114)
       st = sig64 && sig_eq_arena(fs, b, i, acc - 1) ? TXV_S_DUPLICATE : TXV_S_NONDETERMINISTIC;
     } else {
       const uint32_t f = cand_of(cell->cand, b.stamp);

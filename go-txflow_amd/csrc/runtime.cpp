@@ -93,6 +93,7 @@ struct Slot {
   // AddVote derived columns and scan scratch
   uint32_t *d_entry = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
+  uint8_t* d_mark = nullptr;
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
@@ -336,7 +337,7 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_nil, npad)) || (r = dalloc(c, &s.d_nil, npad)) ||
       (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
       (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
-      (r = dalloc(c, &s.d_ev_flag, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
+      (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
     return r;
   s.flow_cap = cap;
@@ -762,7 +763,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.nil = s.has_nil ? s.d_nil : nullptr; b.txkey = s.has_txkey ? s.d_txkey : nullptr;
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
   b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
-  b.ev_flag = s.d_ev_flag; b.blk = s.d_blk;
+  b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk;
   b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
   return b;
 }
@@ -1181,7 +1182,7 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
     hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey);
-    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); hfree(s.h_ev); hfree(s.h_sum);
+    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
@@ -1971,8 +1972,6 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
                          uint8_t* keys_out, const std::function<void()>& overlap) {
   if (!c || !v || (v->n && (!v->sig || !v->sig_len || !keys_out))) return TXV_EINVAL;
   const uint32_t n = v->n;
-  for (uint32_t i = 0; i < n; ++i)
-    if (v->sig_len[i] > 64 && (!sig_full || !sig_full_off)) { c->err = "signature > 64 bytes without sig_full"; return TXV_EINVAL; }
   // its own lock: the pool's keys (TxVotePool.CheckTx on the ingest thread) must not wait for a
   // txv_submit_votes staging on another thread, nor hold it up over the key stream's round trip;
   // the key stream takes both threads' work in enqueue order, the worker pool both threads' passes
@@ -1990,28 +1989,49 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
   std::chrono::steady_clock::time_point tp[5];
   if (prof) tp[0] = std::chrono::steady_clock::now();
-  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-    memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
-    memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
-  }, 8192);
+  // in up to 4 chunks: chunk k+1 is staged into pinned memory while chunk k is uploaded, hashed
+  // and read back on the key stream (a signature longer than 64 bytes is hashed on the host below)
+  const uint32_t K = n >= 32768 ? 4u : 1u;
+  std::atomic<bool> long_sig{false};
+  for (uint32_t k = 0; k < K; ++k) {
+    const uint32_t c0 = (uint32_t)((uint64_t)n * k / K), c1 = (uint32_t)((uint64_t)n * (k + 1) / K);
+    c->pool->parallel_for(c1 - c0, [&](uint32_t lo, uint32_t hi) {
+      lo += c0; hi += c0;
+      memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+      memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+      bool lg = false;
+      for (uint32_t i = lo; i < hi; ++i) lg |= v->sig_len[i] > 64;
+      if (lg) long_sig.store(true, std::memory_order_relaxed);
+    }, 2048);
+    HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig + (size_t)c0 * 16, c->h_pk_sig + (size_t)c0 * 16, (size_t)(c1 - c0) * 64,
+                              hipMemcpyHostToDevice, c->key_stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_pk_len + c0, c->h_pk_len + c0, (size_t)(c1 - c0) * 4, hipMemcpyHostToDevice,
+                              c->key_stream));
+    HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig + (size_t)c0 * 16, c->d_pk_len + c0, c1 - c0,
+                                   c->d_pk_keys + (size_t)c0 * 8, c->key_stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys + (size_t)c0 * 8, c->d_pk_keys + (size_t)c0 * 8, (size_t)(c1 - c0) * 32,
+                              hipMemcpyDeviceToHost, c->key_stream));
+  }
+  if (long_sig.load() && (!sig_full || !sig_full_off)) {
+    HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+    c->err = "signature > 64 bytes without sig_full";
+    return TXV_EINVAL;
+  }
   if (prof) tp[1] = std::chrono::steady_clock::now();
-  HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig, c->h_pk_sig, (size_t)n * 64, hipMemcpyHostToDevice, c->key_stream));
-  HIP_TRY(c, hipMemcpyAsync(c->d_pk_len, c->h_pk_len, (size_t)n * 4, hipMemcpyHostToDevice, c->key_stream));
-  HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig, c->d_pk_len, n, c->d_pk_keys, c->key_stream));
-  HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys, c->d_pk_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->key_stream));
   if (overlap) overlap();
   if (prof) tp[2] = std::chrono::steady_clock::now();
   HIP_TRY(c, hipStreamSynchronize(c->key_stream));
   if (prof) tp[3] = std::chrono::steady_clock::now();
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
-    for (uint32_t i = lo; i < hi; ++i)
-      if (v->sig_len[i] > 64) sha256_host(sig_full + sig_full_off[i], v->sig_len[i], keys_out + (size_t)i * 32);
-  }, 8192);
+    if (long_sig.load(std::memory_order_relaxed))
+      for (uint32_t i = lo; i < hi; ++i)
+        if (v->sig_len[i] > 64) sha256_host(sig_full + sig_full_off[i], v->sig_len[i], keys_out + (size_t)i * 32);
+  }, 2048);
   if (prof) {
     tp[4] = std::chrono::steady_clock::now();
     auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    fprintf(stderr, "[txv keys] stage=%.3f enqueue+overlap=%.3f sync=%.3f copy_out=%.3f ms\n", ms(0), ms(1), ms(2), ms(3));
+    fprintf(stderr, "[txv keys] stage+enqueue=%.3f overlap=%.3f sync=%.3f copy_out=%.3f ms\n", ms(0), ms(1), ms(2), ms(3));
   }
   return TXV_OK;
 }

@@ -169,6 +169,7 @@ struct FlowBatch {
   const uint8_t* ok;            // [n] verify verdicts (1 = valid)
   uint8_t* status;              // [n] tally status of pending votes
   uint8_t* ev_flag;             // [n] this vote's ADDED crossed 2/3 in the batch
+  uint8_t* mark;                // [n] set by tally_min when a smaller arrival index took this vote's cell
   uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
   // outputs in mapped host memory
   uint8_t* status_host;         // [n]
