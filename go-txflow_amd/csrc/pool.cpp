@@ -934,7 +934,7 @@ extern "C" {
 
 // CheckTxWithInfo for n votes whose keys (n x 32 bytes) and Size() values are known (computed on
 // the device from decoded wire records by txv_ingest_msgs, or by the caller); ctx may be NULL
-// (the batch passes then run on the calling thread)
+// (the batch passes then run on the pool's own worker threads)
 int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
                         uint8_t* status_out) {
   if (!p || (n && (!keys32 || !sizes || !status_out))) return TXV_EINVAL;

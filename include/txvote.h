@@ -370,7 +370,8 @@ int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const u
 /* CheckTxWithInfo for n votes given as (txVoteKey, TxVote.Size()) pairs in arrival order: keys32
  * n x 32 bytes (SHA-256(Signature), txvotepool.go:467-469), sizes[i] = Size() (0 when amino
  * rejects the timestamp); status_out[i] = TXV_POOL_*.  ctx (optional) lends its host workers;
- * NULL runs every pass on the calling thread.  txvotepool.go:187-261 */
+ * with NULL a batch of >= 4096 votes runs its passes on worker threads of the pool's own
+ * (TXV_HOST_THREADS, else min(16, cores)), created on the first such call.  txvotepool.go:187-261 */
 int txv_pool_check_keys(txv_pool* pool, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
                         uint8_t* status_out);
 /* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
