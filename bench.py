@@ -521,7 +521,7 @@ def main():
         f"staged in {time.perf_counter() - t_setup:.1f}s")
     red_dev = "cpu" if gloo else f"cuda:{local}"
 
-    step_ms, route_ms, verify_ms, tally_ms = [], [], [], []
+    step_ms, route_ms, verify_ms, tally_ms, k1a_ms, k1b_ms = [], [], [], [], [], []
     t_launch = {}
     launch0 = steps_rt.launch
 
@@ -534,6 +534,8 @@ def main():
         step_ms.append((time.perf_counter() - t_launch[k]) * 1e3)
         ms = ctx.slot_kernel_ms(k % DEPTH)
         route_ms.append(ms[0]); verify_ms.append(ms[1]); tally_ms.append(ms[2])
+        ka, kb = ctx.slot_verify_ms(k % DEPTH)
+        k1a_ms.append(ka); k1b_ms.append(kb)
 
     steps_rt.run(args.warmup)
     # correctness gate on the timed workload: every vote valid -> ADDED; every tx commits once,
@@ -585,12 +587,14 @@ def main():
     r_ms, v_ms, t_ms = statistics.median(route_ms), statistics.median(verify_ms), statistics.median(tally_ms)
     # the same chain run alone (one step at a time, nothing beside it): per-stage device times
     # without the pipeline's co-running kernels (the tally's HBM rate uses these)
-    solo = []
+    solo, solo_split = [], []
     for _ in range(3):
         ctx.reset_flow()
         solo.append(ctx.run_staged(0, timed=True))
+        solo_split.append(ctx.slot_verify_ms(0))
         steps_rt.finish(0)
     s_ms = [statistics.median(x[j] for x in solo) for j in range(4)]
+    s_split = [statistics.median(x[j] for x in solo_split) for j in range(2)]
     if rank == 0:
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
         # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
@@ -626,10 +630,12 @@ def main():
                                "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "") +
                                "; up to three steps enqueued (step k+1's verify overlaps step k's tally)"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
-            "device_ms_p50": {"prep": round(r_ms, 3), "verify": round(v_ms, 3), "tally_after_verify": round(t_ms, 3),
+            "device_ms_p50": {"prep": round(r_ms, 3), "verify": round(v_ms, 3), "k1a": round(statistics.median(k1a_ms), 3),
+                              "k1b": round(statistics.median(k1b_ms), 3), "tally_after_verify": round(t_ms, 3),
                               "note": "in the timed pipeline (HIP events on each stream): prep + SignBytes, K1a + K1b, "
                                       "verify end -> tally end (includes waiting for the flow stream)"},
-            "device_ms_standalone": {"prep": round(s_ms[0], 3), "verify": round(s_ms[1], 3), "tally": round(s_ms[2], 3),
+            "device_ms_standalone": {"prep": round(s_ms[0], 3), "verify": round(s_ms[1], 3), "k1a": round(s_split[0], 3),
+                                     "k1b": round(s_split[1], 3), "tally": round(s_ms[2], 3),
                                      "chain": round(s_ms[3], 3),
                                      "note": "one step alone after the timed region (no co-running kernels)"},
             "roofline": {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),

@@ -841,7 +841,10 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipEventRecord(s.ev[1], ps));
   HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
   HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
-  if (!TXV_K1A_ON_KEY_STREAM) HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
+  if (!TXV_K1A_ON_KEY_STREAM) {
+    HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
+    HIP_TRY(c, hipEventRecord(s.ev[8], c->vstream));   // K1a | K1b split (txv_slot_verify_ms)
+  }
   HIP_TRY(c, txv_launch_scalarmult(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->vstream));
   HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
@@ -1775,6 +1778,23 @@ int txv_slot_kernel_ms(txv_ctx* c, uint32_t slot, float* ms4) {
   if (!s.launched) { c->err = "slot never ran"; return TXV_ESTATE; }
   HIP_TRY(c, hipEventSynchronize(s.ev[4]));
   return slot_kernel_ms(c, s, ms4);
+}
+
+int txv_slot_verify_ms(txv_ctx* c, uint32_t slot, float* ms2) {
+  if (!c || !ms2 || slot >= kStagedSlots) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  Slot& s = c->slots[slot];
+  if (!s.launched) { c->err = "slot never ran"; return TXV_ESTATE; }
+  HIP_TRY(c, hipEventSynchronize(s.ev[4]));
+  if (TXV_K1A_ON_KEY_STREAM) {
+    HIP_TRY(c, hipEventElapsedTime(&ms2[0], s.ev[8], s.ev[1]));
+    HIP_TRY(c, hipEventElapsedTime(&ms2[1], s.ev[7], s.ev[2]));
+  } else {
+    HIP_TRY(c, hipEventElapsedTime(&ms2[0], s.ev[7], s.ev[8]));
+    HIP_TRY(c, hipEventElapsedTime(&ms2[1], s.ev[8], s.ev[2]));
+  }
+  return TXV_OK;
 }
 
 int txv_commit_bitmap(txv_ctx* c, void** dev_ptr, uint64_t* bytes) {

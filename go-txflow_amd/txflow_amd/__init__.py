@@ -160,6 +160,7 @@ def lib():
             "txv_pack_commit_state": ([vp, vp, u32], ctypes.c_int),
             "txv_set_commit_sink": ([vp, u32, vp, u32], ctypes.c_int),
             "txv_slot_kernel_ms": ([vp, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "txv_slot_verify_ms": ([vp, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "txv_read_commit_state": ([vp, vp, u32], ctypes.c_int),
             "txv_commit_state_pack_host": ([u32, vp, vp, u32, vp], ctypes.c_int),
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
@@ -186,7 +187,8 @@ EXPORTED_SYMBOLS = [
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
-    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_flow_stream", "txv_ingest_msgs"]
+    "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
+    "txv_ingest_msgs"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -595,6 +597,12 @@ class Context:
         ms = (ctypes.c_float * 4)()
         self._chk(lib().txv_slot_kernel_ms(self._h, slot, ms), "txv_slot_kernel_ms")
         return (ms[0], ms[1], ms[2], ms[3])
+
+    def slot_verify_ms(self, slot: int):
+        """(K1a, K1b) device ms of the slot's last run (the verify time split in two)"""
+        ms = (ctypes.c_float * 2)()
+        self._chk(lib().txv_slot_verify_ms(self._h, slot, ms), "txv_slot_verify_ms")
+        return (ms[0], ms[1])
 
     def read_commit_state(self, n_sets_cap: int) -> np.ndarray:
         """the device-packed commit state (txv_read_commit_state) as host bytes"""

@@ -268,12 +268,16 @@ int txv_sign_votes(txv_ctx* ctx, const txv_votes* votes, const uint32_t* signer,
  *   txv_fetch_staged.  kernel_ms_out (optional, 4 entries; makes the call
  *   wait): prep + SignBytes / verify (K1a + K1b) / tally after verify / total device time of
  *   this run, measured with HIP events on the streams the kernels run on.
- * txv_slot_kernel_ms: the same 4 times for the slot's last run, waiting for it if needed. */
+ * txv_slot_kernel_ms: the same 4 times for the slot's last run, waiting for it if needed.
+ * txv_slot_verify_ms: the verify time of the slot's last run split in two (2 entries): K1a
+ *   (challenge, SHA-512 mod L) and K1b (the double scalar multiply, encode and compare).
+ *   Measurement only, no reference counterpart. */
 int txv_stage(txv_ctx* ctx, uint32_t slot, const txv_votes* votes);
 int txv_run_staged(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
 int txv_fetch_staged(txv_ctx* ctx, uint32_t slot, uint8_t* status_out, txv_commit_event* ev_out,
                      uint32_t ev_cap, uint32_t* n_ev);
 int txv_slot_kernel_ms(txv_ctx* ctx, uint32_t slot, float* kernel_ms_out);
+int txv_slot_verify_ms(txv_ctx* ctx, uint32_t slot, float* k1a_k1b_ms_out);
 /* caller host memory the AddVote path may DMA from directly (hipHostRegister): columns of a
  * txv_votes batch lying inside a registered range skip the staging copy */
 int txv_host_register(txv_ctx* ctx, void* ptr, uint64_t bytes);
