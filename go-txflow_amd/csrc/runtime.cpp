@@ -210,6 +210,7 @@ struct txv_ctx {
   uint32_t pk_cap = 0;
   std::mutex pk_mu;                  // txv_sig_keys' buffers (not c->mu: CheckTx's keys run beside txv_submit_votes)
   uint32_t *d_pk_sig = nullptr, *d_pk_len = nullptr, *d_pk_keys = nullptr;
+  hipEvent_t pk_ev = nullptr;        // the keys' read-back on the key stream has landed
   uint32_t *h_pk_sig = nullptr, *h_pk_len = nullptr, *h_pk_keys = nullptr;
   // txv_decode_* (TxVoteMessage wire decode): staged messages, packed outputs (one D2H copy)
   uint32_t wd_n = 0, wd_cap = 0;
@@ -1204,6 +1205,7 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_wd_wire); hfree(c->h_wd_wire); dfree(c->d_wd_off); hfree(c->h_wd_off); dfree(c->d_wd_len); hfree(c->h_wd_len);
   dfree(c->d_wd_out); hfree(c->h_wd_out); dfree(c->d_wd_span); hfree(c->h_wd_span);
   for (auto& e : c->wd_ev) if (e) (void)hipEventDestroy(e);
+  if (c->pk_ev) (void)hipEventDestroy(c->pk_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->key_stream) (void)hipStreamDestroy(c->key_stream);
@@ -2006,6 +2008,7 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
       return r;
     c->pk_cap = n;
   }
+  if (!c->pk_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->pk_ev, hipEventDisableTiming));
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
   std::chrono::steady_clock::time_point tp[5];
   if (prof) tp[0] = std::chrono::steady_clock::now();
@@ -2032,15 +2035,19 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
     HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys + (size_t)c0 * 8, c->d_pk_keys + (size_t)c0 * 8, (size_t)(c1 - c0) * 32,
                               hipMemcpyDeviceToHost, c->key_stream));
   }
+  // the wait below is for this event, not the stream: a batch's prep / SignBytes that another
+  // thread's txv_submit_votes enqueues on the key stream after these keys is not waited for
+  // (work enqueued before them still is: the stream is in order)
+  HIP_TRY(c, hipEventRecord(c->pk_ev, c->key_stream));
   if (long_sig.load() && (!sig_full || !sig_full_off)) {
-    HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+    HIP_TRY(c, hipEventSynchronize(c->pk_ev));
     c->err = "signature > 64 bytes without sig_full";
     return TXV_EINVAL;
   }
   if (prof) tp[1] = std::chrono::steady_clock::now();
   if (overlap) overlap();
   if (prof) tp[2] = std::chrono::steady_clock::now();
-  HIP_TRY(c, hipStreamSynchronize(c->key_stream));
+  HIP_TRY(c, hipEventSynchronize(c->pk_ev));
   if (prof) tp[3] = std::chrono::steady_clock::now();
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
