@@ -420,6 +420,8 @@ def test_staged_two_in_flight_with_commit_sinks(oracle_lib):
         assert ctx.num_tx_sets() == n_txs
         ms = ctx.slot_kernel_ms((nb - 1) % 2)
         assert all(x >= 0 for x in ms) and ms[3] >= ms[1] > 0
+        k1a, k1b = ctx.slot_verify_ms((nb - 1) % 2)      # the verify time split at the K1a | K1b event
+        assert k1a > 0 and k1b > 0 and abs(k1a + k1b - ms[1]) < 0.01 + 0.01 * ms[1]
 
         # fresh TxFlow per launch, three slots enqueued (as bench.py runs): every run of batch 0
         # gives batch 0's results and its sink batch 0's state
