@@ -315,12 +315,17 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
 
 def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     """C5 from received wire bytes (SURVEY.md §8f.3 + §8a a15): the C5 stream as TxVoteMessage
-    bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) through txv_ingest_msgs per
-    64k-message batch -- Reactor.Receive / decodeMsg on the GPU, CheckTxWithInfo (keys and sizes
-    computed on the GPU from the decoded records, LRU on the host), TryAddVote for the admitted
-    votes built on the device from the same records: the wire bytes cross PCIe once.
-    Latency-to-commit of a tx = return of the call that reported its commit event - the call's
-    start for the batch holding its first vote (one batch at a time)."""
+    bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) through txv_ingest_submit /
+    txv_ingest_wait per 64k-message batch, two batches in flight -- Reactor.Receive / decodeMsg on
+    the GPU, CheckTxWithInfo (keys and sizes computed on the GPU from the decoded records, LRU on
+    the host), TryAddVote for the admitted votes built on the device from the same records: the
+    wire bytes cross PCIe once, and batch k+1's decode + pool stage run while batch k's TxFlow chain
+    is on the GPU (reactor.go:170-190 -> txvotepool.go:187-261 -> txflow/service.go:123-166).
+    A drain thread waits each ticket as soon as it is submitted.  Latency-to-commit of a tx =
+    return of the wait that reported its commit event - the submit's start for the batch holding
+    its first vote."""
+    import queue
+    import threading
     import txflow_amd as T
     from txflow_amd.workload import StreamWorkload, SEEDS
     ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
@@ -336,22 +341,42 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     pool.flush()
     runs = []
     for rep in range(3):
-        start, commit_t, added, ok = [], {}, 0, True
+        start, sub_ms, commit_t = [], [], {}
+        state = {"added": 0, "ok": True}
+        tickets = queue.Queue()
+        slots = threading.Semaphore(2)
+
+        def drain():
+            while True:
+                item = tickets.get()
+                if item is None:
+                    return
+                k, tk = item
+                ws, ps, fs, ev = pool.ingest_wait(tk)
+                te = time.perf_counter()
+                slots.release()
+                state["ok"] = state["ok"] and bool((ws == T.WIRE_OK).all() and np.array_equal(ps, expect[k]))
+                state["added"] += int(np.count_nonzero((fs & 0x7F) == T.ADDED))
+                for e in ev:
+                    commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
+
+        td = threading.Thread(target=drain, daemon=True)
         t0 = time.perf_counter()
+        td.start()
         for k, w in enumerate(wbs):
+            slots.acquire()
             ts = time.perf_counter()
             start.append(ts)
-            ws, ps, fs, ev = pool.ingest(w)
-            te = time.perf_counter()
-            ok = ok and bool((ws == T.WIRE_OK).all() and np.array_equal(ps, expect[k]))
-            added += int(np.count_nonzero((fs & 0x7F) == T.ADDED))
-            for e in ev:
-                commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
+            tk = pool.ingest_submit(w)
+            sub_ms.append((time.perf_counter() - ts) * 1e3)
+            tickets.put((k, tk))
+        tickets.put(None)
+        td.join()
         total = time.perf_counter() - t0
         lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
-        bl = np.diff(np.array(start + [t0 + total])) * 1e3
-        runs.append({"votes_per_s": round(wl.n / total, 1), "correct": ok and added == wl.n_unique and len(commit_t) == wl.n_txs,
-                     "p50_batch_ms": round(float(np.median(bl)), 3),
+        runs.append({"votes_per_s": round(wl.n / total, 1),
+                     "correct": state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
+                     "p50_submit_ms": round(float(np.median(sub_ms)), 3),
                      "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
                      "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None})
         ctx.reset_flow()
@@ -362,7 +387,8 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     out = dict(runs[1])
     out.update(workload=f"C5 as wire bytes: {n_vals} validators, {wl.n} TxVoteMessages ({wire_bytes / wl.n:.1f} B avg; "
                         f"{wl.n - wl.n_unique} exact replays, CacheSize {C5_CACHE}) in {batch}-message batches through "
-                        f"txv_ingest_msgs (decode -> pool -> TxFlow, device-resident)",
+                        f"txv_ingest_submit / txv_ingest_wait (decode -> pool -> TxFlow, device-resident, two batches "
+                        f"in flight; p50_submit_ms = upload + decode + keys + CheckTx of one batch)",
                passes=3, votes_per_s_passes=[r["votes_per_s"] for r in runs], correct=all(r["correct"] for r in runs),
                pcie_bytes_per_vote_up=round(wire_bytes / wl.n + 16, 1), pcie_bytes_per_vote_down=38)
     return out
@@ -584,6 +610,12 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # RCCL: the per-step commit-state all-gather's device time on the flow stream (events around
+    # it, txflow_amd/pipeline.py), for the timed region's last `depth` steps (their slots' events)
+    gather_ms = None
+    if dist is not None and not gloo:
+        gx = [steps_rt.step_exchange_ms(k) for k in range(max(0, args.steps - DEPTH), args.steps)]
+        gather_ms = round(statistics.median(gx), 4)
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -605,7 +637,7 @@ def main():
         split = verify_split(ctx, 0)
         if split:
             solo_split.append(split)
-        steps_rt.finish(0)
+        ctx.fetch_staged(0, steps_rt.batches[0].n, ev_cap=steps_rt.ev_cap, out=steps_rt.st_buf[0], evs=steps_rt.ev_buf[0])
     s_ms = [statistics.median(x[j] for x in solo) for j in range(4)]
     s_split = [statistics.median(x[j] for x in solo_split) if solo_split else float("nan") for j in range(2)]
     if rank == 0:
@@ -643,6 +675,7 @@ def main():
                                "statuses/events to host" + (" + RCCL all-gather" if world > 1 else "") +
                                "; up to three steps enqueued (step k+1's verify overlaps step k's tally)"},
             "p50_batch_ms": round(statistics.median(step_ms), 3),
+            "gather_ms": gather_ms,
             "device_ms_p50": {"prep": round(r_ms, 3), "verify": round(v_ms, 3), "k1a": round(statistics.median(k1a_ms), 3) if k1a_ms else None,
                               "k1b": round(statistics.median(k1b_ms), 3) if k1b_ms else None, "tally_after_verify": round(t_ms, 3),
                               "note": "in the timed pipeline (HIP events on each stream): prep + SignBytes, K1a + K1b, "

@@ -16,6 +16,7 @@
 // per group of blocks (blocks b, b+8, ... share an XCD) and runs at 2 waves/SIMD with V = 8
 // (batches of >= 768K votes) or V = 4 (configured); smaller batches run one vote per lane
 // (txv_k_scalarmult_points + txv_k_batch_encode, 4 waves/SIMD).
+#include <algorithm>
 #include <cstdlib>
 
 #include "ed25519_dev.h"
@@ -1036,11 +1037,13 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
           // persistent: every resident slot (256-thread blocks, TXV_K1B_DYN_WAVES per SIMD)
           // TXV_K1B_DYN_BLOCKS = blocks per CU x 100 (default: every slot); fewer leave SIMDs with
           // room for the neighbouring batches' TxFlow kernels
-          static int cus = 0, per100 = 0;
-          if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
-          if (!per100) per100 = getenv("TXV_K1B_DYN_BLOCKS") ? atoi(getenv("TXV_K1B_DYN_BLOCKS")) : 100 * TXV_K1B_DYN_WAVES;
+          // (grid capped at the park buffer's capacity: one V-slot park per wave)
+          static const int per100 = getenv("TXV_K1B_DYN_BLOCKS") ? atoi(getenv("TXV_K1B_DYN_BLOCKS")) : 100 * TXV_K1B_DYN_WAVES;
+          const uint32_t want = std::max<uint32_t>(8, args->n_cus * (uint32_t)std::max(per100, 1) / 100u);
+          const uint32_t grid3 = std::min<uint32_t>(want, args->park_waves / 4u);
+          if (!grid3) return hipErrorInvalidValue;
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<256, WB, WA, 8, TXV_K1B_DYN_WAVES>),
-                             dim3(std::max<uint32_t>(8, (uint32_t)cus * (uint32_t)per100 / 100u)), dim3(256), 0, st, *args);
+                             dim3(grid3), dim3(256), 0, st, *args);
         } else {
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
         }

@@ -53,8 +53,8 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
 constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0, 1 also the submit ring)
-constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest
-constexpr uint32_t kSlots = 7;
+constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6, 7)
+constexpr uint32_t kSlots = 8;
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
@@ -222,12 +222,27 @@ struct txv_ctx {
   uint8_t *d_wd_out = nullptr, *h_wd_out = nullptr;
   uint64_t *d_wd_span = nullptr, *h_wd_span = nullptr;   // [chunks][2] byte span of each 128-message chunk
   hipEvent_t wd_ev[2] = {nullptr, nullptr};
-  // txv_ingest_msgs (wire bytes -> pool -> TxFlow, device-resident): per-message status, keys,
-  // sizes and the longest TxHash (device + pinned host), the admitted messages' indices
-  uint32_t ing_cap = 0;
-  uint8_t *d_ing_status = nullptr, *h_ing_status = nullptr;
-  uint32_t *d_ing_keys = nullptr, *h_ing_keys = nullptr, *d_ing_sizes = nullptr, *h_ing_sizes = nullptr;
-  uint32_t *d_ing_list = nullptr, *h_ing_list = nullptr, *d_ing_max = nullptr, *h_ing_max = nullptr;
+  // txv_ingest_submit / txv_ingest_wait (wire bytes -> pool -> TxFlow, device-resident): a ring of
+  // two batches (slots kIngestSlot + 0/1), each with its own offsets, decode records (they stay in
+  // HBM until the admitted votes' columns are built from them), per-message status / pool key /
+  // TxVote.Size, the longest TxHash and the admitted messages' indices
+  struct Ingest {
+    uint32_t cap = 0;
+    uint64_t *d_off = nullptr, *h_off = nullptr;
+    uint32_t *d_len = nullptr, *h_len = nullptr;
+    uint8_t* d_rec = nullptr;
+    uint64_t *d_span = nullptr, *h_span = nullptr;
+    uint8_t *d_status = nullptr, *h_status = nullptr;
+    uint32_t *d_keys = nullptr, *h_keys = nullptr, *d_sizes = nullptr, *h_sizes = nullptr;
+    uint32_t *d_list = nullptr, *h_list = nullptr, *d_max = nullptr, *h_max = nullptr;
+    hipEvent_t kev = nullptr;      // statuses, keys and sizes are back in pinned memory
+    uint64_t ticket = 0;           // in flight (0 = free); guarded by mu
+    uint32_t n = 0, n_adm = 0;     // messages of the batch; votes the pool admitted (h_list)
+    int flow_err = 0;              // the admitted votes' AddVote chain could not be enqueued
+    std::string flow_msg;
+  } ing[2];
+  std::mutex ing_mu;               // ingest submits one at a time: pool order = TxFlow order
+  uint64_t ing_next = 1;           // next ingest ticket; guarded by mu
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -528,6 +543,8 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   a.order = by_val ? s.d_order : nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
   a.park = c->d_park;
+  a.park_waves = (uint32_t)(c->park_words / ((size_t)8 * TXV_PARK_WORDS * 64));
+  a.n_cus = (uint32_t)c->n_cus;
   a.wctr = c->d_wctr;
   a.rpts = s.d_rpts;
   a.lane_votes = c->lane_votes;
@@ -1105,6 +1122,17 @@ hipError_t create_streams(txv_ctx* c) {
     if ((e = hipStreamCreateWithFlags(&c->key_stream, hipStreamNonBlocking)) != hipSuccess) return e;
   }
   if ((e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) return e;
+  // TXV_VERIFY_CUS_OFF=N: the verify stream leaves N CUs (spread over the XCDs) to the flow and
+  // key streams' kernels, which otherwise find no VGPRs beside a 3-wave/SIMD K1b
+  const char* vo = getenv("TXV_VERIFY_CUS_OFF");
+  const int off_cus = vo ? atoi(vo) : 0;
+  if (off_cus > 0 && off_cus < ncu) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+    const int stride = ncu / off_cus;
+    for (int i = 0, k = 0; i < ncu && k < off_cus; i += stride, ++k) mask[i / 32] &= ~(1u << (i % 32));
+    return hipExtStreamCreateWithCUMask(&c->vstream, (uint32_t)mask.size(), mask.data());
+  }
   const char* vp = getenv("TXV_VSTREAM_PRIO");
   if (vp && atoi(vp) > 0) {
     int lo = 0, hi = 0;
@@ -1205,6 +1233,12 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_wd_wire); hfree(c->h_wd_wire); dfree(c->d_wd_off); hfree(c->h_wd_off); dfree(c->d_wd_len); hfree(c->h_wd_len);
   dfree(c->d_wd_out); hfree(c->h_wd_out); dfree(c->d_wd_span); hfree(c->h_wd_span);
   for (auto& e : c->wd_ev) if (e) (void)hipEventDestroy(e);
+  for (auto& g : c->ing) {
+    dfree(g.d_off); hfree(g.h_off); dfree(g.d_len); hfree(g.h_len); dfree(g.d_rec); dfree(g.d_span); hfree(g.h_span);
+    dfree(g.d_status); hfree(g.h_status); dfree(g.d_keys); hfree(g.h_keys); dfree(g.d_sizes); hfree(g.h_sizes);
+    dfree(g.d_list); hfree(g.h_list); dfree(g.d_max); hfree(g.h_max);
+    if (g.kev) (void)hipEventDestroy(g.kev);
+  }
   if (c->pk_ev) (void)hipEventDestroy(c->pk_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -2356,166 +2390,256 @@ uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
 namespace {
 
 // Reactor.Receive -> CheckTxWithInfo -> TryAddVote for one batch of received messages, with the
-// decoded votes kept in HBM (txv_ingest_msgs): c->mu is held.
-int ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
-                const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint8_t* flow_status,
-                txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev) {
-  if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
-  if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
-  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
-  if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
-  for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernels trust these
-    if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
-      c->err = "message " + std::to_string(i) + " outside the wire buffer";
-      return TXV_EINVAL;
-    }
-  if (n_ev) *n_ev = 0;
-  if (!n) return TXV_OK;
-  HostTimer ht(c->profile_host);
-  Slot& s = c->slots[kIngestSlot];
+// decoded votes kept in HBM, split for pipelining (txv_ingest_submit / txv_ingest_wait):
+//   1 (c->mu)  upload the wire bytes into ring slot j's arena, decode (kernels_wire.hip) into
+//              records in HBM, then per decoded message its pool key, TxVote.Size() and status;
+//              only those cross PCIe back
+//   2 (no c->mu; c->ing_mu keeps the submits in order) wait for the keys, CheckTxWithInfo over
+//              the decoded messages in arrival order on the host (pool.cpp)
+//   3 (c->mu)  the admitted votes' TxVote columns built on the device from the same records and
+//              the AddVote chain of txv_add_votes enqueued (run_slot), not waited for
+// so batch k+1's upload, decode and pool stage run while batch k's TxFlow chain is on the GPU, and
+// other threads may submit or wait AddVote batches while a wire batch is in the pool stage.
+// An error after the pool stage (its votes are in the pool already) is kept for the wait, which
+// reports TXV_FLOW_NOT_RUN for the admitted votes instead of dropping them silently.
+int ingest_alloc(txv_ctx* c, txv_ctx::Ingest& g, Slot& s, uint64_t wire_bytes, uint32_t n) {
   int r;
-  // buffers: decode records / offsets (shared with txv_decode_*), the per-message outputs
-  if (n > c->wd_cap) {
+  if (n > g.cap) {
     const uint32_t cap = std::max<uint32_t>(n, 1024);
-    if ((r = dalloc(c, &c->d_wd_off, cap)) || (r = halloc(c, &c->h_wd_off, cap)) || (r = dalloc(c, &c->d_wd_len, cap)) ||
-        (r = halloc(c, &c->h_wd_len, cap)) || (r = dalloc(c, &c->d_wd_out, wire_out_bytes(cap))) ||
-        (r = halloc(c, &c->h_wd_out, wire_out_bytes(cap))) ||
-        (r = dalloc(c, &c->d_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))) ||
-        (r = halloc(c, &c->h_wd_span, (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK))))
+    const size_t nch = (size_t)2 * ((cap + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK);
+    if ((r = dalloc(c, &g.d_off, cap)) || (r = halloc(c, &g.h_off, cap)) || (r = dalloc(c, &g.d_len, cap)) ||
+        (r = halloc(c, &g.h_len, cap)) || (r = dalloc(c, &g.d_rec, wire_out_bytes(cap))) ||
+        (r = dalloc(c, &g.d_span, nch)) || (r = halloc(c, &g.h_span, nch)) ||
+        (r = dalloc(c, &g.d_status, cap)) || (r = halloc(c, &g.h_status, cap)) ||
+        (r = dalloc(c, &g.d_keys, (size_t)cap * 8)) || (r = halloc(c, &g.h_keys, (size_t)cap * 8)) ||
+        (r = dalloc(c, &g.d_sizes, cap)) || (r = halloc(c, &g.h_sizes, cap)) ||
+        (r = dalloc(c, &g.d_list, cap)) || (r = halloc(c, &g.h_list, cap)) ||
+        (r = dalloc(c, &g.d_max, 1)) || (r = halloc(c, &g.h_max, 1)))
       return r;
-    c->wd_cap = cap;
+    g.cap = cap;
   }
-  if (n > c->ing_cap) {
-    const uint32_t cap = std::max<uint32_t>(n, 1024);
-    if ((r = dalloc(c, &c->d_ing_status, cap)) || (r = halloc(c, &c->h_ing_status, cap)) ||
-        (r = dalloc(c, &c->d_ing_keys, (size_t)cap * 8)) || (r = halloc(c, &c->h_ing_keys, (size_t)cap * 8)) ||
-        (r = dalloc(c, &c->d_ing_sizes, cap)) || (r = halloc(c, &c->h_ing_sizes, cap)) ||
-        (r = dalloc(c, &c->d_ing_list, cap)) || (r = halloc(c, &c->h_ing_list, cap)) ||
-        (r = dalloc(c, &c->d_ing_max, 1)) || (r = halloc(c, &c->h_ing_max, 1)))
-      return r;
-    c->ing_cap = cap;
-  }
+  if (!g.kev) HIP_TRY(c, hipEventCreateWithFlags(&g.kev, hipEventDisableTiming));
   // the wire bytes go straight into the slot's TxHash arena: the decoded TxHash offsets index it
   if (wire_bytes + 128 > s.arena_cap) {
     const size_t cap = std::max<size_t>((size_t)wire_bytes + 128, s.arena_cap * 2);
     if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
     s.arena_cap = cap;
   }
-  if ((r = ensure_flow_slot(c, s, n))) return r;
-  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->key_stream, s.ev[4], 0));   // the slot's last chain ended
-  c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
-    const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
-    memcpy(s.h_arena + a, wire + a, b - a);
-  }, 16);
-  memset(s.h_arena + wire_bytes, 0, 128);
-  memcpy(c->h_wd_off, msg_off, (size_t)n * 8);
-  memcpy(c->h_wd_len, msg_len, (size_t)n * 4);
-  const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
-  c->pool->parallel_for(n_chunks, [&](uint32_t lo_c, uint32_t hi_c) {
-    for (uint32_t k = lo_c; k < hi_c; ++k) {
-      uint64_t lo = ~0ull, hi = 0;
-      for (uint32_t i = k * TXV_WIRE_BLOCK; i < std::min<uint32_t>(n, (k + 1) * TXV_WIRE_BLOCK); ++i)
-        if (msg_len[i]) { lo = std::min(lo, msg_off[i]); hi = std::max(hi, msg_off[i] + msg_len[i]); }
-      if (hi == 0) lo = 0;
-      c->h_wd_span[2 * k] = lo & ~15ull;
-      c->h_wd_span[2 * k + 1] = hi;
+  return ensure_flow_slot(c, s, n);
+}
+
+int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                  const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint64_t* ticket) {
+  if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
+  for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernels trust these
+    if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
+      c->err = "message " + std::to_string(i) + " outside the wire buffer";
+      return TXV_EINVAL;
     }
-  }, 64);
-  *c->h_ing_max = 0;
-  hipStream_t ks = c->key_stream;
-  HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->d_wd_off, c->h_wd_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->d_wd_len, c->h_wd_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->d_wd_span, c->h_wd_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->d_ing_max, c->h_ing_max, 4, hipMemcpyHostToDevice, ks));
-  ht.mark("upload");
-  // decodeMsg (kernels_wire.hip) into records in HBM, then per decoded message its pool key and
-  // TxVote.Size(); only statuses, keys and sizes cross PCIe
-  WireArgs a{};
-  a.n = n;
-  a.max_msg_bytes = txv_pool_max_msg_bytes(p);
-  txvote_msg_disfix(&a.disamb, &a.prefix);
-  a.wire = s.d_arena_th; a.off = c->d_wd_off; a.len = c->d_wd_len;
-  a.rec = reinterpret_cast<uint32_t*>(c->d_wd_out);
-  a.n_chunks = n_chunks;
-  a.span = c->d_wd_span;
-  HIP_TRY(c, txv_launch_decode_msgs(&a, (uint32_t)c->n_cus * 5u, ks));
-  HIP_TRY(c, txv_launch_rec_keys(a.rec, s.d_arena_th, n, c->d_ing_status, c->d_ing_keys, c->d_ing_sizes, c->d_ing_max, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->h_ing_status, c->d_ing_status, n, hipMemcpyDeviceToHost, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->h_ing_keys, c->d_ing_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->h_ing_sizes, c->d_ing_sizes, (size_t)n * 4, hipMemcpyDeviceToHost, ks));
-  HIP_TRY(c, hipMemcpyAsync(c->h_ing_max, c->d_ing_max, 4, hipMemcpyDeviceToHost, ks));
-  HIP_TRY(c, hipStreamSynchronize(ks));
+  std::lock_guard<std::mutex> order(c->ing_mu);
+  HostTimer ht(c->profile_host);
+  uint64_t t;
+  uint32_t j;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+    if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+    if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+    t = c->ing_next;
+    j = (uint32_t)((t - 1) % 2);
+    if (c->ing[j].ticket) { c->err = "two ingest batches already in flight: wait for the older one first"; return TXV_ESTATE; }
+  }
+  // ring slot j is free (its last ticket was waited: no DMA or kernel of it is pending), and only
+  // this submitter (c->ing_mu) touches it until its ticket is published
+  txv_ctx::Ingest& g = c->ing[j];
+  Slot& s = c->slots[kIngestSlot + j];
+  int r;
+  if ((r = ingest_alloc(c, g, s, wire_bytes, n))) return r;
+  g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear();
+  const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
+  if (n) {
+    c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
+      const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
+      memcpy(s.h_arena + a, wire + a, b - a);
+    }, 16);
+    memset(s.h_arena + wire_bytes, 0, 128);
+    memcpy(g.h_off, msg_off, (size_t)n * 8);
+    memcpy(g.h_len, msg_len, (size_t)n * 4);
+    c->pool->parallel_for(n_chunks, [&](uint32_t lo_c, uint32_t hi_c) {
+      for (uint32_t k = lo_c; k < hi_c; ++k) {
+        uint64_t lo = ~0ull, hi = 0;
+        for (uint32_t i = k * TXV_WIRE_BLOCK; i < std::min<uint32_t>(n, (k + 1) * TXV_WIRE_BLOCK); ++i)
+          if (msg_len[i]) { lo = std::min(lo, msg_off[i]); hi = std::max(hi, msg_off[i] + msg_len[i]); }
+        if (hi == 0) lo = 0;
+        g.h_span[2 * k] = lo & ~15ull;
+        g.h_span[2 * k + 1] = hi;
+      }
+    }, 64);
+    *g.h_max = 0;
+    ht.mark("stage");
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t ks = c->key_stream;
+    if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[4], 0));   // the slot's last chain ended
+    HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.d_off, g.h_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.d_len, g.h_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.d_span, g.h_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.d_max, g.h_max, 4, hipMemcpyHostToDevice, ks));
+    WireArgs a{};
+    a.n = n;
+    a.max_msg_bytes = txv_pool_max_msg_bytes(p);
+    txvote_msg_disfix(&a.disamb, &a.prefix);
+    a.wire = s.d_arena_th; a.off = g.d_off; a.len = g.d_len;
+    a.rec = reinterpret_cast<uint32_t*>(g.d_rec);
+    a.n_chunks = n_chunks;
+    a.span = g.d_span;
+    HIP_TRY(c, txv_launch_decode_msgs(&a, (uint32_t)c->n_cus * 5u, ks));
+    HIP_TRY(c, txv_launch_rec_keys(a.rec, s.d_arena_th, n, g.d_status, g.d_keys, g.d_sizes, g.d_max, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.h_status, g.d_status, n, hipMemcpyDeviceToHost, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.h_keys, g.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.h_sizes, g.d_sizes, (size_t)n * 4, hipMemcpyDeviceToHost, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.h_max, g.d_max, 4, hipMemcpyDeviceToHost, ks));
+    HIP_TRY(c, hipEventRecord(g.kev, ks));
+  }
+  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
   ht.mark("decode_keys");
   // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it)
   std::vector<uint32_t> ok;
   ok.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
-    if (wire_status) wire_status[i] = c->h_ing_status[i];
+    if (wire_status) wire_status[i] = g.h_status[i];
     if (pool_status) pool_status[i] = TXV_POOL_NOT_CHECKED;
-    if (flow_status) flow_status[i] = TXV_FLOW_NOT_ADDED;
-    if (c->h_ing_status[i] == TXV_WIRE_OK) ok.push_back(i);
+    if (g.h_status[i] == TXV_WIRE_OK) ok.push_back(i);
   }
   const uint32_t m = (uint32_t)ok.size();
   std::vector<uint8_t> keys((size_t)m * 32), pst(m);
   std::vector<uint32_t> sizes(m);
   c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t j = lo; j < hi; ++j) {
-      memcpy(keys.data() + (size_t)j * 32, c->h_ing_keys + (size_t)ok[j] * 8, 32);
-      sizes[j] = c->h_ing_sizes[ok[j]];
+    for (uint32_t q = lo; q < hi; ++q) {
+      memcpy(keys.data() + (size_t)q * 32, g.h_keys + (size_t)ok[q] * 8, 32);
+      sizes[q] = g.h_sizes[ok[q]];
     }
   }, 8192);
-  if ((r = txv_pool_check_keys(p, c, keys.data(), sizes.data(), m, pst.data()))) return r;
+  if ((r = txv_pool_check_keys(p, c, keys.data(), sizes.data(), m, pst.data()))) return r;   // the pool is unchanged
   uint32_t n_adm = 0;
-  for (uint32_t j = 0; j < m; ++j) {
-    if (pool_status) pool_status[ok[j]] = pst[j];
-    if (pst[j] == TXV_POOL_OK) c->h_ing_list[n_adm++] = ok[j];
+  for (uint32_t q = 0; q < m; ++q) {
+    if (pool_status) pool_status[ok[q]] = pst[q];
+    if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
   }
+  g.n_adm = n_adm;
   ht.mark("pool");
-  if (!n_adm) return TXV_OK;
-  // the admitted votes -> the slot's TxVote columns on the device, then the AddVote chain
-  const uint32_t chain_len = (uint32_t)c->chain.size();
-  const uint32_t mw = (signbytes_bound(*c->h_ing_max, chain_len) + 7) / 8;
-  if ((r = ensure_slot(c, s, n_adm, mw))) return r;
-  HIP_TRY(c, hipMemcpyAsync(c->d_ing_list, c->h_ing_list, (size_t)n_adm * 4, hipMemcpyHostToDevice, ks));
-  FlowCols fc{s.d_fh, s.d_fs, s.d_fn, s.d_fo, s.d_fl, s.d_addr, s.d_addr_len, s.d_sigraw, s.d_sig_len, s.d_txkey};
-  HIP_TRY(c, txv_launch_rec_to_flow(a.rec, c->d_ing_list, n_adm, &fc, ks));
-  HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's kernels wait for this
-  s.n = n_adm; s.n_pad = (n_adm + 63) / 64 * 64; s.msg_words = mw;
-  s.has_nil = false;
-  s.has_txkey = true;
-  s.seq_base = c->seq_next;
-  c->seq_next += n_adm;
-  s.staged = true; s.ran = false;
-  if ((r = run_slot(c, kIngestSlot, nullptr))) return r;
-  std::vector<uint8_t> fst(n_adm);
-  std::vector<txv_commit_event> evs(ev_out ? std::min(ev_cap, n_adm) : 0);
-  uint32_t ne = 0;
-  if ((r = fetch_slot(c, kIngestSlot, fst.data(), evs.data(), (uint32_t)evs.size(), &ne))) return r;
-  ht.mark("flow");
-  if (flow_status)
-    for (uint32_t j = 0; j < n_adm; ++j) flow_status[c->h_ing_list[j]] = fst[j];
-  for (uint32_t e = 0; e < std::min<uint32_t>(ne, (uint32_t)evs.size()); ++e) {   // batch index -> message index
-    txv_commit_event x = evs[e];
-    x.vote_index = c->h_ing_list[x.vote_index];
-    ev_out[e] = x;
+  // from here on the admitted votes are in the pool: the batch gets its ticket whatever happens,
+  // and an error is reported by its wait together with the votes it concerns
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto flow_stage = [&]() -> int {
+    if (!n_adm) return TXV_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+    const uint32_t chain_len = (uint32_t)c->chain.size();
+    const uint32_t mw = (signbytes_bound(*g.h_max, chain_len) + 7) / 8;
+    int rr;
+    if ((rr = ensure_slot(c, s, n_adm, mw))) return rr;
+    hipStream_t ks = c->key_stream;
+    HIP_TRY(c, hipMemcpyAsync(g.d_list, g.h_list, (size_t)n_adm * 4, hipMemcpyHostToDevice, ks));
+    FlowCols fc{s.d_fh, s.d_fs, s.d_fn, s.d_fo, s.d_fl, s.d_addr, s.d_addr_len, s.d_sigraw, s.d_sig_len, s.d_txkey};
+    HIP_TRY(c, txv_launch_rec_to_flow(reinterpret_cast<const uint32_t*>(g.d_rec), g.d_list, n_adm, &fc, ks));
+    HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's kernels wait for this
+    s.n = n_adm; s.n_pad = (n_adm + 63) / 64 * 64; s.msg_words = mw;
+    s.has_nil = false;
+    s.has_txkey = true;
+    s.seq_base = c->seq_next;
+    c->seq_next += n_adm;
+    s.staged = true; s.ran = false;
+    return run_slot(c, kIngestSlot + j, nullptr);
+  };
+  if ((r = flow_stage())) {
+    g.flow_err = r;
+    g.flow_msg = c->err.copy();
   }
-  if (n_ev) *n_ev = ne;
+  ht.mark("flow_enqueue");
+  g.ticket = t;
+  c->ing_next = t + 1;
+  *ticket = t;
   return TXV_OK;
+}
+
+int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
+                uint32_t* n_ev) {
+  if (n_ev) *n_ev = 0;
+  if (!ticket) return TXV_EINVAL;
+  const uint32_t j = (uint32_t)((ticket - 1) % 2);
+  txv_ctx::Ingest& g = c->ing[j];
+  Slot& s = c->slots[kIngestSlot + j];
+  hipEvent_t done = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (g.ticket != ticket) { c->err = "unknown or already waited ingest ticket"; return TXV_ESTATE; }
+    const txv_ctx::Ingest& o = c->ing[1 - j];
+    if (o.ticket && o.ticket < ticket) { c->err = "ingest tickets must be waited in submission order"; return TXV_ESTATE; }
+    if (!g.flow_err && g.n_adm && s.ran) done = s.ev[4];
+  }
+  // the batch's chain ends without c->mu held (a submit's device stages may run meanwhile); the
+  // slot is not reused before this ticket is released below
+  if (done) HIP_TRY(c, hipEventSynchronize(done));
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int r = g.flow_err;
+  std::vector<uint8_t> fst(g.n_adm);
+  std::vector<txv_commit_event> evs;
+  uint32_t ne = 0;
+  if (!r && g.n_adm) {
+    evs.resize(ev_out ? std::min(ev_cap, g.n_adm) : 0);
+    r = fetch_slot(c, kIngestSlot + j, fst.data(), evs.data(), (uint32_t)evs.size(), &ne);
+  } else if (r) {
+    c->err = g.flow_msg;
+  }
+  if (flow_status) {
+    for (uint32_t i = 0; i < g.n; ++i) flow_status[i] = TXV_FLOW_NOT_ADDED;
+    for (uint32_t q = 0; q < g.n_adm; ++q) flow_status[g.h_list[q]] = r ? (uint8_t)TXV_FLOW_NOT_RUN : fst[q];
+  }
+  if (!r) {
+    for (uint32_t e = 0; e < std::min<uint32_t>(ne, (uint32_t)evs.size()); ++e) {   // batch index -> message index
+      txv_commit_event x = evs[e];
+      x.vote_index = g.h_list[x.vote_index];
+      ev_out[e] = x;
+    }
+    if (n_ev) *n_ev = ne;
+  }
+  g.ticket = 0;
+  return r;
 }
 
 }  // namespace
 
 extern "C" {
 
+int txv_ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                      const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint64_t* ticket) {
+  if (!c || !p || !ticket || (n && (!wire || !msg_off || !msg_len))) return TXV_EINVAL;
+  *ticket = 0;
+  return ingest_submit(c, p, wire, wire_bytes, msg_off, msg_len, n, wire_status, pool_status, ticket);
+}
+
+int txv_ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
+                    uint32_t* n_ev) {
+  if (!c) return TXV_EINVAL;
+  return ingest_wait(c, ticket, flow_status, ev_out, ev_cap, n_ev);
+}
+
 int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
                     const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status,
                     uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap, uint32_t* n_ev) {
   if (!c || !p || (n && (!wire || !msg_off || !msg_len))) return TXV_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
-  return ingest_msgs(c, p, wire, wire_bytes, msg_off, msg_len, n, wire_status, pool_status, flow_status, ev_out,
-                     ev_cap, n_ev);
+  if (n_ev) *n_ev = 0;
+  uint64_t t = 0;
+  const int r = ingest_submit(c, p, wire, wire_bytes, msg_off, msg_len, n, wire_status, pool_status, &t);
+  if (r) {
+    if (flow_status)
+      for (uint32_t i = 0; i < n; ++i) flow_status[i] = TXV_FLOW_NOT_ADDED;
+    return r;
+  }
+  return ingest_wait(c, t, flow_status, ev_out, ev_cap, n_ev);
 }
 
 }  // extern "C"

@@ -40,6 +40,8 @@ struct VerifyArgs {
                                // then the exclusive prefix product of the lane's Z (K1b -> K1c)
   uint32_t* wctr;              // [8 * 16] chunk counters of the work-stealing K1b (one per XCD
                                // range, 64 B apart), zeroed before each launch
+  uint32_t park_waves;         // waves the park buffer holds (V = 8 slots each): caps persistent grids
+  uint32_t n_cus;              // CUs of the context's device
 };
 
 #define TXV_PARK_WORDS 33          // X, Y, prefix product, Z of one parked vote; its vote index + 1

@@ -147,6 +147,9 @@ def lib():
             "txv_pool_receive": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp], ctypes.c_int),
             "txv_ingest_msgs": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp, vp, vp, u32, ctypes.POINTER(u32)],
                                 ctypes.c_int),
+            "txv_ingest_submit": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp, ctypes.POINTER(ctypes.c_uint64)],
+                                  ctypes.c_int),
+            "txv_ingest_wait": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
@@ -188,7 +191,7 @@ EXPORTED_SYMBOLS = [
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
-    "txv_ingest_msgs"]
+    "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -790,6 +793,25 @@ def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):
 
 POOL_OK, POOL_ERR_FULL, POOL_ERR_TOO_LARGE, POOL_ERR_IN_CACHE, POOL_ERR_ENCODING = range(5)
 FLOW_NOT_ADDED = 0xFE   # TXV_FLOW_NOT_ADDED: a message the pool did not admit (txv_ingest_msgs)
+FLOW_NOT_RUN = 0xFD     # TXV_FLOW_NOT_RUN: admitted by the pool, but the TxFlow stage failed (error returned)
+
+
+class IngestError(TxvInfraError):
+    """txv_ingest_wait / txv_ingest_msgs failed after the pool stage: `result` holds the
+    (wire status, pool status, flow status, events) the call reported -- the pool-admitted votes
+    carry FLOW_NOT_RUN (they are in the pool, not in TxFlow) -- and `rc` the return code."""
+
+    def __init__(self, msg, rc, result):
+        super().__init__(msg)
+        self.rc = rc
+        self.result = result
+
+
+class IngestTicket:
+    """one txv_ingest_submit batch in flight: wire / pool statuses are final at submit"""
+
+    def __init__(self, ticket: int, n: int, ws: np.ndarray, ps: np.ndarray):
+        self.ticket, self.n, self.wire_status, self.pool_status = ticket, n, ws, ps
 POOL_NO_CACHE = 0xFFFFFFFF
 POOL_WAL = 0x1      # TXV_POOL_WAL
 
@@ -822,8 +844,8 @@ class TxVotePool:
         out = np.zeros(max(batch.n, 1), np.uint8)
         full, off = _long_sig_arena(batch, long_sigs)
         vs = batch.c_struct()
-        self.ctx._chk(lib().txv_pool_check(self._h, self.ctx._h, ctypes.byref(vs), full, off, out.ctypes.data),
-                      "txv_pool_check")
+        ctx = self._ctx_or_raise("check_batch")
+        ctx._chk(lib().txv_pool_check(self._h, ctx._h, ctypes.byref(vs), full, off, out.ctypes.data), "txv_pool_check")
         return out[:batch.n]
 
     def check_keys(self, keys: np.ndarray, sizes: np.ndarray) -> np.ndarray:
@@ -844,15 +866,24 @@ class TxVotePool:
         (wire status TXV_WIRE_*, pool status TXV_POOL_* or POOL_NOT_CHECKED) per message."""
         ws = np.zeros(max(wb.n, 1), np.uint8)
         ps = np.zeros(max(wb.n, 1), np.uint8)
-        self.ctx._chk(lib().txv_pool_receive(self._h, self.ctx._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
-                                             wb.len.ctypes.data, wb.n, ws.ctypes.data, ps.ctypes.data),
-                      "txv_pool_receive")
+        ctx = self._ctx_or_raise("receive")
+        ctx._chk(lib().txv_pool_receive(self._h, ctx._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                        wb.len.ctypes.data, wb.n, ws.ctypes.data, ps.ctypes.data), "txv_pool_receive")
         return ws[:wb.n], ps[:wb.n]
+
+    def _ctx_or_raise(self, what: str):
+        if self.ctx is None:
+            raise ValueError(f"TxVotePool.{what} needs a Context (this pool was made with ctx=None: only "
+                             "check_keys runs without one)")
+        return self.ctx
 
     def ingest(self, wb: WireBatch, ev_cap: int = 0):
         """txv_ingest_msgs: Reactor.Receive -> CheckTxWithInfo -> TxFlow.TryAddVote for a batch of
         received messages with the decoded votes kept on the device.  Returns (wire status, pool
-        status, flow status (FLOW_NOT_ADDED unless admitted), commit events by message index)."""
+        status, flow status (FLOW_NOT_ADDED unless admitted), commit events by message index).
+        After the pool stage a failure raises IngestError carrying those arrays (FLOW_NOT_RUN for
+        the admitted votes)."""
+        ctx = self._ctx_or_raise("ingest")
         n = wb.n
         ws = np.zeros(max(n, 1), np.uint8)
         ps = np.zeros(max(n, 1), np.uint8)
@@ -860,16 +891,52 @@ class TxVotePool:
         ev_cap = ev_cap or max(n, 1)
         evs = np.zeros(ev_cap, EVENT_DTYPE)
         nev = ctypes.c_uint32()
-        self.ctx._chk(lib().txv_ingest_msgs(self.ctx._h, self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
-                                            wb.len.ctypes.data, n, ws.ctypes.data, ps.ctypes.data, fs.ctypes.data,
-                                            evs.ctypes.data, ev_cap, ctypes.byref(nev)), "txv_ingest_msgs")
-        return ws[:n], ps[:n], fs[:n], evs[:min(nev.value, ev_cap)]
+        rc = lib().txv_ingest_msgs(ctx._h, self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                   wb.len.ctypes.data, n, ws.ctypes.data, ps.ctypes.data, fs.ctypes.data,
+                                   evs.ctypes.data, ev_cap, ctypes.byref(nev))
+        res = (ws[:n], ps[:n], fs[:n], evs[:min(nev.value, ev_cap)])
+        if rc < 0:
+            msg = f"txv_ingest_msgs failed ({rc}): {lib().txv_last_error(ctx._h).decode()}"
+            if (fs[:n] == FLOW_NOT_RUN).any():
+                raise IngestError(msg, rc, res)
+            raise TxvInfraError(msg)
+        return res
+
+    def ingest_submit(self, wb: WireBatch) -> IngestTicket:
+        """txv_ingest_submit: decode + CheckTxWithInfo now, the admitted votes' TxFlow chain
+        enqueued (two batches in flight; ingest_wait in submission order)"""
+        ctx = self._ctx_or_raise("ingest_submit")
+        n = wb.n
+        ws = np.zeros(max(n, 1), np.uint8)
+        ps = np.zeros(max(n, 1), np.uint8)
+        t = ctypes.c_uint64()
+        ctx._chk(lib().txv_ingest_submit(ctx._h, self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                         wb.len.ctypes.data, n, ws.ctypes.data, ps.ctypes.data, ctypes.byref(t)),
+                 "txv_ingest_submit")
+        return IngestTicket(t.value, n, ws[:n], ps[:n])
+
+    def ingest_wait(self, tk: IngestTicket, ev_cap: int = 0):
+        """txv_ingest_wait: (wire status, pool status, flow status, commit events) of the batch"""
+        ctx = self._ctx_or_raise("ingest_wait")
+        n = tk.n
+        fs = np.zeros(max(n, 1), np.uint8)
+        ev_cap = ev_cap or max(n, 1)
+        evs = np.zeros(ev_cap, EVENT_DTYPE)
+        nev = ctypes.c_uint32()
+        rc = lib().txv_ingest_wait(ctx._h, tk.ticket, fs.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev))
+        res = (tk.wire_status, tk.pool_status, fs[:n], evs[:min(nev.value, ev_cap)])
+        if rc < 0:
+            msg = f"txv_ingest_wait failed ({rc}): {lib().txv_last_error(ctx._h).decode()}"
+            if (fs[:n] == FLOW_NOT_RUN).any():
+                raise IngestError(msg, rc, res)
+            raise TxvInfraError(msg)
+        return res
 
     def update(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
         full, off = _long_sig_arena(batch, long_sigs)
         vs = batch.c_struct()
-        self.ctx._chk(lib().txv_pool_update(self._h, self.ctx._h, height, ctypes.byref(vs), full, off),
-                      "txv_pool_update")
+        ctx = self._ctx_or_raise("update")
+        ctx._chk(lib().txv_pool_update(self._h, ctx._h, height, ctypes.byref(vs), full, off), "txv_pool_update")
 
     def reap(self, max_txs: int = -1):
         """ReapMaxTxs: ([k, 32] keys, [k] sizes) in pool order"""

@@ -15,6 +15,11 @@ ranks:
         until the slot comes round again) queues behind it, and no host thread waits for it;
   gloo  (CPU rehearsal): after the step's results are fetched (the sink is complete then), the
         sink goes to the host and is gathered there.
+Every slot has a gathered buffer of its own, so step k's all-gathered global state (the commit
+set and stakes of every shard as of step k, which the reference's per-vote commit side effects
+act on: txflow/service.go:216-232) survives steps k+1 .. k+depth-1 and is read after finish(k)
+by gathered_state(k) -- also while later steps are enqueued.  Over RCCL a timing event pair on
+the flow stream brackets each step's all-gather (exchange_ms: the per-step exchange cost).
 """
 from __future__ import annotations
 
@@ -43,19 +48,27 @@ class PipelinedSteps:
         self.cap = n_sets_cap
         self.state = self.gathered = None
         self.world, self.gloo, self._ext = 1, False, None
+        self.slot_step = [-1] * depth       # the step whose gathered state slot sl holds
+        self.finished = -1                  # newest step finished
+        self._ev = None                     # RCCL: per slot, events around its step's all-gather
         if dist is not None:
             import torch
             self.world = dist.get_world_size()
             self.gloo = dist.get_backend() == "gloo"
             assert n_sets_cap > 0
             words = commit_state_bytes(n_sets_cap) // 4
-            self.state = [torch.zeros(words, dtype=torch.int32, device=f"cuda:{device}") for _ in range(depth)]
+            # device "cpu": a host-only rehearsal of the ring (gloo; tests/test_dist_gloo.py)
+            sdev = "cpu" if device == "cpu" else f"cuda:{device}"
+            assert sdev != "cpu" or self.gloo
+            self.state = [torch.zeros(words, dtype=torch.int32, device=sdev) for _ in range(depth)]
             for sl in range(depth):
                 ctx.set_commit_sink(sl, self.state[sl].data_ptr(), n_sets_cap)
-            self.gathered = torch.zeros(self.world * words, dtype=torch.int32,
-                                        device="cpu" if self.gloo else f"cuda:{device}")
+            gdev = "cpu" if self.gloo else f"cuda:{device}"
+            self.gathered = [torch.zeros(self.world * words, dtype=torch.int32, device=gdev) for _ in range(depth)]
             if not self.gloo:
                 self._ext = torch.cuda.ExternalStream(ctx.flow_stream(), device=f"cuda:{device}")
+                self._ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                            for _ in range(depth)]
 
     def close(self):
         if self.state is not None:
@@ -65,28 +78,35 @@ class PipelinedSteps:
 
     def launch(self, k: int):
         """enqueue step k (a fresh TxFlow first, in flow-stream order after step k-1) and, over
-        RCCL, its commit-state all-gather on the flow stream behind it"""
+        RCCL, its commit-state all-gather on the flow stream behind it, into slot k % depth's
+        gathered buffer (step k - depth's state there was finished and read before)"""
         sl = k % self.depth
         if self.fresh:
             self.ctx.reset_flow()
         self.ctx.run_staged(sl)
+        self.slot_step[sl] = k
         if self._ext is not None:
             import torch
             with torch.cuda.stream(self._ext):
-                self.dist.all_gather_into_tensor(self.gathered, self.state[sl])
+                self._ev[sl][0].record(self._ext)
+                self.dist.all_gather_into_tensor(self.gathered[sl], self.state[sl])
+                self._ev[sl][1].record(self._ext)
 
     def finish(self, k: int):
         """statuses + commit events of step k (waits for its chain); gloo: gather its sink"""
         sl = k % self.depth
+        assert self.slot_step[sl] == k, "step k's slot was relaunched before step k was finished"
         st, ev = self.ctx.fetch_staged(sl, self.batches[sl].n, ev_cap=self.ev_cap, out=self.st_buf[sl],
                                        evs=self.ev_buf[sl])
         if self.gloo:
-            self.dist.all_gather(list(self.gathered.chunk(self.world)), self.state[sl].cpu())
+            self.dist.all_gather(list(self.gathered[sl].chunk(self.world)), self.state[sl].cpu())
+        self.finished = k                   # the newest finished step (steps finish in order)
         return st, ev
 
     def run(self, m: int, on_finish=None):
         """m steps, up to `depth` enqueued: launch k before waiting for k - depth + 1.
-        on_finish(k, st, ev) is called as each step's results arrive; returns the last step's"""
+        on_finish(k, st, ev) is called as each step's results arrive (gathered_state(k) is valid
+        inside it); returns the last step's"""
         out = None
         for k in range(m):
             self.launch(k)
@@ -101,11 +121,32 @@ class PipelinedSteps:
                 on_finish(j, *out)
         return out
 
+    def gathered_state(self, k: Optional[int] = None) -> Optional[List[tuple]]:
+        """step k's all-gathered state (default: the newest finished step), unpacked per rank:
+        [(committed bool[], sums i64[])].  Valid from finish(k) until step k + depth is launched;
+        waits for step k's all-gather only (later steps may still run)."""
+        if self.gathered is None:
+            return None
+        k = self.finished if k is None else k
+        sl = k % self.depth
+        assert self.slot_step[sl] == k, "step k's slot was reused"
+        if self._ev is not None:
+            self._ev[sl][1].synchronize()
+        g = self.gathered[sl].cpu().numpy().view(np.uint8).reshape(self.world, -1)
+        return [commit_state_unpack(g[r], self.cap) for r in range(self.world)]
+
     def gathered_states(self) -> Optional[List[tuple]]:
-        """the last all-gathered states, unpacked per rank: [(committed bool[], sums i64[])]
-        (waits for the flow stream)"""
+        """the newest finished step's gathered state (waits for the flow stream)"""
         if self.gathered is None:
             return None
         self.ctx.sync()
-        g = self.gathered.cpu().numpy().view(np.uint8).reshape(self.world, -1)
-        return [commit_state_unpack(g[r], self.cap) for r in range(self.world)]
+        return self.gathered_state()
+
+    def step_exchange_ms(self, k: int) -> Optional[float]:
+        """RCCL: device time of step k's all-gather on the flow stream (waits for it)"""
+        if self._ev is None:
+            return None
+        sl = k % self.depth
+        assert self.slot_step[sl] == k
+        self._ev[sl][1].synchronize()
+        return self._ev[sl][0].elapsed_time(self._ev[sl][1])

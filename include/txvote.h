@@ -455,11 +455,34 @@ int txv_pool_receive(txv_pool* pool, txv_ctx* ctx, const uint8_t* wire, uint64_t
  * wire_status[i] = TXV_WIRE_*; pool_status[i] = TXV_POOL_* (TXV_POOL_NOT_CHECKED when not
  * decoded); flow_status[i] = txv_add_votes' status (| TXV_STATUS_FIRED) for admitted votes,
  * TXV_FLOW_NOT_ADDED otherwise; commit events (up to ev_cap; *n_ev = total) carry the MESSAGE
- * index as vote_index.  Any output pointer may be NULL. */
+ * index as vote_index.  Any output pointer may be NULL.  = txv_ingest_submit + txv_ingest_wait.
+ * A failure after the pool stage (e.g. a TxFlow capacity overflow, TXV_ECAPACITY) is returned with
+ * every pool-admitted vote's flow_status = TXV_FLOW_NOT_RUN: those votes are in the pool (a resent
+ * message is ErrTxInCache) but not in TxFlow; the caller re-feeds them through txv_add_votes
+ * (e.g. from txv_decode_msgs' columns) after txv_reset_flow. */
 #define TXV_FLOW_NOT_ADDED 0xFE
+#define TXV_FLOW_NOT_RUN 0xFD
 int txv_ingest_msgs(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
                     const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status,
                     uint8_t* pool_status, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
+                    uint32_t* n_ev);
+/* txv_ingest_msgs split for pipelining (Reactor.Receive -> CheckTxWithInfo -> checkMaj23Routine's
+ * TryAddVote, txvotepool/reactor.go:170-190 -> txvotepool.go:187-261 -> txflow/service.go:123-166,
+ * as the reference's goroutines overlap them): txv_ingest_submit uploads and decodes the batch
+ * on the GPU, runs CheckTxWithInfo for its decoded votes on the host (wire_status / pool_status
+ * are final when it returns) and enqueues the admitted votes' AddVote chain without waiting for
+ * it; txv_ingest_wait(ticket) waits for that chain and reports flow_status [n] and the commit
+ * events as txv_ingest_msgs does.  At most two ingest batches in flight, waited in submission
+ * order; submits are serialised among themselves (pool order = TxFlow order), but the context is
+ * not locked during a submit's pool stage, so AddVote batches (txv_submit_votes / txv_wait_votes)
+ * and ingest waits of other threads proceed meanwhile.  The caller's buffers may be reused once
+ * txv_ingest_submit returns.  An error before the pool stage returns without a ticket and leaves
+ * the pool unchanged; once the pool admitted votes the submit returns a ticket, and a failure of
+ * the TxFlow stage is returned by the wait with TXV_FLOW_NOT_RUN as above. */
+int txv_ingest_submit(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
+                      const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status,
+                      uint8_t* pool_status, uint64_t* ticket);
+int txv_ingest_wait(txv_ctx* ctx, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
                     uint32_t* n_ev);
 
 /* ---- self-test hook: field/scalar ops on device (tests only) ---- */

@@ -113,3 +113,110 @@ def test_shard_rule_and_pack_layout():
     assert np.array_equal(bits, com)
     c2, s2 = T.commit_state_unpack(buf, cap)
     assert np.array_equal(c2, com.astype(bool)) and np.array_equal(s2, sums)
+
+
+class _RingCtx:
+    """stands in for a txv_ctx in the host-only rehearsal of txflow_amd/pipeline.py's ring: a
+    step's 'device' writes the packed commit state of (rank, step) into the slot's commit sink
+    when the step's results are fetched (the sink is complete at fetch, as txv_set_commit_sink
+    promises)"""
+
+    def __init__(self, rank, cap):
+        self.rank, self.cap, self.sink, self.step_of, self.steps = rank, cap, {}, {}, 0
+
+    def stage(self, sl, b):
+        pass
+
+    def set_commit_sink(self, sl, ptr, cap=0):
+        self.sink[sl] = ptr
+
+    def reset_flow(self):
+        pass
+
+    def run_staged(self, sl, timed=False):
+        self.step_of[sl] = self.steps
+        self.steps += 1
+
+    def fetch_staged(self, sl, n, ev_cap=0, out=None, evs=None):
+        import ctypes
+        import txflow_amd as T
+        ns = 3 + self.step_of[sl] % 5
+        com = np.array([(self.step_of[sl] + self.rank + i) % 3 == 0 for i in range(ns)], np.uint8)
+        sums = np.array([self.step_of[sl] * 1000 + self.rank * 100 + i for i in range(ns)], np.int64)
+        buf = np.frombuffer(T.commit_state_pack_host(com, sums, self.cap), np.uint8)
+        if self.sink.get(sl):
+            ctypes.memmove(self.sink[sl], buf.ctypes.data, len(buf))
+        return out[:n], evs[:0]
+
+    def sync(self):
+        pass
+
+
+def _ring_expected(k, r, cap):
+    ns = 3 + k % 5
+    return ([(k + r + i) % 3 == 0 for i in range(ns)], [k * 1000 + r * 100 + i for i in range(ns)])
+
+
+def _ring_worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+        import txflow_amd as T
+        from txflow_amd.pipeline import PipelinedSteps
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        cap = 64
+        b = T.VoteBatch.from_votes([T.TxVote(Height=1, TxHash="AA", Timestamp=(1, 1))])
+        rt = PipelinedSteps(_RingCtx(rank, cap), [b], depth=3, fresh_flow=False, dist=dist, n_sets_cap=cap,
+                            device="cpu")
+        errors = []
+
+        def check(k, st, ev):
+            got = rt.gathered_state(k)
+            for r in range(world):
+                ec, es = _ring_expected(k, r, cap)
+                if list(got[r][0].astype(bool)) != ec or list(got[r][1]) != es:
+                    errors.append(f"rank {rank}: step {k} rank {r} differs at finish")
+
+        rt.run(9, check)
+        # every slot's buffer still holds its own step after the run: steps 6, 7, 8
+        for k in (6, 7, 8):
+            got = rt.gathered_state(k)
+            for r in range(world):
+                ec, es = _ring_expected(k, r, cap)
+                if list(got[r][0].astype(bool)) != ec or list(got[r][1]) != es:
+                    errors.append(f"rank {rank}: step {k} rank {r} lost after later steps")
+        try:
+            rt.gathered_state(5)          # slot reused by step 8
+            errors.append("step 5's state still claimed valid")
+        except AssertionError:
+            pass
+        rt.close()
+        dist.destroy_process_group()
+        q.put((rank, errors))
+    except Exception as e:
+        import traceback
+        q.put((rank, [f"rank {rank} raised {e!r}\n{traceback.format_exc()}"]))
+
+
+def test_pipelined_ring_keeps_every_steps_gathered_state():
+    """txflow_amd/pipeline.py, host-only (gloo, 2 ranks): three slots, up to three steps
+    enqueued; each step's all-gathered commit state lands in its slot's own buffer, so step k's
+    global state (every rank's row) is intact when step k finishes and stays so until step
+    k + 3 reuses the slot (one shared gathered buffer lost all but the last step's)."""
+    port = 31500 + random.Random().randrange(2000)
+    c = mp.get_context("spawn")
+    q = c.Queue()
+    procs = [c.Process(target=_ring_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=120) for _ in range(2)]
+        for p in procs:
+            p.join(timeout=30)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    errs = [e for _, es in res for e in es]
+    assert not errs, "\n".join(errs)

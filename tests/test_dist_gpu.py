@@ -5,7 +5,8 @@
   path (txflow_amd/pipeline.py: staged slots, up to two steps enqueued, each step's packed commit
   state written by the device into the slot's commit sink and all-gathered after the step);
   steps alternate the shard's votes with a batch of replays, conflicting signatures, corrupted
-  signatures and new txs, on one TxFlow.  Every step's per-vote statuses + fired bits equal the
+  signatures and new txs, on one TxFlow, four slots deep: steps k+1 .. k+3 are enqueued before
+  step k is finished, and step k's gathered state (its slot's own buffer) is read then.  Every step's per-vote statuses + fired bits equal the
   sequential oracle's over the shard, and every rank's row of the gathered state equals the host
   pack of the owning rank's oracle state (so every rank holds the global committed set + stakes);
   one rank (nccl = RCCL): the same path with the all-gather enqueued on the context's flow stream
@@ -71,36 +72,51 @@ def _worker(rank, world, port, backend, q):
         wl = Workload(ctx, 100, 1200, SEEDS["c3"], shard=rank, n_shards=2)
         adv = _adversarial(T, wl, ctx, random.Random(100 + rank))
         flow = O.Flow(wl.pubs, wl.powers, b"test_chain_id")
-        runner = PipelinedSteps(ctx, [wl.batch, adv], depth=2, fresh_flow=False, dist=dist, n_sets_cap=cap,
-                                device=0, ev_cap=1 << 17)
+        # the oracle first: every step's expected statuses and, per rank, its state after the step
+        steps = 6
+        exp_st, rows_after = [], []
         keys, seen = [], set()
-        errors = []
-        for k in range(4):
-            b = runner.batches[k % 2]
+        batches = [wl.batch, adv]
+        for k in range(steps):
+            b = batches[k % 2]
             ost, _, ofired = flow.add_batch(b, 8)
-            exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+            exp_st.append(ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7))
             for i in range(b.n):
                 h = b.txhash(i)
                 if h not in seen:
                     seen.add(h)
                     keys.append(h)
-            runner.launch(k)
-            st, ev = runner.finish(k)
-            if not np.array_equal(st, exp):
-                bad = np.nonzero(st != exp)[0]
-                errors.append(f"rank {rank} step {k}: {len(bad)} status mismatches "
-                              f"{[(int(i), int(st[i]), int(exp[i])) for i in bad[:5]]}")
             qv = [flow.query(h) for h in keys]
             mine = T.commit_state_pack_host(np.array([m for _, m in qv], np.uint8),
                                             np.array([s for s, _ in qv], np.int64), cap)
             rows = [None] * world
             dist.all_gather_object(rows, mine)
-            got = runner.gathered_states()
+            rows_after.append([T.commit_state_unpack(r, cap) for r in rows])
+        # then the product: four slots, steps k+1 .. k+3 enqueued before step k is finished (the
+        # exchange of step k runs while later steps verify); every step's gathered state read
+        # when it finishes, with later steps in flight
+        runner = PipelinedSteps(ctx, batches, depth=4, fresh_flow=False, dist=dist, n_sets_cap=cap,
+                                device=0, ev_cap=1 << 17)
+        errors = []
+        last = {}
+
+        def check(k, st, ev):
+            if not np.array_equal(st, exp_st[k]):
+                bad = np.nonzero(st != exp_st[k])[0]
+                errors.append(f"rank {rank} step {k}: {len(bad)} status mismatches "
+                              f"{[(int(i), int(st[i]), int(exp_st[k][i])) for i in bad[:5]]}")
+            got = runner.gathered_state(k)
             for r in range(world):
-                ec, es = T.commit_state_unpack(rows[r], cap)
+                ec, es = rows_after[k][r]
                 gc, gs = got[r]
                 if not (np.array_equal(gc, ec) and np.array_equal(gs, es)):
                     errors.append(f"rank {rank} step {k}: gathered state of rank {r} differs")
+            last["st"] = st.copy()
+
+        runner.run(steps, check)
+        if runner.step_exchange_ms(steps - 1) is None and backend != "gloo":
+            errors.append("no exchange timing over RCCL")
+        st = last["st"]
         by = np.bincount(st & 0x7F, minlength=8)
         runner.close()
         ctx.close()

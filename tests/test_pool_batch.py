@@ -115,3 +115,21 @@ def test_pool_batch_replays_of_evicted_keys():
         assert (st == T.POOL_ERR_IN_CACHE).any() and (st == T.POOL_OK).sum() > 6000
     finally:
         pool.close()
+
+
+def test_contextless_pool_methods_raise_clearly():
+    """a pool made with ctx=None runs check_keys only; the methods that need the GPU
+    context say so (ValueError) instead of failing on a missing attribute."""
+    import txflow_amd as T
+    pool = T.TxVotePool(None, size=16, cache_size=16)
+    try:
+        st = pool.check_keys(np.zeros((2, 32), np.uint8) + np.arange(2, dtype=np.uint8)[:, None], np.array([10, 10], np.uint32))
+        assert list(st) == [T.POOL_OK, T.POOL_OK]
+        b = T.VoteBatch.from_votes([T.TxVote(Height=1, TxHash="AB", Timestamp=(1, 1), ValidatorAddress=b"\1" * 20,
+                                             Signature=b"\2" * 64)])
+        for call in (lambda: pool.check_batch(b), lambda: pool.update(1, b),
+                     lambda: pool.receive(T.WireBatch([b"\x01"])), lambda: pool.ingest(T.WireBatch([b"\x01"]))):
+            with pytest.raises(ValueError, match="ctx=None"):
+                call()
+    finally:
+        pool.close()

@@ -314,14 +314,19 @@ def test_host_encoder_matches_oracle():
 
 
 @pytest.mark.gpu
-def test_gpu_ingest_chain_matches_oracle():
+@pytest.mark.parametrize("mode", ["sync", "pipelined"])
+def test_gpu_ingest_chain_matches_oracle(mode):
     """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
-    kept in HBM) over three batches of received messages against the oracle's decoder, pool and
+    kept in HBM) over batches of received messages against the oracle's decoder, pool and
     sequential TxFlow: signed votes, exact replays of earlier messages (ErrTxInCache while the
     bounded LRU still holds their key, DUPLICATE once it evicted it), conflicting signatures,
     corrupted ones, a 65-byte signature (its key hashes all 65 bytes), non-canonical framings and
     undecodable / oversize messages.  Per message: wire status, pool status, flow status + fired
-    bit; commit events by message index; the pool and TxFlow state at the end."""
+    bit; commit events by message index; the pool and TxFlow state at the end.
+    mode "sync": three batches through txv_ingest_msgs; "pipelined": five batches through
+    txv_ingest_submit / txv_ingest_wait with two in flight (batch k+1 decoded and pool-checked
+    while batch k's TxFlow chain runs; reactor.go:170-190 -> txvotepool.go:187-261 ->
+    txflow/service.go:123-166)."""
     import txflow_amd as T
     rng = random.Random(31)
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16)
@@ -375,11 +380,24 @@ def test_gpu_ingest_chain_matches_oracle():
         pool = T.TxVotePool(ctx, size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
         opool = O.Pool(size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
         flow = O.Flow(pubs, powers, b"test_chain_id")
-        committed, cuts = set(), [0, len(stream) // 3, 2 * len(stream) // 3, len(stream)]
+        nb = 3 if mode == "sync" else 5
+        committed, cuts = set(), [len(stream) * k // nb for k in range(nb + 1)]
         seen = {"cache": 0, "dup": 0, "fired": 0, "undecoded": 0, "nondet": 0, "invalid": 0}
-        for b in range(3):
-            part = stream[cuts[b]:cuts[b + 1]]
-            ws, ps, fs, ev = pool.ingest(T.WireBatch(part))
+        parts = [stream[cuts[b]:cuts[b + 1]] for b in range(nb)]
+        if mode == "sync":
+            results = [pool.ingest(T.WireBatch(part)) for part in parts]
+        else:
+            results, inflight = [], []
+            for part in parts:
+                inflight.append(pool.ingest_submit(T.WireBatch(part)))
+                if len(inflight) == 2:
+                    results.append(pool.ingest_wait(inflight.pop(0)))
+            while inflight:
+                results.append(pool.ingest_wait(inflight.pop(0)))
+            assert len(results) == nb
+        for b in range(nb):
+            part = parts[b]
+            ws, ps, fs, ev = results[b]
             exp_fired = []
             for i, m in enumerate(part):
                 st, f = O.wire_decode(m, max_msg)
@@ -413,6 +431,59 @@ def test_gpu_ingest_chain_matches_oracle():
             h = hashlib.sha256(b"ingest%d" % t).hexdigest().upper().encode()
             assert ctx.query_tx(h) == flow.query(h)
         assert all(seen[k] > 0 for k in seen), seen
+        pool.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ingest_capacity_overflow_reports_not_run():
+    """a TxFlow capacity overflow after the pool stage must not strand the admitted
+    votes silently.  A context with room for 8 TxVoteSets receives messages for 40 txs: the call
+    fails with TXV_ECAPACITY, every pool-admitted message carries FLOW_NOT_RUN (in the pool, not in
+    TxFlow: resending one is ErrTxInCache), the rest FLOW_NOT_ADDED; after txv_reset_flow the
+    admitted votes re-fed through txv_add_votes (from txv_decode_msgs' columns) are ADDED."""
+    import txflow_amd as T
+    rng = random.Random(7)
+    ctx = T.Context(max_batch=1 << 12, max_txs=8, max_validators=8)
+    try:
+        seeds = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(4)]
+        pubs = ctx.keygen(seeds)
+        ctx.set_validators(pubs, [1, 1, 1, 1], "test_chain_id")
+        addrs, _ = ctx.validator_info()
+        votes, signer = [], []
+        for t in range(40):
+            h = hashlib.sha256(b"over%d" % t).hexdigest().upper()
+            for v in range(2):
+                votes.append(T.TxVote(Height=1, TxHash=h, Timestamp=(1_700_000_000, 1 + len(votes)),
+                                      ValidatorAddress=addrs[v]))
+                signer.append(v)
+        sigs = ctx.sign_votes(T.VoteBatch.from_votes(votes), np.array(signer, np.uint32), "test_chain_id")
+        wire = [O.wire_encode(v.Height, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], v.ValidatorAddress,
+                              s.tobytes(), b"\0" * 32) for v, s in zip(votes, sigs)]
+        wire.insert(5, b"\x01\x02")                       # undecodable: never reaches the pool
+        pool = T.TxVotePool(ctx, size=1 << 12, cache_size=1 << 12, max_txs_bytes=1 << 30, max_msg_bytes=4096)
+        with pytest.raises(T.IngestError) as ei:
+            pool.ingest(T.WireBatch(wire))
+        ws, ps, fs, _ = ei.value.result
+        assert ei.value.rc == -28                          # TXV_ECAPACITY
+        adm = (ws == T.WIRE_OK) & (ps == T.POOL_OK)
+        assert adm.sum() == len(votes)
+        assert (fs[adm] == T.FLOW_NOT_RUN).all() and (fs[~adm] == T.FLOW_NOT_ADDED).all()
+        assert pool.Size() == len(votes)
+        ws2, ps2 = pool.receive(T.WireBatch(wire[:3]))   # resent: in the cache already
+        assert (ps2 == T.POOL_ERR_IN_CACHE).all()
+        # the caller's recovery: a fresh TxFlow with room, the admitted votes re-fed
+        ctx.reset_flow()
+        with pytest.raises(T.TxvInfraError):              # still over capacity in one batch
+            ctx.add_votes(T.VoteBatch.from_votes(votes), ev_cap=len(votes))
+        ctx.reset_flow()
+        for k in range(0, 16, 2):                         # 8 txs fit
+            v2 = votes[k:k + 2]
+            for v, s in zip(v2, sigs[k:k + 2]):
+                v.Signature = s.tobytes()
+            st, _ = ctx.add_votes(T.VoteBatch.from_votes(v2), ev_cap=2)
+            assert ((st & 0x7F) == T.ADDED).all()
         pool.close()
     finally:
         ctx.close()

@@ -1,6 +1,6 @@
 """Run the library's VALU issue-rate probe (txv_k_valu_probe: 8 independent v_add_u32 or
 v_mad_u64_u32 per loop iteration, 2048 x 256 threads x 16384 iterations per launch, 4 launches
-each) so a PMC pass sees kernels of known instruction counts (tools/profile/r3_prof.sh)."""
+each) so a PMC pass sees kernels of known instruction counts (the profiling run scripts)."""
 import os
 import sys
 
