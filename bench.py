@@ -55,6 +55,13 @@ W_FM = 1 + 22 * 7 + 6 + 2 + 3 + 8
 W_ALG = 1.1e4 + W_FM * 100.0
 
 
+def w_alg_for(wb: int, wa: int) -> float:
+    """W_ALG of the same algorithm for other table windows (C5's 1000 validators run W_A = 16:
+    11 + 16 = 27 entries): the same terms with nT = ceil(256/wb) + ceil(256/wa) entries"""
+    nt = -(-256 // wb) + -(-256 // wa)
+    return 1.1e4 + (1 + (nt - 2) * 7 + 6 + 2 + 3 + 8) * 100.0
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -236,6 +243,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
         tickets = queue.Queue()
         slots = threading.Semaphore(2)
         pool_st = [None] * len(wl.batches)
+        dev_ms, dev_split = [], []        # per batch in the pipeline: slot events (HIP, per stream)
 
         def ingest():
             for k, b in enumerate(wl.batches):
@@ -255,6 +263,11 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                 k, tk = item
                 st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
                 te = time.perf_counter()
+                if rep == 2:                  # the batch's stage times, before its ring slot is reused
+                    dev_ms.append(ctx.slot_kernel_ms((tk - 1) % 2))
+                    sp = verify_split(ctx, (tk - 1) % 2)
+                    if sp:
+                        dev_split.append(sp)
                 slots.release()
                 done.append(te)
                 added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
@@ -309,6 +322,37 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     out["passes"] = 3
     out["votes_per_s_passes"] = [r["votes_per_s"] for r in runs]
     out["correct"] = all(r["correct"] for r in runs)
+    # where a 64k batch's device time goes: the stage times of every batch of the last
+    # pass inside the pipeline, and of one batch run alone on a fresh TxFlow (staged slot 0: the
+    # submit ring is idle now), with the verify pair's VALU roofline at this batch size
+    b0 = wl.batches[0]
+    b0.is_nil = None
+    ctx.stage(0, b0)
+    solo, solo_sp = [], []
+    for _ in range(4):
+        ctx.reset_flow()
+        solo.append(ctx.run_staged(0, timed=True))
+        sp = verify_split(ctx, 0)
+        if sp:
+            solo_sp.append(sp)
+        ctx.fetch_staged(0, b0.n, ev_cap=b0.n)
+    med = lambda xs, j: round(statistics.median(x[j] for x in xs), 4) if xs else None  # noqa: E731
+    w_c5 = w_alg_for(ctx.base_w, ctx.table_w)
+    v_solo = med(solo[1:], 1)
+    out["device_ms_batch"] = {
+        "votes": b0.n,
+        "in_pipeline_p50": {"prep": med(dev_ms, 0), "verify": med(dev_ms, 1), "k1a": med(dev_split, 0),
+                            "k1b": med(dev_split, 1), "tally_after_verify": med(dev_ms, 2), "chain": med(dev_ms, 3)},
+        "standalone": {"prep": med(solo[1:], 0), "verify": v_solo, "k1a": med(solo_sp[1:], 0),
+                       "k1b": med(solo_sp[1:], 1), "tally": med(solo[1:], 2), "chain": med(solo[1:], 3)},
+        "k1b_kernel": "txv_k_scalarmult_split (4 lanes per vote) + txv_k_batch_encode (K1c)" if b0.n < (3 << 18)
+                      else "txv_k_scalarmult_dyn",
+        "roofline": {"bound": "valu", "alg_lane_ops_per_vote": w_c5,
+                     "achieved": round(b0.n * w_c5 / (v_solo * 1e-3) / 1e12, 3) if v_solo else None,
+                     "peak": round(VALU_PEAK / 1e12, 3), "unit": "Tlane-op/s",
+                     "frac": round(b0.n * w_c5 / (v_solo * 1e-3) / VALU_PEAK, 4) if v_solo else None,
+                     "note": f"standalone K1a + K1b of one batch; W_alg for windows {ctx.base_w}/{ctx.table_w} "
+                             f"(bench.w_alg_for: {-(-256 // ctx.base_w) + -(-256 // ctx.table_w)} table entries)"}}
     ctx.close()
     return out
 

@@ -129,6 +129,26 @@ TXV_HD ge10_ext ge10_from_entry(const fe10& qp, const fe10& qm) {
   return r;
 }
 
+// P + Q for two extended points in fe10 (add-2008-hwcd-3, a = -1, k = 2d): 9 multiplies; the
+// lane-quad combine of the split K1b (txv_k_scalarmult_split).  Inputs carried (fe10_mul outputs
+// or ge10_from_entry), output carried.  Operand bounds: Y - X < 3 * 2^w (g ok), Y + X < 2 * 2^w;
+// D = 2 Z1 Z2 carried once more, so F = D - C < 3 * 2^w and G = D + C < 2 * 2^w; E = B - A
+// < 3 * 2^w is only ever the g operand, F only the f operand.
+TXV_HD ge10_ext ge10_add(const ge10_ext& p, const ge10_ext& q) {
+  const fe10 A = fe10_mul(fe10_sub(p.Y, p.X), fe10_sub(q.Y, q.X));
+  const fe10 B = fe10_mul(fe10_add(p.Y, p.X), fe10_add(q.Y, q.X));
+  const fe10 C = fe10_mul(fe10_mul(p.T, q.T), fe10_from_fe(fe_const_d2()));
+  const fe10 Zz = fe10_mul(p.Z, q.Z);
+  const fe10 D = fe10_carry(fe10_add(Zz, Zz));
+  const fe10 E = fe10_sub(B, A), H = fe10_add(B, A), G = fe10_add(D, C), F = fe10_sub(D, C);
+  ge10_ext r;
+  r.X = fe10_mul(F, E);
+  r.Y = fe10_mul(H, G);
+  r.Z = fe10_mul(F, G);
+  r.T = fe10_mul(H, E);
+  return r;
+}
+
 // (p + 1) / 2
 TXV_HD fe fe_const_half() {
   fe r; const uint32_t k[8] = {0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu,

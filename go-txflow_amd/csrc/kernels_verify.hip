@@ -802,6 +802,234 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_point
   }
 }
 
+// ---------------------------------------------------------------- K1b split (small batches)
+// C5's 64k-vote batches leave a one-vote-per-lane walk with 1024 waves (one per SIMD) and its
+// 26 dependent additions as the critical path.  Here FOUR lanes share a vote: the schedule of its
+// nT = nB + nA table entries (B positions 0..nB-1, then A positions) is cut in four runs of
+// ceil(nT / 4) entries, each lane walks its run with the cooperative LDS-DMA gathers of the big
+// K1b (per-lane entry addresses: a wave's lanes mix B and A runs), and the lane quad combines its
+// four partial sums with two full additions over DPP quad permutes ((0,1)(2,3), then (0,2)(1,3));
+// every lane of the quad ends with [s]B + [k](-A), and lane 0 stores R' for K1c (the batched
+// inversion + encoding + compare).  4x the waves and ~1/3 of the dependent chain for 5 % more
+// multiplies (4 starting entries and 3 x 9-multiply additions instead of 3 mixed additions).
+__device__ __forceinline__ void entries_to_lds_p(const uint32_t* p_l, uint4* buf) {
+  if (TXV_K1B_NO_GATHER) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t addr = (uint64_t)p_l;
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int src = (8 * i + (lane >> 3)) << 2;
+    lo[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)addr);
+    hi[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(addr >> 32));
+  }
+  TXV_SCHED_FENCE();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t piece = (uint32_t)((lane & 7) + 8 * i + (lane >> 3)) & 7u;
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(((uint64_t)hi[i] << 32) | lo[i]) + piece * 4u;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)(buf + 64 * i), 16, 0, 0);
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ fe10 fe10_dpp(const fe10& x) {
+  fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[i], CTRL, 0xF, 0xF, false);
+  return r;
+}
+__device__ __forceinline__ fe10 fe10_sel(bool c, const fe10& x, const fe10& y) {
+  fe10 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = c ? x.v[i] : y.v[i];
+  return r;
+}
+__device__ __forceinline__ fe10 fe10_small(uint32_t k) { fe10 r = fe10_zero(); r.v[0] = k; return r; }
+
+// The lane quad's two combining additions (ge.h ge10_add, add-2008-hwcd-3: A = (Y1-X1)(Y2-X2),
+// B = (Y1+X1)(Y2+X2), C = 2d T1 T2, D = 2 Z1 Z2, then X3 = EF, Y3 = GH, Z3 = FG, T3 = EH) with
+// their products spread over the lanes that compute the same sum -- one multiply instruction
+// stream whose operands are chosen per lane -- and the results exchanged by DPP:
+// level 1 (pairs (0,1), (2,3)): even lanes A, T1T2, C; odd lanes B, Z1Z2, D; then even X3, Y3,
+//   odd Z3, T3: 5 multiplies per lane instead of 9; both lanes of a pair end with the pair's sum
+// level 2 ((0,2), (1,3)): lane q one of A, B, T1T2, Z1Z2, lanes 2 / 3 then C / D, every lane
+//   reads A..D by quad broadcast; lane q then computes X3 / Y3 / Z3 (q = 0 / 1 / 2): 3 multiplies
+//   per lane instead of 9; lane q holds coordinate q of the vote's R' (T3 is not needed)
+// Operand bounds as in ge10_add (multiplying by the constant 2 gives D carried).
+__device__ __forceinline__ ge10_ext ge10_quad_level1(const ge10_ext& p, uint32_t q) {
+  const bool ev = (q & 1u) == 0;
+  // one permute per product: a lane sends what its partner needs (the partner of an even lane is
+  // odd and vice versa), so the permuted operand is dpp(select of the other parity's choice)
+  fe10 r1, r3;
+  {
+    const fe10 ymx = fe10_sub(p.Y, p.X), ypx = fe10_add(p.Y, p.X);
+    r1 = fe10_mul(fe10_sel(ev, ymx, ypx), fe10_dpp<0xB1>(fe10_sel(ev, ypx, ymx)));   // even A, odd B
+  }
+  TXV_SCHED_FENCE();
+  {
+    const fe10 r2 = fe10_mul(fe10_sel(ev, p.T, p.Z), fe10_dpp<0xB1>(fe10_sel(ev, p.Z, p.T)));   // T1T2 / Z1Z2
+    TXV_SCHED_FENCE();
+    r3 = fe10_mul(r2, ev ? fe10_from_fe(fe_const_d2()) : fe10_small(2));   // even C, odd D
+  }
+  TXV_SCHED_FENCE();
+  fe10 E, F, G, H;
+  {
+    const fe10 o1 = fe10_dpp<0xB1>(r1), o3 = fe10_dpp<0xB1>(r3);
+    const fe10 A = fe10_sel(ev, r1, o1), B = fe10_sel(ev, o1, r1), C = fe10_sel(ev, r3, o3), D = fe10_sel(ev, o3, r3);
+    E = fe10_sub(B, A); H = fe10_add(B, A); G = fe10_add(D, C); F = fe10_sub(D, C);
+  }
+  TXV_SCHED_FENCE();
+  const fe10 s1 = fe10_mul(F, fe10_sel(ev, E, G));               // even X3 = FE, odd Z3 = FG
+  TXV_SCHED_FENCE();
+  const fe10 s2 = fe10_mul(H, fe10_sel(ev, G, E));               // even Y3 = HG, odd T3 = HE
+  TXV_SCHED_FENCE();
+  ge10_ext r;
+  {
+    const fe10 t1 = fe10_dpp<0xB1>(s1);
+    r.X = fe10_sel(ev, s1, t1);
+    r.Z = fe10_sel(ev, t1, s1);
+  }
+  {
+    const fe10 t2 = fe10_dpp<0xB1>(s2);
+    r.Y = fe10_sel(ev, s2, t2);
+    r.T = fe10_sel(ev, t2, s2);
+  }
+  return r;
+}
+
+// level 2: returns coordinate q of the quad's sum (X, Y, Z for q = 0, 1, 2; lane 3: junk)
+__device__ __forceinline__ fe10 ge10_quad_level2(const ge10_ext& p, uint32_t q) {
+  fe10 r1;
+  {
+    const fe10 ymx = fe10_sub(p.Y, p.X), ypx = fe10_add(p.Y, p.X);
+    // lane q computes A / B / T1T2 / Z1Z2 with partner q ^ 2, which sends T / Z / ymx / ypx to 0 / 1 / 2 / 3
+    const fe10 f = fe10_sel(q < 2, fe10_sel(q == 0, ymx, ypx), fe10_sel(q == 2, p.T, p.Z));
+    const fe10 h = fe10_sel(q < 2, fe10_sel(q == 0, p.T, p.Z), fe10_sel(q == 2, ymx, ypx));
+    r1 = fe10_mul(f, fe10_dpp<0x4E>(h));
+  }
+  TXV_SCHED_FENCE();
+  const fe10 r2 = fe10_mul(r1, q == 2 ? fe10_from_fe(fe_const_d2()) : fe10_small(2));   // lane 2 C, lane 3 D
+  TXV_SCHED_FENCE();
+  fe10 E, F, G, H;
+  {
+    const fe10 A = fe10_dpp<0x00>(r1), B = fe10_dpp<0x55>(r1), C = fe10_dpp<0xAA>(r2), D = fe10_dpp<0xFF>(r2);
+    E = fe10_sub(B, A); H = fe10_add(B, A); G = fe10_add(D, C); F = fe10_sub(D, C);
+  }
+  // q = 0: X3 = F E, 1: Y3 = H G, 2: Z3 = F G
+  return fe10_mul(fe10_sel(q & 1u, H, F), fe10_sel(q == 0, E, G));
+}
+
+// every signed radix-2^W digit of a scalar < 2^253 at once: digit i from bits [W i, W i + W) plus
+// the carry of digit i - 1, exactly the sequence next_digit<W> produces
+template <int W, int N>
+__device__ __forceinline__ void signed_digits(const uint32_t s[8], int d[N]) {
+  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int b = W * i, w = b >> 5, o = b & 31;
+    uint32_t win = s[w] >> o;
+    if (o + W > 32 && w + 1 < 8) win |= s[w + 1] << (32 - o);
+    const uint32_t dd = (win & mask) + carry;
+    carry = (dd + half) >> W;
+    d[i] = (int)dd - (int)(carry << W);
+  }
+}
+
+#ifndef TXV_SPLIT_WAVES
+#define TXV_SPLIT_WAVES 3
+#endif
+template <int WB, int WA>
+__global__ void __launch_bounds__(256, TXV_SPLIT_WAVES) txv_k_scalarmult_split(VerifyArgs a) {
+  constexpr int nB = Tab<WB>::kPositions, nA = Tab<WA>::kPositions, nT = nB + nA, per = (nT + 3) / 4;
+  __shared__ uint4 pf[4][8 * 64];   // one 8 KiB gather buffer per wave (prefetch one entry ahead)
+  uint4* wbuf = pf[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
+  const uint32_t n_waves = (a.n_work + 15u) / 16u;   // 16 votes per wave
+  const uint32_t stride = gridDim.x * 4u;
+  for (uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6); w < n_waves; w += stride) {   // wave-uniform
+    const uint32_t idx = w * 16u + (lane >> 2);
+    const uint32_t i = idx < a.n_work ? (a.order ? a.order[idx] : idx) : 0u;
+    const bool on = idx < a.n_work && a.ok_out[i] == 2;
+    uint32_t s[8], k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
+      k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
+    }
+    const uint32_t va = on ? a.val[i] : 0u;
+    // every entry of this lane's run up front as (table, entry index), so the scalars are dead
+    // before the walk starts: all signed digits of s and k by direct window extraction (carries
+    // rippled in order, as next_digit), then run entry j of lane q = schedule entry q * per + j,
+    // one of four candidates chosen by q
+    uint32_t eidx[per];
+    uint32_t negm = 0, am = 0;           // per run entry: negate, A table
+    {
+      int dB[nB], dA[nA];
+      signed_digits<WB, nB>(s, dB);
+      signed_digits<WA, nA>(k, dA);
+#pragma unroll
+      for (int j = 0; j < per; ++j) {
+        uint32_t ec[4], nc = 0, ac = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int t = qq * per + j;
+          if (t < nB) {
+            ec[qq] = (uint32_t)t * Tab<WB>::kEntries + (uint32_t)(dB[t] < 0 ? -dB[t] : dB[t]);
+            nc |= (dB[t] < 0 ? 1u : 0u) << qq;
+          } else if (t < nT) {
+            const int d = dA[t - nB];
+            ec[qq] = (va * (uint32_t)nA + (uint32_t)(t - nB)) * (uint32_t)Tab<WA>::kEntries + (uint32_t)(d < 0 ? -d : d);
+            nc |= (d > 0 ? 1u : 0u) << qq;   // [k](-A): a positive digit subtracts
+            ac |= 1u << qq;
+          } else {
+            ec[qq] = 0;                      // beyond the schedule: B position 0, digit 0 = identity
+          }
+        }
+        eidx[j] = q == 0 ? ec[0] : q == 1 ? ec[1] : q == 2 ? ec[2] : ec[3];
+        negm |= ((nc >> q) & 1u) << j;
+        am |= ((ac >> q) & 1u) << j;
+      }
+    }
+    auto entry_ptr = [&](int j) -> const uint32_t* {
+      uint32_t e = eidx[0];
+#pragma unroll
+      for (int jj = 1; jj < per; ++jj) e = (jj == j) ? eidx[jj] : e;   // j is wave-uniform
+      return ((am >> j) & 1u ? a.atables : a.btable) + (size_t)e * kEntryWords;
+    };
+    entries_to_lds_p(entry_ptr(0), wbuf);
+    ge10_ext P;
+#pragma unroll 1
+    for (int j = 0; j < per; ++j) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // entry j landed in LDS
+      const bool nj = (negm >> j) & 1u;
+      auto rd = [&](int role) { return entry_field_lds(wbuf, nj, role); };
+      auto next = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the next DMA lands
+        if (j + 1 < per) entries_to_lds_p(entry_ptr(j + 1), wbuf);
+      };
+      if (j == 0) {
+        const fe10 qp = rd(0), qm = rd(1);
+        next();
+        P = ge10_from_entry(qp, qm);
+      } else {
+        P = ge10_madd_rd<true>(P, rd, nj, next);
+      }
+    }
+    P = ge10_quad_level1(P, q);                 // lanes 0, 1: P0 + P1; lanes 2, 3: P2 + P3
+    const fe10 coord = ge10_quad_level2(P, q);  // lane q < 3: coordinate q of R' = sum of the four
+    if (q < 3 && on) {                          // lane q stores coordinate q (rpts words 8q..8q+7)
+      const fe c = fe_from_fe10(coord);
+      uint32_t* o = a.rpts + idx + (size_t)(8 * q) * a.n_pad;
+      const size_t np = a.n_pad;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) __builtin_nontemporal_store(c.v[j], o + (size_t)j * np);
+    }
+  }
+}
+
 // K1c: lane t takes the work entries (t & ~63) G + 64 h + (t & 63), h < G (a wave reads 64
 // consecutive entries per slot).  Pass 1 stores each active entry's exclusive prefix product
 // E_h = prod of the earlier active Z (words 24..31, skipped for the first); pass 2 walks back
@@ -998,18 +1226,20 @@ static int k1c_votes_per_lane(uint32_t n_work) {
   static const int forced = [] {
     const char* e = getenv("TXV_K1C_G");
     const int g = e ? atoi(e) : 0;
-    return (g == 4 || g == 8 || g == 16 || g == 32) ? g : 0;
+    return (g == 1 || g == 2 || g == 4 || g == 8 || g == 16 || g == 32) ? g : 0;
   }();
   if (forced) return forced;
-  for (int g : {32, 16, 8})
+  for (int g : {32, 16, 8, 4, 2})
     if ((uint64_t)n_work >= (uint64_t)g * 64 * 1024) return g;
-  return 4;
+  return 1;
 }
 
 static hipError_t launch_batch_encode(const VerifyArgs* args, hipStream_t st) {
   const int g = k1c_votes_per_lane(args->n_work);
   const uint32_t grid = (uint32_t)(((uint64_t)args->n_work + 64u * g - 1) / (64u * g));
   switch (g) {
+    case 1: hipLaunchKernelGGL(txv_k_batch_encode<1>, dim3(grid), dim3(64), 0, st, *args); break;
+    case 2: hipLaunchKernelGGL(txv_k_batch_encode<2>, dim3(grid), dim3(64), 0, st, *args); break;
     case 4: hipLaunchKernelGGL(txv_k_batch_encode<4>, dim3(grid), dim3(64), 0, st, *args); break;
     case 8: hipLaunchKernelGGL(txv_k_batch_encode<8>, dim3(grid), dim3(64), 0, st, *args); break;
     case 16: hipLaunchKernelGGL(txv_k_batch_encode<16>, dim3(grid), dim3(64), 0, st, *args); break;
@@ -1024,6 +1254,16 @@ template <int B, int WB, int WA>
 static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_t st) {
   if (args->lane_votes == 1) {
     if (!args->rpts) return hipErrorInvalidValue;
+    if constexpr (WB >= 24) {
+      // TXV_K1B_SPLIT=0 (experiments): the one-vote-per-lane points kernel instead
+      static const bool split = !(getenv("TXV_K1B_SPLIT") && atoi(getenv("TXV_K1B_SPLIT")) == 0);
+      if (split) {
+        const uint32_t waves = (args->n_work + 15u) / 16u;
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((waves + 3u) / 4u, std::max<uint32_t>(args->n_cus, 1u) * TXV_SPLIT_WAVES));
+        hipLaunchKernelGGL((txv_k_scalarmult_split<WB, WA>), dim3(blocks), dim3(256), 0, st, *args);
+        return launch_batch_encode(args, st);
+      }
+    }
     hipLaunchKernelGGL((txv_k_scalarmult_points<B, WB, WA>), dim3(grid), dim3(B), 0, st, *args);
     return launch_batch_encode(args, st);
   } else if (args->lane_votes == 4) {

@@ -952,13 +952,63 @@ int choose_window(const txv_ctx* c, uint32_t n) {
   return 4;
 }
 
+// The wide base-point tables (11.8 GB at b_w = 24, 43 GB at 26) are the same constants for every
+// context: one per (device, window) per process, shared by reference count, built by the first
+// context that asks (under the registry lock, so a second one waits for the build).
+struct SharedBaseTable { int device, w, refs; uint32_t* ptr; };
+std::mutex g_base_mu;
+std::vector<SharedBaseTable> g_base_tabs;
+
+// a reference to the (device, w) table, built if absent; nullptr when it cannot be allocated
+uint32_t* acquire_base_table(txv_ctx* c, int w, int* err) {
+  std::lock_guard<std::mutex> g(g_base_mu);
+  *err = TXV_OK;
+  for (auto& t : g_base_tabs)
+    if (t.device == c->device && t.w == w) { ++t.refs; return t.ptr; }
+  uint32_t* p = nullptr;
+  if (hipMalloc((void**)&p, table_words(w) * 4) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  uint32_t* d_b = nullptr;
+  auto fail = [&](hipError_t e) {
+    c->err = std::string("base table build: ") + hipGetErrorString(e);
+    (void)hipFree(p);
+    if (d_b) (void)hipFree(d_b);
+    *err = TXV_EDEVICE;
+    return nullptr;
+  };
+  hipError_t e;
+  if ((e = hipMalloc((void**)&d_b, 32)) != hipSuccess) return fail(e);
+  const uint32_t bwords[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                              0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  if ((e = hipMemcpyAsync(d_b, bwords, 32, hipMemcpyHostToDevice, c->stream)) != hipSuccess) return fail(e);
+  if ((e = txv_launch_build_tables(w, d_b, 1, p, nullptr, nullptr, c->stream)) != hipSuccess) return fail(e);
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(e);
+  (void)hipFree(d_b);
+  g_base_tabs.push_back(SharedBaseTable{c->device, w, 1, p});
+  return p;
+}
+
+void release_base_table(int device, uint32_t*& p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(g_base_mu);
+  for (size_t i = 0; i < g_base_tabs.size(); ++i)
+    if (g_base_tabs[i].device == device && g_base_tabs[i].ptr == p) {
+      if (--g_base_tabs[i].refs == 0) {
+        (void)hipFree(p);
+        g_base_tabs.erase(g_base_tabs.begin() + (long)i);
+      }
+      break;
+    }
+  p = nullptr;
+}
+
 // make tab_w = w current: its B table exists; then the verify kernel's base-point window
 // b_w: the requested one if the kernels support (b_w, w), else by default the 11.8 GB radix-2^24
 // table over radix-2^12..2^20 validator tables (11 instead of 16..22 additions for [s]B).  The
 // 43 GB radix-2^26 table (10 positions) is selectable (TXV_CFG_SET_B_WINDOW(26)) but not the
-// default: measured 1.42-1.44 vs 1.44-1.46 ms per 1M-vote verify (one addition of 23 saved, paid
-// back in TLB reach), for 31 GB more HBM.  A wide table that cannot be allocated falls back to
-// radix-2^24, then to b_w = w.  d_btable = table of b_w.
+// default: one addition of 23 saved buys +0.7-1.9 % (round 3) / +1.4 % (672.6 vs 662-664M
+// votes/s on one box, profiles/r04/ab1) for 31 GB more HBM, within box-to-box noise.  Wide
+// tables are shared by every context of the process (acquire_base_table).  A wide table that
+// cannot be allocated falls back to radix-2^24, then to b_w = w.  d_btable = table of b_w.
 int select_window(txv_ctx* c, int w) {
   int r;
   // radix-2^18 / 2^20 validator tables only run against the wide base tables
@@ -969,22 +1019,16 @@ int select_window(txv_ctx* c, int w) {
   int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
   if ((c->lane_votes < 4 && c->lane_votes != 1) || !txv_verify_windows_supported(bw, w)) bw = w;
   while (bw != w && c->btable_wide_w != bw) {
-    dfree(c->d_btable_wide);
+    release_base_table(c->device, c->d_btable_wide);
     c->btable_wide_w = 0;
-    if (hipMalloc((void**)&c->d_btable_wide, table_words(bw) * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      c->d_btable_wide = nullptr;
+    int e = TXV_OK;
+    uint32_t* t = acquire_base_table(c, bw, &e);
+    if (e) return e;
+    if (!t) {
       bw = (bw == 26 && txv_verify_windows_supported(24, w)) ? 24 : w;   // no room: a narrower table
       continue;
     }
-    uint32_t* d_b = nullptr;
-    if ((r = dalloc(c, &d_b, 8))) return r;
-    const uint32_t bwords[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                                0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-    HIP_TRY(c, hipMemcpyAsync(d_b, bwords, 32, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, txv_launch_build_tables(bw, d_b, 1, c->d_btable_wide, nullptr, nullptr, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    dfree(d_b);
+    c->d_btable_wide = t;
     c->btable_wide_w = bw;
   }
   if (bw != w) {
@@ -1220,7 +1264,7 @@ void txv_destroy(txv_ctx* c) {
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
   dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
-  dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); dfree(c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
+  dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); release_base_table(c->device, c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
   dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_bitmap);
@@ -2046,6 +2090,26 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;
   std::chrono::steady_clock::time_point tp[5];
   if (prof) tp[0] = std::chrono::steady_clock::now();
+  if (!sig_full || !sig_full_off) {   // a signature > 64 bytes cannot be hashed: reject before any GPU work
+    std::atomic<bool> lg{false};
+    c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      bool l = false;
+      for (uint32_t i = lo; i < hi; ++i) l |= v->sig_len[i] > 64;
+      if (l) lg.store(true, std::memory_order_relaxed);
+    }, 8192);
+    if (lg.load()) { c->err = "signature > 64 bytes without sig_full"; return TXV_EINVAL; }
+  }
+  // a failure after the first enqueue drains the key stream before returning: its copies read
+  // the pinned buffers the next call overwrites
+#define PK_TRY(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      c->err = std::string(#x) + ": " + hipGetErrorString(e_);                            \
+      (void)hipStreamSynchronize(c->key_stream);                                           \
+      return TXV_EDEVICE;                                                                  \
+    }                                                                                      \
+  } while (0)
   // in up to 4 chunks: chunk k+1 is staged into pinned memory while chunk k is uploaded, hashed
   // and read back on the key stream (a signature longer than 64 bytes is hashed on the host below)
   const uint32_t K = n >= 32768 ? 4u : 1u;
@@ -2060,28 +2124,24 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
       for (uint32_t i = lo; i < hi; ++i) lg |= v->sig_len[i] > 64;
       if (lg) long_sig.store(true, std::memory_order_relaxed);
     }, 2048);
-    HIP_TRY(c, hipMemcpyAsync(c->d_pk_sig + (size_t)c0 * 16, c->h_pk_sig + (size_t)c0 * 16, (size_t)(c1 - c0) * 64,
+    PK_TRY(hipMemcpyAsync(c->d_pk_sig + (size_t)c0 * 16, c->h_pk_sig + (size_t)c0 * 16, (size_t)(c1 - c0) * 64,
                               hipMemcpyHostToDevice, c->key_stream));
-    HIP_TRY(c, hipMemcpyAsync(c->d_pk_len + c0, c->h_pk_len + c0, (size_t)(c1 - c0) * 4, hipMemcpyHostToDevice,
+    PK_TRY(hipMemcpyAsync(c->d_pk_len + c0, c->h_pk_len + c0, (size_t)(c1 - c0) * 4, hipMemcpyHostToDevice,
                               c->key_stream));
-    HIP_TRY(c, txv_launch_sig_keys(c->d_pk_sig + (size_t)c0 * 16, c->d_pk_len + c0, c1 - c0,
+    PK_TRY(txv_launch_sig_keys(c->d_pk_sig + (size_t)c0 * 16, c->d_pk_len + c0, c1 - c0,
                                    c->d_pk_keys + (size_t)c0 * 8, c->key_stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_pk_keys + (size_t)c0 * 8, c->d_pk_keys + (size_t)c0 * 8, (size_t)(c1 - c0) * 32,
+    PK_TRY(hipMemcpyAsync(c->h_pk_keys + (size_t)c0 * 8, c->d_pk_keys + (size_t)c0 * 8, (size_t)(c1 - c0) * 32,
                               hipMemcpyDeviceToHost, c->key_stream));
   }
   // the wait below is for this event, not the stream: a batch's prep / SignBytes that another
   // thread's txv_submit_votes enqueues on the key stream after these keys is not waited for
   // (work enqueued before them still is: the stream is in order)
-  HIP_TRY(c, hipEventRecord(c->pk_ev, c->key_stream));
-  if (long_sig.load() && (!sig_full || !sig_full_off)) {
-    HIP_TRY(c, hipEventSynchronize(c->pk_ev));
-    c->err = "signature > 64 bytes without sig_full";
-    return TXV_EINVAL;
-  }
+  PK_TRY(hipEventRecord(c->pk_ev, c->key_stream));
   if (prof) tp[1] = std::chrono::steady_clock::now();
   if (overlap) overlap();
   if (prof) tp[2] = std::chrono::steady_clock::now();
-  HIP_TRY(c, hipEventSynchronize(c->pk_ev));
+  PK_TRY(hipEventSynchronize(c->pk_ev));
+#undef PK_TRY
   if (prof) tp[3] = std::chrono::steady_clock::now();
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     memcpy(keys_out + (size_t)lo * 32, c->h_pk_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);

@@ -1,6 +1,6 @@
 """Verify time of small batches (C5's 64k votes, 1000 validators) for each K1b lane_votes mode,
 against the in-tree build or an experiment build (TXV_LIB_PATH).  Statuses are checked (all
-ADDED): python tools/debug/exp_small_batch.py [n_votes] [n_vals]"""
+ADDED): python tools/debug/exp_small_batch.py [n_votes] [n_vals] [V,V,...]"""
 import os
 import statistics
 import sys
@@ -12,7 +12,8 @@ from txflow_amd.workload import Workload, SEEDS  # noqa: E402
 
 n_votes = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 n_vals = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
-for lv in (1, 4, 8):
+lvs = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 4, 8]
+for lv in lvs:
     ctx = T.Context(max_batch=n_votes, max_txs=n_votes // n_vals + 64, max_validators=n_vals, lane_votes=lv)
     wl = Workload(ctx, n_vals, n_votes // n_vals, SEEDS["c5"])
     ctx.stage(0, wl.batch)
