@@ -963,6 +963,20 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   return pool_admit(p, ctx, keys, v->n, status_out);
 }
 
+// the order-independent half of CheckTxWithInfo for a batch (txvotepool.go:187-261): every vote's
+// txVoteKey (SHA-256(Signature), GPU) and TxVote.Size() (host workers, while the GPU hashes).  No
+// pool state is read or written, so a caller may prepare batch k+1 on one thread while
+// txv_pool_check_keys admits batch k on another (bench.py's C5 leg)
+int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
+                     const uint64_t* sig_full_off, uint8_t* keys_out, uint32_t* sizes_out) {
+  if (!p || !ctx || !v || (v->n && (!keys_out || !sizes_out))) return TXV_EINVAL;
+  return txv_sig_keys_overlap(ctx, v, sig_full, sig_full_off, keys_out, [&] {
+    txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; ++i) sizes_out[i] = vote_size(v, i);
+    });
+  });
+}
+
 int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
                     const uint64_t* sig_full_off) {
   if (!p || !ctx || !v) return TXV_EINVAL;

@@ -2518,12 +2518,22 @@ int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
   if ((r = ingest_alloc(c, g, s, wire_bytes, n))) return r;
   g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear();
   const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
+  // wire bytes inside caller memory registered with txv_host_register are DMA'd from there (no
+  // staging copy; the submit waits for the keys behind the upload, so the caller may reuse the
+  // buffer once it returns)
+  bool wire_reg = false;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    wire_reg = wire_bytes && is_registered(c, wire, wire_bytes);
+  }
   if (n) {
-    c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
-      const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
-      memcpy(s.h_arena + a, wire + a, b - a);
-    }, 16);
-    memset(s.h_arena + wire_bytes, 0, 128);
+    if (!wire_reg) {
+      c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
+        const uint64_t a = (uint64_t)lo * 65536, b = std::min<uint64_t>((uint64_t)hi * 65536, wire_bytes);
+        memcpy(s.h_arena + a, wire + a, b - a);
+      }, 16);
+      memset(s.h_arena + wire_bytes, 0, 128);
+    }
     memcpy(g.h_off, msg_off, (size_t)n * 8);
     memcpy(g.h_len, msg_len, (size_t)n * 4);
     c->pool->parallel_for(n_chunks, [&](uint32_t lo_c, uint32_t hi_c) {
@@ -2541,7 +2551,12 @@ int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     std::lock_guard<std::mutex> lk(c->mu);
     hipStream_t ks = c->key_stream;
     if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[4], 0));   // the slot's last chain ended
-    HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
+    if (wire_reg) {
+      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, wire, wire_bytes, hipMemcpyHostToDevice, ks));
+      HIP_TRY(c, hipMemsetAsync(s.d_arena_th + wire_bytes, 0, 128, ks));
+    } else {
+      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
+    }
     HIP_TRY(c, hipMemcpyAsync(g.d_off, g.h_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
     HIP_TRY(c, hipMemcpyAsync(g.d_len, g.h_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
     HIP_TRY(c, hipMemcpyAsync(g.d_span, g.h_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, ks));

@@ -150,6 +150,7 @@ def lib():
             "txv_ingest_submit": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, vp, vp, ctypes.POINTER(ctypes.c_uint64)],
                                   ctypes.c_int),
             "txv_ingest_wait": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
+            "txv_pool_prepare": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp, vp], ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
@@ -191,7 +192,7 @@ EXPORTED_SYMBOLS = [
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
-    "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait"]
+    "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -315,7 +316,8 @@ class WireBatch:
             off = np.zeros(len(msgs), np.uint64)
             if len(msgs) > 1:
                 off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
-            wire = np.frombuffer(b"".join(msgs), np.uint8) if msgs else np.zeros(0, np.uint8)
+            # a writable buffer (txv_host_register pins it for DMA)
+            wire = np.frombuffer(bytearray(b"".join(msgs)), np.uint8) if msgs else np.zeros(0, np.uint8)
             length = lens
         self.wire = np.ascontiguousarray(wire, dtype=np.uint8)
         if self.wire.size == 0:
@@ -847,6 +849,19 @@ class TxVotePool:
         ctx = self._ctx_or_raise("check_batch")
         ctx._chk(lib().txv_pool_check(self._h, ctx._h, ctypes.byref(vs), full, off, out.ctypes.data), "txv_pool_check")
         return out[:batch.n]
+
+    def prepare(self, batch: VoteBatch, long_sigs: Optional[dict] = None):
+        """txv_pool_prepare: (keys [n, 32] u8, TxVote.Size() [n] u32) of a batch -- the
+        order-independent half of check_batch; check_keys(keys, sizes) is the other half"""
+        ctx = self._ctx_or_raise("prepare")
+        n = batch.n
+        keys = np.zeros((max(n, 1), 32), np.uint8)
+        sizes = np.zeros(max(n, 1), np.uint32)
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        ctx._chk(lib().txv_pool_prepare(self._h, ctx._h, ctypes.byref(vs), full, off, keys.ctypes.data,
+                                        sizes.ctypes.data), "txv_pool_prepare")
+        return keys[:n], sizes[:n]
 
     def check_keys(self, keys: np.ndarray, sizes: np.ndarray) -> np.ndarray:
         """CheckTxWithInfo over (txVoteKey [n, 32] u8, TxVote.Size() [n] u32) pairs in arrival order

@@ -378,6 +378,12 @@ int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const u
  * (TXV_HOST_THREADS, else min(16, cores)), created on the first such call.  txvotepool.go:187-261 */
 int txv_pool_check_keys(txv_pool* pool, txv_ctx* ctx, const uint8_t* keys32, const uint32_t* sizes, uint32_t n,
                         uint8_t* status_out);
+/* The order-independent half of txv_pool_check: keys_out [n][32] = txVoteKey (SHA-256(Signature),
+ * on the GPU) and sizes_out [n] = TxVote.Size() (host workers, while the GPU hashes); reads and
+ * writes no pool state, so batch k+1 may be prepared while txv_pool_check_keys admits batch k on
+ * another thread.  txv_pool_prepare + txv_pool_check_keys = txv_pool_check.  txvotepool.go:187-261 */
+int txv_pool_prepare(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
+                     const uint64_t* sig_full_off, uint8_t* keys_out, uint32_t* sizes_out);
 /* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
  * leaves the pool if its key is there. */
 int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,

@@ -36,3 +36,20 @@ def gpu_ctx(request):
     ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256, table_w=w, lane_votes=lv)
     yield ctx
     ctx.close()
+
+
+_torch_hip_ready = False
+
+
+def pytest_runtest_setup(item):
+    """PyTorch ships its own HIP runtime beside the /opt/rocm one libtxvote.so links.  Initialise
+    torch's first, before any txv context exists (the order bench.py's N>1 path and the multi-rank
+    tests use): brought up after many contexts of the other runtime had come and gone, its device
+    enumeration once reported "No HIP GPUs are available" (profiles/r04/gpu_tests_call3.log)."""
+    global _torch_hip_ready
+    if _torch_hip_ready or item.get_closest_marker("gpu") is None:
+        return
+    _torch_hip_ready = True
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()

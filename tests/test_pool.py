@@ -210,11 +210,14 @@ def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
 
 
 @pytest.mark.gpu
-def test_pool_batch_admit_matches_oracle(oracle_lib):
+@pytest.mark.parametrize("mode", ["check", "prepare"])
+def test_pool_batch_admit_matches_oracle(oracle_lib, mode):
     """Batches of >= 4096 votes take txv_pool_check's batch path (pool.cpp batch_check: LRU
     decisions by stack distance, state written once): all-new keys, a key already cached, a key
     repeated inside the batch, a batch that evicts from the cache.  Every outcome, Size, TxsBytes,
-    ReapMaxTxs order and the LRU order equal the oracle's, including node reuse after Update."""
+    ReapMaxTxs order and the LRU order equal the oracle's, including node reuse after Update.
+    mode "prepare": the same CheckTx in its two halves, txv_pool_prepare (keys on the GPU + Size)
+    then txv_pool_check_keys (the order-dependent admission), as bench.py's C5 leg pipelines them."""
     import txflow_amd as T
     rnd = random.Random(77)
     ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
@@ -227,7 +230,12 @@ def test_pool_batch_admit_matches_oracle(oracle_lib):
 
     def check(votes):
         b, long_sigs = _batch(T, votes)
-        st = pool.check_batch(b, long_sigs)
+        if mode == "check":
+            st = pool.check_batch(b, long_sigs)
+        else:
+            keys, sizes = pool.prepare(b, long_sigs)
+            assert keys.shape == (b.n, 32) and sizes.shape == (b.n,)
+            st = pool.check_keys(keys, sizes)
         exp = ref.check(votes)
         assert np.array_equal(st, exp), np.nonzero(st != exp)[0][:10]
         assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()

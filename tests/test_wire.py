@@ -314,7 +314,7 @@ def test_host_encoder_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["sync", "pipelined"])
+@pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered"])
 def test_gpu_ingest_chain_matches_oracle(mode):
     """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
     kept in HBM) over batches of received messages against the oracle's decoder, pool and
@@ -326,7 +326,8 @@ def test_gpu_ingest_chain_matches_oracle(mode):
     mode "sync": three batches through txv_ingest_msgs; "pipelined": five batches through
     txv_ingest_submit / txv_ingest_wait with two in flight (batch k+1 decoded and pool-checked
     while batch k's TxFlow chain runs; reactor.go:170-190 -> txvotepool.go:187-261 ->
-    txflow/service.go:123-166)."""
+    txflow/service.go:123-166); "pipelined_registered": the same with the receive buffers
+    registered (txv_host_register: the wire bytes are DMA'd without a staging copy)."""
     import txflow_amd as T
     rng = random.Random(31)
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16)
@@ -388,8 +389,12 @@ def test_gpu_ingest_chain_matches_oracle(mode):
             results = [pool.ingest(T.WireBatch(part)) for part in parts]
         else:
             results, inflight = [], []
-            for part in parts:
-                inflight.append(pool.ingest_submit(T.WireBatch(part)))
+            wbs = [T.WireBatch(part) for part in parts]
+            if mode == "pipelined_registered":
+                for w in wbs:
+                    ctx.host_register(w.wire)
+            for w in wbs:
+                inflight.append(pool.ingest_submit(w))
                 if len(inflight) == 2:
                     results.append(pool.ingest_wait(inflight.pop(0)))
             while inflight:
