@@ -385,15 +385,15 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
 
 def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     """C5 from received wire bytes (SURVEY.md §8f.3 + §8a a15): the C5 stream as TxVoteMessage
-    bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) through txv_ingest_submit /
-    txv_ingest_wait per 64k-message batch, two batches in flight -- Reactor.Receive / decodeMsg on
-    the GPU, CheckTxWithInfo (keys and sizes computed on the GPU from the decoded records, LRU on
-    the host), TryAddVote for the admitted votes built on the device from the same records: the
-    wire bytes cross PCIe once, and batch k+1's decode + pool stage run while batch k's TxFlow chain
-    is on the GPU (reactor.go:170-190 -> txvotepool.go:187-261 -> txflow/service.go:123-166).
-    A drain thread waits each ticket as soon as it is submitted.  Latency-to-commit of a tx =
-    return of the wait that reported its commit event - the submit's start for the batch holding
-    its first vote."""
+    bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) per 64k-message batch through
+    txv_ingest_decode (Reactor.Receive / decodeMsg on the GPU, keys and sizes computed there from
+    the decoded records), txv_ingest_admit (CheckTxWithInfo: LRU on the host; TryAddVote for the
+    admitted votes built on the device from the same records, enqueued) and txv_ingest_wait, on
+    three threads with up to three batches in flight: the wire bytes cross PCIe once, and batch
+    k+2 decodes while k+1 is checked and k's TxFlow chain runs (reactor.go:170-190 ->
+    txvotepool.go:187-261 -> txflow/service.go:123-166).  Latency-to-commit of a tx = return of
+    the wait that reported its commit event - the decode's start for the batch holding its first
+    vote."""
     import queue
     import threading
     import txflow_amd as T
@@ -413,14 +413,27 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     pool.flush()
     runs = []
     for rep in range(3):
-        start, sub_ms, commit_t = [], [], {}
+        start, dec_ms, adm_ms, commit_t = [], [], [], {}
         state = {"added": 0, "ok": True}
-        tickets = queue.Queue()
-        slots = threading.Semaphore(2)
+        decoded, admitted = queue.Queue(), queue.Queue()
+        slots = threading.Semaphore(3)              # the library's ingest ring
+
+        # three goroutine-like stages: Receive (decode) -> CheckTx (admit) -> the commit drain (wait)
+        def admit():
+            while True:
+                item = decoded.get()
+                if item is None:
+                    admitted.put(None)
+                    return
+                k, tk = item
+                ta = time.perf_counter()
+                pool.ingest_admit(tk)
+                adm_ms.append((time.perf_counter() - ta) * 1e3)
+                admitted.put((k, tk))
 
         def drain():
             while True:
-                item = tickets.get()
+                item = admitted.get()
                 if item is None:
                     return
                 k, tk = item
@@ -432,23 +445,26 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                 for e in ev:
                     commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
 
-        td = threading.Thread(target=drain, daemon=True)
+        ta_, td_ = threading.Thread(target=admit, daemon=True), threading.Thread(target=drain, daemon=True)
         t0 = time.perf_counter()
-        td.start()
+        ta_.start()
+        td_.start()
         for k, w in enumerate(wbs):
             slots.acquire()
             ts = time.perf_counter()
             start.append(ts)
-            tk = pool.ingest_submit(w)
-            sub_ms.append((time.perf_counter() - ts) * 1e3)
-            tickets.put((k, tk))
-        tickets.put(None)
-        td.join()
+            tk = pool.ingest_decode(w)
+            dec_ms.append((time.perf_counter() - ts) * 1e3)
+            decoded.put((k, tk))
+        decoded.put(None)
+        ta_.join()
+        td_.join()
         total = time.perf_counter() - t0
         lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
         runs.append({"votes_per_s": round(wl.n / total, 1),
                      "correct": state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
-                     "p50_submit_ms": round(float(np.median(sub_ms)), 3),
+                     "p50_decode_ms": round(float(np.median(dec_ms)), 3),
+                     "p50_admit_ms": round(float(np.median(adm_ms)), 3),
                      "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
                      "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None})
         ctx.reset_flow()
@@ -459,9 +475,10 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     out = dict(runs[1])
     out.update(workload=f"C5 as wire bytes: {n_vals} validators, {wl.n} TxVoteMessages ({wire_bytes / wl.n:.1f} B avg; "
                         f"{wl.n - wl.n_unique} exact replays, CacheSize {C5_CACHE}) in {batch}-message batches through "
-                        f"txv_ingest_submit / txv_ingest_wait (decode -> pool -> TxFlow, device-resident, two batches "
-                        f"in flight; receive buffers registered with txv_host_register, so the wire bytes are DMA'd "
-                        f"without a staging copy; p50_submit_ms = upload + decode + keys + CheckTx of one batch)",
+                        f"txv_ingest_decode / txv_ingest_admit / txv_ingest_wait on three threads (decode -> pool -> "
+                        f"TxFlow, device-resident, up to three batches in flight; receive buffers registered with "
+                        f"txv_host_register, so the wire bytes are DMA'd without a staging copy; p50_decode_ms = "
+                        f"the upload + decode enqueue, p50_admit_ms = keys wait + CheckTx + TxFlow enqueue)",
                passes=3, votes_per_s_passes=[r["votes_per_s"] for r in runs], correct=all(r["correct"] for r in runs),
                pcie_bytes_per_vote_up=round(wire_bytes / wl.n + 16, 1), pcie_bytes_per_vote_down=38)
     return out

@@ -53,8 +53,9 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
 constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0, 1 also the submit ring)
-constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6, 7)
-constexpr uint32_t kSlots = 8;
+constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6-8)
+constexpr uint32_t kIngestRing = 3;
+constexpr uint32_t kSlots = kIngestSlot + kIngestRing;
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
@@ -222,9 +223,9 @@ struct txv_ctx {
   uint8_t *d_wd_out = nullptr, *h_wd_out = nullptr;
   uint64_t *d_wd_span = nullptr, *h_wd_span = nullptr;   // [chunks][2] byte span of each 128-message chunk
   hipEvent_t wd_ev[2] = {nullptr, nullptr};
-  // txv_ingest_submit / txv_ingest_wait (wire bytes -> pool -> TxFlow, device-resident): a ring of
-  // two batches (slots kIngestSlot + 0/1), each with its own offsets, decode records (they stay in
-  // HBM until the admitted votes' columns are built from them), per-message status / pool key /
+  // txv_ingest_decode / _admit / _wait (wire bytes -> pool -> TxFlow, device-resident): a ring of
+  // three batches (slots kIngestSlot + 0..2), each with its own offsets, decode records (they stay
+  // in HBM until the admitted votes' columns are built from them), per-message status / pool key /
   // TxVote.Size, the longest TxHash and the admitted messages' indices
   struct Ingest {
     uint32_t cap = 0;
@@ -236,13 +237,17 @@ struct txv_ctx {
     uint32_t *d_keys = nullptr, *h_keys = nullptr, *d_sizes = nullptr, *h_sizes = nullptr;
     uint32_t *d_list = nullptr, *h_list = nullptr, *d_max = nullptr, *h_max = nullptr;
     hipEvent_t kev = nullptr;      // statuses, keys and sizes are back in pinned memory
-    uint64_t ticket = 0;           // in flight (0 = free); guarded by mu
+    uint64_t ticket = 0;           // the batch in this slot (0 = free); guarded by mu
+    int phase = 0;                 // 0 free, 1 decoded (keys in flight), 2 admitted (TxFlow chain enqueued)
+    txv_pool* pool = nullptr;      // the pool the batch is checked against
     uint32_t n = 0, n_adm = 0;     // messages of the batch; votes the pool admitted (h_list)
     int flow_err = 0;              // the admitted votes' AddVote chain could not be enqueued
     std::string flow_msg;
-  } ing[2];
-  std::mutex ing_mu;               // ingest submits one at a time: pool order = TxFlow order
-  uint64_t ing_next = 1;           // next ingest ticket; guarded by mu
+  } ing[kIngestRing];
+  std::mutex ing_dec_mu;           // decodes one at a time (they hand out the tickets)
+  std::mutex ing_adm_mu;           // admissions one at a time, in ticket order: pool order = TxFlow order
+  uint64_t ing_next = 1;           // next ticket to decode; guarded by mu
+  uint64_t ing_admit_next = 1;     // next ticket to admit; guarded by mu
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -2450,18 +2455,21 @@ uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
 namespace {
 
 // Reactor.Receive -> CheckTxWithInfo -> TryAddVote for one batch of received messages, with the
-// decoded votes kept in HBM, split for pipelining (txv_ingest_submit / txv_ingest_wait):
-//   1 (c->mu)  upload the wire bytes into ring slot j's arena, decode (kernels_wire.hip) into
-//              records in HBM, then per decoded message its pool key, TxVote.Size() and status;
-//              only those cross PCIe back
-//   2 (no c->mu; c->ing_mu keeps the submits in order) wait for the keys, CheckTxWithInfo over
-//              the decoded messages in arrival order on the host (pool.cpp)
-//   3 (c->mu)  the admitted votes' TxVote columns built on the device from the same records and
-//              the AddVote chain of txv_add_votes enqueued (run_slot), not waited for
-// so batch k+1's upload, decode and pool stage run while batch k's TxFlow chain is on the GPU, and
-// other threads may submit or wait AddVote batches while a wire batch is in the pool stage.
-// An error after the pool stage (its votes are in the pool already) is kept for the wait, which
-// reports TXV_FLOW_NOT_RUN for the admitted votes instead of dropping them silently.
+// decoded votes kept in HBM, in three phases a node runs on its goroutines' threads:
+//   decode (txv_ingest_decode; c->ing_dec_mu, c->mu around the enqueue) the wire bytes -> ring
+//          slot j's arena (DMA'd straight from registered caller memory, else through pinned
+//          staging), decodeMsg (kernels_wire.hip) into records in HBM, then per decoded message its
+//          pool key, TxVote.Size() and status, whose copies back are enqueued; returns at once
+//   admit  (txv_ingest_admit; c->ing_adm_mu, tickets in order) wait for those keys, CheckTxWithInfo
+//          over the decoded messages in arrival order on the host (pool.cpp), then (c->mu) the
+//          admitted votes' TxVote columns built on the device from the same records and the AddVote
+//          chain of txv_add_votes enqueued (run_slot), not waited for
+//   wait   (txv_ingest_wait) the chain's statuses and commit events
+// so batch k+2 decodes while batch k+1 is in the pool stage and batch k's TxFlow chain runs, and
+// other threads may submit or wait AddVote batches meanwhile (c->mu is not held by the waits for
+// keys or for chains, nor by the pool stage).  An error after the pool stage (its votes are in the
+// pool already) is kept for the wait, which reports TXV_FLOW_NOT_RUN for the admitted votes
+// instead of dropping them silently.
 int ingest_alloc(txv_ctx* c, txv_ctx::Ingest& g, Slot& s, uint64_t wire_bytes, uint32_t n) {
   int r;
   if (n > g.cap) {
@@ -2488,44 +2496,39 @@ int ingest_alloc(txv_ctx* c, txv_ctx::Ingest& g, Slot& s, uint64_t wire_bytes, u
   return ensure_flow_slot(c, s, n);
 }
 
-int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
-                  const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint64_t* ticket) {
+int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                  const uint32_t* msg_len, uint32_t n, uint64_t* ticket) {
   if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
   for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernels trust these
     if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
       c->err = "message " + std::to_string(i) + " outside the wire buffer";
       return TXV_EINVAL;
     }
-  std::lock_guard<std::mutex> order(c->ing_mu);
+  std::lock_guard<std::mutex> order(c->ing_dec_mu);
   HostTimer ht(c->profile_host);
   uint64_t t;
   uint32_t j;
+  bool wire_reg;
   {
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(c, hipSetDevice(c->device));
     if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
     if (n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
     if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
     t = c->ing_next;
-    j = (uint32_t)((t - 1) % 2);
-    if (c->ing[j].ticket) { c->err = "two ingest batches already in flight: wait for the older one first"; return TXV_ESTATE; }
+    j = (uint32_t)((t - 1) % kIngestRing);
+    if (c->ing[j].phase) { c->err = "three ingest batches already in flight: wait for the oldest first"; return TXV_ESTATE; }
+    // registered receive buffers are DMA'd from caller memory (until the batch's admit returns)
+    wire_reg = wire_bytes && is_registered(c, wire, wire_bytes);
   }
   // ring slot j is free (its last ticket was waited: no DMA or kernel of it is pending), and only
-  // this submitter (c->ing_mu) touches it until its ticket is published
+  // this decoder (c->ing_dec_mu) touches it until its ticket is published
   txv_ctx::Ingest& g = c->ing[j];
   Slot& s = c->slots[kIngestSlot + j];
   int r;
   if ((r = ingest_alloc(c, g, s, wire_bytes, n))) return r;
-  g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear();
+  g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear(); g.pool = p;
   const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
-  // wire bytes inside caller memory registered with txv_host_register are DMA'd from there (no
-  // staging copy; the submit waits for the keys behind the upload, so the caller may reuse the
-  // buffer once it returns)
-  bool wire_reg = false;
-  {
-    std::lock_guard<std::mutex> lk(c->mu);
-    wire_reg = wire_bytes && is_registered(c, wire, wire_bytes);
-  }
   if (n) {
     if (!wire_reg) {
       c->pool->parallel_for((uint32_t)((wire_bytes + 65535) / 65536), [&](uint32_t lo, uint32_t hi) {
@@ -2548,7 +2551,9 @@ int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     }, 64);
     *g.h_max = 0;
     ht.mark("stage");
-    std::lock_guard<std::mutex> lk(c->mu);
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n) {
     hipStream_t ks = c->key_stream;
     if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[4], 0));   // the slot's last chain ended
     if (wire_reg) {
@@ -2577,34 +2582,88 @@ int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     HIP_TRY(c, hipMemcpyAsync(g.h_max, g.d_max, 4, hipMemcpyDeviceToHost, ks));
     HIP_TRY(c, hipEventRecord(g.kev, ks));
   }
-  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
-  ht.mark("decode_keys");
-  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it)
-  std::vector<uint32_t> ok;
-  ok.reserve(n);
-  for (uint32_t i = 0; i < n; ++i) {
-    if (wire_status) wire_status[i] = g.h_status[i];
-    if (pool_status) pool_status[i] = TXV_POOL_NOT_CHECKED;
-    if (g.h_status[i] == TXV_WIRE_OK) ok.push_back(i);
+  ht.mark("decode_enqueue");
+  g.ticket = t;
+  g.phase = 1;
+  c->ing_next = t + 1;
+  *ticket = t;
+  return TXV_OK;
+}
+
+int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!t) return TXV_EINVAL;
+  std::lock_guard<std::mutex> order(c->ing_adm_mu);
+  HostTimer ht(c->profile_host);
+  const uint32_t j = (uint32_t)((t - 1) % kIngestRing);
+  txv_ctx::Ingest& g = c->ing[j];
+  Slot& s = c->slots[kIngestSlot + j];
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (g.ticket != t || g.phase != 1) { c->err = "unknown ingest ticket, or not in the decoded phase"; return TXV_ESTATE; }
+    if (t != c->ing_admit_next) { c->err = "ingest tickets must be admitted in decode order"; return TXV_ESTATE; }
   }
-  const uint32_t m = (uint32_t)ok.size();
-  std::vector<uint8_t> keys((size_t)m * 32), pst(m);
-  std::vector<uint32_t> sizes(m);
-  c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t q = lo; q < hi; ++q) {
-      memcpy(keys.data() + (size_t)q * 32, g.h_keys + (size_t)ok[q] * 8, 32);
-      sizes[q] = g.h_sizes[ok[q]];
-    }
-  }, 8192);
-  if ((r = txv_pool_check_keys(p, c, keys.data(), sizes.data(), m, pst.data()))) return r;   // the pool is unchanged
+  const uint32_t n = g.n;
+  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
+  ht.mark("keys_wait");
+  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it).  When
+  // every message decoded (the usual case) the pinned keys / sizes are the pool's input as they
+  // are; otherwise the decoded ones are compacted first.
+  if (wire_status && n) memcpy(wire_status, g.h_status, n);
+  std::atomic<uint32_t> bad{0};
+  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+    uint32_t b = 0;
+    for (uint32_t i = lo; i < hi; ++i) b += g.h_status[i] != TXV_WIRE_OK;
+    if (b) bad.fetch_add(b, std::memory_order_relaxed);
+  }, 16384);
+  const bool all_ok = bad.load() == 0;
+  std::vector<uint32_t> ok;
+  std::vector<uint8_t> keys_c;
+  std::vector<uint32_t> sizes_c;
+  const uint8_t* keys = reinterpret_cast<const uint8_t*>(g.h_keys);
+  const uint32_t* sizes = g.h_sizes;
+  uint32_t m = n;
+  if (!all_ok) {
+    ok.reserve(n);
+    for (uint32_t i = 0; i < n; ++i)
+      if (g.h_status[i] == TXV_WIRE_OK) ok.push_back(i);
+    m = (uint32_t)ok.size();
+    keys_c.resize((size_t)m * 32);
+    sizes_c.resize(m);
+    c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t q = lo; q < hi; ++q) {
+        memcpy(keys_c.data() + (size_t)q * 32, g.h_keys + (size_t)ok[q] * 8, 32);
+        sizes_c[q] = g.h_sizes[ok[q]];
+      }
+    }, 8192);
+    keys = keys_c.data();
+    sizes = sizes_c.data();
+  }
+  std::unique_ptr<uint8_t[]> pst(new uint8_t[std::max<uint32_t>(m, 1)]);
+  int r = txv_pool_check_keys(g.pool, c, keys, sizes, m, pst.get());
+  if (r) {   // the pool is unchanged: the ticket ends here (no wait)
+    std::lock_guard<std::mutex> lk(c->mu);
+    g.phase = 0;
+    g.ticket = 0;
+    c->ing_admit_next = t + 1;
+    return r;
+  }
   uint32_t n_adm = 0;
-  for (uint32_t q = 0; q < m; ++q) {
-    if (pool_status) pool_status[ok[q]] = pst[q];
-    if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
+  if (all_ok) {
+    if (pool_status && m) memcpy(pool_status, pst.get(), m);
+    for (uint32_t q = 0; q < m; ++q) {
+      g.h_list[n_adm] = q;
+      n_adm += pst[q] == TXV_POOL_OK;
+    }
+  } else {
+    if (pool_status) memset(pool_status, TXV_POOL_NOT_CHECKED, n);
+    for (uint32_t q = 0; q < m; ++q) {
+      if (pool_status) pool_status[ok[q]] = pst[q];
+      if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
+    }
   }
   g.n_adm = n_adm;
   ht.mark("pool");
-  // from here on the admitted votes are in the pool: the batch gets its ticket whatever happens,
+  // from here on the admitted votes are in the pool: the batch keeps its ticket whatever happens,
   // and an error is reported by its wait together with the votes it concerns
   std::lock_guard<std::mutex> lk(c->mu);
   auto flow_stage = [&]() -> int {
@@ -2633,9 +2692,8 @@ int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     g.flow_msg = c->err.copy();
   }
   ht.mark("flow_enqueue");
-  g.ticket = t;
-  c->ing_next = t + 1;
-  *ticket = t;
+  g.phase = 2;
+  c->ing_admit_next = t + 1;
   return TXV_OK;
 }
 
@@ -2643,18 +2701,18 @@ int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_ev
                 uint32_t* n_ev) {
   if (n_ev) *n_ev = 0;
   if (!ticket) return TXV_EINVAL;
-  const uint32_t j = (uint32_t)((ticket - 1) % 2);
+  const uint32_t j = (uint32_t)((ticket - 1) % kIngestRing);
   txv_ctx::Ingest& g = c->ing[j];
   Slot& s = c->slots[kIngestSlot + j];
   hipEvent_t done = nullptr;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    if (g.ticket != ticket) { c->err = "unknown or already waited ingest ticket"; return TXV_ESTATE; }
-    const txv_ctx::Ingest& o = c->ing[1 - j];
-    if (o.ticket && o.ticket < ticket) { c->err = "ingest tickets must be waited in submission order"; return TXV_ESTATE; }
+    if (g.ticket != ticket || g.phase != 2) { c->err = "unknown, unadmitted or already waited ingest ticket"; return TXV_ESTATE; }
+    for (const auto& o : c->ing)
+      if (o.phase == 2 && o.ticket < ticket) { c->err = "ingest tickets must be waited in submission order"; return TXV_ESTATE; }
     if (!g.flow_err && g.n_adm && s.ran) done = s.ev[4];
   }
-  // the batch's chain ends without c->mu held (a submit's device stages may run meanwhile); the
+  // the batch's chain ends without c->mu held (another thread's stages may run meanwhile); the
   // slot is not reused before this ticket is released below
   if (done) HIP_TRY(c, hipEventSynchronize(done));
   std::lock_guard<std::mutex> lk(c->mu);
@@ -2682,12 +2740,48 @@ int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_ev
     if (n_ev) *n_ev = ne;
   }
   g.ticket = 0;
+  g.phase = 0;
   return r;
+}
+
+int ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                  const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint64_t* ticket) {
+  // decode + admit back to back (a decode of another thread may slip in between: admits keep
+  // ticket order, so this thread's admit then waits for the other batch's)
+  uint64_t t = 0;
+  int r = ingest_decode(c, p, wire, wire_bytes, msg_off, msg_len, n, &t);
+  if (r) return r;
+  for (;;) {
+    r = ingest_admit(c, t, wire_status, pool_status);
+    if (r != TXV_ESTATE) break;
+    uint64_t next;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      next = c->ing_admit_next;
+    }
+    if (next > t) break;            // a real state error
+    std::this_thread::yield();      // an older ticket of another thread is still to be admitted
+  }
+  if (r) return r;
+  *ticket = t;
+  return TXV_OK;
 }
 
 }  // namespace
 
 extern "C" {
+
+int txv_ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
+                      const uint32_t* msg_len, uint32_t n, uint64_t* ticket) {
+  if (!c || !p || !ticket || (n && (!wire || !msg_off || !msg_len))) return TXV_EINVAL;
+  *ticket = 0;
+  return ingest_decode(c, p, wire, wire_bytes, msg_off, msg_len, n, ticket);
+}
+
+int txv_ingest_admit(txv_ctx* c, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!c) return TXV_EINVAL;
+  return ingest_admit(c, ticket, wire_status, pool_status);
+}
 
 int txv_ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
                       const uint32_t* msg_len, uint32_t n, uint8_t* wire_status, uint8_t* pool_status, uint64_t* ticket) {

@@ -151,6 +151,9 @@ def lib():
                                   ctypes.c_int),
             "txv_ingest_wait": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_pool_prepare": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp, vp], ctypes.c_int),
+            "txv_ingest_decode": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(ctypes.c_uint64)],
+                                  ctypes.c_int),
+            "txv_ingest_admit": ([vp, ctypes.c_uint64, vp, vp], ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
@@ -192,7 +195,8 @@ EXPORTED_SYMBOLS = [
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
-    "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare"]
+    "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare",
+    "txv_ingest_decode", "txv_ingest_admit"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -919,7 +923,7 @@ class TxVotePool:
 
     def ingest_submit(self, wb: WireBatch) -> IngestTicket:
         """txv_ingest_submit: decode + CheckTxWithInfo now, the admitted votes' TxFlow chain
-        enqueued (two batches in flight; ingest_wait in submission order)"""
+        enqueued (up to three batches in flight; ingest_wait in submission order)"""
         ctx = self._ctx_or_raise("ingest_submit")
         n = wb.n
         ws = np.zeros(max(n, 1), np.uint8)
@@ -929,6 +933,25 @@ class TxVotePool:
                                          wb.len.ctypes.data, n, ws.ctypes.data, ps.ctypes.data, ctypes.byref(t)),
                  "txv_ingest_submit")
         return IngestTicket(t.value, n, ws[:n], ps[:n])
+
+    def ingest_decode(self, wb: WireBatch) -> IngestTicket:
+        """txv_ingest_decode: upload + decode + keys enqueued (returns at once); ingest_admit next"""
+        ctx = self._ctx_or_raise("ingest_decode")
+        t = ctypes.c_uint64()
+        ctx._chk(lib().txv_ingest_decode(ctx._h, self._h, wb.wire.ctypes.data, wb.nbytes, wb.off.ctypes.data,
+                                         wb.len.ctypes.data, wb.n, ctypes.byref(t)), "txv_ingest_decode")
+        n = wb.n
+        return IngestTicket(t.value, n, np.zeros(n, np.uint8), np.zeros(n, np.uint8))
+
+    def ingest_admit(self, tk: IngestTicket) -> IngestTicket:
+        """txv_ingest_admit: CheckTxWithInfo of a decoded batch + its TxFlow chain enqueued; fills
+        the ticket's wire / pool statuses"""
+        ctx = self._ctx_or_raise("ingest_admit")
+        ws = np.zeros(max(tk.n, 1), np.uint8)
+        ps = np.zeros(max(tk.n, 1), np.uint8)
+        ctx._chk(lib().txv_ingest_admit(ctx._h, tk.ticket, ws.ctypes.data, ps.ctypes.data), "txv_ingest_admit")
+        tk.wire_status, tk.pool_status = ws[:tk.n], ps[:tk.n]
+        return tk
 
     def ingest_wait(self, tk: IngestTicket, ev_cap: int = 0):
         """txv_ingest_wait: (wire status, pool status, flow status, commit events) of the batch"""

@@ -478,7 +478,7 @@ int txv_ingest_msgs(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t 
  * on the GPU, runs CheckTxWithInfo for its decoded votes on the host (wire_status / pool_status
  * are final when it returns) and enqueues the admitted votes' AddVote chain without waiting for
  * it; txv_ingest_wait(ticket) waits for that chain and reports flow_status [n] and the commit
- * events as txv_ingest_msgs does.  At most two ingest batches in flight, waited in submission
+ * events as txv_ingest_msgs does.  At most three ingest batches in flight, waited in submission
  * order; submits are serialised among themselves (pool order = TxFlow order), but the context is
  * not locked during a submit's pool stage, so AddVote batches (txv_submit_votes / txv_wait_votes)
  * and ingest waits of other threads proceed meanwhile.  The caller's buffers may be reused once
@@ -488,6 +488,18 @@ int txv_ingest_msgs(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t 
 int txv_ingest_submit(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
                       const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint8_t* wire_status,
                       uint8_t* pool_status, uint64_t* ticket);
+/* txv_ingest_submit in its two halves, for a third pipeline stage (a node's Receive goroutine
+ * decoding the next batch while the previous one is in CheckTx): txv_ingest_decode uploads the
+ * batch (wire bytes inside memory registered with txv_host_register are DMA'd from there, and
+ * read until the batch's txv_ingest_admit returns; other buffers may be reused at once), decodes
+ * it and starts its keys' copy back, returning a ticket without waiting; txv_ingest_admit(ticket)
+ * waits for the keys, runs CheckTxWithInfo and enqueues the TxFlow chain (wire_status /
+ * pool_status [n] final on return).  Tickets are admitted in decode order, at most three batches
+ * are between decode and wait; an error from txv_ingest_admit ends its ticket (the pool is
+ * unchanged, no wait follows). */
+int txv_ingest_decode(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
+                      const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint64_t* ticket);
+int txv_ingest_admit(txv_ctx* ctx, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status);
 int txv_ingest_wait(txv_ctx* ctx, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
                     uint32_t* n_ev);
 

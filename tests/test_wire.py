@@ -314,7 +314,7 @@ def test_host_encoder_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered"])
+@pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered", "three_stage"])
 def test_gpu_ingest_chain_matches_oracle(mode):
     """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
     kept in HBM) over batches of received messages against the oracle's decoder, pool and
@@ -327,7 +327,9 @@ def test_gpu_ingest_chain_matches_oracle(mode):
     txv_ingest_submit / txv_ingest_wait with two in flight (batch k+1 decoded and pool-checked
     while batch k's TxFlow chain runs; reactor.go:170-190 -> txvotepool.go:187-261 ->
     txflow/service.go:123-166); "pipelined_registered": the same with the receive buffers
-    registered (txv_host_register: the wire bytes are DMA'd without a staging copy)."""
+    registered (txv_host_register: the wire bytes are DMA'd without a staging copy); "three_stage":
+    txv_ingest_decode / txv_ingest_admit / txv_ingest_wait with three batches in the ring (batch
+    k+2 decoded while k+1 is admitted and k's TxFlow chain runs)."""
     import txflow_amd as T
     rng = random.Random(31)
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16)
@@ -387,6 +389,23 @@ def test_gpu_ingest_chain_matches_oracle(mode):
         parts = [stream[cuts[b]:cuts[b + 1]] for b in range(nb)]
         if mode == "sync":
             results = [pool.ingest(T.WireBatch(part)) for part in parts]
+        elif mode == "three_stage":
+            wbs = [T.WireBatch(part) for part in parts]
+            for w in wbs:
+                ctx.host_register(w.wire)
+            results, dec, adm = [None] * nb, [], []
+            for k, w in enumerate(wbs):
+                dec.append((k, pool.ingest_decode(w)))
+                if len(dec) == 2:
+                    kk, tk = dec.pop(0)
+                    adm.append((kk, pool.ingest_admit(tk)))
+                if len(adm) == 2:
+                    kk, tk = adm.pop(0)
+                    results[kk] = pool.ingest_wait(tk)
+            for kk, tk in dec:
+                adm.append((kk, pool.ingest_admit(tk)))
+            for kk, tk in adm:
+                results[kk] = pool.ingest_wait(tk)
         else:
             results, inflight = [], []
             wbs = [T.WireBatch(part) for part in parts]
