@@ -106,7 +106,7 @@ def main():
         res["hbm_bytes_per_launch"] = sum(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"] for d in pair)
         res["hbm_bytes_per_launch_raw_fetch"] = sum(d["hbm_read_bytes_raw"] + d["hbm_write_bytes"] for d in pair)
     # the tally chain after verify (kernels_flow.hip): HBM bytes per launch from the same passes
-    tally_names = ("txv_k_tally_min", "txv_k_tally_resolve", "txv_k_tally_cross", "txv_k_status_out", "txv_k_event_top",
+    tally_names = ("txv_k_tally_part", "txv_k_tally_min_x", "txv_k_tally_min", "txv_k_tally_resolve", "txv_k_tally_cross", "txv_k_status_out", "txv_k_event_top",
                    "txv_k_scan_count<AddedPred>", "txv_k_scan_apply<AddedPred>", "txv_k_scan_count<TouchedPred>",
                    "txv_k_scan_apply<TouchedPred>", "txv_k_scan_count<EventPred>", "txv_k_scan_apply<EventPred>")
     tk = [res["kernels"][k] for k in tally_names if k in res["kernels"]]
