@@ -271,7 +271,6 @@ __device__ __forceinline__ uint32_t find_validator(const FlowState& fs, const ui
 //         into the set table
 __global__ void __launch_bounds__(256) txv_k_route_prep(FlowState fs, FlowBatch b) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < 8 && b.bucket_n) b.bucket_n[16 * i] = 0;
   if (i >= b.n) return;
   b.ev_flag[i] = 0;
   b.mark[i] = 0;
@@ -498,74 +497,6 @@ __device__ __forceinline__ uint32_t cand_of(uint64_t c, uint32_t stamp) {
   return (uint32_t)(c >> 32) == 0xFFFFFFFFu - stamp ? (uint32_t)c : TXV_NONE;
 }
 
-constexpr uint8_t kReadCell = 1;
-// the cell step for one verified vote i of cell c (any processing order gives the same result:
-// atomicMin keeps the smallest index, and each vote learns from the old value whether it lost)
-__device__ __forceinline__ void cell_post(const FlowBatch& b, TallyCell& c, uint32_t i) {
-  if (c.acc != 0) { b.status[i] = kReadCell; return; }
-  const uint64_t key = cand_key(b.stamp, i);
-  const uint64_t old = atomicMin((unsigned long long*)&c.cand, (unsigned long long)key);
-  uint8_t tf = 0;
-  if (old < key) tf = kReadCell;                           // an earlier vote of the batch holds it
-  else if (cand_of(old, b.stamp) != TXV_NONE) b.mark[(uint32_t)old] = 1;   // took it from a later one
-  b.status[i] = tf;
-}
-
-// arrival order: every vote's set id; the votes that post to a cell go to bucket (set id mod 8)
-// as (cell index, vote) -- one atomic per (wave, bucket) -- so that tally_min can walk each
-// bucket on one XCD: an XCD then touches an eighth of the cell rows (2 MB of 16 MB at C2), which
-// its 4 MB L2 holds, instead of random 128-byte lines of all of them (profiles/r03/tally_calib:
-// a random 16-byte cell access moves ~114 B read + 32 B written)
-__global__ void __launch_bounds__(256) txv_k_tally_part(FlowState fs, FlowBatch b, uint32_t nb) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i == 0) {
-    const uint32_t created = b.blk[nb];
-    const uint32_t ns = fs.ctr->n_sets + created;
-    fs.ctr->n_sets = ns > fs.max_txs ? fs.max_txs : ns;
-  }
-  uint32_t bk = 8;                                         // 8: no bucket
-  uint32_t cidx = 0;
-  if (i < b.n) {
-    const uint32_t e = b.entry[i];
-    const uint32_t s = e == TXV_NONE ? TXV_NONE : fs.tab[e].id;
-    b.set[i] = s;
-    if (s != TXV_NONE && b.pre[i] == TXV_S_PENDING) {
-      if (b.ok[i] != 1) {
-        b.status[i] = kReadCell;
-      } else {
-        bk = s & 7u;
-        cidx = s * fs.n_vals + b.val[i];
-      }
-    }
-  }
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (uint32_t q = 0; q < 8; ++q) {
-    const uint64_t m = __ballot(bk == q);
-    if (!m) continue;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(b.bucket_n + 16 * q, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, leader, 64);
-    if (bk == q) {
-      const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-      b.bucket[(size_t)q * b.n_pad + pos] = ((uint64_t)cidx << 32) | i;
-    }
-  }
-}
-
-// bucket x = block % 8 (blocks b and b + 8 share an XCD under round-robin dispatch): the cell
-// step of the bucket's votes; grid 8 x k blocks, each striding its bucket
-__global__ void __launch_bounds__(256) txv_k_tally_min_x(FlowState fs, FlowBatch b) {
-  const uint32_t x = blockIdx.x & 7u, per = gridDim.x >> 3;
-  const uint32_t cnt = b.bucket_n[16 * x];
-  const uint64_t* bk = b.bucket + (size_t)x * b.n_pad;
-  for (uint32_t p = (blockIdx.x >> 3) * 256 + threadIdx.x; p < cnt; p += per * 256) {
-    const uint64_t ent = bk[p];
-    cell_post(b, fs.cell[ent >> 32], (uint32_t)ent);
-  }
-}
-
 // every vote's set id (after the new-id step); each verified pending vote posts its arrival
 // index to its (set, validator) cell: the cell then holds the FIRST verified vote of the group
 // (cells that already hold an accepted vote skip: their votes are decided without verification).
@@ -574,8 +505,8 @@ __global__ void __launch_bounds__(256) txv_k_tally_min_x(FlowState fs, FlowBatch
 // earlier, not verified, or a smaller arrival index was already there), and a vote that takes
 // the cell from a larger index k marks k.  A vote with status 0 and no mark is its cell's first
 // verified vote: ADDED.  With shuffled arrival order every cell access is a random 128-byte line
-// (profiles/r03/tally_calib), so resolve's re-read was a line per vote.  (Arrival-order version,
-// used when the batch has no bucket buffer; tally_part + tally_min_x otherwise.)
+// (profiles/r03/tally_calib), so resolve's re-read was a line per vote.
+constexpr uint8_t kReadCell = 1;
 __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b, uint32_t nb) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
@@ -589,7 +520,14 @@ __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b
   b.set[i] = s;
   if (s == TXV_NONE || b.pre[i] != TXV_S_PENDING) return;
   if (b.ok[i] != 1) { b.status[i] = kReadCell; return; }
-  cell_post(b, fs.cell[(size_t)s * fs.n_vals + b.val[i]], i);
+  TallyCell& c = fs.cell[(size_t)s * fs.n_vals + b.val[i]];
+  if (c.acc != 0) { b.status[i] = kReadCell; return; }
+  const uint64_t key = cand_key(b.stamp, i);
+  const uint64_t old = atomicMin((unsigned long long*)&c.cand, (unsigned long long)key);
+  uint8_t tf = 0;
+  if (old < key) tf = kReadCell;                           // an earlier vote of the batch holds it
+  else if (cand_of(old, b.stamp) != TXV_NONE) b.mark[(uint32_t)old] = 1;   // took it from a later one
+  b.status[i] = tf;
 }
 
 __device__ __forceinline__ bool pending_in_set(const FlowBatch& b, uint32_t i) {
@@ -1041,16 +979,7 @@ hipError_t txv_flow_new_ids(const FlowState* fs, const FlowBatch* b, hipStream_t
 hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets_bound, hipStream_t st) {
   const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
-  if (!TXV_SKIP(1)) {
-    if (b->bucket && b->n) {
-      hipLaunchKernelGGL(txv_k_tally_part, dim3(g), dim3(256), 0, st, *fs, *b, nb);
-      // 8 x k blocks: block j works on bucket j % 8 on XCD j % 8 (about n / 8 entries each)
-      const uint32_t k = std::max<uint32_t>(1, std::min<uint32_t>((b->n / 8 + 255) / 256, 64));
-      hipLaunchKernelGGL(txv_k_tally_min_x, dim3(8 * k), dim3(256), 0, st, *fs, *b);
-    } else {
-      hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
-    }
-  }
+  if (!TXV_SKIP(1)) hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
   if (b->n && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3((b->n + 1023) / 1024), dim3(1024), 0, st, *fs, *b);
   sets_bound = std::min(sets_bound, fs->max_txs);
   // persistent waves over the set ids: one wave per set (up to 8 waves per SIMD)

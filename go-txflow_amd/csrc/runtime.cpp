@@ -95,8 +95,6 @@ struct Slot {
   uint32_t *d_entry = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
   uint8_t* d_mark = nullptr;
-  uint64_t* d_bucket = nullptr;    // tally_part -> tally_min: [8][n_pad] cell posts by set id mod 8
-  uint32_t* d_bucket_n = nullptr;  // [8 * 16]
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
@@ -180,7 +178,6 @@ struct txv_ctx {
   std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
   bool profile_host = false;                    // TXV_PROFILE_HOST
   bool uniform_cols = true;                     // uniform columns filled on the device (TXV_UNIFORM_COLS=0: off)
-  bool tally_buckets = true;                    // XCD-bucketed tally_min (TXV_TALLY_BUCKETS=0: arrival order)
   // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
   // accepted-vote arena, counters
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
@@ -362,7 +359,6 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
       (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
       (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
-      (r = dalloc(c, &s.d_bucket, 8 * npad)) || (r = dalloc(c, &s.d_bucket_n, 8 * 16)) ||
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
     return r;
   s.flow_cap = cap;
@@ -791,9 +787,6 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
   b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
   b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk;
-  // the bucketed tally needs n_pad >= n entries per bucket: the AddVote slots' npad covers flow_cap
-  b.bucket = (c->tally_buckets && s.d_bucket && s.flow_cap >= s.n) ? s.d_bucket : nullptr;
-  b.bucket_n = b.bucket ? s.d_bucket_n : nullptr;
   b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
   return b;
 }
@@ -1251,7 +1244,6 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     c->pool.reset(new txv_host::WorkerPool(nt));
     c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
     c->uniform_cols = !(getenv("TXV_UNIFORM_COLS") && atoi(getenv("TXV_UNIFORM_COLS")) == 0);
-    c->tally_buckets = !(getenv("TXV_TALLY_BUCKETS") && atoi(getenv("TXV_TALLY_BUCKETS")) == 0);
   }
   *out = c;
   return TXV_OK;
@@ -1271,7 +1263,7 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
     hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey);
-    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); dfree(s.d_bucket); dfree(s.d_bucket_n); hfree(s.h_ev); hfree(s.h_sum);
+    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);

@@ -171,9 +171,6 @@ struct FlowBatch {
   uint8_t* ev_flag;             // [n] this vote's ADDED crossed 2/3 in the batch
   uint8_t* mark;                // [n] set by tally_min when a smaller arrival index took this vote's cell
   uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
-  uint64_t* bucket;             // [8][n_pad] (cell index << 32 | vote) of the verified votes a batch
-                                // posts to cells, by set id mod 8 (tally_part -> tally_min)
-  uint32_t* bucket_n;           // [8 * 16] entries per bucket (64 B apart), zeroed by route_prep
   // outputs in mapped host memory
   uint8_t* status_host;         // [n]
   FlowEvent* ev_host;           // [n]
