@@ -549,7 +549,7 @@ def verify_split(ctx, slot: int):
         return None
 
 
-def load_pmc(table_w: int, n_votes: int):
+def load_pmc(table_w: int, base_w: int, n_votes: int):
     """executed VALU lane-slots / vote and HBM bytes / launch of the verify pair from the committed
     PMC passes (profiles/pmc_verify.json), when they were taken on this kernel configuration"""
     pmc = os.path.join(ROOT, "profiles", "pmc_verify.json")
@@ -560,7 +560,7 @@ def load_pmc(table_w: int, n_votes: int):
             pj = json.load(f)
     except Exception:
         return None, None, None, None, None
-    if pj.get("table_window") != table_w:
+    if pj.get("table_window") != table_w or pj.get("base_window", 24) != base_w:
         return None, None, None, None, None
     same = pj.get("votes_per_launch", n_votes) == n_votes
     traffic = pj.get("hbm_bytes_per_launch") if same else None
@@ -734,8 +734,9 @@ def main():
         # roofline.achieved = algorithmic lane-ops of the verify pair per launch (W_ALG x votes) /
         # the pair's launch time (HIP events on the compute stream); the executed VALU lane-slots
         # (PMC SQ_INSTS_VALU pass of this build, profiles/pmc_verify.json) give exec_frac
-        w_exec, traffic, pmc_src, tally_bytes, k1b_busy = load_pmc(ctx.table_w, wl.n)
-        achieved = wl.n * W_ALG / (v_ms * 1e-3)
+        w_exec, traffic, pmc_src, tally_bytes, k1b_busy = load_pmc(ctx.table_w, ctx.base_w, wl.n)
+        w_alg = w_alg_for(ctx.base_w, ctx.table_w)   # the algorithm that runs: its table entries
+        achieved = wl.n * w_alg / (v_ms * 1e-3)
         exec_rate = wl.n * w_exec / (v_ms * 1e-3) if w_exec else None
         threads = args.cpu_threads or host_cores()
         cpu = None
@@ -779,8 +780,10 @@ def main():
                          "traffic": traffic, "kernel": "txv_k_challenge + txv_k_scalarmult_dyn (verify pair; txv_k_scalarmult_multi when TXV_K1B_DYNAMIC=0)",
                          "alg_bytes_per_launch": round(wl.n * VERIFY_ALG_BYTES),
                          "traffic_over_alg_bytes": None if not traffic else round(traffic / (wl.n * VERIFY_ALG_BYTES), 3),
-                         "alg_lane_ops_per_vote": W_ALG,
-                         "alg_source": f"DESIGN.md §4: SHA-512 2 blocks + ScReduce + {W_FM} field multiplies x 100",
+                         "alg_lane_ops_per_vote": w_alg,
+                         "alg_source": f"DESIGN.md §4: SHA-512 2 blocks + ScReduce + field multiplies x 100 for "
+                                       f"{-(-256 // ctx.base_w) + -(-256 // ctx.table_w)} table entries (windows "
+                                       f"{ctx.base_w}/{ctx.table_w}; bench.w_alg_for)",
                          "k1b_valu_issue_busy": None if k1b_busy is None else round(k1b_busy, 3),
                          "valu_busy_note": "K1b wave-instructions x issue cycles (64-bit class 4, others 2) / SIMD-cycles "
                                            "of the dispatch (GRBM_GUI_ACTIVE), from the committed PMC pass; "
@@ -791,8 +794,8 @@ def main():
                          "exec_frac": None if exec_rate is None else round(exec_rate / VALU_PEAK, 4),
                          "pmc_source": pmc_src,
                          "standalone": {"verify_ms": round(s_ms[1], 3),
-                                        "achieved": round(wl.n * W_ALG / (s_ms[1] * 1e-3) / 1e12, 3),
-                                        "frac": round(wl.n * W_ALG / (s_ms[1] * 1e-3) / VALU_PEAK, 4),
+                                        "achieved": round(wl.n * w_alg / (s_ms[1] * 1e-3) / 1e12, 3),
+                                        "frac": round(wl.n * w_alg / (s_ms[1] * 1e-3) / VALU_PEAK, 4),
                                         "note": "the same pair run alone after the timed region (no co-running "
                                                 "flow kernels)"},
                          "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"},

@@ -49,6 +49,7 @@ def main():
         if line:
             b = json.loads(line[-1])
             res["table_window"] = b["config"].get("table_window")
+            res["base_window"] = b["config"].get("base_window")
             res["bench_line_under_profiler"] = {k: b[k] for k in ("value", "ms_per_step", "verify_kernel_ms",
                                                                   "tally_kernels_ms") if k in b}
     kt = rows(os.path.join(a.root, "kt", "**", "*kernel_stats.csv"))
