@@ -1007,13 +1007,14 @@ void release_base_table(int device, uint32_t*& p) {
 }
 
 // make tab_w = w current: its B table exists; then the verify kernel's base-point window
-// b_w: the requested one if the kernels support (b_w, w), else by default the 43 GB radix-2^26
-// table (10 positions) over radix-2^16..2^20 validator tables and the 11.8 GB radix-2^24 one (11
-// positions) over radix-2^12 / 2^14 (instead of 16..22 additions for [s]B).  26 over 24 saves one
-// addition of 23 per vote: +1.4 % on the C2 pipeline (672.6 vs 662-664M votes/s on one box,
-// profiles/r04/ab1), +0.7-1.9 % in round 3; affordable since every context of the process shares
-// the table (acquire_base_table).  A wide table that cannot be allocated falls back to radix-2^24,
-// then to b_w = w.  d_btable = table of b_w.
+// b_w: the requested one if the kernels support (b_w, w), else by default the 11.8 GB radix-2^24
+// table over radix-2^12..2^20 validator tables (11 instead of 16..22 additions for [s]B).  The
+// 43 GB radix-2^26 table (10 positions) is selectable (TXV_CFG_SET_B_WINDOW(26)) but not the
+// default: one addition of 23 saved buys +0.7-1.9 % (round 3) / +1.4 % (672.6 vs 662-664M
+// votes/s on one box, profiles/r04/ab1), and with it as the default the GPU test suite -- several
+// contexts alive, with throw-away key tables -- ran out of HBM (profiles/r04/v2_oom_gpu_tests.log).
+// Wide tables are shared by every context of the process (acquire_base_table).  A wide table that
+// cannot be allocated falls back to radix-2^24, then to b_w = w.  d_btable = table of b_w.
 int select_window(txv_ctx* c, int w) {
   int r;
   // radix-2^18 / 2^20 validator tables only run against the wide base tables
@@ -1021,7 +1022,7 @@ int select_window(txv_ctx* c, int w) {
   c->tab_w = w;
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
-  int bw = c->cfg_bw ? c->cfg_bw : (w >= 16 ? 26 : w >= 12 ? 24 : w);
+  int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
   if ((c->lane_votes < 4 && c->lane_votes != 1) || !txv_verify_windows_supported(bw, w)) bw = w;
   while (bw != w && c->btable_wide_w != bw) {
     release_base_table(c->device, c->d_btable_wide);

@@ -86,7 +86,8 @@ typedef struct txv_ctx txv_ctx;
 /* HBM footprint of a context (MI355X: 288 GB per GPU), all allocated up front:
  *   validator tables   n_vals x table size of the window (see TXV_CFG_WINDOW): 872 MB each at the
  *                      default radix-2^20 for <= 137 validators (87 GB for 100), within table_budget_mb
- *   base-point table   11.8 GB (radix-2^24) per context, plus 0.5 MB / 74 KB for the small windows
+ *   base-point table   11.8 GB (radix-2^24; 43 GB at radix 2^26) per process and device, shared by
+ *                      its contexts, plus 0.5 MB / 74 KB for the small windows
  *   TxFlow state       12 x max_txs x n_vals B of cells + 128 x max_accepted B of accepted votes +
  *                      64 x 2 (max_txs + max_batch) B of set table + key_arena_bytes (1M sets x 100
  *                      validators: 1.2 + 8.6 + 0.3 + 0.1 GB)
@@ -127,9 +128,9 @@ typedef struct {
 #define TXV_CFG_LANE_VOTES(flags) (((flags) >> 16) & 0xFu)
 #define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
 /* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 11.8 GB, over radix-2^12..2^20
- * validator tables; else the validator window); 24 over windows 12..20; 26 (43 GB, 10 additions
- * for [s]B instead of 11) over windows 16..20; 20 / 22 over window 16 (0.9 / 3.2 GB, 13 / 12
- * additions); or equal to the window */
+ * validator tables; else the validator window; one table per process and device, shared by its
+ * contexts); 24 over windows 12..20; 26 (43 GB, 10 additions for [s]B instead of 11) over windows
+ * 16..20; 20 / 22 over window 16 (0.9 / 3.2 GB, 13 / 12 additions); or equal to the window */
 #define TXV_CFG_B_WINDOW(flags) (((flags) >> 20) & 0xFFu)
 #define TXV_CFG_SET_B_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 20)
 
