@@ -217,6 +217,15 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     ctx.bind_host_numa()
     wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch, replay=C5_REPLAY)
     expect = c5_expected_pool(wl, C5_CACHE)
+    # the batches' columns pinned once (txv_host_register, a node's receive buffers): the key
+    # upload of txv_pool_prepare and txv_submit_votes DMA them without a staging copy
+    seen = set()
+    for b in wl.batches:
+        for col in (b.height, b.ts_sec, b.ts_nanos, b.txhash_off, b.txhash_len, b.addr, b.addr_len, b.sig,
+                    b.sig_len, b.txhash_arena, b.txkey):
+            if col is not None and col.nbytes and col.ctypes.data not in seen:   # the arena is shared
+                seen.add(col.ctypes.data)
+                ctx.host_register(col)
     # Reactor.Receive -> TxVotePool.CheckTxWithInfo (GPU keys + host LRU) -> TxFlow.TryAddVote
     pool = T.TxVotePool(ctx, size=wl.n + 1, cache_size=C5_CACHE, max_txs_bytes=1 << 40)
     for _ in range(2):          # warm-up pass: first-touch of host tables and pinned buffers

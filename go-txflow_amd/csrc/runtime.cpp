@@ -2118,22 +2118,36 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
   } while (0)
   // in up to 4 chunks: chunk k+1 is staged into pinned memory while chunk k is uploaded, hashed
   // and read back on the key stream (a signature longer than 64 bytes is hashed on the host below)
-  const uint32_t K = n >= 32768 ? 4u : 1u;
+  // (every chunk is four queued operations of ~10-20 us launch / DMA latency each: a C5 batch of
+  // 64k keys -- 4 MB up, 2 MB down -- waited 0.35-0.43 ms in four chunks, so chunking starts at
+  // 256k votes, where the staging copy it overlaps is worth it; TXV_KEYS_CHUNKS overrides)
+  static const uint32_t forced_k = getenv("TXV_KEYS_CHUNKS") ? (uint32_t)std::max(1, std::min(8, atoi(getenv("TXV_KEYS_CHUNKS")))) : 0u;
+  const uint32_t K = forced_k ? std::min(forced_k, std::max(n, 1u)) : (n >= 262144 ? 4u : 1u);
   std::atomic<bool> long_sig{false};
+  // signature / length columns inside caller memory registered with txv_host_register are DMA'd
+  // from there (no staging copy)
+  bool reg;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
+  }
   for (uint32_t k = 0; k < K; ++k) {
     const uint32_t c0 = (uint32_t)((uint64_t)n * k / K), c1 = (uint32_t)((uint64_t)n * (k + 1) / K);
     c->pool->parallel_for(c1 - c0, [&](uint32_t lo, uint32_t hi) {
       lo += c0; hi += c0;
-      memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
-      memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+      if (!reg) {
+        memcpy(c->h_pk_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+        memcpy(c->h_pk_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+      }
       bool lg = false;
       for (uint32_t i = lo; i < hi; ++i) lg |= v->sig_len[i] > 64;
       if (lg) long_sig.store(true, std::memory_order_relaxed);
     }, 2048);
-    PK_TRY(hipMemcpyAsync(c->d_pk_sig + (size_t)c0 * 16, c->h_pk_sig + (size_t)c0 * 16, (size_t)(c1 - c0) * 64,
-                              hipMemcpyHostToDevice, c->key_stream));
-    PK_TRY(hipMemcpyAsync(c->d_pk_len + c0, c->h_pk_len + c0, (size_t)(c1 - c0) * 4, hipMemcpyHostToDevice,
-                              c->key_stream));
+    const void* src_sig = reg ? (const void*)(v->sig + (size_t)c0 * 64) : (const void*)(c->h_pk_sig + (size_t)c0 * 16);
+    const void* src_len = reg ? (const void*)(v->sig_len + c0) : (const void*)(c->h_pk_len + c0);
+    PK_TRY(hipMemcpyAsync(c->d_pk_sig + (size_t)c0 * 16, src_sig, (size_t)(c1 - c0) * 64, hipMemcpyHostToDevice,
+                          c->key_stream));
+    PK_TRY(hipMemcpyAsync(c->d_pk_len + c0, src_len, (size_t)(c1 - c0) * 4, hipMemcpyHostToDevice, c->key_stream));
     PK_TRY(txv_launch_sig_keys(c->d_pk_sig + (size_t)c0 * 16, c->d_pk_len + c0, c1 - c0,
                                    c->d_pk_keys + (size_t)c0 * 8, c->key_stream));
     PK_TRY(hipMemcpyAsync(c->h_pk_keys + (size_t)c0 * 8, c->d_pk_keys + (size_t)c0 * 8, (size_t)(c1 - c0) * 32,
