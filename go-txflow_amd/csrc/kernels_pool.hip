@@ -52,3 +52,264 @@ extern "C" hipError_t txv_launch_sig_keys(const uint32_t* sig, const uint32_t* s
   hipLaunchKernelGGL(txv_k_sig_keys, dim3((n + 255) / 256), dim3(256), 0, st, sig, sig_len, n, keys);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// CheckTx decisions for a batch on the GPU (pool_dev.h; the host engine is runtime.cpp's
+// pooldev_*).  The cache's order-dependent semantics are resolved by LRU stack distance, exactly
+// as pool.cpp's batch_check does it on the host: S = the L0 cache entries front to back followed
+// by the batch's pushes; the push of key k at position e hits iff k occurs earlier in S (last at
+// p) and fewer than C distinct keys lie strictly between -- (e - p - 1) minus the pairs of
+// consecutive occurrences of one key nested inside (p, e).  Previous occurrences come from a
+// sort of the pushes by a 32-bit key slice (stable, so equal slices stay in arrival order; the
+// full keys are compared inside a run), cached keys from the cache's index.
+#include <hipcub/hipcub.hpp>
+#include "pool_dev.h"
+#include "../../include/txvote.h"
+
+namespace {
+
+constexpr uint64_t kNoPair = ~0ull;
+
+__device__ __forceinline__ bool key_eq(const uint32_t* keys, uint32_t a, uint32_t b) {
+  const uint4* x = reinterpret_cast<const uint4*>(keys + (size_t)a * 8);
+  const uint4* y = reinterpret_cast<const uint4*>(keys + (size_t)b * 8);
+  const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+  return ((x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) | (x1.y ^ y1.y) |
+          (x1.z ^ y1.z) | (x1.w ^ y1.w)) == 0;
+}
+__device__ __forceinline__ bool key_eq2(const uint32_t* ka, uint32_t a, const uint32_t* kb, uint32_t b) {
+  const uint4* x = reinterpret_cast<const uint4*>(ka + (size_t)a * 8);
+  const uint4* y = reinterpret_cast<const uint4*>(kb + (size_t)b * 8);
+  const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+  return ((x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) | (x1.y ^ y1.y) |
+          (x1.z ^ y1.z) | (x1.w ^ y1.w)) == 0;
+}
+// the index's hash (a key slice the sort does not use): keys are SHA-256 outputs
+__device__ __forceinline__ uint32_t idx_hash(const uint32_t* k) { return k[5] ^ (k[6] * 0x9E3779B1u); }
+
+// position of key (keys + 8 * i) in the cache (ck / ci of length L), or -1
+__device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t* ci, uint32_t icap,
+                                              const uint32_t* keys, uint32_t i) {
+  uint32_t s = idx_hash(keys + (size_t)i * 8) & (icap - 1);
+  for (uint32_t probe = 0; probe < icap; ++probe, s = (s + 1) & (icap - 1)) {
+    const uint32_t v = ci[s];
+    if (!v) return -1;
+    if (key_eq2(ck, v - 1, keys, i)) return (int32_t)(v - 1);
+  }
+  return -1;
+}
+
+// pushes, sort input
+__global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const bool ok = !a.valid || a.valid[i] == a.valid_ok;
+  const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
+  a.push[i] = p;
+  a.hkey[i] = p ? a.keys[(size_t)i * 8 + 2] : 0xFFFFFFFFu;
+  a.hidx[i] = i;
+  a.prev[i] = -1;
+  a.crank[i] = -1;
+  a.last[i] = p;            // cleared below for a push with a later push of its key
+}
+
+// per sorted position: the nearest earlier push of the same key (runs of one slice are in arrival
+// order), else the key's cache position; a later occurrence clears last[] of the earlier one (each
+// push is the nearest later occurrence of at most one push: no two writers)
+__global__ void __launch_bounds__(256) pd_link(PoolDevArgs a) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.n) return;
+  const uint32_t i = a.sidx[j];
+  if (!a.push[i]) return;
+  const uint32_t h = a.skey[j];
+  for (int32_t jj = (int32_t)j - 1; jj >= 0 && a.skey[jj] == h; --jj) {
+    const uint32_t k = a.sidx[jj];
+    if (a.push[k] && key_eq(a.keys, k, i)) {
+      a.prev[i] = (int32_t)k;
+      a.last[k] = 0;
+      return;
+    }
+  }
+  if (a.C && *a.clen) {
+    const int32_t r = cache_find(a.ck_old, a.ci_old, a.icap, a.keys, i);
+    a.crank[i] = r;
+    if (r >= 0) a.detached[r] = 1;
+  }
+}
+
+__device__ __forceinline__ uint32_t n_pushes(const PoolDevArgs& a) {
+  return a.n ? a.aidx[a.n - 1] + a.push[a.n - 1] : 0u;
+}
+
+// the decision of every push (batch_check step 2): miss, hit, or far (counted by pd_far)
+__global__ void __launch_bounds__(256) pd_decide(PoolDevArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  a.pst[i] = kNoPair;
+  a.pend[i] = kNoPair;
+  if (!a.push[i]) { a.dec[i] = 0; return; }
+  const uint64_t C = a.C, L0 = a.C ? *a.clen : 0, na = n_pushes(a);
+  const bool cache_on = a.C != 0, evict = cache_on && L0 + na > C;
+  const uint64_t F = L0 < na ? L0 : na;                    // front entries this batch can evict
+  const uint64_t e2 = 2 * (L0 + a.aidx[i]);
+  uint8_t d = 1;
+  const int32_t pj = a.prev[i];
+  if (pj >= 0) {
+    d = !cache_on ? 1 : ((!evict || a.aidx[i] - a.aidx[pj] - 1 < C) ? 2 : 3);
+    if (evict) { a.pst[i] = 2 * (L0 + a.aidx[pj]); a.pend[i] = e2; }
+  } else if (a.crank[i] >= 0) {
+    const uint64_t r = (uint64_t)a.crank[i];
+    const bool front = evict && r < F;
+    d = (!front || L0 + a.aidx[i] - r - 1 < C) ? 2 : 3;
+    if (evict) { a.pst[i] = front ? 2 * r : 2 * L0 - 1; a.pend[i] = e2; }
+  }
+  a.dec[i] = d;
+  if (d == 3) a.far[atomicAdd(a.nfar, 1u)] = i;
+}
+
+// one block per far push (grid-strided): the pairs nested inside its window, then its decision
+__global__ void __launch_bounds__(256) pd_far(PoolDevArgs a) {
+  __shared__ uint32_t red[4];
+  const uint32_t nf = *a.nfar;
+  const uint64_t C = a.C;
+  for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+    const uint32_t i = a.far[f];
+    const uint64_t fp = a.pst[i], fe = a.pend[i];          // a far push always has its pair (evicting)
+    uint32_t cnt = 0;
+    for (uint32_t k = threadIdx.x; k < a.n; k += 256) {
+      const uint64_t s = a.pst[k];
+      cnt += (s != kNoPair) & (s > fp) & (a.pend[k] < fe);
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t nested = (uint64_t)red[0] + red[1] + red[2] + red[3];
+      const uint64_t window = (fe - fp) / 2 - 1;            // pushes strictly between (fp exact here)
+      a.dec[i] = window - nested < C ? 2 : 1;
+    }
+    __syncthreads();
+  }
+}
+
+// statuses (batch_check step 3, no cut: the host checked the caps) and the old entries' survival
+__global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < a.n) {
+    uint8_t st;
+    if (a.valid && a.valid[i] != a.valid_ok) st = TXV_POOL_NOT_CHECKED;
+    else {
+      const uint8_t d = a.dec[i];
+      st = d == 0 ? TXV_POOL_ERR_TOO_LARGE : d == 2 ? TXV_POOL_ERR_IN_CACHE
+         : (!a.sizes[i] && a.wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
+    }
+    a.status[i] = st;
+  }
+  if (i < a.C) a.surv[i] = i < *a.clen && !a.detached[i];
+}
+
+// the new cache = the last keep_old surviving old entries in order, then the last keepU of the
+// batch's U distinct pushed keys (each at its last push) in push order: the C most recent distinct
+// keys of S (batch_check step 4); the new index is cleared here and filled by pd_index
+__global__ void __launch_bounds__(256) pd_newcache(PoolDevArgs a) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t U = a.n ? a.lpos[a.n - 1] + a.last[a.n - 1] : 0u;
+  const uint32_t L1 = a.spos[a.C - 1] + a.surv[a.C - 1];
+  const uint32_t keepU = U < a.C ? U : a.C;
+  const uint32_t keep_old = L1 < a.C - keepU ? L1 : a.C - keepU;
+  if (t < a.C && a.surv[t]) {
+    const int64_t q = (int64_t)a.spos[t] - (int64_t)(L1 - keep_old);
+    if (q >= 0) {
+      const uint4* s = reinterpret_cast<const uint4*>(a.ck_old + (size_t)t * 8);
+      uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)q * 8);
+      d[0] = s[0];
+      d[1] = s[1];
+    }
+  }
+  if (t < a.n && a.last[t]) {
+    const int64_t u = (int64_t)a.lpos[t] - (int64_t)(U - keepU);
+    if (u >= 0) {
+      const uint4* s = reinterpret_cast<const uint4*>(a.keys + (size_t)t * 8);
+      uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)(keep_old + u) * 8);
+      d[0] = s[0];
+      d[1] = s[1];
+    }
+  }
+  for (uint32_t s = t; s < a.icap; s += gridDim.x * 256) a.ci_new[s] = 0;
+}
+
+// the new index over the new key array; the new length; detached[] cleared for the next batch
+__global__ void __launch_bounds__(256) pd_index(PoolDevArgs a) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t U = a.n ? a.lpos[a.n - 1] + a.last[a.n - 1] : 0u;
+  const uint32_t L1 = a.spos[a.C - 1] + a.surv[a.C - 1];
+  const uint32_t keepU = U < a.C ? U : a.C;
+  const uint32_t keep_old = L1 < a.C - keepU ? L1 : a.C - keepU;
+  const uint32_t L = keep_old + keepU;
+  if (q < a.C) a.detached[q] = 0;
+  if (q < L) {
+    uint32_t s = idx_hash(a.ck_new + (size_t)q * 8) & (a.icap - 1);
+    while (atomicCAS(&a.ci_new[s], 0u, q + 1u) != 0u) s = (s + 1) & (a.icap - 1);
+  }
+  if (q == 0) a.clen[1] = L;   // staged: pd_commit moves it into clen[0] after every reader
+}
+
+__global__ void pd_commit(uint32_t* clen) { clen[0] = clen[1]; }
+
+// an index over keys [L][8] (a cache uploaded from the host)
+__global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= L) return;
+  uint32_t s = idx_hash(ck + (size_t)q * 8) & (icap - 1);
+  while (atomicCAS(&ci[s], 0u, q + 1u) != 0u) s = (s + 1) & (icap - 1);
+}
+
+}  // namespace
+
+// hipcub temporary storage for a batch of n votes and a cache of C entries (scans of n and C,
+// the pair sort of n)
+extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C) {
+  size_t a = 0, b = 0, c = 0;
+  uint32_t* u = nullptr;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, u, u, (int)std::max<uint32_t>(n, 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, u, u, (int)std::max<uint32_t>(C, 1));
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, u, u, u, u, (int)std::max<uint32_t>(n, 1));
+  return std::max(a, std::max(b, c));
+}
+
+// the whole decision + cache update chain for one batch on stream st (a.n > 0; a.C > 0 or 0)
+extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
+  const PoolDevArgs& a = *ap;
+  const uint32_t n = a.n;
+  if (!n) return hipSuccess;
+  const dim3 gn((n + 255) / 256), b(256);
+  hipError_t e;
+  size_t tb = a.tmp_bytes;
+  hipLaunchKernelGGL(pd_init, gn, b, 0, st, a);
+  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.push, a.aidx, (int)n, st))) return e;
+  tb = a.tmp_bytes;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
+  if ((e = hipMemsetAsync(a.nfar, 0, 4, st))) return e;
+  hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
+  hipLaunchKernelGGL(pd_decide, gn, b, 0, st, a);
+  if (a.C) hipLaunchKernelGGL(pd_far, dim3(512), b, 0, st, a);
+  const uint32_t span = std::max(n, a.C);
+  hipLaunchKernelGGL(pd_status, dim3((span + 255) / 256), b, 0, st, a);
+  if (!a.C) return hipGetLastError();
+  tb = a.tmp_bytes;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.last, a.lpos, (int)n, st))) return e;
+  tb = a.tmp_bytes;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.surv, a.spos, (int)a.C, st))) return e;
+  hipLaunchKernelGGL(pd_newcache, dim3((span + 255) / 256), b, 0, st, a);
+  hipLaunchKernelGGL(pd_index, dim3((a.C + 255) / 256), b, 0, st, a);
+  hipLaunchKernelGGL(pd_commit, dim3(1), dim3(1), 0, st, a.clen);
+  return hipGetLastError();
+}
+
+// the index of a cache uploaded from the host (keys already at ck, its length at clen[0])
+extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(ci, 0, (size_t)icap * 4, st))) return e;
+  if (L) hipLaunchKernelGGL(pd_index_only, dim3((L + 255) / 256), dim3(256), 0, st, ck, L, ci, icap);
+  return hipGetLastError();
+}

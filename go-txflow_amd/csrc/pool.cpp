@@ -242,6 +242,17 @@ struct BatchScratch {
 
 }  // namespace
 
+// runtime.cpp: the device cache engine (TXV_POOL_DEVICE_CACHE)
+struct PoolDev;
+void pooldev_free(PoolDev* s);
+bool pooldev_same_device(const txv_ctx* c, const PoolDev* s);
+int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n);
+int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L);
+int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
+int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
+                  const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out);
+
 struct txv_pool {
   txv_pool_config cfg{};
   bool cache_on = true;
@@ -258,6 +269,10 @@ struct txv_pool {
   std::vector<uint8_t> part;                       // batch scratch: index partition per key (batch path)
   BatchScratch bs;                                 // batch scratch (batch path)
   std::shared_ptr<void> workers;                   // batch passes of calls without a context
+  // TXV_POOL_DEVICE_CACHE: the cache's copy in HBM (runtime.cpp's PoolDev) and which copy is current
+  PoolDev* dev = nullptr;
+  enum { kSynced, kDevAhead, kHostAhead } dev_state = kHostAhead;
+  ~txv_pool() { pooldev_free(dev); }
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -880,7 +895,12 @@ namespace {
 
 // CheckTxWithInfo for n votes in arrival order whose keys (keys) and TxVote.Size() values
 // (p->sizes) are known: the order-dependent part (caps, cache, pool list).  p->mu is held.
+int cache_to_host(txv_pool* p, txv_ctx* ctx);
+void host_cache_written(txv_pool* p);
+
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
+  if (int r = cache_to_host(p, ctx)) return r;
+  host_cache_written(p);
   const auto t1 = std::chrono::steady_clock::now();
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;   // calcMaxTxSize
   if (n >= 4096 && batch_check(p, ctx, p->bs, keys, n, status_out)) {
@@ -922,7 +942,151 @@ int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* 
   return TXV_OK;
 }
 
+// ---- TXV_POOL_DEVICE_CACHE: the cache's copy in HBM (pool_dev.h) ----
+// Exactly one of the two copies is current after any call (dev_state): a batch decided on the
+// device leaves the host's list stale (kDevAhead) until a host-side reader or writer of the cache
+// (the sequential / keys-only check paths, Update, cache_keys) fetches it back; a host-side write
+// leaves the device's stale (kHostAhead) until the next device batch uploads the list.
+bool dev_mode(const txv_pool* p) { return (p->cfg.flags & TXV_POOL_DEVICE_CACHE) != 0; }
+
+// the host's cache list = keys [L] front to back, index rebuilt (partitions on the workers)
+void cache_rebuild(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t L) {
+  p->cache.clear();
+  p->cache.nodes.resize(L);
+  for (uint32_t k = 0; k < L; ++k) p->cache.nodes[k] = KeyList::Node{keys[k], 0, (int32_t)k - 1, k + 1 < L ? (int32_t)k + 1 : -1};
+  p->cache.head = L ? 0 : -1;
+  p->cache.tail = (int32_t)L - 1;
+  p->cache.len = L;
+  pool_parallel_for(p, ctx, kParts, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t q = lo; q < hi; ++q) {
+      FlatIndex& f = *p->cache_map.p[q];
+      f.clear();
+      for (uint32_t k = 0; k < L; ++k)
+        if (PartIndex::part(keys[k]) == q) f.put(keys[k], (int32_t)k);
+    }
+  }, 1);
+}
+
+int cache_to_host(txv_pool* p, txv_ctx* ctx) {
+  if (!p->dev || p->dev_state != txv_pool::kDevAhead) return TXV_OK;
+  std::vector<uint8_t> kb;
+  if (int r = pooldev_get_cache(ctx, p->dev, kb)) return r;
+  cache_rebuild(p, ctx, reinterpret_cast<const Key*>(kb.data()), (uint32_t)(kb.size() / 32));
+  p->dev_state = txv_pool::kSynced;
+  return TXV_OK;
+}
+
+void host_cache_written(txv_pool* p) {
+  if (p->dev) p->dev_state = txv_pool::kHostAhead;
+}
+
+int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
+  if (p->dev && !pooldev_same_device(ctx, p->dev))   // moving to another GPU: the current list first
+    if (int r = cache_to_host(p, ctx)) return r;
+  PoolDev* before = p->dev;
+  if (int r = pooldev_bind(ctx, &p->dev, p->cache_on ? p->cfg.cache_size : 0u, n)) return r;
+  if (p->dev != before) p->dev_state = txv_pool::kHostAhead;   // a new device copy starts empty
+  if (p->dev_state != txv_pool::kHostAhead) return TXV_OK;
+  std::vector<Key> kl;
+  kl.reserve(p->cache.len);
+  for (int32_t e = p->cache.head; e >= 0; e = p->cache.nodes[e].next) kl.push_back(p->cache.nodes[e].k);
+  if (int r = pooldev_put_cache(ctx, p->dev, reinterpret_cast<const uint8_t*>(kl.data()), (uint32_t)kl.size())) return r;
+  p->dev_state = txv_pool::kSynced;
+  return TXV_OK;
+}
+
+// addTx for the votes a device batch admitted (status TXV_POOL_OK): txs.PushBack in arrival order,
+// txsMap.Store (a key admitted twice keeps its later node, as the sequential Store does), txsBytes
+void apply_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, const uint8_t* st, uint32_t n) {
+  const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
+  std::vector<uint64_t> cnt_c(P, 0), bytes_c(P, 0), base_c(P, 0);
+  auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
+  };
+  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      uint32_t lo, hi;
+      chunk(c, lo, hi);
+      uint64_t k = 0, b = 0;
+      for (uint32_t i = lo; i < hi; ++i)
+        if (st[i] == TXV_POOL_OK) { ++k; b += sizes[i]; }
+      cnt_c[c] = k;
+      bytes_c[c] = b;
+    }
+  }, 1);
+  uint64_t A = 0, bytes = 0;
+  for (uint32_t c = 0; c < P; ++c) { base_c[c] = A; A += cnt_c[c]; bytes += bytes_c[c]; }
+  if (!A) return;
+  next_indices(p->txs, (uint32_t)A, p->idx_t);
+  p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
+  std::vector<uint32_t>& adm = p->bs.order;                // admitted rank -> arrival index
+  adm.resize(A);
+  const int32_t old_tail = p->txs.tail;
+  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      uint32_t lo, hi;
+      chunk(c, lo, hi);
+      uint32_t a = (uint32_t)base_c[c];
+      for (uint32_t i = lo; i < hi; ++i) {
+        if (st[i] != TXV_POOL_OK) continue;
+        p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[i], sizes[i], a ? p->idx_t[a - 1] : old_tail,
+                                                  a + 1 < A ? p->idx_t[a + 1] : -1};
+        adm[a++] = i;
+      }
+    }
+  }, 1);
+  if (old_tail >= 0) p->txs.nodes[old_tail].next = p->idx_t[0]; else p->txs.head = p->idx_t[0];
+  p->txs.tail = p->idx_t[A - 1];
+  p->txs.len += A;
+  const size_t nf = p->txs.free_.size();
+  p->txs.free_.resize(nf - std::min<size_t>(nf, A));
+  pool_parallel_for(p, ctx, kParts, [&](uint32_t q0, uint32_t q1) {
+    for (uint32_t q = q0; q < q1; ++q) {
+      FlatIndex& f = *p->txs_map.p[q];
+      for (uint64_t a = 0; a < A; ++a) {
+        const Key& k = keys[adm[a]];
+        if (PartIndex::part(k) == q) f.put(k, p->idx_t[a]);
+      }
+    }
+  }, 1);
+  p->txs_bytes += (int64_t)bytes;
+}
+
+// a device batch needs the pool's Size and MaxTxsBytes caps not to bind inside it (pushes: the
+// votes that reach cache.Push, bytes: the Size() sum of the checked votes)
+bool dev_caps_ok(const txv_pool* p, uint64_t pushes, uint64_t bytes) {
+  return (int64_t)p->txs.len + (int64_t)pushes < (int64_t)p->cfg.size &&
+         p->txs_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
+}
+
 }  // namespace
+
+// CheckTxWithInfo for n decoded messages whose keys, sizes and decode statuses are in HBM (the
+// wire ingest, runtime.cpp): decided on the device when the pool keeps its cache there and the
+// caps cannot bind (*done = true; statuses for every message, TXV_POOL_NOT_CHECKED for those that
+// did not decode), else *done = false and the caller runs the host path.  h_keys / h_sizes /
+// h_valid: the same on the host.  Takes p->mu.
+int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
+                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, const uint8_t* h_valid,
+                       uint8_t valid_ok, uint32_t n, uint8_t* status_out, bool* done) {
+  *done = false;
+  std::lock_guard<std::mutex> g(p->mu);
+  if (!dev_mode(p) || !n) return TXV_OK;
+  const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+  uint64_t pushes = 0, bytes = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_valid[i] == valid_ok) { pushes += (int64_t)h_sizes[i] <= max_tx; bytes += h_sizes[i]; }
+  if (!dev_caps_ok(p, pushes, bytes)) return TXV_OK;
+  int r;
+  if ((r = cache_to_dev(p, ctx, n))) return r;
+  if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
+                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out)))
+    return r;
+  if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+  apply_admitted(p, ctx, reinterpret_cast<const Key*>(h_keys), h_sizes, status_out, n);
+  *done = true;
+  return TXV_OK;
+}
 
 // the pool's MaxMsgBytes (Reactor.Receive's decodeMsg cap, reactor.go:278-284)
 uint32_t txv_pool_max_msg_bytes(txv_pool* p) {
@@ -939,6 +1103,21 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
                         uint8_t* status_out) {
   if (!p || (n && (!keys32 || !sizes || !status_out))) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  if (dev_mode(p) && ctx && n) {   // the device path: keys and sizes uploaded, decided on the GPU
+    const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+    uint64_t pushes = 0, bytes = 0;
+    for (uint32_t i = 0; i < n; ++i) { pushes += (int64_t)sizes[i] <= max_tx; bytes += sizes[i]; }
+    if (dev_caps_ok(p, pushes, bytes)) {
+      int r;
+      if ((r = cache_to_dev(p, ctx, n))) return r;
+      if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out)))
+        return r;
+      if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+      apply_admitted(p, ctx, reinterpret_cast<const Key*>(keys32), sizes, status_out, n);
+      return TXV_OK;
+    }
+  }
   p->sizes.assign(sizes, sizes + n);
   return pool_admit(p, ctx, reinterpret_cast<const Key*>(keys32), n, status_out);
 }
@@ -948,8 +1127,43 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   const auto t0 = std::chrono::steady_clock::now();
-  // TxVote.Size() of every vote on the worker threads (order-independent) while the GPU hashes
   p->sizes.resize(v->n);
+  if (dev_mode(p) && v->n) {
+    // the device path: Size() on the host workers (with the pushes, the bytes and any long
+    // signature), then keys, decisions and the new cache in one round trip to the GPU
+    const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+    std::atomic<uint64_t> pushes{0}, bytes{0};
+    std::atomic<bool> long_sig{false};
+    txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
+      uint64_t pu = 0, by = 0;
+      bool lg = false;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t sz = vote_size(v, i);
+        p->sizes[i] = sz;
+        pu += (int64_t)sz <= max_tx;
+        by += sz;
+        lg |= v->sig_len[i] > 64;
+      }
+      pushes.fetch_add(pu, std::memory_order_relaxed);
+      bytes.fetch_add(by, std::memory_order_relaxed);
+      if (lg) long_sig.store(true, std::memory_order_relaxed);
+    });
+    if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
+      int r;
+      p->keys.resize((size_t)v->n * 32 + 32);
+      if ((r = cache_to_dev(p, ctx, v->n))) return r;
+      if ((r = pooldev_check(ctx, p->dev, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, p->keys.data(), status_out)))
+        return r;
+      if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+      apply_admitted(p, ctx, reinterpret_cast<const Key*>(p->keys.data()), p->sizes.data(), status_out, v->n);
+      if (getenv("TXV_PROFILE_HOST"))
+        fprintf(stderr, "[txv pool] device check=%.3fms n=%u\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
+      return TXV_OK;
+    }
+  }
+  // TxVote.Size() of every vote on the worker threads (order-independent) while the GPU hashes
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off, [&] {
     txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
       for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
@@ -984,6 +1198,8 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
   p->height = height;
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
+  if ((r = cache_to_host(p, ctx))) return r;
+  host_cache_written(p);
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
   for (uint32_t i = 0; i < v->n; ++i) {
     if (i + 16 < v->n) {
@@ -1110,6 +1326,7 @@ int txv_pool_flush(txv_pool* p) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   p->cache.clear(); p->cache_map.clear();
+  host_cache_written(p);
   p->txs.clear(); p->txs_map.clear();
   p->txs_bytes = 0;
   return TXV_OK;
@@ -1122,6 +1339,7 @@ int64_t txv_pool_height(txv_pool* p) { return p ? p->height : 0; }
 int txv_pool_cache_keys(txv_pool* p, uint8_t* keys_out, uint64_t cap, uint64_t* n_out) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  if (int r = cache_to_host(p, nullptr)) return r;
   uint64_t n = 0;
   for (int32_t e = p->cache.head; e >= 0; e = p->cache.nodes[e].next, ++n)
     if (keys_out && n < cap) memcpy(keys_out + 32 * n, p->cache.nodes[e].k.b, 32);

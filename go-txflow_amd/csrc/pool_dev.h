@@ -1,0 +1,51 @@
+// pool_dev.h — TxVotePool CheckTx decisions on the GPU (kernels_pool.hip), shared by the kernels
+// and the host engine (runtime.cpp).
+//
+// One batch of CheckTxWithInfo calls (txvotepool/txvotepool.go:187-261) decided in parallel by
+// LRU stack distance, the same formulation as pool.cpp's batch_check, with the cache
+// (mapTxCache, :416-438) held in HBM: a key array in recency order (front = least recent) and an
+// open-addressing index over it, double-buffered (the batch reads buffer `old`, writes `new`).
+// Preconditions the host checks before enqueueing (else pool.cpp's host path runs): the pool's
+// Size / MaxTxsBytes caps cannot bind inside the batch, and every vote's key is on the device.
+#pragma once
+#include <stdint.h>
+
+struct PoolDevArgs {
+  uint32_t n;                 // votes in the batch (arrival order)
+  const uint32_t* keys;       // [n][8] key words (SHA-256(Signature) bytes in memory order)
+  const uint32_t* sizes;      // [n] TxVote.Size()
+  const uint8_t* valid;       // [n] or null: 0 = the message did not decode (no CheckTx, status NOT_CHECKED)
+  uint32_t valid_ok;          // the value of valid[] that means "decoded"
+  int64_t max_tx;             // a vote is pushed to the cache iff Size() <= max_tx (MaxMsgBytes - 8)
+  uint32_t C;                 // cache capacity (config.CacheSize); 0 = nopTxCache
+  uint32_t wal;               // a WAL is configured: Size() == 0 -> ErrEncoding after the push
+  // the cache: keys [C][8] and index [icap] (slot = position + 1, 0 empty), old -> new
+  const uint32_t* ck_old;
+  uint32_t* ck_new;
+  const uint32_t* ci_old;
+  uint32_t* ci_new;
+  uint32_t icap;              // power of two >= 2 C
+  uint32_t* clen;             // [1] cache length: L0 read, the new length written at the end
+  // scratch (n entries unless noted)
+  uint32_t* push;             // 1 = reaches cache.Push
+  uint32_t* aidx;             // exclusive scan of push: the push's index in S after the L0 cache entries
+  uint32_t* hkey;             // sort keys (a 32-bit slice of the key; non-pushes 0xFFFFFFFF)
+  uint32_t* hidx;             // 0..n-1
+  uint32_t* skey;             // sorted
+  uint32_t* sidx;
+  int32_t* prev;              // the previous push of the same key in the batch, or -1
+  int32_t* crank;             // a first push whose key is cached: its cache position, else -1
+  uint32_t* last;             // 1 = the last push of its key in the batch
+  uint32_t* lpos;             // exclusive scan of last
+  uint8_t* dec;               // 0 not pushed, 1 miss, 2 hit, 3 far (decided by the nested-pair count)
+  uint64_t* pst;              // pair (previous occurrence, this push) in doubled S positions, when evicting
+  uint64_t* pend;
+  uint32_t* far;              // [n] far pushes
+  uint32_t* nfar;             // [1]
+  uint8_t* detached;          // [C] cached keys pushed again in this batch (cleared at the end)
+  uint32_t* surv;             // [C] old entries not pushed again
+  uint32_t* spos;             // [C] exclusive scan of surv
+  void* tmp;                  // hipcub temporary storage
+  size_t tmp_bytes;
+  uint8_t* status;            // [n] out: TXV_POOL_* per vote
+};

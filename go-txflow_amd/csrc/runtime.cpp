@@ -2466,6 +2466,9 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
 }  // extern "C"
 
 uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
+int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
+                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, const uint8_t* h_valid,
+                       uint8_t valid_ok, uint32_t n, uint8_t* status_out, bool* done);   // pool.cpp
 
 namespace {
 
@@ -2624,6 +2627,31 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
   // every message decoded (the usual case) the pinned keys / sizes are the pool's input as they
   // are; otherwise the decoded ones are compacted first.
   if (wire_status && n) memcpy(wire_status, g.h_status, n);
+  // TXV_POOL_DEVICE_CACHE: CheckTx for every decoded message decided on the device, from the keys,
+  // sizes and decode statuses the decode left in HBM (txv_pool_check_dev; not done when the pool's
+  // caps could bind -- then the host path below)
+  uint32_t n_adm = 0;
+  bool dev_done = false;
+  if (n) {
+    std::unique_ptr<uint8_t[]> dst(new uint8_t[n]);
+    const int rd = txv_pool_check_dev(g.pool, c, g.d_keys, g.d_sizes, g.d_status, reinterpret_cast<const uint8_t*>(g.h_keys),
+                                      g.h_sizes, g.h_status, TXV_WIRE_OK, n, dst.get(), &dev_done);
+    if (rd) {   // the pool is unchanged: the ticket ends here (no wait)
+      std::lock_guard<std::mutex> lk(c->mu);
+      g.phase = 0;
+      g.ticket = 0;
+      c->ing_admit_next = t + 1;
+      return rd;
+    }
+    if (dev_done) {
+      if (pool_status) memcpy(pool_status, dst.get(), n);
+      for (uint32_t i = 0; i < n; ++i) {
+        g.h_list[n_adm] = i;
+        n_adm += dst[i] == TXV_POOL_OK;
+      }
+    }
+  }
+  if (!dev_done) {
   std::atomic<uint32_t> bad{0};
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     uint32_t b = 0;
@@ -2662,7 +2690,6 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
     c->ing_admit_next = t + 1;
     return r;
   }
-  uint32_t n_adm = 0;
   if (all_ok) {
     if (pool_status && m) memcpy(pool_status, pst.get(), m);
     for (uint32_t q = 0; q < m; ++q) {
@@ -2675,6 +2702,7 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
       if (pool_status) pool_status[ok[q]] = pst[q];
       if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
     }
+  }
   }
   g.n_adm = n_adm;
   ht.mark("pool");
@@ -2702,8 +2730,8 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
     s.staged = true; s.ran = false;
     return run_slot(c, kIngestSlot + j, nullptr);
   };
-  if ((r = flow_stage())) {
-    g.flow_err = r;
+  if (const int rf = flow_stage()) {
+    g.flow_err = rf;
     g.flow_msg = c->err.copy();
   }
   ht.mark("flow_enqueue");
@@ -2827,3 +2855,211 @@ int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// TxVotePool's cache on the GPU (TXV_POOL_DEVICE_CACHE; pool_dev.h, kernels_pool.hip): the
+// engine pool.cpp drives.  Its buffers are plain hipMalloc / hipHostMalloc allocations owned by
+// the pool (freed by pooldev_free, whatever became of the context), on the device of the context
+// first used; the work runs on that context's key stream.
+#include "pool_dev.h"
+extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C);
+extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* a, hipStream_t st);
+extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st);
+
+struct PoolDev {
+  int device = -1;
+  uint32_t C = 0, icap = 0, cap_n = 0, cur = 0;
+  uint32_t* ck[2] = {nullptr, nullptr};
+  uint32_t* ci[2] = {nullptr, nullptr};
+  uint32_t* clen = nullptr;                        // [2]: length, staged new length
+  uint32_t *push = nullptr, *aidx = nullptr, *hkey = nullptr, *hidx = nullptr, *skey = nullptr, *sidx = nullptr;
+  int32_t *prev = nullptr, *crank = nullptr;
+  uint32_t *last = nullptr, *lpos = nullptr, *far = nullptr, *nfar = nullptr, *surv = nullptr, *spos = nullptr;
+  uint8_t *dec = nullptr, *detached = nullptr, *d_status = nullptr;
+  uint64_t *pst = nullptr, *pend = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  // the SoA path's inputs and outputs
+  uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
+  uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr, *h_clen = nullptr;
+  uint8_t* h_status = nullptr;
+  hipEvent_t ev = nullptr;
+  hipStream_t st = nullptr;                        // cache uploads / downloads
+  ~PoolDev() {
+    if (device < 0) return;
+    (void)hipSetDevice(device);
+    for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
+    dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx); dfree(prev);
+    dfree(crank); dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
+    dfree(detached); dfree(d_status); dfree(pst); dfree(pend); dfree(d_sig); dfree(d_len); dfree(d_keys); dfree(d_sizes);
+    if (tmp) (void)hipFree(tmp);
+    hfree(h_sig); hfree(h_len); hfree(h_keys); hfree(h_sizes); hfree(h_clen); hfree(h_status);
+    if (ev) (void)hipEventDestroy(ev);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+void pooldev_free(PoolDev* s) { delete s; }
+bool pooldev_same_device(const txv_ctx* c, const PoolDev* s) { return c && s && c->device == s->device; }
+
+// (re)binds the engine to c's device with capacity C and room for n-vote batches; a new cache
+// starts empty (length 0)
+int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  PoolDev* s = *sp;
+  if (s && (s->device != c->device || s->C != C)) { delete s; s = *sp = nullptr; }
+  const bool fresh = !s;
+  if (fresh) {
+    s = new (std::nothrow) PoolDev();
+    if (!s) return TXV_ENOMEM;
+    *sp = s;
+    s->device = c->device;
+    s->C = C;
+    s->icap = 16;
+    while (s->icap < 2 * std::max<uint32_t>(C, 1)) s->icap *= 2;
+    int r;
+    const size_t cw = (size_t)std::max<uint32_t>(C, 1);
+    if ((r = dalloc(c, &s->ck[0], cw * 8)) || (r = dalloc(c, &s->ck[1], cw * 8)) || (r = dalloc(c, &s->ci[0], s->icap)) ||
+        (r = dalloc(c, &s->ci[1], s->icap)) || (r = dalloc(c, &s->clen, 2)) || (r = dalloc(c, &s->detached, cw)) ||
+        (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 1)) ||
+        (r = halloc(c, &s->h_clen, 2)))
+      return r;
+    HIP_TRY(c, hipMemset(s->ci[0], 0, (size_t)s->icap * 4));
+    HIP_TRY(c, hipMemset(s->clen, 0, 8));
+    HIP_TRY(c, hipMemset(s->detached, 0, cw));
+    HIP_TRY(c, hipEventCreateWithFlags(&s->ev, hipEventDisableTiming));
+  }
+  if (n > s->cap_n) {
+    int r;
+    const uint32_t m = std::max<uint32_t>(n, 1024);
+    if ((r = dalloc(c, &s->push, m)) || (r = dalloc(c, &s->aidx, m)) || (r = dalloc(c, &s->hkey, m)) ||
+        (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
+        (r = dalloc(c, &s->prev, m)) || (r = dalloc(c, &s->crank, m)) || (r = dalloc(c, &s->last, m)) ||
+        (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
+        (r = dalloc(c, &s->d_status, m)) || (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
+        (r = dalloc(c, &s->d_sig, (size_t)m * 16)) || (r = dalloc(c, &s->d_len, m)) || (r = dalloc(c, &s->d_keys, (size_t)m * 8)) ||
+        (r = dalloc(c, &s->d_sizes, m)) || (r = halloc(c, &s->h_sig, (size_t)m * 16)) || (r = halloc(c, &s->h_len, m)) ||
+        (r = halloc(c, &s->h_keys, (size_t)m * 8)) || (r = halloc(c, &s->h_sizes, m)) || (r = halloc(c, &s->h_status, m)))
+      return r;
+    s->cap_n = m;
+    const size_t tb = txv_pooldev_tmp_bytes(m, std::max<uint32_t>(C, 1));
+    if (tb > s->tmp_bytes) {
+      if (s->tmp) (void)hipFree(s->tmp);
+      s->tmp = nullptr;
+      HIP_TRY(c, hipMalloc(&s->tmp, tb));
+      s->tmp_bytes = tb;
+    }
+  }
+  return TXV_OK;
+}
+
+// HIP status -> TXV_EDEVICE (the message into c->err when there is a context)
+#define PD_TRY(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      if (c) c->err = std::string(#x) + ": " + hipGetErrorString(e_);                     \
+      return TXV_EDEVICE;                                                                  \
+    }                                                                                      \
+  } while (0)
+
+// the host's cache (L keys, front to back) becomes the device's (synchronous, on the engine's
+// own stream: every batch is waited for before its call returns; c may be NULL)
+int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L) {
+  PD_TRY(hipSetDevice(s->device));
+  if (L > s->C) { if (c) c->err = "pool cache longer than its capacity"; return TXV_EINVAL; }
+  if (!s->st) PD_TRY(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+  if (L) PD_TRY(hipMemcpyAsync(s->ck[s->cur], keys, (size_t)L * 32, hipMemcpyHostToDevice, s->st));
+  s->h_clen[0] = L;
+  s->h_clen[1] = L;
+  PD_TRY(hipMemcpyAsync(s->clen, s->h_clen, 8, hipMemcpyHostToDevice, s->st));
+  PD_TRY(txv_pooldev_index(s->ck[s->cur], L, s->ci[s->cur], s->icap, s->st));
+  PD_TRY(hipStreamSynchronize(s->st));
+  return TXV_OK;
+}
+
+// the device's cache, front to back, into keys (synchronous; c may be NULL)
+int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
+  PD_TRY(hipSetDevice(s->device));
+  if (!s->st) PD_TRY(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+  PD_TRY(hipMemcpyAsync(s->h_clen, s->clen, 8, hipMemcpyDeviceToHost, s->st));
+  PD_TRY(hipStreamSynchronize(s->st));
+  const uint32_t L = s->h_clen[0];
+  keys.resize((size_t)L * 32);
+  if (L) {
+    PD_TRY(hipMemcpyAsync(keys.data(), s->ck[s->cur], (size_t)L * 32, hipMemcpyDeviceToHost, s->st));
+    PD_TRY(hipStreamSynchronize(s->st));
+  }
+  return TXV_OK;
+}
+#undef PD_TRY
+
+// one batch decided on the device (synchronous), either from a txv_votes batch (v: signatures
+// uploaded, keyed here; keys_out [n][32] receives the keys) or from keys / sizes / validity already
+// in HBM (d_keys, d_sizes, d_valid == valid_ok for a decoded message).  h_sizes: the votes'
+// TxVote.Size() on the host (v path).  status_out [n] = TXV_POOL_*.
+int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
+                  const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!n) return TXV_OK;
+  if (n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
+  hipStream_t ks = c->key_stream;
+  HostTimer ht(c->profile_host);
+  if (v) {
+    bool reg;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
+    }
+    if (!reg)
+      c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+        memcpy(s->h_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+        memcpy(s->h_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+      }, 4096);
+    memcpy(s->h_sizes, h_sizes, (size_t)n * 4);
+    HIP_TRY(c, hipMemcpyAsync(s->d_sig, reg ? (const void*)v->sig : (const void*)s->h_sig, (size_t)n * 64,
+                              hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(s->d_len, reg ? (const void*)v->sig_len : (const void*)s->h_len, (size_t)n * 4,
+                              hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(s->d_sizes, s->h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, txv_launch_sig_keys(s->d_sig, s->d_len, n, s->d_keys, ks));
+    d_keys = s->d_keys;
+    d_sizes = s->d_sizes;
+    d_valid = nullptr;
+  } else if (h_keys_in) {   // keys and sizes given on the host (txv_pool_check_keys)
+    c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      memcpy(s->h_keys + (size_t)lo * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
+      memcpy(s->h_sizes + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
+    }, 8192);
+    HIP_TRY(c, hipMemcpyAsync(s->d_keys, s->h_keys, (size_t)n * 32, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(s->d_sizes, s->h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    d_keys = s->d_keys;
+    d_sizes = s->d_sizes;
+    d_valid = nullptr;
+  }
+  PoolDevArgs a{};
+  a.n = n; a.keys = d_keys; a.sizes = d_sizes; a.valid = d_valid; a.valid_ok = valid_ok;
+  a.max_tx = max_tx; a.C = s->C; a.wal = wal ? 1u : 0u;
+  a.ck_old = s->ck[s->cur]; a.ck_new = s->ck[s->cur ^ 1]; a.ci_old = s->ci[s->cur]; a.ci_new = s->ci[s->cur ^ 1];
+  a.icap = s->icap; a.clen = s->clen;
+  a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
+  a.prev = s->prev; a.crank = s->crank; a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
+  a.pend = s->pend; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
+  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = s->d_status;
+  HIP_TRY(c, txv_pooldev_run(&a, ks));
+  HIP_TRY(c, hipMemcpyAsync(s->h_status, s->d_status, n, hipMemcpyDeviceToHost, ks));
+  if (v && keys_out) HIP_TRY(c, hipMemcpyAsync(s->h_keys, s->d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipEventRecord(s->ev, ks));
+  ht.mark("enqueue");
+  HIP_TRY(c, hipEventSynchronize(s->ev));
+  ht.mark("device");
+  if (s->C) s->cur ^= 1;
+  memcpy(status_out, s->h_status, n);
+  if (v && keys_out)
+    c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      memcpy(keys_out + (size_t)lo * 32, s->h_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
+    }, 8192);
+  ht.mark("out");
+  return TXV_OK;
+}

@@ -820,18 +820,22 @@ class IngestTicket:
         self.ticket, self.n, self.wire_status, self.pool_status = ticket, n, ws, ps
 POOL_NO_CACHE = 0xFFFFFFFF
 POOL_WAL = 0x1      # TXV_POOL_WAL
+POOL_DEVICE_CACHE = 0x2   # TXV_POOL_DEVICE_CACHE: the LRU cache in HBM, CheckTx decisions on the GPU
 
 
 class TxVotePool:
     """TxVotePool (txvotepool/txvotepool.go) over libtxvote.so: CheckTx (:180-261) per vote in
     arrival order with the txVoteKey = SHA-256(Signature) keys computed on the GPU of `ctx`,
     Update (:329-359), ReapMaxTxs (:310-324), Flush (:146-159), Size (:136), TxsBytes (:141).
-    cache_size POOL_NO_CACHE selects nopTxCache; 0 fields take tendermint's defaults."""
+    cache_size POOL_NO_CACHE selects nopTxCache; 0 fields take tendermint's defaults.
+    device_cache: TXV_POOL_DEVICE_CACHE (include/txvote.h) -- the cache lives in the HBM of
+    ctx's GPU and each batch's CheckTx decisions are made there."""
 
     def __init__(self, ctx: Optional[Context], size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
-                 max_msg_bytes: int = 0, height: int = 0, wal: bool = False):
+                 max_msg_bytes: int = 0, height: int = 0, wal: bool = False, device_cache: bool = False):
         self.ctx = ctx
-        cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes, POOL_WAL if wal else 0)
+        cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes,
+                       (POOL_WAL if wal else 0) | (POOL_DEVICE_CACHE if device_cache else 0))
         h = ctypes.c_void_p()
         rc = lib().txv_pool_new(ctypes.byref(cfg), height, ctypes.byref(h))
         if rc != 0:

@@ -351,9 +351,20 @@ typedef struct {
   uint32_t cache_size;      /* MempoolConfig.CacheSize: LRU entries; 0 -> 10000; TXV_POOL_NO_CACHE = nopTxCache */
   uint64_t max_txs_bytes;   /* MempoolConfig.MaxTxsBytes (0 -> 1 GiB) */
   uint32_t max_msg_bytes;   /* MempoolConfig.MaxMsgBytes (0 -> 1 MiB); max tx size = this - 8 (reactor.go:379) */
-  uint32_t flags;           /* TXV_POOL_WAL: the pool writes a WAL (InitWAL, node/node.go:805-807) */
+  uint32_t flags;           /* TXV_POOL_WAL: the pool writes a WAL (InitWAL, node/node.go:805-807);
+                               TXV_POOL_DEVICE_CACHE: see below */
 } txv_pool_config;
 #define TXV_POOL_WAL 0x1u
+/* The LRU cache (mapTxCache, txvotepool.go:416-438) kept in the HBM of the GPU of the context that
+ * txv_pool_check, txv_pool_check_keys (with a ctx) and the wire ingest pass, where each batch's
+ * CheckTx decisions are made in parallel (LRU stack distance: the decisions of the sequential loop)
+ * and the new cache is built; the statuses come back and the admitted votes are appended to the
+ * pool list (txs, txsMap) on the host within the same call.  A batch in which the Size or
+ * MaxTxsBytes cap could bind, or (txv_pool_check) holding a signature longer than 64 bytes, runs on
+ * the host as without the flag, as do Update and txv_pool_check_keys without a ctx: the cache list
+ * is fetched back first and uploaded again by the next device batch.  The device copy is freed with
+ * the pool. */
+#define TXV_POOL_DEVICE_CACHE 0x2u
 #define TXV_POOL_NO_CACHE 0xFFFFFFFFu
 typedef struct txv_pool txv_pool;
 

@@ -168,17 +168,20 @@ def test_sig_keys_match_sha256(gpu_ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("device_cache", [False, True], ids=["host-cache", "device-cache"])
 @pytest.mark.parametrize("cfg", [dict(size=700, cache_size=300), dict(size=2000, cache_size=0xFFFFFFFF),
                                  dict(size=100000, cache_size=50, max_txs_bytes=60000, max_msg_bytes=300),
-                                 dict(size=2000, cache_size=300, wal=True)],
-                         ids=["small-cache", "no-cache", "byte-limits", "wal"])
-def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
+                                 dict(size=2000, cache_size=300, wal=True), dict(size=100000, cache_size=300, wal=True)],
+                         ids=["small-cache", "no-cache", "byte-limits", "wal", "wal-roomy"])
+def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg, device_cache):
     """Random streams with repeated / empty / long (> 64 B) signatures, zero and out-of-range
     timestamps, long TxHashes: per-vote CheckTx results, Update, ReapMaxTxs order + sizes,
-    TxsBytes, Size and the LRU order equal the oracle's, across several batches."""
+    TxsBytes, Size and the LRU order equal the oracle's, across several batches.  device-cache:
+    TXV_POOL_DEVICE_CACHE (batches whose caps cannot bind and without long signatures are decided
+    on the GPU, the others on the host, the cache list moving between the two copies)."""
     import txflow_amd as T
     rnd = random.Random(hash(tuple(sorted(cfg.items()))) & 0xFFFF)
-    pool = T.TxVotePool(gpu_ctx, **cfg)
+    pool = T.TxVotePool(gpu_ctx, **cfg, device_cache=device_cache)
     ref = oracle_lib.Pool(**{k: v for k, v in cfg.items()})
     try:
         seen = set()
@@ -210,19 +213,20 @@ def test_pool_matches_oracle(gpu_ctx, oracle_lib, cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["check", "prepare"])
+@pytest.mark.parametrize("mode", ["check", "prepare", "device", "device-prepare"])
 def test_pool_batch_admit_matches_oracle(oracle_lib, mode):
     """Batches of >= 4096 votes take txv_pool_check's batch path (pool.cpp batch_check: LRU
     decisions by stack distance, state written once): all-new keys, a key already cached, a key
     repeated inside the batch, a batch that evicts from the cache.  Every outcome, Size, TxsBytes,
     ReapMaxTxs order and the LRU order equal the oracle's, including node reuse after Update.
     mode "prepare": the same CheckTx in its two halves, txv_pool_prepare (keys on the GPU + Size)
-    then txv_pool_check_keys (the order-dependent admission), as bench.py's C5 leg pipelines them."""
+    then txv_pool_check_keys (the order-dependent admission), as bench.py's C5 leg pipelines them.
+    mode "device" / "device-prepare": the same two with TXV_POOL_DEVICE_CACHE (decided on the GPU)."""
     import txflow_amd as T
     rnd = random.Random(77)
     ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
     cfg = dict(size=100000, cache_size=30000)
-    pool = T.TxVotePool(ctx, **cfg)
+    pool = T.TxVotePool(ctx, **cfg, device_cache=mode.startswith("device"))
     ref = oracle_lib.Pool(**cfg)
 
     def fresh(n):
@@ -230,7 +234,7 @@ def test_pool_batch_admit_matches_oracle(oracle_lib, mode):
 
     def check(votes):
         b, long_sigs = _batch(T, votes)
-        if mode == "check":
+        if mode in ("check", "device"):
             st = pool.check_batch(b, long_sigs)
         else:
             keys, sizes = pool.prepare(b, long_sigs)
@@ -282,9 +286,10 @@ def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
     def fresh(n):
         return [vote(bytes(rnd.getrandbits(8) for _ in range(64)), ts=(1_700_000_000, 1 + i)) for i in range(n)]
 
-    for cfg in (dict(size=20000, cache_size=0xFFFFFFFF), dict(size=9000, cache_size=50000),
-                dict(size=100000, cache_size=50000, max_txs_bytes=1_000_000)):
-        pool = T.TxVotePool(ctx, **cfg)
+    for cfg, dev in [(c, d) for d in (False, True) for c in (
+            dict(size=20000, cache_size=0xFFFFFFFF), dict(size=9000, cache_size=50000),
+            dict(size=100000, cache_size=50000, max_txs_bytes=1_000_000))]:
+        pool = T.TxVotePool(ctx, **cfg, device_cache=dev)
         ref = oracle_lib.Pool(**cfg)
         try:
             for votes in (fresh(6000), fresh(6000), fresh(5000)):
@@ -293,7 +298,7 @@ def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
                 b, long_sigs = _batch(T, votes)
                 st = pool.check_batch(b, long_sigs)
                 exp = ref.check(votes)
-                assert np.array_equal(st, exp), (cfg, np.nonzero(st != exp)[0][:10])
+                assert np.array_equal(st, exp), (cfg, dev, np.nonzero(st != exp)[0][:10])
                 assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
                 gk, gs = pool.reap(-1)
                 ok, os_ = ref.reap(-1)
@@ -305,7 +310,8 @@ def test_pool_batch_admit_no_cache_and_caps(oracle_lib):
 
 
 @pytest.mark.gpu
-def test_pool_replay_stream_bounded_cache(oracle_lib):
+@pytest.mark.parametrize("device_cache", [False, True], ids=["host-cache", "device-cache"])
+def test_pool_replay_stream_bounded_cache(oracle_lib, device_cache):
     """Appendix C's exact replays (near: within the last 4096 votes; far: any earlier vote) in
     32k-vote batches through txv_pool_check with tendermint's default CacheSize (10000): replays
     still cached -> ErrTxInCache, replays of evicted keys admitted again (second pool element);
@@ -313,7 +319,7 @@ def test_pool_replay_stream_bounded_cache(oracle_lib):
     import txflow_amd as T
     rnd = random.Random(79)
     ctx = T.Context(max_batch=1 << 16, max_txs=1024, max_validators=8)
-    pool = T.TxVotePool(ctx, size=1 << 20, cache_size=0)
+    pool = T.TxVotePool(ctx, size=1 << 20, cache_size=0, device_cache=device_cache)
     ref = oracle_lib.Pool(size=1 << 20, cache_size=10000)
     hist = []
     try:

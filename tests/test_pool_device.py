@@ -1,0 +1,116 @@
+"""TxVotePool.CheckTx with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE, kernels_pool.hip pd_* +
+runtime.cpp pooldev_*): every batch whose caps cannot bind is decided on the GPU by LRU stack
+distance, the others on the host after the cache list came back; the statuses, the LRU order, the
+pool order, Size and TxsBytes must equal the sequential oracle pool's after every batch.
+
+Reference: txvotepool/txvotepool.go:187-261 (CheckTxWithInfo), :416-438 (mapTxCache.Push),
+:265-270 (addTx).  The streams are test_pool_batch.py's (new keys, near / far in-batch repeats,
+replays of cached and of evicted keys, too-large and Size()==0 votes, pools that fill mid-batch),
+through txv_pool_check_keys with a GPU context."""
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+from test_pool_batch import CASES, _check_equal, _stream
+
+
+@pytest.fixture(scope="module")
+def dev_ctx():
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 15, max_txs=1024, max_validators=8)
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_device_cache_matches_oracle(dev_ctx, case):
+    import txflow_amd as T
+    name, cache, size, max_bytes, wal, replay, far, big, zero, nb, batch = case
+    O.build()
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    pool = T.TxVotePool(dev_ctx, size=size, cache_size=cache, max_txs_bytes=max_bytes, wal=wal, device_cache=True)
+    opool = O.Pool(size=size, cache_size=cache, max_txs_bytes=max_bytes, wal=wal)
+    try:
+        for b, (keys, sizes) in enumerate(_stream(rng, nb, batch, replay, far, big, zero)):
+            st = pool.check_keys(keys, sizes)
+            ost = opool.check_keys(keys, sizes)
+            _check_equal(pool, opool, st, ost, f"{name} batch {b}")
+    finally:
+        pool.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cache", [10000, 3000, 64])
+def test_device_cache_consecutive_batches(dev_ctx, cache):
+    """several device batches back to back (the device copy stays ahead of the host's; nothing
+    reads the cache in between), then Update (host) and more device batches: the statuses of
+    every batch and the final state equal the oracle's"""
+    import txflow_amd as T
+    O.build()
+    rng = np.random.default_rng(cache)
+    pool = T.TxVotePool(dev_ctx, size=1 << 20, cache_size=cache, max_txs_bytes=1 << 40, device_cache=True)
+    opool = O.Pool(size=1 << 20, cache_size=cache, max_txs_bytes=1 << 40)
+    try:
+        stream = _stream(rng, 8, 6000, replay=0.08, far_frac=0.5)
+        for b, (keys, sizes) in enumerate(stream[:4]):
+            st = pool.check_keys(keys, sizes)
+            ost = opool.check_keys(keys, sizes)
+            assert np.array_equal(st, ost), f"batch {b}: {int(np.count_nonzero(st != ost))} mismatches"
+        _check_equal(pool, opool, st, ost, "after 4 device batches")
+        for b, (keys, sizes) in enumerate(stream[4:]):
+            st = pool.check_keys(keys, sizes)
+            ost = opool.check_keys(keys, sizes)
+            assert np.array_equal(st, ost), f"batch {4 + b}: {int(np.count_nonzero(st != ost))} mismatches"
+        _check_equal(pool, opool, st, ost, "after 8 device batches")
+        pool.flush()
+        opool.flush()
+        keys, sizes = stream[0]
+        st = pool.check_keys(keys, sizes)                        # the flushed (empty) cache uploaded again
+        _check_equal(pool, opool, st, opool.check_keys(keys, sizes), "after flush")
+        assert (st == T.POOL_OK).sum() > 5000
+    finally:
+        pool.close()
+
+
+@pytest.mark.gpu
+def test_device_cache_soa_batches_with_update(dev_ctx):
+    """txv_pool_check (keys hashed on the GPU from the signatures) with the device cache, Update
+    between batches (the cache list comes back to the host, is pushed to, goes up again): the
+    statuses, Size, TxsBytes, reap order and LRU order equal the oracle's"""
+    import random
+
+    import txflow_amd as T
+    from test_pool import _batch, vote
+    rnd = random.Random(81)
+    cfg = dict(size=1 << 20, cache_size=5000)
+    pool = T.TxVotePool(dev_ctx, **cfg, device_cache=True)
+    ref = O.Pool(**cfg)
+    hist = []
+    try:
+        for b in range(5):
+            votes = []
+            for i in range(8192):
+                if hist and rnd.random() < 0.06:
+                    votes.append(dict(hist[rnd.randrange(len(hist))]))
+                else:
+                    votes.append(vote(rnd.randbytes(64), ts=(1_700_000_000, 1 + len(hist))))
+                hist.append(votes[-1])
+            bt, long_sigs = _batch(T, votes)
+            st = pool.check_batch(bt, long_sigs)
+            exp = ref.check(votes)
+            assert np.array_equal(st, exp), (b, np.nonzero(st != exp)[0][:10])
+            if b % 2:
+                committed = rnd.sample(votes, 700)
+                cb, clong = _batch(T, committed)
+                pool.update(b + 1, cb, clong)
+                ref.update(b + 1, committed)
+            assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+            gk, gs = pool.reap(-1)
+            ok, os_ = ref.reap(-1)
+            assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+        assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+    finally:
+        pool.close()

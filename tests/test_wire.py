@@ -314,7 +314,8 @@ def test_host_encoder_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered", "three_stage"])
+@pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered", "three_stage", "sync_device",
+                                  "three_stage_device"])
 def test_gpu_ingest_chain_matches_oracle(mode):
     """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
     kept in HBM) over batches of received messages against the oracle's decoder, pool and
@@ -329,7 +330,9 @@ def test_gpu_ingest_chain_matches_oracle(mode):
     txflow/service.go:123-166); "pipelined_registered": the same with the receive buffers
     registered (txv_host_register: the wire bytes are DMA'd without a staging copy); "three_stage":
     txv_ingest_decode / txv_ingest_admit / txv_ingest_wait with three batches in the ring (batch
-    k+2 decoded while k+1 is admitted and k's TxFlow chain runs)."""
+    k+2 decoded while k+1 is admitted and k's TxFlow chain runs); "*_device": the same with the
+    pool's cache in HBM (TXV_POOL_DEVICE_CACHE: CheckTx decided on the GPU from the keys, sizes and
+    decode statuses the decode left there)."""
     import txflow_amd as T
     rng = random.Random(31)
     ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16)
@@ -380,7 +383,9 @@ def test_gpu_ingest_chain_matches_oracle(mode):
         for m in junk:
             stream.insert(rng.randrange(len(stream) + 1), m)
         max_msg = 4096
-        pool = T.TxVotePool(ctx, size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
+        pool = T.TxVotePool(ctx, size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg,
+                            device_cache=mode.endswith("_device"))
+        mode = mode.replace("_device", "")
         opool = O.Pool(size=1 << 20, cache_size=150, max_txs_bytes=1 << 30, max_msg_bytes=max_msg)
         flow = O.Flow(pubs, powers, b"test_chain_id")
         nb = 3 if mode == "sync" else 5
