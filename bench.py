@@ -273,7 +273,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                 for k, b in enumerate(wl.batches):
                     ts = time.perf_counter()
                     if device_cache:                     # the whole CheckTx batch, one call
-                        prepared.put((k, ts, time.perf_counter(), None, pool.check_batch(b)))
+                        ps = pool.check_batch(b)
+                        prepared.put((k, ts, time.perf_counter(), None, ps))
                     else:
                         keys, sizes = pool.prepare(b)
                         prepared.put((k, ts, time.perf_counter(), keys, sizes))
@@ -369,11 +370,11 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             runs.append(out)
             ctx.reset_flow()
             pool.flush()
-        return runs
+        return runs, dev_ms, dev_split
 
-    pool_h, runs_h = run_mode(False)
+    pool_h, (runs_h, _, _) = run_mode(False)
     pool_h.close()
-    pool, runs = run_mode(True)
+    pool, (runs, dev_ms, dev_split) = run_mode(True)
     # unloaded latency: one batch at a time (CheckTx -> submit -> wait before the next batch's
     # CheckTx), so a batch's latency is its own chain, with no queueing behind others
     one_start, one_ms, one_commit, one_ok = [], [], {}, True

@@ -102,83 +102,85 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
 // pushes, sort input
 __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) { a.nfar[0] = 0; a.nfar[1] = 0; }   // far pushes, pairs (appended by pd_link)
   if (i >= a.n) return;
   const bool ok = !a.valid || a.valid[i] == a.valid_ok;
   const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
   a.push[i] = p;
   a.hkey[i] = p ? a.keys[(size_t)i * 8 + 2] : 0xFFFFFFFFu;
   a.hidx[i] = i;
-  a.prev[i] = -1;
-  a.crank[i] = -1;
   a.last[i] = p;            // cleared below for a push with a later push of its key
-}
-
-// per sorted position: the nearest earlier push of the same key (runs of one slice are in arrival
-// order), else the key's cache position; a later occurrence clears last[] of the earlier one (each
-// push is the nearest later occurrence of at most one push: no two writers)
-__global__ void __launch_bounds__(256) pd_link(PoolDevArgs a) {
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.n) return;
-  const uint32_t i = a.sidx[j];
-  if (!a.push[i]) return;
-  const uint32_t h = a.skey[j];
-  for (int32_t jj = (int32_t)j - 1; jj >= 0 && a.skey[jj] == h; --jj) {
-    const uint32_t k = a.sidx[jj];
-    if (a.push[k] && key_eq(a.keys, k, i)) {
-      a.prev[i] = (int32_t)k;
-      a.last[k] = 0;
-      return;
-    }
-  }
-  if (a.C && *a.clen) {
-    const int32_t r = cache_find(a.ck_old, a.ci_old, a.icap, a.keys, i);
-    a.crank[i] = r;
-    if (r >= 0) a.detached[r] = 1;
-  }
 }
 
 __device__ __forceinline__ uint32_t n_pushes(const PoolDevArgs& a) {
   return a.n ? a.aidx[a.n - 1] + a.push[a.n - 1] : 0u;
 }
 
-// the decision of every push (batch_check step 2): miss, hit, or far (counted by pd_far)
-__global__ void __launch_bounds__(256) pd_decide(PoolDevArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
+// per sorted position j, for vote i = sidx[j]: the nearest earlier push of the same key (runs of
+// one slice are in arrival order; that push's last[] is cleared -- each push is the nearest later
+// occurrence of at most one push, so no two writers), else the key's cache position; then the
+// push's decision (batch_check step 2): miss, hit, or far (counted by pd_far), with its pair
+// (previous occurrence, this push) in doubled S positions while evicting
+__global__ void __launch_bounds__(256) pd_link(PoolDevArgs a) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.n) return;
+  const uint32_t i = a.sidx[j];
   a.pst[i] = kNoPair;
   a.pend[i] = kNoPair;
   if (!a.push[i]) { a.dec[i] = 0; return; }
+  const uint32_t h = a.skey[j];
+  int32_t pj = -1, cr = -1;
+  for (int32_t jj = (int32_t)j - 1; jj >= 0 && a.skey[jj] == h; --jj) {
+    const uint32_t k = a.sidx[jj];
+    if (a.push[k] && key_eq(a.keys, k, i)) {
+      pj = (int32_t)k;
+      a.last[k] = 0;
+      break;
+    }
+  }
   const uint64_t C = a.C, L0 = a.C ? *a.clen : 0, na = n_pushes(a);
-  const bool cache_on = a.C != 0, evict = cache_on && L0 + na > C;
+  if (pj < 0 && C && L0) {
+    cr = cache_find(a.ck_old, a.ci_old, a.icap, a.keys, i);
+    if (cr >= 0) a.detached[cr] = 1;
+  }
+  const bool cache_on = C != 0, evict = cache_on && L0 + na > C;
   const uint64_t F = L0 < na ? L0 : na;                    // front entries this batch can evict
   const uint64_t e2 = 2 * (L0 + a.aidx[i]);
   uint8_t d = 1;
-  const int32_t pj = a.prev[i];
+  uint64_t ps = kNoPair;
   if (pj >= 0) {
     d = !cache_on ? 1 : ((!evict || a.aidx[i] - a.aidx[pj] - 1 < C) ? 2 : 3);
-    if (evict) { a.pst[i] = 2 * (L0 + a.aidx[pj]); a.pend[i] = e2; }
-  } else if (a.crank[i] >= 0) {
-    const uint64_t r = (uint64_t)a.crank[i];
+    if (evict) ps = 2 * (L0 + a.aidx[pj]);
+  } else if (cr >= 0) {
+    const uint64_t r = (uint64_t)cr;
     const bool front = evict && r < F;
     d = (!front || L0 + a.aidx[i] - r - 1 < C) ? 2 : 3;
-    if (evict) { a.pst[i] = front ? 2 * r : 2 * L0 - 1; a.pend[i] = e2; }
+    if (evict) ps = front ? 2 * r : 2 * L0 - 1;
   }
   a.dec[i] = d;
+  if (ps != kNoPair) {                      // the pair list the far counts scan (order irrelevant)
+    a.pst[i] = ps;
+    a.pend[i] = e2;
+    const uint32_t q = atomicAdd(a.nfar + 1, 1u);
+    a.plist[2 * (size_t)q] = ps;
+    a.plist[2 * (size_t)q + 1] = e2;
+  }
   if (d == 3) a.far[atomicAdd(a.nfar, 1u)] = i;
 }
 
 // one block per far push (grid-strided): the pairs nested inside its window, then its decision
 __global__ void __launch_bounds__(256) pd_far(PoolDevArgs a) {
   __shared__ uint32_t red[4];
-  const uint32_t nf = *a.nfar;
+  const uint32_t nf = a.nfar[0], np = a.nfar[1];
   const uint64_t C = a.C;
+  const ulonglong2* pl = reinterpret_cast<const ulonglong2*>(a.plist);
   for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
     const uint32_t i = a.far[f];
     const uint64_t fp = a.pst[i], fe = a.pend[i];          // a far push always has its pair (evicting)
     uint32_t cnt = 0;
-    for (uint32_t k = threadIdx.x; k < a.n; k += 256) {
-      const uint64_t s = a.pst[k];
-      cnt += (s != kNoPair) & (s > fp) & (a.pend[k] < fe);
+    for (uint32_t k = threadIdx.x; k < np; k += 256) {
+      const ulonglong2 pr = pl[k];
+      cnt += (pr.x > fp) & (pr.y < fe);
     }
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
@@ -251,10 +253,8 @@ __global__ void __launch_bounds__(256) pd_index(PoolDevArgs a) {
     uint32_t s = idx_hash(a.ck_new + (size_t)q * 8) & (a.icap - 1);
     while (atomicCAS(&a.ci_new[s], 0u, q + 1u) != 0u) s = (s + 1) & (a.icap - 1);
   }
-  if (q == 0) a.clen[1] = L;   // staged: pd_commit moves it into clen[0] after every reader
+  if (q == 0) a.clen[0] = L;   // its readers (pd_link .. pd_status) ran in earlier launches
 }
-
-__global__ void pd_commit(uint32_t* clen) { clen[0] = clen[1]; }
 
 // an index over keys [L][8] (a cache uploaded from the host)
 __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap) {
@@ -289,10 +289,8 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.push, a.aidx, (int)n, st))) return e;
   tb = a.tmp_bytes;
   if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
-  if ((e = hipMemsetAsync(a.nfar, 0, 4, st))) return e;
   hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
-  hipLaunchKernelGGL(pd_decide, gn, b, 0, st, a);
-  if (a.C) hipLaunchKernelGGL(pd_far, dim3(512), b, 0, st, a);
+  if (a.C) hipLaunchKernelGGL(pd_far, dim3(256), b, 0, st, a);
   const uint32_t span = std::max(n, a.C);
   hipLaunchKernelGGL(pd_status, dim3((span + 255) / 256), b, 0, st, a);
   if (!a.C) return hipGetLastError();
@@ -302,7 +300,6 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.surv, a.spos, (int)a.C, st))) return e;
   hipLaunchKernelGGL(pd_newcache, dim3((span + 255) / 256), b, 0, st, a);
   hipLaunchKernelGGL(pd_index, dim3((a.C + 255) / 256), b, 0, st, a);
-  hipLaunchKernelGGL(pd_commit, dim3(1), dim3(1), 0, st, a.clen);
   return hipGetLastError();
 }
 

@@ -22,7 +22,9 @@
 #include "amino.hpp"
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <sys/mman.h>
@@ -251,7 +253,7 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L);
 int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out);
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after);
 
 struct txv_pool {
   txv_pool_config cfg{};
@@ -272,7 +274,19 @@ struct txv_pool {
   // TXV_POOL_DEVICE_CACHE: the cache's copy in HBM (runtime.cpp's PoolDev) and which copy is current
   PoolDev* dev = nullptr;
   enum { kSynced, kDevAhead, kHostAhead } dev_state = kHostAhead;
-  ~txv_pool() { pooldev_free(dev); }
+  // ... and the votes a device batch admitted are appended to txs / txsMap by a thread of the
+  // pool's own (on the context's host workers) while the next batch is decided; pend_* = admitted,
+  // not appended yet.  Every reader / writer of txs drains it first (drain_appends); Size and
+  // TxsBytes count the pending votes.  amu guards jobs, pend_*, txs.len and txs_bytes updates
+  // made by the appender.
+  struct Append { std::vector<Key> keys; std::vector<uint32_t> sizes; uint32_t n = 0; uint64_t bytes = 0; txv_ctx* ctx = nullptr; };
+  std::mutex amu;
+  std::condition_variable acv;
+  std::deque<Append> jobs, spare;
+  bool a_stop = false, a_busy = false;
+  int64_t pend_len = 0, pend_bytes = 0;
+  std::thread appender;
+  ~txv_pool();
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
     if (!cache_on) return true;
@@ -866,6 +880,16 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
 
 }  // namespace
 
+txv_pool::~txv_pool() {
+  {
+    std::lock_guard<std::mutex> lk(amu);
+    a_stop = true;
+    acv.notify_all();
+  }
+  if (appender.joinable()) appender.join();              // the queued appends finish first
+  pooldev_free(dev);
+}
+
 extern "C" {
 
 int txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out) {
@@ -883,6 +907,7 @@ int txv_pool_new(const txv_pool_config* cfg, int64_t height, txv_pool** out) {
   p->height = height;
   if (p->cache_on) p->cache_map.reserve(std::min<uint32_t>(p->cfg.cache_size, 1u << 22));
   p->txs_map.reserve(std::min<uint32_t>(p->cfg.size, 1u << 22));
+  p->txs.nodes.reserve(std::min<uint32_t>(p->cfg.size, 1u << 22));   // no reallocation while the pool fills
   *out = p;
   return TXV_OK;
 }
@@ -897,8 +922,10 @@ namespace {
 // (p->sizes) are known: the order-dependent part (caps, cache, pool list).  p->mu is held.
 int cache_to_host(txv_pool* p, txv_ctx* ctx);
 void host_cache_written(txv_pool* p);
+void drain_appends(txv_pool* p);
 
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
+  drain_appends(p);
   if (int r = cache_to_host(p, ctx)) return r;
   host_cache_written(p);
   const auto t1 = std::chrono::steady_clock::now();
@@ -995,95 +1022,152 @@ int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
   return TXV_OK;
 }
 
-// addTx for the votes a device batch admitted (status TXV_POOL_OK): txs.PushBack in arrival order,
-// txsMap.Store (a key admitted twice keeps its later node, as the sequential Store does), txsBytes
-void apply_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, const uint8_t* st, uint32_t n) {
+// addTx for A admitted votes in arrival order (keys / sizes compacted): txs.PushBack, txsMap.Store
+// (a key admitted twice keeps its later node, as the sequential Store does).  txs.len and
+// txs_bytes are the caller's to update.
+void append_list(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, uint32_t A) {
+  if (!A) return;
+  next_indices(p->txs, A, p->idx_t);
+  p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
+  std::vector<uint8_t>& apart = p->part;                   // rank -> index partition
+  apart.resize(A);
+  const int32_t old_tail = p->txs.tail;
+  pool_parallel_for(p, ctx, A, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t a = lo; a < hi; ++a) {
+      p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[a], sizes[a], a ? p->idx_t[a - 1] : old_tail,
+                                                a + 1 < A ? p->idx_t[a + 1] : -1};
+      apart[a] = (uint8_t)PartIndex::part(keys[a]);
+    }
+  }, 4096);
+  if (old_tail >= 0) p->txs.nodes[old_tail].next = p->idx_t[0]; else p->txs.head = p->idx_t[0];
+  p->txs.tail = p->idx_t[A - 1];
+  const size_t nf = p->txs.free_.size();
+  p->txs.free_.resize(nf - std::min<size_t>(nf, A));
+  pool_parallel_for(p, ctx, kParts, [&](uint32_t q0, uint32_t q1) {
+    std::vector<uint32_t> mine;                            // this partition's ranks, in order
+    mine.reserve(A / kParts + A / (2 * kParts) + 16);
+    for (uint32_t q = q0; q < q1; ++q) {
+      FlatIndex& f = *p->txs_map.p[q];
+      mine.clear();
+      for (uint32_t a = 0; a < A; ++a)
+        if (apart[a] == q) mine.push_back(a);
+      const size_t m = mine.size();
+      for (size_t j = 0; j < m; ++j) {                     // DRAM-latency bound: slots prefetched ahead
+        if (j + kAdmitAhead < m) f.prefetch(keys[mine[j + kAdmitAhead]]);
+        f.put(keys[mine[j]], p->idx_t[mine[j]]);
+      }
+    }
+  }, 1);
+}
+
+void appender_loop(txv_pool* p) {
+  std::unique_lock<std::mutex> lk(p->amu);
+  for (;;) {
+    p->acv.wait(lk, [&] { return p->a_stop || !p->jobs.empty(); });
+    if (p->jobs.empty()) return;                           // stopping, nothing left
+    txv_pool::Append j = std::move(p->jobs.front());
+    p->jobs.pop_front();
+    p->a_busy = true;
+    lk.unlock();
+    append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
+    lk.lock();
+    p->txs.len += j.n;
+    p->txs_bytes += (int64_t)j.bytes;
+    p->pend_len -= j.n;
+    p->pend_bytes -= (int64_t)j.bytes;
+    p->a_busy = false;
+    p->spare.push_back(std::move(j));                      // its buffers serve a later batch
+    p->acv.notify_all();
+  }
+}
+
+// every queued append done (the appender idle): txs / txsMap / txs_bytes are the host's to use
+void drain_appends(txv_pool* p) {
+  std::unique_lock<std::mutex> lk(p->amu);
+  p->acv.wait(lk, [&] { return p->jobs.empty() && !p->a_busy; });
+}
+
+// the votes of a device batch with status TXV_POOL_OK, compacted in arrival order, queued for the
+// appender (Size / TxsBytes count them at once)
+void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, const uint8_t* st, uint32_t n) {
+  txv_pool::Append j;
+  {
+    std::lock_guard<std::mutex> lk(p->amu);
+    if (!p->spare.empty()) { j = std::move(p->spare.front()); p->spare.pop_front(); }
+  }
   const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
-  std::vector<uint64_t> cnt_c(P, 0), bytes_c(P, 0), base_c(P, 0);
+  std::vector<uint32_t> cnt_c(P, 0), base_c(P, 0);
+  std::vector<uint64_t> bytes_c(P, 0);
   auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
   };
   pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
     for (uint32_t c = c0; c < c1; ++c) {
-      uint32_t lo, hi;
+      uint32_t lo, hi, k = 0;
+      uint64_t b = 0;
       chunk(c, lo, hi);
-      uint64_t k = 0, b = 0;
       for (uint32_t i = lo; i < hi; ++i)
         if (st[i] == TXV_POOL_OK) { ++k; b += sizes[i]; }
       cnt_c[c] = k;
       bytes_c[c] = b;
     }
   }, 1);
-  uint64_t A = 0, bytes = 0;
+  uint32_t A = 0;
+  uint64_t bytes = 0;
   for (uint32_t c = 0; c < P; ++c) { base_c[c] = A; A += cnt_c[c]; bytes += bytes_c[c]; }
   if (!A) return;
-  next_indices(p->txs, (uint32_t)A, p->idx_t);
-  p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
-  std::vector<uint32_t>& adm = p->bs.order;                // admitted rank -> arrival index
-  adm.resize(A);
-  const int32_t old_tail = p->txs.tail;
+  if (j.keys.size() < A) { j.keys.resize(A); j.sizes.resize(A); }
   pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
     for (uint32_t c = c0; c < c1; ++c) {
-      uint32_t lo, hi;
+      uint32_t lo, hi, a = base_c[c];
       chunk(c, lo, hi);
-      uint32_t a = (uint32_t)base_c[c];
-      for (uint32_t i = lo; i < hi; ++i) {
-        if (st[i] != TXV_POOL_OK) continue;
-        p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[i], sizes[i], a ? p->idx_t[a - 1] : old_tail,
-                                                  a + 1 < A ? p->idx_t[a + 1] : -1};
-        adm[a++] = i;
-      }
+      for (uint32_t i = lo; i < hi; ++i)
+        if (st[i] == TXV_POOL_OK) { j.keys[a] = keys[i]; j.sizes[a] = sizes[i]; ++a; }
     }
   }, 1);
-  if (old_tail >= 0) p->txs.nodes[old_tail].next = p->idx_t[0]; else p->txs.head = p->idx_t[0];
-  p->txs.tail = p->idx_t[A - 1];
-  p->txs.len += A;
-  const size_t nf = p->txs.free_.size();
-  p->txs.free_.resize(nf - std::min<size_t>(nf, A));
-  pool_parallel_for(p, ctx, kParts, [&](uint32_t q0, uint32_t q1) {
-    for (uint32_t q = q0; q < q1; ++q) {
-      FlatIndex& f = *p->txs_map.p[q];
-      for (uint64_t a = 0; a < A; ++a) {
-        const Key& k = keys[adm[a]];
-        if (PartIndex::part(k) == q) f.put(k, p->idx_t[a]);
-      }
-    }
-  }, 1);
-  p->txs_bytes += (int64_t)bytes;
+  j.n = A;
+  j.bytes = bytes;
+  j.ctx = ctx;
+  std::lock_guard<std::mutex> lk(p->amu);
+  if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
+  p->pend_len += A;
+  p->pend_bytes += (int64_t)bytes;
+  p->jobs.push_back(std::move(j));
+  p->acv.notify_all();
 }
 
 // a device batch needs the pool's Size and MaxTxsBytes caps not to bind inside it (pushes: the
 // votes that reach cache.Push, bytes: the Size() sum of the checked votes)
-bool dev_caps_ok(const txv_pool* p, uint64_t pushes, uint64_t bytes) {
-  return (int64_t)p->txs.len + (int64_t)pushes < (int64_t)p->cfg.size &&
-         p->txs_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
+bool dev_caps_ok(txv_pool* p, uint64_t pushes, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(p->amu);
+  return (int64_t)p->txs.len + p->pend_len + (int64_t)pushes < (int64_t)p->cfg.size &&
+         p->txs_bytes + p->pend_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
 }
 
 }  // namespace
 
 // CheckTxWithInfo for n decoded messages whose keys, sizes and decode statuses are in HBM (the
-// wire ingest, runtime.cpp): decided on the device when the pool keeps its cache there and the
-// caps cannot bind (*done = true; statuses for every message, TXV_POOL_NOT_CHECKED for those that
-// did not decode), else *done = false and the caller runs the host path.  h_keys / h_sizes /
-// h_valid: the same on the host.  Takes p->mu.
+// wire ingest, runtime.cpp), enqueued on the context's key stream behind their decode: decided on
+// the device when the pool keeps its cache there and the caps cannot bind even if all n pushed
+// and their sizes summed to bytes_bound (*done = true; statuses for every message,
+// TXV_POOL_NOT_CHECKED for those that did not decode; h_keys / h_sizes, the decode's copies back,
+// are read once the statuses are in), else *done = false and the caller runs the host path.
+// Takes p->mu.
 int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
-                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, const uint8_t* h_valid,
-                       uint8_t valid_ok, uint32_t n, uint8_t* status_out, bool* done) {
+                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, uint8_t valid_ok,
+                       uint32_t n, uint64_t bytes_bound, void* after, uint8_t* status_out, bool* done) {
   *done = false;
   std::lock_guard<std::mutex> g(p->mu);
   if (!dev_mode(p) || !n) return TXV_OK;
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
-  uint64_t pushes = 0, bytes = 0;
-  for (uint32_t i = 0; i < n; ++i)
-    if (h_valid[i] == valid_ok) { pushes += (int64_t)h_sizes[i] <= max_tx; bytes += h_sizes[i]; }
-  if (!dev_caps_ok(p, pushes, bytes)) return TXV_OK;
+  if (!dev_caps_ok(p, n, bytes_bound)) return TXV_OK;
   int r;
   if ((r = cache_to_dev(p, ctx, n))) return r;
   if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
-                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out)))
+                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after)))
     return r;
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-  apply_admitted(p, ctx, reinterpret_cast<const Key*>(h_keys), h_sizes, status_out, n);
+  queue_admitted(p, ctx, reinterpret_cast<const Key*>(h_keys), h_sizes, status_out, n);
   *done = true;
   return TXV_OK;
 }
@@ -1111,10 +1195,10 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
       int r;
       if ((r = cache_to_dev(p, ctx, n))) return r;
       if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out)))
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr)))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      apply_admitted(p, ctx, reinterpret_cast<const Key*>(keys32), sizes, status_out, n);
+      queue_admitted(p, ctx, reinterpret_cast<const Key*>(keys32), sizes, status_out, n);
       return TXV_OK;
     }
   }
@@ -1150,16 +1234,23 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     });
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
+      const auto t1 = std::chrono::steady_clock::now();
       p->keys.resize((size_t)v->n * 32 + 32);
       if ((r = cache_to_dev(p, ctx, v->n))) return r;
       if ((r = pooldev_check(ctx, p->dev, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, p->keys.data(), status_out)))
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, p->keys.data(), status_out, nullptr)))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      apply_admitted(p, ctx, reinterpret_cast<const Key*>(p->keys.data()), p->sizes.data(), status_out, v->n);
-      if (getenv("TXV_PROFILE_HOST"))
-        fprintf(stderr, "[txv pool] device check=%.3fms n=%u\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
+      const auto t2 = std::chrono::steady_clock::now();
+      queue_admitted(p, ctx, reinterpret_cast<const Key*>(p->keys.data()), p->sizes.data(), status_out, v->n);
+      if (getenv("TXV_PROFILE_HOST")) {
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+          return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "[txv pool] device check=%.3fms (sizes %.3f, device %.3f, apply %.3f) n=%u\n",
+                ms(t0, std::chrono::steady_clock::now()), ms(t0, t1), ms(t1, t2), ms(t2, std::chrono::steady_clock::now()),
+                v->n);
+      }
       return TXV_OK;
     }
   }
@@ -1198,6 +1289,7 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
   p->height = height;
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
+  drain_appends(p);
   if ((r = cache_to_host(p, ctx))) return r;
   host_cache_written(p);
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
@@ -1222,6 +1314,7 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
 int txv_pool_reap(txv_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap, uint64_t* n_out) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  drain_appends(p);
   if (max < 0) max = (int64_t)p->txs.len;
   uint64_t n = 0;
   for (int32_t e = p->txs.head; e >= 0 && (int64_t)n <= max; e = p->txs.nodes[e].next, ++n) {
@@ -1325,6 +1418,7 @@ int txv_encode_msgs(const txv_votes* v, const uint8_t* txkey, const uint8_t* sig
 int txv_pool_flush(txv_pool* p) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  drain_appends(p);
   p->cache.clear(); p->cache_map.clear();
   host_cache_written(p);
   p->txs.clear(); p->txs_map.clear();
@@ -1332,8 +1426,23 @@ int txv_pool_flush(txv_pool* p) {
   return TXV_OK;
 }
 
-int64_t txv_pool_size(txv_pool* p) { return p ? (int64_t)p->txs.len : 0; }
-int64_t txv_pool_txs_bytes(txv_pool* p) { return p ? p->txs_bytes : 0; }
+int txv_pool_sync(txv_pool* p) {
+  if (!p) return TXV_EINVAL;
+  drain_appends(p);
+  return TXV_OK;
+}
+
+// Size / TxsBytes count the votes a device batch admitted whose append is still queued
+int64_t txv_pool_size(txv_pool* p) {
+  if (!p) return 0;
+  std::lock_guard<std::mutex> lk(p->amu);
+  return (int64_t)p->txs.len + p->pend_len;
+}
+int64_t txv_pool_txs_bytes(txv_pool* p) {
+  if (!p) return 0;
+  std::lock_guard<std::mutex> lk(p->amu);
+  return p->txs_bytes + p->pend_bytes;
+}
 int64_t txv_pool_height(txv_pool* p) { return p ? p->height : 0; }
 
 int txv_pool_cache_keys(txv_pool* p, uint8_t* keys_out, uint64_t cap, uint64_t* n_out) {

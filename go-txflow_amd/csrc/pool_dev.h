@@ -33,15 +33,14 @@ struct PoolDevArgs {
   uint32_t* hidx;             // 0..n-1
   uint32_t* skey;             // sorted
   uint32_t* sidx;
-  int32_t* prev;              // the previous push of the same key in the batch, or -1
-  int32_t* crank;             // a first push whose key is cached: its cache position, else -1
   uint32_t* last;             // 1 = the last push of its key in the batch
   uint32_t* lpos;             // exclusive scan of last
   uint8_t* dec;               // 0 not pushed, 1 miss, 2 hit, 3 far (decided by the nested-pair count)
   uint64_t* pst;              // pair (previous occurrence, this push) in doubled S positions, when evicting
   uint64_t* pend;
   uint32_t* far;              // [n] far pushes
-  uint32_t* nfar;             // [1]
+  uint32_t* nfar;             // [2] far pushes, pairs
+  uint64_t* plist;            // [n][2] the pairs (previous occurrence, push), any order
   uint8_t* detached;          // [C] cached keys pushed again in this batch (cleared at the end)
   uint32_t* surv;             // [C] old entries not pushed again
   uint32_t* spos;             // [C] exclusive scan of surv

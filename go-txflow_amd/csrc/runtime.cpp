@@ -241,6 +241,7 @@ struct txv_ctx {
     int phase = 0;                 // 0 free, 1 decoded (keys in flight), 2 admitted (TxFlow chain enqueued)
     txv_pool* pool = nullptr;      // the pool the batch is checked against
     uint32_t n = 0, n_adm = 0;     // messages of the batch; votes the pool admitted (h_list)
+    uint64_t wire_bytes = 0;       // bounds the decoded votes' summed TxVote.Size()
     int flow_err = 0;              // the admitted votes' AddVote chain could not be enqueued
     std::string flow_msg;
   } ing[kIngestRing];
@@ -2467,8 +2468,8 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
 
 uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
 int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
-                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, const uint8_t* h_valid,
-                       uint8_t valid_ok, uint32_t n, uint8_t* status_out, bool* done);   // pool.cpp
+                       const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, uint8_t valid_ok,
+                       uint32_t n, uint64_t bytes_bound, void* after, uint8_t* status_out, bool* done);   // pool.cpp
 
 namespace {
 
@@ -2545,7 +2546,7 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
   Slot& s = c->slots[kIngestSlot + j];
   int r;
   if ((r = ingest_alloc(c, g, s, wire_bytes, n))) return r;
-  g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear(); g.pool = p;
+  g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear(); g.pool = p; g.wire_bytes = wire_bytes;
   const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
   if (n) {
     if (!wire_reg) {
@@ -2621,28 +2622,33 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
     if (t != c->ing_admit_next) { c->err = "ingest tickets must be admitted in decode order"; return TXV_ESTATE; }
   }
   const uint32_t n = g.n;
-  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
-  ht.mark("keys_wait");
-  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it).  When
-  // every message decoded (the usual case) the pinned keys / sizes are the pool's input as they
-  // are; otherwise the decoded ones are compacted first.
-  if (wire_status && n) memcpy(wire_status, g.h_status, n);
   // TXV_POOL_DEVICE_CACHE: CheckTx for every decoded message decided on the device, from the keys,
-  // sizes and decode statuses the decode left in HBM (txv_pool_check_dev; not done when the pool's
-  // caps could bind -- then the host path below)
+  // sizes and decode statuses the decode left in HBM, enqueued behind the decode on the key stream
+  // (txv_pool_check_dev waits for its statuses, and so for the decode's copies back too); not done
+  // when the pool's caps could bind with n votes of up to wire_bytes in all -- then the host path
   uint32_t n_adm = 0;
   bool dev_done = false;
+  std::unique_ptr<uint8_t[]> dst;
   if (n) {
-    std::unique_ptr<uint8_t[]> dst(new uint8_t[n]);
+    dst.reset(new uint8_t[n]);
     const int rd = txv_pool_check_dev(g.pool, c, g.d_keys, g.d_sizes, g.d_status, reinterpret_cast<const uint8_t*>(g.h_keys),
-                                      g.h_sizes, g.h_status, TXV_WIRE_OK, n, dst.get(), &dev_done);
+                                      g.h_sizes, TXV_WIRE_OK, n, g.wire_bytes, (void*)g.kev, dst.get(), &dev_done);
     if (rd) {   // the pool is unchanged: the ticket ends here (no wait)
+      (void)hipEventSynchronize(g.kev);
       std::lock_guard<std::mutex> lk(c->mu);
       g.phase = 0;
       g.ticket = 0;
       c->ing_admit_next = t + 1;
       return rd;
     }
+  }
+  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
+  ht.mark("keys_wait");
+  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it).  When
+  // every message decoded (the usual case) the pinned keys / sizes are the pool's input as they
+  // are; otherwise the decoded ones are compacted first.
+  if (wire_status && n) memcpy(wire_status, g.h_status, n);
+  if (n) {
     if (dev_done) {
       if (pool_status) memcpy(pool_status, dst.get(), n);
       for (uint32_t i = 0; i < n; ++i) {
@@ -2873,10 +2879,9 @@ struct PoolDev {
   uint32_t* ci[2] = {nullptr, nullptr};
   uint32_t* clen = nullptr;                        // [2]: length, staged new length
   uint32_t *push = nullptr, *aidx = nullptr, *hkey = nullptr, *hidx = nullptr, *skey = nullptr, *sidx = nullptr;
-  int32_t *prev = nullptr, *crank = nullptr;
   uint32_t *last = nullptr, *lpos = nullptr, *far = nullptr, *nfar = nullptr, *surv = nullptr, *spos = nullptr;
   uint8_t *dec = nullptr, *detached = nullptr, *d_status = nullptr;
-  uint64_t *pst = nullptr, *pend = nullptr;
+  uint64_t *pst = nullptr, *pend = nullptr, *plist = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   // the SoA path's inputs and outputs
@@ -2889,9 +2894,9 @@ struct PoolDev {
     if (device < 0) return;
     (void)hipSetDevice(device);
     for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
-    dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx); dfree(prev);
-    dfree(crank); dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
-    dfree(detached); dfree(d_status); dfree(pst); dfree(pend); dfree(d_sig); dfree(d_len); dfree(d_keys); dfree(d_sizes);
+    dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx);
+    dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
+    dfree(detached); dfree(d_status); dfree(pst); dfree(pend); dfree(plist); dfree(d_sig); dfree(d_len); dfree(d_keys); dfree(d_sizes);
     if (tmp) (void)hipFree(tmp);
     hfree(h_sig); hfree(h_len); hfree(h_keys); hfree(h_sizes); hfree(h_clen); hfree(h_status);
     if (ev) (void)hipEventDestroy(ev);
@@ -2921,22 +2926,28 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     const size_t cw = (size_t)std::max<uint32_t>(C, 1);
     if ((r = dalloc(c, &s->ck[0], cw * 8)) || (r = dalloc(c, &s->ck[1], cw * 8)) || (r = dalloc(c, &s->ci[0], s->icap)) ||
         (r = dalloc(c, &s->ci[1], s->icap)) || (r = dalloc(c, &s->clen, 2)) || (r = dalloc(c, &s->detached, cw)) ||
-        (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 1)) ||
+        (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 2)) ||
         (r = halloc(c, &s->h_clen, 2)))
       return r;
     HIP_TRY(c, hipMemset(s->ci[0], 0, (size_t)s->icap * 4));
     HIP_TRY(c, hipMemset(s->clen, 0, 8));
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
     HIP_TRY(c, hipEventCreateWithFlags(&s->ev, hipEventDisableTiming));
+    // the engine's own stream, at the highest priority: a batch's short kernels go ahead of the
+    // TxFlow chains' work queued on the context's streams whenever a CU frees up
+    int lo = 0, hi = 0;
+    HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(c, hipStreamCreateWithPriority(&s->st, hipStreamNonBlocking, hi));
   }
   if (n > s->cap_n) {
     int r;
     const uint32_t m = std::max<uint32_t>(n, 1024);
     if ((r = dalloc(c, &s->push, m)) || (r = dalloc(c, &s->aidx, m)) || (r = dalloc(c, &s->hkey, m)) ||
         (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
-        (r = dalloc(c, &s->prev, m)) || (r = dalloc(c, &s->crank, m)) || (r = dalloc(c, &s->last, m)) ||
+        (r = dalloc(c, &s->last, m)) ||
         (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
         (r = dalloc(c, &s->d_status, m)) || (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
+        (r = dalloc(c, &s->plist, (size_t)m * 2)) ||
         (r = dalloc(c, &s->d_sig, (size_t)m * 16)) || (r = dalloc(c, &s->d_len, m)) || (r = dalloc(c, &s->d_keys, (size_t)m * 8)) ||
         (r = dalloc(c, &s->d_sizes, m)) || (r = halloc(c, &s->h_sig, (size_t)m * 16)) || (r = halloc(c, &s->h_len, m)) ||
         (r = halloc(c, &s->h_keys, (size_t)m * 8)) || (r = halloc(c, &s->h_sizes, m)) || (r = halloc(c, &s->h_status, m)))
@@ -3000,11 +3011,13 @@ int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
 // TxVote.Size() on the host (v path).  status_out [n] = TXV_POOL_*.
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out) {
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev) {
+  hipEvent_t after = (hipEvent_t)after_ev;
   HIP_TRY(c, hipSetDevice(c->device));
   if (!n) return TXV_OK;
   if (n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
-  hipStream_t ks = c->key_stream;
+  hipStream_t ks = s->st;
+  if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
   HostTimer ht(c->profile_host);
   if (v) {
     bool reg;
@@ -3044,8 +3057,8 @@ int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_k
   a.ck_old = s->ck[s->cur]; a.ck_new = s->ck[s->cur ^ 1]; a.ci_old = s->ci[s->cur]; a.ci_new = s->ci[s->cur ^ 1];
   a.icap = s->icap; a.clen = s->clen;
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
-  a.prev = s->prev; a.crank = s->crank; a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
-  a.pend = s->pend; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
+  a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
+  a.pend = s->pend; a.plist = s->plist; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
   a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = s->d_status;
   HIP_TRY(c, txv_pooldev_run(&a, ks));
   HIP_TRY(c, hipMemcpyAsync(s->h_status, s->d_status, n, hipMemcpyDeviceToHost, ks));

@@ -13,6 +13,7 @@ creating a context without a GPU raises: there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -140,6 +141,7 @@ def lib():
             "txv_pool_txs_bytes": ([vp], i64),
             "txv_pool_height": ([vp], i64),
             "txv_pool_cache_keys": ([vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_pool_sync": ([vp], ctypes.c_int),
             "txv_decode_msgs": ([vp, vp, ctypes.c_uint64, vp, vp, u32, u32, ctypes.POINTER(_WireVotes)], ctypes.c_int),
             "txv_decode_stage": ([vp, vp, ctypes.c_uint64, vp, vp, u32], ctypes.c_int),
             "txv_decode_run": ([vp, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
@@ -190,7 +192,7 @@ EXPORTED_SYMBOLS = [
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
-    "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys",
+    "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
@@ -431,6 +433,8 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None):
+            for pool in list(getattr(self, "_pools", ())):   # their queued appends use this context's workers
+                pool.sync()
             lib().txv_destroy(self._h)
             self._h = None
 
@@ -834,6 +838,10 @@ class TxVotePool:
     def __init__(self, ctx: Optional[Context], size: int = 0, cache_size: int = 0, max_txs_bytes: int = 0,
                  max_msg_bytes: int = 0, height: int = 0, wal: bool = False, device_cache: bool = False):
         self.ctx = ctx
+        if ctx is not None:
+            if not hasattr(ctx, "_pools"):
+                ctx._pools = weakref.WeakSet()
+            ctx._pools.add(self)
         cfg = _PoolCfg(size, cache_size, max_txs_bytes, max_msg_bytes,
                        (POOL_WAL if wal else 0) | (POOL_DEVICE_CACHE if device_cache else 0))
         h = ctypes.c_void_p()
@@ -846,6 +854,11 @@ class TxVotePool:
         if getattr(self, "_h", None):
             lib().txv_pool_free(self._h)
             self._h = None
+
+    def sync(self):
+        """txv_pool_sync: the queued appends of device batches done"""
+        if getattr(self, "_h", None):
+            lib().txv_pool_sync(self._h)
 
     def __del__(self):
         self.close()

@@ -410,6 +410,12 @@ int txv_pool_flush(txv_pool* pool);
 int64_t txv_pool_size(txv_pool* pool);
 int64_t txv_pool_txs_bytes(txv_pool* pool);
 int64_t txv_pool_height(txv_pool* pool);
+/* With TXV_POOL_DEVICE_CACHE the votes a device batch admitted are appended to the pool list by a
+ * thread of the pool's own on the checking context's host workers, while the next batch is
+ * decided (Size and TxsBytes count them at once; every call that reads the pool list waits for
+ * it).  txv_pool_sync waits for those appends: call it before txv_destroy of that context when
+ * the pool outlives it (txv_pool_free waits too). */
+int txv_pool_sync(txv_pool* pool);
 /* LRU cache keys front (oldest) to back; *n_out = cache length (test hook: cache_test.go). */
 int txv_pool_cache_keys(txv_pool* pool, uint8_t* keys_out, uint64_t cap, uint64_t* n_out);
 

@@ -89,7 +89,7 @@ class C4Stream:
 
     def __init__(self, ctx, seed: int = 0x7478763034, batch: int = 1 << 20, batches_per_epoch: int = 4,
                  oracle_threads: int = 16, verify_slice: int = 4096, pool_stage: bool = False,
-                 pool_cache: int = 1 << 20):
+                 pool_cache: int = 1 << 20, pool_device: bool = False):
         import oracle as O
         from txflow_amd.workload import validator_seeds
         self.ctx, self.O = ctx, O
@@ -122,9 +122,11 @@ class C4Stream:
         if pool_stage:
             import txflow_amd as T
             big = (1 << 31) - 1
-            self.pool = T.TxVotePool(ctx, size=big, cache_size=pool_cache, max_txs_bytes=1 << 40)
+            self.pool = T.TxVotePool(ctx, size=big, cache_size=pool_cache, max_txs_bytes=1 << 40,
+                                     device_cache=pool_device)
             self.opool = O.Pool(size=big, cache_size=pool_cache, max_txs_bytes=1 << 40)
-            self.stats.update(pool_votes=0, pool_mismatches=0, pool_by_status={}, pool_cache=pool_cache)
+            self.stats.update(pool_votes=0, pool_mismatches=0, pool_by_status={}, pool_cache=pool_cache,
+                              pool_device_cache=pool_device)
 
     # ---------------------------------------------------------------- epoch state
     def _new_epoch(self):
@@ -425,13 +427,13 @@ class C4Stream:
 
 def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int = 4, threads: int = 16,
              log=print, seed: int = 0x7478763034, pipelined: bool = True, pool_stage: bool = False,
-             pool_cache: int = 1 << 20):
+             pool_cache: int = 1 << 20, pool_device: bool = False):
     """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0).
     pipelined: batches go through txv_submit_votes / txv_wait_votes with two in flight (batch
     k+1 verifies on the device while batch k tallies and is checked against the oracle); the
     pipeline drains at each epoch end, before the per-set check reads the device state."""
     s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads,
-                 pool_stage=pool_stage, pool_cache=pool_cache)
+                 pool_stage=pool_stage, pool_cache=pool_cache, pool_device=pool_device)
     t0 = time.time()
 
     def report(r):

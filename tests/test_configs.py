@@ -101,17 +101,18 @@ def test_c4_adversarial_1m_gate(oracle_lib):
         ctx.close()
 
 
-def test_c4_adversarial_with_pool_stage(oracle_lib):
+@pytest.mark.parametrize("pool_device", [False, True], ids=["host-cache", "device-cache"])
+def test_c4_adversarial_with_pool_stage(oracle_lib, pool_device):
     """C4 with the pool in front (Appendix C): every batch through TxVotePool.CheckTx on the device
     and in the oracle (outcomes compared per vote), the admitted votes through the pipelined
     TxFlow; a small LRU (64k keys) so that some replays are ErrTxInCache and others, evicted,
-    reach the tally as DUPLICATE."""
+    reach the tally as DUPLICATE.  device-cache: the LRU in HBM (TXV_POOL_DEVICE_CACHE)."""
     import adversarial as A
     import txflow_amd as T
     ctx = T.Context(max_batch=1 << 18, max_txs=1 << 16, max_validators=256)
     try:
         st = A.run_gate(ctx, 1 << 20, batch=1 << 18, batches_per_epoch=2, threads=_cores(), log=lambda s: None,
-                        pool_stage=True, pool_cache=1 << 16)
+                        pool_stage=True, pool_cache=1 << 16, pool_device=pool_device)
         assert st["mismatches"] == 0 and st["pool_mismatches"] == 0, st
         assert st["pool_by_status"].get("ErrTxInCache", 0) > 0 and st["by_status"].get("DUPLICATE", 0) > 0, st
         assert st["by_status"].get("ErrVoteNonDeterministicSignature", 0) > 0, st

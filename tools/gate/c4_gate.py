@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8))
     ap.add_argument("--no-pool", action="store_true", help="feed txv_add_votes directly (no TxVotePool stage)")
     ap.add_argument("--pool-cache", type=int, default=1 << 20, help="TxVotePool CacheSize (LRU entries)")
+    ap.add_argument("--pool-device", action="store_true", help="the pool's cache in HBM (TXV_POOL_DEVICE_CACHE)")
     args = ap.parse_args()
     import oracle
     oracle.build()
@@ -39,7 +40,7 @@ def main():
     t0 = time.time()
     st = A.run_gate(ctx, args.votes, batch=args.batch, batches_per_epoch=args.batches_per_epoch,
                     threads=args.threads, log=lambda s: print(s, flush=True), pool_stage=not args.no_pool,
-                    pool_cache=args.pool_cache)
+                    pool_cache=args.pool_cache, pool_device=args.pool_device)
     import subprocess
     try:
         head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
