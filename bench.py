@@ -272,9 +272,9 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             def prepare():
                 for k, b in enumerate(wl.batches):
                     ts = time.perf_counter()
-                    if device_cache:                     # the whole CheckTx batch, one call
-                        ps = pool.check_batch(b)
-                        prepared.put((k, ts, time.perf_counter(), None, ps))
+                    if device_cache:                     # CheckTx submitted: decided on the GPU in order
+                        tk = pool.check_submit(b)
+                        prepared.put((k, ts, time.perf_counter(), None, tk))
                     else:
                         keys, sizes = pool.prepare(b)
                         prepared.put((k, ts, time.perf_counter(), keys, sizes))
@@ -287,8 +287,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                         break
                     k, ts, tq, keys, sizes = item
                     tc = time.perf_counter()
-                    if keys is None:                     # decided already (device cache)
-                        ps = sizes
+                    if keys is None:                     # the submitted batch's statuses
+                        ps = pool.check_wait(sizes)
                     else:
                         ps = pool.check_keys(keys, sizes)
                     tp = time.perf_counter()
@@ -347,9 +347,11 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
             bl = (np.array(done) - np.array(submit)) * 1e3
             allst = np.concatenate(pool_st)
-            stages = ("one txv_pool_check call per batch with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE: "
-                      "keys, stack-distance decisions and the new cache on the GPU, the admitted votes appended to "
-                      "the pool list on the host); p50_pool_check_ms = that call" if device_cache else
+            stages = ("two pipelined stages with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE) -- "
+                      "txv_pool_check_submit (Size on the host, keys, stack-distance decisions and the new cache "
+                      "enqueued on the GPU, one thread) and txv_pool_check_wait (the statuses; the admitted votes "
+                      "appended to the pool list by the pool's own thread, another); p50_pool_check_ms = their sum "
+                      "per batch" if device_cache else
                       "two pipelined stages -- txv_pool_prepare (keys on the GPU + Size, one thread) and "
                       "txv_pool_check_keys (LRU + pool on the host, another); p50_pool_check_ms = their sum per batch")
             out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "

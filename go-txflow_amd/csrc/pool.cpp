@@ -248,12 +248,18 @@ struct BatchScratch {
 struct PoolDev;
 void pooldev_free(PoolDev* s);
 bool pooldev_same_device(const txv_ctx* c, const PoolDev* s);
+uint32_t pooldev_cap(const PoolDev* s);
 int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n);
 int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L);
 int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
                   int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after);
+int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
+                    const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
+                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev);
+int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
+constexpr int kPdRing = 3;   // = PoolDev::kPdRing (runtime.cpp)
 
 struct txv_pool {
   txv_pool_config cfg{};
@@ -286,6 +292,23 @@ struct txv_pool {
   bool a_stop = false, a_busy = false;
   int64_t pend_len = 0, pend_bytes = 0;
   std::thread appender;
+  // device batches submitted (txv_pool_check_submit) and not yet waited, in order; a device one
+  // holds flight slot `slot` of the engine until finished (its statuses then kept in st).
+  // infl_*: the pushes / Size() sums of the unfinished ones (upper bounds for the caps check)
+  struct Ticket {
+    uint64_t id = 0;
+    uint32_t n = 0;
+    int slot = -1;
+    bool done = false;
+    txv_ctx* ctx = nullptr;
+    uint64_t pushes = 0, bytes = 0;
+    std::vector<uint8_t> st;
+    int err = 0;
+  };
+  std::deque<Ticket> tickets;
+  uint64_t next_ticket = 1;
+  int next_slot = 0;
+  int64_t infl_len = 0, infl_bytes = 0;
   ~txv_pool();
 
   bool cache_push(const Key& k) {                  // mapTxCache.Push
@@ -924,7 +947,10 @@ int cache_to_host(txv_pool* p, txv_ctx* ctx);
 void host_cache_written(txv_pool* p);
 void drain_appends(txv_pool* p);
 
+int drain_flights(txv_pool* p);
+
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
+  if (int r = drain_flights(p)) return r;
   drain_appends(p);
   if (int r = cache_to_host(p, ctx)) return r;
   host_cache_written(p);
@@ -1008,7 +1034,11 @@ void host_cache_written(txv_pool* p) {
 }
 
 int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
-  if (p->dev && !pooldev_same_device(ctx, p->dev))   // moving to another GPU: the current list first
+  // a rebind (another GPU, or a batch above the engine's capacity) frees the flight slots: every
+  // submitted batch finished first; moving to another GPU takes the current list along
+  if (p->dev && (!pooldev_same_device(ctx, p->dev) || n > pooldev_cap(p->dev)))
+    if (int r = drain_flights(p)) return r;
+  if (p->dev && !pooldev_same_device(ctx, p->dev))
     if (int r = cache_to_host(p, ctx)) return r;
   PoolDev* before = p->dev;
   if (int r = pooldev_bind(ctx, &p->dev, p->cache_on ? p->cfg.cache_size : 0u, n)) return r;
@@ -1140,8 +1170,33 @@ void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
 // votes that reach cache.Push, bytes: the Size() sum of the checked votes)
 bool dev_caps_ok(txv_pool* p, uint64_t pushes, uint64_t bytes) {
   std::lock_guard<std::mutex> lk(p->amu);
-  return (int64_t)p->txs.len + p->pend_len + (int64_t)pushes < (int64_t)p->cfg.size &&
-         p->txs_bytes + p->pend_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
+  return (int64_t)p->txs.len + p->pend_len + p->infl_len + (int64_t)pushes < (int64_t)p->cfg.size &&
+         p->txs_bytes + p->pend_bytes + p->infl_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
+}
+
+// a submitted device batch's statuses in (its decisions were made in submission order on the
+// engine's stream), its admitted votes queued for the appender, its flight slot free
+int finish_ticket(txv_pool* p, txv_pool::Ticket& t) {
+  if (t.done) return t.err;
+  const uint8_t* st;
+  const uint8_t* kp;
+  const uint32_t* sz;
+  t.done = true;
+  p->infl_len -= (int64_t)t.pushes;
+  p->infl_bytes -= (int64_t)t.bytes;
+  if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
+  t.st.assign(st, st + t.n);
+  queue_admitted(p, t.ctx, reinterpret_cast<const Key*>(kp), sz, st, t.n);
+  return TXV_OK;
+}
+
+// every submitted device batch finished (statuses kept for their waits): the device and host
+// copies can be synchronised, the pool list read
+int drain_flights(txv_pool* p) {
+  int r = TXV_OK;
+  for (auto& t : p->tickets)
+    if (!t.done) { const int e = finish_ticket(p, t); if (e && !r) r = e; }
+  return r;
 }
 
 }  // namespace
@@ -1162,6 +1217,7 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
   if (!dev_caps_ok(p, n, bytes_bound)) return TXV_OK;
   int r;
+  if ((r = drain_flights(p))) return r;
   if ((r = cache_to_dev(p, ctx, n))) return r;
   if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
                          (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after)))
@@ -1193,6 +1249,7 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
     for (uint32_t i = 0; i < n; ++i) { pushes += (int64_t)sizes[i] <= max_tx; bytes += sizes[i]; }
     if (dev_caps_ok(p, pushes, bytes)) {
       int r;
+      if ((r = drain_flights(p))) return r;
       if ((r = cache_to_dev(p, ctx, n))) return r;
       if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
                              (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr)))
@@ -1206,15 +1263,25 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
   return pool_admit(p, ctx, reinterpret_cast<const Key*>(keys32), n, status_out);
 }
 
-int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
-                   const uint64_t* sig_full_off, uint8_t* status_out) {
-  if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
+// CheckTxWithInfo for a batch, submitted: with TXV_POOL_DEVICE_CACHE (and no long signature,
+// caps that cannot bind, a free flight slot) the keys, decisions and new cache are enqueued on
+// the engine's stream and the call returns; otherwise the batch is checked on the host here (any
+// device batches still in flight are finished first).  Either way the batch is CheckTx'd in
+// submission order, and txv_pool_check_wait returns its statuses.
+int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
+                          const uint64_t* sig_full_off, uint64_t* ticket) {
+  if (!p || !ctx || !v || !ticket) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  *ticket = 0;
   const auto t0 = std::chrono::steady_clock::now();
+  txv_pool::Ticket t;
+  t.id = p->next_ticket;
+  t.n = v->n;
+  t.ctx = ctx;
   p->sizes.resize(v->n);
   if (dev_mode(p) && v->n) {
     // the device path: Size() on the host workers (with the pushes, the bytes and any long
-    // signature), then keys, decisions and the new cache in one round trip to the GPU
+    // signature), then keys, decisions and the new cache enqueued on the GPU
     const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
     std::atomic<uint64_t> pushes{0}, bytes{0};
     std::atomic<bool> long_sig{false};
@@ -1234,27 +1301,29 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
     });
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
-      const auto t1 = std::chrono::steady_clock::now();
-      p->keys.resize((size_t)v->n * 32 + 32);
+      const int slot = p->next_slot;
+      for (auto& o : p->tickets)                           // the slot's previous batch, finished
+        if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
       if ((r = cache_to_dev(p, ctx, v->n))) return r;
-      if ((r = pooldev_check(ctx, p->dev, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, p->keys.data(), status_out, nullptr)))
+      if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
+                               (p->cfg.flags & TXV_POOL_WAL) != 0, true, nullptr)))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      const auto t2 = std::chrono::steady_clock::now();
-      queue_admitted(p, ctx, reinterpret_cast<const Key*>(p->keys.data()), p->sizes.data(), status_out, v->n);
-      if (getenv("TXV_PROFILE_HOST")) {
-        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-          return std::chrono::duration<double, std::milli>(b - a).count();
-        };
-        fprintf(stderr, "[txv pool] device check=%.3fms (sizes %.3f, device %.3f, apply %.3f) n=%u\n",
-                ms(t0, std::chrono::steady_clock::now()), ms(t0, t1), ms(t1, t2), ms(t2, std::chrono::steady_clock::now()),
-                v->n);
-      }
+      p->next_slot = (slot + 1) % kPdRing;
+      t.slot = slot;
+      t.pushes = pushes.load();
+      t.bytes = bytes.load();
+      p->infl_len += (int64_t)t.pushes;
+      p->infl_bytes += (int64_t)t.bytes;
+      p->tickets.push_back(std::move(t));
+      *ticket = p->next_ticket++;
+      if (getenv("TXV_PROFILE_HOST"))
+        fprintf(stderr, "[txv pool] device submit=%.3fms n=%u\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
       return TXV_OK;
     }
   }
-  // TxVote.Size() of every vote on the worker threads (order-independent) while the GPU hashes
+  // the host path: TxVote.Size() of every vote on the worker threads while the GPU hashes
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off, [&] {
     txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
       for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
@@ -1265,7 +1334,47 @@ int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t*
   if (getenv("TXV_PROFILE_HOST"))
     fprintf(stderr, "[txv pool] keys+sizes=%.3fms n=%u\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
-  return pool_admit(p, ctx, keys, v->n, status_out);
+  t.st.resize(v->n);
+  if ((r = pool_admit(p, ctx, keys, v->n, t.st.data()))) return r;
+  t.done = true;
+  p->tickets.push_back(std::move(t));
+  *ticket = p->next_ticket++;
+  return TXV_OK;
+}
+
+// the statuses of a submitted batch (tickets in submission order); the engine's event is waited
+// for without p->mu held, so batch k+1 can be submitted meanwhile
+int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
+  if (!p || !ticket) return TXV_EINVAL;
+  txv_ctx* ctx = nullptr;
+  int slot = -1;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = std::find_if(p->tickets.begin(), p->tickets.end(), [&](const txv_pool::Ticket& t) { return t.id == ticket; });
+    if (it == p->tickets.end()) return TXV_ESTATE;
+    if (!it->done) { ctx = it->ctx; slot = it->slot; }
+  }
+  if (slot >= 0) (void)pooldev_finish(ctx, p->dev, slot, nullptr, nullptr, nullptr);   // the wait itself
+  std::lock_guard<std::mutex> g(p->mu);
+  int r = TXV_OK;
+  for (auto it = p->tickets.begin(); it != p->tickets.end(); ++it) {   // the earlier ones first: append order
+    const int e = finish_ticket(p, *it);
+    if (it->id != ticket) continue;
+    r = e;
+    if (!r && it->n && status_out) memcpy(status_out, it->st.data(), it->n);
+    p->tickets.erase(it);
+    return r;
+  }
+  return TXV_ESTATE;
+}
+
+int txv_pool_check(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
+                   const uint64_t* sig_full_off, uint8_t* status_out) {
+  if (!p || !ctx || !v || (v->n && !status_out)) return TXV_EINVAL;
+  uint64_t t = 0;
+  int r = txv_pool_check_submit(p, ctx, v, sig_full, sig_full_off, &t);
+  if (r) return r;
+  return txv_pool_check_wait(p, t, status_out);
 }
 
 // the order-independent half of CheckTxWithInfo for a batch (txvotepool.go:187-261): every vote's
@@ -1289,6 +1398,7 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
   p->height = height;
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
+  if ((r = drain_flights(p))) return r;
   drain_appends(p);
   if ((r = cache_to_host(p, ctx))) return r;
   host_cache_written(p);
@@ -1314,6 +1424,7 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
 int txv_pool_reap(txv_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap, uint64_t* n_out) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  if (int r = drain_flights(p)) return r;
   drain_appends(p);
   if (max < 0) max = (int64_t)p->txs.len;
   uint64_t n = 0;
@@ -1418,6 +1529,7 @@ int txv_encode_msgs(const txv_votes* v, const uint8_t* txkey, const uint8_t* sig
 int txv_pool_flush(txv_pool* p) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  (void)drain_flights(p);
   drain_appends(p);
   p->cache.clear(); p->cache_map.clear();
   host_cache_written(p);
@@ -1448,6 +1560,7 @@ int64_t txv_pool_height(txv_pool* p) { return p ? p->height : 0; }
 int txv_pool_cache_keys(txv_pool* p, uint8_t* keys_out, uint64_t cap, uint64_t* n_out) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
+  if (int r = drain_flights(p)) return r;
   if (int r = cache_to_host(p, nullptr)) return r;
   uint64_t n = 0;
   for (int32_t e = p->cache.head; e >= 0; e = p->cache.nodes[e].next, ++n)

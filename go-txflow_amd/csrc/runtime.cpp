@@ -2884,10 +2884,16 @@ struct PoolDev {
   uint64_t *pst = nullptr, *pend = nullptr, *plist = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  // the SoA path's inputs and outputs
-  uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
-  uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr, *h_clen = nullptr;
-  uint8_t* h_status = nullptr;
+  // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
+  static constexpr int kPdRing = 3;
+  struct Flight {
+    uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
+    uint8_t* d_status = nullptr;
+    uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr;
+    uint8_t* h_status = nullptr;
+    hipEvent_t ev = nullptr;
+  } fl[kPdRing];
+  uint32_t* h_clen = nullptr;
   hipEvent_t ev = nullptr;
   hipStream_t st = nullptr;                        // cache uploads / downloads
   ~PoolDev() {
@@ -2896,9 +2902,14 @@ struct PoolDev {
     for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
     dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx);
     dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
-    dfree(detached); dfree(d_status); dfree(pst); dfree(pend); dfree(plist); dfree(d_sig); dfree(d_len); dfree(d_keys); dfree(d_sizes);
+    dfree(detached); dfree(pst); dfree(pend); dfree(plist);
+    for (Flight& f : fl) {
+      dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
+      hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status);
+      if (f.ev) (void)hipEventDestroy(f.ev);
+    }
     if (tmp) (void)hipFree(tmp);
-    hfree(h_sig); hfree(h_len); hfree(h_keys); hfree(h_sizes); hfree(h_clen); hfree(h_status);
+    hfree(h_clen);
     if (ev) (void)hipEventDestroy(ev);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -2906,6 +2917,7 @@ struct PoolDev {
 
 void pooldev_free(PoolDev* s) { delete s; }
 bool pooldev_same_device(const txv_ctx* c, const PoolDev* s) { return c && s && c->device == s->device; }
+uint32_t pooldev_cap(const PoolDev* s) { return s ? s->cap_n : 0; }
 
 // (re)binds the engine to c's device with capacity C and room for n-vote batches; a new cache
 // starts empty (length 0)
@@ -2933,6 +2945,7 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     HIP_TRY(c, hipMemset(s->clen, 0, 8));
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
     HIP_TRY(c, hipEventCreateWithFlags(&s->ev, hipEventDisableTiming));
+    for (PoolDev::Flight& f : s->fl) HIP_TRY(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     // the engine's own stream, at the highest priority: a batch's short kernels go ahead of the
     // TxFlow chains' work queued on the context's streams whenever a CU frees up
     int lo = 0, hi = 0;
@@ -2946,12 +2959,14 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
         (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
         (r = dalloc(c, &s->last, m)) ||
         (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
-        (r = dalloc(c, &s->d_status, m)) || (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
-        (r = dalloc(c, &s->plist, (size_t)m * 2)) ||
-        (r = dalloc(c, &s->d_sig, (size_t)m * 16)) || (r = dalloc(c, &s->d_len, m)) || (r = dalloc(c, &s->d_keys, (size_t)m * 8)) ||
-        (r = dalloc(c, &s->d_sizes, m)) || (r = halloc(c, &s->h_sig, (size_t)m * 16)) || (r = halloc(c, &s->h_len, m)) ||
-        (r = halloc(c, &s->h_keys, (size_t)m * 8)) || (r = halloc(c, &s->h_sizes, m)) || (r = halloc(c, &s->h_status, m)))
+        (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) || (r = dalloc(c, &s->plist, (size_t)m * 2)))
       return r;
+    for (PoolDev::Flight& f : s->fl)
+      if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
+          (r = dalloc(c, &f.d_sizes, m)) || (r = dalloc(c, &f.d_status, m)) || (r = halloc(c, &f.h_sig, (size_t)m * 16)) ||
+          (r = halloc(c, &f.h_len, m)) || (r = halloc(c, &f.h_keys, (size_t)m * 8)) || (r = halloc(c, &f.h_sizes, m)) ||
+          (r = halloc(c, &f.h_status, m)))
+        return r;
     s->cap_n = m;
     const size_t tb = txv_pooldev_tmp_bytes(m, std::max<uint32_t>(C, 1));
     if (tb > s->tmp_bytes) {
@@ -3005,20 +3020,23 @@ int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
 }
 #undef PD_TRY
 
-// one batch decided on the device (synchronous), either from a txv_votes batch (v: signatures
-// uploaded, keyed here; keys_out [n][32] receives the keys) or from keys / sizes / validity already
-// in HBM (d_keys, d_sizes, d_valid == valid_ok for a decoded message).  h_sizes: the votes'
-// TxVote.Size() on the host (v path).  status_out [n] = TXV_POOL_*.
-int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
-                  const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev) {
+// one batch's decisions enqueued on the engine's stream into flight slot `slot` (whose previous
+// batch the caller has finished), either from a txv_votes batch (v: signatures uploaded -- from
+// caller memory registered with txv_host_register, which must stay valid until the finish -- and
+// keyed here; h_sizes = their TxVote.Size()), from keys / sizes given on the host (h_keys_in), or
+// from keys / sizes / validity already in HBM (d_keys, d_sizes, d_valid == valid_ok for a decoded
+// message; `after` = the event that ends their producer).  The statuses, and with keys_back the
+// keys, come back into the slot's pinned buffers (pooldev_finish).
+int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
+                    const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
+                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev) {
   hipEvent_t after = (hipEvent_t)after_ev;
   HIP_TRY(c, hipSetDevice(c->device));
   if (!n) return TXV_OK;
   if (n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
+  PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = s->st;
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
-  HostTimer ht(c->profile_host);
   if (v) {
     bool reg;
     {
@@ -3027,28 +3045,28 @@ int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_k
     }
     if (!reg)
       c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-        memcpy(s->h_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
-        memcpy(s->h_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+        memcpy(f.h_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+        memcpy(f.h_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
       }, 4096);
-    memcpy(s->h_sizes, h_sizes, (size_t)n * 4);
-    HIP_TRY(c, hipMemcpyAsync(s->d_sig, reg ? (const void*)v->sig : (const void*)s->h_sig, (size_t)n * 64,
+    memcpy(f.h_sizes, h_sizes, (size_t)n * 4);
+    HIP_TRY(c, hipMemcpyAsync(f.d_sig, reg ? (const void*)v->sig : (const void*)f.h_sig, (size_t)n * 64,
                               hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(s->d_len, reg ? (const void*)v->sig_len : (const void*)s->h_len, (size_t)n * 4,
+    HIP_TRY(c, hipMemcpyAsync(f.d_len, reg ? (const void*)v->sig_len : (const void*)f.h_len, (size_t)n * 4,
                               hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(s->d_sizes, s->h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, txv_launch_sig_keys(s->d_sig, s->d_len, n, s->d_keys, ks));
-    d_keys = s->d_keys;
-    d_sizes = s->d_sizes;
+    HIP_TRY(c, hipMemcpyAsync(f.d_sizes, f.h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n, f.d_keys, ks));
+    d_keys = f.d_keys;
+    d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (h_keys_in) {   // keys and sizes given on the host (txv_pool_check_keys)
     c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-      memcpy(s->h_keys + (size_t)lo * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
-      memcpy(s->h_sizes + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
+      memcpy(f.h_keys + (size_t)lo * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
+      memcpy(f.h_sizes + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
     }, 8192);
-    HIP_TRY(c, hipMemcpyAsync(s->d_keys, s->h_keys, (size_t)n * 32, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(s->d_sizes, s->h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-    d_keys = s->d_keys;
-    d_sizes = s->d_sizes;
+    HIP_TRY(c, hipMemcpyAsync(f.d_keys, f.h_keys, (size_t)n * 32, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(f.d_sizes, f.h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    d_keys = f.d_keys;
+    d_sizes = f.d_sizes;
     d_valid = nullptr;
   }
   PoolDevArgs a{};
@@ -3059,19 +3077,48 @@ int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_k
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
   a.pend = s->pend; a.plist = s->plist; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
-  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = s->d_status;
+  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status;
   HIP_TRY(c, txv_pooldev_run(&a, ks));
-  HIP_TRY(c, hipMemcpyAsync(s->h_status, s->d_status, n, hipMemcpyDeviceToHost, ks));
-  if (v && keys_out) HIP_TRY(c, hipMemcpyAsync(s->h_keys, s->d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
-  HIP_TRY(c, hipEventRecord(s->ev, ks));
+  if (s->C) s->cur ^= 1;                                  // the next batch on this stream reads the new cache
+  HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status, n, hipMemcpyDeviceToHost, ks));
+  if (keys_back && d_keys == f.d_keys && v)
+    HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
+  HIP_TRY(c, hipEventRecord(f.ev, ks));
+  return TXV_OK;
+}
+
+// waits for slot's batch; its statuses, keys ([n][32]: the v and h_keys_in paths) and sizes (same)
+// in pinned memory, valid until the slot is enqueued again
+int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys,
+                   const uint32_t** sizes) {
+  PoolDev::Flight& f = s->fl[slot];
+  if (c) HIP_TRY(c, hipEventSynchronize(f.ev));
+  else if (hipEventSynchronize(f.ev) != hipSuccess) return TXV_EDEVICE;
+  if (status) *status = f.h_status;
+  if (keys) *keys = reinterpret_cast<const uint8_t*>(f.h_keys);
+  if (sizes) *sizes = f.h_sizes;
+  return TXV_OK;
+}
+
+// enqueue + finish in one call (synchronous): statuses into status_out, keys (v path) into keys_out
+int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
+                  const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev) {
+  if (!n) return TXV_OK;
+  HostTimer ht(c->profile_host);
+  const int slot = 0;
+  int r = pooldev_enqueue(c, s, slot, v, h_keys_in, h_sizes, d_keys, d_sizes, d_valid, valid_ok, n, max_tx, wal,
+                          keys_out != nullptr, after_ev);
+  if (r) return r;
   ht.mark("enqueue");
-  HIP_TRY(c, hipEventSynchronize(s->ev));
+  const uint8_t* st;
+  const uint8_t* kp;
+  if ((r = pooldev_finish(c, s, slot, &st, &kp, nullptr))) return r;
   ht.mark("device");
-  if (s->C) s->cur ^= 1;
-  memcpy(status_out, s->h_status, n);
+  memcpy(status_out, st, n);
   if (v && keys_out)
     c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-      memcpy(keys_out + (size_t)lo * 32, s->h_keys + (size_t)lo * 8, (size_t)(hi - lo) * 32);
+      memcpy(keys_out + (size_t)lo * 32, kp + (size_t)lo * 32, (size_t)(hi - lo) * 32);
     }, 8192);
   ht.mark("out");
   return TXV_OK;

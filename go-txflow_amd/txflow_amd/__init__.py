@@ -133,6 +133,9 @@ def lib():
             "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
             "txv_pool_free": ([vp], None),
             "txv_pool_check": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
+            "txv_pool_check_submit": ([vp, vp, ctypes.POINTER(_Votes), vp, vp, ctypes.POINTER(ctypes.c_uint64)],
+                                      ctypes.c_int),
+            "txv_pool_check_wait": ([vp, ctypes.c_uint64, vp], ctypes.c_int),
             "txv_pool_check_keys": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_pool_update": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
             "txv_pool_reap": ([vp, i64, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
@@ -193,6 +196,7 @@ EXPORTED_SYMBOLS = [
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
+    "txv_pool_check_submit", "txv_pool_check_wait",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
@@ -869,6 +873,31 @@ class TxVotePool:
         vs = batch.c_struct()
         ctx = self._ctx_or_raise("check_batch")
         ctx._chk(lib().txv_pool_check(self._h, ctx._h, ctypes.byref(vs), full, off, out.ctypes.data), "txv_pool_check")
+        return out[:batch.n]
+
+    def check_submit(self, batch: VoteBatch, long_sigs: Optional[dict] = None) -> int:
+        """txv_pool_check_submit: the batch is CheckTx'd in submission order; with the device cache
+        its decisions are enqueued on the GPU and the call returns (check_wait(ticket) gives the
+        statuses).  The batch's columns are kept referenced until the wait."""
+        ctx = self._ctx_or_raise("check_submit")
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        t = ctypes.c_uint64(0)
+        ctx._chk(lib().txv_pool_check_submit(self._h, ctx._h, ctypes.byref(vs), full, off, ctypes.byref(t)),
+                 "txv_pool_check_submit")
+        if not hasattr(self, "_inflight"):
+            self._inflight = {}
+        self._inflight[t.value] = (batch, vs, full, off)
+        return t.value
+
+    def check_wait(self, ticket: int) -> np.ndarray:
+        """txv_pool_check_wait: the statuses of a submitted batch"""
+        batch = self._inflight[ticket][0]
+        out = np.zeros(max(batch.n, 1), np.uint8)
+        rc = lib().txv_pool_check_wait(self._h, ticket, out.ctypes.data)
+        del self._inflight[ticket]
+        if rc != 0:
+            raise TxvInfraError(f"txv_pool_check_wait failed ({rc})")
         return out[:batch.n]
 
     def prepare(self, batch: VoteBatch, long_sigs: Optional[dict] = None):

@@ -383,6 +383,15 @@ void txv_pool_free(txv_pool* pool);
 /* CheckTxWithInfo for each vote in arrival order (keys on ctx's GPU); status_out[i] = TXV_POOL_*. */
 int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
                    const uint64_t* sig_full_off, uint8_t* status_out);
+/* txv_pool_check in two calls: submit (CheckTx'd in submission order; with TXV_POOL_DEVICE_CACHE
+ * the keys, decisions and new cache are enqueued on the GPU and the call returns, so batch k+1
+ * can be submitted while batch k's statuses are awaited; otherwise the batch is checked on the
+ * host within the call) and wait (status_out[i] = TXV_POOL_*, any order).  A device batch's
+ * registered signature columns are DMA'd from caller memory: they must stay valid until its
+ * wait.  txv_pool_check = submit + wait.  txvotepool.go:187-261 */
+int txv_pool_check_submit(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
+                          const uint64_t* sig_full_off, uint64_t* ticket);
+int txv_pool_check_wait(txv_pool* pool, uint64_t ticket, uint8_t* status_out);
 /* CheckTxWithInfo for n votes given as (txVoteKey, TxVote.Size()) pairs in arrival order: keys32
  * n x 32 bytes (SHA-256(Signature), txvotepool.go:467-469), sizes[i] = Size() (0 when amino
  * rejects the timestamp); status_out[i] = TXV_POOL_*.  ctx (optional) lends its host workers;

@@ -114,3 +114,61 @@ def test_device_cache_soa_batches_with_update(dev_ctx):
         assert np.array_equal(pool.cache_keys(), ref.cache_keys())
     finally:
         pool.close()
+
+
+@pytest.mark.gpu
+def test_device_cache_submitted_batches_in_flight(dev_ctx):
+    """txv_pool_check_submit / _wait with up to four batches submitted before the first wait (the
+    engine has three flight slots: the fourth submit finishes the first), waits out of order, an
+    Update between submits (it finishes every batch in flight first), then check_batch: every
+    batch's statuses, the pool and LRU order equal the oracle's"""
+    import random
+
+    import txflow_amd as T
+    from test_pool import _batch, vote
+    rnd = random.Random(83)
+    cfg = dict(size=1 << 20, cache_size=4000)
+    pool = T.TxVotePool(dev_ctx, **cfg, device_cache=True)
+    ref = O.Pool(**cfg)
+    hist = []
+
+    def make(n):
+        votes = []
+        for _ in range(n):
+            if hist and rnd.random() < 0.08:
+                votes.append(dict(hist[rnd.randrange(len(hist))]))
+            else:
+                votes.append(vote(rnd.randbytes(64), ts=(1_700_000_000, 1 + len(hist))))
+            hist.append(votes[-1])
+        return votes
+
+    try:
+        batches = [make(5000) for _ in range(4)]
+        bts = [_batch(T, v) for v in batches]
+        tickets = [pool.check_submit(bt, ls) for bt, ls in bts]
+        exps = [ref.check(v) for v in batches]
+        for k in (1, 0, 3, 2):                                   # out of order
+            st = pool.check_wait(tickets[k])
+            assert np.array_equal(st, exps[k]), (k, np.nonzero(st != exps[k])[0][:10])
+        batches = [make(5000) for _ in range(2)]
+        bts = [_batch(T, v) for v in batches]
+        t0 = pool.check_submit(*bts[0])
+        e0 = ref.check(batches[0])
+        committed = rnd.sample(hist, 900)
+        cb, clong = _batch(T, committed)
+        pool.update(2, cb, clong)                                # finishes t0 first
+        ref.update(2, committed)
+        t1 = pool.check_submit(*bts[1])
+        e1 = ref.check(batches[1])
+        assert np.array_equal(pool.check_wait(t0), e0)
+        assert np.array_equal(pool.check_wait(t1), e1)
+        last = make(6000)
+        lb, ll = _batch(T, last)
+        assert np.array_equal(pool.check_batch(lb, ll), ref.check(last))
+        assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+        gk, gs = pool.reap(-1)
+        ok, os_ = ref.reap(-1)
+        assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+        assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+    finally:
+        pool.close()
