@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
 #ifndef TXV_K1B_DYN_WAVES
 #define TXV_K1B_DYN_WAVES 2
 #endif
-template <int BLOCK, int WB, int WA, int V, int WAVES = 2>
+template <int BLOCK, int WB, int WA, int V, int WAVES = 2, bool FUSED = false>
 __global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n_chunks = (a.n_work + 63u) / 64u;
@@ -707,12 +707,24 @@ __global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmu
       if (c == 0xFFFFFFFFu) break;
       const uint32_t idx = 64u * c + lane;
       const uint32_t i = idx < a.n_work ? (a.order ? a.order[idx] : idx) : 0u;
-      const bool on = idx < a.n_work && a.ok_out[i] == 2;
+      bool on;
       uint32_t s[8], k[8];
+      if constexpr (FUSED) {
+        // K1a's work for this chunk here (arrival order, every vote of the batch): the SHA-512 of
+        // one wave interleaves with the other wave's walk on the SIMD
+        on = idx < a.n_work && (a.flags[i] & TXV_FLAG_PENDING) && vote_challenge(a, i, k, s);
+        if (idx < a.n_work && !on) a.ok_out[i] = 0;
+        if (!on) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
-        k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
+          for (int j = 0; j < 8; ++j) { s[j] = 0u; k[j] = 0u; }
+        }
+      } else {
+        on = idx < a.n_work && a.ok_out[i] == 2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
+          k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
+        }
       }
       // idle lanes walk the digit-0 (identity) entries of validator 0: the cooperative gathers
       // need every lane of the wave
@@ -1284,6 +1296,8 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
           if (!grid3) return hipErrorInvalidValue;
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<256, WB, WA, 8, TXV_K1B_DYN_WAVES>),
                              dim3(grid3), dim3(256), 0, st, *args);
+        } else if (args->fused_k1a) {
+          hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8, 2, true>), dim3(grid), dim3(B), 0, st, *args);
         } else {
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
         }
@@ -1331,6 +1345,10 @@ bool txv_verify_windows_supported(int wb, int wa) {
   if (wb == 24) return wa == 12 || wa == 14 || wa == 16 || wa == 18 || wa == 20;
   if (wb == 26) return wa == 16 || wa == 18 || wa == 20;
   return wa == 16 && (wb == 20 || wb == 22);
+}
+
+bool txv_k1b_fusable(int wb, const VerifyArgs* args) {
+  return TXV_K1B_DYNAMIC && TXV_K1B_DYN_WAVES < 3 && wb >= 24 && args->lane_votes == 8 && args->wctr && !args->order;
 }
 
 // K1a alone (the AddVote pipeline runs it on another stream than K1b, beside the previous

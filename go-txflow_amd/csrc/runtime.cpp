@@ -856,17 +856,20 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   va.n_work = s.n;
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
   if (!txv_verify_windows_supported(c->b_w, c->tab_w)) { c->err = "verify windows"; return TXV_EDEVICE; }
+  // TXV_K1B_FUSED=1 (experiment): the work-stealing K1b computes each chunk's challenges itself
+  static const bool fuse = getenv("TXV_K1B_FUSED") && atoi(getenv("TXV_K1B_FUSED")) == 1;
+  va.fused_k1a = fuse && txv_k1b_fusable(c->b_w, &va) ? 1u : 0u;
   HIP_TRY(c, txv_flow_prep(&fs, &fb, ps));
   HIP_TRY(c, txv_launch_signbytes(&sa, ps));
-  if (TXV_K1A_ON_KEY_STREAM) {
+  if (TXV_K1A_ON_KEY_STREAM && !va.fused_k1a) {
     HIP_TRY(c, hipEventRecord(s.ev[8], ps));
     HIP_TRY(c, txv_launch_challenge(&va, ps));
   }
   HIP_TRY(c, hipEventRecord(s.ev[1], ps));
   HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
   HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
-  if (!TXV_K1A_ON_KEY_STREAM) {
-    HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
+  if (!TXV_K1A_ON_KEY_STREAM || va.fused_k1a) {
+    if (!va.fused_k1a) HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
     HIP_TRY(c, hipEventRecord(s.ev[8], c->vstream));   // K1a | K1b split (txv_slot_verify_ms)
   }
   HIP_TRY(c, txv_launch_scalarmult(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));

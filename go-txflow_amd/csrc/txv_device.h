@@ -42,6 +42,7 @@ struct VerifyArgs {
                                // range, 64 B apart), zeroed before each launch
   uint32_t park_waves;         // waves the park buffer holds (V = 8 slots each): caps persistent grids
   uint32_t n_cus;              // CUs of the context's device
+  uint32_t fused_k1a;          // TXV_K1B_FUSED: the work-stealing K1b computes the challenges itself (no K1a)
 };
 
 #define TXV_PARK_WORDS 33          // X, Y, prefix product, Z of one parked vote; its vote index + 1
@@ -124,6 +125,7 @@ hipError_t txv_launch_keygen(const uint32_t* seeds_le, uint32_t n, const uint32_
 hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
 hipError_t txv_launch_valu_probe(int op, uint32_t* out, uint32_t blocks, int iters, hipStream_t st);
 hipError_t txv_launch_signbytes(const SignBytesArgs* args, hipStream_t st);
+bool txv_k1b_fusable(int wb, const VerifyArgs* args);   // the launch takes the work-stealing K1b
 hipError_t txv_launch_sig_keys(const uint32_t* sig, const uint32_t* sig_len, uint32_t n, uint32_t* keys,
                                 hipStream_t st);
 hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,
