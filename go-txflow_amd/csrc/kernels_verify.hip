@@ -134,6 +134,12 @@ __device__ __forceinline__ bool vote_challenge(const VerifyArgs& a, uint32_t i, 
   return true;
 }
 
+// the same out of line (the fused K1b: its SHA-512 registers then do not add to the walk's)
+__device__ __attribute__((noinline)) bool vote_challenge_call(const VerifyArgs& a, uint32_t i, uint32_t k_out[8],
+                                                              uint32_t s_out[8]) {
+  return vote_challenge(a, i, k_out, s_out);
+}
+
 // K1a: challenges of every pending vote into kbuf
 #ifndef TXV_K1A_WAVES
 #define TXV_K1A_WAVES 4
@@ -672,8 +678,8 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
 #ifndef TXV_K1B_DYN_WAVES
 #define TXV_K1B_DYN_WAVES 2
 #endif
-template <int BLOCK, int WB, int WA, int V, int WAVES = 2, bool FUSED = false>
-__global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
+template <int BLOCK, int WB, int WA, int V, int WAVES, bool FUSED>
+__device__ __forceinline__ void k1b_dyn_body(const VerifyArgs& a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n_chunks = (a.n_work + 63u) / 64u;
   const uint32_t xg = gridDim.x >= 8 ? 8u : 1u, myx = blockIdx.x % xg;
@@ -712,7 +718,7 @@ __global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmu
       if constexpr (FUSED) {
         // K1a's work for this chunk here (arrival order, every vote of the batch): the SHA-512 of
         // one wave interleaves with the other wave's walk on the SIMD
-        on = idx < a.n_work && (a.flags[i] & TXV_FLAG_PENDING) && vote_challenge(a, i, k, s);
+        on = idx < a.n_work && (a.flags[i] & TXV_FLAG_PENDING) && vote_challenge_call(a, i, k, s);
         if (idx < a.n_work && !on) a.ok_out[i] = 0;
         if (!on) {
 #pragma unroll
@@ -775,6 +781,21 @@ __global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmu
     }
     if (h < (uint32_t)V) break;
   }
+}
+
+template <int BLOCK, int WB, int WA, int V, int WAVES = 2>
+__global__ void __launch_bounds__(BLOCK, WAVES) TXV_K1B_VGPR_ATTR txv_k_scalarmult_dyn(VerifyArgs a) {
+  k1b_dyn_body<BLOCK, WB, WA, V, WAVES, false>(a);
+}
+// TXV_K1B_FUSED=1: K1a's work inside the chunks, capped at the unfused kernel's register budget so
+// the TxFlow kernels of the neighbouring batches still find VGPRs beside two K1b waves
+#ifndef TXV_K1B_FUSED_VGPRS
+#define TXV_K1B_FUSED_VGPRS 200
+#endif
+template <int BLOCK, int WB, int WA>
+__global__ void __launch_bounds__(BLOCK, 2) __attribute__((amdgpu_num_vgpr(TXV_K1B_FUSED_VGPRS)))
+txv_k_scalarmult_dyn_fused(VerifyArgs a) {
+  k1b_dyn_body<BLOCK, WB, WA, 8, 2, true>(a);
 }
 
 // Split mode (lane_votes = 1): the inversion leaves the scalar-multiply kernel.  Under SIMD a
@@ -1297,7 +1318,7 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<256, WB, WA, 8, TXV_K1B_DYN_WAVES>),
                              dim3(grid3), dim3(256), 0, st, *args);
         } else if (args->fused_k1a) {
-          hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8, 2, true>), dim3(grid), dim3(B), 0, st, *args);
+          hipLaunchKernelGGL((txv_k_scalarmult_dyn_fused<B, WB, WA>), dim3(grid), dim3(B), 0, st, *args);
         } else {
           hipLaunchKernelGGL((txv_k_scalarmult_dyn<B, WB, WA, 8>), dim3(grid), dim3(B), 0, st, *args);
         }
