@@ -116,6 +116,50 @@ TXV_HD void sha512_prefixed_pf(uint32_t digest_le[16], const uint64_t* pre, int 
   }
 }
 
+// two digests with their compressions interleaved (sha512_block2): blocks up to the longer
+// message's count, the shorter one's extra blocks computed on zeros and discarded
+TXV_HD void sha512_prefixed2(uint32_t dig0[16], const uint64_t* pre0, const MsgView& m0, uint32_t dig1[16],
+                             const uint64_t* pre1, const MsgView& m1, int pre_words) {
+  uint64_t st0[8], st1[8];
+  sha512_init(st0);
+  sha512_init(st1);
+  const uint32_t tot0 = 8u * (uint32_t)pre_words + m0.len, tot1 = 8u * (uint32_t)pre_words + m1.len;
+  const uint32_t nb0 = sha512_nblocks(tot0), nb1 = sha512_nblocks(tot1), nb = nb0 > nb1 ? nb0 : nb1;
+  const uint32_t pw0 = tot0 >> 3, ps0 = 56u - 8u * (tot0 & 7u), last0 = 16u * nb0 - 1u;
+  const uint32_t pw1 = tot1 >> 3, ps1 = 56u - 8u * (tot1 & 7u), last1 = 16u * nb1 - 1u;
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint64_t w0[16], w1[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t gw = 16u * b + (uint32_t)t;
+      uint64_t v0 = (b == 0 && t < pre_words) ? pre0[t] : msg_word(m0, gw - (uint32_t)pre_words);
+      uint64_t v1 = (b == 0 && t < pre_words) ? pre1[t] : msg_word(m1, gw - (uint32_t)pre_words);
+      if (gw == pw0) v0 |= 0x80ull << ps0;
+      if (gw == last0) v0 = (uint64_t)tot0 * 8u;
+      if (gw == pw1) v1 |= 0x80ull << ps1;
+      if (gw == last1) v1 = (uint64_t)tot1 * 8u;
+      w0[t] = v0;
+      w1[t] = v1;
+    }
+    uint64_t s0[8], s1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s0[k] = st0[k]; s1[k] = st1[k]; }
+    sha512_block2(s0, w0, s1, w1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (b < nb0) st0[k] = s0[k];
+      if (b < nb1) st1[k] = s1[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    dig0[2 * k] = bswap32((uint32_t)(st0[k] >> 32));
+    dig0[2 * k + 1] = bswap32((uint32_t)st0[k]);
+    dig1[2 * k] = bswap32((uint32_t)(st1[k] >> 32));
+    dig1[2 * k + 1] = bswap32((uint32_t)st1[k]);
+  }
+}
+
 // table entry fetch: T[pos][idx] from a flat word array, (qp, qm) swapped for -Q (neg): the
 // swap is the choice of which 16-byte-aligned half of the line is loaded as which
 template <int W, typename Ptr>

@@ -140,6 +140,63 @@ __device__ __attribute__((noinline)) bool vote_challenge_call(const VerifyArgs& 
   return vote_challenge(a, i, k_out, s_out);
 }
 
+// the scalar checks of vote i and its SHA-512 prefix (R || A as big-endian words); false when the
+// vote fails them (then no challenge is needed)
+__device__ __forceinline__ bool vote_checks(const VerifyArgs& a, uint32_t i, uint32_t s[16], uint64_t pre[8]) {
+  const uint8_t fl = a.flags[i];
+  const uint32_t v = a.val[i];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = a.sig[(size_t)j * a.n_pad + i];
+  const bool bad = !(fl & TXV_FLAG_PENDING) || !(fl & TXV_FLAG_SIG64) || (fl & TXV_FLAG_BADMSG) ||
+                   (s[15] & 0xE0000000u) || !a.decode_ok[v] || !sc_lt_L(s + 8);
+  const uint32_t* pw = a.pubs_le + (size_t)v * 8;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pre[j] = be64_from_le32(s[2 * j], s[2 * j + 1]);
+    pre[4 + j] = be64_from_le32(pw[2 * j], pw[2 * j + 1]);
+  }
+  return !bad;
+}
+
+// K1a with two votes per lane (TXV_K1A_PAIR=1, experiment): lane t takes votes t and t + n/2 and
+// runs their SHA-512 compressions interleaved (sha512_block2), so the dependent round chain of one
+// has the other's as independent work; 2 waves/SIMD at ~2x the VGPRs
+__global__ void __launch_bounds__(256, 2) txv_k_challenge2(VerifyArgs a) {
+  const uint32_t half = (a.n + 1) / 2;
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= half) return;
+  const uint32_t i0 = t, i1 = t + half;
+  const bool has1 = i1 < a.n;
+  uint32_t s0[16], s1[16];
+  uint64_t p0[8], p1[8];
+  const bool ok0 = vote_checks(a, i0, s0, p0);
+  const bool ok1 = has1 && vote_checks(a, has1 ? i1 : i0, s1, p1);
+  if (!ok0 && !ok1) {
+    a.ok_out[i0] = 0;
+    if (has1) a.ok_out[i1] = 0;
+    return;
+  }
+  const uint32_t j1 = has1 ? i1 : i0;
+  MsgView m0{a.msg + i0, a.n_pad, a.msg_words, a.msg_len[i0]};
+  MsgView m1{a.msg + j1, a.n_pad, a.msg_words, a.msg_len[j1]};
+  uint32_t d0[16], d1[16];
+  sha512_prefixed2(d0, p0, m0, d1, p1, m1, 8);
+  if (ok0) {
+    const sc k = sc_reduce512(d0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a.kbuf[(size_t)j * a.n_pad + i0] = k.v[j];
+  }
+  a.ok_out[i0] = ok0 ? 2 : 0;
+  if (has1) {
+    if (ok1) {
+      const sc k = sc_reduce512(d1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a.kbuf[(size_t)j * a.n_pad + i1] = k.v[j];
+    }
+    a.ok_out[i1] = ok1 ? 2 : 0;
+  }
+}
+
 // K1a: challenges of every pending vote into kbuf
 #ifndef TXV_K1A_WAVES
 #define TXV_K1A_WAVES 4
@@ -1376,7 +1433,13 @@ bool txv_k1b_fusable(int wb, const VerifyArgs* args) {
 // batch's K1b: K1b leaves ~116 VGPRs per SIMD free, room for one K1a wave)
 hipError_t txv_launch_challenge(const VerifyArgs* args, hipStream_t st) {
   if (!args->n) return hipSuccess;
-  hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
+  static const bool pair = getenv("TXV_K1A_PAIR") && atoi(getenv("TXV_K1A_PAIR")) == 1;
+  if (pair) {
+    const uint32_t half = (args->n + 1) / 2;
+    hipLaunchKernelGGL(txv_k_challenge2, dim3((half + 255) / 256), dim3(256), 0, st, *args);
+  } else {
+    hipLaunchKernelGGL(txv_k_challenge, dim3((args->n + 255) / 256), dim3(256), 0, st, *args);
+  }
   return hipGetLastError();
 }
 

@@ -140,6 +140,51 @@ TXV_HD void sha512_block(uint64_t st[8], uint64_t w[16]) {
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+
+// two independent compressions with their rounds interleaved (K1a's paired variant): every round
+// of one message has the other's as independent neighbours, so a wave's dependent SHA-512 chain
+// issues with ILP 2 instead of waiting on itself
+#define TXV_SHA512_ROUND2(I, J, SCHED, W, A, B, C, D, E, F, G, H)                           \
+  {                                                                                        \
+    uint64_t wi;                                                                           \
+    if (SCHED) {                                                                           \
+      const uint64_t w15 = W[((J) + 1) & 15], w2 = W[((J) + 14) & 15];                      \
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));           \
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));            \
+      wi = W[(J) & 15] + s0 + W[((J) + 9) & 15] + s1;                                      \
+      W[(J) & 15] = wi;                                                                    \
+    } else {                                                                               \
+      wi = W[J];                                                                           \
+    }                                                                                      \
+    const uint64_t S1 = xor3_64(rotr64(E, 14), rotr64(E, 18), rotr64(E, 41));              \
+    const uint64_t ch = G ^ (E & (F ^ G));                                                 \
+    const uint64_t t1 = H + S1 + ch + sha512_k(I) + wi;                                     \
+    const uint64_t S0 = xor3_64(rotr64(A, 28), rotr64(A, 34), rotr64(A, 39));              \
+    const uint64_t mj = maj64(A, B, C);                                                    \
+    const uint64_t t2 = S0 + mj;                                                           \
+    H = G; G = F; F = E; E = D + t1; D = C; C = B; B = A; A = t1 + t2;                    \
+  }
+
+TXV_HD void sha512_block2(uint64_t st0[8], uint64_t w0[16], uint64_t st1[8], uint64_t w1[16]) {
+  uint64_t a0 = st0[0], b0 = st0[1], c0 = st0[2], d0 = st0[3], e0 = st0[4], f0 = st0[5], g0 = st0[6], h0 = st0[7];
+  uint64_t a1 = st1[0], b1 = st1[1], c1 = st1[2], d1 = st1[3], e1 = st1[4], f1 = st1[5], g1 = st1[6], h1 = st1[7];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    TXV_SHA512_ROUND2(j, j, false, w0, a0, b0, c0, d0, e0, f0, g0, h0)
+    TXV_SHA512_ROUND2(j, j, false, w1, a1, b1, c1, d1, e1, f1, g1, h1)
+  }
+#pragma unroll 1
+  for (int i0 = 16; i0 < 80; i0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      TXV_SHA512_ROUND2(i0 + j, j, true, w0, a0, b0, c0, d0, e0, f0, g0, h0)
+      TXV_SHA512_ROUND2(i0 + j, j, true, w1, a1, b1, c1, d1, e1, f1, g1, h1)
+    }
+  }
+  st0[0] += a0; st0[1] += b0; st0[2] += c0; st0[3] += d0; st0[4] += e0; st0[5] += f0; st0[6] += g0; st0[7] += h0;
+  st1[0] += a1; st1[1] += b1; st1[2] += c1; st1[3] += d1; st1[4] += e1; st1[5] += f1; st1[6] += g1; st1[7] += h1;
+}
+#undef TXV_SHA512_ROUND2
 #undef TXV_SHA512_ROUND
 
 TXV_HD uint32_t sha256_k(int i) {
