@@ -138,6 +138,8 @@ struct txv_ctx {
   hipStream_t vstream = nullptr;       // verify: prep + K1a/K1b (batch k+1 verifies while batch k tallies)
   hipStream_t copy_stream = nullptr;   // batch uploads, so batch k+1's H2D overlaps batch k's kernels
   hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest), wire decode, and each batch's prep + SignBytes
+  hipEvent_t tally_ev = nullptr;        // TXV_K1B_AFTER_TALLY: the newest batch's tally end (flow stream)
+  bool tally_ev_set = false;
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   ErrMsg err;
   std::mutex mu;
@@ -868,8 +870,12 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipEventRecord(s.ev[1], ps));
   HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[1], 0));
   HIP_TRY(c, hipEventRecord(s.ev[7], c->vstream));
+  // TXV_K1B_AFTER_TALLY=1 (experiment): K1b waits for the previous batch's tally, which then runs
+  // beside this batch's K1a instead of beside its K1b
+  static const bool after_tally = getenv("TXV_K1B_AFTER_TALLY") && atoi(getenv("TXV_K1B_AFTER_TALLY")) == 1;
   if (!TXV_K1A_ON_KEY_STREAM || va.fused_k1a) {
     if (!va.fused_k1a) HIP_TRY(c, txv_launch_challenge(&va, c->vstream));
+    if (after_tally && c->tally_ev_set) HIP_TRY(c, hipStreamWaitEvent(c->vstream, c->tally_ev, 0));
     HIP_TRY(c, hipEventRecord(s.ev[8], c->vstream));   // K1a | K1b split (txv_slot_verify_ms)
   }
   HIP_TRY(c, txv_launch_scalarmult(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
@@ -887,6 +893,11 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[2], 0));
   HIP_TRY(c, txv_flow_tally(&fs, &fb, sets_bound, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[5], c->stream));
+  if (after_tally) {
+    if (!c->tally_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->tally_ev, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->tally_ev, c->stream));
+    c->tally_ev_set = true;
+  }
   if (s.sink) HIP_TRY(c, txv_flow_pack(&fs, s.sink, (s.sink_cap + 31) / 32, s.sink_cap, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[4], c->stream));
   s.ran = true;
