@@ -140,6 +140,8 @@ struct txv_ctx {
   hipStream_t key_stream = nullptr;    // txv_sig_keys (pool ingest), wire decode, and each batch's prep + SignBytes
   hipEvent_t tally_ev = nullptr;        // TXV_K1B_AFTER_TALLY: the newest batch's tally end (flow stream)
   bool tally_ev_set = false;
+  hipEvent_t vend_ev[4] = {};           // TXV_PREP_AFTER_K1B: the last batches' K1b ends (verify stream)
+  uint64_t vend_n = 0;
   uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
   ErrMsg err;
   std::mutex mu;
@@ -847,6 +849,10 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[3], 0));
   if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[4], 0));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
+  // TXV_PREP_AFTER_K1B=1 (experiment): this batch's prep + SignBytes wait for the K1b two batches
+  // back, so they run beside the next K1a instead of beside a K1b
+  static const bool prep_after = getenv("TXV_PREP_AFTER_K1B") && atoi(getenv("TXV_PREP_AFTER_K1B")) == 1;
+  if (prep_after && c->vend_n >= 2) HIP_TRY(c, hipStreamWaitEvent(ps, c->vend_ev[(c->vend_n - 2) % 4], 0));
   HIP_TRY(c, hipEventRecord(s.ev[0], ps));
   SignBytesArgs sa{};
   sa.n = s.n; sa.n_pad = s.n_pad; sa.msg_words = s.msg_words; sa.chain_len = fb.chain_len;
@@ -880,6 +886,12 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   }
   HIP_TRY(c, txv_launch_scalarmult(c->b_w, c->tab_w, &va, verify_grid(c, s.n), c->vstream));
   HIP_TRY(c, hipEventRecord(s.ev[2], c->vstream));
+  if (prep_after) {
+    hipEvent_t& ve = c->vend_ev[c->vend_n % 4];
+    if (!ve) HIP_TRY(c, hipEventCreateWithFlags(&ve, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(ve, c->vstream));
+    ++c->vend_n;
+  }
   HIP_TRY(c, txv_flow_route(&fs, &fb, c->stream));
   HIP_TRY(c, txv_flow_new_ids(&fs, &fb, c->stream));
   HIP_TRY(c, hipEventRecord(s.ev[6], c->stream));
