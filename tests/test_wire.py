@@ -466,7 +466,8 @@ def test_gpu_ingest_chain_matches_oracle(mode):
 
 
 @pytest.mark.gpu
-def test_gpu_ingest_capacity_overflow_reports_not_run():
+@pytest.mark.parametrize("device_cache", [False, True], ids=["host-cache", "device-cache"])
+def test_gpu_ingest_capacity_overflow_reports_not_run(device_cache):
     """a TxFlow capacity overflow after the pool stage must not strand the admitted
     votes silently.  A context with room for 8 TxVoteSets receives messages for 40 txs: the call
     fails with TXV_ECAPACITY, every pool-admitted message carries FLOW_NOT_RUN (in the pool, not in
@@ -491,7 +492,8 @@ def test_gpu_ingest_capacity_overflow_reports_not_run():
         wire = [O.wire_encode(v.Height, v.TxHash.encode(), v.Timestamp[0], v.Timestamp[1], v.ValidatorAddress,
                               s.tobytes(), b"\0" * 32) for v, s in zip(votes, sigs)]
         wire.insert(5, b"\x01\x02")                       # undecodable: never reaches the pool
-        pool = T.TxVotePool(ctx, size=1 << 12, cache_size=1 << 12, max_txs_bytes=1 << 30, max_msg_bytes=4096)
+        pool = T.TxVotePool(ctx, size=1 << 12, cache_size=1 << 12, max_txs_bytes=1 << 30, max_msg_bytes=4096,
+                            device_cache=device_cache)
         with pytest.raises(T.IngestError) as ei:
             pool.ingest(T.WireBatch(wire))
         ws, ps, fs, _ = ei.value.result
