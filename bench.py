@@ -738,8 +738,8 @@ def main():
     # enqueued, so step k+1's prep runs beside step k's K1b and its K1a/K1b beside step k's tally
     # (txv_run_staged returns as soon as the chain is enqueued).  At N>1 each step's packed
     # per-shard commit state ([n_sets][bitmap][sums], written by the device into the
-    # slot's commit sink) is all-gathered over RCCL on the context's flow stream right behind the
-    # step's chain (txflow_amd/pipeline.py): no host thread waits for the exchange.
+    # slot's commit sink) is all-gathered over RCCL on an exchange stream after the step's chain
+    # (txflow_amd/pipeline.py): the next chains do not queue behind it, no host thread waits.
     from txflow_amd.pipeline import PipelinedSteps
     DEPTH = int(os.environ.get("TXV_BENCH_DEPTH", "3"))   # 2..4 staged slots
     n_cap = max_txs
@@ -802,7 +802,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # RCCL: the per-step commit-state all-gather's device time on the flow stream (events around
+    # RCCL: the per-step commit-state all-gather's device time on the exchange stream (events around
     # it, txflow_amd/pipeline.py), for the timed region's last `depth` steps (their slots' events)
     gather_ms = None
     if dist is not None and not gloo:

@@ -51,7 +51,8 @@ template <int W>
 __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restrict__ pubs_le, uint32_t n_points,
                                                           uint32_t* __restrict__ tables,
                                                           uint8_t* __restrict__ decode_ok,
-                                                          uint32_t* __restrict__ addr_words) {
+                                                          uint32_t* __restrict__ addr_words,
+                                                          const uint32_t* __restrict__ out_slot) {
   constexpr int chunks = (Tab<W>::kEntries - 1) / 8;
   constexpr int per_point = Tab<W>::kPositions * chunks;
   const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
@@ -83,7 +84,7 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
 #pragma unroll
   for (int j = 1; j < 8; ++j) pref[j] = fe_mul(pref[j - 1], M[j].Z);
   fe inv = fe_invert(pref[7]);
-  uint32_t* out = tables + (size_t)pt * Tab<W>::kWords + (size_t)pos * Tab<W>::kEntries * kEntryWords;
+  uint32_t* out = tables + (size_t)(out_slot ? out_slot[pt] : pt) * Tab<W>::kWords + (size_t)pos * Tab<W>::kEntries * kEntryWords;
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
     fe zi = j ? fe_mul(inv, pref[j - 1]) : inv;
@@ -95,6 +96,9 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
 }
 
 // ---------------------------------------------------------------- K1: verify
+// the table slot of validator v: txv_set_validators keeps each key's tables in one slot of the
+// context's table pool across validator-set changes (null: the tables are in validator order)
+__device__ __forceinline__ uint32_t tab_slot(const VerifyArgs& a, uint32_t v) { return a.tslot ? a.tslot[v] : v; }
 // K1 is split in two launches so each phase gets its own register allocation (one fused
 // kernel kept the signature words and digits live across SHA-512 and the table walk and
 // needed 272 VGPRs = 1 wave/SIMD):
@@ -226,7 +230,7 @@ __device__ __forceinline__ void scalarmult_loop(const VerifyArgs& a, PtrB btab, 
     uint32_t s[8], k[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-    const uint32_t* ta = a.atables + (size_t)v * Tab<W>::kWords;
+    const uint32_t* ta = a.atables + (size_t)tab_slot(a, v) * Tab<W>::kWords;
     ge_ext R = double_scalarmult_w<W>(btab, ta, s, k, true);
     uint32_t enc[8];
     ge_encode_zinv(enc, R.X, R.Y, verify_invert(R.Z));
@@ -286,7 +290,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_pair(
         uint32_t s[8], k[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-        R = double_scalarmult_w<W>(a.btable, a.atables + (size_t)v * Tab<W>::kWords, s, k, true);
+        R = double_scalarmult_w<W>(a.btable, a.atables + (size_t)tab_slot(a, v) * Tab<W>::kWords, s, k, true);
       } else {
         R = ge_identity();
       }
@@ -649,7 +653,7 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
 #pragma unroll
         for (int j = 0; j < 8; ++j) { R.X.v[j] = s[j] | 1u; R.Y.v[j] = k[j] | 2u; R.Z.v[j] = s[j] ^ k[j] ^ 5u; R.T.v[j] = 0; }
 #else
-        R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+        R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? tab_slot(a, a.val[i]) : 0u, s, k, wbuf);
 #endif
       }
 #else
@@ -659,7 +663,7 @@ __global__ void __launch_bounds__(BLOCK, V == 8 ? 2 : TXV_V4_WAVES * BLOCK / 512
         uint32_t s[8], k[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * a.n_pad + i]; k[j] = a.kbuf[(size_t)j * a.n_pad + i]; }
-        R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)a.val[i] * Tab<WA>::kWords, s, k, true);
+        R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)tab_slot(a, a.val[i]) * Tab<WA>::kWords, s, k, true);
       } else {
         R = ge_identity();
       }
@@ -791,7 +795,7 @@ __device__ __forceinline__ void k1b_dyn_body(const VerifyArgs& a) {
       }
       // idle lanes walk the digit-0 (identity) entries of validator 0: the cooperative gathers
       // need every lane of the wave
-      R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? a.val[i] : 0u, s, k, wbuf);
+      R = k1b_walk<WB, WA, PD>(a.btable, a.atables, on ? tab_slot(a, a.val[i]) : 0u, s, k, wbuf);
       P = h ? fe_mul(P, R.Z) : R.Z;
       uint32_t* slot = park + h * TXV_PARK_WORDS * 64;
 #pragma unroll
@@ -881,7 +885,7 @@ __global__ void __launch_bounds__(BLOCK, 2 * BLOCK / 256) txv_k_scalarmult_point
     uint32_t s[8], k[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s[j] = a.sig[(size_t)(8 + j) * np + i]; k[j] = a.kbuf[(size_t)j * np + i]; }
-    const ge_ext R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)a.val[i] * Tab<WA>::kWords, s, k, true);
+    const ge_ext R = double_scalarmult_w2<WB, WA>(a.btable, a.atables + (size_t)tab_slot(a, a.val[i]) * Tab<WA>::kWords, s, k, true);
     uint32_t* o = a.rpts + idx;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1049,7 +1053,7 @@ __global__ void __launch_bounds__(256, TXV_SPLIT_WAVES) txv_k_scalarmult_split(V
       s[j] = on ? a.sig[(size_t)(8 + j) * a.n_pad + i] : 0u;
       k[j] = on ? a.kbuf[(size_t)j * a.n_pad + i] : 0u;
     }
-    const uint32_t va = on ? a.val[i] : 0u;
+    const uint32_t va = on ? tab_slot(a, a.val[i]) : 0u;
     // every entry of this lane's run up front as (table, entry index), so the scalars are dead
     // before the walk starts: all signed digits of s and k by direct window extraction (carries
     // rippled in order, as next_digit), then run entry j of lane q = schedule entry q * per + j,
@@ -1303,10 +1307,10 @@ extern "C" {
 
 template <int W>
 static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables, uint8_t* decode_ok,
-                         uint32_t* addr_words, hipStream_t st) {
+                         uint32_t* addr_words, const uint32_t* out_slot, hipStream_t st) {
   const uint64_t lanes = (uint64_t)n_points * Tab<W>::kPositions * ((Tab<W>::kEntries - 1) / 8);
   hipLaunchKernelGGL(txv_k_build_tables<W>, dim3((uint32_t)((lanes + 63) / 64)), dim3(64), 0, st, pubs_le, n_points,
-                     tables, decode_ok, addr_words);
+                     tables, decode_ok, addr_words, out_slot);
 }
 
 // K1c's votes per lane: the largest G whose launch still gives every SIMD of the chip about
@@ -1395,24 +1399,29 @@ static hipError_t launch_multi(const VerifyArgs* args, uint32_t grid, hipStream_
 
 extern "C" {
 
-hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
-                                   uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
+hipError_t txv_launch_build_tables_at(int w, const uint32_t* pubs_le, uint32_t n_points, const uint32_t* out_slot,
+                                      uint32_t* tables, uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
   if (!n_points) return hipSuccess;
   switch (w) {
-    case 4: launch_build<4>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 8: launch_build<8>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 10: launch_build<10>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 12: launch_build<12>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 14: launch_build<14>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 18: launch_build<18>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
-    case 26: launch_build<26>(pubs_le, n_points, tables, decode_ok, addr_words, st); break;
+    case 4: launch_build<4>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 8: launch_build<8>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 10: launch_build<10>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 12: launch_build<12>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 14: launch_build<14>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 18: launch_build<18>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 26: launch_build<26>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
+                                   uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st) {
+  return txv_launch_build_tables_at(w, pubs_le, n_points, nullptr, tables, decode_ok, addr_words, st);
 }
 
 // (wb, wa): base-point and validator windows; supported pairs are (w, w) for every table

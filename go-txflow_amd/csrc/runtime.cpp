@@ -171,9 +171,18 @@ struct txv_ctx {
   bool lane_auto = true;           // no configured V: 8 for batches that still give >= 1.5 waves/SIMD
   uint32_t* d_park = nullptr;      // K1b parked points: [wave][V][33][64]
   uint32_t* d_wctr = nullptr;      // chunk counters of the work-stealing K1b
-  std::vector<uint8_t> built_pubs; // keys the current validator tables were built from
-  uint32_t built_n = 0;
-  int built_w = 0;
+  // the validator tables as a pool of per-key slots: a new validator set builds (K0) only the
+  // keys no slot holds; validator v's tables are at slot vslot[v] (d_vslot, VerifyArgs.tslot)
+  uint32_t tab_slots = 0;              // slots allocated in d_atables
+  int pool_w = 0;                      // window of the pool's tables
+  std::vector<std::string> slot_key;   // key each slot holds ("" = empty)
+  std::vector<uint8_t> slot_ok;        // its decode flag
+  std::vector<uint8_t> slot_addr;      // [slot][20] its address
+  std::vector<uint64_t> slot_gen;      // last validator set that used the slot (eviction order)
+  uint64_t set_gen = 0;
+  std::vector<uint32_t> vslot;         // validator index -> slot
+  uint32_t* d_vslot = nullptr;
+  uint32_t tables_built = 0;           // keys K0 built in the last txv_set_validators
   size_t park_words = 0;
   // scratch registry for caller-supplied keys (txv_verify_batch with pubs32)
   uint32_t tmp_cap = 0;
@@ -544,7 +553,8 @@ uint32_t verify_grid(txv_ctx* c, uint32_t n) {
 // reads (sig, kbuf: 24 words per vote at a stride of ~n_vals votes) over 24 distinct lines per
 // vote (measured at w = 20: 59 L2 line misses per vote, 36 of them table lines); there K1b walks
 // the votes in arrival order (order = null, n_work = n; K1a marks non-pending votes ok = 0).
-VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t* dok, const uint32_t* tabs, int w) {
+VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t* dok, const uint32_t* tabs, int w,
+                       const uint32_t* tslot) {
   VerifyArgs a{};
   a.n = s.n; a.n_pad = s.n_pad; a.msg_words = s.msg_words;
   a.sig = s.d_sig; a.msg = s.d_msg; a.msg_len = s.d_msg_len; a.val = s.d_val; a.flags = s.d_flags;
@@ -552,6 +562,7 @@ VerifyArgs verify_args(txv_ctx* c, Slot& s, const uint32_t* pubs, const uint8_t*
   a.n_work = by_val || !s.n_work ? s.n_work : s.n; a.kbuf = s.d_kbuf;
   a.order = by_val ? s.d_order : nullptr; a.pubs_le = pubs; a.decode_ok = dok; a.atables = tabs; a.btable = c->d_btable;
   a.ok_out = s.d_ok;
+  a.tslot = tslot;
   a.park = c->d_park;
   a.park_waves = (uint32_t)(c->park_words / ((size_t)8 * TXV_PARK_WORDS * 64));
   a.n_cus = (uint32_t)c->n_cus;
@@ -859,7 +870,7 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   sa.height = s.d_fh; sa.ts_sec = s.d_fs; sa.ts_nanos = s.d_fn; sa.txhash_off = s.d_fo; sa.txhash_len = s.d_fl;
   sa.txhash = s.d_arena_th; sa.chain = c->d_chain; sa.msg_len = nullptr; sa.nil = s.has_nil ? s.d_nil : nullptr;
   sa.msg = s.d_msg;
-  VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w);
+  VerifyArgs va = verify_args(c, s, c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w, c->d_vslot);
   va.order = nullptr;          // arrival order; K1a marks the non-pending votes
   va.n_work = s.n;
   va.lane_votes = launch_lane_votes(c, c->b_w, va.n_work);
@@ -1079,9 +1090,10 @@ struct KeySet {
   const uint8_t* ok;
   const uint32_t* tables;
   int w;
+  const uint32_t* slot;   // table slot per key, null = key order
 };
 
-KeySet registry_keys(const txv_ctx* c) { return KeySet{c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w}; }
+KeySet registry_keys(const txv_ctx* c) { return KeySet{c->d_pubs, c->d_decode_ok, c->d_atables, c->tab_w, c->d_vslot}; }
 
 // Caller-supplied keys (txv_verify_batch with pubs32, txv_verify_bytes): de-duplicated into
 // throw-away tables -- the registry's window when they fit the table budget (its B table
@@ -1126,7 +1138,7 @@ int prepare_keys(txv_ctx* c, const uint8_t* pubs32, uint32_t n, std::vector<uint
     if (nu) HIP_TRY(c, hipMemcpyAsync(key_addr->data(), c->d_tmp_addr, (size_t)nu * 20, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  ks = KeySet{c->d_tmp_pubs, c->d_tmp_ok, c->d_tmp_tables, w_keys};
+  ks = KeySet{c->d_tmp_pubs, c->d_tmp_ok, c->d_tmp_tables, w_keys, nullptr};
   return TXV_OK;
 }
 
@@ -1135,7 +1147,7 @@ int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) 
   int r;
   if ((r = upload_slot(c, s)) || (r = ensure_park(c))) return r;
   HIP_TRY(c, hipStreamWaitEvent(c->vstream, s.ev[3], 0));
-  VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables, ks.w);
+  VerifyArgs va = verify_args(c, s, ks.pubs, ks.ok, ks.tables, ks.w, ks.slot);
   const bool reg_w = ks.w == c->tab_w;
   const int w_base = reg_w ? c->b_w : ks.w;
   va.btable = reg_w ? c->d_btable : (ks.w == 4 ? c->d_btable4 : c->d_btable8);
@@ -1296,7 +1308,7 @@ void txv_destroy(txv_ctx* c) {
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
   }
-  dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_addr); dfree(c->d_power);
+  dfree(c->d_pubs); dfree(c->d_decode_ok); dfree(c->d_atables); dfree(c->d_vslot); dfree(c->d_addr); dfree(c->d_power);
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); release_base_table(c->device, c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
@@ -1334,6 +1346,151 @@ int txv_device_name(txv_ctx* c, char* buf, uint32_t cap) {
   return TXV_OK;
 }
 
+// The validator tables of a new set (txv_set_validators; the reference builds each tx's VoteSet
+// from the current state's validators, txflow/service.go:200-207, and that set changes with the
+// chain).  Keys some slot of the pool already holds keep their tables, in any order; the others
+// take empty slots, then the slots of departed keys least recently in a set, and only they run
+// K0 (0.89 s for 100 keys at radix 2^20, 872 MB each).  A set larger than the pool grows it
+// (the kept tables copied device to device, an eighth spare; a full rebuild if HBM cannot hold
+// both pools), a new window empties it.  Then the per-validator arrays: keys, decode flags,
+// addresses (from the slots), vslot.
+int assign_tables(txv_ctx* c, const uint8_t* pubs32, uint32_t n, int w) {
+  // K0 rewrites slots an enqueued verify may still read
+  for (hipStream_t st : {c->copy_stream, c->key_stream, c->vstream, c->stream}) HIP_TRY(c, hipStreamSynchronize(st));
+  c->tables_built = 0;
+  ++c->set_gen;
+  const size_t words = table_words(w);
+  int r;
+  auto reset_pool = [&](uint32_t slots) -> int {
+    c->tab_slots = 0;
+    if ((r = dalloc(c, &c->d_atables, (size_t)slots * words))) return r;
+    c->tab_slots = slots;
+    c->slot_key.assign(slots, std::string());
+    c->slot_ok.assign(slots, 0);
+    c->slot_addr.assign((size_t)slots * 20, 0);
+    c->slot_gen.assign(slots, 0);
+    return TXV_OK;
+  };
+  if (c->pool_w != w) {
+    c->pool_w = w;
+    if ((r = reset_pool(0))) return r;
+  }
+  c->vslot.assign(n, UINT32_MAX);
+  std::vector<char> taken(c->tab_slots, 0);
+  {
+    std::unordered_map<std::string, uint32_t> held;
+    for (uint32_t sl = 0; sl < c->tab_slots; ++sl)
+      if (!c->slot_key[sl].empty()) held.emplace(c->slot_key[sl], sl);
+    for (uint32_t i = 0; i < n; ++i) {
+      auto it = held.find(std::string((const char*)pubs32 + (size_t)i * 32, 32));
+      if (it != held.end() && !taken[it->second]) { c->vslot[i] = it->second; taken[it->second] = 1; }
+    }
+  }
+  if (n > c->tab_slots) {
+    const uint64_t budget_slots = ((uint64_t)c->cfg.table_budget_mb << 20) / (words * 4);
+    const uint32_t cap = c->tab_slots ? (uint32_t)std::max<uint64_t>(n, std::min<uint64_t>(budget_slots, n + std::max(1u, n / 8))) : n;
+    uint32_t* np = nullptr;
+    uint32_t kept = 0;
+    for (char t : taken) kept += t != 0;
+    if (kept && hipMalloc((void**)&np, (size_t)cap * words * 4) == hipSuccess) {
+      // the kept tables to slots 0..kept-1 of the larger pool
+      std::vector<uint32_t> moved(c->tab_slots, UINT32_MAX);
+      std::vector<std::string> key(cap);
+      std::vector<uint8_t> ok(cap, 0), addr((size_t)cap * 20, 0);
+      uint32_t j = 0;
+      for (uint32_t sl = 0; sl < c->tab_slots; ++sl) {
+        if (!taken[sl]) continue;
+        HIP_TRY(c, hipMemcpyAsync(np + (size_t)j * words, c->d_atables + (size_t)sl * words, words * 4,
+                                  hipMemcpyDeviceToDevice, c->stream));
+        key[j] = c->slot_key[sl];
+        ok[j] = c->slot_ok[sl];
+        memcpy(&addr[(size_t)j * 20], &c->slot_addr[(size_t)sl * 20], 20);
+        moved[sl] = j++;
+      }
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(c->d_atables);
+      c->d_atables = np;
+      c->tab_slots = cap;
+      c->slot_key.swap(key);
+      c->slot_ok.swap(ok);
+      c->slot_addr.swap(addr);
+      c->slot_gen.assign(cap, 0);
+      for (auto& v : c->vslot) if (v != UINT32_MAX) v = moved[v];
+      taken.assign(cap, 0);
+      for (uint32_t k = 0; k < kept; ++k) taken[k] = 1;
+    } else {
+      (void)hipGetLastError();
+      if ((r = reset_pool(0)) || (r = reset_pool(cap))) return r;   // free the old pool first
+      c->vslot.assign(n, UINT32_MAX);
+      taken.assign(cap, 0);
+    }
+  }
+  // slots for the keys without one: empty slots first, then the least recently used
+  std::vector<uint32_t> miss, free_sl;
+  for (uint32_t i = 0; i < n; ++i) if (c->vslot[i] == UINT32_MAX) miss.push_back(i);
+  for (uint32_t sl = 0; sl < c->tab_slots; ++sl) if (!taken[sl]) free_sl.push_back(sl);
+  std::stable_sort(free_sl.begin(), free_sl.end(), [&](uint32_t a, uint32_t b) {
+    const bool ea = c->slot_key[a].empty(), eb = c->slot_key[b].empty();
+    return ea != eb ? ea : c->slot_gen[a] < c->slot_gen[b];
+  });
+  const uint32_t m = (uint32_t)miss.size();
+  if (m > free_sl.size()) { c->err = "table pool"; return TXV_EDEVICE; }   // n <= tab_slots by construction
+  if (m) {
+    std::vector<uint8_t> mk((size_t)m * 32);
+    std::vector<uint32_t> ms(m);
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint32_t i = miss[j], sl = free_sl[j];
+      memcpy(&mk[(size_t)j * 32], pubs32 + (size_t)i * 32, 32);
+      ms[j] = sl;
+      c->vslot[i] = sl;
+      c->slot_key[sl] = std::string((const char*)pubs32 + (size_t)i * 32, 32);
+    }
+    uint32_t *d_k = nullptr, *d_s = nullptr, *d_a = nullptr;
+    uint8_t* d_o = nullptr;
+    auto fin = [&](int rr) { dfree(d_k); dfree(d_s); dfree(d_a); dfree(d_o); return rr; };
+    if ((r = dalloc(c, &d_k, (size_t)m * 8)) || (r = dalloc(c, &d_s, m)) || (r = dalloc(c, &d_a, (size_t)m * 5)) ||
+        (r = dalloc(c, &d_o, m)))
+      return fin(r);
+    std::vector<uint8_t> ok(m), addr((size_t)m * 20);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(d_k, mk.data(), mk.size(), hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_s, ms.data(), (size_t)m * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = txv_launch_build_tables_at(w, d_k, m, d_s, c->d_atables, d_o, d_a, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(ok.data(), d_o, m, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(addr.data(), d_a, (size_t)m * 20, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+      for (uint32_t j = 0; j < m; ++j) c->slot_key[ms[j]].clear();   // their tables are not trustworthy
+      c->err = std::string("K0: ") + hipGetErrorString(e);
+      return fin(TXV_EDEVICE);
+    }
+    for (uint32_t j = 0; j < m; ++j) {
+      c->slot_ok[ms[j]] = ok[j];
+      memcpy(&c->slot_addr[(size_t)ms[j] * 20], &addr[(size_t)j * 20], 20);
+    }
+    c->tables_built = m;
+    fin(TXV_OK);
+  }
+  for (uint32_t i = 0; i < n; ++i) c->slot_gen[c->vslot[i]] = c->set_gen;
+  // per-validator arrays, in the set's order
+  c->addrs.resize((size_t)n * 20);
+  c->decode_ok.resize(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(&c->addrs[(size_t)i * 20], &c->slot_addr[(size_t)c->vslot[i] * 20], 20);
+    c->decode_ok[i] = c->slot_ok[c->vslot[i]];
+  }
+  if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
+      (r = dalloc(c, &c->d_addr, (size_t)n * 5)) || (r = dalloc(c, &c->d_vslot, n)))
+    return r;
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_pubs, pubs32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_decode_ok, c->decode_ok.data(), n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_addr, c->addrs.data(), (size_t)n * 20, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_vslot, c->vslot.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return TXV_OK;
+}
+
 int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers, uint32_t n, const char* chain_id,
                        uint32_t chain_len) {
   if (!c || (!pubs32 && n) || (!powers && n)) return TXV_EINVAL;
@@ -1353,35 +1510,9 @@ int txv_set_validators(txv_ctx* c, const uint8_t* pubs32, const int64_t* powers,
   }
   int r;
   const int w = choose_window(c, n);
-  // the same keys in the same order at the same window: the per-validator tables (K0, ~0.9 s for
-  // 100 validators at radix 2^20), addresses and decode flags are kept; powers, quorum and chain
-  // id are taken anew and the TxFlow state is reset as for any new set
-  const bool same_keys = n && c->built_n == n && c->built_w == w && c->d_atables &&
-                         c->built_pubs.size() == (size_t)n * 32 && !memcmp(c->built_pubs.data(), pubs32, (size_t)n * 32);
-  if ((r = select_window(c, w))) return r;
-  if (!same_keys) {
-    c->built_n = 0;
-    if ((r = dalloc(c, &c->d_pubs, (size_t)n * 8)) || (r = dalloc(c, &c->d_decode_ok, n)) ||
-        (r = dalloc(c, &c->d_atables, (size_t)n * table_words(c->tab_w))) || (r = dalloc(c, &c->d_addr, (size_t)n * 5)))
-      return r;
-  }
+  if ((r = select_window(c, w)) || (r = assign_tables(c, pubs32, n, w))) return r;
   if ((r = dalloc(c, &c->d_power, n))) return r;
-  if (n) {
-    HIP_TRY(c, hipMemcpyAsync(c->d_power, powers, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
-    if (!same_keys) {
-      HIP_TRY(c, hipMemcpyAsync(c->d_pubs, pubs32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(c, txv_launch_build_tables(c->tab_w, c->d_pubs, n, c->d_atables, c->d_decode_ok, c->d_addr, c->stream));
-      c->built_pubs.assign(pubs32, pubs32 + (size_t)n * 32);
-      c->built_n = n;
-      c->built_w = w;
-    }
-  }
-  c->addrs.resize((size_t)n * 20);
-  c->decode_ok.resize(n);
-  if (n) {
-    HIP_TRY(c, hipMemcpyAsync(c->addrs.data(), c->d_addr, (size_t)n * 20, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->decode_ok.data(), c->d_decode_ok, n, hipMemcpyDeviceToHost, c->stream));
-  }
+  if (n) HIP_TRY(c, hipMemcpyAsync(c->d_power, powers, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->addr_index.clear();
   for (uint32_t i = 0; i < n; ++i) c->addr_index.emplace(std::string((const char*)c->addrs.data() + 20 * i, 20), i);
@@ -2316,6 +2447,7 @@ int txv_valu_probe(txv_ctx* c, double* add_lane_ops_per_s, double* mad_lane_ops_
 }
 
 int txv_table_window(txv_ctx* c) { return c ? c->tab_w : TXV_EINVAL; }
+int txv_validator_tables_built(txv_ctx* c) { return c ? (int)c->tables_built : TXV_EINVAL; }
 int txv_base_window(txv_ctx* c) { return c ? c->b_w : TXV_EINVAL; }
 
 int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op) {

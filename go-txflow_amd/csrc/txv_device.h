@@ -30,7 +30,7 @@ struct VerifyArgs {
   const uint32_t* order;       // optional processing order (validator-grouped), may be null
   const uint32_t* pubs_le;     // [n_vals][8]
   const uint8_t* decode_ok;    // [n_vals]
-  const uint32_t* atables;     // [n_vals][kTableWords]
+  const uint32_t* atables;     // [slots][kTableWords] (validator v at slot tslot[v])
   const uint32_t* btable;      // [kTableWords]
   uint8_t* ok_out;             // [n]
   uint32_t* park;              // [waves][V-1][32][64] parked points of the multi-vote K1b
@@ -43,6 +43,7 @@ struct VerifyArgs {
   uint32_t park_waves;         // waves the park buffer holds (V = 8 slots each): caps persistent grids
   uint32_t n_cus;              // CUs of the context's device
   uint32_t fused_k1a;          // TXV_K1B_FUSED: the work-stealing K1b computes the challenges itself (no K1a)
+  const uint32_t* tslot;       // [n_vals] table slot of each validator in atables, or null (slot = index)
 };
 
 #define TXV_PARK_WORDS 33          // X, Y, prefix product, Z of one parked vote; its vote index + 1
@@ -115,6 +116,9 @@ hipError_t txv_launch_rec_to_flow(const uint32_t* rec, const uint32_t* list, uin
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
+// the same, point pt's tables written to slot out_slot[pt] of `tables` (decode_ok / addr_words by pt)
+hipError_t txv_launch_build_tables_at(int w, const uint32_t* pubs_le, uint32_t n_points, const uint32_t* out_slot,
+                                      uint32_t* tables, uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
 bool txv_verify_windows_supported(int wb, int wa);
 hipError_t txv_launch_verify(int wb, int wa, const VerifyArgs* args, uint32_t grid, hipStream_t st);
 // the two halves of txv_launch_verify: K1a (challenge), then K1b (+ K1c in split mode)

@@ -123,6 +123,7 @@ def lib():
             "txv_copy_commit_bitmap": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "txv_table_window": ([vp], ctypes.c_int),
+            "txv_validator_tables_built": ([vp], ctypes.c_int),
             "txv_base_window": ([vp], ctypes.c_int),
             "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
             "txv_bind_host_numa": ([vp], ctypes.c_int),
@@ -192,7 +193,7 @@ EXPORTED_SYMBOLS = [
     "txv_get_validator_info", "txv_verify_batch", "txv_verify_bytes", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
-    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_base_window", "txv_sig_keys",
+    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_validator_tables_built", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
@@ -698,6 +699,11 @@ class Context:
     def table_w(self) -> int:
         """fixed-base window of the validator tables in use (0 before set_validators)"""
         return int(lib().txv_table_window(self._h))
+
+    @property
+    def tables_built(self) -> int:
+        """keys whose fixed-base tables the last set_validators built (the rest were kept)"""
+        return int(lib().txv_validator_tables_built(self._h))
 
     def reset_tally(self):
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")

@@ -9,17 +9,21 @@ batch: txflow/service.go:192-234 -> types/vote_set.go:81-166), optionally on a f
 At world > 1 every step's packed commit state -- written by the device into the slot's commit
 sink at the end of the step's TxFlow chain (txv_set_commit_sink) -- is all-gathered across
 ranks:
-  nccl (RCCL over xGMI): the all-gather is enqueued on the context's FLOW stream right behind
-        the step's chain (txv_flow_stream via torch.cuda.ExternalStream), so it reads the sink
-        after the pack, the next step's TxFlow chain (which rewrites nothing the gather reads
-        until the slot comes round again) queues behind it, and no host thread waits for it;
+  nccl (RCCL over xGMI): the all-gather runs on an exchange stream of its own, after an event
+        recorded on the context's FLOW stream (txv_flow_stream via torch.cuda.ExternalStream)
+        behind the step's chain, so it reads the sink after the pack while the next steps'
+        TxFlow chains go on -- a rank's chain does not wait for the other ranks (the collective
+        is the only cross-rank point); the flow stream waits for a slot's previous all-gather
+        only when that slot is launched again (its sink is rewritten then), and no host thread
+        waits for it;
   gloo  (CPU rehearsal): after the step's results are fetched (the sink is complete then), the
         sink goes to the host and is gathered there.
 Every slot has a gathered buffer of its own, so step k's all-gathered global state (the commit
 set and stakes of every shard as of step k, which the reference's per-vote commit side effects
 act on: txflow/service.go:216-232) survives steps k+1 .. k+depth-1 and is read after finish(k)
 by gathered_state(k) -- also while later steps are enqueued.  Over RCCL a timing event pair on
-the flow stream brackets each step's all-gather (exchange_ms: the per-step exchange cost).
+the exchange stream brackets each step's all-gather (exchange_ms: the per-step exchange cost,
+including the wait for the slowest rank).
 """
 from __future__ import annotations
 
@@ -51,6 +55,9 @@ class PipelinedSteps:
         self.slot_step = [-1] * depth       # the step whose gathered state slot sl holds
         self.finished = -1                  # newest step finished
         self._ev = None                     # RCCL: per slot, events around its step's all-gather
+        self._ready = None                  # RCCL: per slot, the step's chain done (flow stream)
+        self._xs = None                     # RCCL: the exchange stream
+        self._gathering = [False] * depth   # an all-gather of the slot was enqueued
         if dist is not None:
             import torch
             self.world = dist.get_world_size()
@@ -69,8 +76,12 @@ class PipelinedSteps:
                 self._ext = torch.cuda.ExternalStream(ctx.flow_stream(), device=f"cuda:{device}")
                 self._ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                             for _ in range(depth)]
+                self._ready = [torch.cuda.Event() for _ in range(depth)]
+                self._xs = torch.cuda.Stream(device=f"cuda:{device}")
 
     def close(self):
+        if self._xs is not None:
+            self._xs.synchronize()          # the all-gathers read the sinks
         if self.state is not None:
             for sl in range(self.depth):
                 self.ctx.set_commit_sink(sl, None)
@@ -78,19 +89,26 @@ class PipelinedSteps:
 
     def launch(self, k: int):
         """enqueue step k (a fresh TxFlow first, in flow-stream order after step k-1) and, over
-        RCCL, its commit-state all-gather on the flow stream behind it, into slot k % depth's
-        gathered buffer (step k - depth's state there was finished and read before)"""
+        RCCL, its commit-state all-gather on the exchange stream once the step's chain is done,
+        into slot k % depth's gathered buffer (step k - depth's state there was finished and
+        read before; its all-gather, which read the slot's sink, is done before the chain
+        rewrites the sink)"""
         sl = k % self.depth
+        if self._ext is not None and self._gathering[sl]:
+            self._ext.wait_event(self._ev[sl][1])
         if self.fresh:
             self.ctx.reset_flow()
         self.ctx.run_staged(sl)
         self.slot_step[sl] = k
         if self._ext is not None:
             import torch
-            with torch.cuda.stream(self._ext):
-                self._ev[sl][0].record(self._ext)
+            self._ready[sl].record(self._ext)
+            with torch.cuda.stream(self._xs):
+                self._xs.wait_event(self._ready[sl])
+                self._ev[sl][0].record(self._xs)
                 self.dist.all_gather_into_tensor(self.gathered[sl], self.state[sl])
-                self._ev[sl][1].record(self._ext)
+                self._ev[sl][1].record(self._xs)
+            self._gathering[sl] = True
 
     def finish(self, k: int):
         """statuses + commit events of step k (waits for its chain); gloo: gather its sink"""
@@ -136,14 +154,14 @@ class PipelinedSteps:
         return [commit_state_unpack(g[r], self.cap) for r in range(self.world)]
 
     def gathered_states(self) -> Optional[List[tuple]]:
-        """the newest finished step's gathered state (waits for the flow stream)"""
+        """the newest finished step's gathered state (waits for the flow stream and its all-gather)"""
         if self.gathered is None:
             return None
         self.ctx.sync()
         return self.gathered_state()
 
     def step_exchange_ms(self, k: int) -> Optional[float]:
-        """RCCL: device time of step k's all-gather on the flow stream (waits for it)"""
+        """RCCL: device time of step k's all-gather on the exchange stream (waits for it)"""
         if self._ev is None:
             return None
         sl = k % self.depth

@@ -92,8 +92,9 @@ typedef struct txv_ctx txv_ctx;
  *                      64 x 2 (max_txs + max_batch) B of set table + key_arena_bytes (1M sets x 100
  *                      validators: 1.2 + 8.6 + 0.3 + 0.1 GB)
  *   per batch slot     ~420 B x max_batch of device columns, ~170 B x max_batch pinned host memory
- * txv_set_validators rebuilds the validator tables on the device (K0: 0.9 s for 100 validators at
- * radix-2^20, once per validator set). */
+ * txv_set_validators builds the validator tables on the device (K0: 0.9 s for 100 validators at
+ * radix-2^20) for keys new to the context's table pool only; a set larger than the pool grows it
+ * by an eighth more slots (within table_budget_mb). */
 typedef struct {
   int32_t  device;          /* HIP device ordinal; -1 = current device */
   uint32_t max_batch;       /* votes per call (default 1<<20, at most 8<<20) */
@@ -165,7 +166,11 @@ const char* txv_last_error(txv_ctx* ctx);
 int  txv_device_name(txv_ctx* ctx, char* buf, uint32_t cap);
 
 /* Validator set + chain id.  pubs32: n x 32-byte ed25519 keys; powers: VotingPower.
- * Builds the per-validator tables on the device (K0).  Resets all tally state. */
+ * Builds the per-validator tables on the device (K0) for the keys that have none: the context
+ * keeps each key's tables in a slot of its table pool, so a set that re-orders, adds or drops
+ * validators rebuilds only the new keys (and keys that left come back without a rebuild while
+ * their slot was not reused).  Resets all tally state.  Replaces the validator set the
+ * reference's TxFlow passes to each new VoteSet (txflow/service.go:200-207). */
 int txv_set_validators(txv_ctx* ctx, const uint8_t* pubs32, const int64_t* powers, uint32_t n,
                        const char* chain_id, uint32_t chain_len);
 /* addresses (n x 20, SHA-256(pub)[:20] computed on device) and decode flags of the set */
@@ -321,6 +326,8 @@ int txv_copy_set_sums(txv_ctx* ctx, void* dst_dev, uint32_t n_sets);
 int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_ops_per_s);
 /* fixed-base window of the current validator tables (4..20), 0 before txv_set_validators */
 int txv_table_window(txv_ctx* ctx);
+/* keys whose tables the last txv_set_validators built (the others were already in the pool) */
+int txv_validator_tables_built(txv_ctx* ctx);
 /* window of the base-point table the verify kernel uses (>= the validator window) */
 int txv_base_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids

@@ -9,8 +9,9 @@
   step k is finished, and step k's gathered state (its slot's own buffer) is read then.  Every step's per-vote statuses + fired bits equal the
   sequential oracle's over the shard, and every rank's row of the gathered state equals the host
   pack of the owning rank's oracle state (so every rank holds the global committed set + stakes);
-  one rank (nccl = RCCL): the same path with the all-gather enqueued on the context's flow stream
-  through torch.cuda.ExternalStream (the bench's N>1 exchange), the gathered state equal to the
+  one rank (nccl = RCCL): the same path with the all-gather enqueued on an exchange stream after
+  an event on the context's flow stream (torch.cuda.ExternalStream; the bench's N>1 exchange),
+  the flow stream waiting for a slot's previous all-gather, the gathered state equal to the
   oracle's after every step.
 """
 import os

@@ -421,7 +421,8 @@ def test_device_signbytes_edge_fields(gpu_ctx, oracle_lib, chain):
 def test_set_validators_same_keys_new_powers(oracle_lib):
     """txv_set_validators with the keys of the current registry (same order) keeps the validator
     tables (no K0 rebuild) but takes the new powers and resets the TxFlow: the tally then follows
-    the new powers exactly (oracle with those powers), and a changed key set rebuilds."""
+    the new powers exactly (oracle with those powers); the same keys in another order keep their
+    tables too (the table pool, test_set_validators_incremental_tables)."""
     import time
     import txflow_amd as T
     rnd = random.Random(35)
@@ -444,12 +445,107 @@ def test_set_validators_same_keys_new_powers(oracle_lib):
             for v in votes:
                 assert ctx.query_tx(v.TxHash.encode()) == flow.query(v.TxHash.encode())
         assert ctx.total_power() == sum([1, 2, 3, 4, 5, 6, 7, 8])
-        # a different key order is a different registry: tables rebuilt, verdicts follow it
+        assert ctx.tables_built == 0
+        # a different key order is a different registry (validator indices move), tables kept
         ctx.set_validators(list(reversed(pubs)), [1] * 8, "test_chain_id")
+        assert ctx.tables_built == 0
         st, _ = ctx.add_votes(b)
         flow = oracle_lib.Flow(list(reversed(pubs)), [1] * 8, b"test_chain_id")
         ost, _, ofired = flow.add_votes(od)
         assert np.array_equal(st, ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7))
         print("set_validators seconds:", [round(t, 4) for t in times])
+    finally:
+        ctx.close()
+
+
+def _pool_model(slots, gens, gen, keys, budget_slots):
+    """the table pool's slot policy (runtime.cpp assign_tables) in Python: returns the number of
+    keys K0 builds for the set `keys` and updates slots / gens in place"""
+    taken = [False] * len(slots)
+    held = {k: i for i, k in enumerate(slots) if k is not None}
+    vs = [None] * len(keys)
+    for i, k in enumerate(keys):
+        s = held.get(k)
+        if s is not None and not taken[s]:
+            vs[i], taken[s] = s, True
+    if len(keys) > len(slots):
+        cap = max(len(keys), min(budget_slots, len(keys) + max(1, len(keys) // 8))) if slots else len(keys)
+        kept = [s for s in range(len(slots)) if taken[s]]
+        if kept:
+            moved = {s: j for j, s in enumerate(kept)}
+            new = [slots[s] for s in kept] + [None] * (cap - len(kept))
+            slots[:] = new
+            gens[:] = [0] * cap
+            vs = [moved[v] if v is not None else None for v in vs]
+            taken = [j < len(kept) for j in range(cap)]
+        else:
+            slots[:] = [None] * cap
+            gens[:] = [0] * cap
+            vs = [None] * len(keys)
+            taken = [False] * cap
+    free = sorted((s for s in range(len(slots)) if not taken[s]), key=lambda s: (slots[s] is not None, gens[s]))
+    miss = [i for i in range(len(keys)) if vs[i] is None]
+    for i, s in zip(miss, free):
+        vs[i], slots[s] = s, keys[i]
+    for s in vs:
+        gens[s] = gen
+    return len(miss)
+
+
+def test_set_validators_incremental_tables(oracle_lib):
+    """txv_set_validators keeps each key's tables in a slot of the context's pool: a new set that
+    re-orders, drops, adds (growing the pool) or brings back validators builds K0 only for keys
+    no slot holds (counted by txv_validator_tables_built, predicted by a model of the slot
+    policy), and every set's verdicts -- votes of its validators, of validators outside it and
+    with corrupted signatures -- equal the oracle TxFlow's for that set."""
+    import hashlib
+    import time
+
+    import txflow_amd as T
+    rnd = random.Random(36)
+    ctx = T.Context(max_batch=1 << 14, max_txs=512, max_validators=24)
+    try:
+        seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(14)]
+        pubs = ctx.keygen(seeds)
+        addr = [hashlib.sha256(p).digest()[:20] for p in pubs]
+        hashes = ["".join(rnd.choice("0123456789ABCDEF") for _ in range(64)) for _ in range(30)]
+        sets = [list(range(8)), list(range(7, -1, -1)), [0, 1, 2, 3, 4, 5, 8, 9], [0, 1, 2, 3, 4, 5, 8, 9, 6],
+                [9, 8, 6, 5, 4, 3, 2, 1, 0, 7], [3, 1, 10, 11], list(range(10)), [12, 13] + list(range(10)),
+                [13, 0]]
+        slots, gens = [], []
+        budget_slots = (112 << 30) // int(_table_mb(20) * 2 ** 20)
+        times = []
+        for gen, ks in enumerate(sets, 1):
+            powers = [1 + (k % 4) for k in ks]
+            t0 = time.perf_counter()
+            ctx.set_validators([pubs[k] for k in ks], powers, "test_chain_id")
+            times.append(round(time.perf_counter() - t0, 4))
+            exp_built = _pool_model(slots, gens, gen, [pubs[k] for k in ks], budget_slots)
+            assert ctx.tables_built == exp_built, (gen, ks, ctx.tables_built, exp_built)
+            got_addr, ok = ctx.validator_info()
+            assert ok.all() and [bytes(a) for a in got_addr] == [addr[k] for k in ks]
+            votes, signer = [], []
+            for i in range(900):
+                k = rnd.choice(ks) if i % 9 else rnd.randrange(14)        # some from outside the set
+                votes.append(T.TxVote(Height=1, TxHash=rnd.choice(hashes), Timestamp=(1_700_000_000, i + 1),
+                                      ValidatorAddress=addr[k], Signature=b""))
+                signer.append(k)
+            ctx.keygen(seeds)                                         # sign with key index k
+            sigs = ctx.sign_votes(T.VoteBatch.from_votes(votes), np.array(signer, np.uint32), "test_chain_id")
+            for i, (v, s) in enumerate(zip(votes, sigs)):
+                s = bytearray(s.tobytes())
+                if i % 11 == 3:
+                    s[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+                v.Signature = bytes(s)
+            st, _ = ctx.add_votes(T.VoteBatch.from_votes(votes))
+            flow = oracle_lib.Flow([pubs[k] for k in ks], powers, b"test_chain_id")
+            od = [dict(height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0], ts_nanos=v.Timestamp[1],
+                       addr=v.ValidatorAddress, sig=v.Signature) for v in votes]
+            ost, _, ofired = flow.add_votes(od)
+            exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+            bad = np.nonzero(st != exp)[0]
+            assert len(bad) == 0, (gen, [(int(i), int(st[i]), int(exp[i])) for i in bad[:10]])
+            assert ((st & 0x7F) == T.ADDED).sum() >= 2 * len(ks)
+        print("set_validators seconds:", times, "slots:", len(slots))
     finally:
         ctx.close()
