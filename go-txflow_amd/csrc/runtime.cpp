@@ -1400,14 +1400,24 @@ int assign_tables(txv_ctx* c, const uint8_t* pubs32, uint32_t n, int w) {
       uint32_t j = 0;
       for (uint32_t sl = 0; sl < c->tab_slots; ++sl) {
         if (!taken[sl]) continue;
-        HIP_TRY(c, hipMemcpyAsync(np + (size_t)j * words, c->d_atables + (size_t)sl * words, words * 4,
-                                  hipMemcpyDeviceToDevice, c->stream));
+        const hipError_t e = hipMemcpyAsync(np + (size_t)j * words, c->d_atables + (size_t)sl * words, words * 4,
+                                            hipMemcpyDeviceToDevice, c->stream);
+        if (e != hipSuccess) {
+          (void)hipStreamSynchronize(c->stream);
+          (void)hipFree(np);
+          c->err = std::string("table pool copy: ") + hipGetErrorString(e);
+          return TXV_EDEVICE;
+        }
         key[j] = c->slot_key[sl];
         ok[j] = c->slot_ok[sl];
         memcpy(&addr[(size_t)j * 20], &c->slot_addr[(size_t)sl * 20], 20);
         moved[sl] = j++;
       }
-      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      if (const hipError_t e = hipStreamSynchronize(c->stream); e != hipSuccess) {
+        (void)hipFree(np);
+        c->err = std::string("table pool copy: ") + hipGetErrorString(e);
+        return TXV_EDEVICE;
+      }
       (void)hipFree(c->d_atables);
       c->d_atables = np;
       c->tab_slots = cap;

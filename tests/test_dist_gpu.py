@@ -156,7 +156,7 @@ def test_two_ranks_one_gpu_sharded_steps_match_oracle():
         assert by[1] > 0 and by[5] > 0 and by[6] > 0, by
 
 
-def test_one_rank_rccl_exchange_on_flow_stream():
+def test_one_rank_rccl_exchange_stream():
     res, codes = _run(1, "nccl")
     errs = [e for _, es, _, _ in res for e in es]
     assert not errs, "\n".join(errs)
