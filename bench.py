@@ -148,11 +148,9 @@ def end_to_end_leg(ctx, wl, steps: int, registered: bool):
         for a in cols:
             ctx.host_register(a)
     col_bytes = sum(a.nbytes for a in cols)
-    # the library fills uniform height / seconds / length columns on the device instead of
-    # uploading them (txv_submit_votes staging)
-    skipped = sum(a.nbytes for a in (b.height, b.ts_sec, b.txhash_len, b.addr_len, b.sig_len)
-                  if a.size and bool((a == a[0]).all()))
-    up_bytes = col_bytes - skipped
+    # the library fills uniform height / seconds / length columns on the device and decodes the
+    # TxKey column from the TxHashes that spell it instead of uploading them (txv_staged_bytes)
+    up_bytes = None
     inflight, lat, ok = [], [], True
     st_buf = None
 
@@ -166,6 +164,7 @@ def end_to_end_leg(ctx, wl, steps: int, registered: bool):
     for _ in range(2):                      # warm-up: first touch of the staging buffers
         ctx.reset_flow()
         inflight.append((time.perf_counter(), ctx.submit_votes(b)))
+        up_bytes = ctx.staged_bytes()
         drain()
     lat.clear()
     ctx.sync()

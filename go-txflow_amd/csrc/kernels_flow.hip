@@ -1000,6 +1000,43 @@ __global__ void __launch_bounds__(256) txv_k_fill64(uint64_t* dst, uint64_t v, u
   if (i < n) dst[i] = v;
 }
 
+// TxKey from TxHash: a batch whose every non-nil vote carries TxKey == the 32 bytes its 64-char
+// upper-hex TxHash spells (TxKey = SHA-256(tx), TxHash = %X of the same digest,
+// types/tx_vote.go:38-45; the host checked it, txv_submit_votes' staging) does not upload the
+// TxKey column: each vote's key is decoded here from the TxHash arena, 8 hex chars per load
+__device__ __forceinline__ uint32_t hex_nibbles8(uint64_t c) {   // 8 chars of [0-9A-F] -> 4 bytes in order
+  uint32_t out = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t ch = (uint32_t)(c >> (8 * k)) & 0xFFu;
+    const uint32_t nib = ch <= '9' ? ch - '0' : ch - 'A' + 10u;
+    out |= nib << ((k & 1) ? 8 * (k >> 1) : 8 * (k >> 1) + 4);
+  }
+  return out;
+}
+
+__global__ void __launch_bounds__(256) txv_k_txkey_from_hash(const uint8_t* th, const uint32_t* off, const uint8_t* nil,
+                                                             uint32_t n, uint8_t* txkey) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!(nil && nil[i])) {
+    const uint8_t* p = th + off[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = hex_nibbles8(ld64u(p + 8 * k));
+  }
+  uint4* d = reinterpret_cast<uint4*>(txkey + (size_t)i * 32);
+  d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+hipError_t txv_txkey_from_hash(const uint8_t* th, const uint32_t* off, const uint8_t* nil, uint32_t n, uint8_t* txkey,
+                               hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_txkey_from_hash, dim3((n + 255) / 256), dim3(256), 0, st, th, off, nil, n, txkey);
+  return hipGetLastError();
+}
+
 hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(txv_k_fill64, dim3((n + 255) / 256), dim3(256), 0, st, dst, v, n);

@@ -191,6 +191,8 @@ struct txv_ctx {
   std::unique_ptr<txv_host::WorkerPool> pool;   // host pack threads
   bool profile_host = false;                    // TXV_PROFILE_HOST
   bool uniform_cols = true;                     // uniform columns filled on the device (TXV_UNIFORM_COLS=0: off)
+  bool derive_txkey = true;                     // TxKey decoded from TxHash on the device when it spells it (TXV_DERIVE_TXKEY=0: off)
+  uint64_t staged_bytes = 0;                    // host bytes the last staged batch moved over PCIe
   // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
   // accepted-vote arena, counters
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
@@ -670,6 +672,21 @@ bool is_registered(const txv_ctx* c, const void* p, uint64_t bytes) {
 // bound).  Registered columns are DMA'd straight from caller memory; the others are copied into
 // the slot's pinned buffers chunk by chunk on the pack threads, each chunk's DMA queued as soon
 // as it is copied, so copies and PCIe transfers overlap.
+// TxKey = SHA-256(tx), TxHash = its upper-hex digest (types/tx_vote.go:38-45): true when the key
+// is the 32 bytes the 64 characters at hex spell
+inline bool txkey_spelled(const uint8_t* key, const uint8_t* hex) {
+  static const struct Tab {
+    uint16_t e[256];
+    Tab() {
+      const char* h = "0123456789ABCDEF";
+      for (int b = 0; b < 256; ++b) e[b] = (uint16_t)((uint8_t)h[b >> 4] | (uint16_t)(uint8_t)h[b & 15] << 8);
+    }
+  } tab;
+  uint16_t enc[32];
+  for (int j = 0; j < 32; ++j) enc[j] = tab.e[key[j]];
+  return memcmp(enc, hex, 64) == 0;
+}
+
 int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
@@ -686,6 +703,10 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   std::atomic<uint32_t> varying{0};
   const bool check_uniform = n > 0 && c->uniform_cols && v->height && v->ts_sec && v->txhash_len && v->addr_len &&
                              v->sig_len;
+  // the TxKey column is decoded from the TxHash arena on the device when every non-nil vote's
+  // key is what its TxHash spells (32 of a vote's bytes)
+  const bool check_key = n > 0 && c->derive_txkey && v->txkey && v->txhash && v->txhash_off && v->txhash_len;
+  std::atomic<bool> key_differs{false};
   c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
     uint64_t ae = 0;
     uint32_t mh = 0, var = 0;
@@ -701,6 +722,15 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
                (uint32_t)(v->addr_len[i] != v->addr_len[0]) << kUAL | (uint32_t)(v->sig_len[i] != v->sig_len[0]) << kUSL;
       }
       if (var) varying.fetch_or(var);
+    }
+    if (check_key && !key_differs.load(std::memory_order_relaxed)) {
+      for (uint32_t i = lo; i < hi; ++i) {
+        if (v->is_nil && v->is_nil[i]) continue;
+        if (v->txhash_len[i] != 64 || !txkey_spelled(v->txkey + (size_t)i * 32, v->txhash + v->txhash_off[i])) {
+          key_differs.store(true, std::memory_order_relaxed);
+          break;
+        }
+      }
     }
     uint64_t ca = arena_end.load();
     while (ae > ca && !arena_end.compare_exchange_weak(ca, ae)) {}
@@ -741,7 +771,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   add(v->sig, s.h_sigraw, s.d_sigraw, 64);
   add((uniform >> kUSL & 1) ? nullptr : v->sig_len, s.h_sig_len, s.d_sig_len, 4);
   add(v->is_nil, s.h_nil, s.d_nil, 1);
-  add(v->txkey, s.h_txkey, s.d_txkey, 32);
+  const bool derive_key = check_key && !key_differs.load();
+  add(derive_key ? nullptr : v->txkey, s.h_txkey, s.d_txkey, 32);
   if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));   // its last chain has ended
   if (uniform >> kUH & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fh), (uint64_t)v->height[0], n, c->copy_stream));
   if (uniform >> kUS & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fs), (uint64_t)v->ts_sec[0], n, c->copy_stream));
@@ -785,6 +816,13 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (!arena_reg) {
     memset(s.h_arena + ae, 0, 16);
     HIP_TRY(c, hipMemcpyAsync(s.d_arena_th + ae, s.h_arena + ae, 16, hipMemcpyHostToDevice, c->copy_stream));
+  }
+  if (derive_key)
+    HIP_TRY(c, txv_txkey_from_hash(s.d_arena_th, s.d_fo, s.has_nil ? s.d_nil : nullptr, n, s.d_txkey, c->copy_stream));
+  {
+    uint64_t up = ae + 16;
+    for (int k = 0; k < nc; ++k) up += (uint64_t)n * cols[k].elem;
+    c->staged_bytes = up;
   }
   HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
   ht.mark("upload");
@@ -1284,6 +1322,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     c->pool.reset(new txv_host::WorkerPool(nt));
     c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
     c->uniform_cols = !(getenv("TXV_UNIFORM_COLS") && atoi(getenv("TXV_UNIFORM_COLS")) == 0);
+    c->derive_txkey = !(getenv("TXV_DERIVE_TXKEY") && atoi(getenv("TXV_DERIVE_TXKEY")) == 0);
   }
   *out = c;
   return TXV_OK;
@@ -2458,6 +2497,7 @@ int txv_valu_probe(txv_ctx* c, double* add_lane_ops_per_s, double* mad_lane_ops_
 
 int txv_table_window(txv_ctx* c) { return c ? c->tab_w : TXV_EINVAL; }
 int txv_validator_tables_built(txv_ctx* c) { return c ? (int)c->tables_built : TXV_EINVAL; }
+int64_t txv_staged_bytes(txv_ctx* c) { return c ? (int64_t)c->staged_bytes : TXV_EINVAL; }
 int txv_base_window(txv_ctx* c) { return c ? c->b_w : TXV_EINVAL; }
 
 int txv_fe_selftest(txv_ctx* c, const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op) {

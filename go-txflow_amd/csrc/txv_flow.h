@@ -195,6 +195,9 @@ hipError_t txv_flow_reset(const FlowState* fs, int keep_ids, hipStream_t st);
 // with clear_acc the accepted votes too
 hipError_t txv_flow_init_cells(const FlowState* fs, uint64_t cells, int clear_acc, hipStream_t st);
 hipError_t txv_fill64(uint64_t* dst, uint64_t v, uint32_t n, hipStream_t st);
+// txkey[i] = the 32 bytes the 64-char upper-hex TxHash of vote i spells (zero for nil votes)
+hipError_t txv_txkey_from_hash(const uint8_t* th, const uint32_t* off, const uint8_t* nil, uint32_t n, uint8_t* txkey,
+                               hipStream_t st);
 // TxHash lookups for the readers: out_id[i] = set id or TXV_NONE
 hipError_t txv_flow_lookup(const FlowState* fs, const uint8_t* keys, const uint32_t* off, const uint32_t* len,
                            uint32_t n, uint32_t* out_id, hipStream_t st);

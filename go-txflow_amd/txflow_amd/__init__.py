@@ -124,6 +124,7 @@ def lib():
             "txv_valu_probe": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "txv_table_window": ([vp], ctypes.c_int),
             "txv_validator_tables_built": ([vp], ctypes.c_int),
+            "txv_staged_bytes": ([vp], ctypes.c_int64),
             "txv_base_window": ([vp], ctypes.c_int),
             "txv_sig_keys": ([vp, ctypes.POINTER(_Votes), vp, vp, vp], ctypes.c_int),
             "txv_bind_host_numa": ([vp], ctypes.c_int),
@@ -193,7 +194,7 @@ EXPORTED_SYMBOLS = [
     "txv_get_validator_info", "txv_verify_batch", "txv_verify_bytes", "txv_add_votes", "txv_query_tx", "txv_num_tx_sets",
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
-    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_validator_tables_built", "txv_base_window", "txv_sig_keys",
+    "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_validator_tables_built", "txv_staged_bytes", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
@@ -699,6 +700,11 @@ class Context:
     def table_w(self) -> int:
         """fixed-base window of the validator tables in use (0 before set_validators)"""
         return int(lib().txv_table_window(self._h))
+
+    def staged_bytes(self) -> int:
+        """host bytes the last staged batch sent over PCIe (uniform columns and a TxKey column
+        its TxHashes spell are produced on the device instead)"""
+        return int(lib().txv_staged_bytes(self._h))
 
     @property
     def tables_built(self) -> int:

@@ -328,6 +328,11 @@ int txv_valu_probe(txv_ctx* ctx, double* add_lane_ops_per_s, double* mad_lane_op
 int txv_table_window(txv_ctx* ctx);
 /* keys whose tables the last txv_set_validators built (the others were already in the pool) */
 int txv_validator_tables_built(txv_ctx* ctx);
+/* host bytes the last staged batch (txv_stage / txv_submit_votes / txv_add_votes) sent over
+ * PCIe: columns whose every element is equal are filled on the device instead, and the TxKey
+ * column is decoded on the device from TxHash when every non-nil vote's TxKey is the 32 bytes its
+ * 64-character upper-hex TxHash spells (TxKey = SHA-256(tx), TxHash = its %X, types/tx_vote.go:38-45) */
+int64_t txv_staged_bytes(txv_ctx* ctx);
 /* window of the base-point table the verify kernel uses (>= the validator window) */
 int txv_base_window(txv_ctx* ctx);
 /* empty every TxVoteSet (votes, stake, commit flags) keeping the validator set; tx-set ids

@@ -327,6 +327,81 @@ def test_make_commit_and_save_tx_match_oracle(oracle_lib):
         ctx.close()
 
 
+def test_txkey_spelled_by_txhash_is_not_uploaded(oracle_lib):
+    """TxKey = SHA-256(tx) and TxHash = its upper-hex %X (types/tx_vote.go:38-45): a batch whose
+    every non-nil vote's TxKey is the 32 bytes its TxHash spells does not upload the TxKey column
+    (txv_staged_bytes: exactly 32 B per vote less), the device decodes it from the TxHash arena;
+    one vote whose TxKey differs (or a lower-case TxHash) uploads the column.  Either way the
+    statuses, each set's first-vote TxKey, MakeCommit and SaveTx bytes (every accepted vote's own
+    TxKey) equal the oracle's."""
+    import txflow_amd as T
+    rnd = random.Random(23)
+    n_vals = 5
+    ctx = T.Context(max_batch=1 << 14, max_txs=1024, max_validators=8)
+    try:
+        seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(n_vals)]
+        pubs = ctx.keygen(seeds)
+        powers = [1] * n_vals
+        ctx.set_validators(pubs, powers, "test_chain_id")
+        addrs, _ = ctx.validator_info()
+        hashes = ["%064X" % rnd.getrandbits(256) for _ in range(24)]
+        votes, signer = [], []
+        for i in range(600):
+            v = rnd.randrange(n_vals)
+            h = rnd.choice(hashes)
+            if 300 <= i < 450 and i % 40 == 3:
+                h = h.lower()                                 # batch 3: TxHashes in lower case
+            votes.append(T.TxVote(Height=1, TxHash=h, TxKey=bytes.fromhex(h),
+                                  Timestamp=(1_700_000_000, rnd.randrange(0, 10 ** 9)), ValidatorAddress=addrs[v]))
+            signer.append(v)
+        sigs = ctx.sign_votes(T.VoteBatch.from_votes(votes), np.array(signer, np.uint32), "test_chain_id")
+        for v, s in zip(votes, sigs):
+            v.Signature = s.tobytes()
+        for i in range(600):
+            if (i % 150) % 37 == 0:
+                votes[i] = None                               # nil votes carry no TxKey
+        votes[150 + 7].TxKey = bytes(rnd.getrandbits(8) for _ in range(32))   # batch 2: one differs
+        flow = oracle_lib.Flow(pubs, powers, b"test_chain_id")
+        staged = []
+        parts = (votes[:150], votes[150:300], votes[300:450], votes[450:])
+        for part in parts:
+            st, _ = ctx.add_votes(T.VoteBatch.from_votes(part))
+            staged.append(ctx.staged_bytes())
+            ost, _, ofired = flow.add_votes([dict(nil=True) if v is None else dict(
+                height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0], ts_nanos=v.Timestamp[1],
+                addr=v.ValidatorAddress, sig=v.Signature) for v in part])
+            assert np.array_equal(st, _expected(ost, ofired))
+        # the four batches have the same shape: only the TxKey column comes and goes
+        assert staged[3] == staged[0] and staged[1] == staged[2] == staged[0] + 32 * 150, staged
+        allv = [v for p in parts for v in p if v is not None]
+        first_key, by_sig = {}, {}
+        for v in allv:
+            first_key.setdefault(v.TxHash, v.TxKey)
+            by_sig.setdefault((v.TxHash, v.Signature), v)
+        n_commit = 0
+        for h in sorted({v.TxHash for v in allv}):
+            hb = h.encode()
+            q = flow.query(hb)
+            ex, _, _, tk = ctx.query_txs([hb])
+            if q is None:
+                assert not ex[0]
+                continue
+            assert tk[0].tobytes() == first_key[h]
+            if not q[1]:
+                continue
+            n_commit += 1
+            acc = []
+            for val, sig in flow.get_votes(hb):
+                v = by_sig[(h, sig)]
+                acc.append(dict(height=v.Height, ts_sec=v.Timestamp[0], ts_nanos=v.Timestamp[1], addr=addrs[val],
+                                sig=sig, txkey=v.TxKey))
+            assert ctx.make_commit(hb) == oracle_lib.commit_bytes(hb, acc)
+            assert ctx.save_tx_bytes(hb) == oracle_lib.save_tx_bytes(hb, first_key[h], acc)
+        assert n_commit > 10
+    finally:
+        ctx.close()
+
+
 def test_lane_votes_8_without_the_wide_base_table(oracle_lib):
     """A configured V = 8 runs the V = 4 kernel whenever the base table is not the radix-2^24 one
     (small windows, caller-supplied keys): verdicts equal the oracle's."""
