@@ -16,7 +16,7 @@ enqueued): step k+1's verify chain runs while step k's TxFlow chain tallies, as 
 batches of a node do.  value = votes processed by all ranks / max-over-ranks time.
 
 Beside it: the end-to-end rate from the caller's host SoA columns (txv_submit_votes /
-txv_wait_votes, two batches in flight: staging copy + PCIe upload + kernels + results), the
+txv_wait_votes, three batches in flight: staging copy + PCIe upload + kernels + results), the
 CPU baseline (the oracle's C restatement on every allowed host core, and 1 thread), the
 TxVoteMessage wire-decode leg and the C5 streaming leg.
 
@@ -138,8 +138,9 @@ def c1_leg(device: int, threads: int):
 
 
 def end_to_end_leg(ctx, wl, steps: int, registered: bool):
-    """Host SoA -> statuses + commit events: txv_reset_flow + txv_submit_votes per step, two steps
-    in flight (step k+1's staging copy and upload overlap step k's kernels), txv_wait_votes."""
+    """Host SoA -> statuses + commit events: txv_reset_flow + txv_submit_votes per step, three steps
+    in flight (step k+1's upload overlaps step k's kernels, step k+2's host pass and staging copy
+    step k+1's upload), txv_wait_votes."""
     import txflow_amd as T
     b = wl.batch
     cols = [b.height, b.ts_sec, b.ts_nanos, b.txhash_off, b.txhash_len, b.addr, b.addr_len, b.sig, b.sig_len,
@@ -171,7 +172,7 @@ def end_to_end_leg(ctx, wl, steps: int, registered: bool):
     t0 = time.perf_counter()
     for _ in range(steps):
         ctx.reset_flow()
-        if len(inflight) == 2:
+        if len(inflight) == T.SUBMIT_RING:
             drain()
         inflight.append((time.perf_counter(), ctx.submit_votes(b)))
     while inflight:
@@ -308,8 +309,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                     st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
                     te = time.perf_counter()
                     if rep == 2:                  # the batch's stage times, before its ring slot is reused
-                        dev_ms.append(ctx.slot_kernel_ms((tk - 1) % 2))
-                        sp = verify_split(ctx, (tk - 1) % 2)
+                        dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
+                        sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
                         if sp:
                             dev_split.append(sp)
                     slots.release()
@@ -926,7 +927,7 @@ def main():
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = {
                 "note": "host SoA columns -> statuses + commit events (staging copy, PCIe upload, kernels, "
-                        "results), txv_submit_votes/txv_wait_votes with two steps in flight",
+                        "results), txv_submit_votes/txv_wait_votes with three steps in flight",
                 "pageable": end_to_end_leg(ctx, wl, max(3, args.steps), registered=False),
                 "registered": end_to_end_leg(ctx, wl, max(3, args.steps), registered=True)}
         if world == 1 and not args.no_wire:

@@ -53,7 +53,8 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #ifndef TXV_K1A_ON_KEY_STREAM
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
-constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0, 1 also the submit ring)
+constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0-2 also the submit ring)
+constexpr uint32_t kSubmitRing = 3;    // txv_submit_votes batches in flight
 constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6-8)
 constexpr uint32_t kIngestRing = 3;
 constexpr uint32_t kSlots = kIngestSlot + kIngestRing;
@@ -143,7 +144,7 @@ struct txv_ctx {
   bool tally_ev_set = false;
   hipEvent_t vend_ev[4] = {};           // TXV_PREP_AFTER_K1B: the last batches' K1b ends (verify stream)
   uint64_t vend_n = 0;
-  uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 and 1
+  uint64_t next_ticket = 1;            // txv_submit_votes ring over slots 0 .. kSubmitRing - 1
   ErrMsg err;
   std::mutex mu;
   // validator registry
@@ -1202,13 +1203,16 @@ int run_verify(txv_ctx* c, Slot& s, const KeySet& ks, std::vector<uint8_t>& ok) 
   return TXV_OK;
 }
 
-// txv_submit_votes ring: ticket t runs in slot (t - 1) % 2; a slot is reused only after
-// its ticket was waited for (its pinned and device buffers are free again)
+// txv_submit_votes ring: ticket t runs in slot (t - 1) % kSubmitRing; a slot is reused only
+// after its ticket was waited for (its pinned and device buffers are free again).  Three slots:
+// batch k+2's host pass and staging run while batch k+1 uploads and batch k computes, so the
+// host pass does not leave the link idle between uploads (two slots: 428.5M votes/s end to end,
+// the host pass between a wait and the next upload)
 int submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
   const uint64_t t = c->next_ticket;
-  const uint32_t slot = (uint32_t)((t - 1) % 2);
+  const uint32_t slot = (uint32_t)((t - 1) % kSubmitRing);
   Slot& s = c->slots[slot];
-  if (s.ticket) { c->err = "two batches already in flight: wait for the older one first"; return TXV_ESTATE; }
+  if (s.ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
   int r;
   if ((r = stage_add(c, slot, v))) return r;
   if ((r = run_slot(c, slot, nullptr))) return r;
@@ -1221,15 +1225,16 @@ int submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
 int wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_event* ev, uint32_t ev_cap,
                uint32_t* n_ev) {
   if (!ticket) return TXV_EINVAL;
-  Slot& s = c->slots[(ticket - 1) % 2];
+  const uint32_t slot = (uint32_t)((ticket - 1) % kSubmitRing);
+  Slot& s = c->slots[slot];
   if (s.ticket != ticket) { c->err = "unknown or already waited ticket"; return TXV_ESTATE; }
-  const uint32_t other = (uint32_t)(ticket % 2);   // the other ring slot
-  if (c->slots[other].ticket && c->slots[other].ticket < ticket) {
-    c->err = "tickets must be waited in submission order";
-    return TXV_ESTATE;
-  }
+  for (uint32_t o = 0; o < kSubmitRing; ++o)   // the other ring slots
+    if (o != slot && c->slots[o].ticket && c->slots[o].ticket < ticket) {
+      c->err = "tickets must be waited in submission order";
+      return TXV_ESTATE;
+    }
   s.ticket = 0;
-  return fetch_slot(c, (uint32_t)((ticket - 1) % 2), status_out, ev, ev_cap, n_ev);
+  return fetch_slot(c, slot, status_out, ev, ev_cap, n_ev);
 }
 
 // The context's four streams.  Experiment knobs (environment, read once per context):
@@ -1716,7 +1721,7 @@ int txv_wait_votes(txv_ctx* c, uint64_t ticket, uint8_t* status_out, txv_commit_
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device));
     if (ticket) {
-      const Slot& s = c->slots[(ticket - 1) % 2];
+      const Slot& s = c->slots[(ticket - 1) % kSubmitRing];
       if (s.ticket == ticket && s.ran) done = s.ev[4];
     }
   }

@@ -532,13 +532,14 @@ class Context:
         return t.value
 
     def wait_votes(self, ticket: int, ev_cap: int = 0):
-        n = self._inflight.pop(ticket)
+        n = getattr(self, "_inflight", {}).get(ticket, 0)   # kept until the library took the ticket
         out = np.zeros(max(n, 1), np.uint8)
         ev_cap = ev_cap or max(n, 1)
         evs = np.zeros(ev_cap, EVENT_DTYPE)
         nev = ctypes.c_uint32()
         self._chk(lib().txv_wait_votes(self._h, ticket, out.ctypes.data, evs.ctypes.data, ev_cap, ctypes.byref(nev)),
                   "txv_wait_votes")
+        self._inflight.pop(ticket, None)
         return out[:n], evs[:min(nev.value, ev_cap)]
 
     def get_votes(self, txhash: bytes):
@@ -840,6 +841,7 @@ class IngestTicket:
         self.ticket, self.n, self.wire_status, self.pool_status = ticket, n, ws, ps
 POOL_NO_CACHE = 0xFFFFFFFF
 POOL_WAL = 0x1      # TXV_POOL_WAL
+SUBMIT_RING = 3         # txv_submit_votes batches in flight (staged slots 0 .. 2)
 POOL_DEVICE_CACHE = 0x2   # TXV_POOL_DEVICE_CACHE: the LRU cache in HBM, CheckTx decisions on the GPU
 
 

@@ -206,8 +206,10 @@ int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
  * txv_submit_votes copies the batch's columns into pinned memory (registered columns: none),
  * queues their upload on the copy stream and the kernel chain on the compute stream, and returns
  * a ticket without waiting; txv_wait_votes(ticket) waits for the results and reports exactly what
- * txv_add_votes would have.  At most two batches may be in flight; tickets are waited in
- * submission order.  The staging of batch k+1 and its upload overlap the kernels of batch k.
+ * txv_add_votes would have.  At most three batches may be in flight (they share staged slots
+ * 0-2 with txv_stage / txv_run_staged: do not mix the two on one context at the same time);
+ * tickets are waited in submission order.  The staging of batch k+1 and its upload overlap the
+ * kernels of batch k, and the staging of batch k+2 the upload of batch k+1.
  * Registered columns (txv_host_register) are read by DMA until txv_wait_votes returns for the
  * ticket; other caller buffers may be reused as soon as txv_submit_votes returns.  The TxVoteSet
  * readers (txv_query_tx*, txv_get_votes, txv_make_commit, ...) run after every submitted batch. */

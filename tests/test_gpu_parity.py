@@ -329,10 +329,10 @@ def test_c4_adversarial_stream_gate(oracle_lib):
 
 
 def test_pipelined_submit_wait_matches_oracle(oracle_lib):
-    """txv_submit_votes / txv_wait_votes with two batches in flight (uploads on the copy stream
+    """txv_submit_votes / txv_wait_votes with three batches in flight (uploads on the copy stream
     overlapping the previous batch's kernels) give exactly the sequential oracle's per-vote
     codes, fire bits and per-tx sums on a C4 adversarial stream (replays / conflicts across
-    batches); waiting out of order is refused."""
+    batches); a fourth batch in flight and waiting out of order are refused."""
     import adversarial as A
     import txflow_amd as T
     ctx = T.Context(max_batch=1 << 16, max_txs=1 << 14, max_validators=256)
@@ -345,12 +345,14 @@ def test_pipelined_submit_wait_matches_oracle(oracle_lib):
             exp.append(st.astype(np.uint8) | (fired.astype(np.uint8) << 7))
         got, inflight = [], []
         for b in batches:
-            if len(inflight) == 2:
+            if len(inflight) == T.SUBMIT_RING:
                 got.append(ctx.wait_votes(inflight.pop(0))[0])
             inflight.append(ctx.submit_votes(b))
-            if len(inflight) == 2 and len(got) == 0:
+            if len(inflight) == T.SUBMIT_RING and len(got) == 0:
                 with pytest.raises(T.TxvInfraError):
-                    ctx.submit_votes(b)          # a third batch in flight is refused
+                    ctx.submit_votes(b)          # a fourth batch in flight is refused
+                with pytest.raises(T.TxvInfraError):
+                    ctx.wait_votes(inflight[1])  # out of order
         while inflight:
             got.append(ctx.wait_votes(inflight.pop(0))[0])
         for g, e in zip(got, exp):
