@@ -297,10 +297,15 @@ __global__ void __launch_bounds__(256) txv_k_route_prep(FlowState fs, FlowBatch 
     return;
   }
   // AddVote pre-checks (types/vote_set.go:93-106)
-  const uint32_t al = b.addr_len[i];
   uint32_t v = TXV_NONE;
   uint8_t pre = TXV_S_PENDING;
-  if (al == 0) {
+  const uint32_t al = b.vcode ? 0u : b.addr_len[i];
+  if (b.vcode) {                             // looked up on the host (txv_submit_votes staging)
+    const uint32_t code = b.vcode[i];
+    if (code == TXV_VCODE_EMPTY) pre = TXV_S_EMPTY_ADDR;
+    else if (code == TXV_VCODE_UNKNOWN) pre = TXV_S_UNKNOWN_VALIDATOR;
+    else v = code;
+  } else if (al == 0) {
     pre = TXV_S_EMPTY_ADDR;
   } else if (al == 20) {
     const uint32_t* ap = reinterpret_cast<const uint32_t*>(b.addr + (size_t)i * 20);

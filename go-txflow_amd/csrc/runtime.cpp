@@ -55,6 +55,7 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 #endif
 constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0-2 also the submit ring)
 constexpr uint32_t kSubmitRing = 3;    // txv_submit_votes batches in flight
+constexpr uint32_t kVcodeEmpty = TXV_VCODE_EMPTY, kVcodeUnknown = TXV_VCODE_UNKNOWN;   // txv_flow.h
 constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6-8)
 constexpr uint32_t kIngestRing = 3;
 constexpr uint32_t kSlots = kIngestSlot + kIngestRing;
@@ -87,7 +88,8 @@ struct Slot {
   uint32_t *h_sig_len = nullptr, *d_sig_len = nullptr;
   uint8_t *h_nil = nullptr, *d_nil = nullptr;
   uint8_t *h_txkey = nullptr, *d_txkey = nullptr;          // [n][32]
-  bool has_nil = false, has_txkey = false;
+  uint16_t *h_vcode = nullptr, *d_vcode = nullptr;         // [n] validator index / kVcode* (host lookup)
+  bool has_nil = false, has_txkey = false, host_val = false;
   bool msg_on_device = false;      // the signer's SignBytes are built by txv_k_signbytes
   uint64_t seq_base = 0;
   uint32_t stamp = 0;              // batch stamp of the staged batch
@@ -194,6 +196,7 @@ struct txv_ctx {
   bool profile_host = false;                    // TXV_PROFILE_HOST
   bool uniform_cols = true;                     // uniform columns filled on the device (TXV_UNIFORM_COLS=0: off)
   bool derive_txkey = true;                     // TxKey decoded from TxHash on the device when it spells it (TXV_DERIVE_TXKEY=0: off)
+  bool host_val = false;                        // validator lookup on the host pack threads (TXV_HOST_VAL=1; default: on the device)
   uint64_t staged_bytes = 0;                    // host bytes the last staged batch moved over PCIe
   // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
   // accepted-vote arena, counters
@@ -375,6 +378,7 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_sig_len, npad)) || (r = dalloc(c, &s.d_sig_len, npad)) ||
       (r = halloc(c, &s.h_nil, npad)) || (r = dalloc(c, &s.d_nil, npad)) ||
       (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
+      (r = halloc(c, &s.h_vcode, npad)) || (r = dalloc(c, &s.d_vcode, npad)) ||
       (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
       (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
@@ -772,8 +776,14 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   add(v->ts_nanos, s.h_fn, s.d_fn, 4);
   add(v->txhash_off, s.h_fo, s.d_fo, 4);
   add((uniform >> kUHL & 1) ? nullptr : v->txhash_len, s.h_fl, s.d_fl, 4);
-  add(v->addr, s.h_addr, s.d_addr, 20);
-  add((uniform >> kUAL & 1) ? nullptr : v->addr_len, s.h_addr_len, s.d_addr_len, 4);
+  // ValidatorSet.GetByAddress on the pack threads (the device's table, host_pack.hpp AddrTable):
+  // a 2-byte code per vote crosses PCIe instead of the 20-byte address and its length
+  const bool host_val = c->host_val && v->addr && v->addr_len && c->n_vals < kVcodeEmpty;
+  s.host_val = host_val;
+  if (!host_val) {
+    add(v->addr, s.h_addr, s.d_addr, 20);
+    add((uniform >> kUAL & 1) ? nullptr : v->addr_len, s.h_addr_len, s.d_addr_len, 4);
+  }
   add(v->sig, s.h_sigraw, s.d_sigraw, 64);
   add((uniform >> kUSL & 1) ? nullptr : v->sig_len, s.h_sig_len, s.d_sig_len, 4);
   add(v->is_nil, s.h_nil, s.d_nil, 1);
@@ -783,7 +793,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (uniform >> kUH & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fh), (uint64_t)v->height[0], n, c->copy_stream));
   if (uniform >> kUS & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fs), (uint64_t)v->ts_sec[0], n, c->copy_stream));
   if (uniform >> kUHL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_fl), (int)v->txhash_len[0], n, c->copy_stream));
-  if (uniform >> kUAL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_addr_len), (int)v->addr_len[0], n, c->copy_stream));
+  if (!host_val && (uniform >> kUAL & 1)) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_addr_len), (int)v->addr_len[0], n, c->copy_stream));
   if (uniform >> kUSL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_sig_len), (int)v->sig_len[0], n, c->copy_stream));
   for (int k = 0; k < nc; ++k)
     if (cols[k].reg && n) HIP_TRY(c, hipMemcpyAsync(cols[k].dev, cols[k].src, (size_t)n * cols[k].elem, hipMemcpyHostToDevice, c->copy_stream));
@@ -806,6 +816,14 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
         const uint32_t va = lo + a, vb = lo + std::min(b, nv);
         for (int q = 0; q < nc; ++q)
           if (!cols[q].reg) memcpy(cols[q].pin + (size_t)va * cols[q].elem, cols[q].src + (size_t)va * cols[q].elem, (size_t)(vb - va) * cols[q].elem);
+        if (host_val)
+          for (uint32_t i = va; i < vb; ++i) {   // vote_set.go:97-106: empty address, then GetByAddress
+            const uint32_t al = v->addr_len[i];
+            uint32_t code = kVcodeUnknown;
+            if (al == 0) code = kVcodeEmpty;
+            else if (al == 20) code = std::min<uint32_t>(c->addr_tab.find(v->addr + (size_t)i * 20), kVcodeUnknown);
+            s.h_vcode[i] = (uint16_t)code;
+          }
       }
       if (b > nv) {
         const uint64_t pa = alo + (uint64_t)(std::max(a, nv) - nv) * 4096, pb = std::min<uint64_t>(alo + (uint64_t)(b - nv) * 4096, ahi);
@@ -816,6 +834,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
       if (!cols[q].reg && hi > lo)
         HIP_TRY(c, hipMemcpyAsync(cols[q].dev + (size_t)lo * cols[q].elem, cols[q].pin + (size_t)lo * cols[q].elem,
                                   (size_t)(hi - lo) * cols[q].elem, hipMemcpyHostToDevice, c->copy_stream));
+    if (host_val && hi > lo)
+      HIP_TRY(c, hipMemcpyAsync(s.d_vcode + lo, s.h_vcode + lo, (size_t)(hi - lo) * 2, hipMemcpyHostToDevice, c->copy_stream));
     if (ahi > alo)
       HIP_TRY(c, hipMemcpyAsync(s.d_arena_th + alo, s.h_arena + alo, ahi - alo, hipMemcpyHostToDevice, c->copy_stream));
   }
@@ -826,7 +846,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   if (derive_key)
     HIP_TRY(c, txv_txkey_from_hash(s.d_arena_th, s.d_fo, s.has_nil ? s.d_nil : nullptr, n, s.d_txkey, c->copy_stream));
   {
-    uint64_t up = ae + 16;
+    uint64_t up = ae + 16 + (host_val ? (uint64_t)n * 2 : 0);
     for (int k = 0; k < nc; ++k) up += (uint64_t)n * cols[k].elem;
     c->staged_bytes = up;
   }
@@ -844,6 +864,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.height = s.d_fh; b.ts_sec = s.d_fs; b.ts_nanos = s.d_fn; b.th_off = s.d_fo; b.th_len = s.d_fl; b.th = s.d_arena_th;
   b.addr = s.d_addr; b.addr_len = s.d_addr_len; b.sig_raw = s.d_sigraw; b.sig_len = s.d_sig_len;
   b.nil = s.has_nil ? s.d_nil : nullptr; b.txkey = s.has_txkey ? s.d_txkey : nullptr;
+  b.vcode = s.host_val ? s.d_vcode : nullptr;
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
   b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
   b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk;
@@ -1333,6 +1354,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
     c->uniform_cols = !(getenv("TXV_UNIFORM_COLS") && atoi(getenv("TXV_UNIFORM_COLS")) == 0);
     c->derive_txkey = !(getenv("TXV_DERIVE_TXKEY") && atoi(getenv("TXV_DERIVE_TXKEY")) == 0);
+    c->host_val = getenv("TXV_HOST_VAL") && atoi(getenv("TXV_HOST_VAL")) != 0;
   }
   *out = c;
   return TXV_OK;
@@ -1351,7 +1373,7 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_sig); hfree(s.h_msg); hfree(s.h_msg_len); hfree(s.h_val); hfree(s.h_set); hfree(s.h_flags);
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
-    hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey);
+    hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey); hfree(s.h_vcode); dfree(s.d_vcode);
     dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);

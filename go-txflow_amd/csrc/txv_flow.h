@@ -141,6 +141,8 @@ struct FlowState {
 };
 
 // one batch (raw columns as the caller passed them, uploaded; derived columns)
+#define TXV_VCODE_EMPTY 0xFFFEu     // empty ValidatorAddress (vote_set.go:97-99)
+#define TXV_VCODE_UNKNOWN 0xFFFFu   // GetByAddress found none (vote_set.go:102-106)
 struct FlowBatch {
   uint32_t n, n_pad, msg_words, chain_len;
   uint64_t seq_base;            // sequence number of vote 0
@@ -158,6 +160,8 @@ struct FlowBatch {
   const uint32_t* sig_len;
   const uint8_t* nil;           // [n] or null
   const uint8_t* txkey;         // [n][32] or null (zero TxKey)
+  const uint16_t* vcode;        // [n] validator index looked up on the host, TXV_VCODE_EMPTY /
+                                // TXV_VCODE_UNKNOWN; or null: route_prep looks addr up itself
   // derived
   uint32_t* sig;                // [16][n_pad] column-major signature words (K1a / K1b / compares)
   uint32_t* msg_len;            // [n] SignBytes length (0: nil / amino error)
