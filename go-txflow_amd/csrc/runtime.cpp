@@ -56,6 +56,10 @@ inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 
 constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0-2 also the submit ring)
 constexpr uint32_t kSubmitRing = 3;    // txv_submit_votes batches in flight
 constexpr uint32_t kVcodeEmpty = TXV_VCODE_EMPTY, kVcodeUnknown = TXV_VCODE_UNKNOWN;   // txv_flow.h
+// batches from which the pack threads look validators up (the link time the 18 bytes per vote
+// save outweighs the host work there: C2's 1M-vote batches 593.4M vs 518.3M votes/s end to end,
+// profiles/r04/hval1; C5's 64k-vote batches keep the device lookup)
+constexpr uint32_t kHostValMin = 1u << 18;
 constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6-8)
 constexpr uint32_t kIngestRing = 3;
 constexpr uint32_t kSlots = kIngestSlot + kIngestRing;
@@ -196,7 +200,8 @@ struct txv_ctx {
   bool profile_host = false;                    // TXV_PROFILE_HOST
   bool uniform_cols = true;                     // uniform columns filled on the device (TXV_UNIFORM_COLS=0: off)
   bool derive_txkey = true;                     // TxKey decoded from TxHash on the device when it spells it (TXV_DERIVE_TXKEY=0: off)
-  bool host_val = false;                        // validator lookup on the host pack threads (TXV_HOST_VAL=1; default: on the device)
+  int host_val = -1;                            // validator lookup on the host pack threads: 1 always, 0 never
+                                                // (TXV_HOST_VAL), -1 for batches of >= kHostValMin votes
   uint64_t staged_bytes = 0;                    // host bytes the last staged batch moved over PCIe
   // TxFlow state on the device (txv_flow.h): set table, key arena, per-set arrays, cells,
   // accepted-vote arena, counters
@@ -778,7 +783,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   add((uniform >> kUHL & 1) ? nullptr : v->txhash_len, s.h_fl, s.d_fl, 4);
   // ValidatorSet.GetByAddress on the pack threads (the device's table, host_pack.hpp AddrTable):
   // a 2-byte code per vote crosses PCIe instead of the 20-byte address and its length
-  const bool host_val = c->host_val && v->addr && v->addr_len && c->n_vals < kVcodeEmpty;
+  const bool host_val = (c->host_val == 1 || (c->host_val < 0 && n >= kHostValMin)) && v->addr && v->addr_len &&
+                        c->n_vals < kVcodeEmpty;
   s.host_val = host_val;
   if (!host_val) {
     add(v->addr, s.h_addr, s.d_addr, 20);
@@ -1354,7 +1360,7 @@ int txv_init(const txv_config* cfg, txv_ctx** out) {
     c->profile_host = getenv("TXV_PROFILE_HOST") != nullptr;
     c->uniform_cols = !(getenv("TXV_UNIFORM_COLS") && atoi(getenv("TXV_UNIFORM_COLS")) == 0);
     c->derive_txkey = !(getenv("TXV_DERIVE_TXKEY") && atoi(getenv("TXV_DERIVE_TXKEY")) == 0);
-    c->host_val = getenv("TXV_HOST_VAL") && atoi(getenv("TXV_HOST_VAL")) != 0;
+    c->host_val = getenv("TXV_HOST_VAL") ? (atoi(getenv("TXV_HOST_VAL")) != 0) : -1;
   }
   *out = c;
   return TXV_OK;
