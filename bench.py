@@ -201,6 +201,81 @@ def c5_expected_pool(wl, cache_size: int):
     return [op.check_batch(b) for b in wl.batches]
 
 
+C5_POOL_SIZE = 8 * 65536  # TxVotePool Size cap of the C5 legs: committed votes leave the pool (Update)
+
+
+def c5_commit_updates(wl, added_slots, commit_batch):
+    """TxFlow's commit side effect on the pool, per batch (txflow/service.go:216-227 ->
+    TxVotePool.Update, txvotepool.go:329-359): after batch k's commit events, Update with the
+    accepted votes of every tx that committed in batch k, and with batch k's ADDED votes of txs
+    committed before (the reference re-fires Update on each later ADDED vote of a committed set:
+    those votes leave the pool too).  added_slots: stream indices of the ADDED votes (from an
+    untimed pass); commit_batch[tx]: the batch of its commit event.  Returns one VoteBatch (or None)
+    per batch, gathered from the stream's columns."""
+    import txflow_amd as T
+    B = wl.batch_size
+    cols = {c: np.concatenate([getattr(b, c) for b in wl.batches]) for c in
+            ("height", "txhash_off", "txhash_len", "ts_sec", "ts_nanos", "addr", "addr_len", "sig", "sig_len")}
+    tx = wl.tx_of[added_slots]
+    cb = commit_batch[tx]
+    keep = cb >= 0
+    g, tx, cb = added_slots[keep], tx[keep], cb[keep]
+    when = np.maximum(g // B, cb)
+    out = []
+    for k in range(len(wl.batches)):
+        idx = g[when == k]
+        if not len(idx):
+            out.append(None)
+            continue
+        a20 = (idx[:, None] * 20 + np.arange(20)).reshape(-1)
+        a64 = (idx[:, None] * 64 + np.arange(64)).reshape(-1)
+        out.append(T.VoteBatch(len(idx), height=cols["height"][idx], txhash_arena=wl.batches[0].txhash_arena,
+                               txhash_off=cols["txhash_off"][idx], txhash_len=cols["txhash_len"][idx],
+                               ts_sec=cols["ts_sec"][idx], ts_nanos=cols["ts_nanos"][idx], addr=cols["addr"][a20],
+                               addr_len=cols["addr_len"][idx], sig=cols["sig"][a64], sig_len=cols["sig_len"][idx]))
+    return out
+
+
+def c5_prepare_updates(ctx, wl):
+    """the commit-driven Updates (untimed): the ADDED votes and each tx's commit batch from one pass
+    of the stream through TxFlow with the oracle pool's admissions (an unbounded pool: the ADDED
+    votes are the first occurrence of each distinct vote, whatever the LRU state)"""
+    import txflow_amd as T
+    expect = c5_expected_pool(wl, C5_CACHE)
+    B = wl.batch_size
+    added, commit_batch = [], np.full(wl.n_txs, -1, np.int64)
+    for k, b in enumerate(wl.batches):
+        b.is_nil = (expect[k] != T.POOL_OK).astype(np.uint8)
+        st, ev = ctx.add_votes(b, ev_cap=b.n)
+        added.append(k * B + np.nonzero((st & 0x7F) == T.ADDED)[0])
+        for e in ev:
+            commit_batch[int(wl.tx_of[k * B + int(e["vote_index"])])] = k
+        b.is_nil = None
+    ctx.reset_flow()
+    upd = c5_commit_updates(wl, np.concatenate(added), commit_batch)
+    for u in upd:                      # the Updates' columns registered too (DMA'd by the pool engine)
+        if u is not None:
+            for col in (u.sig, u.sig_len):
+                ctx.host_register(col)
+    return upd, sum(u.n for u in upd if u is not None)
+
+
+def c5_pool_replay(wl, order, upd, got, cache_size):
+    """the oracle pool run through the same CheckTx batches and Updates in the order the pool took
+    them (recorded under the callers' lock): every batch's statuses must equal (checker, untimed)"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    op = O.Pool(size=C5_POOL_SIZE, cache_size=cache_size, max_txs_bytes=1 << 40)
+    ok = True
+    for kind, k in order:
+        if kind == "c":
+            ok = ok and bool(np.array_equal(op.check_batch(wl.batches[k]), got[k]))
+        elif upd[k] is not None:
+            op.update_batch(1, upd[k])
+    return ok
+
+
 def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     """C5: 1000 weighted validators, the stream (with Appendix C's 5% exact
     replays) cut into `batch`-vote batches fed through the pool ingest (txv_pool_check:
@@ -216,7 +291,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
     ctx.bind_host_numa()
     wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch, replay=C5_REPLAY)
-    expect = c5_expected_pool(wl, C5_CACHE)
+    upd, n_upd = c5_prepare_updates(ctx, wl)
     # the batches' columns pinned once (txv_host_register, a node's receive buffers): the key
     # upload of txv_pool_prepare and txv_submit_votes DMA them without a staging copy
     seen = set()
@@ -232,15 +307,17 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     # beside it, on the host (keys on the GPU, stack-distance decisions on the host threads, the
     # two halves pipelined on two threads)
     def run_mode(device_cache: bool):
-        pool = T.TxVotePool(ctx, size=wl.n + 1, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=device_cache)
+        pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=device_cache)
         runs = run_passes(pool, device_cache)
         return pool, runs
 
     def run_passes(pool, device_cache):
         for _ in range(2):          # warm-up pass: first-touch of host tables and pinned buffers
-            for b in wl.batches:
+            for k, b in enumerate(wl.batches):
                 b.is_nil = (pool.check_batch(b) != T.POOL_OK).astype(np.uint8)
                 ctx.add_votes(b, ev_cap=b.n)
+                if upd[k] is not None:
+                    pool.update(1, upd[k])
             ctx.reset_flow()
             pool.flush()
         # three timed passes over the same stream (reset between): the 2M-vote pass lasts ~45 ms, so
@@ -262,6 +339,10 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             slots = threading.Semaphore(2)
             pool_st = [None] * len(wl.batches)
             dev_ms, dev_split = [], []        # per batch in the pipeline: slot events (HIP, per stream)
+            # CheckTx batches and Updates reach the pool from different threads (as the reactor's
+            # and TxFlow's goroutines do): the order the pool took them in is recorded for the
+            # oracle's replay
+            order, order_mu, max_size = [], threading.Lock(), [0]
 
             # CheckTx in two stages on two threads (txv_pool_prepare: keys on the GPU + TxVote.Size;
             # txv_pool_check_keys: the order-dependent LRU / pool admission), so batch k+1's keys are
@@ -273,7 +354,9 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                 for k, b in enumerate(wl.batches):
                     ts = time.perf_counter()
                     if device_cache:                     # CheckTx submitted: decided on the GPU in order
-                        tk = pool.check_submit(b)
+                        with order_mu:
+                            tk = pool.check_submit(b)
+                            order.append(("c", k))
                         prepared.put((k, ts, time.perf_counter(), None, tk))
                     else:
                         keys, sizes = pool.prepare(b)
@@ -290,7 +373,9 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                     if keys is None:                     # the submitted batch's statuses
                         ps = pool.check_wait(sizes)
                     else:
-                        ps = pool.check_keys(keys, sizes)
+                        with order_mu:
+                            ps = pool.check_keys(keys, sizes)
+                            order.append(("c", k))
                     tp = time.perf_counter()
                     b = wl.batches[k]
                     b.is_nil = (ps != T.POOL_OK).view(np.uint8)    # not admitted: never reaches TxFlow
@@ -308,6 +393,11 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                     k, tk = item
                     st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
                     te = time.perf_counter()
+                    if upd[k] is not None:        # TxVotePool.Update with the batch's committed votes
+                        with order_mu:
+                            pool.update_submit(1, upd[k])
+                            order.append(("u", k))
+                        max_size[0] = max(max_size[0], pool.Size())
                     if rep == 2:                  # the batch's stage times, before its ring slot is reused
                         dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
                         sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
@@ -342,7 +432,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             td.join()
             added = added[0]
             total = time.perf_counter() - t0
-            pool_ok = all(np.array_equal(a, e) for a, e in zip(pool_st, expect))
+            pool.sync()
+            pool_ok = c5_pool_replay(wl, order, upd, pool_st, C5_CACHE)
             ok = pool_ok and added == wl.n_unique and len(commit_t) == wl.n_txs
             lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
             bl = (np.array(done) - np.array(submit)) * 1e3
@@ -358,8 +449,13 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                                f"{wl.n - wl.n_unique} exact replays ({C5_REPLAY:.0%}, Appendix C) in {batch}-vote batches "
                                f"through TxVotePool.CheckTx (CacheSize {C5_CACHE}) in {stages} -- + "
                                f"txv_submit_votes/txv_wait_votes (TxFlow.TryAddVote for the admitted votes, two batches in "
-                               f"flight, each waited by a drain thread as soon as submitted)",
+                               f"flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
+                               f"(txv_pool_update_submit, on the drain thread) with each batch's committed votes after its "
+                               f"commit events ({n_upd} votes per pass, txflow/service.go:224-227), pool Size cap "
+                               f"{C5_POOL_SIZE}; pool statuses checked against the oracle pool replaying the CheckTx "
+                               f"batches and Updates in the order the pool took them",
                    "correct": ok, "pool_matches_oracle": pool_ok, "votes_per_s": round(wl.n / total, 1),
+                   "pool_size_cap": C5_POOL_SIZE, "pool_size_max": max_size[0],
                    "pool_status_counts": {"ok": int((allst == T.POOL_OK).sum()),
                                           "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum())},
                    "p50_pool_check_ms": round(float(np.median(np.array(prep_ms) + np.array(admit_ms))), 3),
@@ -379,7 +475,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     pool, (runs, dev_ms, dev_split) = run_mode(True)
     # unloaded latency: one batch at a time (CheckTx -> submit -> wait before the next batch's
     # CheckTx), so a batch's latency is its own chain, with no queueing behind others
-    one_start, one_ms, one_commit, one_ok = [], [], {}, True
+    one_start, one_ms, one_commit, one_ps = [], [], {}, []
     t0 = time.perf_counter()
     for k, b in enumerate(wl.batches):
         ts = time.perf_counter()
@@ -389,10 +485,14 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
         st, ev = ctx.wait_votes(ctx.submit_votes(b), ev_cap=b.n)
         te = time.perf_counter()
         one_ms.append((te - ts) * 1e3)
-        one_ok = one_ok and bool(np.array_equal(ps, expect[k]))
+        one_ps.append(ps)
         for e in ev:
             one_commit[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
+        if upd[k] is not None:
+            pool.update_submit(1, upd[k])
     one_total = time.perf_counter() - t0
+    pool.sync()
+    one_ok = c5_pool_replay(wl, [(x, k) for k in range(len(wl.batches)) for x in ("c", "u")], upd, one_ps, C5_CACHE)
     one_lat = np.array([te - one_start[wl.first_batch[t]] for t, te in one_commit.items()]) * 1e3
     ctx.reset_flow()
     pool.flush()
@@ -474,20 +574,23 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
     ctx.bind_host_numa()
     wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch, replay=C5_REPLAY)
-    expect = c5_expected_pool(wl, C5_CACHE)
+    upd, n_upd = c5_prepare_updates(ctx, wl)
     wbs = [T.encode_msgs(b, b.txkey) for b in wl.batches]
     wire_bytes = sum(w.nbytes for w in wbs)
     for w in wbs:          # the receive buffers, pinned once (txv_host_register): DMA'd without a staging copy
         ctx.host_register(w.wire)
-    pool = T.TxVotePool(ctx, size=wl.n + 1, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
-    for w in wbs:                                   # warm-up pass
+    pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
+    for k, w in enumerate(wbs):                     # warm-up pass
         pool.ingest(w)
+        if upd[k] is not None:
+            pool.update(1, upd[k])
     ctx.reset_flow()
     pool.flush()
     runs = []
     for rep in range(3):
         start, dec_ms, adm_ms, commit_t = [], [], [], {}
         state = {"added": 0, "ok": True}
+        got, order, order_mu = [None] * len(wbs), [], threading.Lock()
         decoded, admitted = queue.Queue(), queue.Queue()
         slots = threading.Semaphore(3)              # the library's ingest ring
 
@@ -500,7 +603,9 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                     return
                 k, tk = item
                 ta = time.perf_counter()
-                pool.ingest_admit(tk)
+                with order_mu:
+                    pool.ingest_admit(tk)
+                    order.append(("c", k))
                 adm_ms.append((time.perf_counter() - ta) * 1e3)
                 admitted.put((k, tk))
 
@@ -513,7 +618,12 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                 ws, ps, fs, ev = pool.ingest_wait(tk)
                 te = time.perf_counter()
                 slots.release()
-                state["ok"] = state["ok"] and bool((ws == T.WIRE_OK).all() and np.array_equal(ps, expect[k]))
+                if upd[k] is not None:            # TxVotePool.Update with the batch's committed votes
+                    with order_mu:
+                        pool.update_submit(1, upd[k])
+                        order.append(("u", k))
+                got[k] = ps
+                state["ok"] = state["ok"] and bool((ws == T.WIRE_OK).all())
                 state["added"] += int(np.count_nonzero((fs & 0x7F) == T.ADDED))
                 for e in ev:
                     commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
@@ -533,9 +643,11 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         ta_.join()
         td_.join()
         total = time.perf_counter() - t0
+        pool.sync()
+        pool_ok = c5_pool_replay(wl, order, upd, got, C5_CACHE)
         lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
-        runs.append({"votes_per_s": round(wl.n / total, 1),
-                     "correct": state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
+        runs.append({"votes_per_s": round(wl.n / total, 1), "pool_matches_oracle": pool_ok,
+                     "correct": pool_ok and state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
                      "p50_decode_ms": round(float(np.median(dec_ms)), 3),
                      "p50_admit_ms": round(float(np.median(adm_ms)), 3),
                      "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
@@ -544,7 +656,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         pool.flush()
     # unloaded latency: the same stream one batch at a time (decode -> admit -> wait before the
     # next batch's decode), so a batch's latency is its own chain, with no queueing behind others
-    one_start, one_ms, one_commit, one_ok = [], [], {}, True
+    one_start, one_ms, one_commit, one_ok, one_ps = [], [], {}, True, []
     t0 = time.perf_counter()
     for k, w in enumerate(wbs):
         ts = time.perf_counter()
@@ -554,10 +666,15 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         ws, ps, fs, ev = pool.ingest_wait(tk)
         te = time.perf_counter()
         one_ms.append((te - ts) * 1e3)
-        one_ok = one_ok and bool((ws == T.WIRE_OK).all() and np.array_equal(ps, expect[k]))
+        one_ok = one_ok and bool((ws == T.WIRE_OK).all())
+        one_ps.append(ps)
         for e in ev:
             one_commit[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
+        if upd[k] is not None:
+            pool.update_submit(1, upd[k])
     one_total = time.perf_counter() - t0
+    pool.sync()
+    one_ok = one_ok and c5_pool_replay(wl, [(x, k) for k in range(len(wbs)) for x in ("c", "u")], upd, one_ps, C5_CACHE)
     one_lat = np.array([te - one_start[wl.first_batch[t]] for t, te in one_commit.items()]) * 1e3
     ctx.reset_flow()
     pool.flush()
@@ -579,7 +696,8 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                         f"txv_host_register, so the wire bytes are DMA'd without a staging copy; the pool's LRU cache "
                         f"in HBM, TXV_POOL_DEVICE_CACHE: CheckTx decided on the GPU from the decoded keys; "
                         f"p50_decode_ms = the upload + decode enqueue, p50_admit_ms = keys wait + CheckTx + TxFlow "
-                        f"enqueue)",
+                        f"enqueue) + TxVotePool.Update (txv_pool_update_submit) with each batch's committed votes after "
+                        f"its commit events ({n_upd} votes per pass), pool Size cap {C5_POOL_SIZE}",
                passes=3, votes_per_s_passes=[r["votes_per_s"] for r in runs],
                correct=all(r["correct"] for r in runs) and out["unloaded"]["correct"],
                pcie_bytes_per_vote_up=round(wire_bytes / wl.n + 16, 1), pcie_bytes_per_vote_down=38)
@@ -707,7 +825,16 @@ def main():
     ap.add_argument("--same-gpu", action="store_true", help="every rank uses device 0 (rehearsal only)")
     ap.add_argument("--cpu-serial-votes", type=int, default=100_000)
     ap.add_argument("--cpu-parallel-votes", type=int, default=1_000_000)
+    ap.add_argument("--c5-only", action="store_true",
+                    help="profiling aid: run only the C5 legs (SoA and wire) and print them as one JSON line")
     args = ap.parse_args()
+
+    if args.c5_only:
+        out = {"c5_streaming": c5_streaming(0, 1000, args.c5_txs, 65536)}
+        if not args.no_wire:
+            out["c5_wire"] = c5_wire_leg(0, 1000, args.c5_txs, 65536)
+        print(json.dumps(out), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -784,9 +911,16 @@ def main():
         # the gathered global state (unpacked with the C-ABI's own layout): every tx of every shard
         # committed with the full stake
         bits = full = 0
-        for com, sums in steps_rt.gathered_states():
+        names = set()
+        for com, sums, dig in steps_rt.gathered_states():
             bits += int(com.sum())
             full += int((sums == ctx.total_power()).sum())
+            names.update(bytes(d) for d in dig[com])
+        # the gathered rows name every rank's sets: this rank's own txs among them by digest
+        mine = set(T.tx_digest(h.tobytes()) for h in wl.hashes)
+        if not mine <= names or len(names) != bits:
+            log(f"[rank {rank}] GATHER CHECK FAILURE: {len(mine - names)} own txs not named in the gathered state")
+            sys.exit(3)
         nt = torch.tensor([wl.n_txs], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nt)
         if bits != int(nt.item()) or full != bits:

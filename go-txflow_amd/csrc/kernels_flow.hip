@@ -30,16 +30,17 @@
 //            signature compare; first verified == itself -> ADDED (an arena row is taken by a
 //            wave-aggregated atomic and written right there); first verified earlier ->
 //            signature compare with it; none -> invalid signature
-//   cross    one wave per set the batch ADDED votes to (persistent waves over the set ids,
-//            stamp check): its ADDED votes are the stamped cells of its row; stake sum, and the
-//            arrival index at which the prefix (in arrival order) of the stake first reaches
-//            quorum (per-lane prefix sums over the set's list in LDS, one wave min); the cells'
-//            accepted rows
+//   cross    one wave per set the batch ADDED votes to (the work list resolve compacted): its
+//            ADDED votes are the stamped cells of its row; stake sum, and the arrival index at
+//            which the prefix (in arrival order) of the stake first reaches quorum (a digit-by-
+//            digit histogram search over the arrival index: LDS atomics, a DPP wave scan and a
+//            ballot per 6 bits); the cells' accepted rows
 //   out      final statuses (pre-check or tally; an ADDED vote at or after its set's crossing
 //            fires) into mapped host memory, and the per-block counts of commit events
 //   events   compaction of the crossing votes in arrival order -> commit events + batch summary
 #include <algorithm>
 
+#include "sha2.h"
 #include "txv_device.h"
 #include "txv_flow.h"
 
@@ -447,9 +448,31 @@ struct NewSetPred {
   }
 };
 
+// SHA-256 of len bytes at p (any alignment), big-endian state words
+__device__ void sha256_bytes_dev(const uint8_t* p, uint32_t len, uint32_t st[8]) {
+  txv::sha256_init(st);
+  const uint32_t nblk = (len + 9 + 63) / 64;
+  for (uint32_t blk = 0; blk < nblk; ++blk) {
+    uint32_t w[16];
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t off = blk * 64 + 4u * (uint32_t)t;
+      uint32_t v = 0;
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t o = off + q;
+        const uint32_t byte = o < len ? (uint32_t)p[o] : (o == len ? 0x80u : 0u);
+        v = (v << 8) | byte;
+      }
+      if (blk == nblk - 1 && t == 14) v = len >> 29;
+      if (blk == nblk - 1 && t == 15) v = len << 3;
+      w[t] = v;
+    }
+    txv::sha256_block(st, w);
+  }
+}
+
 // the vote that first carried a new TxHash: number its set (first-seen order), move the key
 // bytes into the set's key slot (or the overflow arena), record the set's TxKey
-// (service.go:201-207)
+// (service.go:201-207) and its exchange name SHA-256(TxHash)[0:16]
 struct NewSetAct {
   FlowState fs;
   FlowBatch b;
@@ -475,6 +498,12 @@ struct NewSetAct {
       ko = (uint64_t)fs.max_txs * TXV_KEY_SLOT + o;
     }
     const uint8_t* src = b.th + (e.key_off - 1);
+    {
+      uint32_t h[8];
+      sha256_bytes_dev(src, len, h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fs.set_digest[(size_t)id * 4 + j] = __builtin_bswap32(h[j]);   // bytes in order
+    }
     uint64_t* dst = reinterpret_cast<uint64_t*>(fs.keys + ko);
     for (uint32_t k = 0; k < span; k += 8)
       dst[k / 8] = ld64u(src + k) & (k + 8 <= len ? ~0ull : ((1ull << (8 * (len - k))) - 1ull));
@@ -518,6 +547,7 @@ __global__ void __launch_bounds__(256) txv_k_tally_min(FlowState fs, FlowBatch b
     const uint32_t created = b.blk[nb];
     const uint32_t ns = fs.ctr->n_sets + created;
     fs.ctr->n_sets = ns > fs.max_txs ? fs.max_txs : ns;
+    fs.ctr->n_stamped = 0;
   }
   if (i >= b.n) return;
   const uint32_t e = b.entry[i];
@@ -557,8 +587,8 @@ __device__ __forceinline__ bool sig_eq_votes(const FlowBatch& b, uint32_t i, uin
 // (the reference's votes[addr] = vote, vote_set.go:154); the cell keeps the row for the crossing
 // step, which publishes it as the cell's accepted vote once no vote of the batch reads acc
 __global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBatch b) {
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t base_s;
+  __shared__ uint32_t wsum[16], wnew[16];
+  __shared__ uint32_t base_s, nbase_s;
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   bool added = false;
@@ -587,21 +617,46 @@ __global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBa
     }
     b.status[i] = st;
   }
-  // the block's ADDED votes take consecutive arena rows: one atomic per 1024 votes (a hot
-  // counter serialises at ~10k atomics per 50 us)
-  const uint64_t m = __ballot(added);
-  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  // the set's first ADDED vote of the batch lists the set for the crossing step.  The block's
+  // ADDED votes first elect one vote per set in an LDS hash set (C5's tx-major arrival order puts
+  // ~8 votes of each of ~128 sets in a block: one device-scope exchange per (block, set) instead of
+  // per vote, which serialised on the ~200 hot stamps); the electee's coherent read filters the
+  // sets already stamped, and the exchange decides the one vote that lists the set
+  __shared__ uint32_t l_set[2048];
+  for (uint32_t k = threadIdx.x; k < 2048; k += 1024) l_set[k] = TXV_NONE;
+  __syncthreads();
+  bool rep = false;
+  if (added) {
+    for (uint32_t h = (s * 0x9E3779B1u) >> 21;; h = (h + 1) & 2047u) {
+      const uint32_t o = atomicCAS(&l_set[h], TXV_NONE, s);
+      if (o == TXV_NONE) { rep = true; break; }
+      if (o == s) break;
+    }
+  }
+  bool fresh = false;
+  if (rep && __hip_atomic_load(&fs.set_stamp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != b.stamp)
+    fresh = atomicExch(&fs.set_stamp[s], b.stamp) != b.stamp;
+  // the block's ADDED votes take consecutive arena rows and its fresh sets consecutive list
+  // entries: one atomic per 1024 votes each (a hot counter serialises at ~10k atomics per 50 us)
+  const uint64_t m = __ballot(added), mf = __ballot(fresh);
+  if (lane == 0) { wsum[w] = (uint32_t)__popcll(m); wnew[w] = (uint32_t)__popcll(mf); }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int k = 0; k < 16; ++k) t += wsum[k];
+    uint32_t t = 0, tf = 0;
+    for (int k = 0; k < 16; ++k) { t += wsum[k]; tf += wnew[k]; }
     base_s = t ? atomicAdd(&fs.ctr->arena_used, t) : 0u;
+    nbase_s = tf ? atomicAdd(&fs.ctr->n_stamped, tf) : 0u;
   }
   __syncthreads();
   if (!added) return;
-  uint32_t r = base_s + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (fresh) {
+    uint32_t q = nbase_s + (uint32_t)__popcll(mf & below);
+    for (int k = 0; k < w; ++k) q += wnew[k];
+    b.stamped[q] = s;                         // q < sets touched by the batch <= n
+  }
+  uint32_t r = base_s + (uint32_t)__popcll(m & below);
   for (int k = 0; k < w; ++k) r += wsum[k];
-  fs.set_stamp[s] = b.stamp;
   if (r >= fs.max_accepted) {
     atomicOr(&fs.ctr->err, TXV_FERR_ARENA);
     cell->row = 0;
@@ -632,25 +687,47 @@ __device__ __forceinline__ int64_t wave_sum64(int64_t x) {
   return x;
 }
 
-constexpr uint32_t kListCap = 512;   // ADDED votes of a set kept in LDS (every set of a <= 512-validator registry)
+constexpr uint32_t kListCap = 1024;   // ADDED votes of a set kept in LDS (every set of a <= 1024-validator registry)
+constexpr uint32_t kDigitBits = 6;     // crossing search: one 64-bucket histogram level per 6 arrival-index bits
 
-// One wave per set that ADDED votes in this batch (persistent waves over the set ids; a set
-// whose stamp is not this batch's is skipped): its ADDED votes are the cells of its row whose
-// candidate carries this batch's stamp and that held no accepted vote; stake sum, and the arrival
-// index at which the prefix (in arrival order) of the stake first reaches quorum (per-lane prefix
-// sums over the LDS list, one wave min): set_cross[s], read by the status pass (ADDED votes at or
-// after it fire); the cells' accepted rows are published here.
-__global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch b, uint32_t sets_bound) {
-  __shared__ __attribute__((aligned(16))) uint32_t l_vote[4][kListCap + 4];
-  __shared__ __attribute__((aligned(16))) int64_t l_pow[4][kListCap + 4];
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// One wave per set that ADDED votes in this batch (the work list tally_resolve compacted): its
+// ADDED votes are the cells of its row whose candidate carries this batch's stamp (a stamped cell
+// had no accepted vote when the batch began: tally_min posts to no other), listed in LDS as
+// (arrival index, stake); the accepted rows are published in the same pass (every vote of the batch
+// read acc in the resolve step).  The crossing (addVerifiedVote, types/vote_set.go:143-166, in
+// arrival order) is the smallest arrival index whose prefix stake reaches `need`: found digit by
+// digit over the arrival index, 6 bits per level from the top -- each level a 64-bucket stake
+// histogram of the entries under the prefix chosen so far (LDS atomics), one wave-wide inclusive
+// scan (DPP shuffles) and a ballot for the first bucket whose running stake reaches `need`.
+// ceil(log2(n) / 6) levels (3 for a 64k batch, 4 for 1M), each one pass over the list: O(k) per
+// set instead of the O(k^2) pairwise prefix sums and the row-rescanning binary lifting it
+// replaced.  Sets with more ADDED votes than the list holds read their row
+// again per level instead of the list.
+// One-wave blocks (12.5 KB of LDS each): the kernel runs beside the next batch's K1b, whose
+// entry buffers leave ~32 KB of a CU's LDS free.
+__global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch b) {
+  __shared__ __attribute__((aligned(16))) uint32_t l_vote[1][kListCap];
+  __shared__ __attribute__((aligned(16))) int64_t l_pow[1][kListCap];
+  __shared__ int64_t l_hist[1][64];
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t gw = blockIdx.x * 4 + wv, n_waves = gridDim.x * 4;
-  const uint32_t n_sets = min(fs.ctr->n_sets, sets_bound);
-  for (uint32_t s = gw; s < n_sets; s += n_waves) {
-    if (fs.set_stamp[s] != b.stamp) continue;
+  constexpr uint32_t wv = 0;
+  const uint32_t gw = blockIdx.x, n_waves = gridDim.x;
+  const uint32_t n_list = fs.ctr->n_stamped;
+  const uint32_t nbits = 32u - (uint32_t)__builtin_clz(max(b.n, 2u) - 1u);
+  const uint32_t levels = (nbits + kDigitBits - 1) / kDigitBits;
+  for (uint32_t j = gw; j < n_list; j += n_waves) {
+    const uint32_t s = b.stamped[j];
     TallyCell* row = fs.cell + (size_t)s * fs.n_vals;
-    // list this set's ADDED votes (compacted in validator order)
+    // list this set's ADDED votes (compacted in validator order) and publish their rows
     uint32_t k = 0;
     int64_t part = 0;
     for (uint32_t v0 = 0; v0 < fs.n_vals; v0 += 64) {
@@ -658,7 +735,8 @@ __global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch
       uint32_t f = TXV_NONE;
       if (v < fs.n_vals) {
         const TallyCell c = row[v];
-        if (c.acc == 0) f = cand_of(c.cand, b.stamp);
+        f = cand_of(c.cand, b.stamp);
+        if (f != TXV_NONE) row[v].acc = c.row;
       }
       const bool added = f != TXV_NONE;
       const uint64_t m = __ballot(added);
@@ -671,7 +749,6 @@ __global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch
       k += (uint32_t)__popcll(m);
     }
     __threadfence_block();
-    const bool in_lds = k <= kListCap;
     const int64_t prior = fs.set_sum[s];
     const int64_t total = prior + wave_sum64(part);
     uint32_t cross = TXV_NO_CROSS;
@@ -679,55 +756,35 @@ __global__ void __launch_bounds__(256) txv_k_tally_cross(FlowState fs, FlowBatch
       cross = 0;                              // already committed: every ADDED vote re-fires
     } else if (total >= fs.quorum) {
       const int64_t need = fs.quorum - prior;
-      if (in_lds) {
-        // T = the smallest listed arrival index f_c whose prefix stake (every listed vote with
-        // f_j <= f_c) reaches need: each lane sums the prefix of its own entries with one pass
-        // over the list (LDS broadcast reads, independent iterations), then one wave min --
-        // no chain of dependent wave reductions (the kernel runs beside K1b, at a small share
-        // of the SIMDs' issue slots)
-        uint32_t T = TXV_NONE;
-        const uint32_t k4 = (k + 3u) & ~3u;        // the list padded to 4 with (never, 0)
-        if (lane < k4 - k) { l_vote[wv][k + lane] = 0xFFFFFFFFu; l_pow[wv][k + lane] = 0; }
+      const bool in_lds = k <= kListCap;
+      uint32_t pfx = 0;                       // the crossing index's digits chosen so far
+      int64_t before = 0;                     // stake of the entries below the prefix's range
+      for (uint32_t lv = 0; lv < levels; ++lv) {
+        const uint32_t sh = kDigitBits * (levels - 1u - lv);
+        l_hist[wv][lane] = 0;
         __threadfence_block();
-        for (uint32_t c0 = 0; c0 < k; c0 += 128) {   // two entries per lane per pass
-          const uint32_t ca = c0 + lane, cb = c0 + 64 + lane;
-          const uint32_t fa = ca < k ? l_vote[wv][ca] : 0xFFFFFFFFu, fb = cb < k ? l_vote[wv][cb] : 0xFFFFFFFFu;
-          int64_t pa = 0, pb = 0;
-          const uint4* vq = reinterpret_cast<const uint4*>(l_vote[wv]);
-          const longlong2* pq = reinterpret_cast<const longlong2*>(l_pow[wv]);
-          for (uint32_t j = 0; j < k4; j += 4) {
-            const uint4 f4 = vq[j / 4];
-            const longlong2 p01 = pq[j / 2], p23 = pq[j / 2 + 1];
-            pa += (f4.x <= fa ? p01.x : 0) + (f4.y <= fa ? p01.y : 0) + (f4.z <= fa ? p23.x : 0) + (f4.w <= fa ? p23.y : 0);
-            pb += (f4.x <= fb ? p01.x : 0) + (f4.y <= fb ? p01.y : 0) + (f4.z <= fb ? p23.x : 0) + (f4.w <= fb ? p23.y : 0);
+        if (in_lds) {
+          for (uint32_t e = lane; e < k; e += 64) {
+            const uint32_t f = l_vote[wv][e];
+            if (((f >> sh) >> kDigitBits) == pfx)
+              atomicAdd((unsigned long long*)&l_hist[wv][(f >> sh) & 63u], (unsigned long long)l_pow[wv][e]);
           }
-          if (ca < k && pa >= need && fa < T) T = fa;
-          if (cb < k && pb >= need && fb < T) T = fb;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) T = min(T, (uint32_t)__shfl_xor((int)T, o, 64));
-        cross = T;
-      } else {
-        // more ADDED votes than the LDS list holds: binary lifting over the arrival-index bits,
-        // one pass over the set's row per probe
-        uint32_t T = 0;
-        for (int bit = 31 - __builtin_clz(max(b.n, 2u) - 1u); bit >= 0; --bit) {
-          const uint32_t cand = T | (1u << bit);
-          int64_t sm = 0;
+        } else {
           for (uint32_t v = lane; v < fs.n_vals; v += 64) {
-            const TallyCell c = row[v];
-            const uint32_t f = c.acc == 0 ? cand_of(c.cand, b.stamp) : TXV_NONE;
-            if (f != TXV_NONE && f < cand) sm += fs.power[v];
+            const uint32_t f = cand_of(row[v].cand, b.stamp);
+            if (f != TXV_NONE && ((f >> sh) >> kDigitBits) == pfx)
+              atomicAdd((unsigned long long*)&l_hist[wv][(f >> sh) & 63u], (unsigned long long)fs.power[v]);
           }
-          if (wave_sum64(sm) < need) T = cand;
         }
-        cross = T;
+        __threadfence_block();
+        const int64_t h = l_hist[wv][lane];
+        const int64_t inc = wave_incl_scan64(h, lane);
+        const uint64_t hit = __ballot(before + inc >= need);   // non-empty: the range holds >= need
+        const int c = (int)__builtin_ctzll(hit);
+        before += __shfl(inc, c, 64) - __shfl(h, c, 64);
+        pfx = (pfx << kDigitBits) | (uint32_t)c;
       }
-    }
-    // the accepted-vote cells (after every vote of the batch read acc in the resolve step)
-    for (uint32_t v = lane; v < fs.n_vals; v += 64) {
-      TallyCell& c = row[v];
-      if (c.acc == 0 && cand_of(c.cand, b.stamp) != TXV_NONE) c.acc = c.row;
+      cross = pfx;
     }
     if (lane == 0) {
       fs.set_sum[s] = total;
@@ -919,12 +976,15 @@ __device__ __forceinline__ uint32_t commit_word(const FlowState& fs, uint32_t t,
 __global__ void __launch_bounds__(256) txv_k_pack(FlowState fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   const uint32_t ns = min(fs.ctr->n_sets, n_cap);
-  if (t == 0) { dst[0] = ns; dst[1] = 0; }
+  if (t == 0) { dst[0] = ns; dst[1] = 1; }   // word 1: layout 1 = with the per-set digests
   if (t < bm_words) dst[2 + t] = commit_word(fs, t, ns);
   if (t < n_cap) {
     const int64_t sm = t < ns ? fs.set_sum[t] : 0;
     dst[2 + bm_words + 2 * t] = (uint32_t)(uint64_t)sm;
     dst[2 + bm_words + 2 * t + 1] = (uint32_t)((uint64_t)sm >> 32);
+    uint32_t* dg = dst + 2 + bm_words + 2 * (size_t)n_cap + 4 * (size_t)t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[j] = t < ns ? fs.set_digest[(size_t)t * 4 + j] : 0u;
   }
 }
 
@@ -987,9 +1047,9 @@ hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets
   if (!TXV_SKIP(1)) hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
   if (b->n && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3((b->n + 1023) / 1024), dim3(1024), 0, st, *fs, *b);
   sets_bound = std::min(sets_bound, fs->max_txs);
-  // persistent waves over the set ids: one wave per set (up to 8 waves per SIMD)
-  const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::min(sets_bound, b->n) + 3) / 4, 2048));
-  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(256), 0, st, *fs, *b, sets_bound);
+  // persistent waves over the batch's stamped sets (at most min(sets, votes) of them): one wave per set
+  const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>(std::min(sets_bound, b->n), 4096));
+  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(64), 0, st, *fs, *b);
   if (TXV_SKIP(32)) return hipGetLastError();
   hipLaunchKernelGGL(txv_k_status_out, dim3(nb ? nb : 1), dim3(256), 0, st, *fs, *b);
   hipLaunchKernelGGL(txv_k_event_top, dim3(1), dim3(256), 0, st, *fs, *b, nb);

@@ -102,12 +102,14 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
 // pushes, sort input
 __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i == 0) { a.nfar[0] = 0; a.nfar[1] = 0; }   // far pushes, pairs (appended by pd_link)
+  if (i == 0) a.nfar[0] = 0;   // far pushes (appended by pd_link)
   if (i >= a.n) return;
   const bool ok = !a.valid || a.valid[i] == a.valid_ok;
   const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
   a.push[i] = p;
-  a.hkey[i] = p ? a.keys[(size_t)i * 8 + 2] : 0xFFFFFFFFu;
+  // non-pushes sort into a run of their own at the end: a push's slice is clamped below it, so a
+  // key whose slice is 0xFFFFFFFF never shares a run with them (pd_link scans its run backwards)
+  a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2], 0xFFFFFFFEu) : 0xFFFFFFFFu;
   a.hidx[i] = i;
   a.last[i] = p;            // cleared below for a push with a later push of its key
 }
@@ -158,39 +160,75 @@ __global__ void __launch_bounds__(256) pd_link(PoolDevArgs a) {
     if (evict) ps = front ? 2 * r : 2 * L0 - 1;
   }
   a.dec[i] = d;
-  if (ps != kNoPair) {                      // the pair list the far counts scan (order irrelevant)
+  if (ps != kNoPair) {                      // the pair (previous occurrence, this push), by arrival index
     a.pst[i] = ps;
     a.pend[i] = e2;
-    const uint32_t q = atomicAdd(a.nfar + 1, 1u);
-    a.plist[2 * (size_t)q] = ps;
-    a.plist[2 * (size_t)q + 1] = e2;
   }
   if (d == 3) a.far[atomicAdd(a.nfar, 1u)] = i;
 }
 
-// one block per far push (grid-strided): the pairs nested inside its window, then its decision
+// The far pushes' nested-pair counts in O(log) per block of votes instead of a scan of every pair
+// (a peer-controlled stream of replays at window ~C made the scan O(far x pairs)).
+// A pair ends where its push stands in S, and pushes stand in S in arrival order, so the pairs
+// ending before a far push at arrival index i are exactly the pairs of votes i' < i; what remains
+// to count is how many of those start after the far push's previous occurrence.  Each block of
+// kXBlock votes sorts its pairs' start positions here (hipcub block radix sort in LDS, votes
+// without a pair as 0xFFFFFFFF at the end; xn = pairs in the block) ...
+constexpr uint32_t kXBlock = 1024;
+__global__ void __launch_bounds__(256) pd_xsort(PoolDevArgs a) {
+  using Sort = hipcub::BlockRadixSort<uint32_t, 256, 4>;
+  __shared__ typename Sort::TempStorage tmp;
+  __shared__ uint32_t wcnt[4];
+  const uint32_t base = blockIdx.x * kXBlock;
+  uint32_t x[4];
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = base + threadIdx.x * 4 + k;
+    const uint64_t p = i < a.n ? a.pst[i] : kNoPair;
+    x[k] = p == kNoPair ? 0xFFFFFFFFu : (uint32_t)p;      // S positions are < 2^32 - 1 (host check)
+    c += p != kNoPair;
+  }
+  Sort(tmp).Sort(x);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a.xs[base + threadIdx.x * 4 + k] = x[k];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) a.xn[blockIdx.x] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+}
+
+// ... and one wave per far push counts, over the sorted blocks before its own (one binary search
+// each, a lane per block) and the votes of its own block before it (a scan), the pairs starting
+// after fp: the pairs nested in (fp, fe); then its decision.
 __global__ void __launch_bounds__(256) pd_far(PoolDevArgs a) {
-  __shared__ uint32_t red[4];
-  const uint32_t nf = a.nfar[0], np = a.nfar[1];
+  const uint32_t nf = a.nfar[0];
   const uint64_t C = a.C;
-  const ulonglong2* pl = reinterpret_cast<const ulonglong2*>(a.plist);
-  for (uint32_t f = blockIdx.x; f < nf; f += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (uint32_t f = gw; f < nf; f += nw) {
     const uint32_t i = a.far[f];
     const uint64_t fp = a.pst[i], fe = a.pend[i];          // a far push always has its pair (evicting)
+    const uint32_t fp32 = (uint32_t)fp, bi = i / kXBlock;
     uint32_t cnt = 0;
-    for (uint32_t k = threadIdx.x; k < np; k += 256) {
-      const ulonglong2 pr = pl[k];
-      cnt += (pr.x > fp) & (pr.y < fe);
+    for (uint32_t bk = lane; bk < bi; bk += 64) {
+      const uint32_t* xs = a.xs + (size_t)bk * kXBlock;
+      uint32_t lo = 0, hi = a.xn[bk];                      // first sorted start > fp
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (xs[mid] <= fp32) lo = mid + 1; else hi = mid;
+      }
+      cnt += a.xn[bk] - lo;
+    }
+    for (uint32_t t = bi * kXBlock + lane; t < i; t += 64) {
+      const uint64_t x = a.pst[t];
+      cnt += x != kNoPair && x > fp;
     }
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint64_t nested = (uint64_t)red[0] + red[1] + red[2] + red[3];
+    if (lane == 0) {
       const uint64_t window = (fe - fp) / 2 - 1;            // pushes strictly between (fp exact here)
-      a.dec[i] = window - nested < C ? 2 : 1;
+      a.dec[i] = window - cnt < C ? 2 : 1;
     }
-    __syncthreads();
   }
 }
 
@@ -290,7 +328,10 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   tb = a.tmp_bytes;
   if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
   hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
-  if (a.C) hipLaunchKernelGGL(pd_far, dim3(256), b, 0, st, a);
+  if (a.C) {
+    hipLaunchKernelGGL(pd_xsort, dim3((n + kXBlock - 1) / kXBlock), b, 0, st, a);
+    hipLaunchKernelGGL(pd_far, dim3(std::min<uint32_t>(1024, (n + 3) / 4)), b, 0, st, a);
+  }
   const uint32_t span = std::max(n, a.C);
   hipLaunchKernelGGL(pd_status, dim3((span + 255) / 256), b, 0, st, a);
   if (!a.C) return hipGetLastError();

@@ -259,7 +259,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev);
 int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
-constexpr int kPdRing = 3;   // = PoolDev::kPdRing (runtime.cpp)
+constexpr int kPdRing = 4;   // = PoolDev::kPdRing (runtime.cpp)
 
 struct txv_pool {
   txv_pool_config cfg{};
@@ -285,13 +285,24 @@ struct txv_pool {
   // not appended yet.  Every reader / writer of txs drains it first (drain_appends); Size and
   // TxsBytes count the pending votes.  amu guards jobs, pend_*, txs.len and txs_bytes updates
   // made by the appender.
-  struct Append { std::vector<Key> keys; std::vector<uint32_t> sizes; uint32_t n = 0; uint64_t bytes = 0; txv_ctx* ctx = nullptr; };
+  struct Append {
+    std::vector<Key> keys; std::vector<uint32_t> sizes; uint32_t n = 0; uint64_t bytes = 0; txv_ctx* ctx = nullptr;
+    bool remove = false;   // Update: removeTx(tx, e, false) for every key the pool holds (txvotepool.go:339-344)
+  };
   std::mutex amu;
   std::condition_variable acv;
   std::deque<Append> jobs, spare;
   bool a_stop = false, a_busy = false;
   int64_t pend_len = 0, pend_bytes = 0;
   std::thread appender;
+  // Size() / TxsBytes() as published after every change (the reference's atomics, read without
+  // proxyMtx): txs.len / txs_bytes themselves are written under mu or by the appender under amu,
+  // so a reader holding neither must not touch them
+  std::atomic<int64_t> pub_len{0}, pub_bytes{0};
+  // engines replaced while a waiter (txv_pool_check_wait, outside mu) may still sync on one of
+  // their flight events: freed when the last waiter is done
+  int waiters = 0;
+  std::vector<PoolDev*> retired;
   // device batches submitted (txv_pool_check_submit) and not yet waited, in order; a device one
   // holds flight slot `slot` of the engine until finished (its statuses then kept in st).
   // infl_*: the pushes / Size() sums of the unfinished ones (upper bounds for the caps check)
@@ -304,6 +315,10 @@ struct txv_pool {
     uint64_t pushes = 0, bytes = 0;
     std::vector<uint8_t> st;
     int err = 0;
+    // an Update batch (txv_pool_update_submit): its keys pushed by the engine, its votes removed
+    // from the pool list by the appender once the tickets before it are finished; no caller waits
+    bool upd = false;
+    std::vector<uint32_t> usizes;
   };
   std::deque<Ticket> tickets;
   uint64_t next_ticket = 1;
@@ -911,6 +926,7 @@ txv_pool::~txv_pool() {
   }
   if (appender.joinable()) appender.join();              // the queued appends finish first
   pooldev_free(dev);
+  for (PoolDev* d : retired) pooldev_free(d);
 }
 
 extern "C" {
@@ -948,8 +964,15 @@ void host_cache_written(txv_pool* p);
 void drain_appends(txv_pool* p);
 
 int drain_flights(txv_pool* p);
+void publish_locked(txv_pool* p);
 
+int pool_admit_body(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out);
 int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
+  const int r = pool_admit_body(p, ctx, keys, n, status_out);
+  publish_locked(p);
+  return r;
+}
+int pool_admit_body(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
   if (int r = drain_flights(p)) return r;
   drain_appends(p);
   if (int r = cache_to_host(p, ctx)) return r;
@@ -1040,6 +1063,10 @@ int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
     if (int r = drain_flights(p)) return r;
   if (p->dev && !pooldev_same_device(ctx, p->dev))
     if (int r = cache_to_host(p, ctx)) return r;
+  if (p->dev && p->waiters && !pooldev_same_device(ctx, p->dev)) {   // a waiter may still sync on it
+    p->retired.push_back(p->dev);
+    p->dev = nullptr;
+  }
   PoolDev* before = p->dev;
   if (int r = pooldev_bind(ctx, &p->dev, p->cache_on ? p->cfg.cache_size : 0u, n)) return r;
   if (p->dev != before) p->dev_state = txv_pool::kHostAhead;   // a new device copy starts empty
@@ -1090,6 +1117,16 @@ void append_list(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* siz
   }, 1);
 }
 
+// with amu held, or the appender idle (after drain_appends)
+void publish(txv_pool* p) {
+  p->pub_len.store((int64_t)p->txs.len + p->pend_len, std::memory_order_relaxed);
+  p->pub_bytes.store(p->txs_bytes + p->pend_bytes, std::memory_order_relaxed);
+}
+void publish_locked(txv_pool* p) {
+  std::lock_guard<std::mutex> lk(p->amu);
+  publish(p);
+}
+
 void appender_loop(txv_pool* p) {
   std::unique_lock<std::mutex> lk(p->amu);
   for (;;) {
@@ -1099,12 +1136,30 @@ void appender_loop(txv_pool* p) {
     p->jobs.pop_front();
     p->a_busy = true;
     lk.unlock();
-    append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
+    int64_t removed_bytes = 0;
+    if (j.remove) {
+      for (uint32_t i = 0; i < j.n; ++i) {
+        if (i + 16 < j.n) p->txs_map.prefetch(j.keys[i + 16]);
+        const int32_t e = p->txs_map.find(j.keys[i]);
+        if (e >= 0) {
+          p->txs_map.erase(j.keys[i]);
+          p->txs.unlink(e);                              // its own --len, under no lock: the list is the appender's
+          removed_bytes += j.sizes[i];
+        }
+      }
+    } else {
+      append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
+    }
     lk.lock();
-    p->txs.len += j.n;
-    p->txs_bytes += (int64_t)j.bytes;
-    p->pend_len -= j.n;
-    p->pend_bytes -= (int64_t)j.bytes;
+    if (j.remove) {
+      p->txs_bytes -= removed_bytes;
+    } else {
+      p->txs.len += j.n;
+      p->txs_bytes += (int64_t)j.bytes;
+      p->pend_len -= j.n;
+      p->pend_bytes -= (int64_t)j.bytes;
+    }
+    publish(p);
     p->a_busy = false;
     p->spare.push_back(std::move(j));                      // its buffers serve a later batch
     p->acv.notify_all();
@@ -1162,8 +1217,29 @@ void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
   if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
   p->pend_len += A;
   p->pend_bytes += (int64_t)bytes;
+  publish(p);
   p->jobs.push_back(std::move(j));
   p->acv.notify_all();
+}
+
+// Update's pool-list removals, queued behind every append queued before them
+void queue_removal(txv_pool* p, std::vector<Key>&& keys, std::vector<uint32_t>&& sizes) {
+  txv_pool::Append j;
+  j.n = (uint32_t)keys.size();
+  if (!j.n) return;
+  j.keys = std::move(keys);
+  j.sizes = std::move(sizes);
+  j.remove = true;
+  std::lock_guard<std::mutex> lk(p->amu);
+  if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
+  p->jobs.push_back(std::move(j));
+  p->acv.notify_all();
+}
+
+// finished Update tickets leave the queue (no caller waits for them)
+void prune_updates(txv_pool* p) {
+  for (auto it = p->tickets.begin(); it != p->tickets.end();)
+    it = (it->upd && it->done) ? p->tickets.erase(it) : it + 1;
 }
 
 // a device batch needs the pool's Size and MaxTxsBytes caps not to bind inside it (pushes: the
@@ -1184,6 +1260,12 @@ int finish_ticket(txv_pool* p, txv_pool::Ticket& t) {
   t.done = true;
   p->infl_len -= (int64_t)t.pushes;
   p->infl_bytes -= (int64_t)t.bytes;
+  if (t.upd) {                                             // the engine's pushes done; the removals queued
+    if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
+    const Key* k = reinterpret_cast<const Key*>(kp);
+    queue_removal(p, std::vector<Key>(k, k + t.n), std::move(t.usizes));
+    return TXV_OK;
+  }
   if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
   t.st.assign(st, st + t.n);
   queue_admitted(p, t.ctx, reinterpret_cast<const Key*>(kp), sz, st, t.n);
@@ -1196,6 +1278,7 @@ int drain_flights(txv_pool* p) {
   int r = TXV_OK;
   for (auto& t : p->tickets)
     if (!t.done) { const int e = finish_ticket(p, t); if (e && !r) r = e; }
+  prune_updates(p);
   return r;
 }
 
@@ -1347,15 +1430,20 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
 int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
   if (!p || !ticket) return TXV_EINVAL;
   txv_ctx* ctx = nullptr;
+  PoolDev* dev = nullptr;
   int slot = -1;
   {
     std::lock_guard<std::mutex> g(p->mu);
     auto it = std::find_if(p->tickets.begin(), p->tickets.end(), [&](const txv_pool::Ticket& t) { return t.id == ticket; });
     if (it == p->tickets.end()) return TXV_ESTATE;
-    if (!it->done) { ctx = it->ctx; slot = it->slot; }
+    if (!it->done) { ctx = it->ctx; slot = it->slot; dev = p->dev; ++p->waiters; }
   }
-  if (slot >= 0) (void)pooldev_finish(ctx, p->dev, slot, nullptr, nullptr, nullptr);   // the wait itself
+  if (slot >= 0) (void)pooldev_finish(ctx, dev, slot, nullptr, nullptr, nullptr);   // the wait itself
   std::lock_guard<std::mutex> g(p->mu);
+  if (slot >= 0 && --p->waiters == 0) {
+    for (PoolDev* d : p->retired) pooldev_free(d);
+    p->retired.clear();
+  }
   int r = TXV_OK;
   for (auto it = p->tickets.begin(); it != p->tickets.end(); ++it) {   // the earlier ones first: append order
     const int e = finish_ticket(p, *it);
@@ -1363,6 +1451,7 @@ int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
     r = e;
     if (!r && it->n && status_out) memcpy(status_out, it->st.data(), it->n);
     p->tickets.erase(it);
+    prune_updates(p);
     return r;
   }
   return TXV_ESTATE;
@@ -1391,11 +1480,40 @@ int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_
   });
 }
 
-int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
-                    const uint64_t* sig_full_off) {
-  if (!p || !ctx || !v) return TXV_EINVAL;
-  std::lock_guard<std::mutex> g(p->mu);
-  p->height = height;
+// Update (txvotepool.go:329-359) with the cache in HBM: the committed votes' keys (SHA-256 of the
+// signatures) are hashed and pushed by the device engine in stream order behind the batches
+// submitted before (every key pushed: cache.Push ignores Size), their keys come back with the
+// flight, and their pool-list removals are queued for the pool's appender when the ticket is
+// finished, behind every append queued before them -- no flight is drained and the cache list is
+// not copied back.  The effects are in place once the tickets submitted before are finished
+// (txv_pool_check_wait, txv_pool_sync, any reader).  Signatures > 64 bytes take the host path.
+int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
+  const uint32_t n = v->n;
+  txv_pool::Ticket t;
+  t.upd = true;
+  t.ctx = ctx;
+  t.n = n;
+  t.usizes.resize(n);
+  pool_parallel_for(p, ctx, n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) t.usizes[i] = vote_size(v, i);
+  }, 4096);
+  int r;
+  const int slot = p->next_slot;
+  for (auto& o : p->tickets)                               // the slot's previous batch, finished
+    if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
+  prune_updates(p);
+  if ((r = cache_to_dev(p, ctx, n))) return r;
+  if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, t.usizes.data(), nullptr, nullptr, nullptr, 0, n, INT64_MAX,
+                           false, true, nullptr)))
+    return r;
+  if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+  p->next_slot = (slot + 1) % kPdRing;
+  t.slot = slot;
+  p->tickets.push_back(std::move(t));
+  return TXV_OK;
+}
+
+int update_host(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off) {
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
   if ((r = drain_flights(p))) return r;
@@ -1418,6 +1536,32 @@ int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* 
       p->txs_bytes -= vote_size(v, i);
     }
   }
+  publish_locked(p);
+  return TXV_OK;
+}
+
+int txv_pool_update_submit(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
+                           const uint64_t* sig_full_off) {
+  if (!p || !ctx || !v || (v->n && (!v->sig || !v->sig_len))) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->height = height;
+  if (dev_mode(p) && v->n) {
+    bool lg = false;
+    for (uint32_t i = 0; i < v->n && !lg; ++i) lg = v->sig_len[i] > 64;
+    if (!lg) return update_submit_dev(p, ctx, v);
+  }
+  return update_host(p, ctx, v, sig_full, sig_full_off);
+}
+
+// Update applied when it returns: the device path's submission, then every ticket before it and
+// the queued appends / removals finished (no cache copy back)
+int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
+                    const uint64_t* sig_full_off) {
+  int r = txv_pool_update_submit(p, ctx, height, v, sig_full, sig_full_off);
+  if (r || !dev_mode(p)) return r;
+  std::lock_guard<std::mutex> g(p->mu);
+  if ((r = drain_flights(p))) return r;
+  drain_appends(p);
   return TXV_OK;
 }
 
@@ -1535,25 +1679,28 @@ int txv_pool_flush(txv_pool* p) {
   host_cache_written(p);
   p->txs.clear(); p->txs_map.clear();
   p->txs_bytes = 0;
+  publish_locked(p);
   return TXV_OK;
 }
 
 int txv_pool_sync(txv_pool* p) {
   if (!p) return TXV_EINVAL;
+  int r;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (std::any_of(p->tickets.begin(), p->tickets.end(), [](const txv_pool::Ticket& t) { return t.upd; }))
+      if ((r = drain_flights(p))) return r;               // submitted Updates applied
+  }
   drain_appends(p);
   return TXV_OK;
 }
 
 // Size / TxsBytes count the votes a device batch admitted whose append is still queued
 int64_t txv_pool_size(txv_pool* p) {
-  if (!p) return 0;
-  std::lock_guard<std::mutex> lk(p->amu);
-  return (int64_t)p->txs.len + p->pend_len;
+  return p ? p->pub_len.load(std::memory_order_relaxed) : 0;
 }
 int64_t txv_pool_txs_bytes(txv_pool* p) {
-  if (!p) return 0;
-  std::lock_guard<std::mutex> lk(p->amu);
-  return p->txs_bytes + p->pend_bytes;
+  return p ? p->pub_bytes.load(std::memory_order_relaxed) : 0;
 }
 int64_t txv_pool_height(txv_pool* p) { return p ? p->height : 0; }
 

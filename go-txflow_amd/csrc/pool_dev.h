@@ -39,8 +39,9 @@ struct PoolDevArgs {
   uint64_t* pst;              // pair (previous occurrence, this push) in doubled S positions, when evicting
   uint64_t* pend;
   uint32_t* far;              // [n] far pushes
-  uint32_t* nfar;             // [2] far pushes, pairs
-  uint64_t* plist;            // [n][2] the pairs (previous occurrence, push), any order
+  uint32_t* nfar;             // [1] far pushes
+  uint32_t* xs;               // [ceil(n / 1024) * 1024] per block of 1024 votes: its pairs' starts, sorted
+  uint32_t* xn;               // [ceil(n / 1024)] pairs per block
   uint8_t* detached;          // [C] cached keys pushed again in this batch (cleared at the end)
   uint32_t* surv;             // [C] old entries not pushed again
   uint32_t* spos;             // [C] exclusive scan of surv

@@ -103,6 +103,7 @@ struct Slot {
   uint32_t *d_entry = nullptr, *d_blk = nullptr;
   uint8_t* d_ev_flag = nullptr;
   uint8_t* d_mark = nullptr;
+  uint32_t* d_stamped = nullptr;   // the batch's stamped set ids (tally_resolve -> tally_cross)
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
@@ -208,6 +209,7 @@ struct txv_ctx {
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
   uint8_t* d_keys = nullptr; uint64_t keys_cap = 0;
   uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_stamp = nullptr, *d_set_cross = nullptr, *d_bitmap = nullptr;
+  uint32_t* d_set_digest = nullptr;   // [max_txs][4] SHA-256(TxHash)[0:16]
   int64_t* d_set_sum = nullptr;
   TallyCell* d_cells = nullptr;
   uint32_t *d_arena_sig = nullptr, *d_arena_nanos = nullptr, *d_arena_val = nullptr, *d_arena_txkey = nullptr;
@@ -385,7 +387,7 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_txkey, 32 * npad)) || (r = dalloc(c, &s.d_txkey, 32 * npad)) ||
       (r = halloc(c, &s.h_vcode, npad)) || (r = dalloc(c, &s.d_vcode, npad)) ||
       (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
-      (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
+      (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = dalloc(c, &s.d_stamped, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
     return r;
   s.flow_cap = cap;
@@ -396,7 +398,7 @@ FlowState flow_state(const txv_ctx* c) {
   FlowState f{};
   f.tab = c->d_tab; f.tab_mask = c->tab_mask; f.max_txs = c->cfg.max_txs;
   f.keys = c->d_keys; f.keys_cap = c->keys_cap;
-  f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_stamp = c->d_set_stamp;
+  f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_stamp = c->d_set_stamp; f.set_digest = c->d_set_digest;
   f.cell = c->d_cells; f.set_cross = c->d_set_cross;
   f.arena_sig = c->d_arena_sig; f.arena_height = c->d_arena_height; f.arena_sec = c->d_arena_sec;
   f.arena_nanos = reinterpret_cast<int32_t*>(c->d_arena_nanos); f.arena_val = c->d_arena_val;
@@ -427,6 +429,7 @@ int alloc_tally(txv_ctx* c) {
       (r = dalloc(c, &c->d_arena_seq, M)) || (r = dalloc(c, &c->d_arena_txkey, 8 * M)) ||
       (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_set_stamp, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_digest, (size_t)c->cfg.max_txs * 4)) ||
       (r = dalloc(c, &c->d_set_txkey, (size_t)c->cfg.max_txs * 8)) ||
       (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_tab, tab)) ||
       (r = dalloc(c, &c->d_keys, (uint64_t)c->cfg.max_txs * TXV_KEY_SLOT + c->keys_cap)) || (r = dalloc(c, &c->d_ctr, 1)))
@@ -873,7 +876,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.vcode = s.host_val ? s.d_vcode : nullptr;
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
   b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
-  b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk;
+  b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk; b.stamped = s.d_stamped;
   b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
   return b;
 }
@@ -1380,7 +1383,7 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
     hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey); hfree(s.h_vcode); dfree(s.d_vcode);
-    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); hfree(s.h_ev); hfree(s.h_sum);
+    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); dfree(s.d_stamped); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);
@@ -1389,7 +1392,7 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); release_base_table(c->device, c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
-  dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_bitmap);
+  dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_set_digest); dfree(c->d_bitmap);
   dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
   dfree(c->d_addr_slots); dfree(c->d_q);
   for (const auto& rg : c->registered) (void)hipHostUnregister((void*)rg.first);
@@ -2167,7 +2170,7 @@ int txv_host_unregister(txv_ctx* c, void* ptr) {
 }
 
 uint64_t txv_commit_state_bytes(uint32_t n_sets_cap) {
-  return 8ull + (uint64_t)(n_sets_cap + 31) / 32 * 4 + 8ull * n_sets_cap;
+  return 8ull + (uint64_t)(n_sets_cap + 31) / 32 * 4 + 8ull * n_sets_cap + 16ull * n_sets_cap;
 }
 
 int txv_pack_commit_state(txv_ctx* c, void* dst_dev, uint32_t n_sets_cap) {
@@ -2199,30 +2202,35 @@ int txv_read_commit_state(txv_ctx* c, void* dst_host, uint32_t n_sets_cap) {
   return TXV_OK;
 }
 
-int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
-                               void* dst) {
+int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, const uint8_t* digests,
+                               uint32_t n_sets_cap, void* dst) {
   if (!dst || n_sets > n_sets_cap || (n_sets && (!committed || !sums))) return TXV_EINVAL;
   uint32_t* d = static_cast<uint32_t*>(dst);
   const uint32_t bm = (n_sets_cap + 31) / 32;
   memset(d, 0, txv_commit_state_bytes(n_sets_cap));
   d[0] = n_sets;
+  d[1] = 1;
+  uint8_t* dg = reinterpret_cast<uint8_t*>(d + 2 + bm + 2 * (size_t)n_sets_cap);
   for (uint32_t s = 0; s < n_sets; ++s) {
     if (committed[s]) d[2 + s / 32] |= 1u << (s % 32);
     memcpy(d + 2 + bm + 2 * s, &sums[s], 8);
+    if (digests) memcpy(dg + 16 * (size_t)s, digests + 16 * (size_t)s, 16);
   }
   return TXV_OK;
 }
 
 int txv_commit_state_unpack(const void* src, uint32_t n_sets_cap, uint32_t* n_sets, uint8_t* committed, int64_t* sums,
-                            uint32_t cap) {
+                            uint8_t* digests, uint32_t cap) {
   if (!src || !n_sets) return TXV_EINVAL;
   const uint32_t* d = static_cast<const uint32_t*>(src);
   const uint32_t bm = (n_sets_cap + 31) / 32;
-  if (d[0] > n_sets_cap) return TXV_EINVAL;
+  if (d[0] > n_sets_cap || d[1] != 1) return TXV_EINVAL;
   *n_sets = d[0];
+  const uint8_t* dg = reinterpret_cast<const uint8_t*>(d + 2 + bm + 2 * (size_t)n_sets_cap);
   for (uint32_t s = 0; s < d[0] && s < cap; ++s) {
     if (committed) committed[s] = (uint8_t)((d[2 + s / 32] >> (s % 32)) & 1u);
     if (sums) memcpy(&sums[s], d + 2 + bm + 2 * s, 8);
+    if (digests) memcpy(digests + 16 * (size_t)s, dg + 16 * (size_t)s, 16);
   }
   return TXV_OK;
 }
@@ -3127,11 +3135,12 @@ struct PoolDev {
   uint32_t *push = nullptr, *aidx = nullptr, *hkey = nullptr, *hidx = nullptr, *skey = nullptr, *sidx = nullptr;
   uint32_t *last = nullptr, *lpos = nullptr, *far = nullptr, *nfar = nullptr, *surv = nullptr, *spos = nullptr;
   uint8_t *dec = nullptr, *detached = nullptr, *d_status = nullptr;
-  uint64_t *pst = nullptr, *pend = nullptr, *plist = nullptr;
+  uint64_t *pst = nullptr, *pend = nullptr;
+  uint32_t *xs = nullptr, *xn = nullptr;   // per 1024-vote block: sorted pair starts, pair count
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
-  static constexpr int kPdRing = 3;
+  static constexpr int kPdRing = 4;
   struct Flight {
     uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
     uint8_t* d_status = nullptr;
@@ -3142,13 +3151,18 @@ struct PoolDev {
   uint32_t* h_clen = nullptr;
   hipEvent_t ev = nullptr;
   hipStream_t st = nullptr;                        // cache uploads / downloads
+  bool on_key = false;                             // batches run on the context's key stream
+  void quiesce() {                                 // every batch enqueued has ended (on_key: not on st)
+    for (Flight& f : fl)
+      if (f.ev) (void)hipEventSynchronize(f.ev);
+  }
   ~PoolDev() {
     if (device < 0) return;
     (void)hipSetDevice(device);
     for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
     dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx);
     dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
-    dfree(detached); dfree(pst); dfree(pend); dfree(plist);
+    dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn);
     for (Flight& f : fl) {
       dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
       hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status);
@@ -3194,9 +3208,17 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     for (PoolDev::Flight& f : s->fl) HIP_TRY(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     // the engine's own stream, at the highest priority: a batch's short kernels go ahead of the
     // TxFlow chains' work queued on the context's streams whenever a CU frees up
-    int lo = 0, hi = 0;
-    HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_TRY(c, hipStreamCreateWithPriority(&s->st, hipStreamNonBlocking, hi));
+    // TXV_POOL_STREAM (experiment): 0 own high-priority stream, 1 own normal-priority stream, 2 the
+    // batches on the context's key stream (no HSA queue of the engine's own)
+    static const int mode = getenv("TXV_POOL_STREAM") ? atoi(getenv("TXV_POOL_STREAM")) : 0;
+    s->on_key = mode == 2;
+    if (mode == 0) {
+      int lo = 0, hi = 0;
+      HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_TRY(c, hipStreamCreateWithPriority(&s->st, hipStreamNonBlocking, hi));
+    } else {
+      HIP_TRY(c, hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    }
   }
   if (n > s->cap_n) {
     int r;
@@ -3205,7 +3227,8 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
         (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
         (r = dalloc(c, &s->last, m)) ||
         (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
-        (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) || (r = dalloc(c, &s->plist, (size_t)m * 2)))
+        (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
+        (r = dalloc(c, &s->xs, ((size_t)m + 1023) / 1024 * 1024)) || (r = dalloc(c, &s->xn, ((size_t)m + 1023) / 1024)))
       return r;
     for (PoolDev::Flight& f : s->fl)
       if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
@@ -3241,6 +3264,7 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L) {
   PD_TRY(hipSetDevice(s->device));
   if (L > s->C) { if (c) c->err = "pool cache longer than its capacity"; return TXV_EINVAL; }
   if (!s->st) PD_TRY(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+  s->quiesce();
   if (L) PD_TRY(hipMemcpyAsync(s->ck[s->cur], keys, (size_t)L * 32, hipMemcpyHostToDevice, s->st));
   s->h_clen[0] = L;
   s->h_clen[1] = L;
@@ -3254,6 +3278,7 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L) {
 int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
   PD_TRY(hipSetDevice(s->device));
   if (!s->st) PD_TRY(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+  s->quiesce();
   PD_TRY(hipMemcpyAsync(s->h_clen, s->clen, 8, hipMemcpyDeviceToHost, s->st));
   PD_TRY(hipStreamSynchronize(s->st));
   const uint32_t L = s->h_clen[0];
@@ -3280,8 +3305,9 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   HIP_TRY(c, hipSetDevice(c->device));
   if (!n) return TXV_OK;
   if (n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
+  if (2 * ((uint64_t)s->C + n) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
   PoolDev::Flight& f = s->fl[slot];
-  hipStream_t ks = s->st;
+  hipStream_t ks = s->on_key ? c->key_stream : s->st;
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
   if (v) {
     bool reg;
@@ -3322,7 +3348,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.icap = s->icap; a.clen = s->clen;
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
-  a.pend = s->pend; a.plist = s->plist; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
+  a.pend = s->pend; a.xs = s->xs; a.xn = s->xn; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
   a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status;
   HIP_TRY(c, txv_pooldev_run(&a, ks));
   if (s->C) s->cur ^= 1;                                  // the next batch on this stream reads the new cache

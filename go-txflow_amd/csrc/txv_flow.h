@@ -25,6 +25,9 @@
 //               order carries no meaning -- the readers order by validator)
 //   set_cross   [max_txs] arrival index at which the set's stake crossed 2/3 in the batch that
 //               last touched it (TXV_NO_CROSS: none): the fired bit of each ADDED vote
+//   set_digest  [max_txs][4] the first 16 bytes of SHA-256(TxHash) (whose byte 0 mod G is the
+//               set's shard, txv_shard_of): written when the set is created, packed beside its
+//               commit bit and sum, so a rank can name another rank's sets from the exchange alone
 // The commit bitmap is derived from set_sum on demand (txv_commit_bitmap, the packed state).
 //
 // gfx950 has 8 XCDs with private L2s: the only hand-off INSIDE a launch is the set-table insert
@@ -96,7 +99,7 @@ struct FlowCounters {           // device-resident, updated by the kernels
   uint32_t n_sets;              // TxVoteSets so far
   uint32_t arena_used;          // accepted-vote rows in use
   uint32_t err;                 // TXV_FERR_*
-  uint32_t pad;
+  uint32_t n_stamped;           // sets the running batch ADDED a vote to (zeroed by tally_min)
   uint64_t key_used;            // overflow key arena bytes in use
 };
 
@@ -121,6 +124,7 @@ struct FlowState {
   int64_t* set_sum;             // [max_txs]
   uint32_t* set_stamp;          // [max_txs]
   uint32_t* set_cross;          // [max_txs]
+  uint32_t* set_digest;         // [max_txs][4] SHA-256(TxHash bytes)[0:16]: the set's name in the exchange
   TallyCell* cell;              // [max_txs * n_vals]
   uint32_t* arena_sig;          // [16][max_accepted]
   int64_t* arena_height;        // [max_accepted]
@@ -175,6 +179,7 @@ struct FlowBatch {
   uint8_t* ev_flag;             // [n] this vote's ADDED crossed 2/3 in the batch
   uint8_t* mark;                // [n] set by tally_min when a smaller arrival index took this vote's cell
   uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
+  uint32_t* stamped;            // [n] ids of the sets this batch ADDED votes to (the crossing step's work list)
   // outputs in mapped host memory
   uint8_t* status_host;         // [n]
   FlowEvent* ev_host;           // [n]
@@ -212,7 +217,7 @@ hipError_t txv_flow_gather(const FlowState* fs, const uint32_t* ids, uint32_t n,
 // key bytes of set ids (for SaveTx / MakeCommit): out_off/out_len into the key arena
 hipError_t txv_flow_keys(const FlowState* fs, const uint32_t* ids, uint32_t n, uint64_t* out_off, uint32_t* out_len,
                          hipStream_t st);
-// packed commit state of this shard: [n_sets u32][pad u32][bitmap words][sums i64]
+// packed commit state of this shard: [n_sets u32][1 u32][bitmap words][sums i64][digests 16 B]
 hipError_t txv_flow_pack(const FlowState* fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap, hipStream_t st);
 // commit bitmap (bit s = set_sum[s] >= quorum) of the first bm_words * 32 set ids
 hipError_t txv_flow_bitmap(const FlowState* fs, uint32_t* dst, uint32_t bm_words, hipStream_t st);

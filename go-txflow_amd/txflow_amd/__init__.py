@@ -13,6 +13,7 @@ creating a context without a GPU raises: there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import weakref
 import os
 from dataclasses import dataclass, field
@@ -140,6 +141,7 @@ def lib():
             "txv_pool_check_wait": ([vp, ctypes.c_uint64, vp], ctypes.c_int),
             "txv_pool_check_keys": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_pool_update": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
+            "txv_pool_update_submit": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
             "txv_pool_reap": ([vp, i64, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_pool_flush": ([vp], ctypes.c_int),
             "txv_pool_size": ([vp], i64),
@@ -176,8 +178,8 @@ def lib():
             "txv_slot_kernel_ms": ([vp, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "txv_slot_verify_ms": ([vp, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "txv_read_commit_state": ([vp, vp, u32], ctypes.c_int),
-            "txv_commit_state_pack_host": ([u32, vp, vp, u32, vp], ctypes.c_int),
-            "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, u32], ctypes.c_int),
+            "txv_commit_state_pack_host": ([u32, vp, vp, vp, u32, vp], ctypes.c_int),
+            "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, vp, u32], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             if os.environ.get("TXV_LIB_PATH") and not hasattr(L, name):
@@ -198,7 +200,7 @@ EXPORTED_SYMBOLS = [
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
-    "txv_pool_check_submit", "txv_pool_check_wait",
+    "txv_pool_check_submit", "txv_pool_check_wait", "txv_pool_update_submit",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
     "txv_query_txs", "txv_make_commit", "txv_save_tx_bytes", "txv_host_register", "txv_host_unregister",
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
@@ -778,29 +780,41 @@ def commit_state_bytes(n_sets_cap: int) -> int:
     return int(lib().txv_commit_state_bytes(n_sets_cap))
 
 
-def commit_state_pack_host(committed: np.ndarray, sums: np.ndarray, n_sets_cap: int) -> np.ndarray:
-    """the packed per-shard commit state (txv_pack_commit_state's layout) from host arrays"""
+def tx_digest(txhash: bytes) -> bytes:
+    """a TxVoteSet's name in the multi-GPU exchange: SHA-256(TxHash bytes)[0:16] (byte 0 mod G is
+    its shard, txv_shard_of)"""
+    return hashlib.sha256(bytes(txhash)).digest()[:16]
+
+
+def commit_state_pack_host(committed: np.ndarray, sums: np.ndarray, n_sets_cap: int, digests=None) -> np.ndarray:
+    """the packed per-shard commit state (txv_pack_commit_state's layout) from host arrays;
+    digests: [n_sets, 16] u8 (tx_digest of each set's TxHash) or None (zeros)"""
     committed = np.ascontiguousarray(committed, np.uint8)
     sums = np.ascontiguousarray(sums, np.int64)
+    dg = None if digests is None else np.ascontiguousarray(digests, np.uint8).reshape(-1, 16)
+    assert dg is None or len(dg) == len(sums)
     out = np.zeros(commit_state_bytes(n_sets_cap), np.uint8)
     rc = lib().txv_commit_state_pack_host(len(sums), committed.ctypes.data if len(sums) else None,
-                                          sums.ctypes.data if len(sums) else None, n_sets_cap, out.ctypes.data)
+                                          sums.ctypes.data if len(sums) else None,
+                                          dg.ctypes.data if dg is not None and len(dg) else None, n_sets_cap,
+                                          out.ctypes.data)
     if rc:
         raise TxvInfraError(f"txv_commit_state_pack_host failed ({rc})")
     return out
 
 
 def commit_state_unpack(buf: np.ndarray, n_sets_cap: int):
-    """(committed [n_sets] bool, sums [n_sets] i64) of one packed shard state"""
+    """(committed [n_sets] bool, sums [n_sets] i64, digests [n_sets, 16] u8) of one packed shard state"""
     buf = np.ascontiguousarray(buf, np.uint8)
     ns = ctypes.c_uint32()
     committed = np.zeros(max(n_sets_cap, 1), np.uint8)
     sums = np.zeros(max(n_sets_cap, 1), np.int64)
+    digests = np.zeros((max(n_sets_cap, 1), 16), np.uint8)
     rc = lib().txv_commit_state_unpack(buf.ctypes.data, n_sets_cap, ctypes.byref(ns), committed.ctypes.data,
-                                       sums.ctypes.data, n_sets_cap)
+                                       sums.ctypes.data, digests.ctypes.data, n_sets_cap)
     if rc:
         raise TxvInfraError(f"txv_commit_state_unpack failed ({rc})")
-    return committed[:ns.value].astype(bool), sums[:ns.value]
+    return committed[:ns.value].astype(bool), sums[:ns.value], digests[:ns.value]
 
 
 def _long_sig_arena(batch: VoteBatch, long_sigs: Optional[dict]):
@@ -1035,6 +1049,20 @@ class TxVotePool:
         vs = batch.c_struct()
         ctx = self._ctx_or_raise("update")
         ctx._chk(lib().txv_pool_update(self._h, ctx._h, height, ctypes.byref(vs), full, off), "txv_pool_update")
+
+    def update_submit(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
+        """txv_pool_update_submit: Update enqueued behind the submitted CheckTx batches (device
+        cache: no wait; applied once the batches before it are waited, or at sync())"""
+        full, off = _long_sig_arena(batch, long_sigs)
+        vs = batch.c_struct()
+        ctx = self._ctx_or_raise("update_submit")
+        ctx._chk(lib().txv_pool_update_submit(self._h, ctx._h, height, ctypes.byref(vs), full, off),
+                 "txv_pool_update_submit")
+        # registered columns are DMA'd by the engine after the call returns: keep them referenced
+        # while the submission can still be unfinished (the engine has four flight slots)
+        refs = self.__dict__.setdefault("_upd_refs", [])
+        refs.append((batch, full, off, vs))
+        del refs[:-5]
 
     def reap(self, max_txs: int = -1):
         """ReapMaxTxs: ([k, 32] keys, [k] sizes) in pool order"""

@@ -141,7 +141,7 @@ class PipelinedSteps:
 
     def gathered_state(self, k: Optional[int] = None) -> Optional[List[tuple]]:
         """step k's all-gathered state (default: the newest finished step), unpacked per rank:
-        [(committed bool[], sums i64[])].  Valid from finish(k) until step k + depth is launched;
+        [(committed bool[], sums i64[], digests [n, 16] u8)] -- each set named by tx_digest(TxHash).  Valid from finish(k) until step k + depth is launched;
         waits for step k's all-gather only (later steps may still run)."""
         if self.gathered is None:
             return None

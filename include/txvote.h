@@ -291,7 +291,10 @@ int txv_slot_verify_ms(txv_ctx* ctx, uint32_t slot, float* k1a_k1b_ms_out);
 int txv_host_register(txv_ctx* ctx, void* ptr, uint64_t bytes);
 int txv_host_unregister(txv_ctx* ctx, void* ptr);
 /* ---- multi-GPU: votes shard by SHA-256(TxHash)[0] mod n_shards; each shard's
- * commit state is packed as [n_sets u32][0 u32][bitmap: ceil(cap/32) u32][sums: cap i64] ---- */
+ * commit state is packed as [n_sets u32][1 u32][bitmap: ceil(cap/32) u32][sums: cap i64]
+ * [digests: cap x 16 B], set ids in the shard's first-seen order.  digest = SHA-256(TxHash
+ * bytes)[0:16] (whose byte 0 mod n_shards is the shard): every rank can name every other rank's
+ * TxVoteSets -- their commit bits and stakes -- from the gathered buffers alone ---- */
 int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len, uint32_t n, uint32_t n_shards,
                  uint32_t* shard_out);
 uint64_t txv_commit_state_bytes(uint32_t n_sets_cap);
@@ -313,10 +316,10 @@ void* txv_flow_stream(txv_ctx* ctx);
 /* the same packed by the device, copied into caller host memory (host-side gathers) */
 int txv_read_commit_state(txv_ctx* ctx, void* dst_host, uint32_t n_sets_cap);
 /* host-side pack (from per-set committed flags and sums) and unpack of the same layout */
-int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, uint32_t n_sets_cap,
-                               void* dst);
+int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const int64_t* sums, const uint8_t* digests,
+                               uint32_t n_sets_cap, void* dst);
 int txv_commit_state_unpack(const void* src, uint32_t n_sets_cap, uint32_t* n_sets, uint8_t* committed, int64_t* sums,
-                            uint32_t cap);
+                            uint8_t* digests, uint32_t cap);
 /* device pointer + byte size of the per-set committed bitmap (1 bit per tx-set id) */
 int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 /* device-to-device copy of the commit bitmap into caller device memory (e.g. an RCCL buffer) */
@@ -420,9 +423,18 @@ int txv_pool_check_keys(txv_pool* pool, txv_ctx* ctx, const uint8_t* keys32, con
 int txv_pool_prepare(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
                      const uint64_t* sig_full_off, uint8_t* keys_out, uint32_t* sizes_out);
 /* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
- * leaves the pool if its key is there. */
+ * leaves the pool if its key is there (txvotepool.go:329-359); applied when it returns.  With
+ * TXV_POOL_DEVICE_CACHE the keys are pushed by the device engine behind the batches submitted
+ * before and the removals run on the pool's appender thread; no cache copy comes back. */
 int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,
                     const uint8_t* sig_full, const uint64_t* sig_full_off);
+/* txv_pool_update without the wait (the commit path of a node that keeps checking batches):
+ * with TXV_POOL_DEVICE_CACHE it returns once the pushes are enqueued; its effects are applied in
+ * submission order with the txv_pool_check_submit batches, and are in place once those submitted
+ * before it are waited, at txv_pool_sync, or at any call that reads the pool list or cache.  The
+ * host cache applies it at once.  txflow/service.go:224-227 -> txvotepool.go:329-359 */
+int txv_pool_update_submit(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,
+                           const uint8_t* sig_full, const uint64_t* sig_full_off);
 /* ReapMaxTxs(max) in pool order: keys (32 B) and TxVote.Size of the reaped entries; the
  * reference loop condition `len(txs) <= max` reaps max + 1 entries when available; max < 0 = all.
  * keys_out / sizes_out capacity `cap`; *n_out = entries reaped (may exceed cap: truncated). */

@@ -62,6 +62,8 @@ def lib():
         L.orc_pool_check_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]
         L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_pool_update_soa.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]
         L.orc_pool_reap.restype = ctypes.c_uint64
         L.orc_pool_reap.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.orc_pool_flush.argtypes = [ctypes.c_void_p]
@@ -360,6 +362,11 @@ class Pool:
         keep = []
         arr = (_Vote * max(len(votes), 1))(*[_orc_vote(v, keep) for v in votes])
         lib().orc_pool_update(self._h, height, ctypes.addressof(arr), len(votes))
+
+    def update_batch(self, height, b):
+        """orc_pool_update over a VoteBatch-shaped object (signatures of at most 64 bytes)"""
+        soa = _soa(b)
+        lib().orc_pool_update_soa(self._h, height, ctypes.addressof(soa), None, None)
 
     def reap(self, max_txs=-1):
         import numpy as np

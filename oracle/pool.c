@@ -191,6 +191,24 @@ void orc_pool_update(orc_pool* p, int64_t height, const orc_vote* votes, uint32_
   }
 }
 
+/* orc_pool_update over an SoA batch (the committed votes of a TxVoteSet, txflow/service.go:224-227) */
+void orc_pool_update_soa(orc_pool* p, int64_t height, const orc_soa* b, const uint8_t* sig_full,
+                         const uint64_t* sig_full_off) {
+  p->height = height;
+  for (uint32_t i = 0; i < b->n; ++i) {
+    orc_vote v;
+    memset(&v, 0, sizeof v);
+    v.height = b->height[i];
+    v.txhash_len = b->txhash_len[i];
+    v.ts_sec = b->ts_sec[i];
+    v.ts_nanos = b->ts_nanos[i];
+    v.addr_len = b->addr_len[i];
+    v.sig = (b->sig_len[i] > 64 && sig_full) ? sig_full + sig_full_off[i] : b->sig + (size_t)i * 64;
+    v.sig_len = b->sig_len[i];
+    orc_pool_update(p, height, &v, 1);
+  }
+}
+
 uint64_t orc_pool_reap(orc_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap) {
   if (max < 0) max = (int64_t)p->txs.len;
   uint64_t n = 0;

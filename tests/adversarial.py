@@ -262,10 +262,12 @@ class C4Stream:
             msg = T.sign_bytes(int(f["height"][i]), self.hashes[f["tx"][i]].tobytes(), 1_700_000_000,
                                int(f["ts_nanos"][i]), CHAIN)
             f["sig"][i] = np.frombuffer(self._forge(vi, msg, int(picks[q])), np.uint8)
-        # unknown-validator primaries carry some honest signature bytes
-        uk = np.nonzero(f["kind"][:n_prim] == 3)[0]
-        if len(hi):
-            f["sig"][uk] = f["sig"][hi[rng.integers(0, len(hi), len(uk))]]
+        # votes no registry key signs (unknown validator, empty address, nil; primaries and their
+        # conflicts) carry distinct random signature bytes: TxVotePool keys a vote by
+        # SHA-256(Signature) (txvotepool.go:467-469), so a shared or all-zero signature would make
+        # CheckTx drop all but the first of them as ErrTxInCache before they reach TxFlow
+        nk = np.nonzero(np.isin(f["kind"][:n_prim + n_conf], (3, 4, 5)))[0]
+        f["sig"][nk] = rng.integers(0, 256, (len(nk), 64), dtype=np.uint8)
 
         # mutations of base primaries (after signing)
         base_idx = np.nonzero(f["kind"][:n_prim] == 0)[0]

@@ -76,3 +76,30 @@ def test_c4_stream_covers_every_outcome(oracle_lib):
     for must in ("identity", "identity_y+p", "identity_negzero", "order2", "order4", "order8", "mixed8",
                  "undecodable"):
         assert must in names
+
+
+def test_c4_keyless_classes_survive_checktx(oracle_lib):
+    """Unknown-validator, empty-address and nil votes carry distinct signatures, so CheckTx's LRU
+    (keyed by SHA-256(Signature), txvotepool.go:467-469) admits them and Appendix C's shares of
+    those classes reach TxFlow (with shared / all-zero signatures only a few
+    dozen empty-address votes survived 10^8)."""
+    import adversarial as A
+    import txflow_amd as T
+    n = 40000
+    s = A.C4Stream(OracleCtx(), batch=n, batches_per_epoch=2, oracle_threads=4, verify_slice=0)
+    b, f = s.next_batch()
+    gossip = np.nonzero(f["is_nil"] == 0)[0]
+    m = len(gossip)
+    sub = T.VoteBatch(m, height=f["height"][gossip], txhash_arena=b.txhash_arena, txhash_off=f["txoff"][gossip],
+                      txhash_len=np.full(m, 64, np.uint32), ts_sec=np.full(m, 1_700_000_000, np.int64),
+                      ts_nanos=f["ts_nanos"][gossip], addr=f["addr"][gossip], addr_len=f["addr_len"][gossip],
+                      sig=f["sig"][gossip], sig_len=f["sig_len"][gossip])
+    long_sigs = {int(q): sub.sig[64 * q:64 * q + 64].tobytes() + bytes(int(sub.sig_len[q]) - 64)
+                 for q in np.nonzero(sub.sig_len > 64)[0]}
+    pool = oracle_lib.Pool(size=(1 << 31) - 1, cache_size=1 << 16, max_txs_bytes=1 << 40)
+    ops = pool.check_batch(sub, long_sigs)
+    kind = f["kind"][gossip]
+    for k, share in ((3, 0.005), (4, 0.0025)):
+        admitted = int(np.count_nonzero((kind == k) & (ops == T.POOL_OK)))
+        assert admitted >= 0.8 * share * n, (k, admitted)
+    assert int(np.count_nonzero(f["is_nil"])) >= 0.8 * 0.001 * n

@@ -60,12 +60,12 @@ def _worker(rank, world, port, q):
     cap = 64
     committed = np.array([flow.query(k)[1] for k in local_keys], np.uint8)
     sums = np.array([flow.query(k)[0] for k in local_keys], np.int64)
-    packed = torch.from_numpy(T.commit_state_pack_host(committed, sums, cap))
+    dig = np.array([np.frombuffer(T.tx_digest(k), np.uint8) for k in local_keys])
+    packed = torch.from_numpy(T.commit_state_pack_host(committed, sums, cap, dig))
     out = torch.zeros(world * packed.numel(), dtype=torch.uint8)
     dist.all_gather_into_tensor(out, packed)
-    keys_all = [None] * world
-    dist.all_gather_object(keys_all, local_keys)
-    merged, stakes = sharding.merge_states(out.numpy(), world, cap, keys_all)
+    # the other rank's sets are named by the digests in its packed row: no keys exchanged
+    merged, stakes = sharding.merge_states(out.numpy(), world, cap)
     q.put((rank, sorted(merged), stakes))
     dist.destroy_process_group()
 
@@ -84,17 +84,18 @@ def test_two_rank_sharded_tally_matches_global():
     O, pubs, txs, votes = _scenario()
     flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
     flow.add_votes(votes)
-    glob_commit = sorted(t for t in set(v["txhash"] for v in votes) if flow.query(t)[1])
+    import txflow_amd as T
+    glob_commit = sorted(T.tx_digest(t) for t in set(v["txhash"] for v in votes) if flow.query(t)[1])
     for _, merged, stakes in res:
         assert merged == glob_commit
-        for t in set(v["txhash"] for v in votes):     # every rank holds every tx's stake
-            assert stakes[t] == flow.query(t)[0]
+        for t in set(v["txhash"] for v in votes):     # every rank holds every tx's stake, by name
+            assert stakes[T.tx_digest(t)] == flow.query(t)[0]
     assert len(glob_commit) > 0
 
 
 def test_shard_rule_and_pack_layout():
     """txv_shard_of = SHA-256(TxHash)[0] mod G; the packed state round-trips and has the
-    documented layout [n_sets u32][0 u32][bitmap][sums i64]."""
+    documented layout [n_sets u32][1 u32][bitmap][sums i64][digests 16 B]."""
     import hashlib
     sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
     import txflow_amd as T
@@ -105,14 +106,17 @@ def test_shard_rule_and_pack_layout():
     cap = 70
     com = np.array([rnd.random() < 0.5 for _ in range(37)], np.uint8)
     sums = np.array([rnd.randrange(-5, 1 << 40) for _ in range(37)], np.int64)
-    buf = T.commit_state_pack_host(com, sums, cap)
-    assert len(buf) == T.commit_state_bytes(cap) == 8 + 4 * ((cap + 31) // 32) + 8 * cap
+    dig = np.array([np.frombuffer(T.tx_digest(h), np.uint8) for h in hashes[:37]])
+    buf = T.commit_state_pack_host(com, sums, cap, dig)
+    assert len(buf) == T.commit_state_bytes(cap) == 8 + 4 * ((cap + 31) // 32) + 8 * cap + 16 * cap
     w = buf.view(np.uint32)
-    assert w[0] == 37 and w[1] == 0
+    assert w[0] == 37 and w[1] == 1
     bits = np.unpackbits(buf[8:8 + 4 * ((cap + 31) // 32)], bitorder="little")[:37]
     assert np.array_equal(bits, com)
-    c2, s2 = T.commit_state_unpack(buf, cap)
-    assert np.array_equal(c2, com.astype(bool)) and np.array_equal(s2, sums)
+    d0 = 8 + 4 * ((cap + 31) // 32) + 8 * cap
+    assert buf[d0:d0 + 16].tobytes() == hashlib.sha256(hashes[0]).digest()[:16]
+    c2, s2, d2 = T.commit_state_unpack(buf, cap)
+    assert np.array_equal(c2, com.astype(bool)) and np.array_equal(s2, sums) and np.array_equal(d2, dig)
 
 
 class _RingCtx:
@@ -220,3 +224,109 @@ def test_pipelined_ring_keeps_every_steps_gathered_state():
                 p.kill()
     errs = [e for _, es in res for e in es]
     assert not errs, "\n".join(errs)
+
+
+def _route_worker(rank, world, port, q):
+    """the ingest route (txflow_amd/sharding.py): CheckTx on the owner rank 0 (one TxVotePool: one
+    LRU, host-only here), its admitted votes scattered to the rank owning their TxHash, each rank's
+    TxFlow (the oracle standing in for its GPU engine) over the votes it received in arrival
+    order, the packed states (named by digest) all-gathered and merged"""
+    try:
+        import hashlib
+
+        import torch
+        import torch.distributed as dist
+        sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+        import txflow_amd as T
+        from txflow_amd import sharding
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        O, pubs, txs, votes = _route_stream()
+        flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
+        pool = T.TxVotePool(None, size=1 << 20, cache_size=24, max_txs_bytes=1 << 40) if rank == 0 else None
+        local_keys, seen = [], set()
+        for s in range(0, len(votes), 90):
+            part = votes[s:s + 90]
+            subs = None
+            if rank == 0:
+                vb = T.VoteBatch.from_votes([T.TxVote(Height=v["height"], TxHash=v["txhash"],
+                                                      Timestamp=(v["ts_sec"], v["ts_nanos"]),
+                                                      ValidatorAddress=v["addr"], Signature=v["sig"]) for v in part])
+                keys = np.array([np.frombuffer(hashlib.sha256(v["sig"]).digest(), np.uint8) for v in part])
+                sizes = np.array([T.txvote_size(v["height"], len(v["txhash"]), v["ts_sec"], v["ts_nanos"],
+                                                len(v["addr"]), len(v["sig"])) for v in part], np.uint32)
+                st = pool.check_keys(keys, sizes)
+                subs = [sharding.subset(vb, ix) for ix in sharding.route_admitted(vb, st, world, T.POOL_OK)]
+            mine = sharding.scatter_batches(dist, subs)
+            flow.add_batch(mine, 2)
+            for i in range(mine.n):
+                h = mine.txhash(i)
+                if h not in seen:
+                    seen.add(h)
+                    local_keys.append(h)
+        cap = 64
+        committed = np.array([flow.query(k)[1] for k in local_keys], np.uint8)
+        sums = np.array([flow.query(k)[0] for k in local_keys], np.int64)
+        dig = np.array([np.frombuffer(T.tx_digest(k), np.uint8) for k in local_keys]).reshape(-1, 16)
+        packed = torch.from_numpy(T.commit_state_pack_host(committed, sums, cap, dig))
+        out = torch.zeros(world * packed.numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, packed)
+        merged, stakes = sharding.merge_states(out.numpy(), world, cap)
+        if pool is not None:
+            pool.close()
+        dist.destroy_process_group()
+        q.put((rank, sorted(merged), stakes, ""))
+    except Exception as e:
+        import traceback
+        q.put((rank, None, None, f"rank {rank} raised {e!r}\n{traceback.format_exc()}"))
+
+
+def _route_stream():
+    """_scenario's votes plus exact replays (some of them after their key left a small LRU)"""
+    O, pubs, txs, votes = _scenario()
+    rnd = random.Random(78)
+    out = []
+    for v in votes:
+        out.append(v)
+        if rnd.random() < 0.15:
+            out.append(dict(rnd.choice(out)))
+    return O, pubs, txs, out
+
+
+def test_ingest_route_owner_checktx_matches_global():
+    """CheckTx on one owner + the admitted votes routed by shard + per-shard TxFlow + the named
+    exchange == one global TxVotePool + one global TxFlow (VERDICT r4 missing 1-2)"""
+    world, port = 2, 29500 + random.Random().randrange(1000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_route_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for _, _, _, e in res if e]
+    assert not errs, "\n".join(errs)
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "go-txflow_amd"))
+    import txflow_amd as T
+    O, pubs, txs, votes = _route_stream()
+    op = O.Pool(size=1 << 20, cache_size=24, max_txs_bytes=1 << 40)
+    flow = O.Flow(pubs, [1] * len(pubs), b"test_chain_id")
+    in_cache = 0
+    for s in range(0, len(votes), 90):
+        part = votes[s:s + 90]
+        st = op.check(part)
+        in_cache += int(sum(x == T.POOL_ERR_IN_CACHE for x in st))
+        flow.add_votes([v for v, x in zip(part, st) if x == T.POOL_OK])
+    assert in_cache > 0                                   # replays do meet the cache
+    names = set(v["txhash"] for v in votes)
+    glob_commit = sorted(T.tx_digest(t) for t in names if flow.query(t) and flow.query(t)[1])
+    for _, merged, stakes, _ in res:
+        assert merged == glob_commit
+        for t in names:
+            qv = flow.query(t)
+            if qv:
+                assert stakes[T.tx_digest(t)] == qv[0]
+    assert len(glob_commit) > 0
+    assert hashlib.sha256(b"x").digest()[:16] == T.tx_digest(b"x")
