@@ -201,6 +201,7 @@ def c5_expected_pool(wl, cache_size: int):
     return [op.check_batch(b) for b in wl.batches]
 
 
+C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in flight in the C5 leg (<= 3)
 C5_POOL_SIZE = 8 * 65536  # TxVotePool Size cap of the C5 legs: committed votes leave the pool (Update)
 
 
@@ -336,7 +337,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             import threading
             checked = queue.Queue(maxsize=2)
             tickets = queue.Queue()
-            slots = threading.Semaphore(2)
+            slots = threading.Semaphore(C5_INFLIGHT)
             pool_st = [None] * len(wl.batches)
             dev_ms, dev_split = [], []        # per batch in the pipeline: slot events (HIP, per stream)
             # CheckTx batches and Updates reach the pool from different threads (as the reactor's

@@ -99,19 +99,113 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
   return -1;
 }
 
-// pushes, sort input
+// Single-pass exclusive scans of 0/1 flags (decoupled look-back) fused into the kernels that
+// produce the flags, instead of two hipcub launches per scan.  A block takes the next tile of
+// kTile items by ticket, so every tile it waits for belongs to a block that is already running;
+// it ranks its tile's flags (ballots), publishes the tile's aggregate, sums its predecessors'
+// published words back to the first inclusive prefix, and publishes its own.  The words carry the
+// batch's epoch: nothing is cleared between batches.
+constexpr uint32_t kTile = 1024;               // 256 threads x 4 rounds; item = tile * 1024 + 256 k + t
+__device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint32_t flag, uint32_t v) {
+  return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | ((uint64_t)flag << 32) | v;
+}
+// exclusive prefix of tile `tile` (thread 0 of its block): flag 1 = aggregate, 2 = inclusive
+__device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, uint32_t agg) {
+  if (tile == 0) {
+    __hip_atomic_store(st, tile_word(epoch, 2, agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __hip_atomic_store(st + tile, tile_word(epoch, 1, agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t prefix = 0;
+  uint32_t spins = 0;
+  for (int32_t j = (int32_t)tile - 1; j >= 0;) {
+    const uint64_t w = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t f = (uint32_t)(w >> 32) & 3u;
+    if ((uint32_t)(w >> 34) != (epoch & 0x3FFFFFFFu) || f == 0) {
+      // a predecessor's block is running (tickets are taken at block start): it publishes within
+      // microseconds; the bound only keeps a broken invariant from hanging the queue
+      if (++spins > (1u << 24)) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    prefix += (uint32_t)w;
+    if (f == 2) break;
+    --j;
+  }
+  __hip_atomic_store(st + tile, tile_word(epoch, 2, prefix + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
+// the next tile of chain `ch` for this block
+__device__ __forceinline__ uint32_t take_tile(uint32_t* tk) {
+  __shared__ uint32_t s_tile;
+  if (threadIdx.x == 0) s_tile = atomicAdd(tk, 1u);
+  __syncthreads();
+  return s_tile;
+}
+// exclusive ranks of the 4 flags of each thread in item order, plus the tile's exclusive prefix
+__device__ __forceinline__ void tile_scan(const bool f[4], uint32_t out[4], uint64_t* st, uint32_t tile, uint32_t epoch) {
+  __shared__ uint32_t cnt[4][4];
+  __shared__ uint32_t s_prefix;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    m[k] = __ballot(f[k]);
+    if (lane == 0) cnt[k][w] = (uint32_t)__popcll(m[k]);
+  }
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t before = 0, round = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      before += q < w ? cnt[k][q] : 0u;
+      round += cnt[k][q];
+    }
+    out[k] = run + before + (uint32_t)__popcll(m[k] & below);
+    run += round;
+  }
+  if (threadIdx.x == 0) s_prefix = tile_lookback(st, tile, epoch, run);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[k] += s_prefix;
+}
+
+// pushes, sort input, and aidx = exclusive scan of the pushes (the push's index in S after the
+// cache); the ticket counters of pd_status's two scans are reset here
 __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i == 0) a.nfar[0] = 0;   // far pushes (appended by pd_link)
-  if (i >= a.n) return;
-  const bool ok = !a.valid || a.valid[i] == a.valid_ok;
-  const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
-  a.push[i] = p;
-  // non-pushes sort into a run of their own at the end: a push's slice is clamped below it, so a
-  // key whose slice is 0xFFFFFFFF never shares a run with them (pd_link scans its run backwards)
-  a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2], 0xFFFFFFFEu) : 0xFFFFFFFFu;
-  a.hidx[i] = i;
-  a.last[i] = p;            // cleared below for a push with a later push of its key
+  const uint32_t tile = take_tile(a.tk + 0);
+  if (tile >= (a.n + kTile - 1) / kTile) return;   // (tickets reset by the previous batch: never)
+  if (tile == 0 && threadIdx.x == 0) {
+    a.nfar[0] = 0;          // far pushes (appended by pd_link)
+    a.tk[1] = 0;
+    a.tk[2] = 0;
+  }
+  bool f[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    f[k] = false;
+    if (i >= a.n) continue;
+    const bool ok = !a.valid || a.valid[i] == a.valid_ok;
+    const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
+    f[k] = p;
+    a.push[i] = p;
+    // non-pushes sort into a run of their own at the end: a push's slice is clamped below it, so a
+    // key whose slice is 0xFFFFFFFF never shares a run with them (pd_link scans its run backwards)
+    a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2], 0xFFFFFFFEu) : 0xFFFFFFFFu;
+    a.hidx[i] = i;
+    a.last[i] = p;          // cleared by pd_link for a push with a later push of its key
+  }
+  uint32_t r[4];
+  tile_scan(f, r, a.tiles, tile, a.epoch);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    if (i < a.n) a.aidx[i] = r[k];
+  }
 }
 
 __device__ __forceinline__ uint32_t n_pushes(const PoolDevArgs& a) {
@@ -232,20 +326,44 @@ __global__ void __launch_bounds__(256) pd_far(PoolDevArgs a) {
   }
 }
 
-// statuses (batch_check step 3, no cut: the host checked the caps) and the old entries' survival
+// statuses (batch_check step 3, no cut: the host checked the caps) with lpos = exclusive scan of
+// `last` (the first ceil(n / 1024) blocks), and the old entries' survival with spos = its
+// exclusive scan (the other ceil(C / 1024) blocks): two look-back chains of their own
 __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < a.n) {
-    uint8_t st;
-    if (a.valid && a.valid[i] != a.valid_ok) st = TXV_POOL_NOT_CHECKED;
-    else {
-      const uint8_t d = a.dec[i];
-      st = d == 0 ? TXV_POOL_ERR_TOO_LARGE : d == 2 ? TXV_POOL_ERR_IN_CACHE
-         : (!a.sizes[i] && a.wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
+  const uint32_t nt = (a.n + kTile - 1) / kTile;
+  const bool old = blockIdx.x >= nt;
+  const uint32_t tile = take_tile(a.tk + (old ? 2 : 1));
+  if (tile >= (old ? (a.C + kTile - 1) / kTile : nt)) return;   // (tickets reset by pd_init: never)
+  bool f[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    f[k] = false;
+    if (!old) {
+      if (i >= a.n) continue;
+      uint8_t st;
+      if (a.valid && a.valid[i] != a.valid_ok) st = TXV_POOL_NOT_CHECKED;
+      else {
+        const uint8_t d = a.dec[i];
+        st = d == 0 ? TXV_POOL_ERR_TOO_LARGE : d == 2 ? TXV_POOL_ERR_IN_CACHE
+           : (!a.sizes[i] && a.wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
+      }
+      a.status[i] = st;
+      f[k] = a.last[i] != 0;
+    } else {
+      if (i >= a.C) continue;
+      f[k] = i < *a.clen && !a.detached[i];
+      a.surv[i] = f[k];
     }
-    a.status[i] = st;
   }
-  if (i < a.C) a.surv[i] = i < *a.clen && !a.detached[i];
+  uint32_t r[4];
+  tile_scan(f, r, old ? a.tiles + 2 * (size_t)nt : a.tiles + nt, tile, a.epoch);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    if (!old && i < a.n) a.lpos[i] = r[k];
+    if (old && i < a.C) a.spos[i] = r[k];
+  }
 }
 
 // the new cache = the last keep_old surviving old entries in order, then the last keepU of the
@@ -291,8 +409,14 @@ __global__ void __launch_bounds__(256) pd_index(PoolDevArgs a) {
     uint32_t s = idx_hash(a.ck_new + (size_t)q * 8) & (a.icap - 1);
     while (atomicCAS(&a.ci_new[s], 0u, q + 1u) != 0u) s = (s + 1) & (a.icap - 1);
   }
-  if (q == 0) a.clen[0] = L;   // its readers (pd_link .. pd_status) ran in earlier launches
+  if (q == 0) {
+    a.clen[0] = L;             // its readers (pd_link .. pd_status) ran in earlier launches
+    a.tk[0] = 0;               // pd_init's ticket counter, for the next batch
+  }
 }
+
+// nopTxCache: no pd_index to reset pd_init's ticket counter
+__global__ void pd_tk_reset(PoolDevArgs a) { a.tk[0] = 0; }
 
 // an index over keys [L][8] (a cache uploaded from the host)
 __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap) {
@@ -307,12 +431,11 @@ __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_
 // hipcub temporary storage for a batch of n votes and a cache of C entries (scans of n and C,
 // the pair sort of n)
 extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C) {
-  size_t a = 0, b = 0, c = 0;
+  size_t c = 0;
   uint32_t* u = nullptr;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, u, u, (int)std::max<uint32_t>(n, 1));
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, u, u, (int)std::max<uint32_t>(C, 1));
+  (void)C;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, u, u, u, u, (int)std::max<uint32_t>(n, 1));
-  return std::max(a, std::max(b, c));
+  return c;
 }
 
 // the whole decision + cache update chain for one batch on stream st (a.n > 0; a.C > 0 or 0)
@@ -323,9 +446,8 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   const dim3 gn((n + 255) / 256), b(256);
   hipError_t e;
   size_t tb = a.tmp_bytes;
-  hipLaunchKernelGGL(pd_init, gn, b, 0, st, a);
-  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.push, a.aidx, (int)n, st))) return e;
-  tb = a.tmp_bytes;
+  const uint32_t nt = (n + kTile - 1) / kTile, ntc = (a.C + kTile - 1) / kTile;
+  hipLaunchKernelGGL(pd_init, dim3(nt), b, 0, st, a);
   if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
   hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
   if (a.C) {
@@ -333,12 +455,11 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
     hipLaunchKernelGGL(pd_far, dim3(std::min<uint32_t>(1024, (n + 3) / 4)), b, 0, st, a);
   }
   const uint32_t span = std::max(n, a.C);
-  hipLaunchKernelGGL(pd_status, dim3((span + 255) / 256), b, 0, st, a);
-  if (!a.C) return hipGetLastError();
-  tb = a.tmp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.last, a.lpos, (int)n, st))) return e;
-  tb = a.tmp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(a.tmp, tb, a.surv, a.spos, (int)a.C, st))) return e;
+  hipLaunchKernelGGL(pd_status, dim3(nt + ntc), b, 0, st, a);
+  if (!a.C) {
+    hipLaunchKernelGGL(pd_tk_reset, dim3(1), dim3(1), 0, st, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pd_newcache, dim3((span + 255) / 256), b, 0, st, a);
   hipLaunchKernelGGL(pd_index, dim3((a.C + 255) / 256), b, 0, st, a);
   return hipGetLastError();

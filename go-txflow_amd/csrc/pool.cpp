@@ -1213,6 +1213,7 @@ void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
   j.n = A;
   j.bytes = bytes;
   j.ctx = ctx;
+  j.remove = false;                                        // a spare may have carried Update's removals
   std::lock_guard<std::mutex> lk(p->amu);
   if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
   p->pend_len += A;

@@ -45,6 +45,9 @@ struct PoolDevArgs {
   uint8_t* detached;          // [C] cached keys pushed again in this batch (cleared at the end)
   uint32_t* surv;             // [C] old entries not pushed again
   uint32_t* spos;             // [C] exclusive scan of surv
+  uint64_t* tiles;            // look-back words: [ceil(n/1024)] push, [ceil(n/1024)] last, [ceil(C/1024)] surv
+  uint32_t* tk;               // [4] tile tickets (pd_init, pd_status n-chain, pd_status C-chain)
+  uint32_t epoch;             // this batch's tag for the look-back words (30 bits)
   void* tmp;                  // hipcub temporary storage
   size_t tmp_bytes;
   uint8_t* status;            // [n] out: TXV_POOL_* per vote

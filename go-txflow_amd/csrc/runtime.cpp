@@ -3137,6 +3137,9 @@ struct PoolDev {
   uint8_t *dec = nullptr, *detached = nullptr, *d_status = nullptr;
   uint64_t *pst = nullptr, *pend = nullptr;
   uint32_t *xs = nullptr, *xn = nullptr;   // per 1024-vote block: sorted pair starts, pair count
+  uint64_t* tiles = nullptr;               // look-back words of the fused scans (kernels_pool.hip)
+  uint32_t* tk = nullptr;                  // [4] their tile tickets
+  uint32_t epoch = 0;                      // batches run: the look-back words' tag
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
@@ -3162,7 +3165,7 @@ struct PoolDev {
     for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
     dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx);
     dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
-    dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn);
+    dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn); dfree(tiles); dfree(tk);
     for (Flight& f : fl) {
       dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
       hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status);
@@ -3199,8 +3202,9 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     if ((r = dalloc(c, &s->ck[0], cw * 8)) || (r = dalloc(c, &s->ck[1], cw * 8)) || (r = dalloc(c, &s->ci[0], s->icap)) ||
         (r = dalloc(c, &s->ci[1], s->icap)) || (r = dalloc(c, &s->clen, 2)) || (r = dalloc(c, &s->detached, cw)) ||
         (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 2)) ||
-        (r = halloc(c, &s->h_clen, 2)))
+        (r = halloc(c, &s->h_clen, 2)) || (r = dalloc(c, &s->tk, 4)))
       return r;
+    HIP_TRY(c, hipMemset(s->tk, 0, 16));
     HIP_TRY(c, hipMemset(s->ci[0], 0, (size_t)s->icap * 4));
     HIP_TRY(c, hipMemset(s->clen, 0, 8));
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
@@ -3228,8 +3232,10 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
         (r = dalloc(c, &s->last, m)) ||
         (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
         (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
-        (r = dalloc(c, &s->xs, ((size_t)m + 1023) / 1024 * 1024)) || (r = dalloc(c, &s->xn, ((size_t)m + 1023) / 1024)))
+        (r = dalloc(c, &s->xs, ((size_t)m + 1023) / 1024 * 1024)) || (r = dalloc(c, &s->xn, ((size_t)m + 1023) / 1024)) ||
+        (r = dalloc(c, &s->tiles, 2 * (((size_t)m + 1023) / 1024) + ((size_t)std::max<uint32_t>(C, 1) + 1023) / 1024)))
       return r;
+    HIP_TRY(c, hipMemset(s->tiles, 0, (2 * (((size_t)m + 1023) / 1024) + ((size_t)std::max<uint32_t>(C, 1) + 1023) / 1024) * 8));
     for (PoolDev::Flight& f : s->fl)
       if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
           (r = dalloc(c, &f.d_sizes, m)) || (r = dalloc(c, &f.d_status, m)) || (r = halloc(c, &f.h_sig, (size_t)m * 16)) ||
@@ -3350,6 +3356,12 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
   a.pend = s->pend; a.xs = s->xs; a.xn = s->xn; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
   a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status;
+  a.tiles = s->tiles; a.tk = s->tk;
+  if (((++s->epoch) & 0x3FFFFFFFu) == 0) {          // the tag wrapped: no word may match by accident
+    HIP_TRY(c, hipMemsetAsync(s->tiles, 0, (2 * (((size_t)s->cap_n + 1023) / 1024) + ((size_t)std::max<uint32_t>(s->C, 1) + 1023) / 1024) * 8, ks));
+    ++s->epoch;
+  }
+  a.epoch = s->epoch;
   HIP_TRY(c, txv_pooldev_run(&a, ks));
   if (s->C) s->cur ^= 1;                                  // the next batch on this stream reads the new cache
   HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status, n, hipMemcpyDeviceToHost, ks));

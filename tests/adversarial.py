@@ -49,6 +49,14 @@ import ed_math as E  # noqa: E402
 CHAIN = "test_chain_id"
 N_HONEST = 100
 
+# Appendix C classes, tagged per generated vote (f["cls"]) so a gate can count how many of each
+# reach TxFlow: (name, share of the stream)
+CLASSES = [("base", None), ("r_bit_flip", 0.02), ("s_bit_flip", 0.02), ("field_changed", 0.02), ("s_plus_l", 0.01),
+           ("s_top_bits", 0.005), ("sig_len", 0.005), ("noncanonical_r", 0.005), ("unknown_validator", 0.005),
+           ("empty_address", 0.0025), ("nil", 0.001), ("crafted_key", 0.015), ("conflicting", 0.05),
+           ("exact_replay", 0.05)]
+CLS = {name: i for i, (name, _) in enumerate(CLASSES)}
+
 
 def _expand(seed: bytes):
     h = hashlib.sha512(seed).digest()
@@ -211,8 +219,10 @@ class C4Stream:
                  height=np.ones(n_all, np.int64), ts_nanos=np.zeros(n_all, np.int32),
                  addr=np.zeros((n_all, 20), np.uint8), addr_len=np.full(n_all, 20, np.uint32),
                  sig=np.zeros((n_all, 64), np.uint8), sig_len=np.full(n_all, 64, np.uint32),
-                 is_nil=np.zeros(n_all, np.uint8), txoff=np.zeros(n_all, np.uint32))
+                 is_nil=np.zeros(n_all, np.uint8), txoff=np.zeros(n_all, np.uint32), cls=np.zeros(n_all, np.int8))
         f["tx"][:n_prim], f["val"][:n_prim], f["kind"][:n_prim] = tx, val, kind
+        f["cls"][:n_prim] = np.array([CLS["base"], CLS["crafted_key"], CLS["noncanonical_r"], CLS["unknown_validator"],
+                                      CLS["empty_address"], CLS["nil"]], np.int8)[kind]
         nanos = self.nanos + np.arange(n_all, dtype=np.int64)
         self.nanos += n_all
         f["ts_nanos"][:] = (nanos % 999_999_999 + 1).astype(np.int32)
@@ -289,11 +299,16 @@ class C4Stream:
             f["sig"][i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
         f["sig"][g_top, 63] |= (np.uint8(0x20) << rng.integers(0, 3, len(g_top)).astype(np.uint8))
         f["sig_len"][g_len] = rng.choice(np.array([0, 63, 65], np.uint32), len(g_len))
+        for grp, name in ((g_r, "r_bit_flip"), (g_s, "s_bit_flip"), (g_field, "field_changed"), (g_sl, "s_plus_l"),
+                          (g_top, "s_top_bits"), (g_len, "sig_len")):
+            f["cls"][grp] = CLS[name]
+        f["cls"][cs] = CLS["conflicting"]
 
         # exact replays of final (post-mutation) votes
         rs = slice(n_prim + n_conf, n_all)
         for key in ("tx", "val", "kind", "height", "ts_nanos", "addr", "addr_len", "sig", "sig_len", "is_nil", "txoff"):
             f[key][rs] = src_field(key, r_prev, r_j)
+        f["cls"][rs] = CLS["exact_replay"]
 
         # arrival order: a derived vote comes after its source when the source is in this batch
         sort_key = np.empty(n_all)
@@ -308,6 +323,10 @@ class C4Stream:
             f[key] = f[key][order]
         f["n"] = n_all
         self.prev = f
+        cg = self.stats.setdefault("class_generated", {})
+        for c, cnt in zip(*np.unique(f["cls"], return_counts=True)):
+            cg[CLASSES[int(c)][0]] = cg.get(CLASSES[int(c)][0], 0) + int(cnt)
+        self.stats["generated"] = self.stats.get("generated", 0) + n_all
         batch = T.VoteBatch(n_all, height=f["height"], txhash_arena=hashes_arena, txhash_off=f["txoff"],
                             txhash_len=np.full(n_all, 64, np.uint32),
                             ts_sec=np.full(n_all, 1_700_000_000, np.int64), ts_nanos=f["ts_nanos"],
@@ -402,6 +421,9 @@ class C4Stream:
             self.stats["verify_checked"] += m
         self.stats["votes"] += batch.n
         self.stats["batches"] += 1
+        cc = self.stats.setdefault("class_at_txflow", {})
+        for c, cnt in zip(*np.unique(f["cls"], return_counts=True)):
+            cc[CLASSES[int(c)][0]] = cc.get(CLASSES[int(c)][0], 0) + int(cnt)
         self.stats["events"] += len(ev)
         for code, cnt in zip(*np.unique(exp & 0x7F, return_counts=True)):
             nm = T.STATUS_NAMES.get(int(code), str(code))
@@ -467,6 +489,12 @@ def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int
     if s.stats["batches"] % s.bpe:
         s.stats["mismatches"] += s.check_sets()
     s.stats["seconds"] = round(time.time() - t0, 1)
+    # every Appendix C class's share of the generated stream that reached TxFlow, against its share
+    # (exact replays stop at the pool while their key is cached, by design)
+    gen = max(1, s.stats.get("generated", 0))
+    s.stats["class_share_at_txflow"] = {name: {"share": share, "at_txflow": round(s.stats["class_at_txflow"].get(name, 0) / gen, 5),
+                                               "ratio": round(s.stats["class_at_txflow"].get(name, 0) / gen / share, 3)}
+                                        for name, share in CLASSES if share}
     if s.pool is not None:
         s.pool.close()
     return s.stats

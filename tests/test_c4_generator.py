@@ -70,6 +70,10 @@ def test_c4_stream_covers_every_outcome(oracle_lib):
                  T.ERR_NONDETERMINISTIC, T.ERR_INVALID_SIGNATURE):
         assert seen.get(T.STATUS_NAMES[code], 0) > 0, (T.STATUS_NAMES[code], seen)
     assert s.stats["events"] > 0
+    for name, share in A.CLASSES:               # every Appendix C class is generated at about its share
+        if share:
+            got = s.stats["class_generated"].get(name, 0) / s.stats["generated"]
+            assert 0.7 * share <= got <= 1.4 * share, (name, got, share)
     # crafted keys: identity forgeries verify, order-2/4/8 and mixed-order forgeries verify only
     # when [k]T = 0, the undecodable key never -- so both verdicts occur among crafted votes
     names = [k[0] for k in s.crafted]
