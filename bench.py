@@ -293,6 +293,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     ctx.bind_host_numa()
     wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch, replay=C5_REPLAY)
     upd, n_upd = c5_prepare_updates(ctx, wl)
+    log(f"[c5] stream ready: {wl.n} votes, {n_upd} committed votes for Update per pass")
     # the batches' columns pinned once (txv_host_register, a node's receive buffers): the key
     # upload of txv_pool_prepare and txv_submit_votes DMA them without a staging copy
     seen = set()
@@ -313,7 +314,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
         return pool, runs
 
     def run_passes(pool, device_cache):
-        for _ in range(2):          # warm-up pass: first-touch of host tables and pinned buffers
+        for w in range(2):          # warm-up pass: first-touch of host tables and pinned buffers
             for k, b in enumerate(wl.batches):
                 b.is_nil = (pool.check_batch(b) != T.POOL_OK).astype(np.uint8)
                 ctx.add_votes(b, ev_cap=b.n)
@@ -321,6 +322,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                     pool.update(1, upd[k])
             ctx.reset_flow()
             pool.flush()
+            log(f"[c5] {'device' if device_cache else 'host'} cache warm-up pass {w} done")
         # three timed passes over the same stream (reset between): the 2M-vote pass lasts ~45 ms, so
         # a single host stall moves it; the median pass is reported, all three beside it
         runs = []
@@ -467,6 +469,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                    "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
                    "table_window": ctx.table_w, "base_window": ctx.base_w}
             runs.append(out)
+            log(f"[c5] {'device' if device_cache else 'host'} cache pass {rep}: {out['votes_per_s'] / 1e6:.1f}M votes/s, "
+                f"correct {ok}")
             ctx.reset_flow()
             pool.flush()
         return runs, dev_ms, dev_split
@@ -647,6 +651,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         pool.sync()
         pool_ok = c5_pool_replay(wl, order, upd, got, C5_CACHE)
         lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
+        log(f"[c5 wire] pass {rep}: {wl.n / total / 1e6:.1f}M votes/s, pool {pool_ok}")
         runs.append({"votes_per_s": round(wl.n / total, 1), "pool_matches_oracle": pool_ok,
                      "correct": pool_ok and state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
                      "p50_decode_ms": round(float(np.median(dec_ms)), 3),
@@ -829,6 +834,9 @@ def main():
     ap.add_argument("--c5-only", action="store_true",
                     help="profiling aid: run only the C5 legs (SoA and wire) and print them as one JSON line")
     args = ap.parse_args()
+    if os.environ.get("TXV_BENCH_WATCHDOG"):   # debugging aid: every thread's stack on stderr periodically
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["TXV_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
     if args.c5_only:
         out = {"c5_streaming": c5_streaming(0, 1000, args.c5_txs, 65536)}

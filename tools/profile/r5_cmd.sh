@@ -1,11 +1,9 @@
 set -o pipefail
-O=gpurun_out/r5_ab5
+O=gpurun_out/r5_ab6
 mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTFAIL; grep -E "^E  " $O/tests.log | head -20; tail -5 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
 for m in 0:2 2:2 2:3; do
   ps=${m%:*}; fl=${m#*:}
-  TXV_POOL_STREAM=$ps TXV_C5_INFLIGHT=$fl timeout -k 10 300 python3 bench.py --c5-only > $O/c5_m$ps$fl.json 2> $O/c5_m$ps$fl.err || { echo C5FAIL $m; tail -5 $O/c5_m$ps$fl.err; exit 5; }
+  TXV_BENCH_WATCHDOG=100 TXV_POOL_STREAM=$ps TXV_C5_INFLIGHT=$fl timeout -k 10 330 python3 -u bench.py --c5-only > $O/c5_m$ps$fl.json 2> >(tee $O/c5_m$ps$fl.err >&2) || { echo C5FAIL $m; tail -30 $O/c5_m$ps$fl.err; exit 5; }
   python3 -c "
 import json
 d=json.load(open('$O/c5_m$ps$fl.json'))
