@@ -202,7 +202,10 @@ def c5_expected_pool(wl, cache_size: int):
 
 
 C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in flight in the C5 leg (<= 3)
-C5_POOL_SIZE = 8 * 65536  # TxVotePool Size cap of the C5 legs: committed votes leave the pool (Update)
+# TxVotePool Size cap of the C5 legs: committed votes leave the pool through Update, so the pool
+# holds what CheckTx admitted ahead of the commits (~8 batches in the pipelines below) -- not the
+# stream (2.15M votes)
+C5_POOL_SIZE = 1 << 20
 
 
 def c5_commit_updates(wl, added_slots, commit_batch):
@@ -345,7 +348,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             # CheckTx batches and Updates reach the pool from different threads (as the reactor's
             # and TxFlow's goroutines do): the order the pool took them in is recorded for the
             # oracle's replay
-            order, order_mu, max_size = [], threading.Lock(), [0]
+            order, order_mu, max_size, upd_ms = [], threading.Lock(), [0], []
 
             # CheckTx in two stages on two threads (txv_pool_prepare: keys on the GPU + TxVote.Size;
             # txv_pool_check_keys: the order-dependent LRU / pool admission), so batch k+1's keys are
@@ -396,17 +399,19 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                     k, tk = item
                     st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
                     te = time.perf_counter()
-                    if upd[k] is not None:        # TxVotePool.Update with the batch's committed votes
-                        with order_mu:
-                            pool.update_submit(1, upd[k])
-                            order.append(("u", k))
-                        max_size[0] = max(max_size[0], pool.Size())
                     if rep == 2:                  # the batch's stage times, before its ring slot is reused
                         dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
                         sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
                         if sp:
                             dev_split.append(sp)
                     slots.release()
+                    if upd[k] is not None:        # TxVotePool.Update with the batch's committed votes
+                        tu = time.perf_counter()
+                        with order_mu:
+                            pool.update_submit(1, upd[k])
+                            order.append(("u", k))
+                        upd_ms.append((time.perf_counter() - tu) * 1e3)
+                        max_size[0] = max(max_size[0], pool.Size())
                     done.append(te)
                     added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
                     for e in ev:
@@ -459,8 +464,10 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                                f"batches and Updates in the order the pool took them",
                    "correct": ok, "pool_matches_oracle": pool_ok, "votes_per_s": round(wl.n / total, 1),
                    "pool_size_cap": C5_POOL_SIZE, "pool_size_max": max_size[0],
+                   "p50_pool_update_ms": round(float(np.median(upd_ms)), 3) if upd_ms else None,
                    "pool_status_counts": {"ok": int((allst == T.POOL_OK).sum()),
-                                          "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum())},
+                                          "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum()),
+                                          "full": int((allst == T.POOL_ERR_FULL).sum())},
                    "p50_pool_check_ms": round(float(np.median(np.array(prep_ms) + np.array(admit_ms))), 3),
                    "p50_pool_prepare_ms": round(float(np.median(prep_ms)), 3),
                    "p50_pool_admit_ms": round(float(np.median(admit_ms)), 3),
@@ -470,13 +477,18 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                    "table_window": ctx.table_w, "base_window": ctx.base_w}
             runs.append(out)
             log(f"[c5] {'device' if device_cache else 'host'} cache pass {rep}: {out['votes_per_s'] / 1e6:.1f}M votes/s, "
-                f"correct {ok}")
+                f"correct {ok} (pool {pool_ok}, added {added}/{wl.n_unique}, commits {len(commit_t)}/{wl.n_txs}, "
+                f"statuses {out['pool_status_counts']}, max Size {max_size[0]}; p50 ms prepare {out['p50_pool_prepare_ms']} "
+                f"admit {out['p50_pool_admit_ms']} update {out['p50_pool_update_ms']} batch {out['p50_batch_ms']})")
             ctx.reset_flow()
             pool.flush()
         return runs, dev_ms, dev_split
 
-    pool_h, (runs_h, _, _) = run_mode(False)
-    pool_h.close()
+    if os.environ.get("TXV_C5_DEVICE_ONLY"):   # experiments: the reported mode only
+        runs_h = None
+    else:
+        pool_h, (runs_h, _, _) = run_mode(False)
+        pool_h.close()
     pool, (runs, dev_ms, dev_split) = run_mode(True)
     # unloaded latency: one batch at a time (CheckTx -> submit -> wait before the next batch's
     # CheckTx), so a batch's latency is its own chain, with no queueing behind others
@@ -508,13 +520,15 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     out = dict(runs[1])
     out["passes"] = 3
     out["votes_per_s_passes"] = [r["votes_per_s"] for r in runs]
-    runs_h.sort(key=lambda r: r["votes_per_s"])
-    out["host_cache"] = {k: runs_h[1][k] for k in ("votes_per_s", "correct", "p50_pool_check_ms", "p50_pool_prepare_ms",
-                                                    "p50_pool_admit_ms", "p50_batch_ms", "p50_commit_latency_ms",
-                                                    "p99_commit_latency_ms")}
-    out["host_cache"]["votes_per_s_passes"] = [r["votes_per_s"] for r in runs_h]
-    out["host_cache"]["note"] = ("the same stream with the cache on the host: txv_pool_prepare (keys on the GPU + Size) "
-                                 "and txv_pool_check_keys (stack-distance decisions on the host threads) on two threads")
+    if runs_h:
+        runs_h.sort(key=lambda r: r["votes_per_s"])
+        out["host_cache"] = {k: runs_h[1][k] for k in ("votes_per_s", "correct", "p50_pool_check_ms", "p50_pool_prepare_ms",
+                                                        "p50_pool_admit_ms", "p50_batch_ms", "p50_commit_latency_ms",
+                                                        "p99_commit_latency_ms")}
+        out["host_cache"]["votes_per_s_passes"] = [r["votes_per_s"] for r in runs_h]
+        out["host_cache"]["note"] = ("the same stream with the cache on the host: txv_pool_prepare (keys on the GPU + "
+                                     "Size) and txv_pool_check_keys (stack-distance decisions on the host threads) on "
+                                     "two threads")
     out["unloaded"] = {
         "note": "one batch at a time: txv_pool_check (device cache) -> txv_submit_votes -> txv_wait_votes before the "
                 "next batch's CheckTx",
@@ -525,7 +539,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
         "p99_commit_latency_ms": round(float(np.percentile(one_lat, 99)), 3) if len(one_lat) else None,
         "correct": one_ok and len(one_commit) == wl.n_txs}
     out["correct"] = (all(r["correct"] for r in runs) and out["unloaded"]["correct"] and
-                      all(r["correct"] for r in runs_h))
+                      all(r["correct"] for r in runs_h or []))
     # where a 64k batch's device time goes: the stage times of every batch of the last
     # pass inside the pipeline, and of one batch run alone on a fresh TxFlow (staged slot 0: the
     # submit ring is idle now), with the verify pair's VALU roofline at this batch size

@@ -450,7 +450,9 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   hipLaunchKernelGGL(pd_init, dim3(nt), b, 0, st, a);
   if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
   hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
-  if (a.C) {
+  // an Update batch (every vote pushes: max_tx = INT64_MAX) needs the new cache, not statuses:
+  // its far pushes' decisions are skipped
+  if (a.C && a.max_tx != INT64_MAX) {
     hipLaunchKernelGGL(pd_xsort, dim3((n + kXBlock - 1) / kXBlock), b, 0, st, a);
     hipLaunchKernelGGL(pd_far, dim3(std::min<uint32_t>(1024, (n + 3) / 4)), b, 0, st, a);
   }

@@ -61,6 +61,7 @@ struct FlatIndex {
   struct Slot { uint32_t tag; int32_t idx; };     // tag 0 = empty
   Slot* t = nullptr;
   size_t cap = 0, mask = 0, n = 0;
+  uint32_t shift = 32;                            // home slot = Fibonacci hash of the tag's 32 bits
   const KeyList* owner = nullptr;
   explicit FlatIndex(const KeyList* o) : owner(o) { alloc(1024); }
   ~FlatIndex() { free(t); }
@@ -68,6 +69,10 @@ struct FlatIndex {
   FlatIndex& operator=(const FlatIndex&) = delete;
   static uint64_t h(const Key& k) { uint64_t v; memcpy(&v, k.b, 8); return v ^ (v >> 29); }
   static uint32_t tag(uint64_t hv) { return (uint32_t)(hv >> 32) | 1u; }
+  // the home slot from the stored tag alone (the high bits of its Fibonacci hash: the partition
+  // bits PartIndex takes from the same word are mixed in), so the backward-shift erase and the
+  // rehash never read a node's key
+  size_t home(uint32_t tg) const { return (size_t)((uint32_t)(tg * 0x9E3779B1u) >> shift); }
   void alloc(size_t c) {
     const size_t bytes = c * sizeof(Slot);
     const size_t align = bytes >= (2u << 20) ? (2u << 20) : 64;
@@ -77,13 +82,14 @@ struct FlatIndex {
 #endif
     memset(t, 0, bytes);
     cap = c; mask = c - 1; n = 0;
+    shift = 32;
+    for (size_t x = c; x > 1; x >>= 1) --shift;
   }
   inline const Key& key_of(int32_t idx) const;
-  void prefetch(const Key& k) const { __builtin_prefetch(&t[h(k) & mask]); }
+  void prefetch(const Key& k) const { __builtin_prefetch(&t[home(tag(h(k)))]); }
   int32_t find(const Key& k) const {
-    const uint64_t hv = h(k);
-    const uint32_t tg = tag(hv);
-    for (size_t i = hv & mask; t[i].tag; i = (i + 1) & mask)
+    const uint32_t tg = tag(h(k));
+    for (size_t i = home(tg); t[i].tag; i = (i + 1) & mask)
       if (t[i].tag == tg && key_of(t[i].idx) == k) return t[i].idx;
     return -1;
   }
@@ -92,9 +98,8 @@ struct FlatIndex {
   template <typename F>
   int32_t find_or_insert(const Key& k, F&& make_idx) {
     if ((n + 1) * 2 > cap) grow();
-    const uint64_t hv = h(k);
-    const uint32_t tg = tag(hv);
-    size_t i = hv & mask;
+    const uint32_t tg = tag(h(k));
+    size_t i = home(tg);
     for (; t[i].tag; i = (i + 1) & mask)
       if (t[i].tag == tg && key_of(t[i].idx) == k) return t[i].idx;
     t[i] = Slot{tg, make_idx()};
@@ -103,32 +108,33 @@ struct FlatIndex {
   }
   void put(const Key& k, int32_t idx) {    // insert or overwrite
     if ((n + 1) * 2 > cap) grow();
-    const uint64_t hv = h(k);
-    const uint32_t tg = tag(hv);
-    size_t i = hv & mask;
+    const uint32_t tg = tag(h(k));
+    size_t i = home(tg);
     for (; t[i].tag; i = (i + 1) & mask)
       if (t[i].tag == tg && key_of(t[i].idx) == k) { t[i].idx = idx; return; }
     t[i] = Slot{tg, idx};
     ++n;
   }
-  bool erase(const Key& k) {
-    const uint64_t hv = h(k);
-    const uint32_t tg = tag(hv);
-    size_t i = hv & mask;
+  // remove the key and return its index (-1: absent); one probe
+  int32_t take(const Key& k) {
+    const uint32_t tg = tag(h(k));
+    size_t i = home(tg);
     for (; t[i].tag; i = (i + 1) & mask)
       if (t[i].tag == tg && key_of(t[i].idx) == k) break;
-    if (!t[i].tag) return false;
+    if (!t[i].tag) return -1;
+    const int32_t idx = t[i].idx;
     size_t j = i;
     for (;;) {   // backward shift: entry j moves into hole i iff i lies cyclically in [home(j), j)
       j = (j + 1) & mask;
       if (!t[j].tag) break;
-      const size_t home = h(key_of(t[j].idx)) & mask;
-      if (((j - home) & mask) >= ((j - i) & mask)) { t[i] = t[j]; i = j; }
+      const size_t hj = home(t[j].tag);
+      if (((j - hj) & mask) >= ((j - i) & mask)) { t[i] = t[j]; i = j; }
     }
     t[i].tag = 0;
     --n;
-    return true;
+    return idx;
   }
+  bool erase(const Key& k) { return take(k) >= 0; }
   void clear() { memset(t, 0, cap * sizeof(Slot)); n = 0; }   // keeps the capacity
   void reserve(size_t m) { if (m * 2 > cap) { size_t c = cap; while (m * 2 > c) c *= 2; rehash(c); } }
   void grow() { rehash(cap * 2); }
@@ -138,13 +144,32 @@ struct FlatIndex {
     alloc(c);
     for (size_t i = 0; i < oc; ++i)
       if (old[i].tag) {
-        size_t j = h(key_of(old[i].idx)) & mask;
+        size_t j = home(old[i].tag);
         while (t[j].tag) j = (j + 1) & mask;
         t[j] = old[i];
         ++n;
       }
     free(old);
   }
+};
+
+// TXV_PROFILE_HOST=1: per-call phase times of the pool's calls on stderr ("[txv pool] <what> a=.. b=..")
+struct PTimer {
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  std::string line;
+  explicit PTimer(const char* what) : on(getenv("TXV_PROFILE_HOST") != nullptr), t(std::chrono::steady_clock::now()) {
+    if (on) line = what;
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.3f", what, std::chrono::duration<double, std::milli>(now - t).count());
+    line += b;
+    t = now;
+  }
+  ~PTimer() { if (on) fprintf(stderr, "[txv pool] %s\n", line.c_str()); }
 };
 
 // doubly linked list in a vector (stable indices)
@@ -299,6 +324,10 @@ struct txv_pool {
   // proxyMtx): txs.len / txs_bytes themselves are written under mu or by the appender under amu,
   // so a reader holding neither must not touch them
   std::atomic<int64_t> pub_len{0}, pub_bytes{0};
+  std::vector<uint8_t> rm_flag;                    // remove_keys scratch: per pool-list node
+  std::vector<uint8_t> rm_part;                    // ... per key: its txsMap partition
+  std::vector<uint32_t> rm_order;                  // ... the keys by partition
+  std::vector<int32_t> rm_all;                     // ... the nodes removed
   // engines replaced while a waiter (txv_pool_check_wait, outside mu) may still sync on one of
   // their flight events: freed when the last waiter is done
   int waiters = 0;
@@ -1127,6 +1156,93 @@ void publish_locked(txv_pool* p) {
   publish(p);
 }
 
+// removeTx(tx, e, false) for every key of keys[n] the pool holds (Update, txvotepool.go:339-344),
+// on the worker threads: (1) per txsMap partition, find + erase its keys (a key twice in the batch
+// is found once); (2) the found nodes flagged; (3) one thread per run of consecutive flagged nodes
+// (its first node's predecessor unflagged) relinks around the run -- runs touch disjoint
+// neighbours, so no two threads write one pointer; (4) free list.  Returns the bytes removed (the
+// Update votes' Size(), as the reference subtracts tx.Size()) and *count the nodes removed: the
+// caller lowers txs.len (under amu on the appender).  The caller owns the pool list (the
+// appender, or a host path that drained it).
+int64_t remove_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, uint32_t n, size_t* count) {
+  *count = 0;
+  if (!n) return 0;
+  // the keys' partitions in chunks, then each partition's keys in batch order (a counting sort):
+  // every worker then walks a dense list with its lookups prefetched ahead (DRAM-latency bound)
+  std::vector<uint8_t>& pt = p->rm_part;
+  std::vector<uint32_t>& ord = p->rm_order;
+  pt.resize(n);
+  ord.resize(n);
+  const uint32_t nc = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
+  std::vector<uint32_t> cnt((size_t)nc * kParts, 0);
+  pool_parallel_for(p, ctx, nc, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c)
+      for (uint32_t i = (uint32_t)((uint64_t)n * c / nc); i < (uint32_t)((uint64_t)n * (c + 1) / nc); ++i) {
+        pt[i] = (uint8_t)PartIndex::part(keys[i]);
+        ++cnt[(size_t)c * kParts + pt[i]];
+      }
+  }, 1);
+  std::vector<uint32_t> base(kParts + 1, 0), off((size_t)nc * kParts);
+  uint32_t run = 0;
+  for (uint32_t q = 0; q < kParts; ++q) {
+    base[q] = run;
+    for (uint32_t c = 0; c < nc; ++c) { off[(size_t)c * kParts + q] = run; run += cnt[(size_t)c * kParts + q]; }
+  }
+  base[kParts] = run;
+  pool_parallel_for(p, ctx, nc, [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t c = c0; c < c1; ++c)
+      for (uint32_t i = (uint32_t)((uint64_t)n * c / nc); i < (uint32_t)((uint64_t)n * (c + 1) / nc); ++i)
+        ord[off[(size_t)c * kParts + pt[i]]++] = i;
+  }, 1);
+  std::vector<int32_t> found[kParts];
+  int64_t bytes[kParts] = {};
+  pool_parallel_for(p, ctx, kParts, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t q = lo; q < hi; ++q) {
+      FlatIndex& ix = *p->txs_map.p[q];
+      for (uint32_t a = base[q]; a < base[q + 1]; ++a) {
+        if (a + 16 < base[q + 1]) ix.prefetch(keys[ord[a + 16]]);
+        const uint32_t i = ord[a];
+        const int32_t e = ix.take(keys[i]);       // a key twice in the batch: found once
+        if (e < 0) continue;
+        found[q].push_back(e);
+        bytes[q] += sizes[i];
+      }
+    }
+  }, 1);
+  std::vector<int32_t>& all = p->rm_all;
+  all.clear();
+  int64_t removed_bytes = 0;
+  for (uint32_t q = 0; q < kParts; ++q) {
+    all.insert(all.end(), found[q].begin(), found[q].end());
+    removed_bytes += bytes[q];
+  }
+  if (all.empty()) return 0;
+  KeyList& L = p->txs;
+  std::vector<uint8_t>& rm = p->rm_flag;
+  if (rm.size() < L.nodes.size()) rm.resize(L.nodes.size(), 0);
+  for (int32_t e : all) rm[e] = 1;
+  const uint32_t m = (uint32_t)all.size();
+  pool_parallel_for(p, ctx, m, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t a = lo; a < hi; ++a) {
+      if (a + 8 < hi) __builtin_prefetch(&L.nodes[all[a + 8]]);
+      const int32_t e = all[a];
+      const int32_t pv = L.nodes[e].prev;
+      if (pv >= 0 && rm[pv]) continue;                     // not the first node of its run
+      int32_t r = e;
+      while (L.nodes[r].next >= 0 && rm[L.nodes[r].next]) r = L.nodes[r].next;
+      const int32_t nx = L.nodes[r].next;
+      if (pv >= 0) L.nodes[pv].next = nx; else L.head = nx;
+      if (nx >= 0) L.nodes[nx].prev = pv; else L.tail = pv;
+    }
+  }, 4096);
+  for (int32_t e : all) {
+    rm[e] = 0;
+    L.free_.push_back(e);
+  }
+  *count = m;
+  return removed_bytes;
+}
+
 void appender_loop(txv_pool* p) {
   std::unique_lock<std::mutex> lk(p->amu);
   for (;;) {
@@ -1135,23 +1251,22 @@ void appender_loop(txv_pool* p) {
     txv_pool::Append j = std::move(p->jobs.front());
     p->jobs.pop_front();
     p->a_busy = true;
+    const size_t backlog = p->jobs.size();
     lk.unlock();
     int64_t removed_bytes = 0;
-    if (j.remove) {
-      for (uint32_t i = 0; i < j.n; ++i) {
-        if (i + 16 < j.n) p->txs_map.prefetch(j.keys[i + 16]);
-        const int32_t e = p->txs_map.find(j.keys[i]);
-        if (e >= 0) {
-          p->txs_map.erase(j.keys[i]);
-          p->txs.unlink(e);                              // its own --len, under no lock: the list is the appender's
-          removed_bytes += j.sizes[i];
-        }
+    size_t removed = 0;
+    {
+      PTimer pt(j.remove ? "appender remove" : "appender append");
+      if (j.remove) {
+        removed_bytes = remove_keys(p, j.ctx, j.keys.data(), j.sizes.data(), j.n, &removed);
+      } else {
+        append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
       }
-    } else {
-      append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
+      pt.mark(backlog > 9 ? "n9+" : (backlog > 3 ? "n4+" : "n0+"));
     }
     lk.lock();
     if (j.remove) {
+      p->txs.len -= removed;
       p->txs_bytes -= removed_bytes;
     } else {
       p->txs.len += j.n;
@@ -1224,8 +1339,9 @@ void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
 }
 
 // Update's pool-list removals, queued behind every append queued before them
-void queue_removal(txv_pool* p, std::vector<Key>&& keys, std::vector<uint32_t>&& sizes) {
+void queue_removal(txv_pool* p, txv_ctx* ctx, std::vector<Key>&& keys, std::vector<uint32_t>&& sizes) {
   txv_pool::Append j;
+  j.ctx = ctx;
   j.n = (uint32_t)keys.size();
   if (!j.n) return;
   j.keys = std::move(keys);
@@ -1264,7 +1380,7 @@ int finish_ticket(txv_pool* p, txv_pool::Ticket& t) {
   if (t.upd) {                                             // the engine's pushes done; the removals queued
     if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
     const Key* k = reinterpret_cast<const Key*>(kp);
-    queue_removal(p, std::vector<Key>(k, k + t.n), std::move(t.usizes));
+    queue_removal(p, t.ctx, std::vector<Key>(k, k + t.n), std::move(t.usizes));
     return TXV_OK;
   }
   if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
@@ -1367,6 +1483,7 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
     // the device path: Size() on the host workers (with the pushes, the bytes and any long
     // signature), then keys, decisions and the new cache enqueued on the GPU
     const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+    PTimer pt("check_submit");
     std::atomic<uint64_t> pushes{0}, bytes{0};
     std::atomic<bool> long_sig{false};
     txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
@@ -1383,15 +1500,18 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
       bytes.fetch_add(by, std::memory_order_relaxed);
       if (lg) long_sig.store(true, std::memory_order_relaxed);
     });
+    pt.mark("sizes");
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
       const int slot = p->next_slot;
       for (auto& o : p->tickets)                           // the slot's previous batch, finished
         if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
+      pt.mark("prev");
       if ((r = cache_to_dev(p, ctx, v->n))) return r;
       if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
                                (p->cfg.flags & TXV_POOL_WAL) != 0, true, nullptr)))
         return r;
+      pt.mark("enqueue");
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
       p->next_slot = (slot + 1) % kPdRing;
       t.slot = slot;
@@ -1401,9 +1521,6 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
       p->infl_bytes += (int64_t)t.bytes;
       p->tickets.push_back(std::move(t));
       *ticket = p->next_ticket++;
-      if (getenv("TXV_PROFILE_HOST"))
-        fprintf(stderr, "[txv pool] device submit=%.3fms n=%u\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), v->n);
       return TXV_OK;
     }
   }
@@ -1439,8 +1556,11 @@ int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
     if (it == p->tickets.end()) return TXV_ESTATE;
     if (!it->done) { ctx = it->ctx; slot = it->slot; dev = p->dev; ++p->waiters; }
   }
+  PTimer pt("check_wait");
   if (slot >= 0) (void)pooldev_finish(ctx, dev, slot, nullptr, nullptr, nullptr);   // the wait itself
+  pt.mark("gpu");
   std::lock_guard<std::mutex> g(p->mu);
+  pt.mark("lock");
   if (slot >= 0 && --p->waiters == 0) {
     for (PoolDev* d : p->retired) pooldev_free(d);
     p->retired.clear();
@@ -1453,6 +1573,7 @@ int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
     if (!r && it->n && status_out) memcpy(status_out, it->st.data(), it->n);
     p->tickets.erase(it);
     prune_updates(p);
+    pt.mark("finish");
     return r;
   }
   return TXV_ESTATE;
@@ -1490,6 +1611,7 @@ int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_
 // (txv_pool_check_wait, txv_pool_sync, any reader).  Signatures > 64 bytes take the host path.
 int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   const uint32_t n = v->n;
+  PTimer pt("update_submit");
   txv_pool::Ticket t;
   t.upd = true;
   t.ctx = ctx;
@@ -1498,15 +1620,18 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   pool_parallel_for(p, ctx, n, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t i = lo; i < hi; ++i) t.usizes[i] = vote_size(v, i);
   }, 4096);
+  pt.mark("sizes");
   int r;
   const int slot = p->next_slot;
   for (auto& o : p->tickets)                               // the slot's previous batch, finished
     if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
   prune_updates(p);
+  pt.mark("prev");
   if ((r = cache_to_dev(p, ctx, n))) return r;
   if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, t.usizes.data(), nullptr, nullptr, nullptr, 0, n, INT64_MAX,
                            false, true, nullptr)))
     return r;
+  pt.mark("enqueue");
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
   p->next_slot = (slot + 1) % kPdRing;
   t.slot = slot;
@@ -1522,21 +1647,20 @@ int update_host(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* si
   if ((r = cache_to_host(p, ctx))) return r;
   host_cache_written(p);
   const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
-  for (uint32_t i = 0; i < v->n; ++i) {
-    if (i + 16 < v->n) {
-      if (p->cache_on) p->cache_map.prefetch(keys[i + 16]);
-      p->txs_map.prefetch(keys[i + 16]);
+  if (p->cache_on)                                 // cache.Push of every committed key, in order
+    for (uint32_t i = 0; i < v->n; ++i) {
+      if (i + 16 < v->n) p->cache_map.prefetch(keys[i + 16]);
+      Key k;
+      memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
+      (void)p->cache_push(k);
     }
-    Key k;
-    memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
-    (void)p->cache_push(k);
-    const int32_t e = p->txs_map.find(k);
-    if (e >= 0) {                                   // removeTx(tx, e, false)
-      p->txs_map.erase(k);
-      p->txs.unlink(e);
-      p->txs_bytes -= vote_size(v, i);
-    }
-  }
+  std::vector<uint32_t> sz(v->n);                  // removeTx(tx, e, false) of the ones the pool holds
+  pool_parallel_for(p, ctx, v->n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) sz[i] = vote_size(v, i);
+  }, 4096);
+  size_t removed = 0;
+  p->txs_bytes -= remove_keys(p, ctx, keys, sz.data(), v->n, &removed);
+  p->txs.len -= removed;
   publish_locked(p);
   return TXV_OK;
 }

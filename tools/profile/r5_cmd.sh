@@ -1,14 +1,21 @@
 set -o pipefail
-O=gpurun_out/r5_ab6
+O=gpurun_out/r5_prof2
 mkdir -p $O
-for m in 0:2 2:2 2:3; do
-  ps=${m%:*}; fl=${m#*:}
-  TXV_BENCH_WATCHDOG=100 TXV_POOL_STREAM=$ps TXV_C5_INFLIGHT=$fl timeout -k 10 330 python3 -u bench.py --c5-only > $O/c5_m$ps$fl.json 2> >(tee $O/c5_m$ps$fl.err >&2) || { echo C5FAIL $m; tail -30 $O/c5_m$ps$fl.err; exit 5; }
-  python3 -c "
-import json
-d=json.load(open('$O/c5_m$ps$fl.json'))
-c=d['c5_streaming']; w=d.get('c5_wire',{})
-print('mode $m c5', c['votes_per_s'], c['votes_per_s_passes'], c['correct'], c['pool_matches_oracle'], c['p50_commit_latency_ms'], 'maxsize', c['pool_size_max'], 'host', c['host_cache']['votes_per_s'], 'unl', c['unloaded']['correct'], 'standalone', c['device_ms_batch']['standalone'])
-print('mode $m wire', w.get('votes_per_s'), w.get('votes_per_s_passes'), w.get('correct'), w.get('p50_commit_latency_ms'), w['unloaded']['correct'])"
-done
+TXV_PROFILE_HOST=1 TXV_C5_DEVICE_ONLY=1 TXV_BENCH_WATCHDOG=100 timeout -k 10 300 python3 -u bench.py --c5-only --no-wire > $O/c5.json 2> $O/c5.err || { echo C5FAIL; grep "^\[c5" $O/c5.err; tail -5 $O/c5.err; exit 5; }
+grep "^\[c5" $O/c5.err
+python3 - <<'PY'
+import re, collections, statistics
+d = collections.defaultdict(lambda: collections.defaultdict(list))
+for line in open("gpurun_out/r5_prof2/c5.err"):
+    if not line.startswith("[txv pool]"):
+        continue
+    body = line[len("[txv pool] "):].strip()
+    m = re.match(r"([a-z_ ]+?)((?: \w[\w+]*=[0-9.]+)+)$", body)
+    if not m:
+        continue
+    for k, v in re.findall(r"(\w[\w+]*)=([0-9.]+)", m.group(2)):
+        d[m.group(1).strip()][k].append(float(v))
+for what, kv in d.items():
+    print(what, {k: (len(v), round(statistics.median(v), 3), round(sum(v), 1)) for k, v in kv.items()})
+PY
 echo ALLDONE
