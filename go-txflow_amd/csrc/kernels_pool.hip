@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
     a.nfar[0] = 0;          // far pushes (appended by pd_link)
     a.tk[1] = 0;
     a.tk[2] = 0;
+    if (a.res) a.res[0] = a.res[1] = 0;
   }
   bool f[4];
 #pragma unroll
@@ -364,6 +365,18 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
     if (!old && i < a.n) a.lpos[i] = r[k];
     if (old && i < a.C) a.spos[i] = r[k];
   }
+  if (old || !a.okpos) return;   // (block-uniform) the pool list's appends: a third chain
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    f[k] = i < a.n && a.status[i] == TXV_POOL_OK;   // written by this thread above
+  }
+  tile_scan(f, r, a.tiles + 2 * (size_t)nt + (a.C + kTile - 1) / kTile, tile, a.epoch);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
+    if (i < a.n) a.okpos[i] = r[k];
+  }
 }
 
 // the new cache = the last keep_old surviving old entries in order, then the last keepU of the
@@ -426,6 +439,164 @@ __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_
   while (atomicCAS(&ci[s], 0u, q + 1u) != 0u) s = (s + 1) & (icap - 1);
 }
 
+// ---- the pool list in HBM (pool_dev.h PoolListArgs) ----
+__device__ __forceinline__ uint32_t list_home(const uint32_t* k) { return k[4] ^ (k[7] * 0x9E3779B1u); }
+__device__ __forceinline__ unsigned long long list_slot(uint32_t tag, uint32_t low) {
+  return ((unsigned long long)tag << 32) | low;
+}
+__device__ __forceinline__ unsigned long long slot_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// entry e's key == k, read at the coherence point (the entry may have been written by another CU
+// in this launch, before its index CAS)
+__device__ __forceinline__ bool list_key_eq(const uint32_t* lk, uint32_t e, const uint32_t k[8]) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  uint32_t d = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) d |= __hip_atomic_load(lk + (size_t)e * 8 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ k[w];
+  return d == 0;
+}
+// txsMap.Store(key, pos): insert, or -- the key indexed already (a vote admitted twice, the
+// earlier one still in the list) -- the later position stays indexed, as the sequential Stores
+// leave it; the other entry stays in the list, unindexed
+__device__ void list_insert(unsigned long long* li, uint32_t imask, const uint32_t* lk, uint32_t pos, const uint32_t k[8]) {
+  const uint32_t tg = k[3];
+  const unsigned long long mine = list_slot(tg, pos + 1);
+  uint32_t s = list_home(k) & imask;
+  for (uint32_t probe = 0; probe <= imask; ++probe, s = (s + 1) & imask) {
+    unsigned long long v = slot_load(li + s);
+    if (v == 0) {
+      v = atomicCAS(li + s, 0ull, mine);
+      if (v == 0) return;
+    }
+    if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb || !list_key_eq(lk, (uint32_t)v - 1, k)) continue;
+    for (;;) {
+      if ((uint32_t)v - 1 > pos) return;
+      const unsigned long long prev = atomicCAS(li + s, v, mine);
+      if (prev == v) return;
+      v = prev;                 // another insert of this key took the slot meanwhile
+    }
+  }
+}
+__device__ __forceinline__ void list_account(uint64_t* res, bool hit, uint64_t bytes) {
+  const uint64_t m = __ballot(hit);
+  for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o, 64);
+  if ((threadIdx.x & 63) == 0 && m) {
+    atomicAdd((unsigned long long*)res, (unsigned long long)__popcll(m));
+    atomicAdd((unsigned long long*)res + 1, (unsigned long long)bytes);
+  }
+}
+
+// addTx (txvotepool.go:265-270) for the batch's admitted votes in arrival order: txs.PushBack at
+// tail + rank, txsMap.Store
+__global__ void __launch_bounds__(256) pl_append(PoolListArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t tail = *a.tail_in;
+  bool ok = false;
+  uint64_t sz = 0;
+  if (i < a.n) {
+    ok = a.status[i] == TXV_POOL_OK;
+    if (ok) {
+      const uint32_t pos = tail + a.okpos[i];
+      const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
+      const uint4 k0 = src[0], k1 = src[1];
+      uint4* dst = reinterpret_cast<uint4*>(a.lk + (size_t)pos * 8);
+      dst[0] = k0;
+      dst[1] = k1;
+      sz = a.sizes[i];
+      a.lsz[pos] = (uint32_t)sz;
+      a.lfl[pos] = 1;
+      __threadfence();          // the entry before its index slot
+      const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+      list_insert(a.li, a.imask, a.lk, pos, k);
+    }
+    if (i == a.n - 1) *a.tail_out = tail + a.okpos[i] + (ok ? 1u : 0u);
+  }
+  list_account(a.res, ok, sz);
+}
+
+// Update's removeTx(tx, e, false) (txvotepool.go:339-344) for every committed key the index
+// holds: the slot becomes a tombstone, the entry dead (a key twice in the batch: removed once);
+// the bytes are the committed vote's Size(), as the host path subtracts them
+__global__ void __launch_bounds__(256) pl_remove(PoolListArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  bool hit = false;
+  uint64_t sz = 0;
+  if (i < a.n) {
+    uint32_t k[8];
+    const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
+    const uint4 k0 = src[0], k1 = src[1];
+    k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w; k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
+    const uint32_t tg = k[3];
+    uint32_t s = list_home(k) & a.imask;
+    for (uint32_t probe = 0; probe <= a.imask; ++probe, s = (s + 1) & a.imask) {
+      const unsigned long long v = slot_load(a.li + s);
+      if (v == 0) break;
+      if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb) continue;
+      const uint32_t e = (uint32_t)v - 1;
+      const uint4* ek = reinterpret_cast<const uint4*>(a.lk + (size_t)e * 8);
+      const uint4 e0 = ek[0], e1 = ek[1];
+      if (((e0.x ^ k0.x) | (e0.y ^ k0.y) | (e0.z ^ k0.z) | (e0.w ^ k0.w) | (e1.x ^ k1.x) | (e1.y ^ k1.y) |
+           (e1.z ^ k1.z) | (e1.w ^ k1.w)) != 0)
+        continue;
+      if (atomicCAS(a.li + s, v, list_slot(tg, kListTomb)) == v) {
+        a.lfl[e] = 0;
+        hit = true;
+        sz = a.sizes[i];
+      }
+      break;
+    }
+  }
+  list_account(a.res, hit, sz);
+}
+
+// compaction (the list's positions ran out): the live entries, in order, into the other buffer
+// (npos = exclusive scan of the old alive flags over [0, ocap)); the new flags written over the
+// whole new buffer; the new tail
+__global__ void __launch_bounds__(256) pl_move(const uint32_t* lk, const uint32_t* lsz, const uint8_t* lfl,
+                                               const uint32_t* npos, uint32_t ocap, uint32_t* nk, uint32_t* nsz,
+                                               uint8_t* nfl, uint32_t ncap, uint32_t* tail_out) {
+  const uint32_t o = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t live = npos[ocap - 1] + (lfl[ocap - 1] ? 1u : 0u);
+  if (o < ocap && lfl[o]) {
+    const uint32_t q = npos[o];
+    const uint4* s = reinterpret_cast<const uint4*>(lk + (size_t)o * 8);
+    uint4* d = reinterpret_cast<uint4*>(nk + (size_t)q * 8);
+    d[0] = s[0];
+    d[1] = s[1];
+    nsz[q] = lsz[o];
+  }
+  if (o < ncap) nfl[o] = o < live ? 1 : 0;
+  if (o == 0) *tail_out = live;
+}
+// the index over the moved entries: every indexed (non-tombstone) slot of the old index again at
+// its entry's new position (tombstones dropped; no key is compared: the keys are distinct)
+__global__ void __launch_bounds__(256) pl_reindex(const unsigned long long* oi, uint32_t oicap, const uint32_t* npos,
+                                                  const uint32_t* nk, unsigned long long* ni, uint32_t nmask) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= oicap) return;
+  const unsigned long long v = oi[s];
+  if (v == 0 || (uint32_t)v == kListTomb) return;
+  const uint32_t q = npos[(uint32_t)v - 1];
+  const uint32_t* k = nk + (size_t)q * 8;
+  uint32_t t = list_home(k) & nmask;
+  const unsigned long long mine = list_slot((uint32_t)(v >> 32), q + 1);
+  while (atomicCAS(ni + t, 0ull, mine) != 0ull) t = (t + 1) & nmask;
+}
+// the index of a list uploaded from the host: the positions marked in ins (each key once)
+__global__ void __launch_bounds__(256) pl_index_up(const uint32_t* lk, const uint8_t* ins, uint32_t L,
+                                                   unsigned long long* li, uint32_t imask) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= L || !ins[q]) return;
+  const uint32_t* k = lk + (size_t)q * 8;
+  uint32_t t = list_home(k) & imask;
+  const unsigned long long mine = list_slot(k[3], q + 1);
+  while (atomicCAS(li + t, 0ull, mine) != 0ull) t = (t + 1) & imask;
+}
+struct AliveU32 {
+  __host__ __device__ uint32_t operator()(uint8_t f) const { return f ? 1u : 0u; }
+};
+
 }  // namespace
 
 // hipcub temporary storage for a batch of n votes and a cache of C entries (scans of n and C,
@@ -472,5 +643,51 @@ extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t
   hipError_t e;
   if ((e = hipMemsetAsync(ci, 0, (size_t)icap * 4, st))) return e;
   if (L) hipLaunchKernelGGL(pd_index_only, dim3((L + 255) / 256), dim3(256), 0, st, ck, L, ci, icap);
+  return hipGetLastError();
+}
+
+// the pool list's batch kernels (pool_dev.h PoolListArgs): op 1 append, 2 remove
+extern "C" hipError_t txv_poollist_run(const PoolListArgs* ap, int op, hipStream_t st) {
+  const PoolListArgs& a = *ap;
+  if (!a.n) return hipSuccess;
+  const dim3 g((a.n + 255) / 256), b(256);
+  if (op == 1) hipLaunchKernelGGL(pl_append, g, b, 0, st, a);
+  else hipLaunchKernelGGL(pl_remove, g, b, 0, st, a);
+  return hipGetLastError();
+}
+
+// hipcub temporary storage of the compaction's scan over cap positions
+extern "C" size_t txv_poollist_tmp_bytes(uint32_t cap) {
+  size_t c = 0;
+  uint32_t* u = nullptr;
+  hipcub::TransformInputIterator<uint32_t, AliveU32, const uint8_t*> it(nullptr, AliveU32());
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, it, u, (int)std::max<uint32_t>(cap, 1));
+  return c;
+}
+
+// the compaction: old buffer (ocap positions, index oicap slots) -> new buffer (ncap, nicap);
+// npos [ocap] scratch, tmp hipcub storage
+extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* lsz, const uint8_t* lfl,
+                                           const unsigned long long* li, uint32_t ocap, uint32_t oicap, uint32_t* nk,
+                                           uint32_t* nsz, uint8_t* nfl, unsigned long long* ni, uint32_t ncap,
+                                           uint32_t nicap, uint32_t* npos, void* tmp, size_t tmp_bytes,
+                                           uint32_t* tail_out, hipStream_t st) {
+  hipError_t e;
+  hipcub::TransformInputIterator<uint32_t, AliveU32, const uint8_t*> it(lfl, AliveU32());
+  if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, it, npos, (int)ocap, st))) return e;
+  const uint32_t span = std::max(ocap, ncap);
+  hipLaunchKernelGGL(pl_move, dim3((span + 255) / 256), dim3(256), 0, st, lk, lsz, lfl, npos, ocap, nk, nsz, nfl, ncap,
+                     tail_out);
+  if ((e = hipMemsetAsync(ni, 0, (size_t)nicap * 8, st))) return e;
+  hipLaunchKernelGGL(pl_reindex, dim3((oicap + 255) / 256), dim3(256), 0, st, li, oicap, npos, nk, ni, nicap - 1);
+  return hipGetLastError();
+}
+
+// a list of L entries uploaded from the host (keys / sizes at lk / lsz): flags, index
+extern "C" hipError_t txv_poollist_upload_index(const uint32_t* lk, const uint8_t* ins, uint32_t L,
+                                                unsigned long long* li, uint32_t icap, hipStream_t st) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(li, 0, (size_t)icap * 8, st))) return e;
+  if (L) hipLaunchKernelGGL(pl_index_up, dim3((L + 255) / 256), dim3(256), 0, st, lk, ins, L, li, icap - 1);
   return hipGetLastError();
 }

@@ -279,11 +279,18 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L);
 int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after);
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after, int list_op,
+                  uint64_t live_ub);
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
-                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev);
+                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
+                    int list_op, uint64_t live_ub);
 int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
+int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t* sizes, const uint8_t* ins, uint32_t L);
+int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::vector<uint32_t>& sizes,
+                     std::vector<uint8_t>& ins);
+void pooldev_result(const PoolDev* s, int slot, int64_t* count, int64_t* bytes);
+constexpr int kListAppend = 1, kListRemove = 2;   // pooldev_enqueue's list_op
 constexpr int kPdRing = 4;   // = PoolDev::kPdRing (runtime.cpp)
 
 struct txv_pool {
@@ -305,24 +312,15 @@ struct txv_pool {
   // TXV_POOL_DEVICE_CACHE: the cache's copy in HBM (runtime.cpp's PoolDev) and which copy is current
   PoolDev* dev = nullptr;
   enum { kSynced, kDevAhead, kHostAhead } dev_state = kHostAhead;
-  // ... and the votes a device batch admitted are appended to txs / txsMap by a thread of the
-  // pool's own (on the context's host workers) while the next batch is decided; pend_* = admitted,
-  // not appended yet.  Every reader / writer of txs drains it first (drain_appends); Size and
-  // TxsBytes count the pending votes.  amu guards jobs, pend_*, txs.len and txs_bytes updates
-  // made by the appender.
-  struct Append {
-    std::vector<Key> keys; std::vector<uint32_t> sizes; uint32_t n = 0; uint64_t bytes = 0; txv_ctx* ctx = nullptr;
-    bool remove = false;   // Update: removeTx(tx, e, false) for every key the pool holds (txvotepool.go:339-344)
-  };
-  std::mutex amu;
-  std::condition_variable acv;
-  std::deque<Append> jobs, spare;
-  bool a_stop = false, a_busy = false;
-  int64_t pend_len = 0, pend_bytes = 0;
-  std::thread appender;
+  // ... and the pool list (txs + txsMap) too: a device batch appends its admitted votes there and
+  // a device Update removes its committed ones (runtime.cpp's list kernels), so while list_dev the
+  // host's txs / txs_map are stale -- a host reader or writer brings the list back first
+  // (list_to_host), the next device batch takes it up again (list_to_dev).  txs.len and txs_bytes
+  // stay current either way: they follow each finished device batch's counts.
+  bool list_dev = false;
   // Size() / TxsBytes() as published after every change (the reference's atomics, read without
-  // proxyMtx): txs.len / txs_bytes themselves are written under mu or by the appender under amu,
-  // so a reader holding neither must not touch them
+  // proxyMtx): txs.len / txs_bytes themselves are written under mu, so a reader not holding it
+  // must not touch them
   std::atomic<int64_t> pub_len{0}, pub_bytes{0};
   std::vector<uint8_t> rm_flag;                    // remove_keys scratch: per pool-list node
   std::vector<uint8_t> rm_part;                    // ... per key: its txsMap partition
@@ -344,10 +342,9 @@ struct txv_pool {
     uint64_t pushes = 0, bytes = 0;
     std::vector<uint8_t> st;
     int err = 0;
-    // an Update batch (txv_pool_update_submit): its keys pushed by the engine, its votes removed
-    // from the pool list by the appender once the tickets before it are finished; no caller waits
+    // an Update batch (txv_pool_update_submit): its keys pushed and its votes removed from the
+    // pool list by the engine in submission order; no caller waits for it
     bool upd = false;
-    std::vector<uint32_t> usizes;
   };
   std::deque<Ticket> tickets;
   uint64_t next_ticket = 1;
@@ -948,12 +945,6 @@ bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, ui
 }  // namespace
 
 txv_pool::~txv_pool() {
-  {
-    std::lock_guard<std::mutex> lk(amu);
-    a_stop = true;
-    acv.notify_all();
-  }
-  if (appender.joinable()) appender.join();              // the queued appends finish first
   pooldev_free(dev);
   for (PoolDev* d : retired) pooldev_free(d);
 }
@@ -990,7 +981,7 @@ namespace {
 // (p->sizes) are known: the order-dependent part (caps, cache, pool list).  p->mu is held.
 int cache_to_host(txv_pool* p, txv_ctx* ctx);
 void host_cache_written(txv_pool* p);
-void drain_appends(txv_pool* p);
+int list_to_host(txv_pool* p, txv_ctx* ctx);
 
 int drain_flights(txv_pool* p);
 void publish_locked(txv_pool* p);
@@ -1003,7 +994,7 @@ int pool_admit(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* 
 }
 int pool_admit_body(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out) {
   if (int r = drain_flights(p)) return r;
-  drain_appends(p);
+  if (int r = list_to_host(p, ctx)) return r;
   if (int r = cache_to_host(p, ctx)) return r;
   host_cache_written(p);
   const auto t1 = std::chrono::steady_clock::now();
@@ -1090,8 +1081,10 @@ int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
   // submitted batch finished first; moving to another GPU takes the current list along
   if (p->dev && (!pooldev_same_device(ctx, p->dev) || n > pooldev_cap(p->dev)))
     if (int r = drain_flights(p)) return r;
-  if (p->dev && !pooldev_same_device(ctx, p->dev))
+  if (p->dev && !pooldev_same_device(ctx, p->dev)) {
     if (int r = cache_to_host(p, ctx)) return r;
+    if (int r = list_to_host(p, ctx)) return r;
+  }
   if (p->dev && p->waiters && !pooldev_same_device(ctx, p->dev)) {   // a waiter may still sync on it
     p->retired.push_back(p->dev);
     p->dev = nullptr;
@@ -1108,53 +1101,59 @@ int cache_to_dev(txv_pool* p, txv_ctx* ctx, uint32_t n) {
   return TXV_OK;
 }
 
-// addTx for A admitted votes in arrival order (keys / sizes compacted): txs.PushBack, txsMap.Store
-// (a key admitted twice keeps its later node, as the sequential Store does).  txs.len and
-// txs_bytes are the caller's to update.
-void append_list(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, uint32_t A) {
-  if (!A) return;
-  next_indices(p->txs, A, p->idx_t);
-  p->txs.nodes.resize(std::max<size_t>(p->txs.nodes.size(), (size_t)p->idx_t[A - 1] + 1));
-  std::vector<uint8_t>& apart = p->part;                   // rank -> index partition
-  apart.resize(A);
-  const int32_t old_tail = p->txs.tail;
-  pool_parallel_for(p, ctx, A, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t a = lo; a < hi; ++a) {
-      p->txs.nodes[p->idx_t[a]] = KeyList::Node{keys[a], sizes[a], a ? p->idx_t[a - 1] : old_tail,
-                                                a + 1 < A ? p->idx_t[a + 1] : -1};
-      apart[a] = (uint8_t)PartIndex::part(keys[a]);
-    }
-  }, 4096);
-  if (old_tail >= 0) p->txs.nodes[old_tail].next = p->idx_t[0]; else p->txs.head = p->idx_t[0];
-  p->txs.tail = p->idx_t[A - 1];
-  const size_t nf = p->txs.free_.size();
-  p->txs.free_.resize(nf - std::min<size_t>(nf, A));
-  pool_parallel_for(p, ctx, kParts, [&](uint32_t q0, uint32_t q1) {
-    std::vector<uint32_t> mine;                            // this partition's ranks, in order
-    mine.reserve(A / kParts + A / (2 * kParts) + 16);
-    for (uint32_t q = q0; q < q1; ++q) {
+// the device's pool list back into txs / txsMap, in order (the entries txsMap indexes put there)
+int list_to_host(txv_pool* p, txv_ctx* ctx) {
+  if (!p->list_dev) return TXV_OK;
+  std::vector<uint8_t> kb, ins;
+  std::vector<uint32_t> sz;
+  if (int r = pooldev_list_get(ctx, p->dev, kb, sz, ins)) return r;
+  const uint32_t L = (uint32_t)sz.size();
+  const Key* keys = reinterpret_cast<const Key*>(kb.data());
+  KeyList& T = p->txs;
+  T.clear();
+  T.nodes.resize(L);
+  for (uint32_t e = 0; e < L; ++e) T.nodes[e] = KeyList::Node{keys[e], sz[e], (int32_t)e - 1, e + 1 < L ? (int32_t)e + 1 : -1};
+  T.head = L ? 0 : -1;
+  T.tail = (int32_t)L - 1;
+  T.len = L;
+  pool_parallel_for(p, ctx, kParts, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t q = lo; q < hi; ++q) {
       FlatIndex& f = *p->txs_map.p[q];
-      mine.clear();
-      for (uint32_t a = 0; a < A; ++a)
-        if (apart[a] == q) mine.push_back(a);
-      const size_t m = mine.size();
-      for (size_t j = 0; j < m; ++j) {                     // DRAM-latency bound: slots prefetched ahead
-        if (j + kAdmitAhead < m) f.prefetch(keys[mine[j + kAdmitAhead]]);
-        f.put(keys[mine[j]], p->idx_t[mine[j]]);
-      }
+      f.clear();
+      for (uint32_t e = 0; e < L; ++e)
+        if (ins[e] && PartIndex::part(keys[e]) == q) f.put(keys[e], (int32_t)e);
     }
   }, 1);
+  p->list_dev = false;
+  return TXV_OK;
 }
 
-// with amu held, or the appender idle (after drain_appends)
+// the host's pool list into HBM before a device batch (p->dev bound)
+int list_to_dev(txv_pool* p, txv_ctx* ctx) {
+  if (p->list_dev) return TXV_OK;
+  const KeyList& T = p->txs;
+  std::vector<Key> kl;
+  std::vector<uint32_t> sz;
+  std::vector<uint8_t> ins;
+  kl.reserve(T.len); sz.reserve(T.len); ins.reserve(T.len);
+  for (int32_t e = T.head; e >= 0; e = T.nodes[e].next) {
+    kl.push_back(T.nodes[e].k);
+    sz.push_back(T.nodes[e].size);
+    ins.push_back(p->txs_map.find(T.nodes[e].k) == e);
+  }
+  if (int r = pooldev_list_put(ctx, p->dev, reinterpret_cast<const uint8_t*>(kl.data()), sz.data(), ins.data(),
+                               (uint32_t)kl.size()))
+    return r;
+  p->list_dev = true;
+  return TXV_OK;
+}
+
+// with mu held
 void publish(txv_pool* p) {
-  p->pub_len.store((int64_t)p->txs.len + p->pend_len, std::memory_order_relaxed);
-  p->pub_bytes.store(p->txs_bytes + p->pend_bytes, std::memory_order_relaxed);
+  p->pub_len.store((int64_t)p->txs.len, std::memory_order_relaxed);
+  p->pub_bytes.store(p->txs_bytes, std::memory_order_relaxed);
 }
-void publish_locked(txv_pool* p) {
-  std::lock_guard<std::mutex> lk(p->amu);
-  publish(p);
-}
+void publish_locked(txv_pool* p) { publish(p); }
 
 // removeTx(tx, e, false) for every key of keys[n] the pool holds (Update, txvotepool.go:339-344),
 // on the worker threads: (1) per txsMap partition, find + erase its keys (a key twice in the batch
@@ -1162,11 +1161,11 @@ void publish_locked(txv_pool* p) {
 // (its first node's predecessor unflagged) relinks around the run -- runs touch disjoint
 // neighbours, so no two threads write one pointer; (4) free list.  Returns the bytes removed (the
 // Update votes' Size(), as the reference subtracts tx.Size()) and *count the nodes removed: the
-// caller lowers txs.len (under amu on the appender).  The caller owns the pool list (the
-// appender, or a host path that drained it).
+// caller lowers txs.len.  The pool list is the host's (list_to_host).
 int64_t remove_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, uint32_t n, size_t* count) {
   *count = 0;
   if (!n) return 0;
+  PTimer tm("remove_keys");
   // the keys' partitions in chunks, then each partition's keys in batch order (a counting sort):
   // every worker then walks a dense list with its lookups prefetched ahead (DRAM-latency bound)
   std::vector<uint8_t>& pt = p->rm_part;
@@ -1194,6 +1193,7 @@ int64_t remove_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
       for (uint32_t i = (uint32_t)((uint64_t)n * c / nc); i < (uint32_t)((uint64_t)n * (c + 1) / nc); ++i)
         ord[off[(size_t)c * kParts + pt[i]]++] = i;
   }, 1);
+  tm.mark("order");
   std::vector<int32_t> found[kParts];
   int64_t bytes[kParts] = {};
   pool_parallel_for(p, ctx, kParts, [&](uint32_t lo, uint32_t hi) {
@@ -1216,6 +1216,7 @@ int64_t remove_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
     all.insert(all.end(), found[q].begin(), found[q].end());
     removed_bytes += bytes[q];
   }
+  tm.mark("take");
   if (all.empty()) return 0;
   KeyList& L = p->txs;
   std::vector<uint8_t>& rm = p->rm_flag;
@@ -1235,122 +1236,14 @@ int64_t remove_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* 
       if (nx >= 0) L.nodes[nx].prev = pv; else L.tail = pv;
     }
   }, 4096);
+  tm.mark("relink");
   for (int32_t e : all) {
     rm[e] = 0;
     L.free_.push_back(e);
   }
+  tm.mark("free");
   *count = m;
   return removed_bytes;
-}
-
-void appender_loop(txv_pool* p) {
-  std::unique_lock<std::mutex> lk(p->amu);
-  for (;;) {
-    p->acv.wait(lk, [&] { return p->a_stop || !p->jobs.empty(); });
-    if (p->jobs.empty()) return;                           // stopping, nothing left
-    txv_pool::Append j = std::move(p->jobs.front());
-    p->jobs.pop_front();
-    p->a_busy = true;
-    const size_t backlog = p->jobs.size();
-    lk.unlock();
-    int64_t removed_bytes = 0;
-    size_t removed = 0;
-    {
-      PTimer pt(j.remove ? "appender remove" : "appender append");
-      if (j.remove) {
-        removed_bytes = remove_keys(p, j.ctx, j.keys.data(), j.sizes.data(), j.n, &removed);
-      } else {
-        append_list(p, j.ctx, j.keys.data(), j.sizes.data(), j.n);
-      }
-      pt.mark(backlog > 9 ? "n9+" : (backlog > 3 ? "n4+" : "n0+"));
-    }
-    lk.lock();
-    if (j.remove) {
-      p->txs.len -= removed;
-      p->txs_bytes -= removed_bytes;
-    } else {
-      p->txs.len += j.n;
-      p->txs_bytes += (int64_t)j.bytes;
-      p->pend_len -= j.n;
-      p->pend_bytes -= (int64_t)j.bytes;
-    }
-    publish(p);
-    p->a_busy = false;
-    p->spare.push_back(std::move(j));                      // its buffers serve a later batch
-    p->acv.notify_all();
-  }
-}
-
-// every queued append done (the appender idle): txs / txsMap / txs_bytes are the host's to use
-void drain_appends(txv_pool* p) {
-  std::unique_lock<std::mutex> lk(p->amu);
-  p->acv.wait(lk, [&] { return p->jobs.empty() && !p->a_busy; });
-}
-
-// the votes of a device batch with status TXV_POOL_OK, compacted in arrival order, queued for the
-// appender (Size / TxsBytes count them at once)
-void queue_admitted(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, const uint8_t* st, uint32_t n) {
-  txv_pool::Append j;
-  {
-    std::lock_guard<std::mutex> lk(p->amu);
-    if (!p->spare.empty()) { j = std::move(p->spare.front()); p->spare.pop_front(); }
-  }
-  const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(64, n / 2048));
-  std::vector<uint32_t> cnt_c(P, 0), base_c(P, 0);
-  std::vector<uint64_t> bytes_c(P, 0);
-  auto chunk = [&](uint32_t c, uint32_t& lo, uint32_t& hi) {
-    lo = (uint32_t)((uint64_t)n * c / P); hi = (uint32_t)((uint64_t)n * (c + 1) / P);
-  };
-  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
-    for (uint32_t c = c0; c < c1; ++c) {
-      uint32_t lo, hi, k = 0;
-      uint64_t b = 0;
-      chunk(c, lo, hi);
-      for (uint32_t i = lo; i < hi; ++i)
-        if (st[i] == TXV_POOL_OK) { ++k; b += sizes[i]; }
-      cnt_c[c] = k;
-      bytes_c[c] = b;
-    }
-  }, 1);
-  uint32_t A = 0;
-  uint64_t bytes = 0;
-  for (uint32_t c = 0; c < P; ++c) { base_c[c] = A; A += cnt_c[c]; bytes += bytes_c[c]; }
-  if (!A) return;
-  if (j.keys.size() < A) { j.keys.resize(A); j.sizes.resize(A); }
-  pool_parallel_for(p, ctx, P, [&](uint32_t c0, uint32_t c1) {
-    for (uint32_t c = c0; c < c1; ++c) {
-      uint32_t lo, hi, a = base_c[c];
-      chunk(c, lo, hi);
-      for (uint32_t i = lo; i < hi; ++i)
-        if (st[i] == TXV_POOL_OK) { j.keys[a] = keys[i]; j.sizes[a] = sizes[i]; ++a; }
-    }
-  }, 1);
-  j.n = A;
-  j.bytes = bytes;
-  j.ctx = ctx;
-  j.remove = false;                                        // a spare may have carried Update's removals
-  std::lock_guard<std::mutex> lk(p->amu);
-  if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
-  p->pend_len += A;
-  p->pend_bytes += (int64_t)bytes;
-  publish(p);
-  p->jobs.push_back(std::move(j));
-  p->acv.notify_all();
-}
-
-// Update's pool-list removals, queued behind every append queued before them
-void queue_removal(txv_pool* p, txv_ctx* ctx, std::vector<Key>&& keys, std::vector<uint32_t>&& sizes) {
-  txv_pool::Append j;
-  j.ctx = ctx;
-  j.n = (uint32_t)keys.size();
-  if (!j.n) return;
-  j.keys = std::move(keys);
-  j.sizes = std::move(sizes);
-  j.remove = true;
-  std::lock_guard<std::mutex> lk(p->amu);
-  if (!p->appender.joinable()) p->appender = std::thread(appender_loop, p);
-  p->jobs.push_back(std::move(j));
-  p->acv.notify_all();
 }
 
 // finished Update tickets leave the queue (no caller waits for them)
@@ -1362,30 +1255,33 @@ void prune_updates(txv_pool* p) {
 // a device batch needs the pool's Size and MaxTxsBytes caps not to bind inside it (pushes: the
 // votes that reach cache.Push, bytes: the Size() sum of the checked votes)
 bool dev_caps_ok(txv_pool* p, uint64_t pushes, uint64_t bytes) {
-  std::lock_guard<std::mutex> lk(p->amu);
-  return (int64_t)p->txs.len + p->pend_len + p->infl_len + (int64_t)pushes < (int64_t)p->cfg.size &&
-         p->txs_bytes + p->pend_bytes + p->infl_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
+  return (int64_t)p->txs.len + p->infl_len + (int64_t)pushes < (int64_t)p->cfg.size &&
+         p->txs_bytes + p->infl_bytes + (int64_t)bytes <= (int64_t)p->cfg.max_txs_bytes;
 }
 
-// a submitted device batch's statuses in (its decisions were made in submission order on the
-// engine's stream), its admitted votes queued for the appender, its flight slot free
+// an upper bound of the pool list's live entries before the next device batch (its own excluded)
+uint64_t live_ub(const txv_pool* p) { return (uint64_t)p->txs.len + (uint64_t)std::max<int64_t>(0, p->infl_len); }
+
+// a device batch's list counts in (appended: + ; removed: -)
+void list_counts(txv_pool* p, int slot, bool removed) {
+  int64_t cnt, by;
+  pooldev_result(p->dev, slot, &cnt, &by);
+  if (removed) { p->txs.len -= (size_t)cnt; p->txs_bytes -= by; }
+  else { p->txs.len += (size_t)cnt; p->txs_bytes += by; }
+  publish(p);
+}
+
+// a submitted device batch's statuses in (its decisions, appends and removals were made in
+// submission order on the engine's stream), its list counts taken, its flight slot free
 int finish_ticket(txv_pool* p, txv_pool::Ticket& t) {
   if (t.done) return t.err;
   const uint8_t* st;
-  const uint8_t* kp;
-  const uint32_t* sz;
   t.done = true;
   p->infl_len -= (int64_t)t.pushes;
   p->infl_bytes -= (int64_t)t.bytes;
-  if (t.upd) {                                             // the engine's pushes done; the removals queued
-    if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
-    const Key* k = reinterpret_cast<const Key*>(kp);
-    queue_removal(p, t.ctx, std::vector<Key>(k, k + t.n), std::move(t.usizes));
-    return TXV_OK;
-  }
-  if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, &kp, &sz))) return t.err;
-  t.st.assign(st, st + t.n);
-  queue_admitted(p, t.ctx, reinterpret_cast<const Key*>(kp), sz, st, t.n);
+  if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, nullptr, nullptr))) return t.err;
+  if (!t.upd) t.st.assign(st, st + t.n);
+  list_counts(p, t.slot, t.upd);
   return TXV_OK;
 }
 
@@ -1419,11 +1315,12 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
   int r;
   if ((r = drain_flights(p))) return r;
   if ((r = cache_to_dev(p, ctx, n))) return r;
+  if ((r = list_to_dev(p, ctx))) return r;
   if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
-                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after)))
+                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after, kListAppend, live_ub(p))))
     return r;
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-  queue_admitted(p, ctx, reinterpret_cast<const Key*>(h_keys), h_sizes, status_out, n);
+  list_counts(p, 0, false);
   *done = true;
   return TXV_OK;
 }
@@ -1451,11 +1348,13 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
       int r;
       if ((r = drain_flights(p))) return r;
       if ((r = cache_to_dev(p, ctx, n))) return r;
+      if ((r = list_to_dev(p, ctx))) return r;
       if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr)))
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr, kListAppend,
+                             live_ub(p))))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      queue_admitted(p, ctx, reinterpret_cast<const Key*>(keys32), sizes, status_out, n);
+      list_counts(p, 0, false);
       return TXV_OK;
     }
   }
@@ -1508,8 +1407,9 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
         if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
       pt.mark("prev");
       if ((r = cache_to_dev(p, ctx, v->n))) return r;
+      if ((r = list_to_dev(p, ctx))) return r;
       if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
-                               (p->cfg.flags & TXV_POOL_WAL) != 0, true, nullptr)))
+                               (p->cfg.flags & TXV_POOL_WAL) != 0, false, nullptr, kListAppend, live_ub(p))))
         return r;
       pt.mark("enqueue");
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
@@ -1602,13 +1502,12 @@ int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_
   });
 }
 
-// Update (txvotepool.go:329-359) with the cache in HBM: the committed votes' keys (SHA-256 of the
-// signatures) are hashed and pushed by the device engine in stream order behind the batches
-// submitted before (every key pushed: cache.Push ignores Size), their keys come back with the
-// flight, and their pool-list removals are queued for the pool's appender when the ticket is
-// finished, behind every append queued before them -- no flight is drained and the cache list is
-// not copied back.  The effects are in place once the tickets submitted before are finished
-// (txv_pool_check_wait, txv_pool_sync, any reader).  Signatures > 64 bytes take the host path.
+// Update (txvotepool.go:329-359) with the cache and the pool list in HBM: the committed votes'
+// keys (SHA-256 of the signatures) are hashed, pushed (every key: cache.Push ignores Size) and
+// removed from the pool list by the device engine in stream order behind the batches submitted
+// before -- no flight is drained, nothing is copied back but the removal counts.  Size and
+// TxsBytes follow once the tickets submitted before are finished (txv_pool_check_wait,
+// txv_pool_sync, any reader).  Signatures > 64 bytes take the host path.
 int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   const uint32_t n = v->n;
   PTimer pt("update_submit");
@@ -1616,9 +1515,9 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   t.upd = true;
   t.ctx = ctx;
   t.n = n;
-  t.usizes.resize(n);
+  p->sizes.resize(n);
   pool_parallel_for(p, ctx, n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) t.usizes[i] = vote_size(v, i);
+    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
   }, 4096);
   pt.mark("sizes");
   int r;
@@ -1628,8 +1527,9 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   prune_updates(p);
   pt.mark("prev");
   if ((r = cache_to_dev(p, ctx, n))) return r;
-  if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, t.usizes.data(), nullptr, nullptr, nullptr, 0, n, INT64_MAX,
-                           false, true, nullptr)))
+  if ((r = list_to_dev(p, ctx))) return r;
+  if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, n, INT64_MAX,
+                           false, false, nullptr, kListRemove, live_ub(p))))
     return r;
   pt.mark("enqueue");
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
@@ -1639,30 +1539,37 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   return TXV_OK;
 }
 
+// Update with the committed votes' keys and Size() values known (every flight and append
+// drained first, the cache brought to the host)
+int update_host_keys(txv_pool* p, txv_ctx* ctx, const Key* keys, const uint32_t* sizes, uint32_t n) {
+  int r;
+  if ((r = drain_flights(p))) return r;
+  if ((r = list_to_host(p, ctx))) return r;
+  if ((r = cache_to_host(p, ctx))) return r;
+  host_cache_written(p);
+  PTimer pt("update_host");
+  if (p->cache_on)                                 // cache.Push of every committed key, in order
+    for (uint32_t i = 0; i < n; ++i) {
+      if (i + 16 < n) p->cache_map.prefetch(keys[i + 16]);
+      (void)p->cache_push(keys[i]);
+    }
+  pt.mark("cache");
+  size_t removed = 0;                              // removeTx(tx, e, false) of the ones the pool holds
+  p->txs_bytes -= remove_keys(p, ctx, keys, sizes, n, &removed);
+  p->txs.len -= removed;
+  publish_locked(p);
+  pt.mark("remove");
+  return TXV_OK;
+}
+
 int update_host(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full, const uint64_t* sig_full_off) {
   int r = batch_keys(p, ctx, v, sig_full, sig_full_off);
   if (r) return r;
-  if ((r = drain_flights(p))) return r;
-  drain_appends(p);
-  if ((r = cache_to_host(p, ctx))) return r;
-  host_cache_written(p);
-  const Key* keys = reinterpret_cast<const Key*>(p->keys.data());
-  if (p->cache_on)                                 // cache.Push of every committed key, in order
-    for (uint32_t i = 0; i < v->n; ++i) {
-      if (i + 16 < v->n) p->cache_map.prefetch(keys[i + 16]);
-      Key k;
-      memcpy(k.b, p->keys.data() + (size_t)i * 32, 32);
-      (void)p->cache_push(k);
-    }
-  std::vector<uint32_t> sz(v->n);                  // removeTx(tx, e, false) of the ones the pool holds
+  std::vector<uint32_t> sz(v->n);
   pool_parallel_for(p, ctx, v->n, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t i = lo; i < hi; ++i) sz[i] = vote_size(v, i);
   }, 4096);
-  size_t removed = 0;
-  p->txs_bytes -= remove_keys(p, ctx, keys, sz.data(), v->n, &removed);
-  p->txs.len -= removed;
-  publish_locked(p);
-  return TXV_OK;
+  return update_host_keys(p, ctx, reinterpret_cast<const Key*>(p->keys.data()), sz.data(), v->n);
 }
 
 int txv_pool_update_submit(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
@@ -1678,23 +1585,31 @@ int txv_pool_update_submit(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_
   return update_host(p, ctx, v, sig_full, sig_full_off);
 }
 
-// Update applied when it returns: the device path's submission, then every ticket before it and
-// the queued appends / removals finished (no cache copy back)
+// Update applied when it returns: the device path's submission, then every ticket up to it
+// finished (no cache or list copy back)
 int txv_pool_update(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
                     const uint64_t* sig_full_off) {
   int r = txv_pool_update_submit(p, ctx, height, v, sig_full, sig_full_off);
   if (r || !dev_mode(p)) return r;
   std::lock_guard<std::mutex> g(p->mu);
-  if ((r = drain_flights(p))) return r;
-  drain_appends(p);
-  return TXV_OK;
+  return drain_flights(p);
+}
+
+// Update with the committed votes given as (txVoteKey, Size()) pairs (the keys computed by the
+// caller, as for txv_pool_check_keys); applied when it returns, ctx optional
+int txv_pool_update_keys(txv_pool* p, txv_ctx* ctx, int64_t height, const uint8_t* keys32, const uint32_t* sizes,
+                         uint32_t n) {
+  if (!p || (n && (!keys32 || !sizes))) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->height = height;
+  return update_host_keys(p, ctx, reinterpret_cast<const Key*>(keys32), sizes, n);
 }
 
 int txv_pool_reap(txv_pool* p, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap, uint64_t* n_out) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   if (int r = drain_flights(p)) return r;
-  drain_appends(p);
+  if (int r = list_to_host(p, nullptr)) return r;
   if (max < 0) max = (int64_t)p->txs.len;
   uint64_t n = 0;
   for (int32_t e = p->txs.head; e >= 0 && (int64_t)n <= max; e = p->txs.nodes[e].next, ++n) {
@@ -1799,10 +1714,10 @@ int txv_pool_flush(txv_pool* p) {
   if (!p) return TXV_EINVAL;
   std::lock_guard<std::mutex> g(p->mu);
   (void)drain_flights(p);
-  drain_appends(p);
   p->cache.clear(); p->cache_map.clear();
   host_cache_written(p);
   p->txs.clear(); p->txs_map.clear();
+  p->list_dev = false;                                     // the device's copy is dropped (re-sent empty)
   p->txs_bytes = 0;
   publish_locked(p);
   return TXV_OK;
@@ -1816,11 +1731,10 @@ int txv_pool_sync(txv_pool* p) {
     if (std::any_of(p->tickets.begin(), p->tickets.end(), [](const txv_pool::Ticket& t) { return t.upd; }))
       if ((r = drain_flights(p))) return r;               // submitted Updates applied
   }
-  drain_appends(p);
   return TXV_OK;
 }
 
-// Size / TxsBytes count the votes a device batch admitted whose append is still queued
+// Size / TxsBytes as of the last finished batch
 int64_t txv_pool_size(txv_pool* p) {
   return p ? p->pub_len.load(std::memory_order_relaxed) : 0;
 }

@@ -3125,6 +3125,15 @@ int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_
 extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C);
 extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* a, hipStream_t st);
 extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st);
+extern "C" hipError_t txv_poollist_run(const PoolListArgs* a, int op, hipStream_t st);
+extern "C" size_t txv_poollist_tmp_bytes(uint32_t cap);
+extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* lsz, const uint8_t* lfl,
+                                           const unsigned long long* li, uint32_t ocap, uint32_t oicap, uint32_t* nk,
+                                           uint32_t* nsz, uint8_t* nfl, unsigned long long* ni, uint32_t ncap,
+                                           uint32_t nicap, uint32_t* npos, void* tmp, size_t tmp_bytes,
+                                           uint32_t* tail_out, hipStream_t st);
+extern "C" hipError_t txv_poollist_upload_index(const uint32_t* lk, const uint8_t* ins, uint32_t L,
+                                                unsigned long long* li, uint32_t icap, hipStream_t st);
 
 struct PoolDev {
   int device = -1;
@@ -3142,6 +3151,23 @@ struct PoolDev {
   uint32_t epoch = 0;                      // batches run: the look-back words' tag
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  uint32_t* okpos = nullptr;               // [cap_n] the list appends' ranks
+  // the pool list (pool_dev.h PoolListArgs): two buffers, the current one `lcur` (a compaction
+  // moves the live entries into the other), each with its own capacity; the tail in a pair of
+  // words, ltp the current one (an append writes the other)
+  struct ListBuf {
+    uint32_t *k = nullptr, *sz = nullptr;
+    uint8_t* fl = nullptr;
+    unsigned long long* ix = nullptr;
+    uint32_t cap = 0, icap = 0;
+  } lb[2];
+  int lcur = 0, ltp = 0;
+  uint32_t* ltail = nullptr;               // [2]
+  uint32_t* lnpos = nullptr;               // compaction scratch [lnpos_cap]
+  uint32_t lnpos_cap = 0;
+  void* ltmp = nullptr;
+  size_t ltmp_bytes = 0;
+  uint64_t tail_ub = 0;                    // host: an upper bound of the tail (the appends enqueued)
   // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
   static constexpr int kPdRing = 4;
   struct Flight {
@@ -3149,6 +3175,7 @@ struct PoolDev {
     uint8_t* d_status = nullptr;
     uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr;
     uint8_t* h_status = nullptr;
+    uint64_t *d_res = nullptr, *h_res = nullptr;   // the list kernels' (entries, bytes)
     hipEvent_t ev = nullptr;
   } fl[kPdRing];
   uint32_t* h_clen = nullptr;
@@ -3165,10 +3192,13 @@ struct PoolDev {
     for (int b = 0; b < 2; ++b) { dfree(ck[b]); dfree(ci[b]); }
     dfree(clen); dfree(push); dfree(aidx); dfree(hkey); dfree(hidx); dfree(skey); dfree(sidx);
     dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
-    dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn); dfree(tiles); dfree(tk);
+    dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn); dfree(tiles); dfree(tk); dfree(okpos);
+    for (ListBuf& b : lb) { dfree(b.k); dfree(b.sz); dfree(b.fl); dfree(b.ix); }
+    dfree(ltail); dfree(lnpos);
+    if (ltmp) (void)hipFree(ltmp);
     for (Flight& f : fl) {
-      dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
-      hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status);
+      dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status); dfree(f.d_res);
+      hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status); hfree(f.h_res);
       if (f.ev) (void)hipEventDestroy(f.ev);
     }
     if (tmp) (void)hipFree(tmp);
@@ -3181,6 +3211,12 @@ struct PoolDev {
 void pooldev_free(PoolDev* s) { delete s; }
 bool pooldev_same_device(const txv_ctx* c, const PoolDev* s) { return c && s && c->device == s->device; }
 uint32_t pooldev_cap(const PoolDev* s) { return s ? s->cap_n : 0; }
+
+// look-back words: per 1024 votes the push, last and list-append chains, per 1024 cache entries
+// the survivors' chain
+size_t pooldev_tile_words(uint32_t m, uint32_t C) {
+  return 3 * (((size_t)m + 1023) / 1024) + ((size_t)std::max<uint32_t>(C, 1) + 1023) / 1024;
+}
 
 // (re)binds the engine to c's device with capacity C and room for n-vote batches; a new cache
 // starts empty (length 0)
@@ -3202,9 +3238,10 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     if ((r = dalloc(c, &s->ck[0], cw * 8)) || (r = dalloc(c, &s->ck[1], cw * 8)) || (r = dalloc(c, &s->ci[0], s->icap)) ||
         (r = dalloc(c, &s->ci[1], s->icap)) || (r = dalloc(c, &s->clen, 2)) || (r = dalloc(c, &s->detached, cw)) ||
         (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 2)) ||
-        (r = halloc(c, &s->h_clen, 2)) || (r = dalloc(c, &s->tk, 4)))
+        (r = halloc(c, &s->h_clen, 2)) || (r = dalloc(c, &s->tk, 4)) || (r = dalloc(c, &s->ltail, 2)))
       return r;
     HIP_TRY(c, hipMemset(s->tk, 0, 16));
+    HIP_TRY(c, hipMemset(s->ltail, 0, 8));
     HIP_TRY(c, hipMemset(s->ci[0], 0, (size_t)s->icap * 4));
     HIP_TRY(c, hipMemset(s->clen, 0, 8));
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
@@ -3233,14 +3270,14 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
         (r = dalloc(c, &s->lpos, m)) || (r = dalloc(c, &s->far, m)) || (r = dalloc(c, &s->dec, m)) ||
         (r = dalloc(c, &s->pst, m)) || (r = dalloc(c, &s->pend, m)) ||
         (r = dalloc(c, &s->xs, ((size_t)m + 1023) / 1024 * 1024)) || (r = dalloc(c, &s->xn, ((size_t)m + 1023) / 1024)) ||
-        (r = dalloc(c, &s->tiles, 2 * (((size_t)m + 1023) / 1024) + ((size_t)std::max<uint32_t>(C, 1) + 1023) / 1024)))
+        (r = dalloc(c, &s->tiles, pooldev_tile_words(m, C))) || (r = dalloc(c, &s->okpos, m)))
       return r;
-    HIP_TRY(c, hipMemset(s->tiles, 0, (2 * (((size_t)m + 1023) / 1024) + ((size_t)std::max<uint32_t>(C, 1) + 1023) / 1024) * 8));
+    HIP_TRY(c, hipMemset(s->tiles, 0, pooldev_tile_words(m, C) * 8));
     for (PoolDev::Flight& f : s->fl)
       if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
           (r = dalloc(c, &f.d_sizes, m)) || (r = dalloc(c, &f.d_status, m)) || (r = halloc(c, &f.h_sig, (size_t)m * 16)) ||
           (r = halloc(c, &f.h_len, m)) || (r = halloc(c, &f.h_keys, (size_t)m * 8)) || (r = halloc(c, &f.h_sizes, m)) ||
-          (r = halloc(c, &f.h_status, m)))
+          (r = halloc(c, &f.h_status, m)) || (r = dalloc(c, &f.d_res, 2)) || (r = halloc(c, &f.h_res, 2)))
         return r;
     s->cap_n = m;
     const size_t tb = txv_pooldev_tmp_bytes(m, std::max<uint32_t>(C, 1));
@@ -3297,6 +3334,140 @@ int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
 }
 #undef PD_TRY
 
+// ---- the pool list in HBM (pool_dev.h PoolListArgs) ----
+int list_buf_alloc(txv_ctx* c, PoolDev::ListBuf& b, uint32_t cap) {
+  uint32_t icap = 16;
+  while (icap < 2 * cap) icap *= 2;
+  int r;
+  if ((r = dalloc(c, &b.k, (size_t)cap * 8)) || (r = dalloc(c, &b.sz, cap)) || (r = dalloc(c, &b.fl, cap)) ||
+      (r = dalloc(c, &b.ix, icap)))
+    return r;
+  b.cap = cap;
+  b.icap = icap;
+  return TXV_OK;
+}
+uint32_t list_cap_for(uint64_t need) {   // a power of two >= need, >= 64k
+  uint64_t cap = 1u << 16;
+  while (cap < need) cap *= 2;
+  return cap > (1u << 30) ? 0u : (uint32_t)cap;
+}
+
+// the current buffer exists (first use: empty, room for four batches)
+int list_ready(txv_ctx* c, PoolDev* s) {
+  PoolDev::ListBuf& b = s->lb[s->lcur];
+  if (b.cap) return TXV_OK;
+  int r;
+  if ((r = list_buf_alloc(c, b, list_cap_for(4 * (uint64_t)s->cap_n)))) return r;
+  HIP_TRY(c, hipMemset(b.fl, 0, b.cap));
+  HIP_TRY(c, hipMemset(b.ix, 0, (size_t)b.icap * 8));
+  HIP_TRY(c, hipMemset(s->ltail, 0, 8));
+  s->tail_ub = 0;
+  return TXV_OK;
+}
+
+// positions ran out (the tail bound + n past the capacity): the live entries (at most live_ub)
+// move, in order, into the other buffer, sized so that at least half of it is free after; the
+// index is rebuilt there without its tombstones
+int list_compact(txv_ctx* c, PoolDev* s, hipStream_t ks, uint64_t live_ub, uint32_t n) {
+  PoolDev::ListBuf& o = s->lb[s->lcur];
+  PoolDev::ListBuf& nb = s->lb[s->lcur ^ 1];
+  const uint32_t ncap = std::max(o.cap, list_cap_for(2 * (live_ub + n)));
+  if (!ncap) { c->err = "pool list above 2^30 entries"; return TXV_ECAPACITY; }
+  const size_t tb = txv_poollist_tmp_bytes(o.cap);
+  if (nb.cap < ncap || s->lnpos_cap < o.cap || s->ltmp_bytes < tb) {
+    HIP_TRY(c, hipStreamSynchronize(ks));                // earlier work may still read the buffers
+    int r;
+    if (nb.cap < ncap && (r = list_buf_alloc(c, nb, ncap))) return r;
+    if (s->lnpos_cap < o.cap) {
+      if ((r = dalloc(c, &s->lnpos, o.cap))) return r;
+      s->lnpos_cap = o.cap;
+    }
+    if (s->ltmp_bytes < tb) {
+      if (s->ltmp) (void)hipFree(s->ltmp);
+      s->ltmp = nullptr;
+      HIP_TRY(c, hipMalloc(&s->ltmp, tb));
+      s->ltmp_bytes = tb;
+    }
+  }
+  HIP_TRY(c, txv_poollist_compact(o.k, o.sz, o.fl, o.ix, o.cap, o.icap, nb.k, nb.sz, nb.fl, nb.ix, nb.cap, nb.icap,
+                                  s->lnpos, s->ltmp, s->ltmp_bytes, s->ltail + (s->ltp ^ 1), ks));
+  s->ltp ^= 1;
+  s->lcur ^= 1;
+  s->tail_ub = live_ub;
+  return TXV_OK;
+}
+
+// the host's pool list becomes the device's: L entries in order (keys [L][32], sizes), ins[e] = 1
+// for the entries txsMap indexes (synchronous, on the engine's own stream)
+int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t* sizes, const uint8_t* ins, uint32_t L) {
+  HIP_TRY(c, hipSetDevice(s->device));
+  s->quiesce();
+  int r;
+  const uint32_t cap = list_cap_for(2 * ((uint64_t)L + 4 * (uint64_t)s->cap_n));
+  if (!cap) { c->err = "pool list above 2^30 entries"; return TXV_ECAPACITY; }
+  PoolDev::ListBuf& b = s->lb[s->lcur];
+  if (b.cap < cap && (r = list_buf_alloc(c, b, cap))) return r;
+  uint8_t* d_ins = nullptr;
+  if (L && (r = dalloc(c, &d_ins, L))) return r;
+  HIP_TRY(c, hipMemsetAsync(b.fl, 0, b.cap, s->st));
+  if (L) {
+    HIP_TRY(c, hipMemcpyAsync(b.k, keys, (size_t)L * 32, hipMemcpyHostToDevice, s->st));
+    HIP_TRY(c, hipMemcpyAsync(b.sz, sizes, (size_t)L * 4, hipMemcpyHostToDevice, s->st));
+    HIP_TRY(c, hipMemcpyAsync(d_ins, ins, L, hipMemcpyHostToDevice, s->st));
+    HIP_TRY(c, hipMemsetAsync(b.fl, 1, L, s->st));
+  }
+  HIP_TRY(c, txv_poollist_upload_index(b.k, d_ins, L, b.ix, b.icap, s->st));
+  s->h_clen[0] = L;                                    // (staging word)
+  HIP_TRY(c, hipMemcpyAsync(s->ltail + s->ltp, s->h_clen, 4, hipMemcpyHostToDevice, s->st));
+  HIP_TRY(c, hipStreamSynchronize(s->st));
+  dfree(d_ins);
+  s->tail_ub = L;
+  return TXV_OK;
+}
+
+// the device's pool list, in order: its live entries' keys, sizes and whether txsMap indexes
+// them (synchronous; c may be NULL)
+int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::vector<uint32_t>& sizes,
+                     std::vector<uint8_t>& ins) {
+  keys.clear(); sizes.clear(); ins.clear();
+  const PoolDev::ListBuf& b = s->lb[s->lcur];
+  if (!b.cap) return TXV_OK;
+  if (hipSetDevice(s->device) != hipSuccess) return TXV_EDEVICE;
+  s->quiesce();
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && c) c->err = std::string("pool list download: ") + hipGetErrorString(e);
+    return e == hipSuccess;
+  };
+  if (!ok(hipMemcpyAsync(s->h_clen, s->ltail + s->ltp, 4, hipMemcpyDeviceToHost, s->st)) || !ok(hipStreamSynchronize(s->st)))
+    return TXV_EDEVICE;
+  const uint32_t T = s->h_clen[0];
+  std::vector<uint8_t> k((size_t)T * 32), fl(T);
+  std::vector<uint32_t> sz(T);
+  std::vector<unsigned long long> ix(b.icap);
+  if ((T && (!ok(hipMemcpyAsync(k.data(), b.k, (size_t)T * 32, hipMemcpyDeviceToHost, s->st)) ||
+             !ok(hipMemcpyAsync(sz.data(), b.sz, (size_t)T * 4, hipMemcpyDeviceToHost, s->st)) ||
+             !ok(hipMemcpyAsync(fl.data(), b.fl, T, hipMemcpyDeviceToHost, s->st)))) ||
+      !ok(hipMemcpyAsync(ix.data(), b.ix, (size_t)b.icap * 8, hipMemcpyDeviceToHost, s->st)) ||
+      !ok(hipStreamSynchronize(s->st)))
+    return TXV_EDEVICE;
+  std::vector<uint8_t> indexed(T, 0);
+  for (unsigned long long v : ix)
+    if (v && (uint32_t)v != kListTomb && (uint32_t)v - 1 < T) indexed[(uint32_t)v - 1] = 1;
+  for (uint32_t e = 0; e < T; ++e) {
+    if (!fl[e]) continue;
+    keys.insert(keys.end(), k.begin() + (size_t)e * 32, k.begin() + (size_t)e * 32 + 32);
+    sizes.push_back(sz[e]);
+    ins.push_back(indexed[e]);
+  }
+  return TXV_OK;
+}
+
+// the list kernels' (entries appended / removed, their bytes) of slot's finished batch
+void pooldev_result(const PoolDev* s, int slot, int64_t* count, int64_t* bytes) {
+  *count = (int64_t)s->fl[slot].h_res[0];
+  *bytes = (int64_t)s->fl[slot].h_res[1];
+}
+
 // one batch's decisions enqueued on the engine's stream into flight slot `slot` (whose previous
 // batch the caller has finished), either from a txv_votes batch (v: signatures uploaded -- from
 // caller memory registered with txv_host_register, which must stay valid until the finish -- and
@@ -3306,7 +3477,8 @@ int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys) {
 // keys, come back into the slot's pinned buffers (pooldev_finish).
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
-                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev) {
+                    uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
+                    int list_op, uint64_t live_ub) {
   hipEvent_t after = (hipEvent_t)after_ev;
   HIP_TRY(c, hipSetDevice(c->device));
   if (!n) return TXV_OK;
@@ -3358,12 +3530,29 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status;
   a.tiles = s->tiles; a.tk = s->tk;
   if (((++s->epoch) & 0x3FFFFFFFu) == 0) {          // the tag wrapped: no word may match by accident
-    HIP_TRY(c, hipMemsetAsync(s->tiles, 0, (2 * (((size_t)s->cap_n + 1023) / 1024) + ((size_t)std::max<uint32_t>(s->C, 1) + 1023) / 1024) * 8, ks));
+    HIP_TRY(c, hipMemsetAsync(s->tiles, 0, pooldev_tile_words(s->cap_n, s->C) * 8, ks));
     ++s->epoch;
   }
   a.epoch = s->epoch;
+  if (list_op) {
+    int r;
+    if ((r = list_ready(c, s))) return r;
+    if (list_op == 1 && s->tail_ub + n > s->lb[s->lcur].cap && (r = list_compact(c, s, ks, live_ub, n))) return r;
+    a.okpos = list_op == 1 ? s->okpos : nullptr;
+    a.res = f.d_res;
+  }
   HIP_TRY(c, txv_pooldev_run(&a, ks));
   if (s->C) s->cur ^= 1;                                  // the next batch on this stream reads the new cache
+  if (list_op) {                                          // the pool list's appends / removals
+    const PoolDev::ListBuf& b = s->lb[s->lcur];
+    PoolListArgs l{};
+    l.n = n; l.keys = d_keys; l.sizes = d_sizes; l.status = f.d_status; l.okpos = s->okpos;
+    l.lk = b.k; l.lsz = b.sz; l.lfl = b.fl; l.li = b.ix; l.imask = b.icap - 1;
+    l.tail_in = s->ltail + s->ltp; l.tail_out = s->ltail + (s->ltp ^ 1); l.res = f.d_res;
+    HIP_TRY(c, txv_poollist_run(&l, list_op, ks));
+    if (list_op == 1) { s->ltp ^= 1; s->tail_ub += n; }
+    HIP_TRY(c, hipMemcpyAsync(f.h_res, f.d_res, 16, hipMemcpyDeviceToHost, ks));
+  }
   HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status, n, hipMemcpyDeviceToHost, ks));
   if (keys_back && d_keys == f.d_keys && v)
     HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
@@ -3387,12 +3576,13 @@ int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, con
 // enqueue + finish in one call (synchronous): statuses into status_out, keys (v path) into keys_out
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev) {
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev, int list_op,
+                  uint64_t live_ub) {
   if (!n) return TXV_OK;
   HostTimer ht(c->profile_host);
   const int slot = 0;
   int r = pooldev_enqueue(c, s, slot, v, h_keys_in, h_sizes, d_keys, d_sizes, d_valid, valid_ok, n, max_tx, wal,
-                          keys_out != nullptr, after_ev);
+                          keys_out != nullptr, after_ev, list_op, live_ub);
   if (r) return r;
   ht.mark("enqueue");
   const uint8_t* st;

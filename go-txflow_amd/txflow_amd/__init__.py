@@ -141,6 +141,7 @@ def lib():
             "txv_pool_check_wait": ([vp, ctypes.c_uint64, vp], ctypes.c_int),
             "txv_pool_check_keys": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_pool_update": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
+            "txv_pool_update_keys": ([vp, vp, i64, vp, vp, u32], ctypes.c_int),
             "txv_pool_update_submit": ([vp, vp, i64, ctypes.POINTER(_Votes), vp, vp], ctypes.c_int),
             "txv_pool_reap": ([vp, i64, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_pool_flush": ([vp], ctypes.c_int),
@@ -198,7 +199,7 @@ EXPORTED_SYMBOLS = [
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_validator_tables_built", "txv_staged_bytes", "txv_base_window", "txv_sig_keys",
     "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
-    "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_reap", "txv_pool_flush",
+    "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_update_keys", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
     "txv_pool_check_submit", "txv_pool_check_wait", "txv_pool_update_submit",
     "txv_decode_msgs", "txv_decode_stage", "txv_decode_run", "txv_decode_fetch", "txv_pool_receive", "txv_encode_msgs",
@@ -1049,6 +1050,16 @@ class TxVotePool:
         vs = batch.c_struct()
         ctx = self._ctx_or_raise("update")
         ctx._chk(lib().txv_pool_update(self._h, ctx._h, height, ctypes.byref(vs), full, off), "txv_pool_update")
+
+    def update_keys(self, height: int, keys: np.ndarray, sizes: np.ndarray):
+        """Update over (txVoteKey [n, 32] u8, TxVote.Size() [n] u32) pairs (txv_pool_update_keys);
+        needs no GPU when the pool was made with ctx=None"""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        sizes = np.ascontiguousarray(sizes, np.uint32)
+        rc = lib().txv_pool_update_keys(self._h, self.ctx._h if self.ctx is not None else None, height,
+                                        keys.ctypes.data, sizes.ctypes.data, len(sizes))
+        if rc != 0:
+            raise TxvInfraError(f"txv_pool_update_keys failed ({rc})")
 
     def update_submit(self, height: int, batch: VoteBatch, long_sigs: Optional[dict] = None):
         """txv_pool_update_submit: Update enqueued behind the submitted CheckTx batches (device

@@ -425,9 +425,15 @@ int txv_pool_prepare(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const
 /* Update(height, committed): every committed vote's key is pushed to the cache, and the vote
  * leaves the pool if its key is there (txvotepool.go:329-359); applied when it returns.  With
  * TXV_POOL_DEVICE_CACHE the keys are pushed by the device engine behind the batches submitted
- * before and the removals run on the pool's appender thread; no cache copy comes back. */
+ * before, and the committed votes leave the pool list held in HBM there too; nothing is copied back
+ * but the removal counts. */
 int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,
                     const uint8_t* sig_full, const uint64_t* sig_full_off);
+/* Update with the committed votes given as (txVoteKey, TxVote.Size()) pairs, as
+ * txv_pool_check_keys takes them; applied when it returns, on the host (a pool list or cache held
+ * in HBM comes back first).  ctx (optional) lends its host workers.  txvotepool.go:329-359 */
+int txv_pool_update_keys(txv_pool* pool, txv_ctx* ctx, int64_t height, const uint8_t* keys32, const uint32_t* sizes,
+                         uint32_t n);
 /* txv_pool_update without the wait (the commit path of a node that keeps checking batches):
  * with TXV_POOL_DEVICE_CACHE it returns once the pushes are enqueued; its effects are applied in
  * submission order with the txv_pool_check_submit batches, and are in place once those submitted

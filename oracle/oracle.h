@@ -139,6 +139,7 @@ void orc_pool_check_keys(orc_pool*, const uint8_t* keys32, const uint32_t* sizes
 void orc_pool_check_soa(orc_pool*, const orc_soa* b, const uint8_t* sig_full, const uint64_t* sig_full_off,
                         uint8_t* out);
 void orc_pool_update(orc_pool*, int64_t height, const orc_vote* votes, uint32_t n);
+void orc_pool_update_keys(orc_pool*, int64_t height, const uint8_t* keys32, const uint32_t* sizes, uint32_t n);
 void orc_pool_update_soa(orc_pool*, int64_t height, const orc_soa* b, const uint8_t* sig_full,
                          const uint64_t* sig_full_off);
 uint64_t orc_pool_reap(orc_pool*, int64_t max, uint8_t* keys_out, uint32_t* sizes_out, uint64_t cap);

@@ -62,6 +62,8 @@ def lib():
         L.orc_pool_check_soa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]
         L.orc_pool_update.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_pool_update_keys.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint32]
         L.orc_pool_update_soa.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]
         L.orc_pool_reap.restype = ctypes.c_uint64
@@ -362,6 +364,13 @@ class Pool:
         keep = []
         arr = (_Vote * max(len(votes), 1))(*[_orc_vote(v, keep) for v in votes])
         lib().orc_pool_update(self._h, height, ctypes.addressof(arr), len(votes))
+
+    def update_keys(self, height, keys, sizes):
+        """orc_pool_update over (txVoteKey, Size()) pairs: keys [n, 32] u8, sizes [n] u32"""
+        import numpy as np
+        keys = np.ascontiguousarray(keys, np.uint8)
+        sizes = np.ascontiguousarray(sizes, np.uint32)
+        lib().orc_pool_update_keys(self._h, height, keys.ctypes.data, sizes.ctypes.data, len(sizes))
 
     def update_batch(self, height, b):
         """orc_pool_update over a VoteBatch-shaped object (signatures of at most 64 bytes)"""

@@ -191,6 +191,20 @@ void orc_pool_update(orc_pool* p, int64_t height, const orc_vote* votes, uint32_
   }
 }
 
+/* orc_pool_update over (txVoteKey, Size()) pairs (txvotepool.go:329-359 with the keys given) */
+void orc_pool_update_keys(orc_pool* p, int64_t height, const uint8_t* keys32, const uint32_t* sizes, uint32_t n) {
+  p->height = height;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* k = keys32 + (size_t)i * 32;
+    (void)cache_push(p, k);
+    pnode* e = pl_find(&p->txs, k);
+    if (e) {
+      pl_remove(&p->txs, e);
+      p->txs_bytes -= sizes[i];
+    }
+  }
+}
+
 /* orc_pool_update over an SoA batch (the committed votes of a TxVoteSet, txflow/service.go:224-227) */
 void orc_pool_update_soa(orc_pool* p, int64_t height, const orc_soa* b, const uint8_t* sig_full,
                          const uint64_t* sig_full_off) {

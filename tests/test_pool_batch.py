@@ -133,3 +133,33 @@ def test_contextless_pool_methods_raise_clearly():
                 call()
     finally:
         pool.close()
+
+
+@pytest.mark.parametrize("cache", [10000, T.POOL_NO_CACHE], ids=["cache10k", "no_cache"])
+def test_pool_update_keys_matches_oracle(cache):
+    """Update (txvotepool.go:329-359) over (txVoteKey, Size()) pairs between CheckTx batches:
+    committed keys the pool holds (oldest first, random, twice in one Update), keys it never saw,
+    and -- without a cache -- keys admitted twice (the earlier element stays in the list,
+    unindexed, after the later one is removed).  Statuses, Size, TxsBytes, the LRU and the pool
+    order equal the oracle's after every call."""
+    O.build()
+    rng = np.random.default_rng(91)
+    pool = T.TxVotePool(None, size=1 << 20, cache_size=cache, max_txs_bytes=1 << 40)
+    opool = O.Pool(size=1 << 20, cache_size=cache, max_txs_bytes=1 << 40)
+    seen = []
+    try:
+        for b, (keys, sizes) in enumerate(_stream(rng, 5, 6000, replay=0.05)):
+            st = pool.check_keys(keys, sizes)
+            _check_equal(pool, opool, st, opool.check_keys(keys, sizes), f"check {b}")
+            seen.extend(list(keys))
+            held, _ = pool.reap(-1)
+            pick = [held[:1500], held[rng.permutation(len(held))[:1500]],
+                    rng.integers(0, 256, size=(200, 32), dtype=np.uint8), held[:50]]
+            ukeys = np.concatenate(pick)[rng.permutation(3250)]
+            usizes = rng.integers(100, 200, size=len(ukeys)).astype(np.uint32)
+            pool.update_keys(b + 1, ukeys, usizes)
+            opool.update_keys(b + 1, ukeys, usizes)
+            _check_equal(pool, opool, np.zeros(0, np.uint8), np.zeros(0, np.uint8), f"update {b}")
+        assert pool.Size() > 0
+    finally:
+        pool.close()

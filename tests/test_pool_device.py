@@ -269,9 +269,10 @@ def test_device_cache_slice_ffffffff_beside_non_pushes(big_ctx):
 def test_device_cache_update_submit_between_flights(dev_ctx):
     """The commit path on the device cache (VERDICT r4 missing 3): txv_pool_update_submit between
     txv_pool_check_submit batches that are still in flight -- the committed keys pushed by the
-    engine in submission order, the pool-list removals on the appender behind the earlier
-    batches' appends, nothing copied back -- against the oracle pool running the same calls in the
-    same order: every batch's statuses, then Size, TxsBytes, the pool order and the LRU order"""
+    engine in submission order and the committed votes removed from the pool list in HBM behind
+    the earlier batches' appends, nothing copied back -- against the oracle pool running the same
+    calls in the same order: every batch's statuses, then Size, TxsBytes, the pool order and the
+    LRU order"""
     import random
 
     import txflow_amd as T
@@ -322,5 +323,79 @@ def test_device_cache_update_submit_between_flights(dev_ctx):
         ref.update(20, committed)
         assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
         assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+    finally:
+        pool.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cache", [3000, 0xFFFFFFFF], ids=["cache3000", "no_cache"])
+def test_device_pool_list_compaction_and_round_trips(dev_ctx, cache):
+    """The pool list in HBM (pl_append / pl_remove / compaction): 36 submitted batches of 4000
+    votes with device Updates between them remove most votes but keep a tail of old ones alive, so
+    the list's positions run out and it is compacted (twice at least: 64k positions) with entries
+    still in flight; without a cache a vote admitted twice leaves its earlier element in the list,
+    unindexed.  Midway the list comes back to the host (reap), takes a host Update
+    (txv_pool_update_keys) and goes up again.  Every batch's statuses, then Size, TxsBytes, the
+    pool order and the LRU order equal the oracle's."""
+    import random
+
+    import txflow_amd as T
+    from test_pool import _batch, key, vote
+    rnd = random.Random(87 + (cache & 7))
+    cfg = dict(size=1 << 20, cache_size=cache)
+    pool = T.TxVotePool(dev_ctx, **cfg, device_cache=True)
+    ref = O.Pool(**cfg)
+    hist = []
+
+    def make(n):
+        votes = []
+        for _ in range(n):
+            if hist and rnd.random() < 0.05:
+                votes.append(dict(hist[max(0, len(hist) - 1 - rnd.randrange(6000))]))
+            else:
+                votes.append(vote(rnd.randbytes(64), ts=(1_700_000_000, 1 + len(hist))))
+            hist.append(votes[-1])
+        return votes
+
+    def settle(where):
+        pool.sync()
+        assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes(), where
+        gk, gs = pool.reap(-1)
+        ok, os_ = ref.reap(-1)
+        assert np.array_equal(gk, ok) and np.array_equal(gs, os_), where
+        if cache != 0xFFFFFFFF:
+            assert np.array_equal(pool.cache_keys(), ref.cache_keys()), where
+
+    try:
+        pending = []
+        for b in range(36):
+            votes = make(4000)
+            bt, ls = _batch(T, votes)
+            pending.append((pool.check_submit(bt, ls), ref.check(votes)))
+            if len(pending) == 3:
+                tk, exp = pending.pop(0)
+                assert np.array_equal(pool.check_wait(tk), exp), b
+            if b >= 1 and b % 6 != 5:       # every sixth batch's votes mostly stay behind
+                src = hist[-8000:-4000] if b % 6 else hist[-8000:]
+                committed = [v for i, v in enumerate(src) if i % 10]
+                cb, cl = _batch(T, committed)
+                pool.update_submit(b + 1, cb, cl)
+                ref.update(b + 1, committed)
+            if b == 17:
+                while pending:
+                    tk, exp = pending.pop(0)
+                    assert np.array_equal(pool.check_wait(tk), exp)
+                settle("midway")
+                some = rnd.sample(hist, 3000)
+                ks = np.array([np.frombuffer(key(v["sig"]), np.uint8) for v in some])
+                sz = np.full(len(some), 150, np.uint32)
+                pool.update_keys(19, ks, sz)
+                ref.update_keys(19, ks, sz)
+                settle("after the host Update")
+        while pending:
+            tk, exp = pending.pop(0)
+            assert np.array_equal(pool.check_wait(tk), exp)
+        settle("end")
+        assert 10000 < pool.Size() < 100000
     finally:
         pool.close()
