@@ -472,7 +472,7 @@ __device__ void sha256_bytes_dev(const uint8_t* p, uint32_t len, uint32_t st[8])
 
 // the vote that first carried a new TxHash: number its set (first-seen order), move the key
 // bytes into the set's key slot (or the overflow arena), record the set's TxKey
-// (service.go:201-207) and its exchange name SHA-256(TxHash)[0:16]
+// (service.go:201-207); its exchange name comes later, from the pack's digest pass
 struct NewSetAct {
   FlowState fs;
   FlowBatch b;
@@ -498,12 +498,6 @@ struct NewSetAct {
       ko = (uint64_t)fs.max_txs * TXV_KEY_SLOT + o;
     }
     const uint8_t* src = b.th + (e.key_off - 1);
-    {
-      uint32_t h[8];
-      sha256_bytes_dev(src, len, h);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fs.set_digest[(size_t)id * 4 + j] = __builtin_bswap32(h[j]);   // bytes in order
-    }
     uint64_t* dst = reinterpret_cast<uint64_t*>(fs.keys + ko);
     for (uint32_t k = 0; k < span; k += 8)
       dst[k / 8] = ld64u(src + k) & (k + 8 <= len ? ~0ull : ((1ull << (8 * (len - k))) - 1ull));
@@ -896,6 +890,7 @@ __global__ void __launch_bounds__(256) txv_k_init_cells(FlowState fs, uint64_t c
 __global__ void txv_k_reset_counters(FlowState fs, int keep_ids) {
   if (!keep_ids) {
     fs.ctr->n_sets = 0;
+    fs.ctr->n_digested = 0;
     fs.ctr->key_used = 0;
     fs.ctr->err = 0;
   } else {
@@ -973,10 +968,22 @@ __device__ __forceinline__ uint32_t commit_word(const FlowState& fs, uint32_t t,
   return w;
 }
 
+// the exchange names SHA-256(TxHash)[0:16] of the sets numbered since the last pack (only a
+// multi-rank step packs: the AddVote chain itself computes none)
+__global__ void __launch_bounds__(256) txv_k_digest(FlowState fs, uint32_t n_cap) {
+  const uint32_t id = fs.ctr->n_digested + blockIdx.x * 256 + threadIdx.x;
+  if (id >= min(fs.ctr->n_sets, n_cap)) return;
+  const SetEntry& e = fs.tab[fs.set_entry[id]];
+  uint32_t h[8];
+  sha256_bytes_dev(fs.keys + (e.key_off - 1), e.len, h);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fs.set_digest[(size_t)id * 4 + j] = __builtin_bswap32(h[j]);   // bytes in order
+}
+
 __global__ void __launch_bounds__(256) txv_k_pack(FlowState fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   const uint32_t ns = min(fs.ctr->n_sets, n_cap);
-  if (t == 0) { dst[0] = ns; dst[1] = 1; }   // word 1: layout 1 = with the per-set digests
+  if (t == 0) { dst[0] = ns; dst[1] = 1; fs.ctr->n_digested = ns; }   // word 1: layout 1 = with the per-set digests
   if (t < bm_words) dst[2 + t] = commit_word(fs, t, ns);
   if (t < n_cap) {
     const int64_t sm = t < ns ? fs.set_sum[t] : 0;
@@ -1146,6 +1153,7 @@ hipError_t txv_flow_keys(const FlowState* fs, const uint32_t* ids, uint32_t n, u
 
 hipError_t txv_flow_pack(const FlowState* fs, uint32_t* dst, uint32_t bm_words, uint32_t n_cap, hipStream_t st) {
   const uint32_t t = std::max<uint32_t>(std::max(bm_words, n_cap), 1);
+  hipLaunchKernelGGL(txv_k_digest, dim3((std::max<uint32_t>(n_cap, 1) + 255) / 256), dim3(256), 0, st, *fs, n_cap);
   hipLaunchKernelGGL(txv_k_pack, dim3((t + 255) / 256), dim3(256), 0, st, *fs, dst, bm_words, n_cap);
   return hipGetLastError();
 }

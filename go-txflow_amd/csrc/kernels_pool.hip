@@ -105,21 +105,27 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
 // it ranks its tile's flags (ballots), publishes the tile's aggregate, sums its predecessors'
 // published words back to the first inclusive prefix, and publishes its own.  The words carry the
 // batch's epoch: nothing is cleared between batches.
-constexpr uint32_t kTile = 1024;               // 256 threads x 4 rounds; item = tile * 1024 + 256 k + t
+constexpr uint32_t kTile = 1024;
+// the sort key: a 24-bit key slice (three radix passes; equal slices are told apart by the full
+// key inside their run), the non-pushes on the value above every push's
+constexpr uint32_t kSliceBits = 24, kSliceNone = (1u << kSliceBits) - 1;               // 256 threads x 4 rounds; item = tile * 1024 + 256 k + t
 __device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint32_t flag, uint32_t v) {
   return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | ((uint64_t)flag << 32) | v;
 }
-// exclusive prefix of tile `tile` (thread 0 of its block): flag 1 = aggregate, 2 = inclusive
+// exclusive prefix of tile `tile` (thread 0 of its block): flag 1 = aggregate, 2 = inclusive.
+// The value travels inside the 8-byte word, so relaxed agent-scope atomics on both sides carry
+// it across XCDs (sc1 stores and loads): no release / acquire fence, which would write back or
+// invalidate the whole XCD L2 per tile (MI355X_MICROARCH.md, inter-workgroup visibility)
 __device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, uint32_t agg) {
   if (tile == 0) {
-    __hip_atomic_store(st, tile_word(epoch, 2, agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(st, tile_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  __hip_atomic_store(st + tile, tile_word(epoch, 1, agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + tile, tile_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t prefix = 0;
   uint32_t spins = 0;
   for (int32_t j = (int32_t)tile - 1; j >= 0;) {
-    const uint64_t w = __hip_atomic_load(st + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t w = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t f = (uint32_t)(w >> 32) & 3u;
     if ((uint32_t)(w >> 34) != (epoch & 0x3FFFFFFFu) || f == 0) {
       // a predecessor's block is running (tickets are taken at block start): it publishes within
@@ -132,7 +138,7 @@ __device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, u
     if (f == 2) break;
     --j;
   }
-  __hip_atomic_store(st + tile, tile_word(epoch, 2, prefix + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + tile, tile_word(epoch, 2, prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return prefix;
 }
 // the next tile of chain `ch` for this block
@@ -173,16 +179,105 @@ __device__ __forceinline__ void tile_scan(const bool f[4], uint32_t out[4], uint
   for (int k = 0; k < 4; ++k) out[k] += s_prefix;
 }
 
+// ---- the pool list in HBM (pool_dev.h PoolListArgs) ----
+__device__ __forceinline__ uint32_t list_home(const uint32_t* k) { return k[4] ^ (k[7] * 0x9E3779B1u); }
+__device__ __forceinline__ unsigned long long list_slot(uint32_t tag, uint32_t low) {
+  return ((unsigned long long)tag << 32) | low;
+}
+__device__ __forceinline__ unsigned long long slot_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// entry e's key == k (entries are written by an earlier launch than any reader's)
+__device__ __forceinline__ bool list_key_eq(const uint32_t* lk, uint32_t e, const uint32_t k[8]) {
+  const uint4* x = reinterpret_cast<const uint4*>(lk + (size_t)e * 8);
+  const uint4 x0 = x[0], x1 = x[1];
+  return ((x0.x ^ k[0]) | (x0.y ^ k[1]) | (x0.z ^ k[2]) | (x0.w ^ k[3]) | (x1.x ^ k[4]) | (x1.y ^ k[5]) |
+          (x1.z ^ k[6]) | (x1.w ^ k[7])) == 0;
+}
+// txsMap.Store(key, pos): insert, or -- the key indexed already (a vote admitted twice, the
+// earlier one still in the list) -- the later position stays indexed, as the sequential Stores
+// leave it; the other entry stays in the list, unindexed
+__device__ void list_insert(unsigned long long* li, uint32_t imask, const uint32_t* lk, uint32_t pos, const uint32_t k[8]) {
+  const uint32_t tg = k[3];
+  const unsigned long long mine = list_slot(tg, pos + 1);
+  uint32_t s = list_home(k) & imask;
+  for (uint32_t probe = 0; probe <= imask; ++probe, s = (s + 1) & imask) {
+    unsigned long long v = slot_load(li + s);
+    if (v == 0) {
+      v = atomicCAS(li + s, 0ull, mine);
+      if (v == 0) return;
+    }
+    if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb || !list_key_eq(lk, (uint32_t)v - 1, k)) continue;
+    for (;;) {
+      if ((uint32_t)v - 1 > pos) return;
+      const unsigned long long prev = atomicCAS(li + s, v, mine);
+      if (prev == v) return;
+      v = prev;                 // another insert of this key took the slot meanwhile
+    }
+  }
+}
+// the tile's (entries, bytes) into out[0..1] (one plain store pair per tile, summed on the host:
+// no counter to zero before the launch, no atomic on a shared word)
+__device__ __forceinline__ void list_partial(uint64_t* out, uint32_t hits, uint64_t bytes) {
+  __shared__ uint64_t s_c[4], s_b[4];
+  uint64_t c = hits;
+  for (int o = 32; o > 0; o >>= 1) {
+    bytes += __shfl_xor(bytes, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { s_c[threadIdx.x >> 6] = c; s_b[threadIdx.x >> 6] = bytes; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    out[1] = s_b[0] + s_b[1] + s_b[2] + s_b[3];
+  }
+}
+
+// Update's removeTx(tx, e, false) (txvotepool.go:339-344) for committed key k if the index holds
+// it: the slot becomes a tombstone, the entry dead (a key twice in the batch: removed once)
+__device__ bool list_remove(const PoolListArgs& l, const uint32_t* key) {
+  const uint4* src = reinterpret_cast<const uint4*>(key);
+  const uint4 k0 = src[0], k1 = src[1];
+  const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  const uint32_t tg = k[3];
+  uint32_t s = list_home(k) & l.imask;
+  for (uint32_t probe = 0; probe <= l.imask; ++probe, s = (s + 1) & l.imask) {
+    const unsigned long long v = slot_load(l.li + s);
+    if (v == 0) return false;
+    if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb || !list_key_eq(l.lk, (uint32_t)v - 1, k)) continue;
+    if (atomicCAS(l.li + s, v, list_slot(tg, kListTomb)) != v) return false;   // a twin of this key removed it
+    l.lfl[(uint32_t)v - 1] = 0;
+    return true;
+  }
+  return false;
+}
+
 // pushes, sort input, and aidx = exclusive scan of the pushes (the push's index in S after the
-// cache); the ticket counters of pd_status's two scans are reset here
+// cache); the ticket counters of pd_status's two scans are reset here.  With the pool list in HBM
+// the tiles after the batch's remove Update's committed votes [0, n_force) from it
 __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
   const uint32_t tile = take_tile(a.tk + 0);
-  if (tile >= (a.n + kTile - 1) / kTile) return;   // (tickets reset by the previous batch: never)
+  const uint32_t nt = (a.n + kTile - 1) / kTile;
+  if (tile >= nt) {                                // (tickets reset by the previous batch: never)
+    const uint32_t rt = tile - nt;
+    if (!a.list_on || rt >= (a.n_force + kTile - 1) / kTile) return;
+    uint32_t hits = 0;
+    uint64_t bytes = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = rt * kTile + 256u * k + threadIdx.x;
+      if (i < a.n_force && list_remove(a.l, a.keys + (size_t)i * 8)) {
+        ++hits;
+        bytes += a.sizes[i];      // the committed vote's Size(), as the host path subtracts it
+      }
+    }
+    list_partial(a.res_rm + 2 * rt, hits, bytes);
+    return;
+  }
   if (tile == 0 && threadIdx.x == 0) {
     a.nfar[0] = 0;          // far pushes (appended by pd_link)
     a.tk[1] = 0;
     a.tk[2] = 0;
-    if (a.res) a.res[0] = a.res[1] = 0;
   }
   bool f[4];
 #pragma unroll
@@ -190,13 +285,14 @@ __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
     f[k] = false;
     if (i >= a.n) continue;
-    const bool ok = !a.valid || a.valid[i] == a.valid_ok;
-    const bool p = ok && (int64_t)a.sizes[i] <= a.max_tx;
+    const bool forced = i < a.n_force;             // Update's committed votes: every one pushes
+    const bool ok = forced || !a.valid || a.valid[i] == a.valid_ok;
+    const bool p = forced || (ok && (int64_t)a.sizes[i] <= a.max_tx);
     f[k] = p;
     a.push[i] = p;
     // non-pushes sort into a run of their own at the end: a push's slice is clamped below it, so a
     // key whose slice is 0xFFFFFFFF never shares a run with them (pd_link scans its run backwards)
-    a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2], 0xFFFFFFFEu) : 0xFFFFFFFFu;
+    a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2] >> 8, kSliceNone - 1) : kSliceNone;
     a.hidx[i] = i;
     a.last[i] = p;          // cleared by pd_link for a push with a later push of its key
   }
@@ -365,18 +461,38 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
     if (!old && i < a.n) a.lpos[i] = r[k];
     if (old && i < a.C) a.spos[i] = r[k];
   }
-  if (old || !a.okpos) return;   // (block-uniform) the pool list's appends: a third chain
+  if (old || !a.list_on) return;   // (block-uniform) the pool list's appends: a third chain
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
-    f[k] = i < a.n && a.status[i] == TXV_POOL_OK;   // written by this thread above
+    f[k] = i < a.n && i >= a.n_force && a.status[i] == TXV_POOL_OK;   // written by this thread above
   }
   tile_scan(f, r, a.tiles + 2 * (size_t)nt + (a.C + kTile - 1) / kTile, tile, a.epoch);
+  // addTx (txvotepool.go:265-270), in arrival order: txs.PushBack at tail + rank (txsMap.Store
+  // follows in pl_insert, a launch of its own: a duplicate's key compare reads an entry another
+  // block wrote, which only a launch boundary makes visible across XCDs without a fence per vote)
+  const uint32_t tail = *a.l.tail_in;
+  uint32_t hits = 0;
+  uint64_t bytes = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
-    if (i < a.n) a.okpos[i] = r[k];
+    if (i >= a.n) continue;
+    a.okpos[i] = r[k];
+    if (f[k]) {
+      const uint32_t pos = tail + r[k];
+      const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
+      uint4* dst = reinterpret_cast<uint4*>(a.l.lk + (size_t)pos * 8);
+      dst[0] = src[0];
+      dst[1] = src[1];
+      a.l.lsz[pos] = a.sizes[i];
+      a.l.lfl[pos] = 1;
+      ++hits;
+      bytes += a.sizes[i];
+    }
+    if (i == a.n - 1) *a.l.tail_out = tail + r[k] + (f[k] ? 1u : 0u);
   }
+  list_partial(a.res + 2 * tile, hits, bytes);
 }
 
 // the new cache = the last keep_old surviving old entries in order, then the last keepU of the
@@ -439,115 +555,15 @@ __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_
   while (atomicCAS(&ci[s], 0u, q + 1u) != 0u) s = (s + 1) & (icap - 1);
 }
 
-// ---- the pool list in HBM (pool_dev.h PoolListArgs) ----
-__device__ __forceinline__ uint32_t list_home(const uint32_t* k) { return k[4] ^ (k[7] * 0x9E3779B1u); }
-__device__ __forceinline__ unsigned long long list_slot(uint32_t tag, uint32_t low) {
-  return ((unsigned long long)tag << 32) | low;
-}
-__device__ __forceinline__ unsigned long long slot_load(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// entry e's key == k, read at the coherence point (the entry may have been written by another CU
-// in this launch, before its index CAS)
-__device__ __forceinline__ bool list_key_eq(const uint32_t* lk, uint32_t e, const uint32_t k[8]) {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  uint32_t d = 0;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) d |= __hip_atomic_load(lk + (size_t)e * 8 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ k[w];
-  return d == 0;
-}
-// txsMap.Store(key, pos): insert, or -- the key indexed already (a vote admitted twice, the
-// earlier one still in the list) -- the later position stays indexed, as the sequential Stores
-// leave it; the other entry stays in the list, unindexed
-__device__ void list_insert(unsigned long long* li, uint32_t imask, const uint32_t* lk, uint32_t pos, const uint32_t k[8]) {
-  const uint32_t tg = k[3];
-  const unsigned long long mine = list_slot(tg, pos + 1);
-  uint32_t s = list_home(k) & imask;
-  for (uint32_t probe = 0; probe <= imask; ++probe, s = (s + 1) & imask) {
-    unsigned long long v = slot_load(li + s);
-    if (v == 0) {
-      v = atomicCAS(li + s, 0ull, mine);
-      if (v == 0) return;
-    }
-    if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb || !list_key_eq(lk, (uint32_t)v - 1, k)) continue;
-    for (;;) {
-      if ((uint32_t)v - 1 > pos) return;
-      const unsigned long long prev = atomicCAS(li + s, v, mine);
-      if (prev == v) return;
-      v = prev;                 // another insert of this key took the slot meanwhile
-    }
-  }
-}
-__device__ __forceinline__ void list_account(uint64_t* res, bool hit, uint64_t bytes) {
-  const uint64_t m = __ballot(hit);
-  for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o, 64);
-  if ((threadIdx.x & 63) == 0 && m) {
-    atomicAdd((unsigned long long*)res, (unsigned long long)__popcll(m));
-    atomicAdd((unsigned long long*)res + 1, (unsigned long long)bytes);
-  }
-}
-
-// addTx (txvotepool.go:265-270) for the batch's admitted votes in arrival order: txs.PushBack at
-// tail + rank, txsMap.Store
-__global__ void __launch_bounds__(256) pl_append(PoolListArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t tail = *a.tail_in;
-  bool ok = false;
-  uint64_t sz = 0;
-  if (i < a.n) {
-    ok = a.status[i] == TXV_POOL_OK;
-    if (ok) {
-      const uint32_t pos = tail + a.okpos[i];
-      const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
-      const uint4 k0 = src[0], k1 = src[1];
-      uint4* dst = reinterpret_cast<uint4*>(a.lk + (size_t)pos * 8);
-      dst[0] = k0;
-      dst[1] = k1;
-      sz = a.sizes[i];
-      a.lsz[pos] = (uint32_t)sz;
-      a.lfl[pos] = 1;
-      __threadfence();          // the entry before its index slot
-      const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-      list_insert(a.li, a.imask, a.lk, pos, k);
-    }
-    if (i == a.n - 1) *a.tail_out = tail + a.okpos[i] + (ok ? 1u : 0u);
-  }
-  list_account(a.res, ok, sz);
-}
-
-// Update's removeTx(tx, e, false) (txvotepool.go:339-344) for every committed key the index
-// holds: the slot becomes a tombstone, the entry dead (a key twice in the batch: removed once);
-// the bytes are the committed vote's Size(), as the host path subtracts them
-__global__ void __launch_bounds__(256) pl_remove(PoolListArgs a) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  bool hit = false;
-  uint64_t sz = 0;
-  if (i < a.n) {
-    uint32_t k[8];
-    const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
-    const uint4 k0 = src[0], k1 = src[1];
-    k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w; k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
-    const uint32_t tg = k[3];
-    uint32_t s = list_home(k) & a.imask;
-    for (uint32_t probe = 0; probe <= a.imask; ++probe, s = (s + 1) & a.imask) {
-      const unsigned long long v = slot_load(a.li + s);
-      if (v == 0) break;
-      if ((uint32_t)(v >> 32) != tg || (uint32_t)v == kListTomb) continue;
-      const uint32_t e = (uint32_t)v - 1;
-      const uint4* ek = reinterpret_cast<const uint4*>(a.lk + (size_t)e * 8);
-      const uint4 e0 = ek[0], e1 = ek[1];
-      if (((e0.x ^ k0.x) | (e0.y ^ k0.y) | (e0.z ^ k0.z) | (e0.w ^ k0.w) | (e1.x ^ k1.x) | (e1.y ^ k1.y) |
-           (e1.z ^ k1.z) | (e1.w ^ k1.w)) != 0)
-        continue;
-      if (atomicCAS(a.li + s, v, list_slot(tg, kListTomb)) == v) {
-        a.lfl[e] = 0;
-        hit = true;
-        sz = a.sizes[i];
-      }
-      break;
-    }
-  }
-  list_account(a.res, hit, sz);
+// txsMap.Store for the batch's appended votes (their entries written by pd_status)
+__global__ void __launch_bounds__(256) pl_insert(PoolDevArgs a) {
+  const uint32_t i = a.n_force + blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n || a.status[i] != TXV_POOL_OK) return;
+  const uint32_t pos = *a.l.tail_in + a.okpos[i];
+  const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
+  const uint4 k0 = src[0], k1 = src[1];
+  const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  list_insert(a.l.li, a.l.imask, a.l.lk, pos, k);
 }
 
 // compaction (the list's positions ran out): the live entries, in order, into the other buffer
@@ -618,8 +634,10 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   hipError_t e;
   size_t tb = a.tmp_bytes;
   const uint32_t nt = (n + kTile - 1) / kTile, ntc = (a.C + kTile - 1) / kTile;
-  hipLaunchKernelGGL(pd_init, dim3(nt), b, 0, st, a);
-  if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, 32, st))) return e;
+  const uint32_t nrt = a.list_on ? (a.n_force + kTile - 1) / kTile : 0u;   // pd_init's removal tiles
+  hipLaunchKernelGGL(pd_init, dim3(nt + nrt), b, 0, st, a);
+  if ((e = hipcub::DeviceRadixSort::SortPairs(a.tmp, tb, a.hkey, a.skey, a.hidx, a.sidx, (int)n, 0, kSliceBits, st)))
+    return e;
   hipLaunchKernelGGL(pd_link, gn, b, 0, st, a);
   // an Update batch (every vote pushes: max_tx = INT64_MAX) needs the new cache, not statuses:
   // its far pushes' decisions are skipped
@@ -629,6 +647,8 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   }
   const uint32_t span = std::max(n, a.C);
   hipLaunchKernelGGL(pd_status, dim3(nt + ntc), b, 0, st, a);
+  if (a.list_on && n > a.n_force)
+    hipLaunchKernelGGL(pl_insert, dim3((n - a.n_force + 255) / 256), b, 0, st, a);
   if (!a.C) {
     hipLaunchKernelGGL(pd_tk_reset, dim3(1), dim3(1), 0, st, a);
     return hipGetLastError();
@@ -643,16 +663,6 @@ extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t
   hipError_t e;
   if ((e = hipMemsetAsync(ci, 0, (size_t)icap * 4, st))) return e;
   if (L) hipLaunchKernelGGL(pd_index_only, dim3((L + 255) / 256), dim3(256), 0, st, ck, L, ci, icap);
-  return hipGetLastError();
-}
-
-// the pool list's batch kernels (pool_dev.h PoolListArgs): op 1 append, 2 remove
-extern "C" hipError_t txv_poollist_run(const PoolListArgs* ap, int op, hipStream_t st) {
-  const PoolListArgs& a = *ap;
-  if (!a.n) return hipSuccess;
-  const dim3 g((a.n + 255) / 256), b(256);
-  if (op == 1) hipLaunchKernelGGL(pl_append, g, b, 0, st, a);
-  else hipLaunchKernelGGL(pl_remove, g, b, 0, st, a);
   return hipGetLastError();
 }
 

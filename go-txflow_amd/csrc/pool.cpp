@@ -279,18 +279,18 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L);
 int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after, int list_op,
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after, bool list_on,
                   uint64_t live_ub);
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
-                    int list_op, uint64_t live_ub);
+                    bool list_on, uint64_t live_ub, uint32_t n_upd);
+int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_votes* v, const uint32_t* h_sizes);
 int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
 int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t* sizes, const uint8_t* ins, uint32_t L);
 int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::vector<uint32_t>& sizes,
                      std::vector<uint8_t>& ins);
-void pooldev_result(const PoolDev* s, int slot, int64_t* count, int64_t* bytes);
-constexpr int kListAppend = 1, kListRemove = 2;   // pooldev_enqueue's list_op
+void pooldev_result(const PoolDev* s, int slot, int64_t res[4]);
 constexpr int kPdRing = 4;   // = PoolDev::kPdRing (runtime.cpp)
 
 struct txv_pool {
@@ -342,11 +342,18 @@ struct txv_pool {
     uint64_t pushes = 0, bytes = 0;
     std::vector<uint8_t> st;
     int err = 0;
-    // an Update batch (txv_pool_update_submit): its keys pushed and its votes removed from the
-    // pool list by the engine in submission order; no caller waits for it
+    // an Update batch (txv_pool_update_submit) run alone: its keys pushed and its votes removed
+    // from the pool list by the engine in submission order; no caller waits for it.  (Usually an
+    // Update rides with the next CheckTx batch instead: n_upd entries staged ahead of its votes.)
     bool upd = false;
+    uint32_t n_upd = 0;
   };
   std::deque<Ticket> tickets;
+  // Update entries staged (keyed on the engine's stream) in flight slot pend_slot, decided with the
+  // next device CheckTx batch, which takes that slot, or alone by flush_pending
+  int pend_slot = -1;
+  uint32_t pend_n = 0;
+  txv_ctx* pend_ctx = nullptr;
   uint64_t next_ticket = 1;
   int next_slot = 0;
   int64_t infl_len = 0, infl_bytes = 0;
@@ -1262,12 +1269,12 @@ bool dev_caps_ok(txv_pool* p, uint64_t pushes, uint64_t bytes) {
 // an upper bound of the pool list's live entries before the next device batch (its own excluded)
 uint64_t live_ub(const txv_pool* p) { return (uint64_t)p->txs.len + (uint64_t)std::max<int64_t>(0, p->infl_len); }
 
-// a device batch's list counts in (appended: + ; removed: -)
-void list_counts(txv_pool* p, int slot, bool removed) {
-  int64_t cnt, by;
-  pooldev_result(p->dev, slot, &cnt, &by);
-  if (removed) { p->txs.len -= (size_t)cnt; p->txs_bytes -= by; }
-  else { p->txs.len += (size_t)cnt; p->txs_bytes += by; }
+// a device batch's list counts in: its Update entries' removals, its votes' appends
+void list_counts(txv_pool* p, int slot) {
+  int64_t res[4];
+  pooldev_result(p->dev, slot, res);
+  p->txs.len = (size_t)((int64_t)p->txs.len + res[0] - res[2]);
+  p->txs_bytes += res[1] - res[3];
   publish(p);
 }
 
@@ -1281,14 +1288,41 @@ int finish_ticket(txv_pool* p, txv_pool::Ticket& t) {
   p->infl_bytes -= (int64_t)t.bytes;
   if ((t.err = pooldev_finish(t.ctx, p->dev, t.slot, &st, nullptr, nullptr))) return t.err;
   if (!t.upd) t.st.assign(st, st + t.n);
-  list_counts(p, t.slot, t.upd);
+  list_counts(p, t.slot);
+  return TXV_OK;
+}
+
+// the slot's previous batch, finished
+int finish_slot(txv_pool* p, int slot) {
+  for (auto& o : p->tickets)
+    if (!o.done && o.slot == slot)
+      if (int r = finish_ticket(p, o)) return r;
+  return TXV_OK;
+}
+
+// staged Update entries with no CheckTx batch to ride: decided alone in their slot
+int flush_pending(txv_pool* p) {
+  if (!p->pend_n) return TXV_OK;
+  txv_pool::Ticket t;
+  t.upd = true;
+  t.ctx = p->pend_ctx;
+  t.slot = p->pend_slot;
+  t.n_upd = p->pend_n;
+  p->pend_n = 0;
+  p->pend_slot = -1;
+  if (int r = pooldev_enqueue(t.ctx, p->dev, t.slot, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, INT64_MAX,
+                              false, false, nullptr, true, live_ub(p), t.n_upd))
+    return r;
+  if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+  p->next_slot = (t.slot + 1) % kPdRing;
+  p->tickets.push_back(std::move(t));
   return TXV_OK;
 }
 
 // every submitted device batch finished (statuses kept for their waits): the device and host
 // copies can be synchronised, the pool list read
 int drain_flights(txv_pool* p) {
-  int r = TXV_OK;
+  int r = flush_pending(p);
   for (auto& t : p->tickets)
     if (!t.done) { const int e = finish_ticket(p, t); if (e && !r) r = e; }
   prune_updates(p);
@@ -1317,10 +1351,10 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
   if ((r = cache_to_dev(p, ctx, n))) return r;
   if ((r = list_to_dev(p, ctx))) return r;
   if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
-                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after, kListAppend, live_ub(p))))
+                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after, true, live_ub(p))))
     return r;
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-  list_counts(p, 0, false);
+  list_counts(p, 0);
   *done = true;
   return TXV_OK;
 }
@@ -1350,11 +1384,10 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
       if ((r = cache_to_dev(p, ctx, n))) return r;
       if ((r = list_to_dev(p, ctx))) return r;
       if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr, kListAppend,
-                             live_ub(p))))
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr, true, live_ub(p))))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      list_counts(p, 0, false);
+      list_counts(p, 0);
       return TXV_OK;
     }
   }
@@ -1402,15 +1435,20 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
     pt.mark("sizes");
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
-      const int slot = p->next_slot;
-      for (auto& o : p->tickets)                           // the slot's previous batch, finished
-        if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
-      pt.mark("prev");
-      if ((r = cache_to_dev(p, ctx, v->n))) return r;
+      if (p->pend_n && p->pend_ctx != ctx && (r = flush_pending(p))) return r;
+      // (a rebind drains: staged Update entries are decided alone first)
+      if ((r = cache_to_dev(p, ctx, p->pend_n + v->n))) return r;
       if ((r = list_to_dev(p, ctx))) return r;
+      const int slot = p->next_slot;                       // the staged Update entries' slot, if any
+      const uint32_t n_upd = p->pend_n;
+      if (!n_upd && (r = finish_slot(p, slot))) return r;  // its previous batch (staging finished it)
+      pt.mark("prev");
+      p->pend_n = 0;
+      p->pend_slot = -1;
       if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
-                               (p->cfg.flags & TXV_POOL_WAL) != 0, false, nullptr, kListAppend, live_ub(p))))
+                               (p->cfg.flags & TXV_POOL_WAL) != 0, false, nullptr, true, live_ub(p), n_upd)))
         return r;
+      t.n_upd = n_upd;
       pt.mark("enqueue");
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
       p->next_slot = (slot + 1) % kPdRing;
@@ -1511,31 +1549,26 @@ int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_
 int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   const uint32_t n = v->n;
   PTimer pt("update_submit");
-  txv_pool::Ticket t;
-  t.upd = true;
-  t.ctx = ctx;
-  t.n = n;
   p->sizes.resize(n);
   pool_parallel_for(p, ctx, n, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
   }, 4096);
   pt.mark("sizes");
   int r;
-  const int slot = p->next_slot;
-  for (auto& o : p->tickets)                               // the slot's previous batch, finished
-    if (!o.done && o.slot == slot && (r = finish_ticket(p, o))) return r;
-  prune_updates(p);
-  pt.mark("prev");
-  if ((r = cache_to_dev(p, ctx, n))) return r;
-  if ((r = list_to_dev(p, ctx))) return r;
-  if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, n, INT64_MAX,
-                           false, false, nullptr, kListRemove, live_ub(p))))
+  if (p->pend_n && (p->pend_ctx != ctx || (p->dev && p->pend_n + n > pooldev_cap(p->dev))) && (r = flush_pending(p)))
     return r;
-  pt.mark("enqueue");
-  if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-  p->next_slot = (slot + 1) % kPdRing;
-  t.slot = slot;
-  p->tickets.push_back(std::move(t));
+  if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;   // (a rebind drains: pend_n is 0 then)
+  if ((r = list_to_dev(p, ctx))) return r;
+  if (!p->pend_n) {                                        // a slot for the entries: its previous batch finished
+    if ((r = finish_slot(p, p->next_slot))) return r;
+    prune_updates(p);
+    p->pend_slot = p->next_slot;
+    p->pend_ctx = ctx;
+  }
+  pt.mark("prev");
+  if ((r = pooldev_stage(ctx, p->dev, p->pend_slot, p->pend_n, v, p->sizes.data()))) return r;
+  p->pend_n += n;
+  pt.mark("stage");
   return TXV_OK;
 }
 
@@ -1728,7 +1761,7 @@ int txv_pool_sync(txv_pool* p) {
   int r;
   {
     std::lock_guard<std::mutex> g(p->mu);
-    if (std::any_of(p->tickets.begin(), p->tickets.end(), [](const txv_pool::Ticket& t) { return t.upd; }))
+    if (p->pend_n || std::any_of(p->tickets.begin(), p->tickets.end(), [](const txv_pool::Ticket& t) { return t.upd || t.n_upd; }))
       if ((r = drain_flights(p))) return r;               // submitted Updates applied
   }
   return TXV_OK;

@@ -10,6 +10,22 @@
 #pragma once
 #include <stdint.h>
 
+// The pool list (txs + txsMap, txvotepool.go:265-270 / :339-344) in HBM: entries in insertion
+// order at positions [0, tail) -- key [8] words, TxVote.Size(), alive flag -- and an
+// open-addressing index over them (u64 slots: tag << 32 | position + 1; 0 empty, low word
+// kListTomb a removed entry).  A list position is never reused before a compaction, so the list
+// order is the reference's clist order: appends at the tail, removals leave a dead entry behind.
+constexpr uint32_t kListTomb = 0xFFFFFFFFu;
+struct PoolListArgs {
+  uint32_t* lk;               // [cap][8] entry keys
+  uint32_t* lsz;              // [cap] entry Size()
+  uint8_t* lfl;               // [cap] 1 = alive
+  unsigned long long* li;     // [icap] index slots
+  uint32_t imask;             // icap - 1
+  const uint32_t* tail_in;    // the tail before the batch
+  uint32_t* tail_out;         // the tail after it (the other word of the pair)
+};
+
 struct PoolDevArgs {
   uint32_t n;                 // votes in the batch (arrival order)
   const uint32_t* keys;       // [n][8] key words (SHA-256(Signature) bytes in memory order)
@@ -29,7 +45,7 @@ struct PoolDevArgs {
   // scratch (n entries unless noted)
   uint32_t* push;             // 1 = reaches cache.Push
   uint32_t* aidx;             // exclusive scan of push: the push's index in S after the L0 cache entries
-  uint32_t* hkey;             // sort keys (a 32-bit slice of the key; non-pushes 0xFFFFFFFF)
+  uint32_t* hkey;             // sort keys (a 24-bit slice of the key; non-pushes 0xFFFFFF)
   uint32_t* hidx;             // 0..n-1
   uint32_t* skey;             // sorted
   uint32_t* sidx;
@@ -45,34 +61,21 @@ struct PoolDevArgs {
   uint8_t* detached;          // [C] cached keys pushed again in this batch (cleared at the end)
   uint32_t* surv;             // [C] old entries not pushed again
   uint32_t* spos;             // [C] exclusive scan of surv
-  uint64_t* tiles;            // look-back words: [ceil(n/1024)] push, [ceil(n/1024)] last, [ceil(C/1024)] surv
+  uint64_t* tiles;            // look-back words: [ceil(n/1024)] push, [ceil(n/1024)] last, [ceil(C/1024)] surv,
+                              // [ceil(n/1024)] appends
   uint32_t* tk;               // [4] tile tickets (pd_init, pd_status n-chain, pd_status C-chain)
   uint32_t epoch;             // this batch's tag for the look-back words (30 bits)
-  uint32_t* okpos;            // [n] or null: exclusive scan of status == OK (the pool list's appends)
-  uint64_t* res;              // [2] or null: zeroed by pd_init (the list kernels' count, bytes)
+  uint32_t* okpos;            // [n] exclusive scan of the appended votes (list_on)
+  uint64_t* res;              // (list_on) per 1024-vote tile (appended entries, their Size() sum)
+  uint64_t* res_rm;           // (list_on) per 1024-vote tile of [0, n_force): (removed entries, bytes)
+  // Update's committed votes fused into the batch: entries [0, n_force) push unconditionally, get
+  // no status, and leave the pool list before the batch's own votes (entries [n_force, n)) are
+  // appended (the reference's order: Update, then the CheckTx calls after it)
+  uint32_t n_force;
+  uint32_t list_on;           // the pool list is held in HBM: removals, appends (l)
+  PoolListArgs l;
   void* tmp;                  // hipcub temporary storage
   size_t tmp_bytes;
   uint8_t* status;            // [n] out: TXV_POOL_* per vote
 };
 
-// The pool list (txs + txsMap, txvotepool.go:265-270 / :339-344) in HBM: entries in insertion
-// order at positions [0, tail) -- key [8] words, TxVote.Size(), alive flag -- and an
-// open-addressing index over them (u64 slots: tag << 32 | position + 1; 0 empty, low word
-// kListTomb a removed entry).  A list position is never reused before a compaction, so the list
-// order is the reference's clist order: appends at the tail, removals leave a dead entry behind.
-constexpr uint32_t kListTomb = 0xFFFFFFFFu;
-struct PoolListArgs {
-  uint32_t n;                 // votes of the batch (append: checked votes; remove: committed votes)
-  const uint32_t* keys;       // [n][8]
-  const uint32_t* sizes;      // [n] TxVote.Size()
-  const uint8_t* status;      // append: [n] TXV_POOL_* (OK = appended)
-  const uint32_t* okpos;      // append: [n] exclusive scan of status == OK
-  uint32_t* lk;               // [cap][8] entry keys
-  uint32_t* lsz;              // [cap] entry Size()
-  uint8_t* lfl;               // [cap] 1 = alive
-  unsigned long long* li;     // [icap] index slots
-  uint32_t imask;             // icap - 1
-  const uint32_t* tail_in;    // the tail before the batch
-  uint32_t* tail_out;         // append: the tail after it (the other word of the pair)
-  uint64_t* res;              // [2] += entries appended / removed, their Size() sum
-};

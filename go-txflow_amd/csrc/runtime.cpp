@@ -3125,7 +3125,6 @@ int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_
 extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C);
 extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* a, hipStream_t st);
 extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st);
-extern "C" hipError_t txv_poollist_run(const PoolListArgs* a, int op, hipStream_t st);
 extern "C" size_t txv_poollist_tmp_bytes(uint32_t cap);
 extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* lsz, const uint8_t* lfl,
                                            const unsigned long long* li, uint32_t ocap, uint32_t oicap, uint32_t* nk,
@@ -3175,7 +3174,8 @@ struct PoolDev {
     uint8_t* d_status = nullptr;
     uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr;
     uint8_t* h_status = nullptr;
-    uint64_t *d_res = nullptr, *h_res = nullptr;   // the list kernels' (entries, bytes)
+    uint64_t *d_res = nullptr, *h_res = nullptr;   // per tile (entries, bytes): [2 ntm] appended, [2 ntm] removed
+    uint32_t nt_app = 0, nt_rm = 0;                // tiles of the batch in flight with partials there
     hipEvent_t ev = nullptr;
   } fl[kPdRing];
   uint32_t* h_clen = nullptr;
@@ -3211,6 +3211,9 @@ struct PoolDev {
 void pooldev_free(PoolDev* s) { delete s; }
 bool pooldev_same_device(const txv_ctx* c, const PoolDev* s) { return c && s && c->device == s->device; }
 uint32_t pooldev_cap(const PoolDev* s) { return s ? s->cap_n : 0; }
+
+// the list partials of a flight: (entries, bytes) per 1024-vote tile, appended then removed
+size_t res_words(uint32_t m) { return 4 * (((size_t)m + 1023) / 1024); }
 
 // look-back words: per 1024 votes the push, last and list-append chains, per 1024 cache entries
 // the survivors' chain
@@ -3277,7 +3280,7 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
       if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
           (r = dalloc(c, &f.d_sizes, m)) || (r = dalloc(c, &f.d_status, m)) || (r = halloc(c, &f.h_sig, (size_t)m * 16)) ||
           (r = halloc(c, &f.h_len, m)) || (r = halloc(c, &f.h_keys, (size_t)m * 8)) || (r = halloc(c, &f.h_sizes, m)) ||
-          (r = halloc(c, &f.h_status, m)) || (r = dalloc(c, &f.d_res, 2)) || (r = halloc(c, &f.h_res, 2)))
+          (r = halloc(c, &f.h_status, m)) || (r = dalloc(c, &f.d_res, res_words(m))) || (r = halloc(c, &f.h_res, res_words(m))))
         return r;
     s->cap_n = m;
     const size_t tb = txv_pooldev_tmp_bytes(m, std::max<uint32_t>(C, 1));
@@ -3462,66 +3465,103 @@ int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::ve
   return TXV_OK;
 }
 
-// the list kernels' (entries appended / removed, their bytes) of slot's finished batch
-void pooldev_result(const PoolDev* s, int slot, int64_t* count, int64_t* bytes) {
-  *count = (int64_t)s->fl[slot].h_res[0];
-  *bytes = (int64_t)s->fl[slot].h_res[1];
+// slot's finished batch: (entries appended, their bytes, entries removed, their bytes)
+void pooldev_result(const PoolDev* s, int slot, int64_t res[4]) {
+  const PoolDev::Flight& f = s->fl[slot];
+  const size_t half = res_words(s->cap_n) / 2;
+  uint64_t ac = 0, ab = 0, rc = 0, rb = 0;
+  for (uint32_t t = 0; t < f.nt_app; ++t) { ac += f.h_res[2 * t]; ab += f.h_res[2 * t + 1]; }
+  for (uint32_t t = 0; t < f.nt_rm; ++t) { rc += f.h_res[half + 2 * t]; rb += f.h_res[half + 2 * t + 1]; }
+  res[0] = (int64_t)ac; res[1] = (int64_t)ab; res[2] = (int64_t)rc; res[3] = (int64_t)rb;
+}
+
+// n votes of a txv_votes batch into flight f's entries [off, off + n): signatures uploaded -- from
+// caller memory registered with txv_host_register (which must stay valid until the finish) or
+// through the slot's pinned staging -- and keyed on stream ks, h_sizes = their TxVote.Size()
+int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes* v, uint32_t off, uint32_t n,
+                 const uint32_t* h_sizes) {
+  bool reg;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
+  }
+  if (!reg)
+    c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      memcpy(f.h_sig + (size_t)(off + lo) * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+      memcpy(f.h_len + off + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
+    }, 4096);
+  memcpy(f.h_sizes + off, h_sizes, (size_t)n * 4);
+  HIP_TRY(c, hipMemcpyAsync(f.d_sig + (size_t)off * 16, reg ? (const void*)v->sig : (const void*)(f.h_sig + (size_t)off * 16),
+                            (size_t)n * 64, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(f.d_len + off, reg ? (const void*)v->sig_len : (const void*)(f.h_len + off), (size_t)n * 4,
+                            hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, hipMemcpyAsync(f.d_sizes + off, f.h_sizes + off, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+  HIP_TRY(c, txv_launch_sig_keys(f.d_sig + (size_t)off * 16, f.d_len + off, n, f.d_keys + (size_t)off * 8, ks));
+  return TXV_OK;
+}
+
+// Update's committed votes staged into flight slot `slot` (finished by the caller) at entries
+// [off, off + n): keyed on the engine's stream now, decided with the slot's next enqueue -- the
+// CheckTx batch after them, their pushes and removals first (n_upd), or alone
+int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_votes* v, const uint32_t* h_sizes) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!v->n) return TXV_OK;
+  if ((uint64_t)off + v->n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
+  return upload_votes(c, s->fl[slot], s->on_key ? c->key_stream : s->st, v, off, v->n, h_sizes);
 }
 
 // one batch's decisions enqueued on the engine's stream into flight slot `slot` (whose previous
-// batch the caller has finished), either from a txv_votes batch (v: signatures uploaded -- from
-// caller memory registered with txv_host_register, which must stay valid until the finish -- and
-// keyed here; h_sizes = their TxVote.Size()), from keys / sizes given on the host (h_keys_in), or
-// from keys / sizes / validity already in HBM (d_keys, d_sizes, d_valid == valid_ok for a decoded
-// message; `after` = the event that ends their producer).  The statuses, and with keys_back the
-// keys, come back into the slot's pinned buffers (pooldev_finish).
+// batch the caller has finished), either from a txv_votes batch (v, keyed here; h_sizes = their
+// TxVote.Size()), from keys / sizes given on the host (h_keys_in), or from keys / sizes / validity
+// already in HBM (d_keys, d_sizes, d_valid == valid_ok for a decoded message; `after` = the event
+// that ends their producer).  n_upd Update entries staged in the slot (pooldev_stage) go first:
+// pushed, removed from the pool list, no statuses.  With list_on the batch's admitted votes are
+// appended to the pool list in HBM (live_ub: a bound of its live entries, for a compaction).  The
+// statuses, and with keys_back the keys, come back into the slot's pinned buffers (pooldev_finish).
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
-                    int list_op, uint64_t live_ub) {
+                    bool list_on, uint64_t live_ub, uint32_t n_upd) {
   hipEvent_t after = (hipEvent_t)after_ev;
   HIP_TRY(c, hipSetDevice(c->device));
-  if (!n) return TXV_OK;
-  if (n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
-  if (2 * ((uint64_t)s->C + n) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
+  const uint32_t total = n_upd + n;
+  if (!total) return TXV_OK;
+  if (total > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
+  if (2 * ((uint64_t)s->C + total) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
+  if (n_upd && n && !v && !h_keys_in) { c->err = "staged Update entries beside device-resident keys"; return TXV_EINVAL; }
   PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = s->on_key ? c->key_stream : s->st;
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
   if (v) {
-    bool reg;
-    {
-      std::lock_guard<std::mutex> lk(c->mu);
-      reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
+    if (n) {
+      int r;
+      if ((r = upload_votes(c, f, ks, v, n_upd, n, h_sizes))) return r;
     }
-    if (!reg)
-      c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-        memcpy(f.h_sig + (size_t)lo * 16, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
-        memcpy(f.h_len + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
-      }, 4096);
-    memcpy(f.h_sizes, h_sizes, (size_t)n * 4);
-    HIP_TRY(c, hipMemcpyAsync(f.d_sig, reg ? (const void*)v->sig : (const void*)f.h_sig, (size_t)n * 64,
-                              hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(f.d_len, reg ? (const void*)v->sig_len : (const void*)f.h_len, (size_t)n * 4,
-                              hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(f.d_sizes, f.h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n, f.d_keys, ks));
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (h_keys_in) {   // keys and sizes given on the host (txv_pool_check_keys)
     c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-      memcpy(f.h_keys + (size_t)lo * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
-      memcpy(f.h_sizes + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
+      memcpy(f.h_keys + (size_t)(n_upd + lo) * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
+      memcpy(f.h_sizes + n_upd + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
     }, 8192);
-    HIP_TRY(c, hipMemcpyAsync(f.d_keys, f.h_keys, (size_t)n * 32, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(f.d_sizes, f.h_sizes, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    if (n) {
+      HIP_TRY(c, hipMemcpyAsync(f.d_keys + (size_t)n_upd * 8, f.h_keys + (size_t)n_upd * 8, (size_t)n * 32,
+                                hipMemcpyHostToDevice, ks));
+      HIP_TRY(c, hipMemcpyAsync(f.d_sizes + n_upd, f.h_sizes + n_upd, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    }
+    d_keys = f.d_keys;
+    d_sizes = f.d_sizes;
+    d_valid = nullptr;
+  } else if (n_upd) {       // staged Update entries alone
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   }
   PoolDevArgs a{};
-  a.n = n; a.keys = d_keys; a.sizes = d_sizes; a.valid = d_valid; a.valid_ok = valid_ok;
-  a.max_tx = max_tx; a.C = s->C; a.wal = wal ? 1u : 0u;
+  a.n = total; a.n_force = n_upd; a.keys = d_keys; a.sizes = d_sizes; a.valid = d_valid; a.valid_ok = valid_ok;
+  a.max_tx = n ? max_tx : INT64_MAX;                     // Update alone: no statuses, no far decisions
+  a.C = s->C; a.wal = wal ? 1u : 0u;
   a.ck_old = s->ck[s->cur]; a.ck_new = s->ck[s->cur ^ 1]; a.ci_old = s->ci[s->cur]; a.ci_new = s->ci[s->cur ^ 1];
   a.icap = s->icap; a.clen = s->clen;
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
@@ -3534,28 +3574,31 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     ++s->epoch;
   }
   a.epoch = s->epoch;
-  if (list_op) {
+  f.nt_app = f.nt_rm = 0;
+  if (list_on) {
     int r;
     if ((r = list_ready(c, s))) return r;
-    if (list_op == 1 && s->tail_ub + n > s->lb[s->lcur].cap && (r = list_compact(c, s, ks, live_ub, n))) return r;
-    a.okpos = list_op == 1 ? s->okpos : nullptr;
+    if (s->tail_ub + n > s->lb[s->lcur].cap && (r = list_compact(c, s, ks, live_ub, n))) return r;
+    const PoolDev::ListBuf& b = s->lb[s->lcur];
+    a.list_on = 1;
+    a.okpos = s->okpos;
     a.res = f.d_res;
+    a.res_rm = f.d_res + res_words(s->cap_n) / 2;
+    a.l.lk = b.k; a.l.lsz = b.sz; a.l.lfl = b.fl; a.l.li = b.ix; a.l.imask = b.icap - 1;
+    a.l.tail_in = s->ltail + s->ltp; a.l.tail_out = s->ltail + (s->ltp ^ 1);
+    f.nt_app = (total + 1023) / 1024;
+    f.nt_rm = (n_upd + 1023) / 1024;
   }
   HIP_TRY(c, txv_pooldev_run(&a, ks));
   if (s->C) s->cur ^= 1;                                  // the next batch on this stream reads the new cache
-  if (list_op) {                                          // the pool list's appends / removals
-    const PoolDev::ListBuf& b = s->lb[s->lcur];
-    PoolListArgs l{};
-    l.n = n; l.keys = d_keys; l.sizes = d_sizes; l.status = f.d_status; l.okpos = s->okpos;
-    l.lk = b.k; l.lsz = b.sz; l.lfl = b.fl; l.li = b.ix; l.imask = b.icap - 1;
-    l.tail_in = s->ltail + s->ltp; l.tail_out = s->ltail + (s->ltp ^ 1); l.res = f.d_res;
-    HIP_TRY(c, txv_poollist_run(&l, list_op, ks));
-    if (list_op == 1) { s->ltp ^= 1; s->tail_ub += n; }
-    HIP_TRY(c, hipMemcpyAsync(f.h_res, f.d_res, 16, hipMemcpyDeviceToHost, ks));
+  if (list_on) {                                          // pd_status wrote the tail's other word
+    s->ltp ^= 1;
+    s->tail_ub += n;
+    HIP_TRY(c, hipMemcpyAsync(f.h_res, f.d_res, res_words(s->cap_n) * 8, hipMemcpyDeviceToHost, ks));
   }
-  HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status, n, hipMemcpyDeviceToHost, ks));
-  if (keys_back && d_keys == f.d_keys && v)
-    HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
+  if (n) HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status + n_upd, n, hipMemcpyDeviceToHost, ks));
+  if (keys_back && d_keys == f.d_keys && v && n)
+    HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys + (size_t)n_upd * 8, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
   HIP_TRY(c, hipEventRecord(f.ev, ks));
   return TXV_OK;
 }
@@ -3576,13 +3619,13 @@ int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, con
 // enqueue + finish in one call (synchronous): statuses into status_out, keys (v path) into keys_out
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
-                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev, int list_op,
+                  int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev, bool list_on,
                   uint64_t live_ub) {
   if (!n) return TXV_OK;
   HostTimer ht(c->profile_host);
   const int slot = 0;
   int r = pooldev_enqueue(c, s, slot, v, h_keys_in, h_sizes, d_keys, d_sizes, d_valid, valid_ok, n, max_tx, wal,
-                          keys_out != nullptr, after_ev, list_op, live_ub);
+                          keys_out != nullptr, after_ev, list_on, live_ub, 0);
   if (r) return r;
   ht.mark("enqueue");
   const uint8_t* st;

@@ -100,6 +100,8 @@ struct FlowCounters {           // device-resident, updated by the kernels
   uint32_t arena_used;          // accepted-vote rows in use
   uint32_t err;                 // TXV_FERR_*
   uint32_t n_stamped;           // sets the running batch ADDED a vote to (zeroed by tally_min)
+  uint32_t n_digested;          // sets [0, n_digested) have set_digest (computed by the pack's digest pass)
+  uint32_t pad_;
   uint64_t key_used;            // overflow key arena bytes in use
 };
 
