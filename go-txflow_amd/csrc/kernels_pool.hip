@@ -256,6 +256,9 @@ __device__ bool list_remove(const PoolListArgs& l, const uint32_t* key) {
 // cache); the ticket counters of pd_status's two scans are reset here.  With the pool list in HBM
 // the tiles after the batch's remove Update's committed votes [0, n_force) from it
 __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
+  // the new cache's index, cleared for pd_newcache (this chain reads only the old one)
+  if (a.C)
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.icap; s += gridDim.x * 256) a.ci_new[s] = 0;
   const uint32_t tile = take_tile(a.tk + 0);
   const uint32_t nt = (a.n + kTile - 1) / kTile;
   if (tile >= nt) {                                // (tickets reset by the previous batch: never)
@@ -286,7 +289,7 @@ __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
     f[k] = false;
     if (i >= a.n) continue;
     const bool forced = i < a.n_force;             // Update's committed votes: every one pushes
-    const bool ok = forced || !a.valid || a.valid[i] == a.valid_ok;
+    const bool ok = forced || !a.valid || a.valid[i - a.n_force] == a.valid_ok;
     const bool p = forced || (ok && (int64_t)a.sizes[i] <= a.max_tx);
     f[k] = p;
     a.push[i] = p;
@@ -439,13 +442,14 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
     if (!old) {
       if (i >= a.n) continue;
       uint8_t st;
-      if (a.valid && a.valid[i] != a.valid_ok) st = TXV_POOL_NOT_CHECKED;
+      if (i >= a.n_force && a.valid && a.valid[i - a.n_force] != a.valid_ok) st = TXV_POOL_NOT_CHECKED;
       else {
         const uint8_t d = a.dec[i];
         st = d == 0 ? TXV_POOL_ERR_TOO_LARGE : d == 2 ? TXV_POOL_ERR_IN_CACHE
            : (!a.sizes[i] && a.wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
       }
       a.status[i] = st;
+      if (i >= a.n_force) a.status_out[i - a.n_force] = st;   // mapped host memory: no copy back
       f[k] = a.last[i] != 0;
     } else {
       if (i >= a.C) continue;
@@ -469,7 +473,7 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
   }
   tile_scan(f, r, a.tiles + 2 * (size_t)nt + (a.C + kTile - 1) / kTile, tile, a.epoch);
   // addTx (txvotepool.go:265-270), in arrival order: txs.PushBack at tail + rank (txsMap.Store
-  // follows in pl_insert, a launch of its own: a duplicate's key compare reads an entry another
+  // follows in pd_newcache, a launch of its own: a duplicate's key compare reads an entry another
   // block wrote, which only a launch boundary makes visible across XCDs without a fence per vote)
   const uint32_t tail = *a.l.tail_in;
   uint32_t hits = 0;
@@ -495,9 +499,30 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
   list_partial(a.res + 2 * tile, hits, bytes);
 }
 
+// txsMap.Store for appended vote i (its entry written by pd_status, an earlier launch)
+__device__ __forceinline__ void list_index_vote(const PoolDevArgs& a, uint32_t i) {
+  if (i < a.n_force || i >= a.n || a.status[i] != TXV_POOL_OK) return;
+  const uint32_t pos = *a.l.tail_in + a.okpos[i];
+  const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
+  const uint4 k0 = src[0], k1 = src[1];
+  const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  list_insert(a.l.li, a.l.imask, a.l.lk, pos, k);
+}
+
+__device__ __forceinline__ void cache_put(const PoolDevArgs& a, uint32_t q, const uint4* s) {
+  const uint4 x0 = s[0], x1 = s[1];
+  uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)q * 8);
+  d[0] = x0;
+  d[1] = x1;
+  uint32_t h = (x1.y ^ (x1.z * 0x9E3779B1u)) & (a.icap - 1);          // idx_hash: words 5, 6
+  while (atomicCAS(&a.ci_new[h], 0u, q + 1u) != 0u) h = (h + 1) & (a.icap - 1);
+}
+
 // the new cache = the last keep_old surviving old entries in order, then the last keepU of the
 // batch's U distinct pushed keys (each at its last push) in push order: the C most recent distinct
-// keys of S (batch_check step 4); the new index is cleared here and filled by pd_index
+// keys of S (batch_check step 4), each indexed as it is written (the index was cleared by
+// pd_init); the new length; detached[] cleared for the next batch; pd_init's ticket counter reset;
+// and, with the pool list in HBM, txsMap.Store for the batch's appended votes
 __global__ void __launch_bounds__(256) pd_newcache(PoolDevArgs a) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   const uint32_t U = a.n ? a.lpos[a.n - 1] + a.last[a.n - 1] : 0u;
@@ -506,46 +531,26 @@ __global__ void __launch_bounds__(256) pd_newcache(PoolDevArgs a) {
   const uint32_t keep_old = L1 < a.C - keepU ? L1 : a.C - keepU;
   if (t < a.C && a.surv[t]) {
     const int64_t q = (int64_t)a.spos[t] - (int64_t)(L1 - keep_old);
-    if (q >= 0) {
-      const uint4* s = reinterpret_cast<const uint4*>(a.ck_old + (size_t)t * 8);
-      uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)q * 8);
-      d[0] = s[0];
-      d[1] = s[1];
-    }
+    if (q >= 0) cache_put(a, (uint32_t)q, reinterpret_cast<const uint4*>(a.ck_old + (size_t)t * 8));
   }
   if (t < a.n && a.last[t]) {
     const int64_t u = (int64_t)a.lpos[t] - (int64_t)(U - keepU);
-    if (u >= 0) {
-      const uint4* s = reinterpret_cast<const uint4*>(a.keys + (size_t)t * 8);
-      uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)(keep_old + u) * 8);
-      d[0] = s[0];
-      d[1] = s[1];
-    }
+    if (u >= 0) cache_put(a, keep_old + (uint32_t)u, reinterpret_cast<const uint4*>(a.keys + (size_t)t * 8));
   }
-  for (uint32_t s = t; s < a.icap; s += gridDim.x * 256) a.ci_new[s] = 0;
+  if (t < a.C) a.detached[t] = 0;   // (read by pd_link / pd_status: earlier launches)
+  if (t == 0) {
+    a.clen[0] = keep_old + keepU;
+    a.tk[0] = 0;
+  }
+  if (a.list_on) list_index_vote(a, t);
 }
 
-// the new index over the new key array; the new length; detached[] cleared for the next batch
-__global__ void __launch_bounds__(256) pd_index(PoolDevArgs a) {
-  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t U = a.n ? a.lpos[a.n - 1] + a.last[a.n - 1] : 0u;
-  const uint32_t L1 = a.spos[a.C - 1] + a.surv[a.C - 1];
-  const uint32_t keepU = U < a.C ? U : a.C;
-  const uint32_t keep_old = L1 < a.C - keepU ? L1 : a.C - keepU;
-  const uint32_t L = keep_old + keepU;
-  if (q < a.C) a.detached[q] = 0;
-  if (q < L) {
-    uint32_t s = idx_hash(a.ck_new + (size_t)q * 8) & (a.icap - 1);
-    while (atomicCAS(&a.ci_new[s], 0u, q + 1u) != 0u) s = (s + 1) & (a.icap - 1);
-  }
-  if (q == 0) {
-    a.clen[0] = L;             // its readers (pd_link .. pd_status) ran in earlier launches
-    a.tk[0] = 0;               // pd_init's ticket counter, for the next batch
-  }
+// nopTxCache: the list's index stores and pd_init's ticket counter reset
+__global__ void __launch_bounds__(256) pd_finish_nocache(PoolDevArgs a) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t == 0) a.tk[0] = 0;
+  if (a.list_on) list_index_vote(a, t);
 }
-
-// nopTxCache: no pd_index to reset pd_init's ticket counter
-__global__ void pd_tk_reset(PoolDevArgs a) { a.tk[0] = 0; }
 
 // an index over keys [L][8] (a cache uploaded from the host)
 __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap) {
@@ -553,17 +558,6 @@ __global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_
   if (q >= L) return;
   uint32_t s = idx_hash(ck + (size_t)q * 8) & (icap - 1);
   while (atomicCAS(&ci[s], 0u, q + 1u) != 0u) s = (s + 1) & (icap - 1);
-}
-
-// txsMap.Store for the batch's appended votes (their entries written by pd_status)
-__global__ void __launch_bounds__(256) pl_insert(PoolDevArgs a) {
-  const uint32_t i = a.n_force + blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n || a.status[i] != TXV_POOL_OK) return;
-  const uint32_t pos = *a.l.tail_in + a.okpos[i];
-  const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
-  const uint4 k0 = src[0], k1 = src[1];
-  const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-  list_insert(a.l.li, a.l.imask, a.l.lk, pos, k);
 }
 
 // compaction (the list's positions ran out): the live entries, in order, into the other buffer
@@ -647,14 +641,8 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   }
   const uint32_t span = std::max(n, a.C);
   hipLaunchKernelGGL(pd_status, dim3(nt + ntc), b, 0, st, a);
-  if (a.list_on && n > a.n_force)
-    hipLaunchKernelGGL(pl_insert, dim3((n - a.n_force + 255) / 256), b, 0, st, a);
-  if (!a.C) {
-    hipLaunchKernelGGL(pd_tk_reset, dim3(1), dim3(1), 0, st, a);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(pd_newcache, dim3((span + 255) / 256), b, 0, st, a);
-  hipLaunchKernelGGL(pd_index, dim3((a.C + 255) / 256), b, 0, st, a);
+  if (!a.C) hipLaunchKernelGGL(pd_finish_nocache, gn, b, 0, st, a);
+  else hipLaunchKernelGGL(pd_newcache, dim3((span + 255) / 256), b, 0, st, a);
   return hipGetLastError();
 }
 

@@ -280,12 +280,13 @@ int pooldev_get_cache(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys);
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
                   int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after, bool list_on,
-                  uint64_t live_ub);
+                  uint64_t live_ub, int slot, uint32_t n_upd);
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
                     bool list_on, uint64_t live_ub, uint32_t n_upd);
 int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_votes* v, const uint32_t* h_sizes);
+void pooldev_list_hint(PoolDev* s, uint64_t entries);
 int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
 int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t* sizes, const uint8_t* ins, uint32_t L);
 int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::vector<uint32_t>& sizes,
@@ -990,7 +991,7 @@ int cache_to_host(txv_pool* p, txv_ctx* ctx);
 void host_cache_written(txv_pool* p);
 int list_to_host(txv_pool* p, txv_ctx* ctx);
 
-int drain_flights(txv_pool* p);
+int drain_flights(txv_pool* p, bool flush = true);
 void publish_locked(txv_pool* p);
 
 int pool_admit_body(txv_pool* p, txv_ctx* ctx, const Key* keys, uint32_t n, uint8_t* status_out);
@@ -1138,6 +1139,7 @@ int list_to_host(txv_pool* p, txv_ctx* ctx) {
 // the host's pool list into HBM before a device batch (p->dev bound)
 int list_to_dev(txv_pool* p, txv_ctx* ctx) {
   if (p->list_dev) return TXV_OK;
+  pooldev_list_hint(p->dev, p->cfg.size);
   const KeyList& T = p->txs;
   std::vector<Key> kl;
   std::vector<uint32_t> sz;
@@ -1321,12 +1323,28 @@ int flush_pending(txv_pool* p) {
 
 // every submitted device batch finished (statuses kept for their waits): the device and host
 // copies can be synchronised, the pool list read
-int drain_flights(txv_pool* p) {
-  int r = flush_pending(p);
+int drain_flights(txv_pool* p, bool flush) {
+  int r = flush ? flush_pending(p) : TXV_OK;
   for (auto& t : p->tickets)
     if (!t.done) { const int e = finish_ticket(p, t); if (e && !r) r = e; }
   prune_updates(p);
   return r;
+}
+
+// a synchronous device batch of n votes from ctx: every submitted batch finished, the engine bound
+// and current; the staged Update entries ride with it (their slot and count out) unless they came
+// from another context or would not fit (then decided alone first)
+int sync_batch_begin(txv_pool* p, txv_ctx* ctx, uint32_t n, int* slot, uint32_t* n_upd) {
+  int r;
+  if (p->pend_n && p->pend_ctx != ctx && (r = flush_pending(p))) return r;
+  if ((r = drain_flights(p, false))) return r;
+  if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;   // (a rebind flushes them)
+  if ((r = list_to_dev(p, ctx))) return r;
+  *slot = p->pend_n ? p->pend_slot : 0;                     // (every slot is free now)
+  *n_upd = p->pend_n;
+  p->pend_n = 0;
+  p->pend_slot = -1;
+  return TXV_OK;
 }
 
 }  // namespace
@@ -1346,15 +1364,14 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
   if (!dev_mode(p) || !n) return TXV_OK;
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
   if (!dev_caps_ok(p, n, bytes_bound)) return TXV_OK;
-  int r;
-  if ((r = drain_flights(p))) return r;
-  if ((r = cache_to_dev(p, ctx, n))) return r;
-  if ((r = list_to_dev(p, ctx))) return r;
+  int r, slot;
+  uint32_t n_upd;
+  if ((r = sync_batch_begin(p, ctx, n, &slot, &n_upd))) return r;
   if ((r = pooldev_check(ctx, p->dev, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
-                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after, true, live_ub(p))))
+                         (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, after, true, live_ub(p), slot, n_upd)))
     return r;
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-  list_counts(p, 0);
+  list_counts(p, slot);
   *done = true;
   return TXV_OK;
 }
@@ -1379,15 +1396,15 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
     uint64_t pushes = 0, bytes = 0;
     for (uint32_t i = 0; i < n; ++i) { pushes += (int64_t)sizes[i] <= max_tx; bytes += sizes[i]; }
     if (dev_caps_ok(p, pushes, bytes)) {
-      int r;
-      if ((r = drain_flights(p))) return r;
-      if ((r = cache_to_dev(p, ctx, n))) return r;
-      if ((r = list_to_dev(p, ctx))) return r;
+      int r, slot;
+      uint32_t n_upd;
+      if ((r = sync_batch_begin(p, ctx, n, &slot, &n_upd))) return r;
       if ((r = pooldev_check(ctx, p->dev, nullptr, keys32, sizes, nullptr, nullptr, nullptr, 0, n, max_tx,
-                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr, true, live_ub(p))))
+                             (p->cfg.flags & TXV_POOL_WAL) != 0, nullptr, status_out, nullptr, true, live_ub(p), slot,
+                             n_upd)))
         return r;
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
-      list_counts(p, 0);
+      list_counts(p, slot);
       return TXV_OK;
     }
   }

@@ -30,7 +30,8 @@ struct PoolDevArgs {
   uint32_t n;                 // votes in the batch (arrival order)
   const uint32_t* keys;       // [n][8] key words (SHA-256(Signature) bytes in memory order)
   const uint32_t* sizes;      // [n] TxVote.Size()
-  const uint8_t* valid;       // [n] or null: 0 = the message did not decode (no CheckTx, status NOT_CHECKED)
+  const uint8_t* valid;       // [n - n_force] or null: valid[i - n_force] != valid_ok = the message did not
+                              // decode (no CheckTx, status NOT_CHECKED)
   uint32_t valid_ok;          // the value of valid[] that means "decoded"
   int64_t max_tx;             // a vote is pushed to the cache iff Size() <= max_tx (MaxMsgBytes - 8)
   uint32_t C;                 // cache capacity (config.CacheSize); 0 = nopTxCache
@@ -66,8 +67,8 @@ struct PoolDevArgs {
   uint32_t* tk;               // [4] tile tickets (pd_init, pd_status n-chain, pd_status C-chain)
   uint32_t epoch;             // this batch's tag for the look-back words (30 bits)
   uint32_t* okpos;            // [n] exclusive scan of the appended votes (list_on)
-  uint64_t* res;              // (list_on) per 1024-vote tile (appended entries, their Size() sum)
-  uint64_t* res_rm;           // (list_on) per 1024-vote tile of [0, n_force): (removed entries, bytes)
+  uint64_t* res;              // (list_on) per 1024-vote tile (appended entries, their Size() sum), mapped
+  uint64_t* res_rm;           // (list_on) per 1024-vote tile of [0, n_force): (removed entries, bytes), mapped
   // Update's committed votes fused into the batch: entries [0, n_force) push unconditionally, get
   // no status, and leave the pool list before the batch's own votes (entries [n_force, n)) are
   // appended (the reference's order: Update, then the CheckTx calls after it)
@@ -77,5 +78,6 @@ struct PoolDevArgs {
   void* tmp;                  // hipcub temporary storage
   size_t tmp_bytes;
   uint8_t* status;            // [n] out: TXV_POOL_* per vote
+  uint8_t* status_out;        // [n - n_force] the batch's own statuses again, in mapped host memory
 };
 

@@ -754,7 +754,7 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
     while (ae > ca && !arena_end.compare_exchange_weak(ca, ae)) {}
     uint32_t cm = max_hl.load();
     while (mh > cm && !max_hl.compare_exchange_weak(cm, mh)) {}
-  }, 16384);
+  }, 4096);   // a 64k batch (C5) over 16 workers: this scan sits between CheckTx and the chain
   const uint32_t uniform = check_uniform ? ~varying.load() & ((1u << kU) - 1u) : 0u;
   const uint64_t ae = arena_end.load();
   if (ae >= (1ull << 32)) { c->err = "TxHash arena >= 4 GiB"; return TXV_EINVAL; }
@@ -2777,6 +2777,9 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
       c->err = "message " + std::to_string(i) + " outside the wire buffer";
       return TXV_EINVAL;
     }
+  // the pool's lock is taken before the context's everywhere (pool.cpp calls into the context with
+  // its own lock held): its MaxMsgBytes is read here, before c->mu
+  const uint32_t max_msg = p ? txv_pool_max_msg_bytes(p) : 0u;
   std::lock_guard<std::mutex> order(c->ing_dec_mu);
   HostTimer ht(c->profile_host);
   uint64_t t;
@@ -2841,7 +2844,7 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     HIP_TRY(c, hipMemcpyAsync(g.d_max, g.h_max, 4, hipMemcpyHostToDevice, ks));
     WireArgs a{};
     a.n = n;
-    a.max_msg_bytes = txv_pool_max_msg_bytes(p);
+    a.max_msg_bytes = max_msg;
     txvote_msg_disfix(&a.disamb, &a.prefix);
     a.wire = s.d_arena_th; a.off = g.d_off; a.len = g.d_len;
     a.rec = reinterpret_cast<uint32_t*>(g.d_rec);
@@ -3167,14 +3170,15 @@ struct PoolDev {
   void* ltmp = nullptr;
   size_t ltmp_bytes = 0;
   uint64_t tail_ub = 0;                    // host: an upper bound of the tail (the appends enqueued)
+  uint64_t list_hint = 0;                  // entries the list is expected to hold (the pool's Size cap, clamped)
   // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
   static constexpr int kPdRing = 4;
   struct Flight {
     uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
     uint8_t* d_status = nullptr;
     uint32_t *h_sig = nullptr, *h_len = nullptr, *h_keys = nullptr, *h_sizes = nullptr;
-    uint8_t* h_status = nullptr;
-    uint64_t *d_res = nullptr, *h_res = nullptr;   // per tile (entries, bytes): [2 ntm] appended, [2 ntm] removed
+    uint8_t *h_status = nullptr, *m_status = nullptr;   // mapped: pd_status writes the batch's statuses here
+    uint64_t *h_res = nullptr, *m_res = nullptr;        // mapped, per tile (entries, bytes): [2 ntm] appended, [2 ntm] removed
     uint32_t nt_app = 0, nt_rm = 0;                // tiles of the batch in flight with partials there
     hipEvent_t ev = nullptr;
   } fl[kPdRing];
@@ -3197,7 +3201,7 @@ struct PoolDev {
     dfree(ltail); dfree(lnpos);
     if (ltmp) (void)hipFree(ltmp);
     for (Flight& f : fl) {
-      dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status); dfree(f.d_res);
+      dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
       hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status); hfree(f.h_res);
       if (f.ev) (void)hipEventDestroy(f.ev);
     }
@@ -3250,11 +3254,13 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
     HIP_TRY(c, hipEventCreateWithFlags(&s->ev, hipEventDisableTiming));
     for (PoolDev::Flight& f : s->fl) HIP_TRY(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
-    // the engine's own stream, at the highest priority: a batch's short kernels go ahead of the
-    // TxFlow chains' work queued on the context's streams whenever a CU frees up
-    // TXV_POOL_STREAM (experiment): 0 own high-priority stream, 1 own normal-priority stream, 2 the
-    // batches on the context's key stream (no HSA queue of the engine's own)
-    static const int mode = getenv("TXV_POOL_STREAM") ? atoi(getenv("TXV_POOL_STREAM")) : 0;
+    // the batches run on the context's key stream: no HSA queue of the engine's own.  Measured on
+    // C5 with Update (profiles/r05/c5_ab): an own high-priority stream 49-66M votes/s, an own
+    // normal one 44-88M, the key stream 97-103M -- a fifth queue beside the context's four is
+    // time-sliced by the hardware scheduler, and every launch of the engine's chain waits for it.
+    // TXV_POOL_STREAM (experiment): 0 own high-priority stream, 1 own normal-priority stream,
+    // 2 (default) the key stream; the engine's own stream serves its synchronous uploads either way
+    static const int mode = getenv("TXV_POOL_STREAM") ? atoi(getenv("TXV_POOL_STREAM")) : 2;
     s->on_key = mode == 2;
     if (mode == 0) {
       int lo = 0, hi = 0;
@@ -3266,7 +3272,9 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
   }
   if (n > s->cap_n) {
     int r;
-    const uint32_t m = std::max<uint32_t>(n, 1024);
+    // geometric growth: an Update riding with a batch makes n vary, and every growth reallocates
+    // (hipFree synchronises the device)
+    const uint32_t m = std::max<uint32_t>(std::max<uint32_t>(n, 1024), s->cap_n ? 2 * s->cap_n : 0u);
     if ((r = dalloc(c, &s->push, m)) || (r = dalloc(c, &s->aidx, m)) || (r = dalloc(c, &s->hkey, m)) ||
         (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
         (r = dalloc(c, &s->last, m)) ||
@@ -3280,7 +3288,7 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
       if ((r = dalloc(c, &f.d_sig, (size_t)m * 16)) || (r = dalloc(c, &f.d_len, m)) || (r = dalloc(c, &f.d_keys, (size_t)m * 8)) ||
           (r = dalloc(c, &f.d_sizes, m)) || (r = dalloc(c, &f.d_status, m)) || (r = halloc(c, &f.h_sig, (size_t)m * 16)) ||
           (r = halloc(c, &f.h_len, m)) || (r = halloc(c, &f.h_keys, (size_t)m * 8)) || (r = halloc(c, &f.h_sizes, m)) ||
-          (r = halloc(c, &f.h_status, m)) || (r = dalloc(c, &f.d_res, res_words(m))) || (r = halloc(c, &f.h_res, res_words(m))))
+          (r = halloc_mapped(c, &f.h_status, &f.m_status, m)) || (r = halloc_mapped(c, &f.h_res, &f.m_res, res_words(m))))
         return r;
     s->cap_n = m;
     const size_t tb = txv_pooldev_tmp_bytes(m, std::max<uint32_t>(C, 1));
@@ -3355,12 +3363,20 @@ uint32_t list_cap_for(uint64_t need) {   // a power of two >= need, >= 64k
   return cap > (1u << 30) ? 0u : (uint32_t)cap;
 }
 
-// the current buffer exists (first use: empty, room for four batches)
+// the list's expected size (pool.cpp: the Size cap, clamped): both buffers are sized for it up front,
+// so the compactions of a running pipeline do not reallocate (hipFree synchronises the device)
+void pooldev_list_hint(PoolDev* s, uint64_t entries) { s->list_hint = std::min<uint64_t>(entries, 1u << 22); }
+uint32_t list_cap_initial(const PoolDev* s) { return list_cap_for(2 * (s->list_hint + 4 * (uint64_t)s->cap_n)); }
+
+// the current buffer exists (first use: empty, room for the hinted size and four batches; the
+// other buffer allocated alike)
 int list_ready(txv_ctx* c, PoolDev* s) {
   PoolDev::ListBuf& b = s->lb[s->lcur];
   if (b.cap) return TXV_OK;
   int r;
-  if ((r = list_buf_alloc(c, b, list_cap_for(4 * (uint64_t)s->cap_n)))) return r;
+  const uint32_t cap = list_cap_initial(s);
+  if ((r = list_buf_alloc(c, b, cap))) return r;
+  if (s->lb[s->lcur ^ 1].cap < cap && (r = list_buf_alloc(c, s->lb[s->lcur ^ 1], cap))) return r;
   HIP_TRY(c, hipMemset(b.fl, 0, b.cap));
   HIP_TRY(c, hipMemset(b.ix, 0, (size_t)b.icap * 8));
   HIP_TRY(c, hipMemset(s->ltail, 0, 8));
@@ -3406,10 +3422,11 @@ int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t
   HIP_TRY(c, hipSetDevice(s->device));
   s->quiesce();
   int r;
-  const uint32_t cap = list_cap_for(2 * ((uint64_t)L + 4 * (uint64_t)s->cap_n));
+  const uint32_t cap = std::max(list_cap_for(2 * ((uint64_t)L + 4 * (uint64_t)s->cap_n)), list_cap_initial(s));
   if (!cap) { c->err = "pool list above 2^30 entries"; return TXV_ECAPACITY; }
   PoolDev::ListBuf& b = s->lb[s->lcur];
   if (b.cap < cap && (r = list_buf_alloc(c, b, cap))) return r;
+  if (s->lb[s->lcur ^ 1].cap < cap && (r = list_buf_alloc(c, s->lb[s->lcur ^ 1], cap))) return r;
   uint8_t* d_ins = nullptr;
   if (L && (r = dalloc(c, &d_ins, L))) return r;
   HIP_TRY(c, hipMemsetAsync(b.fl, 0, b.cap, s->st));
@@ -3528,7 +3545,6 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (!total) return TXV_OK;
   if (total > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
   if (2 * ((uint64_t)s->C + total) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
-  if (n_upd && n && !v && !h_keys_in) { c->err = "staged Update entries beside device-resident keys"; return TXV_EINVAL; }
   PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = s->on_key ? c->key_stream : s->st;
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
@@ -3553,10 +3569,13 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
     d_valid = nullptr;
-  } else if (n_upd) {       // staged Update entries alone
+  } else if (n_upd) {       // staged Update entries, alone or before keys already in HBM (moved beside them)
+    if (n) {
+      HIP_TRY(c, hipMemcpyAsync(f.d_keys + (size_t)n_upd * 8, d_keys, (size_t)n * 32, hipMemcpyDeviceToDevice, ks));
+      HIP_TRY(c, hipMemcpyAsync(f.d_sizes + n_upd, d_sizes, (size_t)n * 4, hipMemcpyDeviceToDevice, ks));
+    }
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
-    d_valid = nullptr;
   }
   PoolDevArgs a{};
   a.n = total; a.n_force = n_upd; a.keys = d_keys; a.sizes = d_sizes; a.valid = d_valid; a.valid_ok = valid_ok;
@@ -3567,7 +3586,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
   a.pend = s->pend; a.xs = s->xs; a.xn = s->xn; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
-  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status;
+  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status; a.status_out = f.m_status;
   a.tiles = s->tiles; a.tk = s->tk;
   if (((++s->epoch) & 0x3FFFFFFFu) == 0) {          // the tag wrapped: no word may match by accident
     HIP_TRY(c, hipMemsetAsync(s->tiles, 0, pooldev_tile_words(s->cap_n, s->C) * 8, ks));
@@ -3582,8 +3601,8 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     const PoolDev::ListBuf& b = s->lb[s->lcur];
     a.list_on = 1;
     a.okpos = s->okpos;
-    a.res = f.d_res;
-    a.res_rm = f.d_res + res_words(s->cap_n) / 2;
+    a.res = f.m_res;
+    a.res_rm = f.m_res + res_words(s->cap_n) / 2;
     a.l.lk = b.k; a.l.lsz = b.sz; a.l.lfl = b.fl; a.l.li = b.ix; a.l.imask = b.icap - 1;
     a.l.tail_in = s->ltail + s->ltp; a.l.tail_out = s->ltail + (s->ltp ^ 1);
     f.nt_app = (total + 1023) / 1024;
@@ -3594,9 +3613,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (list_on) {                                          // pd_status wrote the tail's other word
     s->ltp ^= 1;
     s->tail_ub += n;
-    HIP_TRY(c, hipMemcpyAsync(f.h_res, f.d_res, res_words(s->cap_n) * 8, hipMemcpyDeviceToHost, ks));
   }
-  if (n) HIP_TRY(c, hipMemcpyAsync(f.h_status, f.d_status + n_upd, n, hipMemcpyDeviceToHost, ks));
   if (keys_back && d_keys == f.d_keys && v && n)
     HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys + (size_t)n_upd * 8, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
   HIP_TRY(c, hipEventRecord(f.ev, ks));
@@ -3620,12 +3637,11 @@ int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, con
 int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_keys_in, const uint32_t* h_sizes,
                   const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid, uint32_t valid_ok, uint32_t n,
                   int64_t max_tx, bool wal, uint8_t* keys_out, uint8_t* status_out, void* after_ev, bool list_on,
-                  uint64_t live_ub) {
+                  uint64_t live_ub, int slot, uint32_t n_upd) {
   if (!n) return TXV_OK;
   HostTimer ht(c->profile_host);
-  const int slot = 0;
   int r = pooldev_enqueue(c, s, slot, v, h_keys_in, h_sizes, d_keys, d_sizes, d_valid, valid_ok, n, max_tx, wal,
-                          keys_out != nullptr, after_ev, list_on, live_ub, 0);
+                          keys_out != nullptr, after_ev, list_on, live_ub, n_upd);
   if (r) return r;
   ht.mark("enqueue");
   const uint8_t* st;
