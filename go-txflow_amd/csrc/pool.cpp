@@ -1336,7 +1336,7 @@ int drain_flights(txv_pool* p, bool flush) {
 // from another context or would not fit (then decided alone first)
 int sync_batch_begin(txv_pool* p, txv_ctx* ctx, uint32_t n, int* slot, uint32_t* n_upd) {
   int r;
-  if (p->pend_n && p->pend_ctx != ctx && (r = flush_pending(p))) return r;
+  if (p->pend_n && (p->pend_ctx != ctx || p->pend_n + n > pooldev_cap(p->dev)) && (r = flush_pending(p))) return r;
   if ((r = drain_flights(p, false))) return r;
   if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;   // (a rebind flushes them)
   if ((r = list_to_dev(p, ctx))) return r;
@@ -1452,8 +1452,9 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
     pt.mark("sizes");
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
-      if (p->pend_n && p->pend_ctx != ctx && (r = flush_pending(p))) return r;
-      // (a rebind drains: staged Update entries are decided alone first)
+      // staged Update entries from another context, or too many to ride with this batch, are decided
+      // alone first (a rebind to a larger capacity would drain and reallocate mid-stream)
+      if (p->pend_n && (p->pend_ctx != ctx || p->pend_n + v->n > pooldev_cap(p->dev)) && (r = flush_pending(p))) return r;
       if ((r = cache_to_dev(p, ctx, p->pend_n + v->n))) return r;
       if ((r = list_to_dev(p, ctx))) return r;
       const int slot = p->next_slot;                       // the staged Update entries' slot, if any
