@@ -105,40 +105,54 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
 // it ranks its tile's flags (ballots), publishes the tile's aggregate, sums its predecessors'
 // published words back to the first inclusive prefix, and publishes its own.  The words carry the
 // batch's epoch: nothing is cleared between batches.
-constexpr uint32_t kTile = 1024;
+constexpr uint32_t kTile = 1024;               // 256 threads x 4 rounds; item = tile * 1024 + 256 k + t
 // the sort key: a 24-bit key slice (three radix passes; equal slices are told apart by the full
 // key inside their run), the non-pushes on the value above every push's
-constexpr uint32_t kSliceBits = 24, kSliceNone = (1u << kSliceBits) - 1;               // 256 threads x 4 rounds; item = tile * 1024 + 256 k + t
+constexpr uint32_t kSliceBits = 24, kSliceNone = (1u << kSliceBits) - 1;
 __device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint32_t flag, uint32_t v) {
   return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | ((uint64_t)flag << 32) | v;
 }
-// exclusive prefix of tile `tile` (thread 0 of its block): flag 1 = aggregate, 2 = inclusive.
-// The value travels inside the 8-byte word, so relaxed agent-scope atomics on both sides carry
-// it across XCDs (sc1 stores and loads): no release / acquire fence, which would write back or
-// invalidate the whole XCD L2 per tile (MI355X_MICROARCH.md, inter-workgroup visibility)
+// exclusive prefix of tile `tile` (wave 0 of its block, every lane; the result in every lane):
+// flag 1 = aggregate, 2 = inclusive.  The wave reads 64 predecessors' words at once and sums back
+// to the nearest inclusive one (a single lane walking them one by one made the last tiles of a
+// 128-tile chain wait ~100 dependent loads).  The value travels inside the 8-byte word, so relaxed
+// agent-scope atomics on both sides carry it across XCDs (sc1 stores and loads): no release /
+// acquire fence, which would write back or invalidate the whole XCD L2 per tile
+// (MI355X_MICROARCH.md, inter-workgroup visibility)
 __device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, uint32_t agg) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t ep = epoch & 0x3FFFFFFFu;
   if (tile == 0) {
-    __hip_atomic_store(st, tile_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(st, tile_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  __hip_atomic_store(st + tile, tile_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t prefix = 0;
-  uint32_t spins = 0;
+  if (lane == 0) __hip_atomic_store(st + tile, tile_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t prefix = 0, spins = 0;
   for (int32_t j = (int32_t)tile - 1; j >= 0;) {
-    const uint64_t w = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t idx = j - lane;
+    // before tile 0 nothing is counted: such lanes read as an inclusive 0
+    const uint64_t w = idx >= 0 ? __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : tile_word(epoch, 2, 0);
     const uint32_t f = (uint32_t)(w >> 32) & 3u;
-    if ((uint32_t)(w >> 34) != (epoch & 0x3FFFFFFFu) || f == 0) {
+    const bool ok = (uint32_t)(w >> 34) == ep && f != 0;
+    const uint64_t incm = __ballot(ok && f == 2), okm = __ballot(ok);
+    const int first = incm ? __builtin_ctzll(incm) : 64;          // the nearest inclusive word
+    const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+    if ((okm & need) != need) {
       // a predecessor's block is running (tickets are taken at block start): it publishes within
       // microseconds; the bound only keeps a broken invariant from hanging the queue
-      if (++spins > (1u << 24)) break;
+      if (++spins > (1u << 22)) break;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    prefix += (uint32_t)w;
-    if (f == 2) break;
-    --j;
+    uint32_t v = lane <= first ? (uint32_t)w : 0u;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    prefix += v;
+    if (first < 64) break;
+    j -= 64;
   }
-  __hip_atomic_store(st + tile, tile_word(epoch, 2, prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0)
+    __hip_atomic_store(st + tile, tile_word(epoch, 2, prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return prefix;
 }
 // the next tile of chain `ch` for this block
@@ -173,7 +187,10 @@ __device__ __forceinline__ void tile_scan(const bool f[4], uint32_t out[4], uint
     out[k] = run + before + (uint32_t)__popcll(m[k] & below);
     run += round;
   }
-  if (threadIdx.x == 0) s_prefix = tile_lookback(st, tile, epoch, run);
+  if (w == 0) {                                      // wave 0 looks back (run is block-uniform)
+    const uint32_t pre = tile_lookback(st, tile, epoch, run);
+    if (lane == 0) s_prefix = pre;
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) out[k] += s_prefix;

@@ -3496,7 +3496,7 @@ void pooldev_result(const PoolDev* s, int slot, int64_t res[4]) {
 // caller memory registered with txv_host_register (which must stay valid until the finish) or
 // through the slot's pinned staging -- and keyed on stream ks, h_sizes = their TxVote.Size()
 int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes* v, uint32_t off, uint32_t n,
-                 const uint32_t* h_sizes) {
+                 const uint32_t* h_sizes, bool key) {
   bool reg;
   {
     std::lock_guard<std::mutex> lk(c->mu);
@@ -3513,18 +3513,19 @@ int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes
   HIP_TRY(c, hipMemcpyAsync(f.d_len + off, reg ? (const void*)v->sig_len : (const void*)(f.h_len + off), (size_t)n * 4,
                             hipMemcpyHostToDevice, ks));
   HIP_TRY(c, hipMemcpyAsync(f.d_sizes + off, f.h_sizes + off, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, txv_launch_sig_keys(f.d_sig + (size_t)off * 16, f.d_len + off, n, f.d_keys + (size_t)off * 8, ks));
+  if (key) HIP_TRY(c, txv_launch_sig_keys(f.d_sig + (size_t)off * 16, f.d_len + off, n, f.d_keys + (size_t)off * 8, ks));
   return TXV_OK;
 }
 
 // Update's committed votes staged into flight slot `slot` (finished by the caller) at entries
-// [off, off + n): keyed on the engine's stream now, decided with the slot's next enqueue -- the
-// CheckTx batch after them, their pushes and removals first (n_upd), or alone
+// [off, off + n): uploaded now on the engine's stream, keyed and decided with the slot's next
+// enqueue -- the CheckTx batch after them (one SHA-256 launch over both), their pushes and
+// removals first (n_upd), or alone
 int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_votes* v, const uint32_t* h_sizes) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (!v->n) return TXV_OK;
   if ((uint64_t)off + v->n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
-  return upload_votes(c, s->fl[slot], s->on_key ? c->key_stream : s->st, v, off, v->n, h_sizes);
+  return upload_votes(c, s->fl[slot], s->on_key ? c->key_stream : s->st, v, off, v->n, h_sizes, false);
 }
 
 // one batch's decisions enqueued on the engine's stream into flight slot `slot` (whose previous
@@ -3548,15 +3549,17 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = s->on_key ? c->key_stream : s->st;
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
-  if (v) {
+  if (v) {   // the batch's votes beside the staged ones, every signature keyed by one launch
     if (n) {
       int r;
-      if ((r = upload_votes(c, f, ks, v, n_upd, n, h_sizes))) return r;
+      if ((r = upload_votes(c, f, ks, v, n_upd, n, h_sizes, false))) return r;
     }
+    HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, total, f.d_keys, ks));
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (h_keys_in) {   // keys and sizes given on the host (txv_pool_check_keys)
+    if (n_upd) HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n_upd, f.d_keys, ks));
     c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
       memcpy(f.h_keys + (size_t)(n_upd + lo) * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
       memcpy(f.h_sizes + n_upd + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
@@ -3570,6 +3573,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (n_upd) {       // staged Update entries, alone or before keys already in HBM (moved beside them)
+    HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n_upd, f.d_keys, ks));
     if (n) {
       HIP_TRY(c, hipMemcpyAsync(f.d_keys + (size_t)n_upd * 8, d_keys, (size_t)n * 32, hipMemcpyDeviceToDevice, ks));
       HIP_TRY(c, hipMemcpyAsync(f.d_sizes + n_upd, d_sizes, (size_t)n * 4, hipMemcpyDeviceToDevice, ks));

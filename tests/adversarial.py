@@ -116,9 +116,6 @@ class C4Stream:
         self.addrs = np.frombuffer(b"".join(addrs), np.uint8).reshape(self.n_vals, 20)
         exp_ok = [O.decode_ok(p) for p in self.pubs]
         assert list(ok.astype(bool)) == exp_ok, "validator decode flags differ from the oracle"
-        # forgery pool: (r, [r]B)
-        self.pool_r = [int(x) for x in self.rng.integers(1, 2 ** 62, size=256)]
-        self.pool_R = [O.scalarmult_base(r.to_bytes(32, "little")) for r in self.pool_r]
         # epoch size: every honest validator votes every tx once as a base vote
         base_frac = 1.0 - 0.05 - 0.05 - 0.02 - 0.005 - 0.0025 - 0.001
         self.epoch_txs = max(1, int(batch * batches_per_epoch * base_frac) // N_HONEST)
@@ -157,10 +154,9 @@ class C4Stream:
             self.opool.flush()
 
     # ---------------------------------------------------------------- batch construction
-    def _forge(self, vi: int, msg: bytes, pick: int):
-        """forged (R || s) for crafted validator vi (index into self.crafted)"""
+    def _forge(self, vi: int, msg: bytes, r: int, R: bytes):
+        """forged (R || s) for crafted validator vi (index into self.crafted), nonce r with R = [r]B"""
         name, pub, a = self.crafted[vi]
-        r, R = self.pool_r[pick], self.pool_R[pick]
         k = int.from_bytes(hashlib.sha512(R + pub + msg).digest(), "little") % E.L
         s = (r + k * (a or 0)) % E.L
         return R + s.to_bytes(32, "little")
@@ -258,10 +254,19 @@ class C4Stream:
                           sig=np.zeros((len(hi), 64), np.uint8), sig_len=np.full(len(hi), 64, np.uint32))
         f["sig"][hi] = self.ctx.sign_votes(sub, f["val"][hi].astype(np.uint32), CHAIN)
 
-        # crafted-key votes (primaries and conflicts): forged
+        # crafted-key votes (primaries and conflicts): forged, each with a fresh nonce r (R = [r]B by
+        # the device keygen from a random seed, r its clamped expansion): with a small-order key
+        # s = r whatever the message, so nonces from a fixed pool would repeat whole signatures and
+        # CheckTx (keyed by SHA-256(Signature)) would drop all but the first as ErrTxInCache
         ci = np.nonzero(((f["kind"] == 1) | (f["kind"] == 2)) & (np.arange(n_all) < n_prim + n_conf))[0]
-        picks = rng.integers(0, len(self.pool_r), len(ci))
+        n_fresh = int((f["kind"][ci] == 1).sum())
+        seeds = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n_fresh)]
+        fresh_R = self.ctx.keygen(seeds) if n_fresh else []
+        if n_fresh:
+            self.ctx.keygen(self.seeds)           # keygen also sets the signer keys: the honest ones back
+        fresh_r = [_expand(sd) for sd in seeds]
         nc_form = rng.integers(0, 3, len(ci))
+        q_f = 0
         for q, i in enumerate(ci):
             vi = int(f["val"][i]) - N_HONEST
             if f["kind"][i] == 2:
@@ -271,7 +276,8 @@ class C4Stream:
                 continue
             msg = T.sign_bytes(int(f["height"][i]), self.hashes[f["tx"][i]].tobytes(), 1_700_000_000,
                                int(f["ts_nanos"][i]), CHAIN)
-            f["sig"][i] = np.frombuffer(self._forge(vi, msg, int(picks[q])), np.uint8)
+            f["sig"][i] = np.frombuffer(self._forge(vi, msg, fresh_r[q_f], fresh_R[q_f]), np.uint8)
+            q_f += 1
         # votes no registry key signs (unknown validator, empty address, nil; primaries and their
         # conflicts) carry distinct random signature bytes: TxVotePool keys a vote by
         # SHA-256(Signature) (txvotepool.go:467-469), so a shared or all-zero signature would make
@@ -298,7 +304,12 @@ class C4Stream:
             s = int.from_bytes(f["sig"][i, 32:].tobytes(), "little") + E.L
             f["sig"][i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
         f["sig"][g_top, 63] |= (np.uint8(0x20) << rng.integers(0, 3, len(g_top)).astype(np.uint8))
-        f["sig_len"][g_len] = rng.choice(np.array([0, 63, 65], np.uint32), len(g_len))
+        # lengths != 64: mostly 1..63 and 65..72 (distinct signature bytes, so CheckTx keys them apart),
+        # a few empty signatures (one key for all of them: the first is admitted, the rest are
+        # ErrTxInCache, as the reference pool does)
+        g_lens = np.where(rng.random(len(g_len)) < 0.5, rng.integers(1, 64, len(g_len)), rng.integers(65, 73, len(g_len)))
+        g_lens[rng.random(len(g_len)) < 0.01] = 0
+        f["sig_len"][g_len] = g_lens.astype(np.uint32)
         for grp, name in ((g_r, "r_bit_flip"), (g_s, "s_bit_flip"), (g_field, "field_changed"), (g_sl, "s_plus_l"),
                           (g_top, "s_top_bits"), (g_len, "sig_len")):
             f["cls"][grp] = CLS[name]

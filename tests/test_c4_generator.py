@@ -15,7 +15,7 @@ class OracleCtx:
         self.flow = None
 
     def keygen(self, seeds):
-        self.seeds = list(seeds)
+        self.seeds = list(seeds)              # the signer keys, as txv_keygen sets them
         return [self.O.pubkey(s) for s in seeds]
 
     def set_validators(self, pubs, powers, chain):

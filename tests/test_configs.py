@@ -120,6 +120,12 @@ def test_c4_adversarial_with_pool_stage(oracle_lib, pool_device):
         for name, share in (("ErrVoteInvalidValidatorAddress(empty)", 0.0025),
                             ("ErrVoteInvalidValidatorIndex", 0.005), ("ErrVoteNil", 0.001)):
             assert st["by_status"].get(name, 0) >= 0.8 * share * st["votes"], (name, st)
+        # ... counted per generated class: all but the two whose signatures repeat by construction
+        # (exact replays; the identity key's non-canonical R with s = 0 has four signatures in all),
+        # which CheckTx keys by SHA-256(Signature) and drops as ErrTxInCache while cached
+        for name, c in st["class_share_at_txflow"].items():
+            if name not in ("exact_replay", "noncanonical_r"):
+                assert c["ratio"] >= 0.8, (name, c)
     finally:
         ctx.close()
 
