@@ -3181,6 +3181,7 @@ struct PoolDev {
     uint64_t *h_res = nullptr, *m_res = nullptr;        // mapped, per tile (entries, bytes): [2 ntm] appended, [2 ntm] removed
     uint32_t nt_app = 0, nt_rm = 0;                // tiles of the batch in flight with partials there
     hipEvent_t ev = nullptr;
+    hipEvent_t up_ev = nullptr;                    // the slot's signature uploads done (copy stream)
   } fl[kPdRing];
   uint32_t* h_clen = nullptr;
   hipEvent_t ev = nullptr;
@@ -3204,6 +3205,7 @@ struct PoolDev {
       dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
       hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status); hfree(f.h_res);
       if (f.ev) (void)hipEventDestroy(f.ev);
+      if (f.up_ev) (void)hipEventDestroy(f.up_ev);
     }
     if (tmp) (void)hipFree(tmp);
     hfree(h_clen);
@@ -3253,7 +3255,10 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     HIP_TRY(c, hipMemset(s->clen, 0, 8));
     HIP_TRY(c, hipMemset(s->detached, 0, cw));
     HIP_TRY(c, hipEventCreateWithFlags(&s->ev, hipEventDisableTiming));
-    for (PoolDev::Flight& f : s->fl) HIP_TRY(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+    for (PoolDev::Flight& f : s->fl) {
+      HIP_TRY(c, hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&f.up_ev, hipEventDisableTiming));
+    }
     // the batches run on the context's key stream: no HSA queue of the engine's own.  Measured on
     // C5 with Update (profiles/r05/c5_ab): an own high-priority stream 49-66M votes/s, an own
     // normal one 44-88M, the key stream 97-103M -- a fifth queue beside the context's four is
@@ -3494,9 +3499,14 @@ void pooldev_result(const PoolDev* s, int slot, int64_t res[4]) {
 
 // n votes of a txv_votes batch into flight f's entries [off, off + n): signatures uploaded -- from
 // caller memory registered with txv_host_register (which must stay valid until the finish) or
-// through the slot's pinned staging -- and keyed on stream ks, h_sizes = their TxVote.Size()
+// through the slot's pinned staging -- on the context's copy stream (the DMA does not hold up the
+// kernels queued on the engine's stream meanwhile; f.up_ev marks it done), h_sizes = their
+// TxVote.Size(); with key, keyed on stream ks once uploaded
 int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes* v, uint32_t off, uint32_t n,
                  const uint32_t* h_sizes, bool key) {
+  // TXV_POOL_UPLOAD_STREAM (experiment): 1 (default) the copy stream, 0 the engine's stream itself
+  static const int up_mode = getenv("TXV_POOL_UPLOAD_STREAM") ? atoi(getenv("TXV_POOL_UPLOAD_STREAM")) : 1;
+  hipStream_t us = up_mode ? c->copy_stream : ks;
   bool reg;
   {
     std::lock_guard<std::mutex> lk(c->mu);
@@ -3509,11 +3519,15 @@ int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes
     }, 4096);
   memcpy(f.h_sizes + off, h_sizes, (size_t)n * 4);
   HIP_TRY(c, hipMemcpyAsync(f.d_sig + (size_t)off * 16, reg ? (const void*)v->sig : (const void*)(f.h_sig + (size_t)off * 16),
-                            (size_t)n * 64, hipMemcpyHostToDevice, ks));
+                            (size_t)n * 64, hipMemcpyHostToDevice, us));
   HIP_TRY(c, hipMemcpyAsync(f.d_len + off, reg ? (const void*)v->sig_len : (const void*)(f.h_len + off), (size_t)n * 4,
-                            hipMemcpyHostToDevice, ks));
-  HIP_TRY(c, hipMemcpyAsync(f.d_sizes + off, f.h_sizes + off, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-  if (key) HIP_TRY(c, txv_launch_sig_keys(f.d_sig + (size_t)off * 16, f.d_len + off, n, f.d_keys + (size_t)off * 8, ks));
+                            hipMemcpyHostToDevice, us));
+  HIP_TRY(c, hipMemcpyAsync(f.d_sizes + off, f.h_sizes + off, (size_t)n * 4, hipMemcpyHostToDevice, us));
+  HIP_TRY(c, hipEventRecord(f.up_ev, us));
+  if (key) {
+    HIP_TRY(c, hipStreamWaitEvent(ks, f.up_ev, 0));
+    HIP_TRY(c, txv_launch_sig_keys(f.d_sig + (size_t)off * 16, f.d_len + off, n, f.d_keys + (size_t)off * 8, ks));
+  }
   return TXV_OK;
 }
 
@@ -3554,12 +3568,16 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
       int r;
       if ((r = upload_votes(c, f, ks, v, n_upd, n, h_sizes, false))) return r;
     }
+    HIP_TRY(c, hipStreamWaitEvent(ks, f.up_ev, 0));       // the staged and the batch's uploads (copy stream, in order)
     HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, total, f.d_keys, ks));
     d_keys = f.d_keys;
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (h_keys_in) {   // keys and sizes given on the host (txv_pool_check_keys)
-    if (n_upd) HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n_upd, f.d_keys, ks));
+    if (n_upd) {
+      HIP_TRY(c, hipStreamWaitEvent(ks, f.up_ev, 0));
+      HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n_upd, f.d_keys, ks));
+    }
     c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
       memcpy(f.h_keys + (size_t)(n_upd + lo) * 8, h_keys_in + (size_t)lo * 32, (size_t)(hi - lo) * 32);
       memcpy(f.h_sizes + n_upd + lo, h_sizes + lo, (size_t)(hi - lo) * 4);
@@ -3573,6 +3591,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     d_sizes = f.d_sizes;
     d_valid = nullptr;
   } else if (n_upd) {       // staged Update entries, alone or before keys already in HBM (moved beside them)
+    HIP_TRY(c, hipStreamWaitEvent(ks, f.up_ev, 0));
     HIP_TRY(c, txv_launch_sig_keys(f.d_sig, f.d_len, n_upd, f.d_keys, ks));
     if (n) {
       HIP_TRY(c, hipMemcpyAsync(f.d_keys + (size_t)n_upd * 8, d_keys, (size_t)n * 32, hipMemcpyDeviceToDevice, ks));
