@@ -206,6 +206,11 @@ C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in 
 # holds what CheckTx admitted ahead of the commits (~8 batches in the pipelines below) -- not the
 # stream (2.15M votes)
 C5_POOL_SIZE = 1 << 20
+# TXV_C5_NO_UPDATE=1 (experiment: the "without Update" figure of the same build): no Update calls,
+# and a Size cap above the stream so nothing fills
+C5_NO_UPDATE = bool(os.environ.get("TXV_C5_NO_UPDATE"))
+if C5_NO_UPDATE:
+    C5_POOL_SIZE = 1 << 23
 
 
 def c5_commit_updates(wl, added_slots, commit_batch):
@@ -257,6 +262,8 @@ def c5_prepare_updates(ctx, wl):
         b.is_nil = None
     ctx.reset_flow()
     upd = c5_commit_updates(wl, np.concatenate(added), commit_batch)
+    if C5_NO_UPDATE:
+        upd = [None] * len(upd)
     for u in upd:                      # the Updates' columns registered too (DMA'd by the pool engine)
         if u is not None:
             for col in (u.sig, u.sig_len):
@@ -307,8 +314,8 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                 seen.add(col.ctypes.data)
                 ctx.host_register(col)
     # Reactor.Receive -> TxVotePool.CheckTxWithInfo -> TxFlow.TryAddVote, with the pool's LRU cache
-    # in HBM (TXV_POOL_DEVICE_CACHE: keys, decisions and the new cache in one GPU round trip per
-    # batch, the admitted votes appended to the pool list on the host) -- the reported mode -- and,
+    # in HBM (TXV_POOL_DEVICE_CACHE: keys, decisions, the new cache and the pool list's appends and
+    # Update removals in one GPU chain per batch) -- the reported mode -- and,
     # beside it, on the host (keys on the GPU, stack-distance decisions on the host threads, the
     # two halves pipelined on two threads)
     def run_mode(device_cache: bool):
@@ -448,10 +455,10 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
             bl = (np.array(done) - np.array(submit)) * 1e3
             allst = np.concatenate(pool_st)
             stages = ("two pipelined stages with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE) -- "
-                      "txv_pool_check_submit (Size on the host, keys, stack-distance decisions and the new cache "
-                      "enqueued on the GPU, one thread) and txv_pool_check_wait (the statuses; the admitted votes "
-                      "appended to the pool list by the pool's own thread, another); p50_pool_check_ms = their sum "
-                      "per batch" if device_cache else
+                      "txv_pool_check_submit (Size on the host; keys, stack-distance decisions, the new cache and "
+                      "the pool list in HBM -- the staged Update's pushes and removals first, then the batch's "
+                      "appends -- enqueued on the GPU, one thread) and txv_pool_check_wait (the statuses, "
+                      "another); p50_pool_check_ms = their sum per batch" if device_cache else
                       "two pipelined stages -- txv_pool_prepare (keys on the GPU + Size, one thread) and "
                       "txv_pool_check_keys (LRU + pool on the host, another); p50_pool_check_ms = their sum per batch")
             out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "
@@ -838,8 +845,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
     ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20),
                     help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
-    ap.add_argument("--base-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24, 26),
-                    help="base-point table window (0 = library default)")
+    # the C2 context's base-point table: radix 2^26 (43 GB of HBM, one per process and device; 22
+    # mixed additions per verify instead of 23): +3.0 % on one box (688.3M vs 668.3M votes/s,
+    # profiles/r05/val1).  The library's default stays radix 2^24 (11.8 GB): a test session holds
+    # several contexts.  The other legs' contexts take the library default.
+    ap.add_argument("--base-w", type=int, default=26, choices=(0, 4, 8, 10, 12, 14, 16, 20, 22, 24, 26),
+                    help="base-point table window of the C2 context (0 = library default: 24)")
     ap.add_argument("--lane-votes", type=int, default=0, choices=(0, 1, 2, 4, 8),
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")

@@ -580,7 +580,7 @@ __device__ __forceinline__ bool sig_eq_votes(const FlowBatch& b, uint32_t i, uin
 // arena row (one atomic per 1024-vote block for the block's ADDED votes) and stores the accepted vote in full
 // (the reference's votes[addr] = vote, vote_set.go:154); the cell keeps the row for the crossing
 // step, which publishes it as the cell's accepted vote once no vote of the batch reads acc
-__global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBatch b) {
+__global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBatch b, int stamp_only) {
   __shared__ uint32_t wsum[16], wnew[16];
   __shared__ uint32_t base_s, nbase_s;
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
@@ -615,21 +615,29 @@ __global__ void __launch_bounds__(1024) txv_k_tally_resolve(FlowState fs, FlowBa
   // ADDED votes first elect one vote per set in an LDS hash set (C5's tx-major arrival order puts
   // ~8 votes of each of ~128 sets in a block: one device-scope exchange per (block, set) instead of
   // per vote, which serialised on the ~200 hot stamps); the electee's coherent read filters the
-  // sets already stamped, and the exchange decides the one vote that lists the set
-  __shared__ uint32_t l_set[2048];
-  for (uint32_t k = threadIdx.x; k < 2048; k += 1024) l_set[k] = TXV_NONE;
-  __syncthreads();
-  bool rep = false;
-  if (added) {
-    for (uint32_t h = (s * 0x9E3779B1u) >> 21;; h = (h + 1) & 2047u) {
-      const uint32_t o = atomicCAS(&l_set[h], TXV_NONE, s);
-      if (o == TXV_NONE) { rep = true; break; }
-      if (o == s) break;
-    }
-  }
+  // sets already stamped, and the exchange decides the one vote that lists the set.
+  // stamp_only (large batches, random arrival: a 1024-vote block holds ~1000 sets, each set
+  // ~100 blocks' electees, and their exchanges cost C2's resolve 146 -> 387 us): the electee only
+  // stamps the set with a plain store (every writer stores the same value), and a compaction
+  // over the set ids after this launch lists the stamped ones
   bool fresh = false;
-  if (rep && __hip_atomic_load(&fs.set_stamp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != b.stamp)
-    fresh = atomicExch(&fs.set_stamp[s], b.stamp) != b.stamp;
+  if (stamp_only) {               // (block-uniform) no election: a store per ADDED vote whose XCD
+    if (added && fs.set_stamp[s] != b.stamp) fs.set_stamp[s] = b.stamp;   // has not seen the stamp
+  } else {
+    __shared__ uint32_t l_set[2048];
+    for (uint32_t k = threadIdx.x; k < 2048; k += 1024) l_set[k] = TXV_NONE;
+    __syncthreads();
+    bool rep = false;
+    if (added) {
+      for (uint32_t h = (s * 0x9E3779B1u) >> 21;; h = (h + 1) & 2047u) {
+        const uint32_t o = atomicCAS(&l_set[h], TXV_NONE, s);
+        if (o == TXV_NONE) { rep = true; break; }
+        if (o == s) break;
+      }
+    }
+    if (rep && __hip_atomic_load(&fs.set_stamp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != b.stamp)
+      fresh = atomicExch(&fs.set_stamp[s], b.stamp) != b.stamp;
+  }
   // the block's ADDED votes take consecutive arena rows and its fresh sets consecutive list
   // entries: one atomic per 1024 votes each (a hot counter serialises at ~10k atomics per 50 us)
   const uint64_t m = __ballot(added), mf = __ballot(fresh);
@@ -708,14 +716,14 @@ __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 // again per level instead of the list.
 // One-wave blocks (12.5 KB of LDS each): the kernel runs beside the next batch's K1b, whose
 // entry buffers leave ~32 KB of a CU's LDS free.
-__global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch b) {
+__global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch b, const uint32_t* n_stamped) {
   __shared__ __attribute__((aligned(16))) uint32_t l_vote[1][kListCap];
   __shared__ __attribute__((aligned(16))) int64_t l_pow[1][kListCap];
   __shared__ int64_t l_hist[1][64];
   const int lane = threadIdx.x & 63;
   constexpr uint32_t wv = 0;
   const uint32_t gw = blockIdx.x, n_waves = gridDim.x;
-  const uint32_t n_list = fs.ctr->n_stamped;
+  const uint32_t n_list = *n_stamped;
   const uint32_t nbits = 32u - (uint32_t)__builtin_clz(max(b.n, 2u) - 1u);
   const uint32_t levels = (nbits + kDigitBits - 1) / kDigitBits;
   for (uint32_t j = gw; j < n_list; j += n_waves) {
@@ -1000,6 +1008,18 @@ __global__ void __launch_bounds__(256) txv_k_bitmap(FlowState fs, uint32_t* dst,
   if (t < bm_words) dst[t] = commit_word(fs, t, min(fs.ctr->n_sets, fs.max_txs));
 }
 
+// the sets the batch stamped (tally_resolve with stamp_only), listed in id order
+constexpr uint32_t kStampCompactMin = 1u << 18;
+struct StampPred {
+  FlowState fs;
+  FlowBatch b;
+  __device__ bool operator()(uint32_t s) const { return fs.set_stamp[s] == b.stamp; }
+};
+struct StampAct {
+  FlowBatch b;
+  __device__ void operator()(uint32_t s, uint32_t rank) const { b.stamped[rank] = s; }
+};
+
 template <class Pred, class Act>
 hipError_t compact(Pred p, Act act, uint32_t n, uint32_t* blk, hipStream_t st) {
   const uint32_t nb = (n + kScanItems - 1) / kScanItems;
@@ -1052,11 +1072,20 @@ hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets
   const uint32_t nb = (b->n + kScanItems - 1) / kScanItems;
   const uint32_t g = (b->n + 255) / 256;
   if (!TXV_SKIP(1)) hipLaunchKernelGGL(txv_k_tally_min, dim3(g ? g : 1), dim3(256), 0, st, *fs, *b, nb);
-  if (b->n && !TXV_SKIP(2)) hipLaunchKernelGGL(txv_k_tally_resolve, dim3((b->n + 1023) / 1024), dim3(1024), 0, st, *fs, *b);
   sets_bound = std::min(sets_bound, fs->max_txs);
+  // large batches list their stamped sets by a compaction over the set ids (see tally_resolve)
+  const bool stamp_only = b->n >= kStampCompactMin;
+  if (b->n && !TXV_SKIP(2))
+    hipLaunchKernelGGL(txv_k_tally_resolve, dim3((b->n + 1023) / 1024), dim3(1024), 0, st, *fs, *b, stamp_only ? 1 : 0);
+  const uint32_t* n_stamped = &fs->ctr->n_stamped;
+  if (stamp_only) {
+    hipError_t e;
+    if ((e = compact(StampPred{*fs, *b}, StampAct{*b}, sets_bound, fs->set_blk, st))) return e;
+    n_stamped = fs->set_blk + (sets_bound + kScanItems - 1) / kScanItems;   // scan_top's total
+  }
   // persistent waves over the batch's stamped sets (at most min(sets, votes) of them): one wave per set
   const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>(std::min(sets_bound, b->n), 4096));
-  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(64), 0, st, *fs, *b);
+  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(64), 0, st, *fs, *b, n_stamped);
   if (TXV_SKIP(32)) return hipGetLastError();
   hipLaunchKernelGGL(txv_k_status_out, dim3(nb ? nb : 1), dim3(256), 0, st, *fs, *b);
   hipLaunchKernelGGL(txv_k_event_top, dim3(1), dim3(256), 0, st, *fs, *b, nb);

@@ -209,6 +209,7 @@ struct txv_ctx {
   SetEntry* d_tab = nullptr; uint32_t tab_mask = 0;
   uint8_t* d_keys = nullptr; uint64_t keys_cap = 0;
   uint32_t *d_set_entry = nullptr, *d_set_txkey = nullptr, *d_set_stamp = nullptr, *d_set_cross = nullptr, *d_bitmap = nullptr;
+  uint32_t* d_set_blk = nullptr;   // scan blocks over the set ids (the stamped-set compaction of large batches)
   uint32_t* d_set_digest = nullptr;   // [max_txs][4] SHA-256(TxHash)[0:16]
   int64_t* d_set_sum = nullptr;
   TallyCell* d_cells = nullptr;
@@ -399,6 +400,7 @@ FlowState flow_state(const txv_ctx* c) {
   f.tab = c->d_tab; f.tab_mask = c->tab_mask; f.max_txs = c->cfg.max_txs;
   f.keys = c->d_keys; f.keys_cap = c->keys_cap;
   f.set_entry = c->d_set_entry; f.set_txkey = c->d_set_txkey; f.set_sum = c->d_set_sum; f.set_stamp = c->d_set_stamp; f.set_digest = c->d_set_digest;
+  f.set_blk = c->d_set_blk;
   f.cell = c->d_cells; f.set_cross = c->d_set_cross;
   f.arena_sig = c->d_arena_sig; f.arena_height = c->d_arena_height; f.arena_sec = c->d_arena_sec;
   f.arena_nanos = reinterpret_cast<int32_t*>(c->d_arena_nanos); f.arena_val = c->d_arena_val;
@@ -428,7 +430,7 @@ int alloc_tally(txv_ctx* c) {
       (r = dalloc(c, &c->d_arena_sec, M)) || (r = dalloc(c, &c->d_arena_nanos, M)) || (r = dalloc(c, &c->d_arena_val, M)) ||
       (r = dalloc(c, &c->d_arena_seq, M)) || (r = dalloc(c, &c->d_arena_txkey, 8 * M)) ||
       (r = dalloc(c, &c->d_set_sum, c->cfg.max_txs)) ||
-      (r = dalloc(c, &c->d_set_stamp, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
+      (r = dalloc(c, &c->d_set_stamp, c->cfg.max_txs)) || (r = dalloc(c, &c->d_set_blk, (size_t)c->cfg.max_txs / 1024 + 2)) || (r = dalloc(c, &c->d_set_entry, c->cfg.max_txs)) ||
       (r = dalloc(c, &c->d_set_digest, (size_t)c->cfg.max_txs * 4)) ||
       (r = dalloc(c, &c->d_set_txkey, (size_t)c->cfg.max_txs * 8)) ||
       (r = dalloc(c, &c->d_bitmap, (c->cfg.max_txs + 31) / 32)) || (r = dalloc(c, &c->d_tab, tab)) ||
@@ -1392,7 +1394,7 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_btable4); dfree(c->d_btable8); dfree(c->d_park); dfree(c->d_wctr); release_base_table(c->device, c->d_btable_wide); c->d_btable = nullptr; dfree(c->d_tmp_pubs); dfree(c->d_tmp_ok); dfree(c->d_tmp_tables); dfree(c->d_tmp_addr);
   dfree(c->d_cells); dfree(c->d_set_cross); dfree(c->d_set_sum);
   dfree(c->d_arena_sig); dfree(c->d_arena_height); dfree(c->d_arena_sec); dfree(c->d_arena_nanos); dfree(c->d_arena_val);
-  dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_set_digest); dfree(c->d_bitmap);
+  dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_set_blk); dfree(c->d_set_digest); dfree(c->d_bitmap);
   dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
   dfree(c->d_addr_slots); dfree(c->d_q);
   for (const auto& rg : c->registered) (void)hipHostUnregister((void*)rg.first);

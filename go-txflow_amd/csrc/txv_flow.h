@@ -125,6 +125,7 @@ struct FlowState {
   uint32_t* set_txkey;          // [max_txs][8]
   int64_t* set_sum;             // [max_txs]
   uint32_t* set_stamp;          // [max_txs]
+  uint32_t* set_blk;            // [max_txs / 1024 + 2] scan blocks of the stamped-set compaction (large batches)
   uint32_t* set_cross;          // [max_txs]
   uint32_t* set_digest;         // [max_txs][4] SHA-256(TxHash bytes)[0:16]: the set's name in the exchange
   TallyCell* cell;              // [max_txs * n_vals]
