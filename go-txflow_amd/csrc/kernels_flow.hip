@@ -714,11 +714,14 @@ __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 // set instead of the O(k^2) pairwise prefix sums and the row-rescanning binary lifting it
 // replaced.  Sets with more ADDED votes than the list holds read their row
 // again per level instead of the list.
-// One-wave blocks (12.5 KB of LDS each): the kernel runs beside the next batch's K1b, whose
-// entry buffers leave ~32 KB of a CU's LDS free.
+// One-wave blocks: the kernel runs beside the next batch's K1b, whose entry buffers leave ~32 KB
+// of a CU's LDS free -- so the list holds Cap entries: 1024 (12.5 KB) for large validator sets,
+// 128 (2 KB) when no set can have more (n_vals <= 128, C2's 100), which lets 16 blocks share a CU
+// beside K1b instead of 2 (with 2 the C2 tally's crossing pass crawled beside the whole K1b).
+template <uint32_t Cap>
 __global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch b, const uint32_t* n_stamped) {
-  __shared__ __attribute__((aligned(16))) uint32_t l_vote[1][kListCap];
-  __shared__ __attribute__((aligned(16))) int64_t l_pow[1][kListCap];
+  __shared__ __attribute__((aligned(16))) uint32_t l_vote[1][Cap];
+  __shared__ __attribute__((aligned(16))) int64_t l_pow[1][Cap];
   __shared__ int64_t l_hist[1][64];
   const int lane = threadIdx.x & 63;
   constexpr uint32_t wv = 0;
@@ -745,7 +748,7 @@ __global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch 
       if (added) {
         const uint32_t e = k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         const int64_t pw = fs.power[v];
-        if (e < kListCap) { l_vote[wv][e] = f; l_pow[wv][e] = pw; }
+        if (e < Cap) { l_vote[wv][e] = f; l_pow[wv][e] = pw; }
         part += pw;
       }
       k += (uint32_t)__popcll(m);
@@ -758,7 +761,7 @@ __global__ void __launch_bounds__(64) txv_k_tally_cross(FlowState fs, FlowBatch 
       cross = 0;                              // already committed: every ADDED vote re-fires
     } else if (total >= fs.quorum) {
       const int64_t need = fs.quorum - prior;
-      const bool in_lds = k <= kListCap;
+      const bool in_lds = k <= Cap;
       uint32_t pfx = 0;                       // the crossing index's digits chosen so far
       int64_t before = 0;                     // stake of the entries below the prefix's range
       for (uint32_t lv = 0; lv < levels; ++lv) {
@@ -1084,8 +1087,13 @@ hipError_t txv_flow_tally(const FlowState* fs, const FlowBatch* b, uint32_t sets
     n_stamped = fs->set_blk + (sets_bound + kScanItems - 1) / kScanItems;   // scan_top's total
   }
   // persistent waves over the batch's stamped sets (at most min(sets, votes) of them): one wave per set
-  const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>(std::min(sets_bound, b->n), 4096));
-  if (!TXV_SKIP(16)) hipLaunchKernelGGL(txv_k_tally_cross, dim3(cross_blocks), dim3(64), 0, st, *fs, *b, n_stamped);
+  // TXV_CROSS_BLOCKS (experiment): the persistent one-wave blocks' cap (default 4096)
+  static const uint32_t cross_cap = getenv("TXV_CROSS_BLOCKS") ? (uint32_t)atoi(getenv("TXV_CROSS_BLOCKS")) : 4096u;
+  const uint32_t cross_blocks = std::max<uint32_t>(1, std::min<uint32_t>(std::min(sets_bound, b->n), cross_cap));
+  if (!TXV_SKIP(16)) {
+    if (fs->n_vals <= 128) hipLaunchKernelGGL(txv_k_tally_cross<128>, dim3(cross_blocks), dim3(64), 0, st, *fs, *b, n_stamped);
+    else hipLaunchKernelGGL(txv_k_tally_cross<kListCap>, dim3(cross_blocks), dim3(64), 0, st, *fs, *b, n_stamped);
+  }
   if (TXV_SKIP(32)) return hipGetLastError();
   hipLaunchKernelGGL(txv_k_status_out, dim3(nb ? nb : 1), dim3(256), 0, st, *fs, *b);
   hipLaunchKernelGGL(txv_k_event_top, dim3(1), dim3(256), 0, st, *fs, *b, nb);
