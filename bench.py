@@ -55,10 +55,16 @@ W_FM = 1 + 22 * 7 + 6 + 2 + 3 + 8
 W_ALG = 1.1e4 + W_FM * 100.0
 
 
+def table_positions(w: int) -> int:
+    """table positions (one entry read per position and vote) of a radix-2^w table: ceil(256/w),
+    12 for the long-top radix-2^21 layout (ed25519_dev.h Tab<21>)"""
+    return 12 if w == 21 else -(-256 // w)
+
+
 def w_alg_for(wb: int, wa: int) -> float:
     """W_ALG of the same algorithm for other table windows (C5's 1000 validators run W_A = 16:
-    11 + 16 = 27 entries): the same terms with nT = ceil(256/wb) + ceil(256/wa) entries"""
-    nt = -(-256 // wb) + -(-256 // wa)
+    11 + 16 = 27 entries): the same terms with nT = positions(wb) + positions(wa) entries"""
+    nt = table_positions(wb) + table_positions(wa)
     return 1.1e4 + (1 + (nt - 2) * 7 + 6 + 2 + 3 + 8) * 100.0
 
 
@@ -580,7 +586,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
                      "peak": round(VALU_PEAK / 1e12, 3), "unit": "Tlane-op/s",
                      "frac": round(b0.n * w_c5 / (v_solo * 1e-3) / VALU_PEAK, 4) if v_solo else None,
                      "note": f"standalone K1a + K1b of one batch; W_alg for windows {ctx.base_w}/{ctx.table_w} "
-                             f"(bench.w_alg_for: {-(-256 // ctx.base_w) + -(-256 // ctx.table_w)} table entries)"}}
+                             f"(bench.w_alg_for: {table_positions(ctx.base_w) + table_positions(ctx.table_w)} table entries)"}}
     ctx.close()
     return out
 
@@ -843,8 +849,12 @@ def main():
                     help="0 = 10,000 at N=1 (C2) / 20,000 at N>1 (C3: 160k txs at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every host core this process may use")
-    ap.add_argument("--table-w", type=int, default=0, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20),
-                    help="fixed-base window; 0 = auto (largest whose tables fit the HBM budget)")
+    # the C2 context's validator tables: radix 2^21 in the 12-position long-top layout (1.70 GB per
+    # validator, 170 GB for C2's 100; 21 mixed additions per verify with the radix-2^26 base table
+    # instead of 22): 738-743M vs 717-721M votes/s at radix 2^20 on one box (profiles/r05/w21)
+    ap.add_argument("--table-w", type=int, default=21, choices=(0, 4, 8, 10, 12, 14, 16, 18, 20, 21),
+                    help="fixed-base window of the C2 context; 0 = auto (largest whose tables fit the HBM "
+                         "budget); 21 = 12-position tables, 1.70 GB per validator")
     # the C2 context's base-point table: radix 2^26 (43 GB of HBM, one per process and device; 22
     # mixed additions per verify instead of 23): +3.0 % on one box (688.3M vs 668.3M votes/s,
     # profiles/r05/val1).  The library's default stays radix 2^24 (11.8 GB): a test session holds
@@ -1060,7 +1070,7 @@ def main():
                          "traffic_over_alg_bytes": None if not traffic else round(traffic / (wl.n * VERIFY_ALG_BYTES), 3),
                          "alg_lane_ops_per_vote": w_alg,
                          "alg_source": f"DESIGN.md §4: SHA-512 2 blocks + ScReduce + field multiplies x 100 for "
-                                       f"{-(-256 // ctx.base_w) + -(-256 // ctx.table_w)} table entries (windows "
+                                       f"{table_positions(ctx.base_w) + table_positions(ctx.table_w)} table entries (windows "
                                        f"{ctx.base_w}/{ctx.table_w}; bench.w_alg_for)",
                          "k1b_valu_issue_busy": None if k1b_busy is None else round(k1b_busy, 3),
                          "valu_busy_note": "K1b wave-instructions x issue cycles (64-bit class 4, others 2) / SIMD-cycles "

@@ -13,6 +13,7 @@
 //   W = 4:  64 positions x    9 entries x 128 B =    73,728 B per point (B fits in LDS)
 //   W = 8:  32 positions x  129 entries x 128 B =   528,384 B per point (L2/MALL resident)
 //   W = 20: 13 positions x 2^19+1 entries x 128 B = 872 MB per point (HBM)
+//   W = 21: 12 positions (11 x 2^20+1, the top one 2^21+9 entries) = 1.70 GB per point (Tab<21>)
 // ceil(256/W_B) + ceil(256/W_A) table additions per verification, the first of them free
 // (the accumulator starts as the first B entry's point).
 #pragma once
@@ -27,7 +28,27 @@ template <int W>
 struct Tab {
   static constexpr int kPositions = (256 + W - 1) / W;
   static constexpr int kEntries = (1 << (W - 1)) + 1;
+  static constexpr bool kLongTop = false;     // see Tab<21>
+  static constexpr int kTopEntries = kEntries;
   static constexpr size_t kWords = (size_t)kPositions * kEntries * kEntryWords;   // > 2^31 at W = 24
+  // K0 lanes per point: one per (position, chunk of 8 multiples)
+  static constexpr uint64_t kBuildLanes = (uint64_t)kPositions * ((kEntries - 1) / 8);
+};
+
+// Radix 2^21 over 253 bits: 12 positions, one table addition fewer than radix 2^20's 13 (every
+// verified scalar is below L < 2^253).  Eleven signed digits in [-2^20, 2^20) cannot reach 2^252,
+// so the top position (bits 231..252) takes an unsigned digit: the remaining scalar plus the
+// carry, at most floor((L - 1) / 2^231) + 1 = 2^21 + 1.  Positions 0..10 hold 2^20 + 1 entries,
+// the top one 2^21 + 9 (K0 builds it in chunks of 8; entries above 2^21 + 1 are never read), so
+// T[pos][idx] stays at entry pos * kEntries + idx: 1.70 GB per point, against 0.87 GB at W = 20.
+template <>
+struct Tab<21> {
+  static constexpr int kPositions = 12;
+  static constexpr int kEntries = (1 << 20) + 1;
+  static constexpr bool kLongTop = true;
+  static constexpr int kTopEntries = (1 << 21) + 9;
+  static constexpr size_t kWords = ((size_t)(kPositions - 1) * kEntries + kTopEntries) * kEntryWords;
+  static constexpr uint64_t kBuildLanes = (uint64_t)(kPositions - 1) * ((kEntries - 1) / 8) + (kTopEntries - 1) / 8;
 };
 
 // legacy W = 4 names (keygen/sign and the host emulation)
@@ -223,8 +244,42 @@ TXV_HD int next_digit(uint32_t s[8], uint32_t& carry) {
   return (int)d - (int)(carry << W);
 }
 
+// digit of table position `pos` (in order, pos = 0, 1, ...): next_digit<W>, except for a
+// long-top table's last position, whose digit is the whole remaining scalar plus the carry
+// (non-negative, <= 2^21 + 1 for W = 21; s < 2^253)
+template <int W>
+TXV_HD int table_digit(uint32_t s[8], uint32_t& carry, int pos) {
+  if constexpr (Tab<W>::kLongTop) {
+    if (pos == Tab<W>::kPositions - 1) return (int)(s[0] + carry);
+  }
+  return next_digit<W>(s, carry);
+}
+
+// every signed radix-2^W digit of a scalar < 2^253 at once: digit i from bits [W i, W i + W) plus
+// the carry of digit i - 1, exactly the sequence table_digit<W> produces (the split K1b kernel)
+template <int W, int N>
+TXV_HD void signed_digits(const uint32_t s[8], int d[N]) {
+  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int b = W * i, w = b >> 5, o = b & 31;
+    uint32_t win = s[w] >> o;
+    if (o + W > 32 && w + 1 < 8) win |= s[w + 1] << (32 - o);
+    if (Tab<W>::kLongTop && i == Tab<W>::kPositions - 1) {   // table_digit: the rest + carry
+      static_assert(!Tab<W>::kLongTop || W * (Tab<W>::kPositions - 1) % 32 + 22 <= 32, "top digit in one word");
+      d[i] = (int)(win + carry);
+      break;
+    }
+    const uint32_t dd = (win & mask) + carry;
+    carry = (dd + half) >> W;
+    d[i] = (int)dd - (int)(carry << W);
+  }
+}
+
 // sum_i T_B[i][s_i] + T_A[i][-k_i] over raw scalars s, k < 2^253 (digits of k negated,
-// giving [k](-A)); digits are produced on the fly, so any windows < 32 work.  The base
+// giving [k](-A)); digits are produced on the fly, so any windows < 32 work (a long-top WA
+// table's last digit by table_digit).  The base
 // point's table may use a wider window WB than the validators' WA (one table serves every
 // vote, so it can take gigabytes of HBM).  The walk runs in fe10 (ge10_madd); the result is
 // handed back in radix 2^32 (X, Y, Z; T is not produced).
@@ -248,7 +303,7 @@ TXV_HD ge_ext double_scalarmult_w2(PtrB tb, PtrA ta, const uint32_t s_in[8], con
       P = ge10_madd(P, qp, qm, qd, ds < 0);
     }
     if (use_a) {
-      const int dk = next_digit<WA>(k, ck);
+      const int dk = table_digit<WA>(k, ck, pos);
       load_entry_w<WA>(ta, pos, dk < 0 ? -dk : dk, dk > 0, qp, qm, qd);
       P = ge10_madd(P, qp, qm, qd, dk > 0);
     }

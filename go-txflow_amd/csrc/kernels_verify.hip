@@ -54,12 +54,15 @@ __global__ void __launch_bounds__(64) txv_k_build_tables(const uint32_t* __restr
                                                           uint32_t* __restrict__ addr_words,
                                                           const uint32_t* __restrict__ out_slot) {
   constexpr int chunks = (Tab<W>::kEntries - 1) / 8;
-  constexpr int per_point = Tab<W>::kPositions * chunks;
+  constexpr uint64_t per_point = Tab<W>::kBuildLanes;
   const uint64_t gid = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   const uint32_t pt = (uint32_t)(gid / per_point);
   const int t = (int)(gid % per_point);
   if (pt >= n_points) return;
-  const int pos = t / chunks, c = t % chunks;
+  // a long-top table's last position takes the lanes past the others' (kTopEntries - 1) / 8 chunks
+  constexpr int last = Tab<W>::kPositions - 1;
+  const bool top = Tab<W>::kLongTop && t >= last * chunks;
+  const int pos = top ? last : t / chunks, c = top ? t - last * chunks : t % chunks;
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = pubs_le[pt * 8 + i];
@@ -414,8 +417,8 @@ __device__ __forceinline__ ge_ext double_scalarmult_pf(const uint32_t* tb, const
       entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), b);
       return d < 0;
     }
-    const int d = next_digit<WA>(k, ck);
-    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
+    const int d = table_digit<WA>(k, ck, pos);
+    entries_to_lds(ta, (uint32_t)(va * (uint32_t)(Tab<WA>::kWords / kEntryWords) + pos * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
     return d > 0;                                   // [k](-A): a positive digit subtracts
   };
   ge10_ext P;
@@ -484,8 +487,8 @@ __device__ __forceinline__ ge_ext double_scalarmult_rs(const uint32_t* tb, const
       entries_to_lds(tb, (uint32_t)(pos * Tab<WB>::kEntries + (d < 0 ? -d : d)), b);
       return d < 0;
     }
-    const int d = next_digit<WA>(k, ck);
-    entries_to_lds(ta, (uint32_t)((va * Tab<WA>::kPositions + pos) * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
+    const int d = table_digit<WA>(k, ck, pos);
+    entries_to_lds(ta, (uint32_t)(va * (uint32_t)(Tab<WA>::kWords / kEntryWords) + pos * Tab<WA>::kEntries + (d < 0 ? -d : d)), b);
     return d > 0;                                   // [k](-A): a positive digit subtracts
   };
   const bool n0 = issue(0), n1a = issue(1);
@@ -1015,23 +1018,6 @@ __device__ __forceinline__ fe10 ge10_quad_level2(const ge10_ext& p, uint32_t q) 
   return fe10_mul(fe10_sel(q & 1u, H, F), fe10_sel(q == 0, E, G));
 }
 
-// every signed radix-2^W digit of a scalar < 2^253 at once: digit i from bits [W i, W i + W) plus
-// the carry of digit i - 1, exactly the sequence next_digit<W> produces
-template <int W, int N>
-__device__ __forceinline__ void signed_digits(const uint32_t s[8], int d[N]) {
-  constexpr uint32_t mask = (1u << W) - 1u, half = 1u << (W - 1);
-  uint32_t carry = 0;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int b = W * i, w = b >> 5, o = b & 31;
-    uint32_t win = s[w] >> o;
-    if (o + W > 32 && w + 1 < 8) win |= s[w + 1] << (32 - o);
-    const uint32_t dd = (win & mask) + carry;
-    carry = (dd + half) >> W;
-    d[i] = (int)dd - (int)(carry << W);
-  }
-}
-
 #ifndef TXV_SPLIT_WAVES
 #define TXV_SPLIT_WAVES 3
 #endif
@@ -1075,7 +1061,7 @@ __global__ void __launch_bounds__(256, TXV_SPLIT_WAVES) txv_k_scalarmult_split(V
             nc |= (dB[t] < 0 ? 1u : 0u) << qq;
           } else if (t < nT) {
             const int d = dA[t - nB];
-            ec[qq] = (va * (uint32_t)nA + (uint32_t)(t - nB)) * (uint32_t)Tab<WA>::kEntries + (uint32_t)(d < 0 ? -d : d);
+            ec[qq] = va * (uint32_t)(Tab<WA>::kWords / kEntryWords) + (uint32_t)(t - nB) * (uint32_t)Tab<WA>::kEntries + (uint32_t)(d < 0 ? -d : d);
             nc |= (d > 0 ? 1u : 0u) << qq;   // [k](-A): a positive digit subtracts
             ac |= 1u << qq;
           } else {
@@ -1308,7 +1294,7 @@ extern "C" {
 template <int W>
 static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables, uint8_t* decode_ok,
                          uint32_t* addr_words, const uint32_t* out_slot, hipStream_t st) {
-  const uint64_t lanes = (uint64_t)n_points * Tab<W>::kPositions * ((Tab<W>::kEntries - 1) / 8);
+  const uint64_t lanes = (uint64_t)n_points * Tab<W>::kBuildLanes;
   hipLaunchKernelGGL(txv_k_build_tables<W>, dim3((uint32_t)((lanes + 63) / 64)), dim3(64), 0, st, pubs_le, n_points,
                      tables, decode_ok, addr_words, out_slot);
 }
@@ -1411,6 +1397,7 @@ hipError_t txv_launch_build_tables_at(int w, const uint32_t* pubs_le, uint32_t n
     case 16: launch_build<16>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     case 18: launch_build<18>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     case 20: launch_build<20>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
+    case 21: launch_build<21>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     case 22: launch_build<22>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     case 24: launch_build<24>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
     case 26: launch_build<26>(pubs_le, n_points, tables, decode_ok, addr_words, out_slot, st); break;
@@ -1426,11 +1413,12 @@ hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_po
 
 // (wb, wa): base-point and validator windows; supported pairs are (w, w) for every table
 // window, the radix-2^24 base table over wa = 12..20, the radix-2^26 one (43 GB: 10 positions
-// instead of 11) over wa = 16..20, and wb in {20, 22} over wa = 16
+// instead of 11) over wa = 16..21 (21: the 12-position long-top layout, Tab<21>), and wb in
+// {20, 22} over wa = 16
 bool txv_verify_windows_supported(int wb, int wa) {
   if (wb == wa) return wa == 4 || wa == 8 || wa == 10 || wa == 12 || wa == 14 || wa == 16;
   if (wb == 24) return wa == 12 || wa == 14 || wa == 16 || wa == 18 || wa == 20;
-  if (wb == 26) return wa == 16 || wa == 18 || wa == 20;
+  if (wb == 26) return wa == 16 || wa == 18 || wa == 20 || wa == 21;
   return wa == 16 && (wb == 20 || wb == 22);
 }
 
@@ -1486,6 +1474,7 @@ hipError_t txv_launch_scalarmult(int wb, int wa, const VerifyArgs* args, uint32_
       case 2616: e = launch_multi<B, 26, 16>(args, grid, st); break;
       case 2618: e = launch_multi<B, 26, 18>(args, grid, st); break;
       case 2620: e = launch_multi<B, 26, 20>(args, grid, st); break;
+      case 2621: e = launch_multi<B, 26, 21>(args, grid, st); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

@@ -42,10 +42,18 @@ void txv_sha256_bytes(const uint8_t* p, uint64_t n, uint8_t out[32]);   // SHA-2
 namespace {
 
 // fixed-base table words per point for window W: ceil(256/W) positions x (2^(W-1)+1) entries x 32
-// (one 128-byte half-Niels entry each, ge.h)
-inline size_t table_words(int w) { return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32; }
+// (one 128-byte half-Niels entry each, ge.h); W = 21 is the 12-position long-top layout
+// (ed25519_dev.h Tab<21>: 11 x (2^20+1) + 2^21+9 entries)
+inline size_t table_words(int w) {
+  if (w == 21) return ((size_t)11 * ((1u << 20) + 1) + (1u << 21) + 9) * 32;
+  return (size_t)((256 + w - 1) / w) * ((1u << (w - 1)) + 1) * 32;
+}
 constexpr uint32_t kTableWords4 = 64 * 9 * 32;
-inline bool valid_window(int w) { return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20; }
+// 21 only on request (TXV_CFG_WINDOW): 1.70 GB of tables per validator, against the radix-2^26
+// base table (select_window)
+inline bool valid_window(int w) {
+  return w == 4 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16 || w == 18 || w == 20 || w == 21;
+}
 // TXV_K1A_ON_KEY_STREAM=1 runs K1a on the key stream, beside the previous batch's K1b (its 99
 // VGPRs do not fit beside two K1b waves, so it mostly fills K1b's tail): measured 614-621 vs
 // 608M votes/s (within box noise, profiles/r02/ab), while the two kernels' overlapping durations
@@ -1136,7 +1144,7 @@ int select_window(txv_ctx* c, int w) {
   c->tab_w = w;
   c->d_btable = w == 4 ? c->d_btable4 : c->d_btable8;
   c->b_w = w;
-  int bw = c->cfg_bw ? c->cfg_bw : (w >= 12 ? 24 : w);
+  int bw = c->cfg_bw ? c->cfg_bw : (w == 21 ? 26 : w >= 12 ? 24 : w);
   if ((c->lane_votes < 4 && c->lane_votes != 1) || !txv_verify_windows_supported(bw, w)) bw = w;
   while (bw != w && c->btable_wide_w != bw) {
     release_base_table(c->device, c->d_btable_wide);

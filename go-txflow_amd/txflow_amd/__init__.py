@@ -424,10 +424,12 @@ class Context:
                  max_validators: int = 1024, max_accepted: int = 0, max_msg_bytes: int = 256,
                  table_w: int | None = None, table_budget_mb: int = 0, lane_votes: int = 0,
                  base_w: int = 0, key_arena_bytes: int = 0):
-        """table_w: fixed-base window (4, 8, 10, 12, 14, 16, 18, 20) or None = the largest whose
-        per-validator tables fit ``table_budget_mb`` (0 = library default, 8 GiB)."""
-        if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20):
-            raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16, 18, 20")
+        """table_w: fixed-base window (4, 8, 10, 12, 14, 16, 18, 20, 21) or None = the largest
+        whose per-validator tables fit ``table_budget_mb`` (0 = library default, 112 GiB); 21 (the
+        12-position layout, 1.70 GB per validator, one table addition per vote fewer than 20) is
+        only taken on request and runs against the radix-2^26 base table."""
+        if table_w not in (None, 4, 8, 10, 12, 14, 16, 18, 20, 21):
+            raise ValueError("table_w must be None or one of 4, 8, 10, 12, 14, 16, 18, 20, 21")
         if lane_votes not in (0, 1, 2, 4, 8):
             raise ValueError("lane_votes must be 0 (default), 1 (split K1b/K1c), 2, 4 or 8")
         cfg = _Cfg(device, max_batch, max_txs, max_validators, max_accepted, max_msg_bytes,

@@ -32,7 +32,33 @@ static void build_table(std::vector<uint32_t>& tab, const uint32_t w[8], bool* o
   }
 }
 
+template <int W>
+static int digits_w(const uint32_t* s_in, int mode, int32_t* out) {
+  constexpr int n = Tab<W>::kPositions;
+  if (mode == 0) {          // the walks' streaming digits (table_digit)
+    uint32_t s[8], c = 0;
+    for (int i = 0; i < 8; ++i) s[i] = s_in[i];
+    for (int pos = 0; pos < n; ++pos) out[pos] = table_digit<W>(s, c, pos);
+  } else {                  // the split kernel's all-at-once digits
+    int d[n];
+    signed_digits<W, n>(s_in, d);
+    for (int pos = 0; pos < n; ++pos) out[pos] = d[pos];
+  }
+  return n;
+}
+
 extern "C" {
+
+// digits of scalar s for table window w (20, 21, 24, 26); returns the number of positions
+int emu_digits(int w, const uint32_t* s, int mode, int32_t* out) {
+  switch (w) {
+    case 20: return digits_w<20>(s, mode, out);
+    case 21: return digits_w<21>(s, mode, out);
+    case 24: return digits_w<24>(s, mode, out);
+    case 26: return digits_w<26>(s, mode, out);
+    default: return -1;
+  }
+}
 
 int emu_fe(const uint32_t* a, const uint32_t* b, uint32_t* out, int op) {
   fe x, y, r;

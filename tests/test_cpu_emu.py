@@ -32,6 +32,7 @@ def emu():
     E.emu_ge10_madd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     E.emu_ge10_madd_rd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     E.emu_entry.argtypes = [ctypes.c_void_p] * 3
+    E.emu_digits.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     E.emu_inv_var.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     E.emu_inv_var_counts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     E.emu_wire_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -258,3 +259,29 @@ def test_wire_decoder_source_vs_oracle(emu):
         assert rb[32:52] == f["addr"][:20] + bytes(20 - min(al, 20)), k
         assert rb[52:116] == f["sig"][:64] + bytes(64 - min(sl, 64)), k
     assert emu.emu_wire_fast_hits() - h0 > 2500   # canonical messages with <= 7-byte varints: fast path
+
+
+def test_table_digits_cover_every_scalar_below_L(emu):
+    """The walks' digit recoding (ed25519_dev.h table_digit / signed_digits): the digits of every
+    scalar < L sum back to it, and each indexes an existing entry of its table position -- for
+    the long-top radix-2^21 layout (Tab<21>: 12 positions, the top one unsigned in [0, 2^21 + 1])
+    at the top of the range too, where 11 signed radix-2^21 digits alone cannot reach"""
+    rnd = random.Random(21)
+    edges = [0, 1, L - 1, L - 2, 2 ** 252, 2 ** 252 - 1, 2 ** 252 - 2 ** 231, 2 ** 252 - 2 ** 230,
+             2 ** 252 + 2 ** 124, (2 ** 231 - 1) * (2 ** 21 + 1), sum(1 << (21 * i + 20) for i in range(12)) % L,
+             sum(1 << (21 * i + 20) for i in range(11)), sum(1 << (21 * i + 19) for i in range(12)) % L]
+    scalars = edges + [rnd.randrange(L) for _ in range(300)] + [L - 1 - rnd.getrandbits(130) for _ in range(50)]
+    for wd, top_max in ((20, 1 << 19), (21, (1 << 21) + 1), (24, 1 << 23), (26, 1 << 25)):
+        for mode in (0, 1):
+            for x in scalars:
+                out = (ctypes.c_int32 * 16)()
+                n = emu.emu_digits(wd, w(x), mode, out)
+                d = list(out[:n])
+                assert sum(di << (wd * i) for i, di in enumerate(d)) == x, (wd, mode, hex(x))
+                half = 1 << (wd - 1)
+                for i, di in enumerate(d[:-1]):
+                    assert -half <= di < half, (wd, i, di)
+                if wd == 21:
+                    assert n == 12 and 0 <= d[-1] <= top_max, (hex(x), d[-1])
+                else:
+                    assert n == -(-256 // wd) and -half <= d[-1] <= top_max

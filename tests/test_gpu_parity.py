@@ -265,16 +265,21 @@ def test_window_policy_and_parity(oracle_lib, budget_mb, exp_w):
         ctx2.close()
 
 
-@pytest.mark.parametrize("table_w,base_w", [(16, 20), (16, 24), (12, 24), (14, 24), (18, 24), (20, 24), (16, 26),
-                                            (18, 26), (20, 26)])
-def test_wide_base_table_parity(oracle_lib, table_w, base_w):
-    """Radix-2^20 / 2^24 / 2^26 base-point tables (0.9 / 11.8 / 43 GB) over radix-2^12..2^20
-    validator tables: the same verdicts as the oracle on valid and corrupted votes."""
+@pytest.mark.parametrize("table_w,base_w,lane_votes,n_votes",
+                         [(16, 20, 0, 800), (16, 24, 0, 800), (12, 24, 0, 800), (14, 24, 0, 800), (18, 24, 0, 800),
+                          (20, 24, 0, 800), (16, 26, 0, 800), (18, 26, 0, 800), (20, 26, 0, 800),
+                          (21, 26, 0, 800), (21, 26, 1, 3000), (21, 26, 4, 3000), (21, 26, 8, 20000)])
+def test_wide_base_table_parity(oracle_lib, table_w, base_w, lane_votes, n_votes):
+    """Radix-2^20 / 2^24 / 2^26 base-point tables (0.9 / 11.8 / 43 GB) over radix-2^12..2^21
+    validator tables (21: the 12-position long-top layout, through the split, 4-vote and
+    8-vote work-stealing K1b kernels): the same verdicts as the oracle on valid and corrupted
+    votes."""
     import txflow_amd as T
-    ctx = T.Context(max_batch=1 << 14, max_txs=1 << 12, max_validators=16, table_w=table_w, base_w=base_w)
+    ctx = T.Context(max_batch=1 << 15, max_txs=1 << 12, max_validators=16, table_w=table_w, base_w=base_w,
+                    lane_votes=lane_votes)
     try:
-        rnd = random.Random(base_w * 100 + table_w)
-        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 4, 800, rnd)
+        rnd = random.Random(base_w * 100 + table_w + lane_votes)
+        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 4, n_votes, rnd)
         assert (ctx.table_w, ctx.base_w) == (table_w, base_w)
         for i, v in enumerate(votes):
             if i % 3 == 1:
