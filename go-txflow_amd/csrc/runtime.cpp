@@ -112,6 +112,7 @@ struct Slot {
   uint8_t* d_ev_flag = nullptr;
   uint8_t* d_mark = nullptr;
   uint32_t* d_stamped = nullptr;   // the batch's stamped set ids (tally_resolve -> tally_cross)
+  uint64_t* d_ev_tiles = nullptr;  // look-back words of the event compaction (zeroed once: stamp-tagged)
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
@@ -397,8 +398,9 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc(c, &s.h_vcode, npad)) || (r = dalloc(c, &s.d_vcode, npad)) ||
       (r = dalloc(c, &s.d_entry, npad)) || (r = dalloc(c, &s.d_blk, nblk)) ||
       (r = dalloc(c, &s.d_ev_flag, npad)) || (r = dalloc(c, &s.d_mark, npad)) || (r = dalloc(c, &s.d_stamped, npad)) || (r = halloc_mapped(c, &s.h_ev, &s.m_ev, npad)) ||
-      (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)))
+      (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)) || (r = dalloc(c, &s.d_ev_tiles, nblk)))
     return r;
+  HIP_TRY(c, hipMemset(s.d_ev_tiles, 0, nblk * sizeof(uint64_t)));   // epoch 0: no stamp matches
   s.flow_cap = cap;
   return TXV_OK;
 }
@@ -886,7 +888,7 @@ FlowBatch flow_batch(const txv_ctx* c, const Slot& s) {
   b.vcode = s.host_val ? s.d_vcode : nullptr;
   b.sig = s.d_sig; b.msg_len = s.d_msg_len; b.val = s.d_val; b.flags = s.d_flags; b.pre = s.d_pre;
   b.entry = s.d_entry; b.set = s.d_set; b.ok = s.d_ok; b.status = s.d_status;
-  b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk; b.stamped = s.d_stamped;
+  b.ev_flag = s.d_ev_flag; b.mark = s.d_mark; b.blk = s.d_blk; b.stamped = s.d_stamped; b.ev_tiles = s.d_ev_tiles;
   b.status_host = s.m_out; b.ev_host = s.m_ev; b.summary_host = s.m_sum;
   return b;
 }
@@ -1393,7 +1395,7 @@ void txv_destroy(txv_ctx* c) {
     hfree(s.h_status); hfree(s.h_out);
     hfree(s.h_addr); dfree(s.d_addr); hfree(s.h_addr_len); dfree(s.d_addr_len); hfree(s.h_sigraw); dfree(s.d_sigraw);
     hfree(s.h_sig_len); dfree(s.d_sig_len); hfree(s.h_nil); dfree(s.d_nil); hfree(s.h_txkey); dfree(s.d_txkey); hfree(s.h_vcode); dfree(s.d_vcode);
-    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); dfree(s.d_stamped); hfree(s.h_ev); hfree(s.h_sum);
+    dfree(s.d_entry); dfree(s.d_blk); dfree(s.d_ev_flag); dfree(s.d_mark); dfree(s.d_stamped); dfree(s.d_ev_tiles); hfree(s.h_ev); hfree(s.h_sum);
     hfree(s.h_fh); hfree(s.h_fs); hfree(s.h_fn); hfree(s.h_fo); hfree(s.h_fl); hfree(s.h_arena);
     dfree(s.d_fh); dfree(s.d_fs); dfree(s.d_fn); dfree(s.d_fo); dfree(s.d_fl); dfree(s.d_arena_th);
     for (auto& e : s.ev) if (e) (void)hipEventDestroy(e);

@@ -101,7 +101,7 @@ struct FlowCounters {           // device-resident, updated by the kernels
   uint32_t err;                 // TXV_FERR_*
   uint32_t n_stamped;           // sets the running batch ADDED a vote to (zeroed by tally_min)
   uint32_t n_digested;          // sets [0, n_digested) have set_digest (computed by the pack's digest pass)
-  uint32_t pad_;
+  uint32_t ev_ticket;           // event-compaction tiles taken by the running batch (zeroed by tally_min)
   uint64_t key_used;            // overflow key arena bytes in use
 };
 
@@ -183,6 +183,8 @@ struct FlowBatch {
   uint8_t* mark;                // [n] set by tally_min when a smaller arrival index took this vote's cell
   uint32_t* blk;                // scan scratch: [ceil(n / 1024) + 1]
   uint32_t* stamped;            // [n] ids of the sets this batch ADDED votes to (the crossing step's work list)
+  uint64_t* ev_tiles;           // [ceil(n / 1024)] look-back words of the event compaction (tagged with the
+                                // stamp, so never cleared)
   // outputs in mapped host memory
   uint8_t* status_host;         // [n]
   FlowEvent* ev_host;           // [n]
