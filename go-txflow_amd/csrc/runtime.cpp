@@ -3198,8 +3198,10 @@ struct PoolDev {
   uint32_t* h_clen = nullptr;
   hipEvent_t ev = nullptr;
   hipStream_t st = nullptr;                        // cache uploads / downloads
-  bool on_key = false;                             // batches run on the context's key stream
-  void quiesce() {                                 // every batch enqueued has ended (on_key: not on st)
+  int on_ctx = 0;                                  // batches run on a context stream: 2 key, 3 copy (0: st)
+  hipStream_t last_ks = nullptr;                   // the stream of the last batch enqueued, and its end
+  hipEvent_t last_ev = nullptr;
+  void quiesce() {                                 // every batch enqueued has ended (on_ctx: not on st)
     for (Flight& f : fl)
       if (f.ev) (void)hipEventSynchronize(f.ev);
   }
@@ -3276,9 +3278,10 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     // normal one 44-88M, the key stream 97-103M -- a fifth queue beside the context's four is
     // time-sliced by the hardware scheduler, and every launch of the engine's chain waits for it.
     // TXV_POOL_STREAM (experiment): 0 own high-priority stream, 1 own normal-priority stream,
-    // 2 (default) the key stream; the engine's own stream serves its synchronous uploads either way
+    // 2 (default) the key stream, 3 the copy stream; the engine's own stream serves its synchronous
+    // uploads either way
     static const int mode = getenv("TXV_POOL_STREAM") ? atoi(getenv("TXV_POOL_STREAM")) : 2;
-    s->on_key = mode == 2;
+    s->on_ctx = (mode == 2 || mode == 3) ? mode : 0;
     if (mode == 0) {
       int lo = 0, hi = 0;
       HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -3509,6 +3512,11 @@ void pooldev_result(const PoolDev* s, int slot, int64_t res[4]) {
   res[0] = (int64_t)ac; res[1] = (int64_t)ab; res[2] = (int64_t)rc; res[3] = (int64_t)rb;
 }
 
+// the stream the engine's batches run on
+hipStream_t engine_stream(txv_ctx* c, const PoolDev* s) {
+  return s->on_ctx == 2 ? c->key_stream : s->on_ctx == 3 ? c->copy_stream : s->st;
+}
+
 // n votes of a txv_votes batch into flight f's entries [off, off + n): signatures uploaded -- from
 // caller memory registered with txv_host_register (which must stay valid until the finish) or
 // through the slot's pinned staging -- on the context's copy stream (the DMA does not hold up the
@@ -3551,7 +3559,7 @@ int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_vote
   HIP_TRY(c, hipSetDevice(c->device));
   if (!v->n) return TXV_OK;
   if ((uint64_t)off + v->n > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
-  return upload_votes(c, s->fl[slot], s->on_key ? c->key_stream : s->st, v, off, v->n, h_sizes, false);
+  return upload_votes(c, s->fl[slot], engine_stream(c, s), v, off, v->n, h_sizes, false);
 }
 
 // one batch's decisions enqueued on the engine's stream into flight slot `slot` (whose previous
@@ -3573,7 +3581,16 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (total > s->cap_n) { c->err = "pool device batch above its capacity"; return TXV_ECAPACITY; }
   if (2 * ((uint64_t)s->C + total) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
   PoolDev::Flight& f = s->fl[slot];
-  hipStream_t ks = s->on_key ? c->key_stream : s->st;
+  hipStream_t ks = engine_stream(c, s);
+  // batches whose keys are already in HBM (the wire ingest: decoded on the key stream, which also
+  // carries the batches' prep and SignBytes) run on the copy stream, which the wire path leaves to
+  // the Update uploads: C5 from wire bytes 74-76M vs 56-71M votes/s, while the SoA path's batches
+  // (uploaded on the copy stream) stay on the key stream (93M there vs 130M, profiles/r05/pstream).
+  // TXV_POOL_DEV_STREAM=2 (experiment) keeps them on the key stream.
+  static const int dev_stream = getenv("TXV_POOL_DEV_STREAM") ? atoi(getenv("TXV_POOL_DEV_STREAM")) : 3;
+  if (!v && !h_keys_in && d_keys && n && dev_stream == 3 && s->on_ctx == 2) ks = c->copy_stream;
+  // each batch reads the cache and pool list the previous one wrote, on whichever stream it ran
+  if (s->last_ks && s->last_ks != ks) HIP_TRY(c, hipStreamWaitEvent(ks, s->last_ev, 0));
   if (after) HIP_TRY(c, hipStreamWaitEvent(ks, after, 0));   // device-resident inputs: their producer first
   if (v) {   // the batch's votes beside the staged ones, every signature keyed by one launch
     if (n) {
@@ -3652,6 +3669,8 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (keys_back && d_keys == f.d_keys && v && n)
     HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys + (size_t)n_upd * 8, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
   HIP_TRY(c, hipEventRecord(f.ev, ks));
+  s->last_ks = ks;
+  s->last_ev = f.ev;
   return TXV_OK;
 }
 
