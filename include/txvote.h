@@ -114,12 +114,14 @@ typedef struct {
 /* verify with radix-16 tables (B staged in LDS, 74 KB/validator) instead of the wider
  * L2/HBM-resident tables */
 #define TXV_CFG_TABLE_W4 0x1u
-/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18 or 20; 0 = auto: the
- * largest whose n_vals tables fit table_budget_mb, radix-2^20 for <= 137 validators): per
- * validator 74 KB / 0.5 MB / 1.7 MB / 5.8 MB / 20 MB / 67 MB / 252 MB / 872 MB (128-byte entries).
- * Windows >= 12 run against the 11.8 GB radix-2^24 base-point table: 10 + ceil(256/W) point
- * additions per verified vote (32 / 29 / 26 / 25 / 23 at W = 12..20; the first B entry is the
- * starting point); W = 4 / 8 / 10: 2 * ceil(256/W) - 1 = 127 / 63 / 51 */
+/* explicit fixed-base window in bits 8-15 (4, 8, 10, 12, 14, 16, 18, 20 or 21; 0 = auto: the
+ * largest of 8..20 whose n_vals tables fit table_budget_mb, radix-2^20 for <= 137 validators): per
+ * validator 74 KB / 0.5 MB / 1.7 MB / 5.8 MB / 20 MB / 67 MB / 252 MB / 872 MB / 1.70 GB (128-byte
+ * entries).  Windows >= 12 run against the 11.8 GB radix-2^24 base-point table: 10 + ceil(256/W)
+ * point additions per verified vote (32 / 29 / 26 / 25 / 23 at W = 12..20; the first B entry is
+ * the starting point); W = 4 / 8 / 10: 2 * ceil(256/W) - 1 = 127 / 63 / 51.  W = 21 (on request
+ * only; 12 positions over the 253 bits a scalar below L needs, the top one unsigned) runs against
+ * the radix-2^26 base table: 9 + 12 = 21 additions (bench.py's C2 context) */
 #define TXV_CFG_WINDOW(flags) (((flags) >> 8) & 0xFFu)
 #define TXV_CFG_SET_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 8)
 /* votes per lane sharing one field inversion in the W >= 8 verify kernel, bits 16-19:
@@ -130,8 +132,9 @@ typedef struct {
 #define TXV_CFG_SET_LANE_VOTES(v) (((uint32_t)(v) & 0xFu) << 16)
 /* base-point (B) table window, bits 20-27: 0 = auto (radix-2^24, 11.8 GB, over radix-2^12..2^20
  * validator tables; else the validator window; one table per process and device, shared by its
- * contexts); 24 over windows 12..20; 26 (43 GB, 10 additions for [s]B instead of 11) over windows
- * 16..20; 20 / 22 over window 16 (0.9 / 3.2 GB, 13 / 12 additions); or equal to the window */
+ * contexts; radix-2^26 by default under window 21); 24 over windows 12..20; 26 (43 GB, 10
+ * additions for [s]B instead of 11) over windows 16..21; 20 / 22 over window 16 (0.9 / 3.2 GB,
+ * 13 / 12 additions); or equal to the window */
 #define TXV_CFG_B_WINDOW(flags) (((flags) >> 20) & 0xFFu)
 #define TXV_CFG_SET_B_WINDOW(w) (((uint32_t)(w) & 0xFFu) << 20)
 
