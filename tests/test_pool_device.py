@@ -399,3 +399,69 @@ def test_device_pool_list_compaction_and_round_trips(dev_ctx, cache):
         assert 10000 < pool.Size() < 100000
     finally:
         pool.close()
+
+
+@pytest.mark.gpu
+def test_device_cache_wire_and_soa_batches_interleaved():
+    """The wire ingest's CheckTx batches (keys decoded into HBM: the engine runs them on the copy
+    stream) interleaved with SoA batches (keys hashed from uploaded signatures: on the key stream)
+    and Updates staged between them, on one device-cache pool: every batch's pool statuses, Size,
+    TxsBytes and the LRU order equal the oracle pool's fed the same calls in the same order
+    (txvotepool.go:187-261, :329-359)"""
+    import hashlib
+    import random
+
+    import txflow_amd as T
+    from test_pool import _batch, vote
+    rnd = random.Random(90)
+    ctx = T.Context(max_batch=1 << 13, max_txs=1024, max_validators=8)
+    try:
+        seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(4)]
+        pubs = ctx.keygen(seeds)
+        ctx.set_validators(pubs, [1, 1, 1, 1], "test_chain_id")
+        addrs, _ = ctx.validator_info()
+        cfg = dict(size=1 << 20, cache_size=3000)
+        pool = T.TxVotePool(ctx, **cfg, device_cache=True)
+        ref = O.Pool(**cfg)
+        hashes = [hashlib.sha256(b"mix%d" % t).hexdigest().upper().encode() for t in range(24)]
+        hist = []
+
+        def fresh(n):
+            out = []
+            for _ in range(n):
+                if hist and rnd.random() < 0.1:
+                    out.append(dict(hist[rnd.randrange(len(hist))]))      # a replay, near or far
+                else:
+                    out.append(vote(rnd.randbytes(64), txhash=rnd.choice(hashes), ts=(1_700_000_000, 1 + len(hist)),
+                                    addr=addrs[rnd.randrange(4)]))
+                hist.append(out[-1])
+            return out
+
+        for b in range(8):
+            votes = fresh(1500)
+            if b % 2 == 0:                                   # the wire ingest
+                wire = [O.wire_encode(v["height"], v["txhash"], v["ts_sec"], v["ts_nanos"], v["addr"], v["sig"])
+                        for v in votes]
+                ws, ps, fs, ev = pool.ingest(T.WireBatch(wire))
+                assert (ws == T.WIRE_OK).all()
+            else:                                            # SoA, submitted then waited
+                bt, ls = _batch(T, votes)
+                ps = pool.check_wait(pool.check_submit(bt, ls))
+            exp = ref.check(votes)
+            assert np.array_equal(ps, exp), (b, np.nonzero(ps != exp)[0][:10])
+            # the batch waited: the Update staged before it has been applied with it
+            assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes(), b
+            if b % 3 != 2:                                   # Update staged, applied with the next batch
+                committed = rnd.sample(hist, 300)
+                cb, clong = _batch(T, committed)
+                pool.update_submit(b + 1, cb, clong)
+                ref.update(b + 1, committed)
+        pool.sync()
+        assert pool.Size() == ref.size() and pool.TxsBytes() == ref.txs_bytes()
+        assert np.array_equal(pool.cache_keys(), ref.cache_keys())
+        gk, gs = pool.reap(-1)
+        ok, os_ = ref.reap(-1)
+        assert np.array_equal(gk, ok) and np.array_equal(gs, os_)
+        pool.close()
+    finally:
+        ctx.close()
