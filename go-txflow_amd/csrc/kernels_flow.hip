@@ -449,28 +449,6 @@ struct NewSetPred {
   }
 };
 
-// SHA-256 of len bytes at p (any alignment), big-endian state words
-__device__ void sha256_bytes_dev(const uint8_t* p, uint32_t len, uint32_t st[8]) {
-  txv::sha256_init(st);
-  const uint32_t nblk = (len + 9 + 63) / 64;
-  for (uint32_t blk = 0; blk < nblk; ++blk) {
-    uint32_t w[16];
-    for (int t = 0; t < 16; ++t) {
-      const uint32_t off = blk * 64 + 4u * (uint32_t)t;
-      uint32_t v = 0;
-      for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t o = off + q;
-        const uint32_t byte = o < len ? (uint32_t)p[o] : (o == len ? 0x80u : 0u);
-        v = (v << 8) | byte;
-      }
-      if (blk == nblk - 1 && t == 14) v = len >> 29;
-      if (blk == nblk - 1 && t == 15) v = len << 3;
-      w[t] = v;
-    }
-    txv::sha256_block(st, w);
-  }
-}
-
 // the vote that first carried a new TxHash: number its set (first-seen order), move the key
 // bytes into the set's key slot (or the overflow arena), record the set's TxKey
 // (service.go:201-207); its exchange name comes later, from the pack's digest pass
@@ -911,7 +889,7 @@ __global__ void __launch_bounds__(256) txv_k_status_events(FlowState fs, FlowBat
     f[k] = b.ev_flag[i] != 0;
   }
   uint32_t rank[4], total;
-  tile_scan(f, rank, b.ev_tiles, tile, b.stamp, &total);
+  tile_scan(f, rank, b.ev_tiles, tile, b.stamp, &fs.ctr->err, TXV_FERR_LOOKBACK, &total);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (!f[k]) continue;
@@ -927,7 +905,8 @@ __global__ void __launch_bounds__(256) txv_k_status_events(FlowState fs, FlowBat
     sm.n_sets = fs.ctr->n_sets;
     sm.n_events = total;
     sm.arena_used = min(fs.ctr->arena_used, fs.max_accepted);
-    sm.err = fs.ctr->err;
+    // (a tile that timed out in its look-back or-ed its bit in before it published its word)
+    sm.err = __hip_atomic_load(&fs.ctr->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sm.key_used = fs.ctr->key_used;
     *b.summary_host = sm;
   }
@@ -1045,7 +1024,7 @@ __global__ void __launch_bounds__(256) txv_k_digest(FlowState fs, uint32_t n_cap
   if (id >= min(fs.ctr->n_sets, n_cap)) return;
   const SetEntry& e = fs.tab[fs.set_entry[id]];
   uint32_t h[8];
-  sha256_bytes_dev(fs.keys + (e.key_off - 1), e.len, h);
+  txv::sha256_bytes(fs.keys + (e.key_off - 1), e.len, h);
 #pragma unroll
   for (int j = 0; j < 4; ++j) fs.set_digest[(size_t)id * 4 + j] = __builtin_bswap32(h[j]);   // bytes in order
 }

@@ -5,6 +5,7 @@
 // Verify anyway but still occupy pool/cache entries, so their keys must be exact).
 #include "sha2.h"
 #include "txv_device.h"
+#include "txv_hash.h"
 #include "lookback.h"
 
 using namespace txv;
@@ -85,13 +86,20 @@ __device__ __forceinline__ bool key_eq2(const uint32_t* ka, uint32_t a, const ui
   return ((x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) | (x1.y ^ y1.y) |
           (x1.z ^ y1.z) | (x1.w ^ y1.w)) == 0;
 }
-// the index's hash (a key slice the sort does not use): keys are SHA-256 outputs
-__device__ __forceinline__ uint32_t idx_hash(const uint32_t* k) { return k[5] ^ (k[6] * 0x9E3779B1u); }
+// Every placement of a key -- the cache index, the pool list's index, the sort slice that groups
+// a batch's repeats -- goes through txv_hash::key32 under the engine's secret seed (a different
+// derived seed each), never through a raw key slice: the keys are SHA-256 of peer-supplied
+// signature bytes that CheckTx never verifies (txvotepool.go:467-469), so a peer could grind keys
+// onto one home slot or one sort slice and make every probe or run scan of the batch quadratic.
+constexpr uint64_t kSeedIdx = 0x243F6A8885A308D3ull, kSeedList = 0x13198A2E03707344ull, kSeedSort = 0xA4093822299F31D0ull;
+__device__ __forceinline__ uint32_t idx_hash(const uint32_t* k, uint64_t seed) {
+  return (uint32_t)txv_hash::key32(k, seed ^ kSeedIdx);
+}
 
 // position of key (keys + 8 * i) in the cache (ck / ci of length L), or -1
 __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t* ci, uint32_t icap,
-                                              const uint32_t* keys, uint32_t i) {
-  uint32_t s = idx_hash(keys + (size_t)i * 8) & (icap - 1);
+                                              const uint32_t* keys, uint32_t i, uint64_t seed) {
+  uint32_t s = idx_hash(keys + (size_t)i * 8, seed) & (icap - 1);
   for (uint32_t probe = 0; probe < icap; ++probe, s = (s + 1) & (icap - 1)) {
     const uint32_t v = ci[s];
     if (!v) return -1;
@@ -101,12 +109,18 @@ __device__ __forceinline__ int32_t cache_find(const uint32_t* ck, const uint32_t
 }
 
 constexpr uint32_t kTile = kLookbackTile;
-// the sort key: a 24-bit key slice (three radix passes; equal slices are told apart by the full
-// key inside their run), the non-pushes on the value above every push's
+// the sort key: a 24-bit slice of the key's seeded hash (three radix passes; equal slices are told
+// apart by the full key inside their run, and only repeats of one key or a chance collision share
+// a run), the non-pushes on the value above every push's
 constexpr uint32_t kSliceBits = 24, kSliceNone = (1u << kSliceBits) - 1;
+__device__ __forceinline__ uint32_t sort_slice(const uint32_t* k, uint64_t seed) {
+  return (uint32_t)(txv_hash::key32(k, seed ^ kSeedSort) >> (64 - kSliceBits));
+}
 
 // ---- the pool list in HBM (pool_dev.h PoolListArgs) ----
-__device__ __forceinline__ uint32_t list_home(const uint32_t* k) { return k[4] ^ (k[7] * 0x9E3779B1u); }
+__device__ __forceinline__ uint32_t list_home(const uint32_t* k, uint64_t seed) {
+  return (uint32_t)txv_hash::key32(k, seed ^ kSeedList);
+}
 __device__ __forceinline__ unsigned long long list_slot(uint32_t tag, uint32_t low) {
   return ((unsigned long long)tag << 32) | low;
 }
@@ -123,10 +137,11 @@ __device__ __forceinline__ bool list_key_eq(const uint32_t* lk, uint32_t e, cons
 // txsMap.Store(key, pos): insert, or -- the key indexed already (a vote admitted twice, the
 // earlier one still in the list) -- the later position stays indexed, as the sequential Stores
 // leave it; the other entry stays in the list, unindexed
-__device__ void list_insert(unsigned long long* li, uint32_t imask, const uint32_t* lk, uint32_t pos, const uint32_t k[8]) {
+__device__ void list_insert(unsigned long long* li, uint32_t imask, const uint32_t* lk, uint32_t pos, const uint32_t k[8],
+                            uint64_t seed) {
   const uint32_t tg = k[3];
   const unsigned long long mine = list_slot(tg, pos + 1);
-  uint32_t s = list_home(k) & imask;
+  uint32_t s = list_home(k, seed) & imask;
   for (uint32_t probe = 0; probe <= imask; ++probe, s = (s + 1) & imask) {
     unsigned long long v = slot_load(li + s);
     if (v == 0) {
@@ -166,7 +181,7 @@ __device__ bool list_remove(const PoolListArgs& l, const uint32_t* key) {
   const uint4 k0 = src[0], k1 = src[1];
   const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
   const uint32_t tg = k[3];
-  uint32_t s = list_home(k) & l.imask;
+  uint32_t s = list_home(k, l.seed) & l.imask;
   for (uint32_t probe = 0; probe <= l.imask; ++probe, s = (s + 1) & l.imask) {
     const unsigned long long v = slot_load(l.li + s);
     if (v == 0) return false;
@@ -221,12 +236,12 @@ __global__ void __launch_bounds__(256) pd_init(PoolDevArgs a) {
     a.push[i] = p;
     // non-pushes sort into a run of their own at the end: a push's slice is clamped below it, so a
     // key whose slice is 0xFFFFFFFF never shares a run with them (pd_link scans its run backwards)
-    a.hkey[i] = p ? min(a.keys[(size_t)i * 8 + 2] >> 8, kSliceNone - 1) : kSliceNone;
+    a.hkey[i] = p ? min(sort_slice(a.keys + (size_t)i * 8, a.seed), kSliceNone - 1) : kSliceNone;
     a.hidx[i] = i;
     a.last[i] = p;          // cleared by pd_link for a push with a later push of its key
   }
   uint32_t r[4];
-  tile_scan(f, r, a.tiles, tile, a.epoch);
+  tile_scan(f, r, a.tiles, tile, a.epoch, a.err, 1u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
@@ -262,7 +277,7 @@ __global__ void __launch_bounds__(256) pd_link(PoolDevArgs a) {
   }
   const uint64_t C = a.C, L0 = a.C ? *a.clen : 0, na = n_pushes(a);
   if (pj < 0 && C && L0) {
-    cr = cache_find(a.ck_old, a.ci_old, a.icap, a.keys, i);
+    cr = cache_find(a.ck_old, a.ci_old, a.icap, a.keys, i, a.seed);
     if (cr >= 0) a.detached[cr] = 1;
   }
   const bool cache_on = C != 0, evict = cache_on && L0 + na > C;
@@ -384,7 +399,7 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
     }
   }
   uint32_t r[4];
-  tile_scan(f, r, old ? a.tiles + 2 * (size_t)nt : a.tiles + nt, tile, a.epoch);
+  tile_scan(f, r, old ? a.tiles + 2 * (size_t)nt : a.tiles + nt, tile, a.epoch, a.err, 1u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
@@ -397,7 +412,7 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
     const uint32_t i = tile * kTile + 256u * k + threadIdx.x;
     f[k] = i < a.n && i >= a.n_force && a.status[i] == TXV_POOL_OK;   // written by this thread above
   }
-  tile_scan(f, r, a.tiles + 2 * (size_t)nt + (a.C + kTile - 1) / kTile, tile, a.epoch);
+  tile_scan(f, r, a.tiles + 2 * (size_t)nt + (a.C + kTile - 1) / kTile, tile, a.epoch, a.err, 1u);
   // addTx (txvotepool.go:265-270), in arrival order: txs.PushBack at tail + rank (txsMap.Store
   // follows in pd_newcache, a launch of its own: a duplicate's key compare reads an entry another
   // block wrote, which only a launch boundary makes visible across XCDs without a fence per vote)
@@ -432,7 +447,7 @@ __device__ __forceinline__ void list_index_vote(const PoolDevArgs& a, uint32_t i
   const uint4* src = reinterpret_cast<const uint4*>(a.keys + (size_t)i * 8);
   const uint4 k0 = src[0], k1 = src[1];
   const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-  list_insert(a.l.li, a.l.imask, a.l.lk, pos, k);
+  list_insert(a.l.li, a.l.imask, a.l.lk, pos, k, a.l.seed);
 }
 
 __device__ __forceinline__ void cache_put(const PoolDevArgs& a, uint32_t q, const uint4* s) {
@@ -440,7 +455,8 @@ __device__ __forceinline__ void cache_put(const PoolDevArgs& a, uint32_t q, cons
   uint4* d = reinterpret_cast<uint4*>(a.ck_new + (size_t)q * 8);
   d[0] = x0;
   d[1] = x1;
-  uint32_t h = (x1.y ^ (x1.z * 0x9E3779B1u)) & (a.icap - 1);          // idx_hash: words 5, 6
+  const uint32_t k[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  uint32_t h = idx_hash(k, a.seed) & (a.icap - 1);
   while (atomicCAS(&a.ci_new[h], 0u, q + 1u) != 0u) h = (h + 1) & (a.icap - 1);
 }
 
@@ -467,6 +483,7 @@ __global__ void __launch_bounds__(256) pd_newcache(PoolDevArgs a) {
   if (t == 0) {
     a.clen[0] = keep_old + keepU;
     a.tk[0] = 0;
+    if (const uint32_t e = *a.err) *a.err_host = e;   // (the scans ran in earlier launches)
   }
   if (a.list_on) list_index_vote(a, t);
 }
@@ -474,15 +491,19 @@ __global__ void __launch_bounds__(256) pd_newcache(PoolDevArgs a) {
 // nopTxCache: the list's index stores and pd_init's ticket counter reset
 __global__ void __launch_bounds__(256) pd_finish_nocache(PoolDevArgs a) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-  if (t == 0) a.tk[0] = 0;
+  if (t == 0) {
+    a.tk[0] = 0;
+    if (const uint32_t e = *a.err) *a.err_host = e;
+  }
   if (a.list_on) list_index_vote(a, t);
 }
 
 // an index over keys [L][8] (a cache uploaded from the host)
-__global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap) {
+__global__ void __launch_bounds__(256) pd_index_only(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap,
+                                                     uint64_t seed) {
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   if (q >= L) return;
-  uint32_t s = idx_hash(ck + (size_t)q * 8) & (icap - 1);
+  uint32_t s = idx_hash(ck + (size_t)q * 8, seed) & (icap - 1);
   while (atomicCAS(&ci[s], 0u, q + 1u) != 0u) s = (s + 1) & (icap - 1);
 }
 
@@ -508,24 +529,24 @@ __global__ void __launch_bounds__(256) pl_move(const uint32_t* lk, const uint32_
 // the index over the moved entries: every indexed (non-tombstone) slot of the old index again at
 // its entry's new position (tombstones dropped; no key is compared: the keys are distinct)
 __global__ void __launch_bounds__(256) pl_reindex(const unsigned long long* oi, uint32_t oicap, const uint32_t* npos,
-                                                  const uint32_t* nk, unsigned long long* ni, uint32_t nmask) {
+                                                  const uint32_t* nk, unsigned long long* ni, uint32_t nmask, uint64_t seed) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   if (s >= oicap) return;
   const unsigned long long v = oi[s];
   if (v == 0 || (uint32_t)v == kListTomb) return;
   const uint32_t q = npos[(uint32_t)v - 1];
   const uint32_t* k = nk + (size_t)q * 8;
-  uint32_t t = list_home(k) & nmask;
+  uint32_t t = list_home(k, seed) & nmask;
   const unsigned long long mine = list_slot((uint32_t)(v >> 32), q + 1);
   while (atomicCAS(ni + t, 0ull, mine) != 0ull) t = (t + 1) & nmask;
 }
 // the index of a list uploaded from the host: the positions marked in ins (each key once)
 __global__ void __launch_bounds__(256) pl_index_up(const uint32_t* lk, const uint8_t* ins, uint32_t L,
-                                                   unsigned long long* li, uint32_t imask) {
+                                                   unsigned long long* li, uint32_t imask, uint64_t seed) {
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   if (q >= L || !ins[q]) return;
   const uint32_t* k = lk + (size_t)q * 8;
-  uint32_t t = list_home(k) & imask;
+  uint32_t t = list_home(k, seed) & imask;
   const unsigned long long mine = list_slot(k[3], q + 1);
   while (atomicCAS(li + t, 0ull, mine) != 0ull) t = (t + 1) & imask;
 }
@@ -573,10 +594,11 @@ extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
 }
 
 // the index of a cache uploaded from the host (keys already at ck, its length at clen[0])
-extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st) {
+extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, uint64_t seed,
+                                        hipStream_t st) {
   hipError_t e;
   if ((e = hipMemsetAsync(ci, 0, (size_t)icap * 4, st))) return e;
-  if (L) hipLaunchKernelGGL(pd_index_only, dim3((L + 255) / 256), dim3(256), 0, st, ck, L, ci, icap);
+  if (L) hipLaunchKernelGGL(pd_index_only, dim3((L + 255) / 256), dim3(256), 0, st, ck, L, ci, icap, seed);
   return hipGetLastError();
 }
 
@@ -595,7 +617,7 @@ extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* l
                                            const unsigned long long* li, uint32_t ocap, uint32_t oicap, uint32_t* nk,
                                            uint32_t* nsz, uint8_t* nfl, unsigned long long* ni, uint32_t ncap,
                                            uint32_t nicap, uint32_t* npos, void* tmp, size_t tmp_bytes,
-                                           uint32_t* tail_out, hipStream_t st) {
+                                           uint32_t* tail_out, uint64_t seed, hipStream_t st) {
   hipError_t e;
   hipcub::TransformInputIterator<uint32_t, AliveU32, const uint8_t*> it(lfl, AliveU32());
   if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, it, npos, (int)ocap, st))) return e;
@@ -603,15 +625,15 @@ extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* l
   hipLaunchKernelGGL(pl_move, dim3((span + 255) / 256), dim3(256), 0, st, lk, lsz, lfl, npos, ocap, nk, nsz, nfl, ncap,
                      tail_out);
   if ((e = hipMemsetAsync(ni, 0, (size_t)nicap * 8, st))) return e;
-  hipLaunchKernelGGL(pl_reindex, dim3((oicap + 255) / 256), dim3(256), 0, st, li, oicap, npos, nk, ni, nicap - 1);
+  hipLaunchKernelGGL(pl_reindex, dim3((oicap + 255) / 256), dim3(256), 0, st, li, oicap, npos, nk, ni, nicap - 1, seed);
   return hipGetLastError();
 }
 
 // a list of L entries uploaded from the host (keys / sizes at lk / lsz): flags, index
 extern "C" hipError_t txv_poollist_upload_index(const uint32_t* lk, const uint8_t* ins, uint32_t L,
-                                                unsigned long long* li, uint32_t icap, hipStream_t st) {
+                                                unsigned long long* li, uint32_t icap, uint64_t seed, hipStream_t st) {
   hipError_t e;
   if ((e = hipMemsetAsync(li, 0, (size_t)icap * 8, st))) return e;
-  if (L) hipLaunchKernelGGL(pl_index_up, dim3((L + 255) / 256), dim3(256), 0, st, lk, ins, L, li, icap - 1);
+  if (L) hipLaunchKernelGGL(pl_index_up, dim3((L + 255) / 256), dim3(256), 0, st, lk, ins, L, li, icap - 1, seed);
   return hipGetLastError();
 }

@@ -170,33 +170,7 @@ __global__ void __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu
 // (txv_ingest_msgs: Reactor.Receive -> TxVotePool.CheckTxWithInfo -> TxFlow.TryAddVote without
 // the decoded records leaving HBM)
 
-namespace {
-
-// SHA-256 of n bytes at p (any alignment; the wire buffer is padded behind its last message)
-__device__ void sha256_bytes(const uint8_t* p, uint32_t n, uint32_t st[8]) {
-  txv::sha256_init(st);
-  const uint32_t nblk = (n + 9 + 63) / 64;       // message + 0x80 + 8-byte length
-  for (uint32_t b = 0; b < nblk; ++b) {
-    uint32_t w[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t k = 64u * b + 4u * (uint32_t)t + (uint32_t)q;   // byte index in the padded message
-        uint32_t byte = 0;
-        if (k < n) byte = p[k];
-        else if (k == n) byte = 0x80u;
-        v = (v << 8) | byte;
-      }
-      w[t] = v;
-    }
-    if (b == nblk - 1) { w[14] = (uint32_t)((uint64_t)n >> 29); w[15] = n << 3; }
-    txv::sha256_block(st, w);
-  }
-}
-
-}  // namespace
+// (txv::sha256_bytes, sha2.h: the wire buffer is padded behind its last message)
 
 // Per decoded message (records of txv_k_decode_msgs): its wire status, and for the decoded ones
 // txVoteKey = SHA-256(Signature) (txvotepool/txvotepool.go:467-469: the first 64 bytes come from
@@ -235,7 +209,7 @@ __global__ void __launch_bounds__(256) txv_k_rec_keys(const uint32_t* __restrict
       txv::sha256_block(st, w);
     }
   } else {
-    sha256_bytes(wire + r[9], sl, st);
+    txv::sha256_bytes(wire + r[9], sl, st);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) keys[(size_t)i * 8 + j] = txv::bswap32(st[j]);

@@ -23,8 +23,12 @@ __device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint32_t flag, uin
 // 128-tile chain wait ~100 dependent loads).  The value travels inside the 8-byte word, so relaxed
 // agent-scope atomics on both sides carry it across XCDs (sc1 stores and loads): no release /
 // acquire fence, which would write back or invalidate the whole XCD L2 per tile
-// (MI355X_MICROARCH.md, inter-workgroup visibility)
-__device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, uint32_t agg) {
+// (MI355X_MICROARCH.md, inter-workgroup visibility).  A predecessor that never publishes (a broken
+// invariant: a stale tag, a ticket left unreset by a failed launch) ends the wait after 2^22 spins
+// with err_val or-ed into *err (a sticky device word the host learns of: the batch fails loudly
+// instead of carrying a partial prefix), before this tile publishes its own word.
+__device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, uint32_t agg, uint32_t* err,
+                                  uint32_t err_val) {
   const int lane = threadIdx.x & 63;
   const uint32_t ep = epoch & 0x3FFFFFFFu;
   if (tile == 0) {
@@ -46,7 +50,13 @@ __device__ uint32_t tile_lookback(uint64_t* st, uint32_t tile, uint32_t epoch, u
     if ((okm & need) != need) {
       // a predecessor's block is running (tickets are taken at block start): it publishes within
       // microseconds; the bound only keeps a broken invariant from hanging the queue
-      if (++spins > (1u << 22)) break;
+      if (++spins > (1u << 22)) {
+        if (lane == 0 && err) {
+          __hip_atomic_fetch_or(err, err_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __threadfence();
+        }
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
@@ -70,7 +80,7 @@ __device__ __forceinline__ uint32_t take_tile(uint32_t* tk) {
 // exclusive ranks of the 4 flags of each thread in item order, plus the tile's exclusive prefix;
 // *incl (optional) = the inclusive count through this tile, in every thread
 __device__ __forceinline__ void tile_scan(const bool f[4], uint32_t out[4], uint64_t* st, uint32_t tile, uint32_t epoch,
-                                          uint32_t* incl = nullptr) {
+                                          uint32_t* err, uint32_t err_val, uint32_t* incl = nullptr) {
   __shared__ uint32_t cnt[4][4];
   __shared__ uint32_t s_prefix;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -95,7 +105,7 @@ __device__ __forceinline__ void tile_scan(const bool f[4], uint32_t out[4], uint
     run += round;
   }
   if (w == 0) {                                      // wave 0 looks back (run is block-uniform)
-    const uint32_t pre = tile_lookback(st, tile, epoch, run);
+    const uint32_t pre = tile_lookback(st, tile, epoch, run, err, err_val);
     if (lane == 0) s_prefix = pre;
   }
   __syncthreads();

@@ -20,6 +20,8 @@
 // not restated.
 #include "../../include/txvote.h"
 #include "amino.hpp"
+#include "txv_hash.h"
+#include <random>
 
 #include <chrono>
 #include <condition_variable>
@@ -44,13 +46,19 @@ struct Key {
   uint8_t b[32];
   bool operator==(const Key& o) const { return memcmp(b, o.b, 32) == 0; }
 };
-struct KeyHash {
-  size_t operator()(const Key& k) const {   // SHA-256 output: any 8 bytes are uniform
-    uint64_t h;
-    memcpy(&h, k.b, 8);
-    return (size_t)(h ^ (h >> 29));
-  }
-};
+// Keys are SHA-256 of peer-supplied signature bytes that CheckTx never verifies
+// (txvotepool.go:467-469): a peer can grind signatures until their keys share any fixed slice, so
+// the host tables place keys by txv_hash::key32 under a secret per-process seed (an unseeded slice
+// let one peer's ground keys pile onto one home slot: every probe of a batch walks the cluster).
+uint64_t key_seed() {
+  static const uint64_t s = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x686f73746b657973ULL;
+  return s;
+}
+inline uint64_t key_hash(const Key& k, uint64_t salt) {
+  uint32_t w[8];
+  memcpy(w, k.b, 32);
+  return txv_hash::key32(w, key_seed() ^ salt);
+}
 
 // open-addressing index Key -> node of a KeyList (linear probing, backward-shift deletion, no
 // tombstones).  A slot is 8 bytes (32-bit hash tag + node index; the key itself is compared in
@@ -67,7 +75,7 @@ struct FlatIndex {
   ~FlatIndex() { free(t); }
   FlatIndex(const FlatIndex&) = delete;
   FlatIndex& operator=(const FlatIndex&) = delete;
-  static uint64_t h(const Key& k) { uint64_t v; memcpy(&v, k.b, 8); return v ^ (v >> 29); }
+  static uint64_t h(const Key& k) { return key_hash(k, 0); }
   static uint32_t tag(uint64_t hv) { return (uint32_t)(hv >> 32) | 1u; }
   // the home slot from the stored tag alone (the high bits of its Fibonacci hash: the partition
   // bits PartIndex takes from the same word are mixed in), so the backward-shift erase and the
@@ -490,7 +498,7 @@ constexpr uint32_t kAdmitAhead = 16;
 // The state is then written directly: the new LRU = the C most recent distinct keys, the pool list
 // = the admitted votes appended in order (txsMap.Store overwriting, as addTx does).
 
-uint64_t batch_tab_hash(const Key& k) { uint64_t v; memcpy(&v, k.b + 16, 8); return v ^ (v >> 31); }
+uint64_t batch_tab_hash(const Key& k) { return key_hash(k, 0x9e3779b97f4a7c15ULL); }
 
 bool batch_check(txv_pool* p, txv_ctx* ctx, BatchScratch& S, const Key* keys, uint32_t n, uint8_t* status_out) {
   static const bool prof = getenv("TXV_PROFILE_HOST") != nullptr;

@@ -22,6 +22,7 @@ struct PoolListArgs {
   uint8_t* lfl;               // [cap] 1 = alive
   unsigned long long* li;     // [icap] index slots
   uint32_t imask;             // icap - 1
+  uint64_t seed;              // the engine's secret hash seed (list_home)
   const uint32_t* tail_in;    // the tail before the batch
   uint32_t* tail_out;         // the tail after it (the other word of the pair)
 };
@@ -46,7 +47,7 @@ struct PoolDevArgs {
   // scratch (n entries unless noted)
   uint32_t* push;             // 1 = reaches cache.Push
   uint32_t* aidx;             // exclusive scan of push: the push's index in S after the L0 cache entries
-  uint32_t* hkey;             // sort keys (a 24-bit slice of the key; non-pushes 0xFFFFFF)
+  uint32_t* hkey;             // sort keys (a 24-bit slice of the key's seeded hash; non-pushes 0xFFFFFF)
   uint32_t* hidx;             // 0..n-1
   uint32_t* skey;             // sorted
   uint32_t* sidx;
@@ -66,6 +67,9 @@ struct PoolDevArgs {
                               // [ceil(n/1024)] appends
   uint32_t* tk;               // [4] tile tickets (pd_init, pd_status n-chain, pd_status C-chain)
   uint32_t epoch;             // this batch's tag for the look-back words (30 bits)
+  uint64_t seed;              // the engine's secret hash seed (sort slice, cache index: kernels_pool.hip)
+  uint32_t* err;              // [1] sticky: 1 = a look-back scan timed out (a broken invariant)
+  uint32_t* err_host;         // [1] mapped: *err copied there by the chain's last launch
   uint32_t* okpos;            // [n] exclusive scan of the appended votes (list_on)
   uint64_t* res;              // (list_on) per 1024-vote tile (appended entries, their Size() sum), mapped
   uint64_t* res_rm;           // (list_on) per 1024-vote tile of [0, n_force): (removed entries, bytes), mapped

@@ -18,6 +18,7 @@
 #include "amino.hpp"
 #include "host_pack.hpp"
 #include "sha2.h"
+#include "route.h"
 
 #include <hip/hip_runtime.h>
 #include <emmintrin.h>
@@ -70,7 +71,8 @@ constexpr uint32_t kVcodeEmpty = TXV_VCODE_EMPTY, kVcodeUnknown = TXV_VCODE_UNKN
 constexpr uint32_t kHostValMin = 1u << 18;
 constexpr uint32_t kSignerSlot = 4, kVerifySlot = 5, kIngestSlot = 6;   // signer, verify-only, wire ingest ring (6-8)
 constexpr uint32_t kIngestRing = 3;
-constexpr uint32_t kSlots = kIngestSlot + kIngestRing;
+constexpr uint32_t kRouteSlot = kIngestSlot + kIngestRing;   // txv_route_admitted's columns
+constexpr uint32_t kSlots = kRouteSlot + 1;
 
 struct Slot {
   uint32_t cap = 0, n = 0, n_pad = 0, msg_words = 0, msg_cap_words = 0;
@@ -93,6 +95,7 @@ struct Slot {
   uint32_t *h_fo = nullptr, *h_fl = nullptr, *d_fo = nullptr, *d_fl = nullptr;     // txhash off / len
   uint8_t *h_arena = nullptr, *d_arena_th = nullptr;                               // TxHash arena
   size_t arena_cap = 0;
+  uint64_t arena_end = 0;          // the staged batch's TxHash arena extent
   uint32_t flow_cap = 0;           // capacity of the AddVote-only buffers below
   uint8_t *h_addr = nullptr, *d_addr = nullptr;            // [n][20]
   uint32_t *h_addr_len = nullptr, *d_addr_len = nullptr;
@@ -112,7 +115,8 @@ struct Slot {
   uint8_t* d_ev_flag = nullptr;
   uint8_t* d_mark = nullptr;
   uint32_t* d_stamped = nullptr;   // the batch's stamped set ids (tally_resolve -> tally_cross)
-  uint64_t* d_ev_tiles = nullptr;  // look-back words of the event compaction (zeroed once: stamp-tagged)
+  uint64_t* d_ev_tiles = nullptr;  // look-back words of the event compaction (stamp-tagged: zeroed per tag cycle)
+  uint32_t ev_tiles_n = 0;
   // results, written by the kernels straight into mapped host memory (m_* = device views)
   uint8_t* h_out = nullptr; uint8_t* m_out = nullptr;
   FlowEvent* h_ev = nullptr; FlowEvent* m_ev = nullptr;
@@ -244,6 +248,15 @@ struct txv_ctx {
   uint32_t n_signers = 0;
   uint32_t *d_sk_scal = nullptr, *d_sk_araw = nullptr, *d_sk_prefix = nullptr, *d_sk_pub = nullptr;
   Slot slots[kSlots];
+  // txv_route_admitted scratch (kernels_route.hip): per-vote shard, per-wave counts / bytes, per
+  // shard longest TxHash and totals, the metas in mapped memory; route_mu serialises route calls
+  std::mutex route_mu;
+  uint32_t route_n_cap = 0, route_w_cap = 0;
+  uint8_t* d_rshard = nullptr;
+  uint32_t *d_rw = nullptr, *d_rmax = nullptr;
+  uint64_t* d_rtot = nullptr;
+  txv_route_meta *h_rmeta = nullptr, *m_rmeta = nullptr;
+  hipEvent_t route_ev = nullptr;
   // txv_sig_keys scratch: signatures [n][16] u32, lengths, keys [n][8] u32
   uint32_t pk_cap = 0;
   std::mutex pk_mu;                  // txv_sig_keys' buffers (not c->mu: CheckTx's keys run beside txv_submit_votes)
@@ -401,6 +414,7 @@ int ensure_flow_slot(txv_ctx* c, Slot& s, uint32_t n) {
       (r = halloc_mapped(c, &s.h_sum, &s.m_sum, 1)) || (r = dalloc(c, &s.d_ev_tiles, nblk)))
     return r;
   HIP_TRY(c, hipMemset(s.d_ev_tiles, 0, nblk * sizeof(uint64_t)));   // epoch 0: no stamp matches
+  s.ev_tiles_n = (uint32_t)nblk;
   s.flow_cap = cap;
   return TXV_OK;
 }
@@ -717,10 +731,12 @@ inline bool txkey_spelled(const uint8_t* key, const uint8_t* hex) {
   return ok == 0xFFFF;
 }
 
-int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
-  if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+// route = true: the columns of a batch txv_route_admitted packs for the ranks (no TxFlow run: no
+// validator set needed, no sequence numbers taken, every address column uploaded)
+int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v, bool route = false) {
+  if (!route && !c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
   if (v->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
-  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+  if (!route && c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
   Slot& s = c->slots[slot];
   const uint32_t n = v->n;
   const uint32_t chain_len = (uint32_t)c->chain.size();
@@ -781,8 +797,11 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
   s.has_nil = v->is_nil != nullptr;
   s.has_txkey = v->txkey != nullptr;
-  s.seq_base = c->seq_next;
-  c->seq_next += n;
+  s.arena_end = ae;
+  if (!route) {
+    s.seq_base = c->seq_next;
+    c->seq_next += n;
+  }
   ht.mark("scan");
   struct Col { const uint8_t* src; uint8_t* pin; uint8_t* dev; size_t elem; bool reg; };
   Col cols[11];
@@ -798,8 +817,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v) {
   add((uniform >> kUHL & 1) ? nullptr : v->txhash_len, s.h_fl, s.d_fl, 4);
   // ValidatorSet.GetByAddress on the pack threads (the device's table, host_pack.hpp AddrTable):
   // a 2-byte code per vote crosses PCIe instead of the 20-byte address and its length
-  const bool host_val = (c->host_val == 1 || (c->host_val < 0 && n >= kHostValMin)) && v->addr && v->addr_len &&
-                        c->n_vals < kVcodeEmpty;
+  const bool host_val = !route && (c->host_val == 1 || (c->host_val < 0 && n >= kHostValMin)) && v->addr &&
+                        v->addr_len && c->n_vals < kVcodeEmpty;
   s.host_val = host_val;
   if (!host_val) {
     add(v->addr, s.h_addr, s.d_addr, 20);
@@ -926,6 +945,13 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
     c->stamp = 0;
   }
   s.stamp = ++c->stamp;            // every run of a batch gets a stamp of its own
+  // The event compaction's look-back words carry the stamp's low 30 bits and are never cleared
+  // between runs.  A new tag cycle -- the first run after alloc_tally or the wrap above reset the
+  // stamp, or every 2^30 runs -- could meet a word an earlier cycle left with the same tag (ADVICE
+  // r5): every slot's words are zeroed first, on the flow stream behind the runs before.
+  if ((s.stamp & 0x3FFFFFFFu) == 1u)
+    for (Slot& o : c->slots)
+      if (o.d_ev_tiles) HIP_TRY(c, hipMemsetAsync(o.d_ev_tiles, 0, (size_t)o.ev_tiles_n * sizeof(uint64_t), c->stream));
   s.run_seq = ++c->run_seq;
   const FlowState fs = flow_state(c);
   const FlowBatch fb = flow_batch(c, s);
@@ -1034,6 +1060,11 @@ int fetch_slot(txv_ctx* c, uint32_t slot, uint8_t* status_out, txv_commit_event*
   }
   c->unfetched -= s.counted;
   s.counted = 0;
+  if (sm.err & TXV_FERR_LOOKBACK) {   // a broken invariant, not a capacity: the event ranks are not trusted
+    c->poisoned |= sm.err;
+    c->err = "TxFlow event compaction: look-back timed out (device error; txv_reset_flow to recover)";
+    return TXV_EDEVICE;
+  }
   if (sm.err) {
     c->poisoned |= sm.err;
     c->err = std::string("TxFlow capacity exceeded:") + ((sm.err & TXV_FERR_SETS) ? " max_txs" : "") +
@@ -1407,6 +1438,8 @@ void txv_destroy(txv_ctx* c) {
   dfree(c->d_arena_seq); dfree(c->d_arena_txkey); dfree(c->d_set_stamp); dfree(c->d_set_blk); dfree(c->d_set_digest); dfree(c->d_bitmap);
   dfree(c->d_set_entry); dfree(c->d_set_txkey); dfree(c->d_tab); dfree(c->d_keys); dfree(c->d_ctr);
   dfree(c->d_addr_slots); dfree(c->d_q);
+  dfree(c->d_rshard); dfree(c->d_rw); dfree(c->d_rmax); dfree(c->d_rtot); hfree(c->h_rmeta);
+  if (c->route_ev) (void)hipEventDestroy(c->route_ev);
   for (const auto& rg : c->registered) (void)hipHostUnregister((void*)rg.first);
   dfree(c->d_sk_scal); dfree(c->d_sk_araw); dfree(c->d_sk_prefix); dfree(c->d_sk_pub);
   dfree(c->d_chain); dfree(c->d_chain_sign);
@@ -2268,6 +2301,248 @@ int txv_shard_of(const uint8_t* txhash, const uint32_t* off, const uint32_t* len
   }
   work(0);
   for (auto& x : th) x.join();
+  return TXV_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// ---- the multi-GPU ingest route (include/txvote.h txv_route_admitted; kernels_route.hip) ----
+uint32_t route_flags(const txv_votes* v) {
+  return (v->txkey ? TXV_ROUTE_TXKEY : 0u) | (v->is_nil ? TXV_ROUTE_NIL : 0u);
+}
+
+int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G, void* dst, uint64_t stride,
+                   txv_route_meta* meta) {
+  const uint32_t n = v->n;
+  const uint32_t flags = route_flags(v);
+  int r;
+  hipEvent_t done;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if ((r = stage_add(c, kRouteSlot, v, true))) return r;
+    Slot& s = c->slots[kRouteSlot];
+    const uint64_t need = txv_route_bytes(n, s.arena_end, flags);
+    if (stride < need) {
+      c->err = "route stride below txv_route_bytes(n, TxHash arena extent, flags) = " + std::to_string(need);
+      return TXV_EINVAL;
+    }
+    if (st && n) {   // the pool's statuses beside the columns (the slot's pre-check column is free here)
+      memcpy(s.h_status, st, n);
+      HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, n, hipMemcpyHostToDevice, c->copy_stream));
+      HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));
+    }
+    const uint32_t nw = (n + 63) / 64;
+    if (n > c->route_n_cap) {
+      if ((r = dalloc(c, &c->d_rshard, std::max<uint32_t>(n, 64)))) return r;
+      c->route_n_cap = n;
+    }
+    if ((uint64_t)nw * G > c->route_w_cap) {
+      if ((r = dalloc(c, &c->d_rw, 2 * (size_t)std::max<uint32_t>(nw, 1) * G))) return r;
+      c->route_w_cap = std::max<uint32_t>(nw, 1) * G;
+    }
+    if (!c->d_rmax) {
+      if ((r = dalloc(c, &c->d_rmax, 256)) || (r = dalloc(c, &c->d_rtot, 512)) ||
+          (r = halloc_mapped(c, &c->h_rmeta, &c->m_rmeta, 256)))
+        return r;
+      HIP_TRY(c, hipEventCreateWithFlags(&c->route_ev, hipEventDisableTiming));
+    }
+    RouteArgs a{};
+    a.n = n; a.G = G; a.nw = nw;
+    a.height = s.d_fh; a.ts_sec = s.d_fs; a.ts_nanos = s.d_fn; a.th_off = s.d_fo; a.th_len = s.d_fl; a.th = s.d_arena_th;
+    a.addr = s.d_addr; a.addr_len = s.d_addr_len; a.sig = s.d_sigraw; a.sig_len = s.d_sig_len;
+    a.txkey = s.has_txkey ? s.d_txkey : nullptr;
+    a.nil = s.has_nil ? s.d_nil : nullptr;
+    a.status = st ? s.d_pre : nullptr;
+    a.flags = flags;
+    a.shard = c->d_rshard; a.wcnt = c->d_rw; a.wbytes = c->d_rw + (size_t)std::max<uint32_t>(nw, 1) * G;
+    a.maxhl = c->d_rmax; a.tot = c->d_rtot;
+    a.dst = static_cast<uint8_t*>(dst); a.stride = stride; a.meta = c->m_rmeta;
+    // on the key stream (CheckTx's engine and the batches' prep run there too): after the uploads
+    HIP_TRY(c, hipStreamWaitEvent(c->key_stream, s.ev[3], 0));
+    HIP_TRY(c, txv_launch_route(&a, c->key_stream));
+    HIP_TRY(c, hipEventRecord(s.ev[4], c->key_stream));   // the slot's next staging waits for it
+    HIP_TRY(c, hipEventRecord(c->route_ev, c->key_stream));
+    s.launched = true;
+    s.staged = false;
+    done = c->route_ev;
+  }
+  HIP_TRY(c, hipEventSynchronize(done));
+  memcpy(meta, c->h_rmeta, (size_t)G * sizeof(txv_route_meta));
+  return TXV_OK;
+}
+
+// the receiving rank: a route buffer (on this context's device) into AddVote slot `slot`, by
+// device-to-device copies on the copy stream (stage_add's counterpart: nothing crosses PCIe)
+int stage_routed(txv_ctx* c, uint32_t slot, const uint8_t* buf, const txv_route_meta* m) {
+  if (!c->n_vals) { c->err = "no validator set"; return TXV_ESTATE; }
+  if (m->n > c->cfg.max_batch) { c->err = "batch exceeds max_batch"; return TXV_ECAPACITY; }
+  if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+  if (m->arena_bytes >= (1ull << 32)) { c->err = "TxHash arena >= 4 GiB"; return TXV_EINVAL; }
+  Slot& s = c->slots[slot];
+  const uint32_t n = m->n;
+  uint64_t off[txv_route::kNCols];
+  if (txv_route::layout(n, m->arena_bytes, m->flags, off) != m->bytes) { c->err = "route meta: inconsistent sizes"; return TXV_EINVAL; }
+  const uint32_t mw = (signbytes_bound(m->max_txhash_len, (uint32_t)c->chain.size()) + 7) / 8;
+  int r;
+  if ((r = ensure_slot(c, s, n, mw)) || (r = ensure_flow_slot(c, s, n))) return r;
+  const uint64_t ae = m->arena_bytes;
+  if (ae + 16 > s.arena_cap) {
+    const size_t cap = std::max<size_t>((size_t)ae + 16, s.arena_cap * 2);
+    if ((r = halloc(c, &s.h_arena, cap)) || (r = dalloc(c, &s.d_arena_th, cap))) return r;
+    s.arena_cap = cap;
+  }
+  s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
+  s.has_nil = (m->flags & TXV_ROUTE_NIL) != 0;
+  s.has_txkey = (m->flags & TXV_ROUTE_TXKEY) != 0;
+  s.host_val = false;
+  s.arena_end = ae;
+  s.seq_base = c->seq_next;
+  c->seq_next += n;
+  if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));   // its last chain has ended
+  struct { int col; void* dev; size_t elem; } cols[] = {
+      {txv_route::kHeight, s.d_fh, 8}, {txv_route::kSec, s.d_fs, 8}, {txv_route::kNanos, s.d_fn, 4},
+      {txv_route::kOff, s.d_fo, 4}, {txv_route::kLen, s.d_fl, 4}, {txv_route::kAddrLen, s.d_addr_len, 4},
+      {txv_route::kSigLen, s.d_sig_len, 4}, {txv_route::kAddr, s.d_addr, 20}, {txv_route::kSig, s.d_sigraw, 64},
+      {txv_route::kTxKey, s.has_txkey ? s.d_txkey : nullptr, 32}, {txv_route::kNil, s.has_nil ? s.d_nil : nullptr, 1}};
+  for (const auto& k : cols)
+    if (k.dev && n) HIP_TRY(c, hipMemcpyAsync(k.dev, buf + off[k.col], (size_t)n * k.elem, hipMemcpyDeviceToDevice, c->copy_stream));
+  HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, buf + off[txv_route::kArena], ae + 16, hipMemcpyDeviceToDevice, c->copy_stream));
+  c->staged_bytes = 0;
+  HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
+  s.staged = true; s.ran = false;
+  return TXV_OK;
+}
+
+// host: shard of every admitted vote, then each rank's buffer in arrival order (route.h)
+int route_pack_host(const txv_votes* v, const uint8_t* st, uint32_t G, uint8_t* dst, uint64_t stride,
+                    txv_route_meta* meta) {
+  const uint32_t n = v->n;
+  const uint32_t flags = route_flags(v);
+  std::vector<uint8_t> shard(n, 0xFF);
+  std::vector<uint32_t> cnt(G, 0), mx(G, 0);
+  std::vector<uint64_t> ab(G, 0);
+  uint64_t ae = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!(v->is_nil && v->is_nil[i])) ae = std::max<uint64_t>(ae, (uint64_t)v->txhash_off[i] + v->txhash_len[i]);
+    if (st && st[i] != TXV_POOL_OK) continue;
+    const uint32_t len = (v->is_nil && v->is_nil[i]) ? 0u : v->txhash_len[i];
+    uint8_t h[32];
+    txv_sha256_bytes(len ? v->txhash + v->txhash_off[i] : nullptr, len, h);
+    const uint32_t r = h[0] % G;
+    shard[i] = (uint8_t)r;
+    ++cnt[r];
+    ab[r] += len;
+    mx[r] = std::max(mx[r], len);
+  }
+  if (stride < txv_route_bytes(n, ae, flags)) return TXV_EINVAL;
+  std::vector<uint64_t> pos(G, 0), bpos(G, 0);
+  for (uint32_t r = 0; r < G; ++r) {
+    uint64_t off[txv_route::kNCols];
+    const uint64_t total = txv_route::layout(cnt[r], ab[r], flags, off);
+    uint8_t* b = dst + (size_t)r * stride;
+    memset(b, 0, total);
+    const uint64_t hdr[8] = {txv_route::kMagic, cnt[r], ab[r], flags, mx[r], total, 0, 0};
+    memcpy(b, hdr, 64);
+    meta[r] = txv_route_meta{cnt[r], mx[r], flags, 0, ab[r], total};
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = shard[i];
+    if (r == 0xFF) continue;
+    uint64_t off[txv_route::kNCols];
+    (void)txv_route::layout(cnt[r], ab[r], flags, off);
+    uint8_t* b = dst + (size_t)r * stride;
+    const uint64_t j = pos[r]++;
+    const bool nil = v->is_nil && v->is_nil[i];
+    const uint32_t len = nil ? 0u : v->txhash_len[i];
+    const uint32_t bo = (uint32_t)bpos[r];
+    memcpy(b + off[txv_route::kHeight] + 8 * j, &v->height[i], 8);
+    memcpy(b + off[txv_route::kSec] + 8 * j, &v->ts_sec[i], 8);
+    memcpy(b + off[txv_route::kNanos] + 4 * j, &v->ts_nanos[i], 4);
+    memcpy(b + off[txv_route::kOff] + 4 * j, &bo, 4);
+    memcpy(b + off[txv_route::kLen] + 4 * j, &len, 4);
+    memcpy(b + off[txv_route::kAddrLen] + 4 * j, &v->addr_len[i], 4);
+    memcpy(b + off[txv_route::kSigLen] + 4 * j, &v->sig_len[i], 4);
+    memcpy(b + off[txv_route::kAddr] + 20 * j, v->addr + (size_t)i * 20, 20);
+    memcpy(b + off[txv_route::kSig] + 64 * j, v->sig + (size_t)i * 64, 64);
+    if (flags & TXV_ROUTE_TXKEY) memcpy(b + off[txv_route::kTxKey] + 32 * j, v->txkey + (size_t)i * 32, 32);
+    if (flags & TXV_ROUTE_NIL) b[off[txv_route::kNil] + j] = nil ? 1 : 0;
+    if (len) memcpy(b + off[txv_route::kArena] + bo, v->txhash + v->txhash_off[i], len);
+    bpos[r] += len;
+  }
+  return TXV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t txv_route_bytes(uint32_t n, uint64_t arena_bytes, uint32_t flags) {
+  uint64_t off[txv_route::kNCols];
+  return txv_route::layout(n, arena_bytes, flags, off);
+}
+
+int txv_route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* pool_status, uint32_t n_shards, void* dst_dev,
+                       uint64_t stride, txv_route_meta* meta_out) {
+  if (!c || !v || !dst_dev || !meta_out || !n_shards || n_shards > 255) return TXV_EINVAL;
+  if (v->n && (!v->height || !v->txhash || !v->txhash_off || !v->txhash_len || !v->ts_sec || !v->ts_nanos || !v->addr ||
+               !v->addr_len || !v->sig || !v->sig_len))
+    return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->route_mu);
+  return route_admitted(c, v, pool_status, n_shards, dst_dev, stride, meta_out);
+}
+
+int txv_route_pack_host(const txv_votes* v, const uint8_t* pool_status, uint32_t n_shards, void* dst, uint64_t stride,
+                        txv_route_meta* meta_out) {
+  if (!v || !dst || !meta_out || !n_shards || n_shards > 255) return TXV_EINVAL;
+  if (v->n && (!v->height || !v->txhash || !v->txhash_off || !v->txhash_len || !v->ts_sec || !v->ts_nanos || !v->addr ||
+               !v->addr_len || !v->sig || !v->sig_len))
+    return TXV_EINVAL;
+  return route_pack_host(v, pool_status, n_shards, static_cast<uint8_t*>(dst), stride, meta_out);
+}
+
+int txv_route_view(const void* buf, uint64_t bytes, txv_votes* out) {
+  if (!buf || !out || bytes < 64) return TXV_EINVAL;
+  const uint8_t* b = static_cast<const uint8_t*>(buf);
+  uint64_t h[8];
+  memcpy(h, b, 64);
+  if (h[0] != txv_route::kMagic || h[1] > 0xFFFFFFFFull) return TXV_EINVAL;
+  uint64_t off[txv_route::kNCols];
+  const uint64_t total = txv_route::layout(h[1], h[2], (uint32_t)h[3], off);
+  if (total != h[5] || total > bytes) return TXV_EINVAL;
+  const uint32_t flags = (uint32_t)h[3];
+  out->n = (uint32_t)h[1];
+  out->height = reinterpret_cast<const int64_t*>(b + off[txv_route::kHeight]);
+  out->ts_sec = reinterpret_cast<const int64_t*>(b + off[txv_route::kSec]);
+  out->ts_nanos = reinterpret_cast<const int32_t*>(b + off[txv_route::kNanos]);
+  out->txhash_off = reinterpret_cast<const uint32_t*>(b + off[txv_route::kOff]);
+  out->txhash_len = reinterpret_cast<const uint32_t*>(b + off[txv_route::kLen]);
+  out->addr_len = reinterpret_cast<const uint32_t*>(b + off[txv_route::kAddrLen]);
+  out->sig_len = reinterpret_cast<const uint32_t*>(b + off[txv_route::kSigLen]);
+  out->addr = b + off[txv_route::kAddr];
+  out->sig = b + off[txv_route::kSig];
+  out->txkey = (flags & TXV_ROUTE_TXKEY) ? b + off[txv_route::kTxKey] : nullptr;
+  out->is_nil = (flags & TXV_ROUTE_NIL) ? b + off[txv_route::kNil] : nullptr;
+  out->txhash = b + off[txv_route::kArena];
+  return TXV_OK;
+}
+
+int txv_submit_routed(txv_ctx* c, const void* buf_dev, const txv_route_meta* meta, uint64_t* ticket) {
+  if (!c || !buf_dev || !meta || !ticket) return TXV_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t t = c->next_ticket;
+  const uint32_t slot = (uint32_t)((t - 1) % kSubmitRing);
+  Slot& s = c->slots[slot];
+  if (s.ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
+  int r;
+  if ((r = stage_routed(c, slot, static_cast<const uint8_t*>(buf_dev), meta))) return r;
+  if ((r = run_slot(c, slot, nullptr))) return r;
+  s.ticket = t;
+  c->next_ticket = t + 1;
+  *ticket = t;
   return TXV_OK;
 }
 
@@ -3139,19 +3414,21 @@ int txv_ingest_msgs(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_
 #include "pool_dev.h"
 extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C);
 extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* a, hipStream_t st);
-extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, hipStream_t st);
+extern "C" hipError_t txv_pooldev_index(const uint32_t* ck, uint32_t L, uint32_t* ci, uint32_t icap, uint64_t seed,
+                                        hipStream_t st);
 extern "C" size_t txv_poollist_tmp_bytes(uint32_t cap);
 extern "C" hipError_t txv_poollist_compact(const uint32_t* lk, const uint32_t* lsz, const uint8_t* lfl,
                                            const unsigned long long* li, uint32_t ocap, uint32_t oicap, uint32_t* nk,
                                            uint32_t* nsz, uint8_t* nfl, unsigned long long* ni, uint32_t ncap,
                                            uint32_t nicap, uint32_t* npos, void* tmp, size_t tmp_bytes,
-                                           uint32_t* tail_out, hipStream_t st);
+                                           uint32_t* tail_out, uint64_t seed, hipStream_t st);
 extern "C" hipError_t txv_poollist_upload_index(const uint32_t* lk, const uint8_t* ins, uint32_t L,
-                                                unsigned long long* li, uint32_t icap, hipStream_t st);
+                                                unsigned long long* li, uint32_t icap, uint64_t seed, hipStream_t st);
 
 struct PoolDev {
   int device = -1;
   uint32_t C = 0, icap = 0, cap_n = 0, cur = 0;
+  uint64_t seed = 0;                       // secret hash seed of every key placement (kernels_pool.hip)
   uint32_t* ck[2] = {nullptr, nullptr};
   uint32_t* ci[2] = {nullptr, nullptr};
   uint32_t* clen = nullptr;                        // [2]: length, staged new length
@@ -3163,6 +3440,8 @@ struct PoolDev {
   uint64_t* tiles = nullptr;               // look-back words of the fused scans (kernels_pool.hip)
   uint32_t* tk = nullptr;                  // [4] their tile tickets
   uint32_t epoch = 0;                      // batches run: the look-back words' tag
+  uint32_t* d_err = nullptr;               // sticky look-back timeout flag (kernels_pool.hip) ...
+  uint32_t *h_err = nullptr, *m_err = nullptr;   // ... copied into mapped memory by each chain's last launch
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   uint32_t* okpos = nullptr;               // [cap_n] the list appends' ranks
@@ -3213,7 +3492,7 @@ struct PoolDev {
     dfree(last); dfree(lpos); dfree(far); dfree(nfar); dfree(surv); dfree(spos); dfree(dec);
     dfree(detached); dfree(pst); dfree(pend); dfree(xs); dfree(xn); dfree(tiles); dfree(tk); dfree(okpos);
     for (ListBuf& b : lb) { dfree(b.k); dfree(b.sz); dfree(b.fl); dfree(b.ix); }
-    dfree(ltail); dfree(lnpos);
+    dfree(ltail); dfree(lnpos); dfree(d_err); hfree(h_err);
     if (ltmp) (void)hipFree(ltmp);
     for (Flight& f : fl) {
       dfree(f.d_sig); dfree(f.d_len); dfree(f.d_keys); dfree(f.d_sizes); dfree(f.d_status);
@@ -3254,6 +3533,7 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     *sp = s;
     s->device = c->device;
     s->C = C;
+    s->seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x706f6f6c6b657973ULL;
     s->icap = 16;
     while (s->icap < 2 * std::max<uint32_t>(C, 1)) s->icap *= 2;
     int r;
@@ -3261,8 +3541,11 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     if ((r = dalloc(c, &s->ck[0], cw * 8)) || (r = dalloc(c, &s->ck[1], cw * 8)) || (r = dalloc(c, &s->ci[0], s->icap)) ||
         (r = dalloc(c, &s->ci[1], s->icap)) || (r = dalloc(c, &s->clen, 2)) || (r = dalloc(c, &s->detached, cw)) ||
         (r = dalloc(c, &s->surv, cw)) || (r = dalloc(c, &s->spos, cw)) || (r = dalloc(c, &s->nfar, 2)) ||
-        (r = halloc(c, &s->h_clen, 2)) || (r = dalloc(c, &s->tk, 4)) || (r = dalloc(c, &s->ltail, 2)))
+        (r = halloc(c, &s->h_clen, 2)) || (r = dalloc(c, &s->tk, 4)) || (r = dalloc(c, &s->ltail, 2)) ||
+        (r = dalloc(c, &s->d_err, 1)) || (r = halloc_mapped(c, &s->h_err, &s->m_err, 1)))
       return r;
+    HIP_TRY(c, hipMemset(s->d_err, 0, 4));
+    *s->h_err = 0;
     HIP_TRY(c, hipMemset(s->tk, 0, 16));
     HIP_TRY(c, hipMemset(s->ltail, 0, 8));
     HIP_TRY(c, hipMemset(s->ci[0], 0, (size_t)s->icap * 4));
@@ -3343,7 +3626,7 @@ int pooldev_put_cache(txv_ctx* c, PoolDev* s, const uint8_t* keys, uint32_t L) {
   s->h_clen[0] = L;
   s->h_clen[1] = L;
   PD_TRY(hipMemcpyAsync(s->clen, s->h_clen, 8, hipMemcpyHostToDevice, s->st));
-  PD_TRY(txv_pooldev_index(s->ck[s->cur], L, s->ci[s->cur], s->icap, s->st));
+  PD_TRY(txv_pooldev_index(s->ck[s->cur], L, s->ci[s->cur], s->icap, s->seed, s->st));
   PD_TRY(hipStreamSynchronize(s->st));
   return TXV_OK;
 }
@@ -3429,7 +3712,7 @@ int list_compact(txv_ctx* c, PoolDev* s, hipStream_t ks, uint64_t live_ub, uint3
     }
   }
   HIP_TRY(c, txv_poollist_compact(o.k, o.sz, o.fl, o.ix, o.cap, o.icap, nb.k, nb.sz, nb.fl, nb.ix, nb.cap, nb.icap,
-                                  s->lnpos, s->ltmp, s->ltmp_bytes, s->ltail + (s->ltp ^ 1), ks));
+                                  s->lnpos, s->ltmp, s->ltmp_bytes, s->ltail + (s->ltp ^ 1), s->seed, ks));
   s->ltp ^= 1;
   s->lcur ^= 1;
   s->tail_ub = live_ub;
@@ -3456,7 +3739,7 @@ int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t
     HIP_TRY(c, hipMemcpyAsync(d_ins, ins, L, hipMemcpyHostToDevice, s->st));
     HIP_TRY(c, hipMemsetAsync(b.fl, 1, L, s->st));
   }
-  HIP_TRY(c, txv_poollist_upload_index(b.k, d_ins, L, b.ix, b.icap, s->st));
+  HIP_TRY(c, txv_poollist_upload_index(b.k, d_ins, L, b.ix, b.icap, s->seed, s->st));
   s->h_clen[0] = L;                                    // (staging word)
   HIP_TRY(c, hipMemcpyAsync(s->ltail + s->ltp, s->h_clen, 4, hipMemcpyHostToDevice, s->st));
   HIP_TRY(c, hipStreamSynchronize(s->st));
@@ -3639,7 +3922,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
   a.pend = s->pend; a.xs = s->xs; a.xn = s->xn; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
   a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status; a.status_out = f.m_status;
-  a.tiles = s->tiles; a.tk = s->tk;
+  a.tiles = s->tiles; a.tk = s->tk; a.err = s->d_err; a.err_host = s->m_err; a.seed = s->seed;
   if (((++s->epoch) & 0x3FFFFFFFu) == 0) {          // the tag wrapped: no word may match by accident
     HIP_TRY(c, hipMemsetAsync(s->tiles, 0, pooldev_tile_words(s->cap_n, s->C) * 8, ks));
     ++s->epoch;
@@ -3655,7 +3938,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
     a.okpos = s->okpos;
     a.res = f.m_res;
     a.res_rm = f.m_res + res_words(s->cap_n) / 2;
-    a.l.lk = b.k; a.l.lsz = b.sz; a.l.lfl = b.fl; a.l.li = b.ix; a.l.imask = b.icap - 1;
+    a.l.lk = b.k; a.l.lsz = b.sz; a.l.lfl = b.fl; a.l.li = b.ix; a.l.imask = b.icap - 1; a.l.seed = s->seed;
     a.l.tail_in = s->ltail + s->ltp; a.l.tail_out = s->ltail + (s->ltp ^ 1);
     f.nt_app = (total + 1023) / 1024;
     f.nt_rm = (n_upd + 1023) / 1024;
@@ -3681,6 +3964,10 @@ int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, con
   PoolDev::Flight& f = s->fl[slot];
   if (c) HIP_TRY(c, hipEventSynchronize(f.ev));
   else if (hipEventSynchronize(f.ev) != hipSuccess) return TXV_EDEVICE;
+  if (*(volatile uint32_t*)s->h_err) {   // a look-back scan of this or an earlier chain timed out (sticky)
+    if (c) c->err = "pool engine: look-back scan timed out (device error; statuses not trusted)";
+    return TXV_EDEVICE;
+  }
   if (status) *status = f.h_status;
   if (keys) *keys = reinterpret_cast<const uint8_t*>(f.h_keys);
   if (sizes) *sizes = f.h_sizes;

@@ -245,4 +245,29 @@ TXV_HD void sha256_32bytes(uint32_t out[8], const uint32_t in_le[8]) {
   for (int i = 0; i < 8; ++i) out[i] = st[i];
 }
 
+// SHA-256 of len bytes at p (any alignment), big-endian state words (TxHash digests: the
+// exchange names of the sets, kernels_flow.hip, and the ingest route's shard, kernels_route.hip)
+TXV_HD void sha256_bytes(const uint8_t* p, uint32_t n, uint32_t st[8]) {
+  sha256_init(st);
+  const uint32_t nblk = (n + 9 + 63) / 64;       // message + 0x80 + 8-byte length
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t k = 64u * b + 4u * (uint32_t)t + (uint32_t)q;   // byte index in the padded message
+        uint32_t byte = 0;
+        if (k < n) byte = p[k];
+        else if (k == n) byte = 0x80u;
+        v = (v << 8) | byte;
+      }
+      w[t] = v;
+    }
+    if (b == nblk - 1) { w[14] = (uint32_t)((uint64_t)n >> 29); w[15] = n << 3; }
+    sha256_block(st, w);
+  }
+}
+
 }  // namespace txv

@@ -61,6 +61,7 @@
 #define TXV_FERR_TABLE 0x2u     // set table full (probe bound)
 #define TXV_FERR_KEYS 0x4u      // TxHash overflow key arena full
 #define TXV_FERR_ARENA 0x8u     // accepted-vote arena full (max_accepted)
+#define TXV_FERR_LOOKBACK 0x10u // the event compaction's look-back timed out (a broken invariant: device error)
 
 struct TallyCell {              // 16 B, see the header comment
   uint64_t cand;

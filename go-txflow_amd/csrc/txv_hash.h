@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define TXV_HASH_HD __host__ __device__ __forceinline__
 #else
 #define TXV_HASH_HD inline
@@ -30,6 +31,18 @@ TXV_HASH_HD uint64_t hash_chunks(uint32_t n, uint64_t seed, Get get) {
     h = mix64(h ^ t ^ ((uint64_t)(n - i) << 56));
   }
   return mix64(h) | 1ull;   // never 0
+}
+
+// seeded hash of a 32-byte TxVotePool key (SHA-256(Signature), as 8 words in memory order).  The
+// keys are peer-chosen (a peer can grind signatures until their keys share any unseeded slice), so
+// every table or sort over them places a key by this hash under a secret per-process / per-engine
+// seed: a run of colliding keys costs 2^bits tries per key only for someone who knows the seed.
+// All 8 words are mixed, each through a bijection keyed by the running state, so no two distinct
+// keys collide for every seed.
+TXV_HASH_HD uint64_t key32(const uint32_t* k, uint64_t seed) {
+  uint64_t h = seed;
+  for (int j = 0; j < 4; ++j) h = mix64(h ^ ((uint64_t)k[2 * j] | ((uint64_t)k[2 * j + 1] << 32))) + 0x9e3779b97f4a7c15ULL;
+  return mix64(h);
 }
 
 }  // namespace txv_hash

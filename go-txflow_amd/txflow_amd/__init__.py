@@ -81,6 +81,10 @@ class _Event(ctypes.Structure):
 
 
 EVENT_DTYPE = np.dtype([("vote_index", "<u4"), ("tx_index", "<u4"), ("sum", "<i8")])   # txv_commit_event
+# txv_route_meta: one rank's ingest-route buffer (include/txvote.h txv_route_admitted)
+ROUTE_META_DTYPE = np.dtype([("n", "<u4"), ("max_txhash_len", "<u4"), ("flags", "<u4"), ("reserved", "<u4"),
+                             ("arena_bytes", "<u8"), ("bytes", "<u8")])
+ROUTE_TXKEY, ROUTE_NIL = 0x1, 0x2
 
 
 _lib = None
@@ -181,6 +185,11 @@ def lib():
             "txv_read_commit_state": ([vp, vp, u32], ctypes.c_int),
             "txv_commit_state_pack_host": ([u32, vp, vp, vp, u32, vp], ctypes.c_int),
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, vp, u32], ctypes.c_int),
+            "txv_route_bytes": ([u32, ctypes.c_uint64, u32], ctypes.c_uint64),
+            "txv_route_admitted": ([vp, ctypes.POINTER(_Votes), vp, u32, vp, ctypes.c_uint64, vp], ctypes.c_int),
+            "txv_route_pack_host": ([ctypes.POINTER(_Votes), vp, u32, vp, ctypes.c_uint64, vp], ctypes.c_int),
+            "txv_route_view": ([vp, ctypes.c_uint64, ctypes.POINTER(_Votes)], ctypes.c_int),
+            "txv_submit_routed": ([vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             if os.environ.get("TXV_LIB_PATH") and not hasattr(L, name):
@@ -207,7 +216,8 @@ EXPORTED_SYMBOLS = [
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
     "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare",
-    "txv_ingest_decode", "txv_ingest_admit"]
+    "txv_ingest_decode", "txv_ingest_admit", "txv_route_bytes", "txv_route_admitted", "txv_route_pack_host",
+    "txv_route_view", "txv_submit_routed"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -315,6 +325,57 @@ class VoteBatch:
     def txhash(self, i: int) -> bytes:
         o, l = int(self.txhash_off[i]), int(self.txhash_len[i])
         return self.txhash_arena[o:o + l].tobytes()
+
+
+def route_flags(batch: VoteBatch) -> int:
+    return (ROUTE_TXKEY if batch.txkey is not None else 0) | (ROUTE_NIL if batch.is_nil is not None else 0)
+
+
+def route_stride(batch: VoteBatch) -> int:
+    """bytes every rank's route buffer needs for this batch whatever the split
+    (txv_route_bytes of all n votes and the whole TxHash arena extent)"""
+    live = np.ones(batch.n, bool) if batch.is_nil is None else batch.is_nil == 0
+    ext = int((batch.txhash_off[live].astype(np.int64) + batch.txhash_len[live]).max()) if live.any() else 0
+    return int(lib().txv_route_bytes(batch.n, ext, route_flags(batch)))
+
+
+def route_pack_host(batch: VoteBatch, pool_status=None, n_shards: int = 1):
+    """txv_route_pack_host: the votes pool_status admits (TXV_POOL_OK; None = all), each rank's
+    in arrival order, as [n_shards, stride] route buffers built on the host, and their metas"""
+    stride = route_stride(batch)
+    out = np.zeros((n_shards, stride), np.uint8)
+    meta = np.zeros(n_shards, ROUTE_META_DTYPE)
+    st = None if pool_status is None else np.ascontiguousarray(pool_status, np.uint8)
+    vs = batch.c_struct()
+    r = lib().txv_route_pack_host(ctypes.byref(vs), None if st is None else st.ctypes.data, n_shards, out.ctypes.data,
+                                  stride, meta.ctypes.data)
+    if r:
+        raise ValueError(f"txv_route_pack_host: {r}")
+    return out, meta
+
+
+def route_view(buf) -> VoteBatch:
+    """a route buffer (host bytes) as a VoteBatch (copies; txv_route_view)"""
+    b = np.ascontiguousarray(buf, np.uint8)
+    v = _Votes()
+    r = lib().txv_route_view(b.ctypes.data, b.size, ctypes.byref(v))
+    if r:
+        raise ValueError(f"txv_route_view: {r}")
+    n = v.n
+
+    def col(ptr, dt, count):
+        if not ptr or not count:
+            return np.zeros(count, dt)
+        return np.frombuffer((ctypes.c_uint8 * (count * np.dtype(dt).itemsize)).from_address(ptr), dt).copy()
+    off = col(v.txhash_off, np.uint32, n)
+    ln = col(v.txhash_len, np.uint32, n)
+    ab = int((off.astype(np.int64) + ln).max()) if n else 0
+    return VoteBatch(n, height=col(v.height, np.int64, n), txhash_arena=col(v.txhash, np.uint8, ab), txhash_off=off,
+                     txhash_len=ln, ts_sec=col(v.ts_sec, np.int64, n), ts_nanos=col(v.ts_nanos, np.int32, n),
+                     addr=col(v.addr, np.uint8, 20 * n), addr_len=col(v.addr_len, np.uint32, n),
+                     sig=col(v.sig, np.uint8, 64 * n), sig_len=col(v.sig_len, np.uint32, n),
+                     is_nil=col(v.is_nil, np.uint8, n) if v.is_nil else None,
+                     txkey=col(v.txkey, np.uint8, 32 * n) if v.txkey else None)
 
 
 # ------------------------------------------------------------------ received wire messages
@@ -526,6 +587,27 @@ class Context:
         self._chk(lib().txv_add_votes(self._h, ctypes.byref(vs), out.ctypes.data, evs.ctypes.data, ev_cap,
                                       ctypes.byref(nev)), "txv_add_votes")
         return out[:batch.n], evs[:min(nev.value, ev_cap)]
+
+    def route_admitted(self, batch: VoteBatch, pool_status, n_shards: int, dst_ptr: int, stride: int) -> np.ndarray:
+        """txv_route_admitted: the admitted votes packed on this context's GPU into rank r's buffer at
+        device address dst_ptr + r * stride (>= route_stride(batch)); returns the metas"""
+        meta = np.zeros(n_shards, ROUTE_META_DTYPE)
+        st = None if pool_status is None else np.ascontiguousarray(pool_status, np.uint8)
+        vs = batch.c_struct()
+        self._chk(lib().txv_route_admitted(self._h, ctypes.byref(vs), None if st is None else st.ctypes.data, n_shards,
+                                           ctypes.c_void_p(dst_ptr), stride, meta.ctypes.data), "txv_route_admitted")
+        return meta
+
+    def submit_routed(self, buf_ptr: int, meta) -> int:
+        """txv_submit_routed: TryAddVote for a route buffer already in this context's HBM (at device
+        address buf_ptr, e.g. what the node's RCCL scatter delivered); a ticket for wait_votes"""
+        m = np.ascontiguousarray(np.asarray(meta, ROUTE_META_DTYPE).reshape(1))
+        t = ctypes.c_uint64()
+        self._chk(lib().txv_submit_routed(self._h, ctypes.c_void_p(buf_ptr), m.ctypes.data, ctypes.byref(t)),
+                  "txv_submit_routed")
+        self._inflight = getattr(self, "_inflight", {})
+        self._inflight[t.value] = int(m[0]["n"])
+        return t.value
 
     def submit_votes(self, batch: VoteBatch) -> int:
         """asynchronous TryAddVote batch (txv_submit_votes): returns a ticket for wait_votes"""

@@ -12,9 +12,13 @@ arrival order of its own votes).
 Ingest (txvotepool/reactor.go:170-190 -> txvotepool.go:187-261): TxVotePool is ONE
 order-dependent LRU keyed by SHA-256(Signature) with one Size cap, so CheckTx cannot be split by
 shard without changing which votes it admits.  It runs on one owner rank (the node's reactor
-process); the votes it admits are routed to the rank owning their TxHash (route_admitted), in
-arrival order, by one scatter per batch (scatter_batches) -- the path's one real data exchange
-besides the commit-state all-gather.
+process); the votes it admits are packed per rank on the owner's GPU by the C-ABI's
+txv_route_admitted (kernels_route.hip: shard, arrival-order rank and TxHash arena offset of every
+admitted vote, each rank's columns written into its own buffer) -- or on the host by
+txv_route_pack_host -- sent buffer r to rank r (scatter_routed: one meta broadcast + point-to-point
+sends, RCCL over xGMI), and each rank runs its TxFlow chain straight from the received buffer in
+its HBM (Context.submit_routed): the path's one real data exchange besides the commit-state
+all-gather.
 
 Exchange: one all-gather per batch of the packed per-shard commit state --
 [n_sets][commit bitmap][stake sums][digests] over the shard's set ids, numbered in first-seen
@@ -28,7 +32,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import VoteBatch, commit_state_unpack, shard_of as _shard_of, tx_digest
+from . import ROUTE_META_DTYPE, VoteBatch, commit_state_unpack, lib, shard_of as _shard_of, tx_digest
 
 
 def shard_of(txhashes: Sequence[bytes], n_shards: int) -> np.ndarray:
@@ -59,17 +63,20 @@ def merge_states(gathered: np.ndarray, n_shards: int, n_sets_cap: int) -> Tuple[
 
 
 def subset(b: VoteBatch, idx: np.ndarray) -> VoteBatch:
-    """the votes idx of b (in that order) as a batch with a compact TxHash arena of their own"""
+    """the votes idx of b (in that order) as a batch with a compact TxHash arena of their own
+    (numpy gathers, no per-vote loop)"""
     idx = np.asarray(idx, np.int64)
     n = len(idx)
     ln = b.txhash_len[idx].astype(np.int64)
     off = np.zeros(n, np.int64)
     if n:
         off[1:] = np.cumsum(ln)[:-1]
-    arena = np.zeros(max(int(ln.sum()), 1), np.uint8)
-    for j, i in enumerate(idx):          # TxHashes are short; the arena is rebuilt per rank
-        o, l = int(b.txhash_off[i]), int(b.txhash_len[i])
-        arena[off[j]:off[j] + l] = b.txhash_arena[o:o + l]
+    total = int(ln.sum())
+    if total:
+        src = np.repeat(b.txhash_off[idx].astype(np.int64) - off, ln) + np.arange(total, dtype=np.int64)
+        arena = b.txhash_arena[src]
+    else:
+        arena = np.zeros(1, np.uint8)
     a20 = (idx[:, None] * 20 + np.arange(20)).reshape(-1)
     a64 = (idx[:, None] * 64 + np.arange(64)).reshape(-1)
     return VoteBatch(n, height=b.height[idx], txhash_arena=arena, txhash_off=off.astype(np.uint32),
@@ -79,71 +86,53 @@ def subset(b: VoteBatch, idx: np.ndarray) -> VoteBatch:
                      txkey=None if b.txkey is None else b.txkey[(idx[:, None] * 32 + np.arange(32)).reshape(-1)])
 
 
+def batch_shards(b: VoteBatch, n_shards: int) -> np.ndarray:
+    """txv_shard_of of every vote of b, straight over its TxHash arena (a nil vote: the shard of
+    the empty TxHash, as the route takes it)"""
+    if n_shards <= 1 or b.n == 0:
+        return np.zeros(b.n, np.uint32)
+    ln = b.txhash_len if b.is_nil is None else np.where(b.is_nil != 0, 0, b.txhash_len).astype(np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint32)
+    out = np.zeros(b.n, np.uint32)
+    rc = lib().txv_shard_of(b.txhash_arena.ctypes.data, b.txhash_off.ctypes.data, ln.ctypes.data, b.n, n_shards,
+                            out.ctypes.data)
+    if rc:
+        raise ValueError(f"txv_shard_of failed ({rc})")
+    return out
+
+
 def route_admitted(b: VoteBatch, pool_status: np.ndarray, n_shards: int, ok: int = 0) -> List[np.ndarray]:
     """CheckTx ran on the owner (pool_status per vote, TXV_POOL_*); each admitted vote goes to the
-    rank owning its TxHash: per rank, the indices of its admitted votes in arrival order"""
-    adm = np.nonzero(np.asarray(pool_status) == ok)[0]
-    owner = shard_of([b.txhash(int(i)) for i in adm], n_shards)
-    return [adm[owner == r] for r in range(n_shards)]
+    rank owning its TxHash: per rank, the indices of its admitted votes in arrival order (the
+    index view of what txv_route_admitted packs)"""
+    adm = np.asarray(pool_status) == ok
+    owner = batch_shards(b, n_shards)
+    return [np.nonzero(adm & (owner == r))[0] for r in range(n_shards)]
 
 
-_COLS = (("height", np.int64, 1), ("txhash_off", np.uint32, 1), ("txhash_len", np.uint32, 1),
-         ("ts_sec", np.int64, 1), ("ts_nanos", np.int32, 1), ("addr", np.uint8, 20), ("addr_len", np.uint32, 1),
-         ("sig", np.uint8, 64), ("sig_len", np.uint32, 1), ("txkey", np.uint8, 32))
-
-
-def pack_batch(b: VoteBatch) -> np.ndarray:
-    """a batch as one byte buffer (n, arena length, then the columns): what the route sends"""
-    parts = [np.array([b.n, len(b.txhash_arena), int(b.txkey is not None)], np.int64).view(np.uint8)]
-    parts.append(b.txhash_arena)
-    for name, dt, _ in _COLS:
-        col = getattr(b, name)
-        if col is None:
-            continue
-        parts.append(np.ascontiguousarray(col, dt).view(np.uint8).reshape(-1))
-    return np.concatenate(parts)
-
-
-def unpack_batch(buf: np.ndarray) -> VoteBatch:
-    buf = np.ascontiguousarray(buf, np.uint8)
-    n, al, has_key = (int(x) for x in buf[:24].view(np.int64))
-    o = 24
-    arena = buf[o:o + al].copy()
-    o += al
-    cols = {}
-    for name, dt, w in _COLS:
-        if name == "txkey" and not has_key:
-            cols[name] = None
-            continue
-        nb = n * w * np.dtype(dt).itemsize
-        cols[name] = buf[o:o + nb].view(dt).copy()
-        o += nb
-    return VoteBatch(n, txhash_arena=arena, **cols)
-
-
-def scatter_batches(dist, batches: Optional[Sequence[VoteBatch]], src: int = 0, device: str = "cpu") -> VoteBatch:
-    """the route's exchange: rank src sends batches[r] to rank r (torch.distributed scatter of the
-    packed buffers, padded to the largest; gloo on the CPU, RCCL with device='cuda:k'); every
-    rank returns its own batch"""
+def scatter_routed(dist, bufs, metas: Optional[np.ndarray], src: int = 0, device: str = "cpu"):
+    """the route's exchange: rank src holds the n_shards route buffers ([n_shards, stride] uint8
+    torch tensor on `device`, from txv_route_admitted / txv_route_pack_host) and their metas; one
+    broadcast of the metas, then buffer r to rank r point to point, exactly meta[r].bytes of it
+    (RCCL over xGMI with device='cuda:k': the buffers never leave HBM).  Every rank returns (its
+    buffer as a uint8 tensor on `device`, its meta)."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
-    size = torch.zeros(world, dtype=torch.int64, device=device)
-    bufs = None
+    mt = torch.zeros(world * 4, dtype=torch.int64, device=device)
     if rank == src:
-        bufs = [pack_batch(b) for b in batches]
-        size = torch.tensor([len(x) for x in bufs], dtype=torch.int64, device=device)
-    dist.broadcast(size, src)
-    m = int(size.max().item())
-    out = torch.zeros(m, dtype=torch.uint8, device=device)
-    lst = None
+        mt.copy_(torch.from_numpy(np.ascontiguousarray(metas, ROUTE_META_DTYPE).view(np.int64).reshape(-1)).to(device))
+    dist.broadcast(mt, src)
+    allm = mt.cpu().numpy().view(ROUTE_META_DTYPE)
+    mine = allm[rank].copy()
+    size = int(mine["bytes"])
     if rank == src:
-        lst = []
-        for x in bufs:
-            t = torch.zeros(m, dtype=torch.uint8, device=device)
-            t[:len(x)] = torch.from_numpy(x).to(device)
-            lst.append(t)
-    dist.scatter(out, lst, src=src)
-    return unpack_batch(out[:int(size[rank].item())].cpu().numpy())
+        reqs = [dist.isend(bufs[r, :int(allm[r]["bytes"])].contiguous(), dst=r) for r in range(world) if r != src]
+        for q in reqs:
+            q.wait()
+        return bufs[src, :size], mine
+    out = torch.empty(size, dtype=torch.uint8, device=device)
+    dist.recv(out, src=src)
+    return out, mine
 
 
 def name_sets(txhashes: Sequence[bytes]) -> Dict[bytes, bytes]:

@@ -323,6 +323,40 @@ int txv_commit_state_pack_host(uint32_t n_sets, const uint8_t* committed, const 
                                uint32_t n_sets_cap, void* dst);
 int txv_commit_state_unpack(const void* src, uint32_t n_sets_cap, uint32_t* n_sets, uint8_t* committed, int64_t* sums,
                             uint8_t* digests, uint32_t cap);
+/* ---- multi-GPU ingest route (replaces the reactor -> TxFlow hand-off of
+ * txvotepool/reactor.go:170-190 -> txvotepool.go:187-261 -> txflow/service.go:123-166 across
+ * ranks).  TxVotePool is one order-dependent LRU with one Size cap, so CheckTx runs once for the
+ * node, on its owner (reactor) rank; each vote it admits belongs to the rank txv_shard_of names.
+ * txv_route_admitted packs, on the owner's GPU, every admitted vote (pool_status[i] ==
+ * TXV_POOL_OK; pool_status NULL = all) into the buffer of its rank r at dst_dev + r * stride, in
+ * arrival order, and returns each rank's txv_route_meta (the header's values: the receiving rank
+ * needs n, max_txhash_len and the byte count before it receives); synchronous (dst_dev is written
+ * when it returns).  stride >= txv_route_bytes(votes->n, TxHash arena extent, flags).  The
+ * node's collective then sends buffer r to rank r as it is (RCCL over xGMI: no host copy), and
+ * rank r runs its TxFlow chain straight from it: txv_submit_routed (a txv_submit_votes ticket,
+ * collected by txv_wait_votes; the buffer may be reused once the call returns).  Buffer layout
+ * (go-txflow_amd/csrc/route.h): a 64-byte header, then the txv_votes columns at 16-byte aligned
+ * offsets, TxHash offsets relative to the buffer's own arena; a nil vote (TXV_ROUTE_NIL) carries
+ * an empty TxHash and goes to the shard of "".  txv_route_view: a txv_votes view of a buffer
+ * copied to host memory (pointers into buf).  txv_route_pack_host: the same buffers built on the
+ * host (no GPU; the parity reference of the device route and the CPU test path). */
+#define TXV_ROUTE_TXKEY 0x1u   /* the buffers carry the TxKey column */
+#define TXV_ROUTE_NIL 0x2u     /* the buffers carry the is_nil column */
+typedef struct {
+  uint32_t n;                /* votes routed to the rank */
+  uint32_t max_txhash_len;   /* their longest TxHash (the receiver's SignBytes bound) */
+  uint32_t flags;            /* TXV_ROUTE_* */
+  uint32_t reserved;
+  uint64_t arena_bytes;      /* TxHash bytes */
+  uint64_t bytes;            /* the buffer's size (txv_route_bytes) */
+} txv_route_meta;
+uint64_t txv_route_bytes(uint32_t n, uint64_t arena_bytes, uint32_t flags);
+int txv_route_admitted(txv_ctx* ctx, const txv_votes* votes, const uint8_t* pool_status, uint32_t n_shards,
+                       void* dst_dev, uint64_t stride, txv_route_meta* meta_out);
+int txv_route_pack_host(const txv_votes* votes, const uint8_t* pool_status, uint32_t n_shards, void* dst,
+                        uint64_t stride, txv_route_meta* meta_out);
+int txv_route_view(const void* buf, uint64_t bytes, txv_votes* out);
+int txv_submit_routed(txv_ctx* ctx, const void* buf_dev, const txv_route_meta* meta, uint64_t* ticket);
 /* device pointer + byte size of the per-set committed bitmap (1 bit per tx-set id) */
 int txv_commit_bitmap(txv_ctx* ctx, void** dev_ptr, uint64_t* bytes);
 /* device-to-device copy of the commit bitmap into caller device memory (e.g. an RCCL buffer) */

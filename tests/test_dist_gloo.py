@@ -227,8 +227,9 @@ def test_pipelined_ring_keeps_every_steps_gathered_state():
 
 
 def _route_worker(rank, world, port, q):
-    """the ingest route (txflow_amd/sharding.py): CheckTx on the owner rank 0 (one TxVotePool: one
-    LRU, host-only here), its admitted votes scattered to the rank owning their TxHash, each rank's
+    """the ingest route: CheckTx on the owner rank 0 (one TxVotePool: one LRU, host-only here), its
+    admitted votes packed per rank in the C-ABI route layout (txv_route_pack_host, the host twin of
+    txv_route_admitted) and sent buffer r to rank r (sharding.scatter_routed), each rank's
     TxFlow (the oracle standing in for its GPU engine) over the votes it received in arrival
     order, the packed states (named by digest) all-gathered and merged"""
     try:
@@ -247,7 +248,7 @@ def _route_worker(rank, world, port, q):
         local_keys, seen = [], set()
         for s in range(0, len(votes), 90):
             part = votes[s:s + 90]
-            subs = None
+            bufs = metas = None
             if rank == 0:
                 vb = T.VoteBatch.from_votes([T.TxVote(Height=v["height"], TxHash=v["txhash"],
                                                       Timestamp=(v["ts_sec"], v["ts_nanos"]),
@@ -256,8 +257,11 @@ def _route_worker(rank, world, port, q):
                 sizes = np.array([T.txvote_size(v["height"], len(v["txhash"]), v["ts_sec"], v["ts_nanos"],
                                                 len(v["addr"]), len(v["sig"])) for v in part], np.uint32)
                 st = pool.check_keys(keys, sizes)
-                subs = [sharding.subset(vb, ix) for ix in sharding.route_admitted(vb, st, world, T.POOL_OK)]
-            mine = sharding.scatter_batches(dist, subs)
+                hb, metas = T.route_pack_host(vb, st, world)          # the C-ABI route layout, host-built
+                bufs = torch.from_numpy(hb)
+            buf, meta = sharding.scatter_routed(dist, bufs, metas)
+            mine = T.route_view(buf.numpy())
+            assert mine.n == int(meta["n"])
             flow.add_batch(mine, 2)
             for i in range(mine.n):
                 h = mine.txhash(i)

@@ -556,3 +556,42 @@ def test_set_validators_incremental_tables(oracle_lib):
         print("set_validators seconds:", times, "slots:", len(slots))
     finally:
         ctx.close()
+
+
+def test_event_ranks_after_flow_reallocated(oracle_lib):
+    """the fused status / event kernel (batches of <= 128 scan tiles) ranks commit events
+    by a look-back over words tagged with the batch stamp, and txv_set_validators restarts the
+    stamps (alloc_tally).  After each restart, new batches -- other votes, so other event counts
+    per tile -- must still list their commit events exactly in arrival order: the words an earlier
+    run left under the same tag are cleared when a new tag cycle starts (runtime.cpp run_slot)."""
+    import txflow_amd as T
+    ctx = T.Context(max_batch=1 << 15, max_txs=1 << 12, max_validators=16)
+    try:
+        rnd = random.Random(505)
+        seeds, pubs, addrs, votes, signer = _signed_set(ctx, T, 8, 36000, rnd, n_txs=2500)
+        powers = [1 + (i % 3) for i in range(len(pubs))]
+        for rep in range(3):
+            ctx.set_validators(pubs, powers, "test_chain_id")     # a new TxFlow: stamps start again
+            flow = oracle_lib.Flow(pubs, powers, b"test_chain_id")
+            order = list(range(len(votes)))
+            rnd.shuffle(order)
+            order = order[:24000 - 4000 * rep]
+            committed = set()
+            for lo in range(0, len(order), 12000):
+                part = [votes[i] for i in order[lo:lo + 12000]]
+                st, ev = ctx.add_votes(T.VoteBatch.from_votes(part))
+                ost, _, ofired = flow.add_votes([dict(height=v.Height, txhash=v.TxHash.encode(), ts_sec=v.Timestamp[0],
+                                                      ts_nanos=v.Timestamp[1], addr=v.ValidatorAddress, sig=v.Signature)
+                                                 for v in part])
+                exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+                assert np.array_equal(st, exp), f"rep {rep} batch {lo}"
+                first = []
+                for i in np.nonzero(ofired)[0]:
+                    h = part[int(i)].TxHash
+                    if h not in committed:
+                        committed.add(h)
+                        first.append(int(i))
+                assert [int(e["vote_index"]) for e in ev] == first, f"rep {rep} batch {lo}: event order"
+                assert len(first) > 50
+    finally:
+        ctx.close()

@@ -1,0 +1,172 @@
+"""The multi-GPU ingest route (include/txvote.h txv_route_admitted): the votes the
+owner rank's CheckTx admitted (txvotepool/txvotepool.go:187-261) go to the rank owning their
+TxHash (txv_shard_of: SHA-256(TxHash)[0] mod G), in arrival order, each rank's votes packed into
+one buffer (go-txflow_amd/csrc/route.h) that the node's collective sends as it is and the rank's
+TxFlow chain runs from (txv_submit_routed; reference hand-off txvotepool/reactor.go:170-190 ->
+txflow/service.go:123-166).
+
+CPU: the host packer (txv_route_pack_host) against the index view (sharding.route_admitted +
+sharding.subset): every rank's votes, in order, every column, is_nil and TxKey carried (ADVICE r5:
+the old packed route dropped is_nil).  GPU: the device packer byte-identical to the host packer
+(pool statuses, nil votes, empty / long TxHashes, G = 1..8), and the routed buffers' TryAddVote
+outcomes on a receiving context equal the sequential oracle's over the same votes."""
+import random
+
+import numpy as np
+import pytest
+
+import txflow_amd as T
+from txflow_amd import sharding
+
+
+def _batch(rnd, n, with_nil=True, long_frac=0.05):
+    votes = []
+    hashes = ["".join(rnd.choice("0123456789ABCDEF") for _ in range(64)) for _ in range(max(1, n // 7))]
+    for i in range(n):
+        r = rnd.random()
+        if with_nil and r < 0.03:
+            votes.append(None)
+            continue
+        if r < 0.03 + long_frac:
+            th = "".join(rnd.choice("0123456789abcdef") for _ in range(rnd.randrange(65, 200)))
+        elif r < 0.04 + long_frac:
+            th = ""
+        else:
+            th = rnd.choice(hashes)
+        votes.append(T.TxVote(Height=1 + (i % 3), TxHash=th, Timestamp=(1_700_000_000 + (i % 5), i + 1),
+                              TxKey=bytes(rnd.getrandbits(8) for _ in range(32)),
+                              ValidatorAddress=bytes(rnd.getrandbits(8) for _ in range(20 if r > 0.5 else rnd.randrange(21))),
+                              Signature=bytes(rnd.getrandbits(8) for _ in range(64 if r > 0.2 else rnd.randrange(70)))))
+    return T.VoteBatch.from_votes(votes)
+
+
+def _same(a: T.VoteBatch, b: T.VoteBatch):
+    assert a.n == b.n
+    for name in ("height", "ts_sec", "ts_nanos", "txhash_len", "addr", "addr_len", "sig", "sig_len", "txkey", "is_nil"):
+        x, y = getattr(a, name), getattr(b, name)
+        assert (x is None) == (y is None), name
+        if x is not None:
+            assert np.array_equal(x, y), name
+    for i in range(a.n):
+        assert a.txhash(i) == b.txhash(i)
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+def test_route_pack_host_matches_index_view(G):
+    rnd = random.Random(60 + G)
+    b = _batch(rnd, 3000)
+    st = np.array([rnd.choice([T.POOL_OK] * 6 + [T.POOL_ERR_IN_CACHE, T.POOL_ERR_TOO_LARGE]) for _ in range(b.n)],
+                  np.uint8)
+    bufs, metas = T.route_pack_host(b, st, G)
+    idx = sharding.route_admitted(b, st, G, T.POOL_OK)
+    assert sum(len(x) for x in idx) == int((st == T.POOL_OK).sum())
+    for r in range(G):
+        got = T.route_view(bufs[r, :int(metas[r]["bytes"])])
+        want = sharding.subset(b, idx[r])
+        # a nil vote travels with an empty TxHash
+        if want.is_nil is not None:
+            want.txhash_len = np.where(want.is_nil != 0, 0, want.txhash_len).astype(np.uint32)
+        _same(got, want)
+        assert int(metas[r]["n"]) == len(idx[r])
+        assert int(metas[r]["max_txhash_len"]) == (int(want.txhash_len.max()) if want.n else 0)
+        assert int(metas[r]["flags"]) == T.ROUTE_TXKEY | T.ROUTE_NIL
+    assert (bufs.shape[1] >= metas["bytes"]).all()
+
+
+def test_route_pack_host_all_admitted_and_empty():
+    rnd = random.Random(7)
+    b = _batch(rnd, 500, with_nil=False)
+    b.is_nil = None
+    bufs, metas = T.route_pack_host(b, None, 4)
+    assert int(metas["n"].sum()) == b.n
+    assert all(int(m["flags"]) == T.ROUTE_TXKEY for m in metas)
+    assert T.route_view(bufs[0, :int(metas[0]["bytes"])]).is_nil is None
+    e = T.VoteBatch.from_votes([])
+    bufs, metas = T.route_pack_host(e, None, 3)
+    assert (metas["n"] == 0).all() and all(T.route_view(bufs[r, :int(metas[r]["bytes"])]).n == 0 for r in range(3))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+def test_device_route_matches_host_pack(G):
+    import torch
+    ctx = T.Context(max_batch=1 << 16, max_txs=1 << 10, max_validators=8)
+    try:
+        rnd = random.Random(80 + G)
+        for n in (0, 1, 63, 4097, 50000):
+            b = _batch(rnd, n)
+            st = np.array([rnd.choice([T.POOL_OK] * 5 + [T.POOL_ERR_IN_CACHE]) for _ in range(b.n)], np.uint8)
+            for status in (st, None):
+                hb, hm = T.route_pack_host(b, status, G)
+                stride = T.route_stride(b)
+                dev = torch.zeros(G * stride, dtype=torch.uint8, device="cuda:0")
+                dm = ctx.route_admitted(b, status, G, dev.data_ptr(), stride)
+                assert np.array_equal(dm, hm), (n, G)
+                db = dev.view(G, stride).cpu().numpy()
+                for r in range(G):
+                    k = int(hm[r]["bytes"])
+                    assert np.array_equal(db[r, :k], hb[r, :k]), (n, G, r)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_routed_buffers_tally_like_the_oracle(oracle_lib):
+    """owner context: device-signed votes + replays / conflicts / corrupted ones, pool statuses
+    mixed in, routed to 3 ranks on the device; each rank's context runs its buffer from HBM
+    (txv_submit_routed) and its statuses + fired bits equal the sequential oracle's over that
+    rank's votes; the rank buffers' TxHash sets are disjoint"""
+    import torch
+    G = 3
+    owner = T.Context(max_batch=1 << 15, max_txs=1 << 11, max_validators=16)
+    ranks = []
+    try:
+        rnd = random.Random(303)
+        seeds = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(6)]
+        pubs = owner.keygen(seeds)
+        powers = [1, 2, 3, 1, 2, 3]
+        owner.set_validators(pubs, powers, "test_chain_id")
+        addrs, _ = owner.validator_info()
+        hashes = ["".join(rnd.choice("0123456789ABCDEF") for _ in range(64)) for _ in range(300)]
+        votes, signer = [], []
+        for i in range(6000):
+            vi = rnd.randrange(6)
+            votes.append(T.TxVote(Height=1, TxHash=rnd.choice(hashes), Timestamp=(1_700_000_000, i + 1),
+                                  ValidatorAddress=addrs[vi]))
+            signer.append(vi)
+        sigs = owner.sign_votes(T.VoteBatch.from_votes(votes), np.array(signer, np.uint32), "test_chain_id")
+        for v, s in zip(votes, sigs):
+            v.Signature = s.tobytes()
+        for i in range(0, 6000, 9):
+            s = bytearray(votes[i].Signature); s[7] ^= 2; votes[i].Signature = bytes(s)
+        votes += [votes[rnd.randrange(6000)] for _ in range(600)] + [None] * 20
+        rnd.shuffle(votes)
+        b = T.VoteBatch.from_votes(votes)
+        st = np.array([T.POOL_OK if rnd.random() < 0.9 else T.POOL_ERR_IN_CACHE for _ in range(b.n)], np.uint8)
+        stride = T.route_stride(b)
+        dev = torch.zeros(G * stride, dtype=torch.uint8, device="cuda:0")
+        metas = owner.route_admitted(b, st, G, dev.data_ptr(), stride)
+        idx = sharding.route_admitted(b, st, G, T.POOL_OK)
+        seen = []
+        for r in range(G):
+            ctx = T.Context(max_batch=1 << 15, max_txs=1 << 11, max_validators=16)
+            ranks.append(ctx)
+            ctx.set_validators(pubs, powers, "test_chain_id")
+            t = ctx.submit_routed(dev.data_ptr() + r * stride, metas[r])
+            got, ev = ctx.wait_votes(t)
+            mine = sharding.subset(b, idx[r])
+            flow = oracle_lib.Flow(pubs, powers, b"test_chain_id")
+            od = [dict(nil=True) if (mine.is_nil is not None and mine.is_nil[j]) else
+                  dict(height=int(mine.height[j]), txhash=mine.txhash(j), ts_sec=int(mine.ts_sec[j]),
+                       ts_nanos=int(mine.ts_nanos[j]), addr=mine.addr[20 * j:20 * j + int(mine.addr_len[j])].tobytes(),
+                       sig=mine.sig[64 * j:64 * j + int(mine.sig_len[j])].tobytes()) for j in range(mine.n)]
+            ost, _, ofired = flow.add_votes(od)
+            exp = ost.astype(np.uint8) | (ofired.astype(np.uint8) << 7)
+            assert np.array_equal(got, exp), f"rank {r}: {int(np.count_nonzero(got != exp))} mismatches"
+            seen.append(set(mine.txhash(j) for j in range(mine.n) if not mine.is_nil[j]))
+            assert int(metas[r]["n"]) == mine.n and mine.n > 1000
+        assert not (seen[0] & seen[1]) and not (seen[0] & seen[2]) and not (seen[1] & seen[2])
+    finally:
+        owner.close()
+        for c in ranks:
+            c.close()

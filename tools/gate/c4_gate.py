@@ -30,13 +30,17 @@ def main():
     ap.add_argument("--no-pool", action="store_true", help="feed txv_add_votes directly (no TxVotePool stage)")
     ap.add_argument("--pool-cache", type=int, default=1 << 20, help="TxVotePool CacheSize (LRU entries)")
     ap.add_argument("--pool-device", action="store_true", help="the pool's cache in HBM (TXV_POOL_DEVICE_CACHE)")
+    ap.add_argument("--table-w", type=int, default=0, choices=(0, 12, 16, 18, 20, 21),
+                    help="validator table window (0 = the library's automatic one; 21 = bench.py's C2 context)")
+    ap.add_argument("--base-w", type=int, default=0, choices=(0, 24, 26),
+                    help="base-point table window (0 = automatic; 26 = bench.py's C2 context)")
     args = ap.parse_args()
     import oracle
     oracle.build()
     import txflow_amd as T
     import adversarial as A
     ctx = T.Context(device=0, max_batch=args.batch + args.batch // 4, max_txs=1 << 17, max_validators=256,
-                    lane_votes=args.lane_votes)
+                    lane_votes=args.lane_votes, table_w=args.table_w or None, base_w=args.base_w)
     t0 = time.time()
     st = A.run_gate(ctx, args.votes, batch=args.batch, batches_per_epoch=args.batches_per_epoch,
                     threads=args.threads, log=lambda s: print(s, flush=True), pool_stage=not args.no_pool,
