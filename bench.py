@@ -236,9 +236,12 @@ def c5_commit_updates(wl, added_slots, commit_batch):
     keep = cb >= 0
     g, tx, cb = added_slots[keep], tx[keep], cb[keep]
     when = np.maximum(g // B, cb)
+    order = np.argsort(when, kind="stable")          # grouped by batch, stream order inside each
+    g, when = g[order], when[order]
+    cut = np.searchsorted(when, np.arange(len(wl.batches) + 1))
     out = []
     for k in range(len(wl.batches)):
-        idx = g[when == k]
+        idx = g[cut[k]:cut[k + 1]]
         if not len(idx):
             out.append(None)
             continue
@@ -293,6 +296,167 @@ def c5_pool_replay(wl, order, upd, got, cache_size):
     return ok
 
 
+def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, label: str = "", collect_dev: bool = False):
+    """One pipelined pass of the C5 stream (c5_streaming's timed pass, c5_long's one long pass):
+    CheckTx -> TryAddVote -> Update on the node's threads, two batches in flight.  Returns the
+    pass's report, the per-batch device stage times (collect_dev) and per-batch wall times
+    (submission and completion of every batch, for deciles / percentiles over a long pass)."""
+    import queue
+    import threading
+    import txflow_amd as T
+    submit, done, commit_t = [], [], {}
+    added = [0]
+
+    # Three threads, as a node's goroutines: Reactor.Receive -> CheckTx (ingest), the
+    # checkMaj23Routine submitting each checked batch (main), and a drain thread waiting each
+    # ticket in order as soon as it is submitted (commit events reported when the device is
+    # done, not when a third batch arrives).  At most two batches in flight (txv_submit_votes);
+    # ctypes releases the GIL inside every call.
+    import queue
+    import threading
+    checked = queue.Queue(maxsize=2)
+    tickets = queue.Queue()
+    slots = threading.Semaphore(C5_INFLIGHT)
+    pool_st = [None] * len(wl.batches)
+    dev_ms, dev_split = [], []        # per batch in the pipeline: slot events (HIP, per stream)
+    # CheckTx batches and Updates reach the pool from different threads (as the reactor's
+    # and TxFlow's goroutines do): the order the pool took them in is recorded for the
+    # oracle's replay
+    order, order_mu, max_size, upd_ms = [], threading.Lock(), [0], []
+
+    # CheckTx in two stages on two threads (txv_pool_prepare: keys on the GPU + TxVote.Size;
+    # txv_pool_check_keys: the order-dependent LRU / pool admission), so batch k+1's keys are
+    # hashed while batch k is admitted
+    prepared = queue.Queue(maxsize=2)
+    prep_ms, admit_ms = [], []
+
+    def prepare():
+        for k, b in enumerate(wl.batches):
+            ts = time.perf_counter()
+            if device_cache:                     # CheckTx submitted: decided on the GPU in order
+                with order_mu:
+                    tk = pool.check_submit(b)
+                    order.append(("c", k))
+                prepared.put((k, ts, time.perf_counter(), None, tk))
+            else:
+                keys, sizes = pool.prepare(b)
+                prepared.put((k, ts, time.perf_counter(), keys, sizes))
+        prepared.put(None)
+
+    def ingest():
+        while True:
+            item = prepared.get()
+            if item is None:
+                break
+            k, ts, tq, keys, sizes = item
+            tc = time.perf_counter()
+            if keys is None:                     # the submitted batch's statuses
+                ps = pool.check_wait(sizes)
+            else:
+                with order_mu:
+                    ps = pool.check_keys(keys, sizes)
+                    order.append(("c", k))
+            tp = time.perf_counter()
+            b = wl.batches[k]
+            b.is_nil = (ps != T.POOL_OK).view(np.uint8)    # not admitted: never reaches TxFlow
+            pool_st[k] = ps
+            prep_ms.append((tq - ts) * 1e3)
+            admit_ms.append((tp - tc) * 1e3)
+            checked.put((k, ts, tp))
+        checked.put(None)
+
+    def drain():
+        while True:
+            item = tickets.get()
+            if item is None:
+                return
+            k, tk = item
+            st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
+            te = time.perf_counter()
+            if collect_dev:               # the batch's stage times, before its ring slot is reused
+                dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
+                sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
+                if sp:
+                    dev_split.append(sp)
+            slots.release()
+            if upd[k] is not None:        # TxVotePool.Update with the batch's committed votes
+                tu = time.perf_counter()
+                with order_mu:
+                    pool.update_submit(1, upd[k])
+                    order.append(("u", k))
+                upd_ms.append((time.perf_counter() - tu) * 1e3)
+                max_size[0] = max(max_size[0], pool.Size())
+            done.append(te)
+            added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
+            for e in ev:
+                tx = int(wl.tx_of[k * batch + int(e["vote_index"])])
+                assert tx not in commit_t, "tx committed twice"
+                commit_t[tx] = te
+
+    t0 = time.perf_counter()
+    tpp = threading.Thread(target=prepare, daemon=True)
+    th = threading.Thread(target=ingest, daemon=True)
+    td = threading.Thread(target=drain, daemon=True)
+    tpp.start()
+    th.start()
+    td.start()
+    while True:
+        item = checked.get()
+        if item is None:
+            break
+        k, ts, tp = item
+        slots.acquire()
+        submit.append(ts)
+        tickets.put((k, ctx.submit_votes(wl.batches[k])))
+    tpp.join()
+    th.join()
+    tickets.put(None)
+    td.join()
+    added = added[0]
+    total = time.perf_counter() - t0
+    pool.sync()
+    pool_ok = c5_pool_replay(wl, order, upd, pool_st, C5_CACHE)
+    ok = pool_ok and added == wl.n_unique and len(commit_t) == wl.n_txs
+    lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
+    bl = (np.array(done) - np.array(submit)) * 1e3
+    allst = np.concatenate(pool_st)
+    stages = ("two pipelined stages with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE) -- "
+              "txv_pool_check_submit (Size on the host; keys, stack-distance decisions, the new cache and "
+              "the pool list in HBM -- the staged Update's pushes and removals first, then the batch's "
+              "appends -- enqueued on the GPU, one thread) and txv_pool_check_wait (the statuses, "
+              "another); p50_pool_check_ms = their sum per batch" if device_cache else
+              "two pipelined stages -- txv_pool_prepare (keys on the GPU + Size, one thread) and "
+              "txv_pool_check_keys (LRU + pool on the host, another); p50_pool_check_ms = their sum per batch")
+    out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "
+                       f"{wl.n - wl.n_unique} exact replays ({C5_REPLAY:.0%}, Appendix C) in {batch}-vote batches "
+                       f"through TxVotePool.CheckTx (CacheSize {C5_CACHE}) in {stages} -- + "
+                       f"txv_submit_votes/txv_wait_votes (TxFlow.TryAddVote for the admitted votes, two batches in "
+                       f"flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
+                       f"(txv_pool_update_submit, on the drain thread) with each batch's committed votes after its "
+                       f"commit events ({n_upd} votes per pass, txflow/service.go:224-227), pool Size cap "
+                       f"{C5_POOL_SIZE}; pool statuses checked against the oracle pool replaying the CheckTx "
+                       f"batches and Updates in the order the pool took them",
+           "correct": ok, "pool_matches_oracle": pool_ok, "votes_per_s": round(wl.n / total, 1),
+           "pool_size_cap": C5_POOL_SIZE, "pool_size_max": max_size[0],
+           "p50_pool_update_ms": round(float(np.median(upd_ms)), 3) if upd_ms else None,
+           "pool_status_counts": {"ok": int((allst == T.POOL_OK).sum()),
+                                  "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum()),
+                                  "full": int((allst == T.POOL_ERR_FULL).sum())},
+           "p50_pool_check_ms": round(float(np.median(np.array(prep_ms) + np.array(admit_ms))), 3),
+           "p50_pool_prepare_ms": round(float(np.median(prep_ms)), 3),
+           "p50_pool_admit_ms": round(float(np.median(admit_ms)), 3),
+           "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
+           "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
+           "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
+           "table_window": ctx.table_w, "base_window": ctx.base_w}
+    log(f"[c5] {'device' if device_cache else 'host'} cache {label}: "
+        f"{out['votes_per_s'] / 1e6:.1f}M votes/s, "
+        f"correct {ok} (pool {pool_ok}, added {added}/{wl.n_unique}, commits {len(commit_t)}/{wl.n_txs}, "
+        f"statuses {out['pool_status_counts']}, max Size {max_size[0]}; p50 ms prepare {out['p50_pool_prepare_ms']} "
+        f"admit {out['p50_pool_admit_ms']} update {out['p50_pool_update_ms']} batch {out['p50_batch_ms']})")
+    return out, dev_ms, dev_split, {"submit": submit, "done": done, "lat": lat, "bl": bl}
+
+
 def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     """C5: 1000 weighted validators, the stream (with Appendix C's 5% exact
     replays) cut into `batch`-vote batches fed through the pool ingest (txv_pool_check:
@@ -344,158 +508,11 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
         # ~20-45 ms, so a single host stall moves it; the median pass is reported, all three beside it
         runs = []
         for rep in range(-1, 3):
-            submit, done, commit_t = [], [], {}
-            added = [0]
-
-            # Three threads, as a node's goroutines: Reactor.Receive -> CheckTx (ingest), the
-            # checkMaj23Routine submitting each checked batch (main), and a drain thread waiting each
-            # ticket in order as soon as it is submitted (commit events reported when the device is
-            # done, not when a third batch arrives).  At most two batches in flight (txv_submit_votes);
-            # ctypes releases the GIL inside every call.
-            import queue
-            import threading
-            checked = queue.Queue(maxsize=2)
-            tickets = queue.Queue()
-            slots = threading.Semaphore(C5_INFLIGHT)
-            pool_st = [None] * len(wl.batches)
-            dev_ms, dev_split = [], []        # per batch in the pipeline: slot events (HIP, per stream)
-            # CheckTx batches and Updates reach the pool from different threads (as the reactor's
-            # and TxFlow's goroutines do): the order the pool took them in is recorded for the
-            # oracle's replay
-            order, order_mu, max_size, upd_ms = [], threading.Lock(), [0], []
-
-            # CheckTx in two stages on two threads (txv_pool_prepare: keys on the GPU + TxVote.Size;
-            # txv_pool_check_keys: the order-dependent LRU / pool admission), so batch k+1's keys are
-            # hashed while batch k is admitted
-            prepared = queue.Queue(maxsize=2)
-            prep_ms, admit_ms = [], []
-
-            def prepare():
-                for k, b in enumerate(wl.batches):
-                    ts = time.perf_counter()
-                    if device_cache:                     # CheckTx submitted: decided on the GPU in order
-                        with order_mu:
-                            tk = pool.check_submit(b)
-                            order.append(("c", k))
-                        prepared.put((k, ts, time.perf_counter(), None, tk))
-                    else:
-                        keys, sizes = pool.prepare(b)
-                        prepared.put((k, ts, time.perf_counter(), keys, sizes))
-                prepared.put(None)
-
-            def ingest():
-                while True:
-                    item = prepared.get()
-                    if item is None:
-                        break
-                    k, ts, tq, keys, sizes = item
-                    tc = time.perf_counter()
-                    if keys is None:                     # the submitted batch's statuses
-                        ps = pool.check_wait(sizes)
-                    else:
-                        with order_mu:
-                            ps = pool.check_keys(keys, sizes)
-                            order.append(("c", k))
-                    tp = time.perf_counter()
-                    b = wl.batches[k]
-                    b.is_nil = (ps != T.POOL_OK).view(np.uint8)    # not admitted: never reaches TxFlow
-                    pool_st[k] = ps
-                    prep_ms.append((tq - ts) * 1e3)
-                    admit_ms.append((tp - tc) * 1e3)
-                    checked.put((k, ts, tp))
-                checked.put(None)
-
-            def drain():
-                while True:
-                    item = tickets.get()
-                    if item is None:
-                        return
-                    k, tk = item
-                    st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
-                    te = time.perf_counter()
-                    if rep == 2:                  # the batch's stage times, before its ring slot is reused
-                        dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
-                        sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
-                        if sp:
-                            dev_split.append(sp)
-                    slots.release()
-                    if upd[k] is not None:        # TxVotePool.Update with the batch's committed votes
-                        tu = time.perf_counter()
-                        with order_mu:
-                            pool.update_submit(1, upd[k])
-                            order.append(("u", k))
-                        upd_ms.append((time.perf_counter() - tu) * 1e3)
-                        max_size[0] = max(max_size[0], pool.Size())
-                    done.append(te)
-                    added[0] += int(np.count_nonzero((st & 0x7F) == T.ADDED))
-                    for e in ev:
-                        tx = int(wl.tx_of[k * batch + int(e["vote_index"])])
-                        assert tx not in commit_t, "tx committed twice"
-                        commit_t[tx] = te
-
-            t0 = time.perf_counter()
-            tpp = threading.Thread(target=prepare, daemon=True)
-            th = threading.Thread(target=ingest, daemon=True)
-            td = threading.Thread(target=drain, daemon=True)
-            tpp.start()
-            th.start()
-            td.start()
-            while True:
-                item = checked.get()
-                if item is None:
-                    break
-                k, ts, tp = item
-                slots.acquire()
-                submit.append(ts)
-                tickets.put((k, ctx.submit_votes(wl.batches[k])))
-            tpp.join()
-            th.join()
-            tickets.put(None)
-            td.join()
-            added = added[0]
-            total = time.perf_counter() - t0
-            pool.sync()
-            pool_ok = c5_pool_replay(wl, order, upd, pool_st, C5_CACHE)
-            ok = pool_ok and added == wl.n_unique and len(commit_t) == wl.n_txs
-            lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
-            bl = (np.array(done) - np.array(submit)) * 1e3
-            allst = np.concatenate(pool_st)
-            stages = ("two pipelined stages with the LRU cache in HBM (TXV_POOL_DEVICE_CACHE) -- "
-                      "txv_pool_check_submit (Size on the host; keys, stack-distance decisions, the new cache and "
-                      "the pool list in HBM -- the staged Update's pushes and removals first, then the batch's "
-                      "appends -- enqueued on the GPU, one thread) and txv_pool_check_wait (the statuses, "
-                      "another); p50_pool_check_ms = their sum per batch" if device_cache else
-                      "two pipelined stages -- txv_pool_prepare (keys on the GPU + Size, one thread) and "
-                      "txv_pool_check_keys (LRU + pool on the host, another); p50_pool_check_ms = their sum per batch")
-            out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "
-                               f"{wl.n - wl.n_unique} exact replays ({C5_REPLAY:.0%}, Appendix C) in {batch}-vote batches "
-                               f"through TxVotePool.CheckTx (CacheSize {C5_CACHE}) in {stages} -- + "
-                               f"txv_submit_votes/txv_wait_votes (TxFlow.TryAddVote for the admitted votes, two batches in "
-                               f"flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
-                               f"(txv_pool_update_submit, on the drain thread) with each batch's committed votes after its "
-                               f"commit events ({n_upd} votes per pass, txflow/service.go:224-227), pool Size cap "
-                               f"{C5_POOL_SIZE}; pool statuses checked against the oracle pool replaying the CheckTx "
-                               f"batches and Updates in the order the pool took them",
-                   "correct": ok, "pool_matches_oracle": pool_ok, "votes_per_s": round(wl.n / total, 1),
-                   "pool_size_cap": C5_POOL_SIZE, "pool_size_max": max_size[0],
-                   "p50_pool_update_ms": round(float(np.median(upd_ms)), 3) if upd_ms else None,
-                   "pool_status_counts": {"ok": int((allst == T.POOL_OK).sum()),
-                                          "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum()),
-                                          "full": int((allst == T.POOL_ERR_FULL).sum())},
-                   "p50_pool_check_ms": round(float(np.median(np.array(prep_ms) + np.array(admit_ms))), 3),
-                   "p50_pool_prepare_ms": round(float(np.median(prep_ms)), 3),
-                   "p50_pool_admit_ms": round(float(np.median(admit_ms)), 3),
-                   "p50_batch_ms": round(float(np.median(bl)), 3), "p99_batch_ms": round(float(np.percentile(bl, 99)), 3),
-                   "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
-                   "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None,
-                   "table_window": ctx.table_w, "base_window": ctx.base_w}
+            out, dev_ms, dev_split, _ = c5_pass(ctx, wl, pool, upd, device_cache, batch, n_vals,
+                                                label=("pass %d" % rep) if rep >= 0 else "pipelined warm-up",
+                                                collect_dev=rep == 2)
             if rep >= 0:
                 runs.append(out)
-            log(f"[c5] {'device' if device_cache else 'host'} cache {'pass %d' % rep if rep >= 0 else 'pipelined warm-up'}: "
-                f"{out['votes_per_s'] / 1e6:.1f}M votes/s, "
-                f"correct {ok} (pool {pool_ok}, added {added}/{wl.n_unique}, commits {len(commit_t)}/{wl.n_txs}, "
-                f"statuses {out['pool_status_counts']}, max Size {max_size[0]}; p50 ms prepare {out['p50_pool_prepare_ms']} "
-                f"admit {out['p50_pool_admit_ms']} update {out['p50_pool_update_ms']} batch {out['p50_batch_ms']})")
             ctx.reset_flow()
             pool.flush()
         return runs, dev_ms, dev_split
@@ -591,14 +608,86 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     return out
 
 
+def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
+    """C5 as ONE long-running TxFlow (VERDICT r5 missing 3): the reference keeps every TxVoteSet for
+    the life of the node (TxVoteSets map, txflow/service.go:27, 200-209) and fires the commit side
+    effects on every later ADDED vote of a committed set (:216-232).  Here one context and one pool
+    take the whole stream -- `n_txs` x `n_vals` votes (+ Appendix C's 5% replays) in `batch`-vote
+    batches -- in one pipelined pass (c5_pass: CheckTx in HBM -> TryAddVote -> Update, two batches
+    in flight) with no txv_reset_flow: the set table, the cells and the accepted-vote arena keep
+    every set, sized up front (max_txs = n_txs + 64, max_accepted = min(max_txs x n_vals, 2^26)).
+    Reported: the pass's rate, p50 / p99 batch and commit latency over all its batches, the rate of
+    each tenth of the pass (flat = per-batch cost independent of the sets accumulated), and the
+    same size-independent checks as C5 (every distinct vote ADDED once, every tx committed once,
+    pool statuses equal to the oracle pool replaying the calls)."""
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    t_gen = time.perf_counter()
+    ctx = T.Context(device=device, max_batch=batch, max_txs=n_txs + 64, max_validators=n_vals)
+    ctx.bind_host_numa()
+    wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"] + 0x10, batch, replay=C5_REPLAY)
+    upd, n_upd = c5_prepare_updates(ctx, wl)
+    seen = set()
+    for b in wl.batches:
+        for col in (b.height, b.ts_sec, b.ts_nanos, b.txhash_off, b.txhash_len, b.addr, b.addr_len, b.sig,
+                    b.sig_len, b.txhash_arena, b.txkey):
+            if col is not None and col.nbytes and col.ctypes.data not in seen:
+                seen.add(col.ctypes.data)
+                ctx.host_register(col)
+    log(f"[c5-long] stream ready: {wl.n} votes in {len(wl.batches)} batches, {wl.n_txs} txs, {n_upd} committed votes "
+        f"for Update ({time.perf_counter() - t_gen:.1f} s)")
+    pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
+    for k in range(min(8, len(wl.batches))):        # warm-up: buffers and host tables, then a fresh flow and pool
+        b = wl.batches[k]
+        b.is_nil = (pool.check_batch(b) != T.POOL_OK).astype(np.uint8)
+        ctx.add_votes(b, ev_cap=b.n)
+        if upd[k] is not None:
+            pool.update(1, upd[k])
+    ctx.reset_flow()
+    pool.flush()
+    out, _, _, per = c5_pass(ctx, wl, pool, upd, True, batch, n_vals, label="one long pass")
+    n_sets = ctx.num_tx_sets()
+    pool.close()
+    ctx.close()
+    submit, done = np.array(per["submit"]), np.array(per["done"])
+    sizes = np.array([b.n for b in wl.batches], np.int64)
+    nb = len(done)
+    edges = [round(nb * d / 10) for d in range(11)]
+    dec = []
+    for d in range(10):
+        lo, hi = edges[d], edges[d + 1]
+        t0 = done[lo - 1] if lo > 0 else submit[0]
+        dec.append(round(float(sizes[lo:hi].sum() / (done[hi - 1] - t0)), 1))
+    bl = np.array(per["bl"])
+    res = {k: out[k] for k in ("correct", "pool_matches_oracle", "votes_per_s", "p50_batch_ms", "p99_batch_ms",
+                               "p50_commit_latency_ms", "p99_commit_latency_ms", "pool_size_max", "p50_pool_check_ms",
+                               "pool_status_counts", "table_window", "base_window")}
+    res.update({
+        "workload": f"C5 as one TxFlow: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "
+                    f"{wl.n - wl.n_unique} exact replays in {nb} batches of {batch}, one pass, no txv_reset_flow; "
+                    f"TxVotePool.CheckTx in HBM + TryAddVote + Update (as c5_streaming)",
+        "passes": 1, "votes": int(wl.n), "batches": nb, "tx_sets_at_end": int(n_sets),
+        "votes_per_s_by_decile": dec,
+        "decile_min_over_max": round(min(dec) / max(dec), 3),
+        "p90_batch_ms": round(float(np.percentile(bl, 90)), 3),
+        "flow_sizing": {"max_txs": n_txs + 64, "max_accepted": int(min((n_txs + 64) * n_vals, 1 << 26)),
+                        "note": "the reference never prunes TxVoteSets; here the flow holds max_txs sets and "
+                                "max_accepted accepted votes (sized for the node's horizon: 1M sets x 100 "
+                                "validators = 10 GB of HBM), and a batch that would exceed either fails with "
+                                "TXV_ECAPACITY and stops the flow until txv_reset_flow (DESIGN.md §3)"}})
+    res["correct"] = bool(res["correct"] and n_sets == wl.n_txs)
+    return res
+
+
 def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     """C5 from received wire bytes (SURVEY.md §8f.3 + §8a a15): the C5 stream as TxVoteMessage
     bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) per 64k-message batch through
     txv_ingest_decode (Reactor.Receive / decodeMsg on the GPU, keys and sizes computed there from
-    the decoded records), txv_ingest_admit (CheckTxWithInfo: LRU on the host; TryAddVote for the
-    admitted votes built on the device from the same records, enqueued) and txv_ingest_wait, on
-    three threads with up to three batches in flight: the wire bytes cross PCIe once, and batch
-    k+2 decodes while k+1 is checked and k's TxFlow chain runs (reactor.go:170-190 ->
+    the decoded records), txv_ingest_admit_submit (CheckTxWithInfo handed to the device: the LRU
+    cache and pool list in HBM, decided behind the decode), txv_ingest_admit_finish (the statuses;
+    TryAddVote for the admitted votes built on the device from the same records, enqueued) and
+    txv_ingest_wait, on four threads with up to three batches in flight: the wire bytes cross PCIe
+    once, and batch k+2 decodes while k+1 is checked and k's TxFlow chain runs (reactor.go:170-190 ->
     txvotepool.go:187-261 -> txflow/service.go:123-166).  Latency-to-commit of a tx = return of
     the wait that reported its commit event - the decode's start for the batch holding its first
     vote."""
@@ -626,21 +715,36 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         start, dec_ms, adm_ms, commit_t = [], [], [], {}
         state = {"added": 0, "ok": True}
         got, order, order_mu = [None] * len(wbs), [], threading.Lock()
-        decoded, admitted = queue.Queue(), queue.Queue()
+        decoded, submitted, admitted = queue.Queue(), queue.Queue(), queue.Queue()
         slots = threading.Semaphore(3)              # the library's ingest ring
+        sub_ms = []
 
-        # three goroutine-like stages: Receive (decode) -> CheckTx (admit) -> the commit drain (wait)
+        # four goroutine-like stages: Receive (decode) -> CheckTx handed to the device
+        # (txv_ingest_admit_submit) -> its statuses + the TxFlow chain enqueued
+        # (txv_ingest_admit_finish) -> the commit drain (wait)
         def admit():
             while True:
                 item = decoded.get()
+                if item is None:
+                    submitted.put(None)
+                    return
+                k, tk = item
+                ta = time.perf_counter()
+                with order_mu:
+                    pool.ingest_admit_submit(tk)
+                    order.append(("c", k))
+                sub_ms.append((time.perf_counter() - ta) * 1e3)
+                submitted.put((k, tk))
+
+        def finish():
+            while True:
+                item = submitted.get()
                 if item is None:
                     admitted.put(None)
                     return
                 k, tk = item
                 ta = time.perf_counter()
-                with order_mu:
-                    pool.ingest_admit(tk)
-                    order.append(("c", k))
+                pool.ingest_admit_finish(tk)
                 adm_ms.append((time.perf_counter() - ta) * 1e3)
                 admitted.put((k, tk))
 
@@ -664,8 +768,10 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                     commit_t[int(wl.tx_of[k * batch + int(e["vote_index"])])] = te
 
         ta_, td_ = threading.Thread(target=admit, daemon=True), threading.Thread(target=drain, daemon=True)
+        tf_ = threading.Thread(target=finish, daemon=True)
         t0 = time.perf_counter()
         ta_.start()
+        tf_.start()
         td_.start()
         for k, w in enumerate(wbs):
             slots.acquire()
@@ -676,6 +782,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
             decoded.put((k, tk))
         decoded.put(None)
         ta_.join()
+        tf_.join()
         td_.join()
         total = time.perf_counter() - t0
         pool.sync()
@@ -690,6 +797,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         runs.append({"votes_per_s": round(wl.n / total, 1), "pool_matches_oracle": pool_ok,
                      "correct": pool_ok and state["ok"] and state["added"] == wl.n_unique and len(commit_t) == wl.n_txs,
                      "p50_decode_ms": round(float(np.median(dec_ms)), 3),
+                     "p50_admit_submit_ms": round(float(np.median(sub_ms)), 3),
                      "p50_admit_ms": round(float(np.median(adm_ms)), 3),
                      "p50_commit_latency_ms": round(float(np.median(lat)), 3) if len(lat) else None,
                      "p99_commit_latency_ms": round(float(np.percentile(lat, 99)), 3) if len(lat) else None})
@@ -868,6 +976,8 @@ def main():
     ap.add_argument("--no-wire", action="store_true", help="skip the TxVoteMessage wire-decode leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host SoA) leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
+    ap.add_argument("--c5-long-txs", type=int, default=16384,
+                    help="txs of the one-long-TxFlow C5 pass (x 1000 validators: 16.4M votes by default; 0 = skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl = RCCL over xGMI (the measured path); gloo = CPU-side rehearsal of the N>1 "
                          "code path (with --same-gpu, several ranks on one GPU)")
@@ -885,6 +995,8 @@ def main():
         out = {"c5_streaming": c5_streaming(0, 1000, args.c5_txs, 65536)}
         if not args.no_wire:
             out["c5_wire"] = c5_wire_leg(0, 1000, args.c5_txs, 65536)
+        if args.c5_long_txs:
+            out["c5_long"] = c5_long(0, 1000, args.c5_long_txs, 65536)
         print(json.dumps(out), flush=True)
         return
 
@@ -1122,6 +1234,8 @@ def main():
             ctx.close()
             out["c5_streaming"] = c5_streaming(local, 1000, args.c5_txs, 65536)
             out["c5_wire"] = c5_wire_leg(local, 1000, args.c5_txs, 65536)
+            if args.c5_long_txs:
+                out["c5_long"] = c5_long(local, 1000, args.c5_long_txs, 65536)
         if world == 1 and not args.no_c1:
             out["c1"] = c1_leg(local, threads)
         print(json.dumps(out), flush=True)

@@ -1384,6 +1384,51 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
   return TXV_OK;
 }
 
+// The same, submitted (the wire ingest's split admit, runtime.cpp ingest_admit_submit): the
+// decisions are enqueued into the engine's next flight slot behind `after` and the call returns
+// with a pool ticket (*done = true) whose statuses txv_pool_check_wait collects -- so the admit
+// thread hands batch k+1's CheckTx to the GPU while batch k's statuses are still on their way.
+// The caps are checked against n pushes of bytes_bound bytes in all (upper bounds: the decode
+// has not reported yet), beside the batches in flight.  *done = false: the host path is needed.
+int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
+                              const uint8_t* d_valid, uint8_t valid_ok, uint32_t n, uint64_t bytes_bound, void* after,
+                              uint64_t* ticket, bool* done) {
+  *done = false;
+  *ticket = 0;
+  std::lock_guard<std::mutex> g(p->mu);
+  if (!dev_mode(p) || !n) return TXV_OK;
+  if (!dev_caps_ok(p, n, bytes_bound)) return TXV_OK;
+  const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+  int r;
+  if (p->pend_n && (p->pend_ctx != ctx || p->pend_n + n > pooldev_cap(p->dev)) && (r = flush_pending(p))) return r;
+  if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;
+  if ((r = list_to_dev(p, ctx))) return r;
+  const int slot = p->next_slot;                       // the staged Update entries' slot, if any
+  const uint32_t n_upd = p->pend_n;
+  if (!n_upd && (r = finish_slot(p, slot))) return r;  // its previous batch
+  p->pend_n = 0;
+  p->pend_slot = -1;
+  if ((r = pooldev_enqueue(ctx, p->dev, slot, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
+                           (p->cfg.flags & TXV_POOL_WAL) != 0, false, after, true, live_ub(p), n_upd)))
+    return r;
+  if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
+  p->next_slot = (slot + 1) % kPdRing;
+  txv_pool::Ticket t;
+  t.id = p->next_ticket;
+  t.n = n;
+  t.ctx = ctx;
+  t.slot = slot;
+  t.n_upd = n_upd;
+  t.pushes = n;
+  t.bytes = bytes_bound;
+  p->infl_len += (int64_t)t.pushes;
+  p->infl_bytes += (int64_t)t.bytes;
+  p->tickets.push_back(std::move(t));
+  *ticket = p->next_ticket++;
+  *done = true;
+  return TXV_OK;
+}
+
 // the pool's MaxMsgBytes (Reactor.Receive's decodeMsg cap, reactor.go:278-284)
 uint32_t txv_pool_max_msg_bytes(txv_pool* p) {
   std::lock_guard<std::mutex> g(p->mu);

@@ -288,7 +288,9 @@ struct txv_ctx {
     uint32_t *d_list = nullptr, *h_list = nullptr, *d_max = nullptr, *h_max = nullptr;
     hipEvent_t kev = nullptr;      // statuses, keys and sizes are back in pinned memory
     uint64_t ticket = 0;           // the batch in this slot (0 = free); guarded by mu
-    int phase = 0;                 // 0 free, 1 decoded (keys in flight), 2 admitted (TxFlow chain enqueued)
+    int phase = 0;                 // 0 free, 1 decoded (keys in flight), 3 CheckTx submitted to the device
+                                   // (pool_ticket), 2 admitted (TxFlow chain enqueued)
+    uint64_t pool_ticket = 0;      // phase 3: the pool's ticket (txv_pool_check_wait) of its decisions
     txv_pool* pool = nullptr;      // the pool the batch is checked against
     uint32_t n = 0, n_adm = 0;     // messages of the batch; votes the pool admitted (h_list)
     uint64_t wire_bytes = 0;       // bounds the decoded votes' summed TxVote.Size()
@@ -297,8 +299,9 @@ struct txv_ctx {
   } ing[kIngestRing];
   std::mutex ing_dec_mu;           // decodes one at a time (they hand out the tickets)
   std::mutex ing_adm_mu;           // admissions one at a time, in ticket order: pool order = TxFlow order
+  std::mutex ing_fin_mu;           // the admissions' second halves (ingest_admit_finish), in ticket order
   uint64_t ing_next = 1;           // next ticket to decode; guarded by mu
-  uint64_t ing_admit_next = 1;     // next ticket to admit; guarded by mu
+  uint64_t ing_admit_next = 1;     // next ticket to admit (submit half); guarded by mu
 };
 
 #define HIP_TRY(ctx, x)                                                                    \
@@ -3008,6 +3011,9 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
 }  // extern "C"
 
 uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
+int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
+                              const uint8_t* d_valid, uint8_t valid_ok, uint32_t n, uint64_t bytes_bound, void* after,
+                              uint64_t* ticket, bool* done);   // pool.cpp
 int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
                        const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, uint8_t valid_ok,
                        uint32_t n, uint64_t bytes_bound, void* after, uint8_t* status_out, bool* done);   // pool.cpp
@@ -3153,112 +3159,15 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
   return TXV_OK;
 }
 
-int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_status) {
-  if (!t) return TXV_EINVAL;
-  std::lock_guard<std::mutex> order(c->ing_adm_mu);
-  HostTimer ht(c->profile_host);
+// the admitted votes' TxFlow chain (the second half of an admission): their TxVote columns built
+// on the device from the decode records, run_slot enqueued; c->mu held by the caller.  From here
+// on the admitted votes are in the pool: the batch keeps its ticket whatever happens, and an
+// error is reported by its wait together with the votes it concerns
+void ingest_flow_stage(txv_ctx* c, uint64_t t, uint32_t n_adm) {
   const uint32_t j = (uint32_t)((t - 1) % kIngestRing);
   txv_ctx::Ingest& g = c->ing[j];
   Slot& s = c->slots[kIngestSlot + j];
-  {
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (g.ticket != t || g.phase != 1) { c->err = "unknown ingest ticket, or not in the decoded phase"; return TXV_ESTATE; }
-    if (t != c->ing_admit_next) { c->err = "ingest tickets must be admitted in decode order"; return TXV_ESTATE; }
-  }
-  const uint32_t n = g.n;
-  // TXV_POOL_DEVICE_CACHE: CheckTx for every decoded message decided on the device, from the keys,
-  // sizes and decode statuses the decode left in HBM, enqueued behind the decode on the key stream
-  // (txv_pool_check_dev waits for its statuses, and so for the decode's copies back too); not done
-  // when the pool's caps could bind with n votes of up to wire_bytes in all -- then the host path
-  uint32_t n_adm = 0;
-  bool dev_done = false;
-  std::unique_ptr<uint8_t[]> dst;
-  if (n) {
-    dst.reset(new uint8_t[n]);
-    const int rd = txv_pool_check_dev(g.pool, c, g.d_keys, g.d_sizes, g.d_status, reinterpret_cast<const uint8_t*>(g.h_keys),
-                                      g.h_sizes, TXV_WIRE_OK, n, g.wire_bytes, (void*)g.kev, dst.get(), &dev_done);
-    if (rd) {   // the pool is unchanged: the ticket ends here (no wait)
-      (void)hipEventSynchronize(g.kev);
-      std::lock_guard<std::mutex> lk(c->mu);
-      g.phase = 0;
-      g.ticket = 0;
-      c->ing_admit_next = t + 1;
-      return rd;
-    }
-  }
-  if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
-  ht.mark("keys_wait");
-  // CheckTxWithInfo over the decoded messages in arrival order (the others never reach it).  When
-  // every message decoded (the usual case) the pinned keys / sizes are the pool's input as they
-  // are; otherwise the decoded ones are compacted first.
-  if (wire_status && n) memcpy(wire_status, g.h_status, n);
-  if (n) {
-    if (dev_done) {
-      if (pool_status) memcpy(pool_status, dst.get(), n);
-      for (uint32_t i = 0; i < n; ++i) {
-        g.h_list[n_adm] = i;
-        n_adm += dst[i] == TXV_POOL_OK;
-      }
-    }
-  }
-  if (!dev_done) {
-  std::atomic<uint32_t> bad{0};
-  c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
-    uint32_t b = 0;
-    for (uint32_t i = lo; i < hi; ++i) b += g.h_status[i] != TXV_WIRE_OK;
-    if (b) bad.fetch_add(b, std::memory_order_relaxed);
-  }, 16384);
-  const bool all_ok = bad.load() == 0;
-  std::vector<uint32_t> ok;
-  std::vector<uint8_t> keys_c;
-  std::vector<uint32_t> sizes_c;
-  const uint8_t* keys = reinterpret_cast<const uint8_t*>(g.h_keys);
-  const uint32_t* sizes = g.h_sizes;
-  uint32_t m = n;
-  if (!all_ok) {
-    ok.reserve(n);
-    for (uint32_t i = 0; i < n; ++i)
-      if (g.h_status[i] == TXV_WIRE_OK) ok.push_back(i);
-    m = (uint32_t)ok.size();
-    keys_c.resize((size_t)m * 32);
-    sizes_c.resize(m);
-    c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t q = lo; q < hi; ++q) {
-        memcpy(keys_c.data() + (size_t)q * 32, g.h_keys + (size_t)ok[q] * 8, 32);
-        sizes_c[q] = g.h_sizes[ok[q]];
-      }
-    }, 8192);
-    keys = keys_c.data();
-    sizes = sizes_c.data();
-  }
-  std::unique_ptr<uint8_t[]> pst(new uint8_t[std::max<uint32_t>(m, 1)]);
-  int r = txv_pool_check_keys(g.pool, c, keys, sizes, m, pst.get());
-  if (r) {   // the pool is unchanged: the ticket ends here (no wait)
-    std::lock_guard<std::mutex> lk(c->mu);
-    g.phase = 0;
-    g.ticket = 0;
-    c->ing_admit_next = t + 1;
-    return r;
-  }
-  if (all_ok) {
-    if (pool_status && m) memcpy(pool_status, pst.get(), m);
-    for (uint32_t q = 0; q < m; ++q) {
-      g.h_list[n_adm] = q;
-      n_adm += pst[q] == TXV_POOL_OK;
-    }
-  } else {
-    if (pool_status) memset(pool_status, TXV_POOL_NOT_CHECKED, n);
-    for (uint32_t q = 0; q < m; ++q) {
-      if (pool_status) pool_status[ok[q]] = pst[q];
-      if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
-    }
-  }
-  }
   g.n_adm = n_adm;
-  ht.mark("pool");
-  // from here on the admitted votes are in the pool: the batch keeps its ticket whatever happens,
-  // and an error is reported by its wait together with the votes it concerns
-  std::lock_guard<std::mutex> lk(c->mu);
   auto flow_stage = [&]() -> int {
     if (!n_adm) return TXV_OK;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -3284,10 +3193,178 @@ int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_sta
     g.flow_err = rf;
     g.flow_msg = c->err.copy();
   }
-  ht.mark("flow_enqueue");
   g.phase = 2;
-  c->ing_admit_next = t + 1;
+}
+
+// the ticket ends without TxFlow (CheckTx failed before touching the pool); c->mu held
+void ingest_drop(txv_ctx* c, txv_ctx::Ingest& g, uint64_t t) {
+  g.phase = 0;
+  g.ticket = 0;
+  if (c->ing_admit_next == t) c->ing_admit_next = t + 1;
+}
+
+// an earlier ticket's admission is submitted to the device but not finished (c->mu held)
+bool ingest_earlier_pending(const txv_ctx* c, uint64_t t) {
+  for (const auto& o : c->ing)
+    if (o.phase == 3 && o.ticket && o.ticket < t) return true;
+  return false;
+}
+
+// First half of an admission (tickets in decode order): with TXV_POOL_DEVICE_CACHE and caps that
+// cannot bind, CheckTx for every decoded message is enqueued on the device from the keys, sizes
+// and decode statuses the decode left in HBM, behind the decode (txv_pool_check_dev_submit), and
+// the call returns (phase 3) -- ingest_admit_finish collects the statuses.  Otherwise the whole
+// admission runs here on the host path (phase 2 when it returns).
+int ingest_admit_submit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_status, bool* pending) {
+  *pending = false;
+  if (!t) return TXV_EINVAL;
+  std::lock_guard<std::mutex> order(c->ing_adm_mu);
+  HostTimer ht(c->profile_host);
+  const uint32_t j = (uint32_t)((t - 1) % kIngestRing);
+  txv_ctx::Ingest& g = c->ing[j];
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (g.ticket != t || g.phase != 1) { c->err = "unknown ingest ticket, or not in the decoded phase"; return TXV_ESTATE; }
+    if (t != c->ing_admit_next) { c->err = "ingest tickets must be admitted in decode order"; return TXV_ESTATE; }
+  }
+  const uint32_t n = g.n;
+  if (n) {
+    bool dev = false;
+    uint64_t pt = 0;
+    const int rd = txv_pool_check_dev_submit(g.pool, c, g.d_keys, g.d_sizes, g.d_status, TXV_WIRE_OK, n, g.wire_bytes,
+                                             (void*)g.kev, &pt, &dev);
+    if (rd) {   // the pool is unchanged: the ticket ends here (no wait)
+      (void)hipEventSynchronize(g.kev);
+      std::lock_guard<std::mutex> lk(c->mu);
+      ingest_drop(c, g, t);
+      return rd;
+    }
+    if (dev) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      g.pool_ticket = pt;
+      g.phase = 3;
+      c->ing_admit_next = t + 1;
+      *pending = true;
+      ht.mark("pool_submit");
+      return TXV_OK;
+    }
+  }
+  // the host path: CheckTxWithInfo over the decoded messages in arrival order on the host (the
+  // others never reach it), every earlier submitted admission finished first (pool order)
+  {
+    std::lock_guard<std::mutex> fin(c->ing_fin_mu);
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (ingest_earlier_pending(c, t)) { c->err = "finish the earlier ingest admissions before a host-path batch"; return TXV_ESTATE; }
+    }
+    if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
+    ht.mark("keys_wait");
+    if (wire_status && n) memcpy(wire_status, g.h_status, n);
+    std::atomic<uint32_t> bad{0};
+    c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      uint32_t b = 0;
+      for (uint32_t i = lo; i < hi; ++i) b += g.h_status[i] != TXV_WIRE_OK;
+      if (b) bad.fetch_add(b, std::memory_order_relaxed);
+    }, 16384);
+    const bool all_ok = bad.load() == 0;
+    std::vector<uint32_t> ok;
+    std::vector<uint8_t> keys_c;
+    std::vector<uint32_t> sizes_c;
+    const uint8_t* keys = reinterpret_cast<const uint8_t*>(g.h_keys);
+    const uint32_t* sizes = g.h_sizes;
+    uint32_t m = n;
+    if (!all_ok) {
+      ok.reserve(n);
+      for (uint32_t i = 0; i < n; ++i)
+        if (g.h_status[i] == TXV_WIRE_OK) ok.push_back(i);
+      m = (uint32_t)ok.size();
+      keys_c.resize((size_t)m * 32);
+      sizes_c.resize(m);
+      c->pool->parallel_for(m, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t q = lo; q < hi; ++q) {
+          memcpy(keys_c.data() + (size_t)q * 32, g.h_keys + (size_t)ok[q] * 8, 32);
+          sizes_c[q] = g.h_sizes[ok[q]];
+        }
+      }, 8192);
+      keys = keys_c.data();
+      sizes = sizes_c.data();
+    }
+    std::unique_ptr<uint8_t[]> pst(new uint8_t[std::max<uint32_t>(m, 1)]);
+    int r = txv_pool_check_keys(g.pool, c, keys, sizes, m, pst.get());
+    if (r) {   // the pool is unchanged: the ticket ends here (no wait)
+      std::lock_guard<std::mutex> lk(c->mu);
+      ingest_drop(c, g, t);
+      return r;
+    }
+    uint32_t n_adm = 0;
+    if (all_ok) {
+      if (pool_status && m) memcpy(pool_status, pst.get(), m);
+      for (uint32_t q = 0; q < m; ++q) {
+        g.h_list[n_adm] = q;
+        n_adm += pst[q] == TXV_POOL_OK;
+      }
+    } else {
+      if (pool_status) memset(pool_status, TXV_POOL_NOT_CHECKED, n);
+      for (uint32_t q = 0; q < m; ++q) {
+        if (pool_status) pool_status[ok[q]] = pst[q];
+        if (pst[q] == TXV_POOL_OK) g.h_list[n_adm++] = ok[q];
+      }
+    }
+    ht.mark("pool");
+    std::lock_guard<std::mutex> lk(c->mu);
+    ingest_flow_stage(c, t, n_adm);
+    c->ing_admit_next = t + 1;
+    ht.mark("flow_enqueue");
+  }
   return TXV_OK;
+}
+
+// Second half (tickets in order): the submitted CheckTx's statuses (txv_pool_check_wait, no
+// context lock held while the GPU finishes), the admitted messages listed, their TxFlow chain
+// enqueued (phase 2).  A batch the first half admitted on the host is finished already.
+int ingest_admit_finish(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!t) return TXV_EINVAL;
+  std::lock_guard<std::mutex> order(c->ing_fin_mu);
+  HostTimer ht(c->profile_host);
+  const uint32_t j = (uint32_t)((t - 1) % kIngestRing);
+  txv_ctx::Ingest& g = c->ing[j];
+  uint64_t pt;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (g.ticket != t || (g.phase != 3 && g.phase != 2)) { c->err = "unknown ingest ticket, or not submitted for admission"; return TXV_ESTATE; }
+    if (g.phase == 2) return TXV_OK;
+    if (ingest_earlier_pending(c, t)) { c->err = "ingest admissions must be finished in ticket order"; return TXV_ESTATE; }
+    pt = g.pool_ticket;
+  }
+  const uint32_t n = g.n;
+  std::unique_ptr<uint8_t[]> dst(new uint8_t[std::max<uint32_t>(n, 1)]);
+  const int rw = txv_pool_check_wait(g.pool, pt, dst.get());
+  ht.mark("pool_wait");
+  HIP_TRY(c, hipEventSynchronize(g.kev));   // (ended before the decisions began)
+  if (wire_status && n) memcpy(wire_status, g.h_status, n);
+  if (rw) {   // the device decisions failed: nothing of the batch reached TxFlow
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->err = "ingest: the device CheckTx of the batch failed";
+    ingest_drop(c, g, t);
+    return rw;
+  }
+  if (pool_status) memcpy(pool_status, dst.get(), n);
+  uint32_t n_adm = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    g.h_list[n_adm] = i;
+    n_adm += dst[i] == TXV_POOL_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  ingest_flow_stage(c, t, n_adm);
+  ht.mark("flow_enqueue");
+  return TXV_OK;
+}
+
+int ingest_admit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* pool_status) {
+  bool pending = false;
+  int r = ingest_admit_submit(c, t, wire_status, pool_status, &pending);
+  if (r || !pending) return r;
+  return ingest_admit_finish(c, t, wire_status, pool_status);
 }
 
 int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
@@ -3374,6 +3451,17 @@ int txv_ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wir
 int txv_ingest_admit(txv_ctx* c, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status) {
   if (!c) return TXV_EINVAL;
   return ingest_admit(c, ticket, wire_status, pool_status);
+}
+
+int txv_ingest_admit_submit(txv_ctx* c, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!c) return TXV_EINVAL;
+  bool pending = false;
+  return ingest_admit_submit(c, ticket, wire_status, pool_status, &pending);
+}
+
+int txv_ingest_admit_finish(txv_ctx* c, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status) {
+  if (!c) return TXV_EINVAL;
+  return ingest_admit_finish(c, ticket, wire_status, pool_status);
 }
 
 int txv_ingest_submit(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,

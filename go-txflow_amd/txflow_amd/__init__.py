@@ -168,6 +168,8 @@ def lib():
             "txv_ingest_decode": ([vp, vp, vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(ctypes.c_uint64)],
                                   ctypes.c_int),
             "txv_ingest_admit": ([vp, ctypes.c_uint64, vp, vp], ctypes.c_int),
+            "txv_ingest_admit_submit": ([vp, ctypes.c_uint64, vp, vp], ctypes.c_int),
+            "txv_ingest_admit_finish": ([vp, ctypes.c_uint64, vp, vp], ctypes.c_int),
             "txv_encode_msgs": ([ctypes.POINTER(_Votes), vp, vp, vp, vp, ctypes.c_uint64, vp, vp,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "txv_query_txs": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], ctypes.c_int),
@@ -217,7 +219,7 @@ EXPORTED_SYMBOLS = [
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
     "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare",
     "txv_ingest_decode", "txv_ingest_admit", "txv_route_bytes", "txv_route_admitted", "txv_route_pack_host",
-    "txv_route_view", "txv_submit_routed"]
+    "txv_route_view", "txv_submit_routed", "txv_ingest_admit_submit", "txv_ingest_admit_finish"]
 
 
 # ------------------------------------------------------------------ host-only helpers
@@ -1109,6 +1111,25 @@ class TxVotePool:
         ws = np.zeros(max(tk.n, 1), np.uint8)
         ps = np.zeros(max(tk.n, 1), np.uint8)
         ctx._chk(lib().txv_ingest_admit(ctx._h, tk.ticket, ws.ctypes.data, ps.ctypes.data), "txv_ingest_admit")
+        tk.wire_status, tk.pool_status = ws[:tk.n], ps[:tk.n]
+        return tk
+
+    def ingest_admit_submit(self, tk: IngestTicket) -> IngestTicket:
+        """txv_ingest_admit_submit: the batch's CheckTx handed to the device (returns at once), or
+        the whole admission on the host path; ingest_admit_finish next"""
+        ctx = self._ctx_or_raise("ingest_admit_submit")
+        tk.wire_status = np.zeros(max(tk.n, 1), np.uint8)
+        tk.pool_status = np.zeros(max(tk.n, 1), np.uint8)
+        ctx._chk(lib().txv_ingest_admit_submit(ctx._h, tk.ticket, tk.wire_status.ctypes.data, tk.pool_status.ctypes.data),
+                 "txv_ingest_admit_submit")
+        return tk
+
+    def ingest_admit_finish(self, tk: IngestTicket) -> IngestTicket:
+        """txv_ingest_admit_finish: the submitted CheckTx's statuses in, the admitted votes' TxFlow
+        chain enqueued; fills the ticket's wire / pool statuses"""
+        ctx = self._ctx_or_raise("ingest_admit_finish")
+        ws, ps = tk.wire_status, tk.pool_status
+        ctx._chk(lib().txv_ingest_admit_finish(ctx._h, tk.ticket, ws.ctypes.data, ps.ctypes.data), "txv_ingest_admit_finish")
         tk.wire_status, tk.pool_status = ws[:tk.n], ps[:tk.n]
         return tk
 

@@ -596,6 +596,17 @@ int txv_ingest_submit(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_
 int txv_ingest_decode(txv_ctx* ctx, txv_pool* pool, const uint8_t* wire, uint64_t wire_bytes,
                       const uint64_t* msg_off, const uint32_t* msg_len, uint32_t n, uint64_t* ticket);
 int txv_ingest_admit(txv_ctx* ctx, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status);
+/* txv_ingest_admit in its two halves, for a fourth stage (the admit thread waited for
+ * each batch's pool statuses): txv_ingest_admit_submit hands the batch's CheckTx to the device (the
+ * pool keeps its cache in HBM and the caps cannot bind: the decisions are enqueued behind the
+ * decode in the pool engine's next flight slot) and returns; txv_ingest_admit_finish (tickets in
+ * order) collects the statuses, lists the admitted messages and enqueues their TxFlow chain.
+ * wire_status / pool_status are final when the finish returns (when the submit had to run the
+ * host path, the whole admission is done by the submit -- it requires every earlier submitted
+ * admission finished, else TXV_ESTATE -- and the finish returns at once).  A registered wire
+ * buffer is read until the finish returns. */
+int txv_ingest_admit_submit(txv_ctx* ctx, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status);
+int txv_ingest_admit_finish(txv_ctx* ctx, uint64_t ticket, uint8_t* wire_status, uint8_t* pool_status);
 int txv_ingest_wait(txv_ctx* ctx, uint64_t ticket, uint8_t* flow_status, txv_commit_event* ev_out, uint32_t ev_cap,
                     uint32_t* n_ev);
 

@@ -315,7 +315,7 @@ def test_host_encoder_matches_oracle():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["sync", "pipelined", "pipelined_registered", "three_stage", "sync_device",
-                                  "three_stage_device"])
+                                  "three_stage_device", "four_stage", "four_stage_device"])
 def test_gpu_ingest_chain_matches_oracle(mode):
     """txv_ingest_msgs (Reactor.Receive -> CheckTxWithInfo -> TryAddVote with the decoded votes
     kept in HBM) over batches of received messages against the oracle's decoder, pool and
@@ -330,7 +330,9 @@ def test_gpu_ingest_chain_matches_oracle(mode):
     txflow/service.go:123-166); "pipelined_registered": the same with the receive buffers
     registered (txv_host_register: the wire bytes are DMA'd without a staging copy); "three_stage":
     txv_ingest_decode / txv_ingest_admit / txv_ingest_wait with three batches in the ring (batch
-    k+2 decoded while k+1 is admitted and k's TxFlow chain runs); "*_device": the same with the
+    k+2 decoded while k+1 is admitted and k's TxFlow chain runs); "four_stage": the admission in
+    its two halves (txv_ingest_admit_submit / _finish), batches k+1 and k+2 submitted to the pool
+    before batch k's statuses are collected; "*_device": the same with the
     pool's cache in HBM (TXV_POOL_DEVICE_CACHE: CheckTx decided on the GPU from the keys, sizes and
     decode statuses the decode left there)."""
     import txflow_amd as T
@@ -411,6 +413,19 @@ def test_gpu_ingest_chain_matches_oracle(mode):
                 adm.append((kk, pool.ingest_admit(tk)))
             for kk, tk in adm:
                 results[kk] = pool.ingest_wait(tk)
+        elif mode == "four_stage":
+            wbs = [T.WireBatch(part) for part in parts]
+            for w in wbs:
+                ctx.host_register(w.wire)
+            results, ring = [None] * nb, []
+            for k, w in enumerate(wbs):
+                tk = pool.ingest_decode(w)
+                ring.append((k, pool.ingest_admit_submit(tk)))
+                if len(ring) == 3:
+                    kk, tk = ring.pop(0)
+                    results[kk] = pool.ingest_wait(pool.ingest_admit_finish(tk))
+            for kk, tk in ring:
+                results[kk] = pool.ingest_wait(pool.ingest_admit_finish(tk))
         else:
             results, inflight = [], []
             wbs = [T.WireBatch(part) for part in parts]
