@@ -679,6 +679,82 @@ def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
     return res
 
 
+def owner_route_leg(device: int, n_vals: int, n_txs: int, batch: int, n_ranks: int = 8):
+    """The multi-GPU ingest's owner rank on one GPU: every C5 batch
+    through TxVotePool.CheckTx with the cache in HBM (txv_pool_check_submit / _wait) and its
+    admitted votes packed for `n_ranks` ranks on the device (txv_route_admitted), on two threads
+    (batch k+1's CheckTx enqueued while batch k is routed).  Its rate bounds what a node of
+    n_ranks GPUs can admit when one owner runs CheckTx for all of them; the ranks' scatter and
+    TxFlow chains are not in it.  Checked: every admitted vote routed exactly once (the metas sum
+    to the admitted count), one batch's device buffers byte-identical to txv_route_pack_host."""
+    import queue
+    import threading
+    import torch
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    ctx = T.Context(device=device, max_batch=batch, max_txs=64, max_validators=n_vals)
+    ctx.bind_host_numa()
+    wl = StreamWorkload(ctx, n_vals, n_txs, SEEDS["c5"], batch, replay=C5_REPLAY)
+    seen = set()
+    for b in wl.batches:
+        b.is_nil = None
+        for col in (b.height, b.ts_sec, b.ts_nanos, b.txhash_off, b.txhash_len, b.addr, b.addr_len, b.sig,
+                    b.sig_len, b.txhash_arena, b.txkey):
+            if col is not None and col.nbytes and col.ctypes.data not in seen:
+                seen.add(col.ctypes.data)
+                ctx.host_register(col)
+    stride = max(T.route_stride(b) for b in wl.batches)
+    buf = torch.zeros(n_ranks * stride, dtype=torch.uint8, device=f"cuda:{device}")
+    pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
+    # parity of one batch: device route == host route (untimed)
+    st0 = pool.check_batch(wl.batches[0])
+    m0 = ctx.route_admitted(wl.batches[0], st0, n_ranks, buf.data_ptr(), stride)
+    hb, hm = T.route_pack_host(wl.batches[0], st0, n_ranks)
+    db = buf.view(n_ranks, stride).cpu().numpy()
+    same = bool(np.array_equal(m0, hm)) and all(np.array_equal(db[r, :int(hm[r]["bytes"])], hb[r, :int(hm[r]["bytes"])])
+                                                 for r in range(n_ranks))
+    pool.flush()
+    runs = []
+    for rep in range(3):
+        tickets = queue.Queue(maxsize=2)
+        routed, admitted, route_ms = [0], [0], []
+
+        def submit():
+            for b in wl.batches:
+                tickets.put((b, pool.check_submit(b)))
+            tickets.put(None)
+
+        t0 = time.perf_counter()
+        th = threading.Thread(target=submit, daemon=True)
+        th.start()
+        while True:
+            item = tickets.get()
+            if item is None:
+                break
+            b, tk = item
+            ps = pool.check_wait(tk)
+            tr = time.perf_counter()
+            m = ctx.route_admitted(b, ps, n_ranks, buf.data_ptr(), stride)
+            route_ms.append((time.perf_counter() - tr) * 1e3)
+            routed[0] += int(m["n"].sum())
+            admitted[0] += int((ps == T.POOL_OK).sum())
+        th.join()
+        total = time.perf_counter() - t0
+        runs.append({"votes_per_s": round(wl.n / total, 1), "p50_route_ms": round(float(np.median(route_ms)), 3),
+                     "routed": routed[0], "admitted": admitted[0]})
+        pool.flush()
+    pool.close()
+    ctx.close()
+    runs.sort(key=lambda r: r["votes_per_s"])
+    out = dict(runs[1])
+    out.update({"workload": f"owner rank: the C5 stream ({wl.n} votes, {batch}-vote batches, {n_vals} validators) "
+                            f"through TxVotePool.CheckTx (cache in HBM) + txv_route_admitted to {n_ranks} ranks",
+                "n_ranks": n_ranks, "votes_per_s_passes": [r["votes_per_s"] for r in runs],
+                "device_route_equals_host": same,
+                "correct": same and all(r["routed"] == r["admitted"] for r in runs)})
+    return out
+
+
 def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
     """C5 from received wire bytes (SURVEY.md §8f.3 + §8a a15): the C5 stream as TxVoteMessage
     bytes (the sender's cdc.MarshalBinaryBare, txv_encode_msgs) per 64k-message batch through
@@ -973,6 +1049,7 @@ def main():
                     help="votes per lane sharing one inversion in the W>=8 verify kernel (0 = library default)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming-latency leg")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 leg")
+    ap.add_argument("--no-route", action="store_true", help="skip the owner-rank CheckTx + ingest-route leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the TxVoteMessage wire-decode leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host SoA) leg")
     ap.add_argument("--c5-txs", type=int, default=2048)
@@ -1003,6 +1080,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and not args.no_route:
+        # torch's HIP runtime first, before any txv context (the route leg's device buffers are
+        # torch tensors; tests/conftest.py, the N>1 path: the same order)
+        import torch
+        torch.cuda.init()
     txs_per_gpu = args.txs_per_gpu or (10_000 if world == 1 else 20_000)
     dist = None
     gloo = args.dist_backend == "gloo"
@@ -1236,6 +1318,8 @@ def main():
             out["c5_wire"] = c5_wire_leg(local, 1000, args.c5_txs, 65536)
             if args.c5_long_txs:
                 out["c5_long"] = c5_long(local, 1000, args.c5_long_txs, 65536)
+        if world == 1 and not args.no_route:
+            out["owner_route"] = owner_route_leg(local, 1000, args.c5_txs, 65536)
         if world == 1 and not args.no_c1:
             out["c1"] = c1_leg(local, threads)
         print(json.dumps(out), flush=True)

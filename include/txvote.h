@@ -36,6 +36,9 @@
  *                         txvotepool/reactor.go:248 (the sending side of the same wire format)
  *   txv_pool_receive   <- func (txR *Reactor) Receive(chID byte, src p2p.Peer, msgBytes []byte)
  *                         txvotepool/reactor.go:170-190 (decodeMsg + CheckTxWithInfo per message)
+ *   txv_route_admitted / txv_submit_routed <- the Receive -> CheckTxWithInfo -> TryAddVote hand-off
+ *                         (txvotepool/reactor.go:170-190 -> txvotepool.go:187-261 -> txflow/service.go:
+ *                         123-166) across the GPUs of a node, CheckTx on one owner
  */
 #ifndef TXVOTE_H
 #define TXVOTE_H

@@ -97,7 +97,7 @@ class C4Stream:
 
     def __init__(self, ctx, seed: int = 0x7478763034, batch: int = 1 << 20, batches_per_epoch: int = 4,
                  oracle_threads: int = 16, verify_slice: int = 4096, pool_stage: bool = False,
-                 pool_cache: int = 1 << 20, pool_device: bool = False):
+                 pool_cache: int = 1 << 20, pool_device: bool = False, n_honest: int = N_HONEST):
         import oracle as O
         from txflow_amd.workload import validator_seeds
         self.ctx, self.O = ctx, O
@@ -105,7 +105,8 @@ class C4Stream:
         self.batch, self.bpe = batch, batches_per_epoch
         self.threads = oracle_threads
         self.verify_slice = verify_slice
-        self.seeds = validator_seeds(N_HONEST)
+        self.n_honest = n_honest
+        self.seeds = validator_seeds(n_honest)
         honest = ctx.keygen(self.seeds)
         self.crafted = crafted_keys()
         self.pubs = honest + [k[1] for k in self.crafted]
@@ -118,7 +119,7 @@ class C4Stream:
         assert list(ok.astype(bool)) == exp_ok, "validator decode flags differ from the oracle"
         # epoch size: every honest validator votes every tx once as a base vote
         base_frac = 1.0 - 0.05 - 0.05 - 0.02 - 0.005 - 0.0025 - 0.001
-        self.epoch_txs = max(1, int(batch * batches_per_epoch * base_frac) // N_HONEST)
+        self.epoch_txs = max(1, int(batch * batches_per_epoch * base_frac) // self.n_honest)
         self.epoch = -1
         self.generated = 0
         self.stats = dict(votes=0, batches=0, epochs=0, mismatches=0, verify_checked=0, events=0,
@@ -142,7 +143,7 @@ class C4Stream:
         first = (self.epoch + 1) << 32
         from txflow_amd.workload import tx_hashes
         self.hashes = tx_hashes(self.epoch_txs, self.rng, first)          # [T, 64] u8
-        pairs = np.arange(self.epoch_txs * N_HONEST, dtype=np.int64)
+        pairs = np.arange(self.epoch_txs * self.n_honest, dtype=np.int64)
         self.pairs = self.rng.permutation(pairs)                          # (tx, val) = divmod(pair, 100)
         self.pair_pos = 0
         self.prev = None
@@ -179,13 +180,13 @@ class C4Stream:
         val = np.empty(n_prim, np.int64)
         pr = self.pairs[self.pair_pos:self.pair_pos + n_base]
         self.pair_pos += n_base
-        tx[:n_base], val[:n_base] = pr // N_HONEST, pr % N_HONEST
+        tx[:n_base], val[:n_base] = pr // self.n_honest, pr % self.n_honest
         o = n_base
         tx[o:] = rng.integers(0, self.epoch_txs, n_prim - o)
         n_cr = len(self.crafted)
-        val[o:o + n_craft] = N_HONEST + rng.integers(0, n_cr, n_craft)
+        val[o:o + n_craft] = self.n_honest + rng.integers(0, n_cr, n_craft)
         o += n_craft
-        id_keys = [N_HONEST + i for i, k in enumerate(self.crafted) if k[0].startswith("identity")]
+        id_keys = [self.n_honest + i for i, k in enumerate(self.crafted) if k[0].startswith("identity")]
         val[o:o + n_nc] = rng.choice(id_keys, n_nc)
         o += n_nc
         val[o:] = -1                     # unknown / empty / nil: no validator
@@ -246,7 +247,7 @@ class C4Stream:
         # device signing of base + conflict votes by honest validators
         honest = np.zeros(n_all, bool)
         honest[:n_prim] = f["kind"][:n_prim] == 0
-        honest[cs] = (f["kind"][cs] == 0) & (f["val"][cs] >= 0) & (f["val"][cs] < N_HONEST)
+        honest[cs] = (f["kind"][cs] == 0) & (f["val"][cs] >= 0) & (f["val"][cs] < self.n_honest)
         hi = np.nonzero(honest)[0]
         sub = T.VoteBatch(len(hi), height=f["height"][hi], txhash_arena=hashes_arena, txhash_off=f["txoff"][hi],
                           txhash_len=np.full(len(hi), 64, np.uint32), ts_sec=np.full(len(hi), 1_700_000_000, np.int64),
@@ -268,7 +269,7 @@ class C4Stream:
         nc_form = rng.integers(0, 3, len(ci))
         q_f = 0
         for q, i in enumerate(ci):
-            vi = int(f["val"][i]) - N_HONEST
+            vi = int(f["val"][i]) - self.n_honest
             if f["kind"][i] == 2:
                 # identity key, r = 0: R = identity (canonical / x=0 with sign bit / y+p), s = 0
                 R = (E.encode((0, 1)), E.encode_raw(1, 1), E.encode_raw(1 + E.P, 0))[nc_form[q]]
@@ -462,13 +463,13 @@ class C4Stream:
 
 def run_gate(ctx, total_votes: int, batch: int = 1 << 20, batches_per_epoch: int = 4, threads: int = 16,
              log=print, seed: int = 0x7478763034, pipelined: bool = True, pool_stage: bool = False,
-             pool_cache: int = 1 << 20, pool_device: bool = False):
+             pool_cache: int = 1 << 20, pool_device: bool = False, n_honest: int = N_HONEST):
     """Stream `total_votes` C4 votes; returns the stats dict (stats['mismatches'] must be 0).
     pipelined: batches go through txv_submit_votes / txv_wait_votes with two in flight (batch
     k+1 verifies on the device while batch k tallies and is checked against the oracle); the
     pipeline drains at each epoch end, before the per-set check reads the device state."""
     s = C4Stream(ctx, seed=seed, batch=batch, batches_per_epoch=batches_per_epoch, oracle_threads=threads,
-                 pool_stage=pool_stage, pool_cache=pool_cache, pool_device=pool_device)
+                 pool_stage=pool_stage, pool_cache=pool_cache, pool_device=pool_device, n_honest=n_honest)
     t0 = time.time()
 
     def report(r):
