@@ -219,32 +219,44 @@ if C5_NO_UPDATE:
     C5_POOL_SIZE = 1 << 23
 
 
-def c5_commit_updates(wl, added_slots, commit_batch):
+def c5_commit_updates(wl, added_slots, fired_slots):
     """TxFlow's commit side effect on the pool, per batch (txflow/service.go:216-227 ->
-    TxVotePool.Update, txvotepool.go:329-359): after batch k's commit events, Update with the
-    accepted votes of every tx that committed in batch k, and with batch k's ADDED votes of txs
-    committed before (the reference re-fires Update on each later ADDED vote of a committed set:
-    those votes leave the pool too).  added_slots: stream indices of the ADDED votes (from an
-    untimed pass); commit_batch[tx]: the batch of its commit event.  Returns one VoteBatch (or None)
-    per batch, gathered from the stream's columns."""
+    TxVotePool.Update, txvotepool.go:329-359).  The reference calls Update(height, set.GetVotes())
+    after EVERY fired vote (an ADDED vote of a set with 2/3: the crossing vote and each later
+    ADDED one), each time with the set's whole vote list.  A key's last push decides its LRU place
+    and removals are idempotent, so that sequence leaves the pool exactly as this one does, issued
+    once per batch: the sets that fired in the batch, ordered by their last fired vote, each set's
+    accepted votes so far in one block (GetVotes iterates a Go map, so the reference's order inside
+    a block is unspecified; arrival order is one of its orders).  tests/test_update_cadence.py
+    checks the equivalence on the oracle pool.  added_slots / fired_slots: stream indices of the
+    ADDED / fired votes (an untimed pass).  Returns one VoteBatch (or None) per batch, gathered
+    from the stream's columns."""
     import txflow_amd as T
     B = wl.batch_size
     cols = {c: np.concatenate([getattr(b, c) for b in wl.batches]) for c in
             ("height", "txhash_off", "txhash_len", "ts_sec", "ts_nanos", "addr", "addr_len", "sig", "sig_len")}
-    tx = wl.tx_of[added_slots]
-    cb = commit_batch[tx]
-    keep = cb >= 0
-    g, tx, cb = added_slots[keep], tx[keep], cb[keep]
-    when = np.maximum(g // B, cb)
-    order = np.argsort(when, kind="stable")          # grouped by batch, stream order inside each
-    g, when = g[order], when[order]
-    cut = np.searchsorted(when, np.arange(len(wl.batches) + 1))
+    added_slots = np.sort(added_slots)
+    atx = wl.tx_of[added_slots]
+    by_tx = np.argsort(atx, kind="stable")               # each tx's ADDED votes, in stream order
+    tcut = np.searchsorted(atx[by_tx], np.arange(wl.n_txs + 1))
+    fired_slots = np.sort(fired_slots)
+    fb = fired_slots // B
     out = []
     for k in range(len(wl.batches)):
-        idx = g[cut[k]:cut[k + 1]]
-        if not len(idx):
+        f = fired_slots[(fb == k)] if len(fired_slots) else fired_slots
+        if not len(f):
             out.append(None)
             continue
+        ftx = wl.tx_of[f]
+        last = {}
+        for g_, t_ in zip(f.tolist(), ftx.tolist()):      # the set's last fired vote in the batch
+            last[t_] = g_
+        end = (k + 1) * B
+        blocks = []
+        for t_ in sorted(last, key=last.get):
+            v = added_slots[by_tx[tcut[t_]:tcut[t_ + 1]]]
+            blocks.append(v[v < end])
+        idx = np.concatenate(blocks)
         a20 = (idx[:, None] * 20 + np.arange(20)).reshape(-1)
         a64 = (idx[:, None] * 64 + np.arange(64)).reshape(-1)
         out.append(T.VoteBatch(len(idx), height=cols["height"][idx], txhash_arena=wl.batches[0].txhash_arena,
@@ -261,16 +273,15 @@ def c5_prepare_updates(ctx, wl):
     import txflow_amd as T
     expect = c5_expected_pool(wl, C5_CACHE)
     B = wl.batch_size
-    added, commit_batch = [], np.full(wl.n_txs, -1, np.int64)
+    added, fired = [], []
     for k, b in enumerate(wl.batches):
         b.is_nil = (expect[k] != T.POOL_OK).astype(np.uint8)
         st, ev = ctx.add_votes(b, ev_cap=b.n)
         added.append(k * B + np.nonzero((st & 0x7F) == T.ADDED)[0])
-        for e in ev:
-            commit_batch[int(wl.tx_of[k * B + int(e["vote_index"])])] = k
+        fired.append(k * B + np.nonzero(st & T.STATUS_FIRED)[0])
         b.is_nil = None
     ctx.reset_flow()
-    upd = c5_commit_updates(wl, np.concatenate(added), commit_batch)
+    upd = c5_commit_updates(wl, np.concatenate(added), np.concatenate(fired))
     if C5_NO_UPDATE:
         upd = [None] * len(upd)
     for u in upd:                      # the Updates' columns registered too (DMA'd by the pool engine)
