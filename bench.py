@@ -315,6 +315,7 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
     import queue
     import threading
     import txflow_amd as T
+    n_upd = sum(u.n for u in upd if u is not None)
     submit, done, commit_t = [], [], {}
     added = [0]
 
