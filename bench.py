@@ -212,6 +212,7 @@ C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in 
 # holds what CheckTx admitted ahead of the commits (~8 batches in the pipelines below) -- not the
 # stream (2.15M votes)
 C5_POOL_SIZE = 1 << 20
+C5_LONG_POOL_SIZE = 1 << 23     # c5_long: leaked replay entries accumulate over 16M votes (see c5_long)
 # TXV_C5_NO_UPDATE=1 (experiment: the "without Update" figure of the same build): no Update calls,
 # and a Size cap above the stream so nothing fills
 C5_NO_UPDATE = bool(os.environ.get("TXV_C5_NO_UPDATE"))
@@ -291,13 +292,13 @@ def c5_prepare_updates(ctx, wl):
     return upd, sum(u.n for u in upd if u is not None)
 
 
-def c5_pool_replay(wl, order, upd, got, cache_size):
+def c5_pool_replay(wl, order, upd, got, cache_size, pool_size: int = C5_POOL_SIZE):
     """the oracle pool run through the same CheckTx batches and Updates in the order the pool took
     them (recorded under the callers' lock): every batch's statuses must equal (checker, untimed)"""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
-    op = O.Pool(size=C5_POOL_SIZE, cache_size=cache_size, max_txs_bytes=1 << 40)
+    op = O.Pool(size=pool_size, cache_size=cache_size, max_txs_bytes=1 << 40)
     ok = True
     for kind, k in order:
         if kind == "c":
@@ -307,7 +308,8 @@ def c5_pool_replay(wl, order, upd, got, cache_size):
     return ok
 
 
-def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, label: str = "", collect_dev: bool = False):
+def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, label: str = "", collect_dev: bool = False,
+            pool_size: int = C5_POOL_SIZE):
     """One pipelined pass of the C5 stream (c5_streaming's timed pass, c5_long's one long pass):
     CheckTx -> TryAddVote -> Update on the node's threads, two batches in flight.  Returns the
     pass's report, the per-batch device stage times (collect_dev) and per-batch wall times
@@ -341,6 +343,12 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
     # hashed while batch k is admitted
     prepared = queue.Queue(maxsize=2)
     prep_ms, admit_ms = [], []
+    # TXV_C5_TRACE=path (debugging aid): every thread's stage intervals of the pass, as JSON
+    trace = [] if os.environ.get("TXV_C5_TRACE") else None
+
+    def mark(what, k, a, b):
+        if trace is not None:
+            trace.append((what, k, round((a - t0) * 1e3, 4), round((b - t0) * 1e3, 4)))
 
     def prepare():
         for k, b in enumerate(wl.batches):
@@ -349,6 +357,7 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
                 with order_mu:
                     tk = pool.check_submit(b)
                     order.append(("c", k))
+                mark("check_submit", k, ts, time.perf_counter())
                 prepared.put((k, ts, time.perf_counter(), None, tk))
             else:
                 keys, sizes = pool.prepare(b)
@@ -369,6 +378,7 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
                     ps = pool.check_keys(keys, sizes)
                     order.append(("c", k))
             tp = time.perf_counter()
+            mark("check_wait", k, tc, tp)
             b = wl.batches[k]
             b.is_nil = (ps != T.POOL_OK).view(np.uint8)    # not admitted: never reaches TxFlow
             pool_st[k] = ps
@@ -383,8 +393,10 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
             if item is None:
                 return
             k, tk = item
+            tw = time.perf_counter()
             st, ev = ctx.wait_votes(tk, ev_cap=wl.batches[k].n)
             te = time.perf_counter()
+            mark("wait_votes", k, tw, te)
             if collect_dev:               # the batch's stage times, before its ring slot is reused
                 dev_ms.append(ctx.slot_kernel_ms((tk - 1) % T.SUBMIT_RING))
                 sp = verify_split(ctx, (tk - 1) % T.SUBMIT_RING)
@@ -396,6 +408,7 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
                 with order_mu:
                     pool.update_submit(1, upd[k])
                     order.append(("u", k))
+                mark("update_submit", k, tu, time.perf_counter())
                 upd_ms.append((time.perf_counter() - tu) * 1e3)
                 max_size[0] = max(max_size[0], pool.Size())
             done.append(te)
@@ -417,17 +430,24 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
         if item is None:
             break
         k, ts, tp = item
+        ta = time.perf_counter()
         slots.acquire()
+        tb = time.perf_counter()
         submit.append(ts)
         tickets.put((k, ctx.submit_votes(wl.batches[k])))
+        mark("slot_wait", k, ta, tb)
+        mark("submit_votes", k, tb, time.perf_counter())
     tpp.join()
     th.join()
     tickets.put(None)
     td.join()
     added = added[0]
     total = time.perf_counter() - t0
+    if trace is not None:
+        with open(os.environ["TXV_C5_TRACE"] + f".{label.replace(' ', '_')}.json", "w") as f:
+            json.dump(trace, f)
     pool.sync()
-    pool_ok = c5_pool_replay(wl, order, upd, pool_st, C5_CACHE)
+    pool_ok = c5_pool_replay(wl, order, upd, pool_st, C5_CACHE, pool_size)
     ok = pool_ok and added == wl.n_unique and len(commit_t) == wl.n_txs
     lat = np.array([commit_t[t] - submit[wl.first_batch[t]] for t in commit_t]) * 1e3
     bl = (np.array(done) - np.array(submit)) * 1e3
@@ -444,12 +464,14 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
                        f"through TxVotePool.CheckTx (CacheSize {C5_CACHE}) in {stages} -- + "
                        f"txv_submit_votes/txv_wait_votes (TxFlow.TryAddVote for the admitted votes, two batches in "
                        f"flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
-                       f"(txv_pool_update_submit, on the drain thread) with each batch's committed votes after its "
-                       f"commit events ({n_upd} votes per pass, txflow/service.go:224-227), pool Size cap "
-                       f"{C5_POOL_SIZE}; pool statuses checked against the oracle pool replaying the CheckTx "
+                       f"(txv_pool_update_submit, on the drain thread) after each batch's commit events, with the whole "
+                       f"vote list of every set that fired in the batch, by last fired vote ({n_upd} votes per pass; "
+                       f"the reference's Update(GetVotes()) per fired vote, txflow/service.go:216-227, leaves the same "
+                       f"pool: tests/test_update_cadence.py), pool Size cap "
+                       f"{pool_size}; pool statuses checked against the oracle pool replaying the CheckTx "
                        f"batches and Updates in the order the pool took them",
            "correct": ok, "pool_matches_oracle": pool_ok, "votes_per_s": round(wl.n / total, 1),
-           "pool_size_cap": C5_POOL_SIZE, "pool_size_max": max_size[0],
+           "pool_size_cap": pool_size, "pool_size_max": max_size[0],
            "p50_pool_update_ms": round(float(np.median(upd_ms)), 3) if upd_ms else None,
            "pool_status_counts": {"ok": int((allst == T.POOL_OK).sum()),
                                   "in_cache": int((allst == T.POOL_ERR_IN_CACHE).sum()),
@@ -648,7 +670,11 @@ def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
                 ctx.host_register(col)
     log(f"[c5-long] stream ready: {wl.n} votes in {len(wl.batches)} batches, {wl.n_txs} txs, {n_upd} committed votes "
         f"for Update ({time.perf_counter() - t_gen:.1f} s)")
-    pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
+    # the pool's Size cap above the long pass's need: a replay admitted again after its key left the
+    # cache is a second list element that txsMap no longer indexes, so Update never removes it (the
+    # reference's clist + txsMap.Store, txvotepool.go:265-270, 339-344): the pool keeps growing by
+    # ~3% of the stream over the pass, and a cap that could bind sends batches to the host path
+    pool = T.TxVotePool(ctx, size=C5_LONG_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
     for k in range(min(8, len(wl.batches))):        # warm-up: buffers and host tables, then a fresh flow and pool
         b = wl.batches[k]
         b.is_nil = (pool.check_batch(b) != T.POOL_OK).astype(np.uint8)
@@ -657,7 +683,7 @@ def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
             pool.update(1, upd[k])
     ctx.reset_flow()
     pool.flush()
-    out, _, _, per = c5_pass(ctx, wl, pool, upd, True, batch, n_vals, label="one long pass")
+    out, _, _, per = c5_pass(ctx, wl, pool, upd, True, batch, n_vals, label="one long pass", pool_size=C5_LONG_POOL_SIZE)
     n_sets = ctx.num_tx_sets()
     pool.close()
     ctx.close()
@@ -717,7 +743,8 @@ def owner_route_leg(device: int, n_vals: int, n_txs: int, batch: int, n_ranks: i
                 ctx.host_register(col)
     stride = max(T.route_stride(b) for b in wl.batches)
     buf = torch.zeros(n_ranks * stride, dtype=torch.uint8, device=f"cuda:{device}")
-    pool = T.TxVotePool(ctx, size=C5_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
+    # no Update here (the ranks' commits are not in this leg): a Size cap above the stream
+    pool = T.TxVotePool(ctx, size=C5_LONG_POOL_SIZE, cache_size=C5_CACHE, max_txs_bytes=1 << 40, device_cache=True)
     # parity of one batch: device route == host route (untimed)
     st0 = pool.check_batch(wl.batches[0])
     m0 = ctx.route_admitted(wl.batches[0], st0, n_ranks, buf.data_ptr(), stride)

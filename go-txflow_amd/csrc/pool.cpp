@@ -50,14 +50,14 @@ struct Key {
 // (txvotepool.go:467-469): a peer can grind signatures until their keys share any fixed slice, so
 // the host tables place keys by txv_hash::key32 under a secret per-process seed (an unseeded slice
 // let one peer's ground keys pile onto one home slot: every probe of a batch walks the cluster).
-uint64_t key_seed() {
-  static const uint64_t s = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x686f73746b657973ULL;
-  return s;
+uint64_t make_key_seed() {
+  return ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) ^ 0x686f73746b657973ULL;
 }
+const uint64_t g_key_seed = make_key_seed();   // drawn once per process, at load
 inline uint64_t key_hash(const Key& k, uint64_t salt) {
   uint32_t w[8];
   memcpy(w, k.b, 32);
-  return txv_hash::key32(w, key_seed() ^ salt);
+  return txv_hash::key32(w, g_key_seed ^ salt);
 }
 
 // open-addressing index Key -> node of a KeyList (linear probing, backward-shift deletion, no
@@ -365,6 +365,7 @@ struct txv_pool {
   txv_ctx* pend_ctx = nullptr;
   uint64_t next_ticket = 1;
   int next_slot = 0;
+  uint32_t batch_hint = 0;                         // the largest CheckTx batch submitted to the device
   int64_t infl_len = 0, infl_bytes = 0;
   ~txv_pool();
 
@@ -1400,6 +1401,7 @@ int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys,
   if (!dev_caps_ok(p, n, bytes_bound)) return TXV_OK;
   const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
   int r;
+  p->batch_hint = std::max(p->batch_hint, n);
   if (p->pend_n && (p->pend_ctx != ctx || p->pend_n + n > pooldev_cap(p->dev)) && (r = flush_pending(p))) return r;
   if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;
   if ((r = list_to_dev(p, ctx))) return r;
@@ -1505,6 +1507,7 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
     pt.mark("sizes");
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
+      p->batch_hint = std::max(p->batch_hint, v->n);
       // staged Update entries from another context, or too many to ride with this batch, are decided
       // alone first (a rebind to a larger capacity would drain and reallocate mid-stream)
       if (p->pend_n && (p->pend_ctx != ctx || p->pend_n + v->n > pooldev_cap(p->dev)) && (r = flush_pending(p))) return r;
@@ -1628,7 +1631,9 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
   int r;
   if (p->pend_n && (p->pend_ctx != ctx || (p->dev && p->pend_n + n > pooldev_cap(p->dev))) && (r = flush_pending(p)))
     return r;
-  if ((r = cache_to_dev(p, ctx, p->pend_n + n))) return r;   // (a rebind drains: pend_n is 0 then)
+  // room for the next CheckTx batch beside the staged entries, so they ride with it instead of
+  // being decided alone (a chain of their own) when it comes
+  if ((r = cache_to_dev(p, ctx, p->pend_n + n + p->batch_hint))) return r;   // (a rebind drains: pend_n is 0 then)
   if ((r = list_to_dev(p, ctx))) return r;
   if (!p->pend_n) {                                        // a slot for the entries: its previous batch finished
     if ((r = finish_slot(p, p->next_slot))) return r;

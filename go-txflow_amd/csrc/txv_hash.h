@@ -34,15 +34,19 @@ TXV_HASH_HD uint64_t hash_chunks(uint32_t n, uint64_t seed, Get get) {
 }
 
 // seeded hash of a 32-byte TxVotePool key (SHA-256(Signature), as 8 words in memory order).  The
-// keys are peer-chosen (a peer can grind signatures until their keys share any unseeded slice), so
+// keys are peer-chosen (a peer can grind signatures until their keys share any fixed slice), so
 // every table or sort over them places a key by this hash under a secret per-process / per-engine
-// seed: a run of colliding keys costs 2^bits tries per key only for someone who knows the seed.
-// All 8 words are mixed, each through a bijection keyed by the running state, so no two distinct
-// keys collide for every seed.
+// seed: the four 64-bit words folded (rotated apart, so a key differing in any byte folds apart)
+// and one mix64, a bijection of the fold xor the seed.  Two keys land together for every seed only
+// if their folds are equal -- 64 bits of SHA-256 output to match: pairs cost ~2^32 hashes, but k
+// keys with one fold ~2^(64 (k-1) / k) (runs of ten: 2^57), so a run or a probe cluster stays a
+// handful of keys whatever a peer grinds -- and the single mix keeps the host CheckTx loop at its
+// unseeded speed (five mixes over the words made it 3-5x slower).
+TXV_HASH_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 TXV_HASH_HD uint64_t key32(const uint32_t* k, uint64_t seed) {
-  uint64_t h = seed;
-  for (int j = 0; j < 4; ++j) h = mix64(h ^ ((uint64_t)k[2 * j] | ((uint64_t)k[2 * j + 1] << 32))) + 0x9e3779b97f4a7c15ULL;
-  return mix64(h);
+  const uint64_t w0 = (uint64_t)k[0] | ((uint64_t)k[1] << 32), w1 = (uint64_t)k[2] | ((uint64_t)k[3] << 32);
+  const uint64_t w2 = (uint64_t)k[4] | ((uint64_t)k[5] << 32), w3 = (uint64_t)k[6] | ((uint64_t)k[7] << 32);
+  return mix64(w0 ^ rotl64(w1, 16) ^ rotl64(w2, 32) ^ rotl64(w3, 48) ^ seed);
 }
 
 }  // namespace txv_hash

@@ -475,10 +475,14 @@ int txv_pool_update(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_vote
 int txv_pool_update_keys(txv_pool* pool, txv_ctx* ctx, int64_t height, const uint8_t* keys32, const uint32_t* sizes,
                          uint32_t n);
 /* txv_pool_update without the wait (the commit path of a node that keeps checking batches):
- * with TXV_POOL_DEVICE_CACHE it returns once the pushes are enqueued; its effects are applied in
- * submission order with the txv_pool_check_submit batches, and are in place once those submitted
- * before it are waited, at txv_pool_sync, or at any call that reads the pool list or cache.  The
- * host cache applies it at once.  txflow/service.go:224-227 -> txvotepool.go:329-359 */
+ * with TXV_POOL_DEVICE_CACHE it stages the committed votes (their signatures uploaded) and returns;
+ * the staged pushes and removals are applied ahead of the NEXT device CheckTx batch submitted
+ * (txv_pool_check_submit, txv_pool_check_keys with a context, the wire ingest), in that batch's
+ * engine chain -- the reference's order: Update, then the CheckTx calls after it -- or alone at
+ * txv_pool_sync, at any call that reads the pool list or cache, or when staged entries from
+ * another context or too many for one flight would otherwise wait.  Waiting on tickets submitted
+ * before the Update does not apply it.  The host cache applies it at once.
+ * txflow/service.go:224-227 -> txvotepool.go:329-359 */
 int txv_pool_update_submit(txv_pool* pool, txv_ctx* ctx, int64_t height, const txv_votes* committed,
                            const uint8_t* sig_full, const uint64_t* sig_full_off);
 /* ReapMaxTxs(max) in pool order: keys (32 B) and TxVote.Size of the reaped entries; the
