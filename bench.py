@@ -708,6 +708,7 @@ def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
         "votes_per_s_by_decile": dec,
         "decile_min_over_max": round(min(dec) / max(dec), 3),
         "p90_batch_ms": round(float(np.percentile(bl, 90)), 3),
+        "slowest_batches_ms": {int(k): round(float(bl[k]), 3) for k in np.argsort(bl)[::-1][:6]},
         "flow_sizing": {"max_txs": n_txs + 64, "max_accepted": int(min((n_txs + 64) * n_vals, 1 << 26)),
                         "note": "the reference never prunes TxVoteSets; here the flow holds max_txs sets and "
                                 "max_accepted accepted votes (sized for the node's horizon: 1M sets x 100 "
@@ -1102,11 +1103,15 @@ def main():
     ap.add_argument("--cpu-parallel-votes", type=int, default=1_000_000)
     ap.add_argument("--c5-only", action="store_true",
                     help="profiling aid: run only the C5 legs (SoA and wire) and print them as one JSON line")
+    ap.add_argument("--c5-long-only", action="store_true", help="profiling aid: only the one-long-TxFlow C5 leg")
     args = ap.parse_args()
     if os.environ.get("TXV_BENCH_WATCHDOG"):   # debugging aid: every thread's stack on stderr periodically
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["TXV_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
+    if args.c5_long_only:
+        print(json.dumps({"c5_long": c5_long(0, 1000, args.c5_long_txs, 65536)}), flush=True)
+        return
     if args.c5_only:
         out = {"c5_streaming": c5_streaming(0, 1000, args.c5_txs, 65536)}
         if not args.no_wire:

@@ -3768,6 +3768,18 @@ int list_ready(txv_ctx* c, PoolDev* s) {
   const uint32_t cap = list_cap_initial(s);
   if ((r = list_buf_alloc(c, b, cap))) return r;
   if (s->lb[s->lcur ^ 1].cap < cap && (r = list_buf_alloc(c, s->lb[s->lcur ^ 1], cap))) return r;
+  // the compaction's scratch too: a compaction at this capacity then neither allocates nor
+  // synchronises the stream it runs on
+  if (s->lnpos_cap < cap) {
+    if ((r = dalloc(c, &s->lnpos, cap))) return r;
+    s->lnpos_cap = cap;
+  }
+  if (const size_t tb = txv_poollist_tmp_bytes(cap); s->ltmp_bytes < tb) {
+    if (s->ltmp) (void)hipFree(s->ltmp);
+    s->ltmp = nullptr;
+    HIP_TRY(c, hipMalloc(&s->ltmp, tb));
+    s->ltmp_bytes = tb;
+  }
   HIP_TRY(c, hipMemset(b.fl, 0, b.cap));
   HIP_TRY(c, hipMemset(b.ix, 0, (size_t)b.icap * 8));
   HIP_TRY(c, hipMemset(s->ltail, 0, 8));
