@@ -212,6 +212,7 @@ C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in 
 # holds what CheckTx admitted ahead of the commits (~8 batches in the pipelines below) -- not the
 # stream (2.15M votes)
 C5_POOL_SIZE = 1 << 20
+WIRE_INFLIGHT = int(os.environ.get("TXV_WIRE_INFLIGHT", "3"))   # wire batches between decode and wait (<= 3, the ingest ring)
 C5_LONG_POOL_SIZE = 1 << 23     # c5_long: leaked replay entries accumulate over 16M votes (see c5_long)
 # TXV_C5_NO_UPDATE=1 (experiment: the "without Update" figure of the same build): no Update calls,
 # and a Size cap above the stream so nothing fills
@@ -832,8 +833,13 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         state = {"added": 0, "ok": True}
         got, order, order_mu = [None] * len(wbs), [], threading.Lock()
         decoded, submitted, admitted = queue.Queue(), queue.Queue(), queue.Queue()
-        slots = threading.Semaphore(3)              # the library's ingest ring
+        slots = threading.Semaphore(WIRE_INFLIGHT)  # within the library's ingest ring
         sub_ms = []
+        trace = [] if os.environ.get("TXV_C5_TRACE") else None
+
+        def mark(what, k, a, b):
+            if trace is not None:
+                trace.append((what, k, round((a - t0) * 1e3, 4), round((b - t0) * 1e3, 4)))
 
         # four goroutine-like stages: Receive (decode) -> CheckTx handed to the device
         # (txv_ingest_admit_submit) -> its statuses + the TxFlow chain enqueued
@@ -850,6 +856,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                     pool.ingest_admit_submit(tk)
                     order.append(("c", k))
                 sub_ms.append((time.perf_counter() - ta) * 1e3)
+                mark("admit_submit", k, ta, time.perf_counter())
                 submitted.put((k, tk))
 
         def finish():
@@ -862,6 +869,7 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                 ta = time.perf_counter()
                 pool.ingest_admit_finish(tk)
                 adm_ms.append((time.perf_counter() - ta) * 1e3)
+                mark("admit_finish", k, ta, time.perf_counter())
                 admitted.put((k, tk))
 
         def drain():
@@ -870,13 +878,16 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                 if item is None:
                     return
                 k, tk = item
+                tw = time.perf_counter()
                 ws, ps, fs, ev = pool.ingest_wait(tk)
                 te = time.perf_counter()
+                mark("ingest_wait", k, tw, te)
                 slots.release()
                 if upd[k] is not None:            # TxVotePool.Update with the batch's committed votes
                     with order_mu:
                         pool.update_submit(1, upd[k])
                         order.append(("u", k))
+                    mark("update_submit", k, te, time.perf_counter())
                 got[k] = ps
                 state["ok"] = state["ok"] and bool((ws == T.WIRE_OK).all())
                 state["added"] += int(np.count_nonzero((fs & 0x7F) == T.ADDED))
@@ -890,17 +901,23 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
         tf_.start()
         td_.start()
         for k, w in enumerate(wbs):
+            tq = time.perf_counter()
             slots.acquire()
             ts = time.perf_counter()
             start.append(ts)
             tk = pool.ingest_decode(w)
             dec_ms.append((time.perf_counter() - ts) * 1e3)
+            mark("slot_wait", k, tq, ts)
+            mark("decode", k, ts, time.perf_counter())
             decoded.put((k, tk))
         decoded.put(None)
         ta_.join()
         tf_.join()
         td_.join()
         total = time.perf_counter() - t0
+        if trace is not None:
+            with open(os.environ["TXV_C5_TRACE"] + f".wire_{rep}.json", "w") as f:
+                json.dump(trace, f)
         pool.sync()
         pool_ok = c5_pool_replay(wl, order, upd, got, C5_CACHE)
         lat = np.array([commit_t[t] - start[wl.first_batch[t]] for t in commit_t]) * 1e3
@@ -1104,11 +1121,15 @@ def main():
     ap.add_argument("--c5-only", action="store_true",
                     help="profiling aid: run only the C5 legs (SoA and wire) and print them as one JSON line")
     ap.add_argument("--c5-long-only", action="store_true", help="profiling aid: only the one-long-TxFlow C5 leg")
+    ap.add_argument("--c5-wire-only", action="store_true", help="profiling aid: only the C5 wire-bytes leg")
     args = ap.parse_args()
     if os.environ.get("TXV_BENCH_WATCHDOG"):   # debugging aid: every thread's stack on stderr periodically
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["TXV_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
+    if args.c5_wire_only:
+        print(json.dumps({"c5_wire": c5_wire_leg(0, 1000, args.c5_txs, 65536)}), flush=True)
+        return
     if args.c5_long_only:
         print(json.dumps({"c5_long": c5_long(0, 1000, args.c5_long_txs, 65536)}), flush=True)
         return

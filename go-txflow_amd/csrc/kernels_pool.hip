@@ -390,7 +390,10 @@ __global__ void __launch_bounds__(256) pd_status(PoolDevArgs a) {
            : (!a.sizes[i] && a.wal) ? TXV_POOL_ERR_ENCODING : TXV_POOL_OK;
       }
       a.status[i] = st;
-      if (i >= a.n_force) a.status_out[i - a.n_force] = st;   // mapped host memory: no copy back
+      if (i >= a.n_force) {
+        a.status_out[i - a.n_force] = st;                     // mapped host memory: no copy back
+        if (a.status_copy) a.status_copy[i - a.n_force] = st;
+      }
       f[k] = a.last[i] != 0;
     } else {
       if (i >= a.C) continue;

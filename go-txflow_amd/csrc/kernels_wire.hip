@@ -19,6 +19,7 @@
 #include "sha2.h"
 #include "txv_device.h"
 #include "wire_dev.h"
+#include "../../include/txvote.h"
 
 using namespace txv::wire;
 
@@ -239,6 +240,44 @@ __global__ void __launch_bounds__(256) txv_k_rec_to_flow(const uint32_t* __restr
   uint4* tk = reinterpret_cast<uint4*>(c.txkey + (size_t)j * 32);
   tk[0] = make_uint4(r[11], r[12], r[13], r[14]);
   tk[1] = make_uint4(r[15], r[16], r[17], r[18]);
+}
+
+// Every decoded message -> the flow slot's columns, the pool's rejections (and the messages that
+// did not decode: TXV_POOL_NOT_CHECKED) as nil entries, which AddVote drops before any state
+// (types/vote_set.go:93): the TxFlow chain of a wire batch is enqueued behind the pool's device
+// decisions without their statuses making a host round trip first.
+__global__ void __launch_bounds__(256) txv_k_rec_to_flow_nil(const uint32_t* __restrict__ rec,
+                                                             const uint8_t* __restrict__ pool_status, uint32_t n,
+                                                             FlowCols c, uint8_t* __restrict__ nil) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t* r = rec + (size_t)j * TXV_WIRE_REC_WORDS;
+  const bool ok = pool_status[j] == TXV_POOL_OK;
+  nil[j] = ok ? 0 : 1;
+  c.height[j] = ok ? (int64_t)((uint64_t)r[1] | ((uint64_t)r[2] << 32)) : 0;
+  c.ts_sec[j] = ok ? (int64_t)((uint64_t)r[3] | ((uint64_t)r[4] << 32)) : 0;
+  c.ts_nanos[j] = ok ? (int32_t)r[5] : 0;
+  c.th_off[j] = ok ? r[6] : 0u;
+  c.th_len[j] = ok ? r[7] : 0u;
+  c.addr_len[j] = ok ? r[8] : 0u;
+  c.sig_len[j] = ok ? r[10] : 0u;
+  if (!ok) return;
+  uint32_t* a = reinterpret_cast<uint32_t*>(c.addr + (size_t)j * 20);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) a[q] = r[19 + q];
+  uint4* sg = reinterpret_cast<uint4*>(c.sig + (size_t)j * 64);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sg[q] = make_uint4(r[24 + 4 * q], r[25 + 4 * q], r[26 + 4 * q], r[27 + 4 * q]);
+  uint4* tk = reinterpret_cast<uint4*>(c.txkey + (size_t)j * 32);
+  tk[0] = make_uint4(r[11], r[12], r[13], r[14]);
+  tk[1] = make_uint4(r[15], r[16], r[17], r[18]);
+}
+
+extern "C" hipError_t txv_launch_rec_to_flow_nil(const uint32_t* rec, const uint8_t* pool_status, uint32_t n,
+                                                 const FlowCols* c, uint8_t* nil, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_rec_to_flow_nil, dim3((n + 255) / 256), dim3(256), 0, st, rec, pool_status, n, *c, nil);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t txv_launch_rec_keys(const uint32_t* rec, const uint8_t* wire, uint32_t n, uint8_t* status,

@@ -292,7 +292,8 @@ int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_k
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
-                    bool list_on, uint64_t live_ub, uint32_t n_upd);
+                    bool list_on, uint64_t live_ub, uint32_t n_upd, uint8_t* d_status_copy = nullptr,
+                    void* then_stream = nullptr);
 int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_votes* v, const uint32_t* h_sizes);
 void pooldev_list_hint(PoolDev* s, uint64_t entries);
 int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, const uint8_t** keys, const uint32_t** sizes);
@@ -1391,9 +1392,11 @@ int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const 
 // thread hands batch k+1's CheckTx to the GPU while batch k's statuses are still on their way.
 // The caps are checked against n pushes of bytes_bound bytes in all (upper bounds: the decode
 // has not reported yet), beside the batches in flight.  *done = false: the host path is needed.
+// d_status_copy (or null): the batch's statuses written to HBM there too, and then_stream (or null)
+// made to wait for them -- the ingest's TxFlow chain reads them without a host round trip.
 int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
                               const uint8_t* d_valid, uint8_t valid_ok, uint32_t n, uint64_t bytes_bound, void* after,
-                              uint64_t* ticket, bool* done) {
+                              uint8_t* d_status_copy, void* then_stream, uint64_t* ticket, bool* done) {
   *done = false;
   *ticket = 0;
   std::lock_guard<std::mutex> g(p->mu);
@@ -1411,7 +1414,8 @@ int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys,
   p->pend_n = 0;
   p->pend_slot = -1;
   if ((r = pooldev_enqueue(ctx, p->dev, slot, nullptr, nullptr, nullptr, d_keys, d_sizes, d_valid, valid_ok, n, max_tx,
-                           (p->cfg.flags & TXV_POOL_WAL) != 0, false, after, true, live_ub(p), n_upd)))
+                           (p->cfg.flags & TXV_POOL_WAL) != 0, false, after, true, live_ub(p), n_upd, d_status_copy,
+                           then_stream)))
     return r;
   if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
   p->next_slot = (slot + 1) % kPdRing;

@@ -83,5 +83,6 @@ struct PoolDevArgs {
   size_t tmp_bytes;
   uint8_t* status;            // [n] out: TXV_POOL_* per vote
   uint8_t* status_out;        // [n - n_force] the batch's own statuses again, in mapped host memory
+  uint8_t* status_copy;       // [n - n_force] and once more in HBM for a consumer's kernels, or null
 };
 

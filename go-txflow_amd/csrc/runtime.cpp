@@ -286,13 +286,17 @@ struct txv_ctx {
     uint8_t *d_status = nullptr, *h_status = nullptr;
     uint32_t *d_keys = nullptr, *h_keys = nullptr, *d_sizes = nullptr, *h_sizes = nullptr;
     uint32_t *d_list = nullptr, *h_list = nullptr, *d_max = nullptr, *h_max = nullptr;
-    hipEvent_t kev = nullptr;      // statuses, keys and sizes are back in pinned memory
+    uint8_t* d_pstat = nullptr;    // the pool's device statuses of the batch (the early TxFlow chain's nil column)
+    hipEvent_t kev = nullptr;      // statuses (and, for a host-path admission, keys and sizes) are back in pinned memory
+    hipEvent_t uev = nullptr;      // the batch's uploads have landed (the decode kernels' stream waits for it)
     uint64_t ticket = 0;           // the batch in this slot (0 = free); guarded by mu
     int phase = 0;                 // 0 free, 1 decoded (keys in flight), 3 CheckTx submitted to the device
                                    // (pool_ticket), 2 admitted (TxFlow chain enqueued)
     uint64_t pool_ticket = 0;      // phase 3: the pool's ticket (txv_pool_check_wait) of its decisions
     txv_pool* pool = nullptr;      // the pool the batch is checked against
     uint32_t n = 0, n_adm = 0;     // messages of the batch; votes the pool admitted (h_list)
+    uint32_t max_len = 0;          // the longest message: bounds every TxHash (SignBytes column words)
+    bool early = false;            // TxFlow chain enqueued over all n messages behind the device CheckTx
     uint64_t wire_bytes = 0;       // bounds the decoded votes' summed TxVote.Size()
     int flow_err = 0;              // the admitted votes' AddVote chain could not be enqueued
     std::string flow_msg;
@@ -1453,8 +1457,9 @@ void txv_destroy(txv_ctx* c) {
   for (auto& g : c->ing) {
     dfree(g.d_off); hfree(g.h_off); dfree(g.d_len); hfree(g.h_len); dfree(g.d_rec); dfree(g.d_span); hfree(g.h_span);
     dfree(g.d_status); hfree(g.h_status); dfree(g.d_keys); hfree(g.h_keys); dfree(g.d_sizes); hfree(g.h_sizes);
-    dfree(g.d_list); hfree(g.h_list); dfree(g.d_max); hfree(g.h_max);
+    dfree(g.d_list); hfree(g.h_list); dfree(g.d_max); hfree(g.h_max); dfree(g.d_pstat);
     if (g.kev) (void)hipEventDestroy(g.kev);
+    if (g.uev) (void)hipEventDestroy(g.uev);
   }
   if (c->pk_ev) (void)hipEventDestroy(c->pk_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -3013,7 +3018,7 @@ int txv_decode_msgs(txv_ctx* c, const uint8_t* wire, uint64_t wire_bytes, const 
 uint32_t txv_pool_max_msg_bytes(txv_pool* p);  // pool.cpp
 int txv_pool_check_dev_submit(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
                               const uint8_t* d_valid, uint8_t valid_ok, uint32_t n, uint64_t bytes_bound, void* after,
-                              uint64_t* ticket, bool* done);   // pool.cpp
+                              uint8_t* d_status_copy, void* then_stream, uint64_t* ticket, bool* done);   // pool.cpp
 int txv_pool_check_dev(txv_pool* p, txv_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_sizes,
                        const uint8_t* d_valid, const uint8_t* h_keys, const uint32_t* h_sizes, uint8_t valid_ok,
                        uint32_t n, uint64_t bytes_bound, void* after, uint8_t* status_out, bool* done);   // pool.cpp
@@ -3047,12 +3052,13 @@ int ingest_alloc(txv_ctx* c, txv_ctx::Ingest& g, Slot& s, uint64_t wire_bytes, u
         (r = dalloc(c, &g.d_status, cap)) || (r = halloc(c, &g.h_status, cap)) ||
         (r = dalloc(c, &g.d_keys, (size_t)cap * 8)) || (r = halloc(c, &g.h_keys, (size_t)cap * 8)) ||
         (r = dalloc(c, &g.d_sizes, cap)) || (r = halloc(c, &g.h_sizes, cap)) ||
-        (r = dalloc(c, &g.d_list, cap)) || (r = halloc(c, &g.h_list, cap)) ||
+        (r = dalloc(c, &g.d_list, cap)) || (r = halloc(c, &g.h_list, cap)) || (r = dalloc(c, &g.d_pstat, cap)) ||
         (r = dalloc(c, &g.d_max, 1)) || (r = halloc(c, &g.h_max, 1)))
       return r;
     g.cap = cap;
   }
   if (!g.kev) HIP_TRY(c, hipEventCreateWithFlags(&g.kev, hipEventDisableTiming));
+  if (!g.uev) HIP_TRY(c, hipEventCreateWithFlags(&g.uev, hipEventDisableTiming));
   // the wire bytes go straight into the slot's TxHash arena: the decoded TxHash offsets index it
   if (wire_bytes + 128 > s.arena_cap) {
     const size_t cap = std::max<size_t>((size_t)wire_bytes + 128, s.arena_cap * 2);
@@ -3065,11 +3071,14 @@ int ingest_alloc(txv_ctx* c, txv_ctx::Ingest& g, Slot& s, uint64_t wire_bytes, u
 int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_bytes, const uint64_t* msg_off,
                   const uint32_t* msg_len, uint32_t n, uint64_t* ticket) {
   if (wire_bytes >= (1ull << 32)) { c->err = "wire buffer >= 4 GiB"; return TXV_EINVAL; }
-  for (uint32_t i = 0; i < n; ++i)   // every message inside the buffer: the kernels trust these
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < n; ++i) {   // every message inside the buffer: the kernels trust these
     if (msg_off[i] > wire_bytes || msg_len[i] > wire_bytes - msg_off[i]) {
       c->err = "message " + std::to_string(i) + " outside the wire buffer";
       return TXV_EINVAL;
     }
+    max_len = std::max(max_len, msg_len[i]);
+  }
   // the pool's lock is taken before the context's everywhere (pool.cpp calls into the context with
   // its own lock held): its MaxMsgBytes is read here, before c->mu
   const uint32_t max_msg = p ? txv_pool_max_msg_bytes(p) : 0u;
@@ -3097,6 +3106,7 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
   int r;
   if ((r = ingest_alloc(c, g, s, wire_bytes, n))) return r;
   g.n = n; g.n_adm = 0; g.flow_err = 0; g.flow_msg.clear(); g.pool = p; g.wire_bytes = wire_bytes;
+  g.max_len = max_len; g.early = false;
   const uint32_t n_chunks = (n + TXV_WIRE_BLOCK - 1) / TXV_WIRE_BLOCK;
   if (n) {
     if (!wire_reg) {
@@ -3123,18 +3133,30 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
   }
   std::lock_guard<std::mutex> lk(c->mu);
   if (n) {
-    hipStream_t ks = c->key_stream;
-    if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[4], 0));   // the slot's last chain ended
+    // the uploads run on the copy stream, which then carries DMA only (these, the Update entries'
+    // signatures, the statuses back), the decode kernels on the key stream after them, in order with
+    // the pool's device decisions and the TxFlow chains' prep that follow there.
+    // TXV_WIRE_DECODE_STREAM (experiment): "copy" -- uploads and kernels on the copy stream, "key" --
+    // both on the key stream (round 5)
+    static const char* dsv = getenv("TXV_WIRE_DECODE_STREAM");
+    static const int dmode = !dsv ? 0 : !strcmp(dsv, "copy") ? 1 : !strcmp(dsv, "key") ? 2 : 0;
+    hipStream_t us = dmode == 2 ? c->key_stream : c->copy_stream;   // uploads
+    hipStream_t ks = dmode == 1 ? c->copy_stream : c->key_stream;   // decode kernels
+    if (s.launched) HIP_TRY(c, hipStreamWaitEvent(us, s.ev[4], 0));   // the slot's last chain ended
     if (wire_reg) {
-      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, wire, wire_bytes, hipMemcpyHostToDevice, ks));
-      HIP_TRY(c, hipMemsetAsync(s.d_arena_th + wire_bytes, 0, 128, ks));
+      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, wire, wire_bytes, hipMemcpyHostToDevice, us));
+      HIP_TRY(c, hipMemsetAsync(s.d_arena_th + wire_bytes, 0, 128, us));
     } else {
-      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, ks));
+      HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, s.h_arena, wire_bytes + 128, hipMemcpyHostToDevice, us));
     }
-    HIP_TRY(c, hipMemcpyAsync(g.d_off, g.h_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(g.d_len, g.h_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(g.d_span, g.h_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, ks));
-    HIP_TRY(c, hipMemcpyAsync(g.d_max, g.h_max, 4, hipMemcpyHostToDevice, ks));
+    HIP_TRY(c, hipMemcpyAsync(g.d_off, g.h_off, (size_t)n * 8, hipMemcpyHostToDevice, us));
+    HIP_TRY(c, hipMemcpyAsync(g.d_len, g.h_len, (size_t)n * 4, hipMemcpyHostToDevice, us));
+    HIP_TRY(c, hipMemcpyAsync(g.d_span, g.h_span, (size_t)n_chunks * 16, hipMemcpyHostToDevice, us));
+    HIP_TRY(c, hipMemcpyAsync(g.d_max, g.h_max, 4, hipMemcpyHostToDevice, us));
+    if (us != ks) {
+      HIP_TRY(c, hipEventRecord(g.uev, us));
+      HIP_TRY(c, hipStreamWaitEvent(ks, g.uev, 0));
+    }
     WireArgs a{};
     a.n = n;
     a.max_msg_bytes = max_msg;
@@ -3145,9 +3167,9 @@ int ingest_decode(txv_ctx* c, txv_pool* p, const uint8_t* wire, uint64_t wire_by
     a.span = g.d_span;
     HIP_TRY(c, txv_launch_decode_msgs(&a, (uint32_t)c->n_cus * 5u, ks));
     HIP_TRY(c, txv_launch_rec_keys(a.rec, s.d_arena_th, n, g.d_status, g.d_keys, g.d_sizes, g.d_max, ks));
+    // back: the wire statuses and the longest TxHash; the keys and sizes only if the admission
+    // takes the host path (ingest_admit_submit)
     HIP_TRY(c, hipMemcpyAsync(g.h_status, g.d_status, n, hipMemcpyDeviceToHost, ks));
-    HIP_TRY(c, hipMemcpyAsync(g.h_keys, g.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
-    HIP_TRY(c, hipMemcpyAsync(g.h_sizes, g.d_sizes, (size_t)n * 4, hipMemcpyDeviceToHost, ks));
     HIP_TRY(c, hipMemcpyAsync(g.h_max, g.d_max, 4, hipMemcpyDeviceToHost, ks));
     HIP_TRY(c, hipEventRecord(g.kev, ks));
   }
@@ -3196,6 +3218,43 @@ void ingest_flow_stage(txv_ctx* c, uint64_t t, uint32_t n_adm) {
   g.phase = 2;
 }
 
+// The early TxFlow chain of a batch whose CheckTx was handed to the device: every message enters
+// it, the pool's rejections and the messages that did not decode as nil entries built on the
+// device from the statuses the pool's chain writes to g.d_pstat (the key stream waits for them:
+// txv_pool_check_dev_submit), so the chain is enqueued without those statuses' host round trip.
+// The SignBytes column is sized by the longest message (it bounds every TxHash).  c->mu held;
+// an error is kept for the wait, as ingest_flow_stage's.
+constexpr uint32_t kEarlyMaxLen = 1024;   // longer messages in a batch: ingest_flow_stage at finish
+void ingest_flow_stage_early(txv_ctx* c, uint64_t t) {
+  const uint32_t j = (uint32_t)((t - 1) % kIngestRing);
+  txv_ctx::Ingest& g = c->ing[j];
+  Slot& s = c->slots[kIngestSlot + j];
+  g.early = true;
+  auto flow_stage = [&]() -> int {
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->poisoned) { c->err = "a TxFlow capacity was exceeded: txv_reset_flow first"; return TXV_ECAPACITY; }
+    const uint32_t n = g.n;
+    const uint32_t mw = (signbytes_bound(g.max_len, (uint32_t)c->chain.size()) + 7) / 8;
+    int rr;
+    if ((rr = ensure_slot(c, s, n, mw))) return rr;
+    hipStream_t ks = c->key_stream;
+    FlowCols fc{s.d_fh, s.d_fs, s.d_fn, s.d_fo, s.d_fl, s.d_addr, s.d_addr_len, s.d_sigraw, s.d_sig_len, s.d_txkey};
+    HIP_TRY(c, txv_launch_rec_to_flow_nil(reinterpret_cast<const uint32_t*>(g.d_rec), g.d_pstat, n, &fc, s.d_nil, ks));
+    HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's kernels wait for this
+    s.n = n; s.n_pad = (n + 63) / 64 * 64; s.msg_words = mw;
+    s.has_nil = true;
+    s.has_txkey = true;
+    s.seq_base = c->seq_next;
+    c->seq_next += n;
+    s.staged = true; s.ran = false;
+    return run_slot(c, kIngestSlot + j, nullptr);
+  };
+  if (const int rf = flow_stage()) {
+    g.flow_err = rf;
+    g.flow_msg = c->err.copy();
+  }
+}
+
 // the ticket ends without TxFlow (CheckTx failed before touching the pool); c->mu held
 void ingest_drop(txv_ctx* c, txv_ctx::Ingest& g, uint64_t t) {
   g.phase = 0;
@@ -3231,8 +3290,10 @@ int ingest_admit_submit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* p
   if (n) {
     bool dev = false;
     uint64_t pt = 0;
+    const bool early = g.max_len <= kEarlyMaxLen;
     const int rd = txv_pool_check_dev_submit(g.pool, c, g.d_keys, g.d_sizes, g.d_status, TXV_WIRE_OK, n, g.wire_bytes,
-                                             (void*)g.kev, &pt, &dev);
+                                             (void*)g.kev, early ? g.d_pstat : nullptr,
+                                             early ? (void*)c->key_stream : nullptr, &pt, &dev);
     if (rd) {   // the pool is unchanged: the ticket ends here (no wait)
       (void)hipEventSynchronize(g.kev);
       std::lock_guard<std::mutex> lk(c->mu);
@@ -3246,6 +3307,10 @@ int ingest_admit_submit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* p
       c->ing_admit_next = t + 1;
       *pending = true;
       ht.mark("pool_submit");
+      if (early) {                 // TxFlow order = pool order: enqueued here, in ticket order
+        ingest_flow_stage_early(c, t);
+        ht.mark("flow_enqueue");
+      }
       return TXV_OK;
     }
   }
@@ -3257,7 +3322,16 @@ int ingest_admit_submit(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* p
       std::lock_guard<std::mutex> lk(c->mu);
       if (ingest_earlier_pending(c, t)) { c->err = "finish the earlier ingest admissions before a host-path batch"; return TXV_ESTATE; }
     }
-    if (n) HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
+    if (n) {
+      {   // the keys and sizes back (the decode left them in HBM): after the decode, on the copy stream
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, g.kev, 0));
+        HIP_TRY(c, hipMemcpyAsync(g.h_keys, g.d_keys, (size_t)n * 32, hipMemcpyDeviceToHost, c->copy_stream));
+        HIP_TRY(c, hipMemcpyAsync(g.h_sizes, g.d_sizes, (size_t)n * 4, hipMemcpyDeviceToHost, c->copy_stream));
+        HIP_TRY(c, hipEventRecord(g.kev, c->copy_stream));
+      }
+      HIP_TRY(c, hipEventSynchronize(g.kev));   // no lock held: the keys' round trip only
+    }
     ht.mark("keys_wait");
     if (wire_status && n) memcpy(wire_status, g.h_status, n);
     std::atomic<uint32_t> bad{0};
@@ -3345,6 +3419,8 @@ int ingest_admit_finish(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* p
   if (rw) {   // the device decisions failed: nothing of the batch reached TxFlow
     std::lock_guard<std::mutex> lk(c->mu);
     c->err = "ingest: the device CheckTx of the batch failed";
+    // an early chain read statuses the failed decisions left: TxFlow's state is unknown from here
+    if (g.early && !g.flow_err) c->poisoned = true;
     ingest_drop(c, g, t);
     return rw;
   }
@@ -3355,6 +3431,12 @@ int ingest_admit_finish(txv_ctx* c, uint64_t t, uint8_t* wire_status, uint8_t* p
     n_adm += dst[i] == TXV_POOL_OK;
   }
   std::lock_guard<std::mutex> lk(c->mu);
+  if (g.early) {              // the chain runs already (every message, the rejected ones nil)
+    g.n_adm = n_adm;
+    g.phase = 2;
+    ht.mark("list");
+    return TXV_OK;
+  }
   ingest_flow_stage(c, t, n_adm);
   ht.mark("flow_enqueue");
   return TXV_OK;
@@ -3380,7 +3462,7 @@ int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_ev
     if (g.ticket != ticket || g.phase != 2) { c->err = "unknown, unadmitted or already waited ingest ticket"; return TXV_ESTATE; }
     for (const auto& o : c->ing)
       if (o.phase == 2 && o.ticket < ticket) { c->err = "ingest tickets must be waited in submission order"; return TXV_ESTATE; }
-    if (!g.flow_err && g.n_adm && s.ran) done = s.ev[4];
+    if (!g.flow_err && (g.n_adm || g.early) && s.ran) done = s.ev[4];
   }
   // the batch's chain ends without c->mu held (another thread's stages may run meanwhile); the
   // slot is not reused before this ticket is released below
@@ -3388,10 +3470,12 @@ int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_ev
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   int r = g.flow_err;
-  std::vector<uint8_t> fst(g.n_adm);
+  // an early chain ran over every message (its statuses by message index), a late one over the
+  // admitted ones (by their place in h_list)
+  std::vector<uint8_t> fst(g.early ? g.n : g.n_adm);
   std::vector<txv_commit_event> evs;
   uint32_t ne = 0;
-  if (!r && g.n_adm) {
+  if (!r && (g.n_adm || (g.early && s.ran))) {
     evs.resize(ev_out ? std::min(ev_cap, g.n_adm) : 0);
     r = fetch_slot(c, kIngestSlot + j, fst.data(), evs.data(), (uint32_t)evs.size(), &ne);
   } else if (r) {
@@ -3399,12 +3483,13 @@ int ingest_wait(txv_ctx* c, uint64_t ticket, uint8_t* flow_status, txv_commit_ev
   }
   if (flow_status) {
     for (uint32_t i = 0; i < g.n; ++i) flow_status[i] = TXV_FLOW_NOT_ADDED;
-    for (uint32_t q = 0; q < g.n_adm; ++q) flow_status[g.h_list[q]] = r ? (uint8_t)TXV_FLOW_NOT_RUN : fst[q];
+    for (uint32_t q = 0; q < g.n_adm; ++q)
+      flow_status[g.h_list[q]] = r ? (uint8_t)TXV_FLOW_NOT_RUN : fst[g.early ? g.h_list[q] : q];
   }
   if (!r) {
     for (uint32_t e = 0; e < std::min<uint32_t>(ne, (uint32_t)evs.size()); ++e) {   // batch index -> message index
       txv_commit_event x = evs[e];
-      x.vote_index = g.h_list[x.vote_index];
+      if (!g.early) x.vote_index = g.h_list[x.vote_index];
       ev_out[e] = x;
     }
     if (n_ev) *n_ev = ne;
@@ -3956,7 +4041,7 @@ int pooldev_stage(txv_ctx* c, PoolDev* s, int slot, uint32_t off, const txv_vote
 int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const uint8_t* h_keys_in,
                     const uint32_t* h_sizes, const uint32_t* d_keys, const uint32_t* d_sizes, const uint8_t* d_valid,
                     uint32_t valid_ok, uint32_t n, int64_t max_tx, bool wal, bool keys_back, void* after_ev,
-                    bool list_on, uint64_t live_ub, uint32_t n_upd) {
+                    bool list_on, uint64_t live_ub, uint32_t n_upd, uint8_t* d_status_copy, void* then_stream) {
   hipEvent_t after = (hipEvent_t)after_ev;
   HIP_TRY(c, hipSetDevice(c->device));
   const uint32_t total = n_upd + n;
@@ -3965,12 +4050,13 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (2 * ((uint64_t)s->C + total) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
   PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = engine_stream(c, s);
-  // batches whose keys are already in HBM (the wire ingest: decoded on the key stream, which also
-  // carries the batches' prep and SignBytes) run on the copy stream, which the wire path leaves to
-  // the Update uploads: C5 from wire bytes 74-76M vs 56-71M votes/s, while the SoA path's batches
-  // (uploaded on the copy stream) stay on the key stream (93M there vs 130M, profiles/r05/pstream).
-  // TXV_POOL_DEV_STREAM=2 (experiment) keeps them on the key stream.
-  static const int dev_stream = getenv("TXV_POOL_DEV_STREAM") ? atoi(getenv("TXV_POOL_DEV_STREAM")) : 3;
+  // every batch runs on the key stream: the wire ingest's uploads and decodes are on the copy
+  // stream (ingest_decode), so its decisions overlap the next batch's upload there.  Round 5 ran
+  // the wire batches' decisions on the copy stream while the decode sat on the key stream (74-76M
+  // votes/s); with the decode moved, the copy stream serialised each batch's 19 MB of uploads with
+  // its decisions (79-81M), the key stream overlaps them (98-100M, C5 from wire bytes, round 6).
+  // TXV_POOL_DEV_STREAM=3 (experiment): the wire batches' decisions on the copy stream.
+  static const int dev_stream = getenv("TXV_POOL_DEV_STREAM") ? atoi(getenv("TXV_POOL_DEV_STREAM")) : 2;
   if (!v && !h_keys_in && d_keys && n && dev_stream == 3 && s->on_ctx == 2) ks = c->copy_stream;
   // each batch reads the cache and pool list the previous one wrote, on whichever stream it ran
   if (s->last_ks && s->last_ks != ks) HIP_TRY(c, hipStreamWaitEvent(ks, s->last_ev, 0));
@@ -4021,7 +4107,7 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   a.push = s->push; a.aidx = s->aidx; a.hkey = s->hkey; a.hidx = s->hidx; a.skey = s->skey; a.sidx = s->sidx;
   a.last = s->last; a.lpos = s->lpos; a.dec = s->dec; a.pst = s->pst;
   a.pend = s->pend; a.xs = s->xs; a.xn = s->xn; a.far = s->far; a.nfar = s->nfar; a.detached = s->detached; a.surv = s->surv; a.spos = s->spos;
-  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status; a.status_out = f.m_status;
+  a.tmp = s->tmp; a.tmp_bytes = s->tmp_bytes; a.status = f.d_status; a.status_out = f.m_status; a.status_copy = d_status_copy;
   a.tiles = s->tiles; a.tk = s->tk; a.err = s->d_err; a.err_host = s->m_err; a.seed = s->seed;
   if (((++s->epoch) & 0x3FFFFFFFu) == 0) {          // the tag wrapped: no word may match by accident
     HIP_TRY(c, hipMemsetAsync(s->tiles, 0, pooldev_tile_words(s->cap_n, s->C) * 8, ks));
@@ -4052,6 +4138,8 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (keys_back && d_keys == f.d_keys && v && n)
     HIP_TRY(c, hipMemcpyAsync(f.h_keys, f.d_keys + (size_t)n_upd * 8, (size_t)n * 32, hipMemcpyDeviceToHost, ks));
   HIP_TRY(c, hipEventRecord(f.ev, ks));
+  // a consumer of the statuses in HBM (the wire ingest's TxFlow chain) waits for them on its stream
+  if (then_stream) HIP_TRY(c, hipStreamWaitEvent((hipStream_t)then_stream, f.ev, 0));
   s->last_ks = ks;
   s->last_ev = f.ev;
   return TXV_OK;
@@ -4082,7 +4170,7 @@ int pooldev_check(txv_ctx* c, PoolDev* s, const txv_votes* v, const uint8_t* h_k
   if (!n) return TXV_OK;
   HostTimer ht(c->profile_host);
   int r = pooldev_enqueue(c, s, slot, v, h_keys_in, h_sizes, d_keys, d_sizes, d_valid, valid_ok, n, max_tx, wal,
-                          keys_out != nullptr, after_ev, list_on, live_ub, n_upd);
+                          keys_out != nullptr, after_ev, list_on, live_ub, n_upd, nullptr, nullptr);
   if (r) return r;
   ht.mark("enqueue");
   const uint8_t* st;

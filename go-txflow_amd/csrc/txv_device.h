@@ -113,6 +113,8 @@ hipError_t txv_launch_rec_keys(const uint32_t* rec, const uint8_t* wire, uint32_
                                uint32_t* sizes, uint32_t* max_hl, hipStream_t st);
 hipError_t txv_launch_rec_to_flow(const uint32_t* rec, const uint32_t* list, uint32_t n, const FlowCols* c,
                                   hipStream_t st);
+hipError_t txv_launch_rec_to_flow_nil(const uint32_t* rec, const uint8_t* pool_status, uint32_t n, const FlowCols* c,
+                                      uint8_t* nil, hipStream_t st);
 // w = table window (4: LDS-staged B, 55 KB/point; 8: L2/MALL-resident, 396 KB/point)
 hipError_t txv_launch_build_tables(int w, const uint32_t* pubs_le, uint32_t n_points, uint32_t* tables,
                                    uint8_t* decode_ok, uint32_t* addr_words, hipStream_t st);
