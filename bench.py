@@ -178,7 +178,7 @@ def end_to_end_leg(ctx, wl, steps: int, registered: bool):
     t0 = time.perf_counter()
     for _ in range(steps):
         ctx.reset_flow()
-        if len(inflight) == T.SUBMIT_RING:
+        if len(inflight) == E2E_INFLIGHT:
             drain()
         inflight.append((time.perf_counter(), ctx.submit_votes(b)))
     while inflight:
@@ -194,6 +194,7 @@ def end_to_end_leg(ctx, wl, steps: int, registered: bool):
             "pcie_GBps": round(up_bytes * steps / el / 1e9, 2), "correct": ok}
 
 
+E2E_INFLIGHT = 3        # end-to-end leg: steps in flight (of the library's four-slot submit ring)
 C5_REPLAY = 0.05        # 5% exact replays in the stream
 C5_CACHE = 10000        # TxVotePool CacheSize: tendermint's default (config.DefaultMempoolConfig)
 
@@ -207,11 +208,12 @@ def c5_expected_pool(wl, cache_size: int):
     return [op.check_batch(b) for b in wl.batches]
 
 
-C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "2"))   # TxFlow batches in flight in the C5 leg (<= 3)
+C5_INFLIGHT = int(os.environ.get("TXV_C5_INFLIGHT", "4"))   # TxFlow batches in flight in the C5 leg (<= 4, the submit ring)
 # TxVotePool Size cap of the C5 legs: committed votes leave the pool through Update, so the pool
 # holds what CheckTx admitted ahead of the commits (~8 batches in the pipelines below) -- not the
 # stream (2.15M votes)
 C5_POOL_SIZE = 1 << 20
+C5_CHECKED = os.environ.get("TXV_C5_CHECKED", "1") != "0"   # C5 SoA: txv_submit_checked (0: statuses waited first)
 WIRE_INFLIGHT = int(os.environ.get("TXV_WIRE_INFLIGHT", "3"))   # wire batches between decode and wait (<= 3, the ingest ring)
 C5_LONG_POOL_SIZE = 1 << 23     # c5_long: leaked replay entries accumulate over 16M votes (see c5_long)
 # TXV_C5_NO_UPDATE=1 (experiment: the "without Update" figure of the same build): no Update calls,
@@ -351,6 +353,15 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
         if trace is not None:
             trace.append((what, k, round((a - t0) * 1e3, 4), round((b - t0) * 1e3, 4)))
 
+    # checked: the TxFlow submit of a device CheckTx batch (txv_submit_checked) does not wait for
+    # its statuses -- the AddVote chain reads them (and the signatures the CheckTx uploaded) in HBM
+    # behind the decisions; a status thread collects them for the report meanwhile
+    checked_mode = device_cache and C5_CHECKED
+    status_q = queue.Queue()
+    if checked_mode:                             # no host nil column: TxFlow takes the pool's from HBM
+        for b in wl.batches:
+            b.is_nil = None
+
     def prepare():
         for k, b in enumerate(wl.batches):
             ts = time.perf_counter()
@@ -359,11 +370,32 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
                     tk = pool.check_submit(b)
                     order.append(("c", k))
                 mark("check_submit", k, ts, time.perf_counter())
+                if checked_mode:
+                    status_q.put((k, ts, time.perf_counter(), tk))
+                    checked.put((k, ts, time.perf_counter(), tk))
+                    continue
                 prepared.put((k, ts, time.perf_counter(), None, tk))
             else:
                 keys, sizes = pool.prepare(b)
                 prepared.put((k, ts, time.perf_counter(), keys, sizes))
-        prepared.put(None)
+        if checked_mode:
+            status_q.put(None)
+            checked.put(None)
+        else:
+            prepared.put(None)
+
+    def statuses():                              # checked mode: the pool's statuses, for the report
+        while True:
+            item = status_q.get()
+            if item is None:
+                return
+            k, ts, tq, tk = item
+            tc = time.perf_counter()
+            pool_st[k] = pool.check_wait(tk)
+            tp = time.perf_counter()
+            mark("check_wait", k, tc, tp)
+            prep_ms.append((tq - ts) * 1e3)
+            admit_ms.append((tp - tc) * 1e3)
 
     def ingest():
         while True:
@@ -421,7 +453,7 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
 
     t0 = time.perf_counter()
     tpp = threading.Thread(target=prepare, daemon=True)
-    th = threading.Thread(target=ingest, daemon=True)
+    th = threading.Thread(target=statuses if checked_mode else ingest, daemon=True)
     td = threading.Thread(target=drain, daemon=True)
     tpp.start()
     th.start()
@@ -430,12 +462,15 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
         item = checked.get()
         if item is None:
             break
-        k, ts, tp = item
+        if checked_mode:
+            k, ts, tp, ptk = item
+        else:
+            k, ts, tp = item
         ta = time.perf_counter()
         slots.acquire()
         tb = time.perf_counter()
         submit.append(ts)
-        tickets.put((k, ctx.submit_votes(wl.batches[k])))
+        tickets.put((k, ctx.submit_checked(wl.batches[k], pool, ptk) if checked_mode else ctx.submit_votes(wl.batches[k])))
         mark("slot_wait", k, ta, tb)
         mark("submit_votes", k, tb, time.perf_counter())
     tpp.join()

@@ -569,6 +569,23 @@ extern "C" size_t txv_pooldev_tmp_bytes(uint32_t n, uint32_t C) {
   return c;
 }
 
+// a CheckTx batch's statuses as a TxFlow nil column (txv_submit_checked): the votes the pool did
+// not admit never reach AddVote's state (types/vote_set.go:93)
+__global__ void __launch_bounds__(256) txv_k_nil_from_status(const uint8_t* __restrict__ st, uint32_t n,
+                                                             uint8_t* __restrict__ nil, uint32_t or_nil) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t rej = st[i] != TXV_POOL_OK ? 1 : 0;
+  nil[i] = or_nil ? (uint8_t)(nil[i] | rej) : rej;
+}
+
+extern "C" hipError_t txv_launch_nil_from_status(const uint8_t* st, uint32_t n, uint8_t* nil, uint32_t or_nil,
+                                                 hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(txv_k_nil_from_status, dim3((n + 255) / 256), dim3(256), 0, s, st, n, nil, or_nil);
+  return hipGetLastError();
+}
+
 // the whole decision + cache update chain for one batch on stream st (a.n > 0; a.C > 0 or 0)
 extern "C" hipError_t txv_pooldev_run(const PoolDevArgs* ap, hipStream_t st) {
   const PoolDevArgs& a = *ap;

@@ -302,6 +302,12 @@ int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::ve
                      std::vector<uint8_t>& ins);
 void pooldev_result(const PoolDev* s, int slot, int64_t res[4]);
 constexpr int kPdRing = 4;   // = PoolDev::kPdRing (runtime.cpp)
+void pooldev_set_occupant(PoolDev* s, int slot, uint64_t id, uint32_t n_upd, uint32_t n);
+bool pooldev_holds(const PoolDev* s, uint64_t id);
+std::mutex& txv_ctx_submit_mu(txv_ctx* c);
+int submit_checked_stage(txv_ctx* c, const txv_votes* v, uint32_t* slot_out);
+int submit_checked_consume(txv_ctx* c, uint32_t slot, PoolDev* dev, uint64_t pool_ticket, const txv_votes* v);
+int submit_checked_run(txv_ctx* c, uint32_t slot, const txv_votes* v, const uint8_t* host_st, int why, uint64_t* ticket);
 
 struct txv_pool {
   txv_pool_config cfg{};
@@ -359,6 +365,8 @@ struct txv_pool {
     uint32_t n_upd = 0;
   };
   std::deque<Ticket> tickets;
+  // the statuses of the last tickets waited (txv_submit_checked may come after the wait)
+  std::deque<std::pair<uint64_t, std::vector<uint8_t>>> recent;
   // Update entries staged (keyed on the engine's stream) in flight slot pend_slot, decided with the
   // next device CheckTx batch, which takes that slot, or alone by flush_pending
   int pend_slot = -1;
@@ -1479,27 +1487,24 @@ int txv_pool_check_keys(txv_pool* p, txv_ctx* ctx, const uint8_t* keys32, const 
 int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* sig_full,
                           const uint64_t* sig_full_off, uint64_t* ticket) {
   if (!p || !ctx || !v || !ticket) return TXV_EINVAL;
-  std::lock_guard<std::mutex> g(p->mu);
   *ticket = 0;
   const auto t0 = std::chrono::steady_clock::now();
-  txv_pool::Ticket t;
-  t.id = p->next_ticket;
-  t.n = v->n;
-  t.ctx = ctx;
-  p->sizes.resize(v->n);
-  if (dev_mode(p) && v->n) {
-    // the device path: Size() on the host workers (with the pushes, the bytes and any long
-    // signature), then keys, decisions and the new cache enqueued on the GPU
-    const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
-    PTimer pt("check_submit");
-    std::atomic<uint64_t> pushes{0}, bytes{0};
-    std::atomic<bool> long_sig{false};
+  // the device path: Size() on the host workers (with the pushes, the bytes and any long
+  // signature) before the pool's lock is taken (cfg is fixed at txv_pool_new), then keys,
+  // decisions and the new cache enqueued on the GPU
+  const bool dev = dev_mode(p) && v->n;
+  const int64_t max_tx = (int64_t)p->cfg.max_msg_bytes - 8;
+  std::vector<uint32_t> dsz;
+  std::atomic<uint64_t> pushes{0}, bytes{0};
+  std::atomic<bool> long_sig{false};
+  if (dev) {
+    dsz.resize(v->n);
     txv_host_parallel_for(ctx, v->n, [&](uint32_t lo, uint32_t hi) {
       uint64_t pu = 0, by = 0;
       bool lg = false;
       for (uint32_t i = lo; i < hi; ++i) {
         const uint32_t sz = vote_size(v, i);
-        p->sizes[i] = sz;
+        dsz[i] = sz;
         pu += (int64_t)sz <= max_tx;
         by += sz;
         lg |= v->sig_len[i] > 64;
@@ -1508,7 +1513,15 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
       bytes.fetch_add(by, std::memory_order_relaxed);
       if (lg) long_sig.store(true, std::memory_order_relaxed);
     });
-    pt.mark("sizes");
+  }
+  std::lock_guard<std::mutex> g(p->mu);
+  txv_pool::Ticket t;
+  t.id = p->next_ticket;
+  t.n = v->n;
+  t.ctx = ctx;
+  p->sizes.resize(v->n);
+  if (dev) {
+    PTimer pt("check_submit");
     if (!long_sig.load() && dev_caps_ok(p, pushes.load(), bytes.load())) {
       int r;
       p->batch_hint = std::max(p->batch_hint, v->n);
@@ -1523,10 +1536,11 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
       pt.mark("prev");
       p->pend_n = 0;
       p->pend_slot = -1;
-      if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, p->sizes.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
+      if ((r = pooldev_enqueue(ctx, p->dev, slot, v, nullptr, dsz.data(), nullptr, nullptr, nullptr, 0, v->n, max_tx,
                                (p->cfg.flags & TXV_POOL_WAL) != 0, false, nullptr, true, live_ub(p), n_upd)))
         return r;
       t.n_upd = n_upd;
+      pooldev_set_occupant(p->dev, slot, t.id, n_upd, v->n);   // txv_submit_checked may read it from HBM
       pt.mark("enqueue");
       if (p->cache_on) p->dev_state = txv_pool::kDevAhead;
       p->next_slot = (slot + 1) % kPdRing;
@@ -1559,6 +1573,58 @@ int txv_pool_check_submit(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const u
   return TXV_OK;
 }
 
+// TryAddVote for the batch a CheckTx ticket is deciding (include/txvote.h): while the batch is in
+// the engine's flight slot its signatures and statuses are read there on the GPU (the TxFlow chain
+// queued behind the decisions, no host round trip, no second upload); otherwise the ticket's
+// statuses are taken on the host (waiting for them if need be) and the caller's columns staged.
+// The pool ticket stays the caller's to wait (txv_pool_check_wait).  Takes p->mu, then the
+// context's lock.
+int txv_submit_checked(txv_ctx* ctx, const txv_votes* v, txv_pool* p, uint64_t pool_ticket, uint64_t* ticket) {
+  if (!ctx || !v || !p || !pool_ticket || !ticket) return TXV_EINVAL;
+  std::lock_guard<std::mutex> so(txv_ctx_submit_mu(ctx));   // no other submit between the steps
+  uint32_t slot;
+  int r;
+  if ((r = submit_checked_stage(ctx, v, &slot))) return r;   // the host staging: no pool lock held
+  std::vector<uint8_t> st;
+  int why = 0;
+  bool consumed = false;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    // the reads of the engine's slot are enqueued under the pool's lock: a later writer of the
+    // slot (also under it) waits for them on the GPU
+    if (p->dev && pooldev_same_device(ctx, p->dev) && pooldev_holds(p->dev, pool_ticket)) {
+      if ((r = submit_checked_consume(ctx, slot, p->dev, pool_ticket, v)) < 0) return r;
+      consumed = r == 0;
+    }
+  }
+  if (consumed) return submit_checked_run(ctx, slot, v, nullptr, 0, ticket);
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = std::find_if(p->tickets.begin(), p->tickets.end(), [&](const txv_pool::Ticket& t) { return t.id == pool_ticket; });
+    if (it == p->tickets.end()) {                  // waited already: its statuses, if still kept
+      why = 1;
+      for (const auto& rc : p->recent)
+        if (rc.first == pool_ticket) {
+          why = rc.second.size() != v->n ? 2 : 0;
+          if (!why) st = rc.second;
+        }
+    } else if (it->upd) {
+      why = 1;
+    } else if (it->n != v->n) {
+      why = 2;
+    } else {
+      if (!it->done)
+        for (auto jt = p->tickets.begin(); jt != p->tickets.end(); ++jt) {   // the earlier ones first: append order
+          if (int e = finish_ticket(p, *jt)) return e;
+          if (jt == it) break;
+        }
+      if (it->err) return it->err;
+      st = it->st;
+    }
+  }
+  return submit_checked_run(ctx, slot, v, why ? nullptr : st.data(), why, ticket);
+}
+
 // the statuses of a submitted batch (tickets in submission order); the engine's event is waited
 // for without p->mu held, so batch k+1 can be submitted meanwhile
 int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
@@ -1587,6 +1653,10 @@ int txv_pool_check_wait(txv_pool* p, uint64_t ticket, uint8_t* status_out) {
     if (it->id != ticket) continue;
     r = e;
     if (!r && it->n && status_out) memcpy(status_out, it->st.data(), it->n);
+    if (!r && !it->upd) {
+      if (p->recent.size() >= 8) p->recent.pop_front();
+      p->recent.emplace_back(it->id, std::move(it->st));
+    }
     p->tickets.erase(it);
     prune_updates(p);
     pt.mark("finish");
@@ -1624,14 +1694,9 @@ int txv_pool_prepare(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_
 // before -- no flight is drained, nothing is copied back but the removal counts.  Size and
 // TxsBytes follow once the tickets submitted before are finished (txv_pool_check_wait,
 // txv_pool_sync, any reader).  Signatures > 64 bytes take the host path.
-int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
+int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint32_t* sizes) {
   const uint32_t n = v->n;
   PTimer pt("update_submit");
-  p->sizes.resize(n);
-  pool_parallel_for(p, ctx, n, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) p->sizes[i] = vote_size(v, i);
-  }, 4096);
-  pt.mark("sizes");
   int r;
   // room for the next CheckTx batch beside the staged entries, so they ride with it instead of
   // being decided alone (a chain of their own) when it comes.  Updates that stack up before the
@@ -1650,7 +1715,7 @@ int update_submit_dev(txv_pool* p, txv_ctx* ctx, const txv_votes* v) {
     p->pend_ctx = ctx;
   }
   pt.mark("prev");
-  if ((r = pooldev_stage(ctx, p->dev, p->pend_slot, p->pend_n, v, p->sizes.data()))) return r;
+  if ((r = pooldev_stage(ctx, p->dev, p->pend_slot, p->pend_n, v, sizes))) return r;
   p->pend_n += n;
   pt.mark("stage");
   return TXV_OK;
@@ -1692,13 +1757,23 @@ int update_host(txv_pool* p, txv_ctx* ctx, const txv_votes* v, const uint8_t* si
 int txv_pool_update_submit(txv_pool* p, txv_ctx* ctx, int64_t height, const txv_votes* v, const uint8_t* sig_full,
                            const uint64_t* sig_full_off) {
   if (!p || !ctx || !v || (v->n && (!v->sig || !v->sig_len))) return TXV_EINVAL;
+  // the device path's TxVote.Size() values before the pool's lock is taken
+  std::vector<uint32_t> dsz;
+  bool lg = false;
+  if (dev_mode(p) && v->n) {
+    for (uint32_t i = 0; i < v->n && !lg; ++i) lg = v->sig_len[i] > 64;
+    if (!lg) {
+      dsz.resize(v->n);
+      auto fill = [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; ++i) dsz[i] = vote_size(v, i);
+      };
+      if (ctx) txv_host_parallel_for(ctx, v->n, fill);
+      else fill(0, v->n);
+    }
+  }
   std::lock_guard<std::mutex> g(p->mu);
   p->height = height;
-  if (dev_mode(p) && v->n) {
-    bool lg = false;
-    for (uint32_t i = 0; i < v->n && !lg; ++i) lg = v->sig_len[i] > 64;
-    if (!lg) return update_submit_dev(p, ctx, v);
-  }
+  if (!dsz.empty()) return update_submit_dev(p, ctx, v, dsz.data());
   return update_host(p, ctx, v, sig_full, sig_full_off);
 }
 

@@ -63,7 +63,7 @@ inline bool valid_window(int w) {
 #define TXV_K1A_ON_KEY_STREAM 0
 #endif
 constexpr uint32_t kStagedSlots = 4;   // 0-3 staged (0-2 also the submit ring)
-constexpr uint32_t kSubmitRing = 3;    // txv_submit_votes batches in flight
+constexpr uint32_t kSubmitRing = 4;    // txv_submit_votes batches in flight
 constexpr uint32_t kVcodeEmpty = TXV_VCODE_EMPTY, kVcodeUnknown = TXV_VCODE_UNKNOWN;   // txv_flow.h
 // batches from which the pack threads look validators up (the link time the 18 bytes per vote
 // save outweighs the host work there: C2's 1M-vote batches 593.4M vs 518.3M votes/s end to end,
@@ -301,6 +301,8 @@ struct txv_ctx {
     int flow_err = 0;              // the admitted votes' AddVote chain could not be enqueued
     std::string flow_msg;
   } ing[kIngestRing];
+  std::mutex sub_mu;               // txv_submit_votes / txv_submit_checked one at a time (the latter stages,
+                                   // takes the pool's lock, then runs: no other submit in between)
   std::mutex ing_dec_mu;           // decodes one at a time (they hand out the tickets)
   std::mutex ing_adm_mu;           // admissions one at a time, in ticket order: pool order = TxFlow order
   std::mutex ing_fin_mu;           // the admissions' second halves (ingest_admit_finish), in ticket order
@@ -1789,6 +1791,7 @@ int txv_add_votes(txv_ctx* c, const txv_votes* v, uint8_t* status_out, txv_commi
 
 int txv_submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
   if (!c || !v || !ticket) return TXV_EINVAL;
+  std::lock_guard<std::mutex> so(c->sub_mu);
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   return submit_votes(c, v, ticket);
@@ -3646,6 +3649,14 @@ struct PoolDev {
     uint32_t nt_app = 0, nt_rm = 0;                // tiles of the batch in flight with partials there
     hipEvent_t ev = nullptr;
     hipEvent_t up_ev = nullptr;                    // the slot's signature uploads done (copy stream)
+    // a CheckTx batch whose signatures and statuses a TxFlow chain reads straight from this slot
+    // (txv_submit_checked): the pool ticket holding them (0 once anything else is staged here),
+    // its Update entries ahead of it and its votes; cons_ev ends the reads (every later write to
+    // the slot waits for it on the GPU)
+    uint64_t occ = 0;
+    uint32_t occ_upd = 0, occ_n = 0;
+    hipEvent_t cons_ev = nullptr;
+    bool cons = false;
   } fl[kPdRing];
   uint32_t* h_clen = nullptr;
   hipEvent_t ev = nullptr;
@@ -3672,6 +3683,7 @@ struct PoolDev {
       hfree(f.h_sig); hfree(f.h_len); hfree(f.h_keys); hfree(f.h_sizes); hfree(f.h_status); hfree(f.h_res);
       if (f.ev) (void)hipEventDestroy(f.ev);
       if (f.up_ev) (void)hipEventDestroy(f.up_ev);
+      if (f.cons_ev) (void)hipEventDestroy(f.cons_ev);
     }
     if (tmp) (void)hipFree(tmp);
     hfree(h_clen);
@@ -3751,6 +3763,7 @@ int pooldev_bind(txv_ctx* c, PoolDev** sp, uint32_t C, uint32_t n) {
     // geometric growth: an Update riding with a batch makes n vary, and every growth reallocates
     // (hipFree synchronises the device)
     const uint32_t m = std::max<uint32_t>(std::max<uint32_t>(n, 1024), s->cap_n ? 2 * s->cap_n : 0u);
+    if (getenv("TXV_PROFILE_HOST")) fprintf(stderr, "[txv pool] engine grows %u -> %u entries\n", s->cap_n, m);
     if ((r = dalloc(c, &s->push, m)) || (r = dalloc(c, &s->aidx, m)) || (r = dalloc(c, &s->hkey, m)) ||
         (r = dalloc(c, &s->hidx, m)) || (r = dalloc(c, &s->skey, m)) || (r = dalloc(c, &s->sidx, m)) ||
         (r = dalloc(c, &s->last, m)) ||
@@ -3879,6 +3892,8 @@ int list_compact(txv_ctx* c, PoolDev* s, hipStream_t ks, uint64_t live_ub, uint3
   PoolDev::ListBuf& o = s->lb[s->lcur];
   PoolDev::ListBuf& nb = s->lb[s->lcur ^ 1];
   const uint32_t ncap = std::max(o.cap, list_cap_for(2 * (live_ub + n)));
+  if (getenv("TXV_PROFILE_HOST"))
+    fprintf(stderr, "[txv pool] list compaction: cap %u -> %u, live <= %llu\n", o.cap, ncap, (unsigned long long)live_ub);
   if (!ncap) { c->err = "pool list above 2^30 entries"; return TXV_ECAPACITY; }
   const size_t tb = txv_poollist_tmp_bytes(o.cap);
   if (nb.cap < ncap || s->lnpos_cap < o.cap || s->ltmp_bytes < tb) {
@@ -4006,6 +4021,8 @@ int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes
       memcpy(f.h_len + off + lo, v->sig_len + lo, (size_t)(hi - lo) * 4);
     }, 4096);
   memcpy(f.h_sizes + off, h_sizes, (size_t)n * 4);
+  f.occ = 0;
+  if (f.cons) HIP_TRY(c, hipStreamWaitEvent(us, f.cons_ev, 0));   // a TxFlow chain's reads of the slot first
   HIP_TRY(c, hipMemcpyAsync(f.d_sig + (size_t)off * 16, reg ? (const void*)v->sig : (const void*)(f.h_sig + (size_t)off * 16),
                             (size_t)n * 64, hipMemcpyHostToDevice, us));
   HIP_TRY(c, hipMemcpyAsync(f.d_len + off, reg ? (const void*)v->sig_len : (const void*)(f.h_len + off), (size_t)n * 4,
@@ -4050,6 +4067,8 @@ int pooldev_enqueue(txv_ctx* c, PoolDev* s, int slot, const txv_votes* v, const 
   if (2 * ((uint64_t)s->C + total) >= 0xFFFFFFFFull) { c->err = "pool device batch: S positions exceed 32 bits"; return TXV_ECAPACITY; }
   PoolDev::Flight& f = s->fl[slot];
   hipStream_t ks = engine_stream(c, s);
+  f.occ = 0;
+  if (f.cons) HIP_TRY(c, hipStreamWaitEvent(ks, f.cons_ev, 0));   // a TxFlow chain's reads of the slot first
   // every batch runs on the key stream: the wire ingest's uploads and decodes are on the copy
   // stream (ingest_decode), so its decisions overlap the next batch's upload there.  Round 5 ran
   // the wire batches' decisions on the copy stream while the decode sat on the key stream (74-76M
@@ -4159,6 +4178,113 @@ int pooldev_finish(txv_ctx* c, PoolDev* s, int slot, const uint8_t** status, con
   if (status) *status = f.h_status;
   if (keys) *keys = reinterpret_cast<const uint8_t*>(f.h_keys);
   if (sizes) *sizes = f.h_sizes;
+  return TXV_OK;
+}
+
+// flight slot `slot` holds pool ticket `id`'s batch (n votes after n_upd Update entries): a TxFlow
+// chain may read its signatures and statuses from HBM (pooldev_consume) until the slot is reused
+void pooldev_set_occupant(PoolDev* s, int slot, uint64_t id, uint32_t n_upd, uint32_t n) {
+  PoolDev::Flight& f = s->fl[slot];
+  f.occ = id;
+  f.occ_upd = n_upd;
+  f.occ_n = n;
+}
+
+// txv_submit_checked: pool ticket `id`'s signatures ([n][64] bytes) into sig_out and its statuses
+// as the nil column (nil_out[i] = status != TXV_POOL_OK, or-ed into the column's caller values
+// when or_nil) on stream st, behind the batch's decisions; the slot's next writer waits for these
+// reads.  1: the ticket's batch is no longer in any slot (the caller takes its host statuses).
+int pooldev_consume(txv_ctx* c, PoolDev* s, uint64_t id, uint32_t n, hipStream_t st, uint8_t* sig_out, uint8_t* nil_out,
+                    bool or_nil) {
+  if (!s || !id) return 1;
+  for (PoolDev::Flight& f : s->fl) {
+    if (f.occ != id) continue;
+    if (f.occ_n != n) { c->err = "txv_submit_checked: the batch differs from the pool ticket's"; return TXV_EINVAL; }
+    if (!f.cons_ev) HIP_TRY(c, hipEventCreateWithFlags(&f.cons_ev, hipEventDisableTiming));
+    HIP_TRY(c, hipStreamWaitEvent(st, f.ev, 0));
+    HIP_TRY(c, hipMemcpyAsync(sig_out, f.d_sig + (size_t)f.occ_upd * 16, (size_t)n * 64, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, txv_launch_nil_from_status(f.d_status + f.occ_upd, n, nil_out, or_nil ? 1u : 0u, st));
+    HIP_TRY(c, hipEventRecord(f.cons_ev, st));
+    f.cons = true;
+    return 0;
+  }
+  return 1;
+}
+
+bool pooldev_holds(const PoolDev* s, uint64_t id) {
+  if (!s || !id) return false;
+  for (const PoolDev::Flight& f : s->fl)
+    if (f.occ == id) return true;
+  return false;
+}
+
+// txv_submit_checked's context half, in three steps (pool.cpp drives them, one submitter at a
+// time under txv_ctx::sub_mu): stage the batch's columns but its signatures, then -- the pool's
+// lock held -- take the signatures and nil column from the CheckTx batch still in the pool
+// engine's flight slot (pooldev_consume), or else upload them from the caller's columns with the
+// ticket's host statuses as the nil column, then enqueue the AddVote chain.
+std::mutex& txv_ctx_submit_mu(txv_ctx* c) { return c->sub_mu; }
+
+int submit_checked_stage(txv_ctx* c, const txv_votes* v, uint32_t* slot_out) {
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t slot = (uint32_t)((c->next_ticket - 1) % kSubmitRing);
+  if (c->slots[slot].ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
+  txv_votes w = *v;
+  w.sig = nullptr;                 // from the pool's flight slot (or uploaded late)
+  w.is_nil = nullptr;              // written on the device (or uploaded late)
+  if (int r = stage_add(c, slot, &w)) return r;
+  *slot_out = slot;
+  return TXV_OK;
+}
+
+// the device source (the pool's lock held): 1 = the batch is no longer in the engine
+int submit_checked_consume(txv_ctx* c, uint32_t slot, PoolDev* dev, uint64_t pool_ticket, const txv_votes* v) {
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  Slot& s = c->slots[slot];
+  if (!v->n) return TXV_OK;
+  // behind the uploads (and the slot's previous chain: stage_add's copy stream waited for it), on
+  // the key stream, which carries the pool's decisions too
+  hipStream_t ks = c->key_stream;
+  HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[3], 0));
+  if (v->is_nil) {                 // the caller's nil column first, or-ed into below
+    memcpy(s.h_nil, v->is_nil, v->n);
+    HIP_TRY(c, hipMemcpyAsync(s.d_nil, s.h_nil, v->n, hipMemcpyHostToDevice, ks));
+  }
+  const int r = pooldev_consume(c, dev, pool_ticket, v->n, ks, s.d_sigraw, s.d_nil, v->is_nil != nullptr);
+  if (r) return r;
+  HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's streams wait for the columns here
+  return TXV_OK;
+}
+
+// the host source / the chain: why 1 = unknown pool ticket, 2 = another batch size; host_st (or
+// null after a device consume) = the ticket's statuses
+int submit_checked_run(txv_ctx* c, uint32_t slot, const txv_votes* v, const uint8_t* host_st, int why, uint64_t* ticket) {
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (why == 1) { c->err = "txv_submit_checked: unknown pool ticket (already waited?)"; return TXV_ESTATE; }
+  if (why == 2) { c->err = "txv_submit_checked: the batch differs from the pool ticket's"; return TXV_EINVAL; }
+  Slot& s = c->slots[slot];
+  const uint32_t n = v->n;
+  if (host_st && n) {              // the signatures and nil column from the host after all
+    for (uint32_t i = 0; i < n; ++i) s.h_nil[i] = (host_st[i] != TXV_POOL_OK || (v->is_nil && v->is_nil[i])) ? 1 : 0;
+    const bool reg = is_registered(c, v->sig, (uint64_t)n * 64);
+    if (!reg) c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+      memcpy(s.h_sigraw + (size_t)lo * 64, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+    }, 4096);
+    HIP_TRY(c, hipMemcpyAsync(s.d_sigraw, reg ? (const void*)v->sig : (const void*)s.h_sigraw, (size_t)n * 64,
+                              hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(c, hipMemcpyAsync(s.d_nil, s.h_nil, n, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));
+  }
+  s.has_nil = true;
+  int r;
+  if ((r = run_slot(c, slot, nullptr))) return r;
+  const uint64_t t = c->next_ticket;
+  s.ticket = t;
+  c->next_ticket = t + 1;
+  *ticket = t;
   return TXV_OK;
 }
 

@@ -132,6 +132,7 @@ hipError_t txv_launch_sign(const SignArgs* args, hipStream_t st);
 hipError_t txv_launch_valu_probe(int op, uint32_t* out, uint32_t blocks, int iters, hipStream_t st);
 hipError_t txv_launch_signbytes(const SignBytesArgs* args, hipStream_t st);
 bool txv_k1b_fusable(int wb, const VerifyArgs* args);   // the launch takes the work-stealing K1b
+hipError_t txv_launch_nil_from_status(const uint8_t* st, uint32_t n, uint8_t* nil, uint32_t or_nil, hipStream_t s);
 hipError_t txv_launch_sig_keys(const uint32_t* sig, const uint32_t* sig_len, uint32_t n, uint32_t* keys,
                                 hipStream_t st);
 hipError_t txv_launch_fe_selftest(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n, int op,

@@ -136,6 +136,8 @@ def lib():
             "txv_copy_set_sums": ([vp, vp, u32], ctypes.c_int),
             "txv_get_votes": ([vp, ctypes.c_char_p, u32, vp, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_submit_votes": ([vp, ctypes.POINTER(_Votes), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "txv_submit_checked": ([vp, ctypes.POINTER(_Votes), vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)],
+                                   ctypes.c_int),
             "txv_wait_votes": ([vp, ctypes.c_uint64, vp, vp, u32, ctypes.POINTER(u32)], ctypes.c_int),
             "txv_pool_new": ([ctypes.POINTER(_PoolCfg), i64, ctypes.POINTER(vp)], ctypes.c_int),
             "txv_pool_free": ([vp], None),
@@ -209,7 +211,7 @@ EXPORTED_SYMBOLS = [
     "txv_total_power", "txv_signbytes", "txv_txvote_size", "txv_keygen", "txv_sign_votes", "txv_stage",
     "txv_run_staged", "txv_fetch_staged", "txv_commit_bitmap", "txv_reset_tally", "txv_reset_flow", "txv_sync", "txv_fe_selftest",
     "txv_copy_commit_bitmap", "txv_valu_probe", "txv_table_window", "txv_validator_tables_built", "txv_staged_bytes", "txv_base_window", "txv_sig_keys",
-    "txv_submit_votes", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
+    "txv_submit_votes", "txv_submit_checked", "txv_wait_votes", "txv_bind_host_numa", "txv_get_votes", "txv_copy_set_sums",
     "txv_pool_new", "txv_pool_free", "txv_pool_check", "txv_pool_check_keys", "txv_pool_update", "txv_pool_update_keys", "txv_pool_reap", "txv_pool_flush",
     "txv_pool_size", "txv_pool_txs_bytes", "txv_pool_height", "txv_pool_cache_keys", "txv_pool_sync",
     "txv_pool_check_submit", "txv_pool_check_wait", "txv_pool_update_submit",
@@ -620,6 +622,18 @@ class Context:
         self._inflight[t.value] = batch.n
         return t.value
 
+    def submit_checked(self, batch: VoteBatch, pool, pool_ticket: int) -> int:
+        """txv_submit_checked: TryAddVote for the batch TxVotePool.check_submit(batch) returned
+        pool_ticket for -- the votes the pool did not admit as nil entries, decided on the device
+        behind the pool's decisions (no wait for its statuses); a ticket for wait_votes"""
+        t = ctypes.c_uint64()
+        vs = batch.c_struct()
+        self._chk(lib().txv_submit_checked(self._h, ctypes.byref(vs), pool._h, pool_ticket, ctypes.byref(t)),
+                  "txv_submit_checked")
+        self._inflight = getattr(self, "_inflight", {})
+        self._inflight[t.value] = batch.n
+        return t.value
+
     def wait_votes(self, ticket: int, ev_cap: int = 0):
         n = getattr(self, "_inflight", {}).get(ticket, 0)   # kept until the library took the ticket
         out = np.zeros(max(n, 1), np.uint8)
@@ -942,7 +956,7 @@ class IngestTicket:
         self.ticket, self.n, self.wire_status, self.pool_status = ticket, n, ws, ps
 POOL_NO_CACHE = 0xFFFFFFFF
 POOL_WAL = 0x1      # TXV_POOL_WAL
-SUBMIT_RING = 3         # txv_submit_votes batches in flight (staged slots 0 .. 2)
+SUBMIT_RING = 4         # txv_submit_votes batches in flight (staged slots 0 .. 3)
 POOL_DEVICE_CACHE = 0x2   # TXV_POOL_DEVICE_CACHE: the LRU cache in HBM, CheckTx decisions on the GPU
 
 

@@ -449,6 +449,16 @@ int txv_pool_check(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const u
 int txv_pool_check_submit(txv_pool* pool, txv_ctx* ctx, const txv_votes* votes, const uint8_t* sig_full,
                           const uint64_t* sig_full_off, uint64_t* ticket);
 int txv_pool_check_wait(txv_pool* pool, uint64_t ticket, uint8_t* status_out);
+/* TryAddVote for the batch pool_ticket (txv_pool_check_submit on the same batch) is deciding, as
+ * the reactor hands CheckTx's accepted votes to checkMaj23Routine (txvotepool/reactor.go:170-190 ->
+ * txflow/service.go:123-166): like txv_submit_votes (ticket for txv_wait_votes), the votes the
+ * pool did not admit as nil entries.  While the CheckTx batch is still in the pool engine's flight
+ * slot (TXV_POOL_DEVICE_CACHE) the AddVote chain is enqueued behind its decisions and reads its
+ * statuses and already uploaded signatures in HBM: the call does not wait for them; otherwise
+ * the ticket's statuses are taken on the host.  votes->is_nil, if given, is or-ed in.  The pool
+ * ticket is still waited by the caller (txv_pool_check_wait, before or after this call).  Takes
+ * the pool's lock, then the context's. */
+int txv_submit_checked(txv_ctx* ctx, const txv_votes* votes, txv_pool* pool, uint64_t pool_ticket, uint64_t* ticket);
 /* CheckTxWithInfo for n votes given as (txVoteKey, TxVote.Size()) pairs in arrival order: keys32
  * n x 32 bytes (SHA-256(Signature), txvotepool.go:467-469), sizes[i] = Size() (0 when amino
  * rejects the timestamp); status_out[i] = TXV_POOL_*.  ctx (optional) lends its host workers;

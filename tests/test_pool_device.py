@@ -503,3 +503,78 @@ def test_device_cache_wire_and_soa_batches_interleaved():
         pool.close()
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["device", "ahead", "waited"])
+def test_submit_checked_equals_host_statuses(mode):
+    """txv_submit_checked (TryAddVote for the batch a CheckTx ticket is deciding; the pool's
+    rejections as nil entries read from HBM behind its decisions, the signatures the CheckTx
+    uploaded reused) against the two-call path -- txv_pool_check's statuses as the host's is_nil
+    column of txv_submit_votes -- on a C5-like stream with 5 % exact replays and a small cache:
+    every TxFlow status (fired bits included), commit event and pool status equal.  "device":
+    submitted right after each CheckTx; "ahead": six CheckTx batches submitted first (the engine's
+    four flight slots reused: the first batches take the host statuses); "waited": each pool ticket
+    waited before its TxFlow submit.  Reference: txvotepool/reactor.go:170-190 ->
+    txflow/service.go:123-166."""
+    import txflow_amd as T
+    from txflow_amd.workload import StreamWorkload, SEEDS
+    ctx = T.Context(max_batch=4096, max_txs=1024, max_validators=32)
+    try:
+        wl = StreamWorkload(ctx, 24, 800, SEEDS["c5"] + 7, 2048, replay=0.05)
+        cfg = dict(size=1 << 20, cache_size=600, max_txs_bytes=1 << 40)
+
+        def reference():
+            pool = T.TxVotePool(ctx, **cfg, device_cache=True)
+            out = []
+            for b in wl.batches:
+                ps = pool.check_batch(b)
+                b.is_nil = (ps != T.POOL_OK).astype(np.uint8)
+                st, ev = ctx.wait_votes(ctx.submit_votes(b), ev_cap=b.n)
+                b.is_nil = None
+                out.append((ps, st, sorted((int(e["vote_index"]), int(e["tx_index"]), int(e["sum"])) for e in ev)))
+            pool.close()
+            ctx.reset_flow()
+            return out
+
+        def checked():
+            pool = T.TxVotePool(ctx, **cfg, device_cache=True)
+            out = [None] * len(wl.batches)
+            ahead = 6 if mode == "ahead" else 1
+            tks, flows = {}, []
+
+            def flow_submit(j):
+                if len(flows) == 2:                     # two TxFlow batches in flight
+                    jj, ft, pps = flows.pop(0)
+                    st, ev = ctx.wait_votes(ft, ev_cap=wl.batches[jj].n)
+                    out[jj] = (pps if pps is not None else pool.check_wait(tks[jj]), st,
+                               sorted((int(e["vote_index"]), int(e["tx_index"]), int(e["sum"])) for e in ev))
+                ps = pool.check_wait(tks[j]) if mode == "waited" else None
+                flows.append((j, ctx.submit_checked(wl.batches[j], pool, tks[j]), ps))
+
+            for k, b in enumerate(wl.batches):
+                tks[k] = pool.check_submit(b)
+                if k - ahead + 1 >= 0:
+                    flow_submit(k - ahead + 1)
+            for j in range(max(0, len(wl.batches) - ahead + 1), len(wl.batches)):
+                flow_submit(j)
+            while flows:
+                jj, ft, pps = flows.pop(0)
+                st, ev = ctx.wait_votes(ft, ev_cap=wl.batches[jj].n)
+                out[jj] = (pps if pps is not None else pool.check_wait(tks[jj]), st,
+                           sorted((int(e["vote_index"]), int(e["tx_index"]), int(e["sum"])) for e in ev))
+            pool.close()
+            ctx.reset_flow()
+            return out
+
+        ref = reference()
+        got = checked()
+        assert len(ref) == len(got) >= 8
+        for k, ((rps, rst, rev), (gps, gst, gev)) in enumerate(zip(ref, got)):
+            assert np.array_equal(rps, gps), f"batch {k}: pool statuses differ"
+            assert np.array_equal(rst, gst), f"batch {k}: {int(np.count_nonzero(rst != gst))} TxFlow statuses differ"
+            assert rev == gev, f"batch {k}: commit events differ"
+        assert sum(int((r[0] == T.POOL_ERR_IN_CACHE).sum()) for r in ref) > 0
+        assert sum(len(r[2]) for r in ref) > 0
+    finally:
+        ctx.close()
