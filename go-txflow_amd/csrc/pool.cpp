@@ -167,7 +167,11 @@ struct PTimer {
   std::chrono::steady_clock::time_point t;
   std::string line;
   explicit PTimer(const char* what) : on(getenv("TXV_PROFILE_HOST") != nullptr), t(std::chrono::steady_clock::now()) {
-    if (on) line = what;
+    if (on) {   // the start on the monotonic clock (Python's time.perf_counter), for traces
+      char b[48];
+      snprintf(b, sizeof b, " @%.4f", std::chrono::duration<double>(t.time_since_epoch()).count());
+      line = std::string(what) + b;
+    }
   }
   void mark(const char* what) {
     if (!on) return;

@@ -326,7 +326,13 @@ struct HostTimer {
   bool on;
   std::chrono::steady_clock::time_point t;
   std::string line;
-  explicit HostTimer(bool o) : on(o), t(std::chrono::steady_clock::now()) {}
+  explicit HostTimer(bool o) : on(o), t(std::chrono::steady_clock::now()) {
+    if (on) {   // the start on the monotonic clock (Python's time.perf_counter), for traces
+      char b[48];
+      snprintf(b, sizeof b, " @%.4f", std::chrono::duration<double>(t.time_since_epoch()).count());
+      line = b;
+    }
+  }
   void mark(const char* what) {
     if (!on) return;
     const auto now = std::chrono::steady_clock::now();
@@ -335,7 +341,7 @@ struct HostTimer {
     line += b;
     t = now;
   }
-  ~HostTimer() { if (on && !line.empty()) fprintf(stderr, "[txv host]%s\n", line.c_str()); }
+  ~HostTimer() { if (on && line.find('=') != std::string::npos) fprintf(stderr, "[txv host]%s\n", line.c_str()); }
 };
 
 template <typename T>
@@ -1294,7 +1300,7 @@ int submit_votes(txv_ctx* c, const txv_votes* v, uint64_t* ticket) {
   const uint64_t t = c->next_ticket;
   const uint32_t slot = (uint32_t)((t - 1) % kSubmitRing);
   Slot& s = c->slots[slot];
-  if (s.ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
+  if (s.ticket) { c->err = "four batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
   int r;
   if ((r = stage_add(c, slot, v))) return r;
   if ((r = run_slot(c, slot, nullptr))) return r;
@@ -2547,7 +2553,7 @@ int txv_submit_routed(txv_ctx* c, const void* buf_dev, const txv_route_meta* met
   const uint64_t t = c->next_ticket;
   const uint32_t slot = (uint32_t)((t - 1) % kSubmitRing);
   Slot& s = c->slots[slot];
-  if (s.ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
+  if (s.ticket) { c->err = "four batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
   int r;
   if ((r = stage_routed(c, slot, static_cast<const uint8_t*>(buf_dev), meta))) return r;
   if ((r = run_slot(c, slot, nullptr))) return r;
@@ -4229,7 +4235,7 @@ int submit_checked_stage(txv_ctx* c, const txv_votes* v, uint32_t* slot_out) {
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   const uint32_t slot = (uint32_t)((c->next_ticket - 1) % kSubmitRing);
-  if (c->slots[slot].ticket) { c->err = "three batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
+  if (c->slots[slot].ticket) { c->err = "four batches already in flight: wait for the oldest one first"; return TXV_ESTATE; }
   txv_votes w = *v;
   w.sig = nullptr;                 // from the pool's flight slot (or uploaded late)
   w.is_nil = nullptr;              // written on the device (or uploaded late)

@@ -212,8 +212,8 @@ int txv_add_votes(txv_ctx* ctx, const txv_votes* votes, uint8_t* status_out,
  * txv_submit_votes copies the batch's columns into pinned memory (registered columns: none),
  * queues their upload on the copy stream and the kernel chain on the compute stream, and returns
  * a ticket without waiting; txv_wait_votes(ticket) waits for the results and reports exactly what
- * txv_add_votes would have.  At most three batches may be in flight (they share staged slots
- * 0-2 with txv_stage / txv_run_staged: do not mix the two on one context at the same time);
+ * txv_add_votes would have.  At most four batches may be in flight (they share staged slots
+ * 0-3 with txv_stage / txv_run_staged: do not mix the two on one context at the same time);
  * tickets are waited in submission order.  The staging of batch k+1 and its upload overlap the
  * kernels of batch k, and the staging of batch k+2 the upload of batch k+1.
  * Registered columns (txv_host_register) are read by DMA until txv_wait_votes returns for the
@@ -616,8 +616,11 @@ int txv_ingest_admit(txv_ctx* ctx, uint64_t ticket, uint8_t* wire_status, uint8_
 /* txv_ingest_admit in its two halves, for a fourth stage (the admit thread waited for
  * each batch's pool statuses): txv_ingest_admit_submit hands the batch's CheckTx to the device (the
  * pool keeps its cache in HBM and the caps cannot bind: the decisions are enqueued behind the
- * decode in the pool engine's next flight slot) and returns; txv_ingest_admit_finish (tickets in
- * order) collects the statuses, lists the admitted messages and enqueues their TxFlow chain.
+ * decode in the pool engine's next flight slot) together with the batch's TxFlow chain over every
+ * decoded message, the pool's rejections and the undecodable messages as nil entries built on the
+ * device from those decisions (messages of up to 1024 bytes; a batch with a longer one has its
+ * chain enqueued by the finish), and returns; txv_ingest_admit_finish (tickets in order) collects
+ * the statuses and lists the admitted messages.
  * wire_status / pool_status are final when the finish returns (when the submit had to run the
  * host path, the whole admission is done by the submit -- it requires every earlier submitted
  * admission finished, else TXV_ESTATE -- and the finish returns at once).  A registered wire
