@@ -819,7 +819,10 @@ class Context:
         self._chk(lib().txv_reset_tally(self._h), "txv_reset_tally")
 
     def bind_host_numa(self) -> bool:
-        """pin this thread and the library's pack threads to the GPU-local NUMA node (True on success)"""
+        """pin this thread and the library's pack threads to the GPU-local NUMA node (True on success;
+        TXV_NUMA_BIND=0 leaves the affinity alone, experiment)"""
+        if os.environ.get("TXV_NUMA_BIND") == "0":
+            return False
         return lib().txv_bind_host_numa(self._h) == 0
 
     def reset_flow(self):
