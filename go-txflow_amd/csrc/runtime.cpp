@@ -105,6 +105,12 @@ struct Slot {
   uint8_t *h_txkey = nullptr, *d_txkey = nullptr;          // [n][32]
   uint16_t *h_vcode = nullptr, *d_vcode = nullptr;         // [n] validator index / kVcode* (host lookup)
   bool has_nil = false, has_txkey = false, host_val = false;
+  // uniform columns (and a TxKey column spelled by the TxHashes) filled on the device at the next
+  // run_slot, on the key stream, instead of on the copy stream at staging (stage_add)
+  uint32_t fill_mask = 0;
+  int64_t fill_h = 0, fill_s = 0;
+  uint32_t fill_hl = 0, fill_al = 0, fill_sl = 0;
+  bool fill_key = false;
   bool msg_on_device = false;      // the signer's SignBytes are built by txv_k_signbytes
   uint64_t seq_base = 0;
   uint32_t stamp = 0;              // batch stamp of the staged batch
@@ -746,6 +752,24 @@ inline bool txkey_spelled(const uint8_t* key, const uint8_t* hex) {
   return ok == 0xFFFF;
 }
 
+// the staged batch's pending fills (Slot::fill_*) on stream st, behind its uploads
+int slot_fills(txv_ctx* c, Slot& s, hipStream_t st) {
+  const uint32_t n = s.n;
+  enum { kUH, kUS, kUHL, kUAL, kUSL };
+  if (n && s.fill_mask) {
+    if (s.fill_mask >> kUH & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fh), (uint64_t)s.fill_h, n, st));
+    if (s.fill_mask >> kUS & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fs), (uint64_t)s.fill_s, n, st));
+    if (s.fill_mask >> kUHL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_fl), (int)s.fill_hl, n, st));
+    if (s.fill_mask >> kUAL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_addr_len), (int)s.fill_al, n, st));
+    if (s.fill_mask >> kUSL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_sig_len), (int)s.fill_sl, n, st));
+  }
+  if (n && s.fill_key)
+    HIP_TRY(c, txv_txkey_from_hash(s.d_arena_th, s.d_fo, s.has_nil ? s.d_nil : nullptr, n, s.d_txkey, st));
+  s.fill_mask = 0;
+  s.fill_key = false;
+  return TXV_OK;
+}
+
 // route = true: the columns of a batch txv_route_admitted packs for the ranks (no TxFlow run: no
 // validator set needed, no sequence numbers taken, every address column uploaded)
 int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v, bool route = false) {
@@ -845,11 +869,12 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v, bool route = false)
   const bool derive_key = check_key && !key_differs.load();
   add(derive_key ? nullptr : v->txkey, s.h_txkey, s.d_txkey, 32);
   if (s.launched) HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, s.ev[4], 0));   // its last chain has ended
-  if (uniform >> kUH & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fh), (uint64_t)v->height[0], n, c->copy_stream));
-  if (uniform >> kUS & 1) HIP_TRY(c, txv_fill64(reinterpret_cast<uint64_t*>(s.d_fs), (uint64_t)v->ts_sec[0], n, c->copy_stream));
-  if (uniform >> kUHL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_fl), (int)v->txhash_len[0], n, c->copy_stream));
-  if (!host_val && (uniform >> kUAL & 1)) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_addr_len), (int)v->addr_len[0], n, c->copy_stream));
-  if (uniform >> kUSL & 1) HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_sig_len), (int)v->sig_len[0], n, c->copy_stream));
+  // the fills: a TxFlow batch's at its run_slot on the key stream (the copy stream keeps to DMA), a
+  // route batch's here (its columns are read by the route kernels, not a chain)
+  s.fill_mask = uniform & ~(host_val ? (1u << kUAL) : 0u);
+  s.fill_h = n ? v->height[0] : 0; s.fill_s = n ? v->ts_sec[0] : 0;
+  s.fill_hl = n ? v->txhash_len[0] : 0; s.fill_al = n ? v->addr_len[0] : 0; s.fill_sl = n ? v->sig_len[0] : 0;
+  if (route && (r = slot_fills(c, s, c->copy_stream))) return r;
   for (int k = 0; k < nc; ++k)
     if (cols[k].reg && n) HIP_TRY(c, hipMemcpyAsync(cols[k].dev, cols[k].src, (size_t)n * cols[k].elem, hipMemcpyHostToDevice, c->copy_stream));
   // TxHash arena (+ 16 zero bytes: the device reads keys 8 bytes at a time)
@@ -898,8 +923,8 @@ int stage_add(txv_ctx* c, uint32_t slot, const txv_votes* v, bool route = false)
     memset(s.h_arena + ae, 0, 16);
     HIP_TRY(c, hipMemcpyAsync(s.d_arena_th + ae, s.h_arena + ae, 16, hipMemcpyHostToDevice, c->copy_stream));
   }
-  if (derive_key)
-    HIP_TRY(c, txv_txkey_from_hash(s.d_arena_th, s.d_fo, s.has_nil ? s.d_nil : nullptr, n, s.d_txkey, c->copy_stream));
+  s.fill_key = derive_key;
+  if (route && (r = slot_fills(c, s, c->copy_stream))) return r;
   {
     uint64_t up = ae + 16 + (host_val ? (uint64_t)n * 2 : 0);
     for (int k = 0; k < nc; ++k) up += (uint64_t)n * cols[k].elem;
@@ -986,6 +1011,10 @@ int run_slot(txv_ctx* c, uint32_t slot, float* ms) {
   hipStream_t ps = c->key_stream;
   HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[3], 0));
   if (s.launched) HIP_TRY(c, hipStreamWaitEvent(ps, s.ev[4], 0));
+  if (s.fill_mask || s.fill_key) {   // the staging's fills (first run of a staging only)
+    if ((r = slot_fills(c, s, ps))) return r;
+    HIP_TRY(c, hipEventRecord(s.ev[3], ps));
+  }
   HIP_TRY(c, hipStreamWaitEvent(c->stream, s.ev[3], 0));
   // TXV_PREP_AFTER_K1B=1 (experiment): this batch's prep + SignBytes wait for the K1b two batches
   // back, so they run beside the next K1a instead of beside a K1b
@@ -2429,7 +2458,7 @@ int stage_routed(txv_ctx* c, uint32_t slot, const uint8_t* buf, const txv_route_
   HIP_TRY(c, hipMemcpyAsync(s.d_arena_th, buf + off[txv_route::kArena], ae + 16, hipMemcpyDeviceToDevice, c->copy_stream));
   c->staged_bytes = 0;
   HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));   // run_slot's kernels wait for this
-  s.staged = true; s.ran = false;
+  s.staged = true; s.ran = false; s.fill_mask = 0; s.fill_key = false;
   return TXV_OK;
 }
 
@@ -3217,7 +3246,7 @@ void ingest_flow_stage(txv_ctx* c, uint64_t t, uint32_t n_adm) {
     s.has_txkey = true;
     s.seq_base = c->seq_next;
     c->seq_next += n_adm;
-    s.staged = true; s.ran = false;
+    s.staged = true; s.ran = false; s.fill_mask = 0; s.fill_key = false;
     return run_slot(c, kIngestSlot + j, nullptr);
   };
   if (const int rf = flow_stage()) {
@@ -3255,7 +3284,7 @@ void ingest_flow_stage_early(txv_ctx* c, uint64_t t) {
     s.has_txkey = true;
     s.seq_base = c->seq_next;
     c->seq_next += n;
-    s.staged = true; s.ran = false;
+    s.staged = true; s.ran = false; s.fill_mask = 0; s.fill_key = false;
     return run_slot(c, kIngestSlot + j, nullptr);
   };
   if (const int rf = flow_stage()) {
