@@ -305,7 +305,7 @@ int pooldev_list_put(txv_ctx* c, PoolDev* s, const uint8_t* keys, const uint32_t
 int pooldev_list_get(txv_ctx* c, PoolDev* s, std::vector<uint8_t>& keys, std::vector<uint32_t>& sizes,
                      std::vector<uint8_t>& ins);
 void pooldev_result(const PoolDev* s, int slot, int64_t res[4]);
-constexpr int kPdRing = 4;   // = PoolDev::kPdRing (runtime.cpp)
+constexpr int kPdRing = 8;   // = PoolDev::kPdRing (runtime.cpp)
 void pooldev_set_occupant(PoolDev* s, int slot, uint64_t id, uint32_t n_upd, uint32_t n);
 bool pooldev_holds(const PoolDev* s, uint64_t id);
 std::mutex& txv_ctx_submit_mu(txv_ctx* c);

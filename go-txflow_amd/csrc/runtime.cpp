@@ -316,9 +316,25 @@ struct txv_ctx {
   uint64_t ing_admit_next = 1;     // next ticket to admit (submit half); guarded by mu
 };
 
+// TXV_PROFILE_SLOW=1 (debugging aid): every HIP call made through HIP_TRY that takes longer than
+// 1 ms on the host is reported on stderr with its start on the monotonic clock
+inline bool txv_profile_slow() {
+  static const bool on = getenv("TXV_PROFILE_SLOW") && atoi(getenv("TXV_PROFILE_SLOW")) == 1;
+  return on;
+}
+inline void txv_slow_report(const char* what, std::chrono::steady_clock::time_point t0) {
+  const auto t1 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (ms > 1.0)
+    fprintf(stderr, "[txv slow] @%.4f %.3fms %s\n", std::chrono::duration<double>(t0.time_since_epoch()).count(), ms, what);
+}
+
 #define HIP_TRY(ctx, x)                                                                    \
   do {                                                                                     \
+    const bool sl_ = txv_profile_slow();                                                   \
+    const auto t0_ = sl_ ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{}; \
     hipError_t e_ = (x);                                                                   \
+    if (sl_) txv_slow_report(#x, t0_);                                                     \
     if (e_ != hipSuccess) {                                                                \
       (ctx)->err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
       return TXV_EDEVICE;                                                                  \
@@ -722,6 +738,9 @@ uint32_t signbytes_bound(uint32_t max_hl, uint32_t chain_len) {
 }
 
 bool is_registered(const txv_ctx* c, const void* p, uint64_t bytes) {
+  // TXV_IGNORE_REGISTERED=1 (experiment): every upload through the library's own pinned staging
+  static const bool ignore = getenv("TXV_IGNORE_REGISTERED") && atoi(getenv("TXV_IGNORE_REGISTERED")) == 1;
+  if (ignore) return false;
   const uintptr_t a = (uintptr_t)p;
   for (const auto& r : c->registered)
     if (a >= r.first && a + bytes <= r.first + r.second) return true;
@@ -3674,7 +3693,7 @@ struct PoolDev {
   uint64_t tail_ub = 0;                    // host: an upper bound of the tail (the appends enqueued)
   uint64_t list_hint = 0;                  // entries the list is expected to hold (the pool's Size cap, clamped)
   // per batch in flight (kPdRing): its inputs, statuses and keys, and the event that ends it
-  static constexpr int kPdRing = 4;
+  static constexpr int kPdRing = 8;
   struct Flight {
     uint32_t *d_sig = nullptr, *d_len = nullptr, *d_keys = nullptr, *d_sizes = nullptr;
     uint8_t* d_status = nullptr;

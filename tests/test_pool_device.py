@@ -118,8 +118,8 @@ def test_device_cache_soa_batches_with_update(dev_ctx):
 
 @pytest.mark.gpu
 def test_device_cache_submitted_batches_in_flight(dev_ctx):
-    """txv_pool_check_submit / _wait with up to four batches submitted before the first wait (the
-    engine has four flight slots), waits out of order, an
+    """txv_pool_check_submit / _wait with four batches submitted before the first wait (the
+    engine has eight flight slots), waits out of order, an
     Update between submits (it finishes every batch in flight first), then check_batch: every
     batch's statuses, the pool and LRU order equal the oracle's"""
     import random
@@ -513,15 +513,15 @@ def test_submit_checked_equals_host_statuses(mode):
     uploaded reused) against the two-call path -- txv_pool_check's statuses as the host's is_nil
     column of txv_submit_votes -- on a C5-like stream with 5 % exact replays and a small cache:
     every TxFlow status (fired bits included), commit event and pool status equal.  "device":
-    submitted right after each CheckTx; "ahead": six CheckTx batches submitted first (the engine's
-    four flight slots reused: the first batches take the host statuses); "waited": each pool ticket
+    submitted right after each CheckTx; "ahead": ten CheckTx batches submitted first (the engine's
+    eight flight slots reused: the first batches take the host statuses); "waited": each pool ticket
     waited before its TxFlow submit.  Reference: txvotepool/reactor.go:170-190 ->
     txflow/service.go:123-166."""
     import txflow_amd as T
     from txflow_amd.workload import StreamWorkload, SEEDS
-    ctx = T.Context(max_batch=4096, max_txs=1024, max_validators=32)
+    ctx = T.Context(max_batch=4096, max_txs=1536, max_validators=32)
     try:
-        wl = StreamWorkload(ctx, 24, 800, SEEDS["c5"] + 7, 2048, replay=0.05)
+        wl = StreamWorkload(ctx, 24, 1280, SEEDS["c5"] + 7, 2048, replay=0.05)
         cfg = dict(size=1 << 20, cache_size=600, max_txs_bytes=1 << 40)
 
         def reference():
@@ -540,7 +540,7 @@ def test_submit_checked_equals_host_statuses(mode):
         def checked():
             pool = T.TxVotePool(ctx, **cfg, device_cache=True)
             out = [None] * len(wl.batches)
-            ahead = 6 if mode == "ahead" else 1
+            ahead = 10 if mode == "ahead" else 1
             tks, flows = {}, []
 
             def flow_submit(j):
@@ -569,7 +569,7 @@ def test_submit_checked_equals_host_statuses(mode):
 
         ref = reference()
         got = checked()
-        assert len(ref) == len(got) >= 8
+        assert len(ref) == len(got) >= 14
         for k, ((rps, rst, rev), (gps, gst, gev)) in enumerate(zip(ref, got)):
             assert np.array_equal(rps, gps), f"batch {k}: pool statuses differ"
             assert np.array_equal(rst, gst), f"batch {k}: {int(np.count_nonzero(rst != gst))} TxFlow statuses differ"
