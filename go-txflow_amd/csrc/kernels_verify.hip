@@ -1299,9 +1299,12 @@ static void launch_build(const uint32_t* pubs_le, uint32_t n_points, uint32_t* t
                      tables, decode_ok, addr_words, out_slot);
 }
 
-// K1c's votes per lane: the largest G whose launch still gives every SIMD of the chip about
-// one wave (1024 SIMDs on MI355X), so the inversion's share per vote falls as the batch grows
-// without leaving SIMDs idle; TXV_K1C_G overrides it (experiments)
+// K1c's votes per lane: the largest G whose launch still gives every SIMD of the chip about a
+// quarter wave (1024 SIMDs on MI355X), so the inversion's share per vote falls as the batch grows.
+// K1c runs beside the other batches' kernels in a pipeline, so it need not fill the SIMDs itself:
+// at C5's 64k-vote batches G = 4 (256 waves) took K1b + K1c from 0.159-0.163 to 0.154 ms in the
+// pipeline and the latency to commit from 3.0-3.3 to 2.5-2.9 ms against G = 1 (one wave per SIMD)
+// (round 6, same boxes).  TXV_K1C_G overrides it (experiments)
 static int k1c_votes_per_lane(uint32_t n_work) {
   static const int forced = [] {
     const char* e = getenv("TXV_K1C_G");
@@ -1310,7 +1313,7 @@ static int k1c_votes_per_lane(uint32_t n_work) {
   }();
   if (forced) return forced;
   for (int g : {32, 16, 8, 4, 2})
-    if ((uint64_t)n_work >= (uint64_t)g * 64 * 1024) return g;
+    if ((uint64_t)n_work >= (uint64_t)g * 64 * 256) return g;
   return 1;
 }
 
