@@ -248,6 +248,8 @@ struct txv_ctx {
   uint32_t poisoned = 0;            // TXV_FERR_* seen: every AddVote call fails until txv_reset_flow
   // caller memory registered with txv_host_register (DMA'd without a staging copy)
   std::vector<std::pair<uintptr_t, uint64_t>> registered;
+  std::mutex reg_mu;               // `registered` is changed under mu and reg_mu: read under either (the
+                                   // pool's uploads check it under reg_mu, off the context's lock)
   // reader scratch (lookups / gathers)
   uint8_t* d_q = nullptr; uint64_t q_cap = 0;
   // signer slots (load generator)
@@ -2259,6 +2261,7 @@ int txv_host_register(txv_ctx* c, void* ptr, uint64_t bytes) {
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  std::lock_guard<std::mutex> rg(c->reg_mu);
   c->registered.emplace_back((uintptr_t)ptr, bytes);
   return TXV_OK;
 }
@@ -2272,6 +2275,7 @@ int txv_host_unregister(txv_ctx* c, void* ptr) {
       // no DMA of an in-flight batch may still read it
       HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
       HIP_TRY(c, hipHostUnregister(ptr));
+      std::lock_guard<std::mutex> rg(c->reg_mu);
       c->registered.erase(c->registered.begin() + (long)k);
       return TXV_OK;
     }
@@ -2733,7 +2737,7 @@ int txv_sig_keys_overlap(txv_ctx* c, const txv_votes* v, const uint8_t* sig_full
   // from there (no staging copy)
   bool reg;
   {
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::mutex> lk(c->reg_mu);
     reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
   }
   for (uint32_t k = 0; k < K; ++k) {
@@ -4066,7 +4070,7 @@ int upload_votes(txv_ctx* c, PoolDev::Flight& f, hipStream_t ks, const txv_votes
   hipStream_t us = up_mode ? c->copy_stream : ks;
   bool reg;
   {
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::mutex> lk(c->reg_mu);
     reg = is_registered(c, v->sig, (uint64_t)n * 64) && is_registered(c, v->sig_len, (uint64_t)n * 4);
   }
   if (!reg)
