@@ -315,7 +315,7 @@ def c5_pool_replay(wl, order, upd, got, cache_size, pool_size: int = C5_POOL_SIZ
 def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, label: str = "", collect_dev: bool = False,
             pool_size: int = C5_POOL_SIZE):
     """One pipelined pass of the C5 stream (c5_streaming's timed pass, c5_long's one long pass):
-    CheckTx -> TryAddVote -> Update on the node's threads, two batches in flight.  Returns the
+    CheckTx -> TryAddVote -> Update on the node's threads, C5_INFLIGHT TxFlow batches in flight.  Returns the
     pass's report, the per-batch device stage times (collect_dev) and per-batch wall times
     (submission and completion of every batch, for deciles / percentiles over a long pass)."""
     import queue
@@ -325,11 +325,12 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
     submit, done, commit_t = [], [], {}
     added = [0]
 
-    # Three threads, as a node's goroutines: Reactor.Receive -> CheckTx (ingest), the
-    # checkMaj23Routine submitting each checked batch (main), and a drain thread waiting each
-    # ticket in order as soon as it is submitted (commit events reported when the device is
-    # done, not when a third batch arrives).  At most two batches in flight (txv_submit_votes);
-    # ctypes releases the GIL inside every call.
+    # Threads as a node's goroutines: Reactor.Receive -> CheckTx (prepare; with the device cache
+    # txv_pool_check_submit), the checkMaj23Routine submitting each checked batch (main;
+    # txv_submit_checked with the device cache), the statuses' collection (txv_pool_check_wait,
+    # off the TryAddVote path), and a drain thread waiting each ticket in order as soon as it is
+    # submitted (commit events reported when the device is done) and issuing the Update.  At most
+    # C5_INFLIGHT TxFlow batches in flight; ctypes releases the GIL inside every call.
     import queue
     import threading
     checked = queue.Queue(maxsize=2)
@@ -499,8 +500,8 @@ def c5_pass(ctx, wl, pool, upd, device_cache: bool, batch: int, n_vals: int, lab
     out = {"workload": f"C5: {n_vals} validators (power 1 + rand mod 1e6), {wl.n_unique} votes + "
                        f"{wl.n - wl.n_unique} exact replays ({C5_REPLAY:.0%}, Appendix C) in {batch}-vote batches "
                        f"through TxVotePool.CheckTx (CacheSize {C5_CACHE}) in {stages} -- + "
-                       f"txv_submit_votes/txv_wait_votes (TxFlow.TryAddVote for the admitted votes, two batches in "
-                       f"flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
+                       f"{'txv_submit_checked (TxFlow.TryAddVote enqueued behind the device CheckTx, the pool rejections as nil entries read in HBM)' if checked_mode else 'txv_submit_votes (TxFlow.TryAddVote for the admitted votes)'} / "
+                       f"txv_wait_votes ({C5_INFLIGHT} batches in flight, each waited by a drain thread as soon as submitted) + TxVotePool.Update "
                        f"(txv_pool_update_submit, on the drain thread) after each batch's commit events, with the whole "
                        f"vote list of every set that fired in the batch, by last fired vote ({n_upd} votes per pass; "
                        f"the reference's Update(GetVotes()) per fired vote, txflow/service.go:216-227, leaves the same "
@@ -533,7 +534,7 @@ def c5_streaming(device: int, n_vals: int, n_txs: int, batch: int):
     replays) cut into `batch`-vote batches fed through the pool ingest (txv_pool_check:
     SHA-256(Signature) keys on the GPU, LRU of tendermint's default 10000 entries + pool list on the
     host) and txv_submit_votes / txv_wait_votes (columns staged + uploaded on the copy stream, the
-    whole AddVote chain on the GPU, statuses and commit events back), two batches in flight.  The
+    whole AddVote chain on the GPU, statuses and commit events back), C5_INFLIGHT batches in flight.  The
     votes CheckTx rejects (ErrTxInCache) never reach TxFlow: they travel as nil entries of the
     batch, which AddVote drops before any state (is_nil column).  Latency-to-commit of a tx =
     return of the call that reported its commit event - submission of the batch holding its first
@@ -1011,8 +1012,8 @@ def c5_wire_leg(device: int, n_vals: int, n_txs: int, batch: int):
                        "correct": one_ok and len(one_commit) == wl.n_txs}
     out.update(workload=f"C5 as wire bytes: {n_vals} validators, {wl.n} TxVoteMessages ({wire_bytes / wl.n:.1f} B avg; "
                         f"{wl.n - wl.n_unique} exact replays, CacheSize {C5_CACHE}) in {batch}-message batches through "
-                        f"txv_ingest_decode / txv_ingest_admit / txv_ingest_wait on three threads (decode -> pool -> "
-                        f"TxFlow, device-resident, up to three batches in flight; receive buffers registered with "
+                        f"txv_ingest_decode / txv_ingest_admit_submit / _admit_finish / txv_ingest_wait on four threads (decode -> "
+                        f"pool + TxFlow enqueued together -> statuses -> commit events, device-resident, up to three batches in flight; receive buffers registered with "
                         f"txv_host_register, so the wire bytes are DMA'd without a staging copy; the pool's LRU cache "
                         f"in HBM, TXV_POOL_DEVICE_CACHE: CheckTx decided on the GPU from the decoded keys; "
                         f"p50_decode_ms = the upload + decode enqueue, p50_admit_ms = keys wait + CheckTx + TxFlow "
