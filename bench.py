@@ -761,8 +761,8 @@ def c5_long(device: int, n_vals: int, n_txs: int, batch: int):
 def owner_route_leg(device: int, n_vals: int, n_txs: int, batch: int, n_ranks: int = 8):
     """The multi-GPU ingest's owner rank on one GPU: every C5 batch
     through TxVotePool.CheckTx with the cache in HBM (txv_pool_check_submit / _wait) and its
-    admitted votes packed for `n_ranks` ranks on the device (txv_route_admitted), on two threads
-    (batch k+1's CheckTx enqueued while batch k is routed).  Its rate bounds what a node of
+    admitted votes packed for `n_ranks` ranks on the device from the pool's statuses in HBM
+    (txv_route_checked), on two threads (batch k+1's CheckTx enqueued while batch k is routed).  Its rate bounds what a node of
     n_ranks GPUs can admit when one owner runs CheckTx for all of them; the ranks' scatter and
     TxFlow chains are not in it.  Checked: every admitted vote routed exactly once (the metas sum
     to the admitted count), one batch's device buffers byte-identical to txv_route_pack_host."""
@@ -812,10 +812,12 @@ def owner_route_leg(device: int, n_vals: int, n_txs: int, batch: int, n_ranks: i
             if item is None:
                 break
             b, tk = item
-            ps = pool.check_wait(tk)
             tr = time.perf_counter()
-            m = ctx.route_admitted(b, ps, n_ranks, buf.data_ptr(), stride)
+            # the route kernels read the batch's statuses (and the signatures the CheckTx uploaded)
+            # in HBM behind the pool's decisions: txv_route_checked; the statuses come back after
+            m = ctx.route_checked(b, pool, tk, n_ranks, buf.data_ptr(), stride)
             route_ms.append((time.perf_counter() - tr) * 1e3)
+            ps = pool.check_wait(tk)
             routed[0] += int(m["n"].sum())
             admitted[0] += int((ps == T.POOL_OK).sum())
         th.join()
@@ -828,7 +830,7 @@ def owner_route_leg(device: int, n_vals: int, n_txs: int, batch: int, n_ranks: i
     runs.sort(key=lambda r: r["votes_per_s"])
     out = dict(runs[1])
     out.update({"workload": f"owner rank: the C5 stream ({wl.n} votes, {batch}-vote batches, {n_vals} validators) "
-                            f"through TxVotePool.CheckTx (cache in HBM) + txv_route_admitted to {n_ranks} ranks",
+                            f"through TxVotePool.CheckTx (cache in HBM) + txv_route_checked to {n_ranks} ranks",
                 "n_ranks": n_ranks, "votes_per_s_passes": [r["votes_per_s"] for r in runs],
                 "device_route_equals_host": same,
                 "correct": same and all(r["routed"] == r["admitted"] for r in runs)})
@@ -1161,11 +1163,17 @@ def main():
                     help="profiling aid: run only the C5 legs (SoA and wire) and print them as one JSON line")
     ap.add_argument("--c5-long-only", action="store_true", help="profiling aid: only the one-long-TxFlow C5 leg")
     ap.add_argument("--c5-wire-only", action="store_true", help="profiling aid: only the C5 wire-bytes leg")
+    ap.add_argument("--route-only", action="store_true", help="profiling aid: only the owner-rank route leg")
     args = ap.parse_args()
     if os.environ.get("TXV_BENCH_WATCHDOG"):   # debugging aid: every thread's stack on stderr periodically
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["TXV_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
+    if args.route_only:
+        import torch
+        torch.cuda.init()
+        print(json.dumps({"owner_route": owner_route_leg(0, 1000, args.c5_txs, 65536)}), flush=True)
+        return
     if args.c5_wire_only:
         print(json.dumps({"c5_wire": c5_wire_leg(0, 1000, args.c5_txs, 65536)}), flush=True)
         return

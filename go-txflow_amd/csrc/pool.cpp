@@ -309,6 +309,12 @@ constexpr int kPdRing = 8;   // = PoolDev::kPdRing (runtime.cpp)
 void pooldev_set_occupant(PoolDev* s, int slot, uint64_t id, uint32_t n_upd, uint32_t n);
 bool pooldev_holds(const PoolDev* s, uint64_t id);
 std::mutex& txv_ctx_submit_mu(txv_ctx* c);
+std::mutex& txv_ctx_route_mu(txv_ctx* c);
+int txv_ctx_fail(txv_ctx* c, int code, const char* msg);
+int route_checked_stage(txv_ctx* c, const txv_votes* v, uint64_t stride);
+int route_checked_consume(txv_ctx* c, PoolDev* dev, uint64_t pool_ticket, uint32_t n);
+int route_checked_launch(txv_ctx* c, const txv_votes* v, const uint8_t* host_st, uint32_t G, void* dst, uint64_t stride,
+                         txv_route_meta* meta);
 int submit_checked_stage(txv_ctx* c, const txv_votes* v, uint32_t* slot_out);
 int submit_checked_consume(txv_ctx* c, uint32_t slot, PoolDev* dev, uint64_t pool_ticket, const txv_votes* v);
 int submit_checked_run(txv_ctx* c, uint32_t slot, const txv_votes* v, const uint8_t* host_st, int why, uint64_t* ticket);
@@ -1627,6 +1633,50 @@ int txv_submit_checked(txv_ctx* ctx, const txv_votes* v, txv_pool* p, uint64_t p
     }
   }
   return submit_checked_run(ctx, slot, v, why ? nullptr : st.data(), why, ticket);
+}
+
+// txv_route_admitted for the batch a CheckTx ticket is deciding (include/txvote.h): the route
+// kernels read its statuses and signatures in HBM behind the decisions while the batch is in the
+// engine's flight slot, else the ticket's host statuses and the caller's signatures.  Takes the
+// context's route lock, then the pool's, then the context's.
+int txv_route_checked(txv_ctx* ctx, const txv_votes* v, txv_pool* p, uint64_t pool_ticket, uint32_t n_shards,
+                      void* dst_dev, uint64_t stride, txv_route_meta* meta_out) {
+  if (!ctx || !v || !p || !pool_ticket || !dst_dev || !meta_out || !n_shards || n_shards > 255) return TXV_EINVAL;
+  if (v->n && (!v->height || !v->txhash || !v->txhash_off || !v->txhash_len || !v->ts_sec || !v->ts_nanos || !v->addr ||
+               !v->addr_len || !v->sig || !v->sig_len))
+    return TXV_EINVAL;
+  std::lock_guard<std::mutex> rl(txv_ctx_route_mu(ctx));
+  int r;
+  if ((r = route_checked_stage(ctx, v, stride))) return r;
+  std::vector<uint8_t> st;
+  bool consumed = false;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (p->dev && pooldev_same_device(ctx, p->dev) && pooldev_holds(p->dev, pool_ticket)) {
+      if ((r = route_checked_consume(ctx, p->dev, pool_ticket, v->n)) < 0) return r;
+      consumed = r == 0;
+    }
+    if (!consumed) {
+      auto it = std::find_if(p->tickets.begin(), p->tickets.end(), [&](const txv_pool::Ticket& t) { return t.id == pool_ticket; });
+      if (it == p->tickets.end()) {
+        for (const auto& rc : p->recent)
+          if (rc.first == pool_ticket) st = rc.second;
+        if (st.empty() && v->n) return txv_ctx_fail(ctx, TXV_ESTATE, "txv_route_checked: unknown pool ticket (already waited?)");
+      } else if (it->upd) {
+        return txv_ctx_fail(ctx, TXV_ESTATE, "txv_route_checked: unknown pool ticket");
+      } else {
+        if (!it->done)
+          for (auto jt = p->tickets.begin(); jt != p->tickets.end(); ++jt) {
+            if (int e = finish_ticket(p, *jt)) return e;
+            if (jt == it) break;
+          }
+        if (it->err) return it->err;
+        st = it->st;
+      }
+      if (st.size() != v->n) return txv_ctx_fail(ctx, TXV_EINVAL, "txv_route_checked: the batch differs from the pool ticket's");
+    }
+  }
+  return route_checked_launch(ctx, v, consumed ? nullptr : st.data(), n_shards, dst_dev, stride, meta_out);
 }
 
 // the statuses of a submitted batch (tickets in submission order); the engine's event is waited

@@ -2382,8 +2382,30 @@ uint32_t route_flags(const txv_votes* v) {
   return (v->txkey ? TXV_ROUTE_TXKEY : 0u) | (v->is_nil ? TXV_ROUTE_NIL : 0u);
 }
 
-int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G, void* dst, uint64_t stride,
-                   txv_route_meta* meta) {
+// txv_route_admitted's steps (route_mu held by the caller).  Stage: the batch's columns into the
+// route slot (without its signatures when sig_later: txv_route_checked takes them from the pool's
+// flight slot), c->mu held inside.
+int route_stage(txv_ctx* c, const txv_votes* v, bool sig_later, uint64_t stride) {
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  txv_votes w = *v;
+  if (sig_later) w.sig = nullptr;
+  int r;
+  if ((r = stage_add(c, kRouteSlot, &w, true))) return r;
+  Slot& s = c->slots[kRouteSlot];
+  const uint64_t need = txv_route_bytes(v->n, s.arena_end, route_flags(v));
+  if (stride < need) {
+    c->err = "route stride below txv_route_bytes(n, TxHash arena extent, flags) = " + std::to_string(need);
+    return TXV_EINVAL;
+  }
+  return TXV_OK;
+}
+
+// Launch: the pool's statuses either given on the host (st: uploaded beside the columns, with the
+// signatures too when they were left out) or already in the slot's pre-check column (st null,
+// dev_status: txv_route_checked), then the three route kernels; waits for the metas.
+int route_launch(txv_ctx* c, const txv_votes* v, const uint8_t* st, bool dev_status, bool sig_later, uint32_t G,
+                 void* dst, uint64_t stride, txv_route_meta* meta) {
   const uint32_t n = v->n;
   const uint32_t flags = route_flags(v);
   int r;
@@ -2391,16 +2413,18 @@ int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G
   {
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device));
-    if ((r = stage_add(c, kRouteSlot, v, true))) return r;
     Slot& s = c->slots[kRouteSlot];
-    const uint64_t need = txv_route_bytes(n, s.arena_end, flags);
-    if (stride < need) {
-      c->err = "route stride below txv_route_bytes(n, TxHash arena extent, flags) = " + std::to_string(need);
-      return TXV_EINVAL;
-    }
     if (st && n) {   // the pool's statuses beside the columns (the slot's pre-check column is free here)
       memcpy(s.h_status, st, n);
       HIP_TRY(c, hipMemcpyAsync(s.d_pre, s.h_status, n, hipMemcpyHostToDevice, c->copy_stream));
+      if (sig_later) {          // the signatures the pool's slot no longer holds, from the caller
+        const bool reg = is_registered(c, v->sig, (uint64_t)n * 64);
+        if (!reg) c->pool->parallel_for(n, [&](uint32_t lo, uint32_t hi) {
+          memcpy(s.h_sigraw + (size_t)lo * 64, v->sig + (size_t)lo * 64, (size_t)(hi - lo) * 64);
+        }, 4096);
+        HIP_TRY(c, hipMemcpyAsync(s.d_sigraw, reg ? (const void*)v->sig : (const void*)s.h_sigraw, (size_t)n * 64,
+                                  hipMemcpyHostToDevice, c->copy_stream));
+      }
       HIP_TRY(c, hipEventRecord(s.ev[3], c->copy_stream));
     }
     const uint32_t nw = (n + 63) / 64;
@@ -2424,7 +2448,7 @@ int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G
     a.addr = s.d_addr; a.addr_len = s.d_addr_len; a.sig = s.d_sigraw; a.sig_len = s.d_sig_len;
     a.txkey = s.has_txkey ? s.d_txkey : nullptr;
     a.nil = s.has_nil ? s.d_nil : nullptr;
-    a.status = st ? s.d_pre : nullptr;
+    a.status = (st || dev_status) ? s.d_pre : nullptr;
     a.flags = flags;
     a.shard = c->d_rshard; a.wcnt = c->d_rw; a.wbytes = c->d_rw + (size_t)std::max<uint32_t>(nw, 1) * G;
     a.maxhl = c->d_rmax; a.tot = c->d_rtot;
@@ -2441,6 +2465,13 @@ int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G
   HIP_TRY(c, hipEventSynchronize(done));
   memcpy(meta, c->h_rmeta, (size_t)G * sizeof(txv_route_meta));
   return TXV_OK;
+}
+
+int route_admitted(txv_ctx* c, const txv_votes* v, const uint8_t* st, uint32_t G, void* dst, uint64_t stride,
+                   txv_route_meta* meta) {
+  int r;
+  if ((r = route_stage(c, v, false, stride))) return r;
+  return route_launch(c, v, st, false, false, G, dst, stride, meta);
 }
 
 // the receiving rank: a route buffer (on this context's device) into AddVote slot `slot`, by
@@ -4253,7 +4284,7 @@ void pooldev_set_occupant(PoolDev* s, int slot, uint64_t id, uint32_t n_upd, uin
 // when or_nil) on stream st, behind the batch's decisions; the slot's next writer waits for these
 // reads.  1: the ticket's batch is no longer in any slot (the caller takes its host statuses).
 int pooldev_consume(txv_ctx* c, PoolDev* s, uint64_t id, uint32_t n, hipStream_t st, uint8_t* sig_out, uint8_t* nil_out,
-                    bool or_nil) {
+                    bool or_nil, bool raw_status) {
   if (!s || !id) return 1;
   for (PoolDev::Flight& f : s->fl) {
     if (f.occ != id) continue;
@@ -4261,7 +4292,10 @@ int pooldev_consume(txv_ctx* c, PoolDev* s, uint64_t id, uint32_t n, hipStream_t
     if (!f.cons_ev) HIP_TRY(c, hipEventCreateWithFlags(&f.cons_ev, hipEventDisableTiming));
     HIP_TRY(c, hipStreamWaitEvent(st, f.ev, 0));
     HIP_TRY(c, hipMemcpyAsync(sig_out, f.d_sig + (size_t)f.occ_upd * 16, (size_t)n * 64, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(c, txv_launch_nil_from_status(f.d_status + f.occ_upd, n, nil_out, or_nil ? 1u : 0u, st));
+    if (raw_status)   // the statuses themselves (txv_route_checked: the route kernels read TXV_POOL_*)
+      HIP_TRY(c, hipMemcpyAsync(nil_out, f.d_status + f.occ_upd, n, hipMemcpyDeviceToDevice, st));
+    else
+      HIP_TRY(c, txv_launch_nil_from_status(f.d_status + f.occ_upd, n, nil_out, or_nil ? 1u : 0u, st));
     HIP_TRY(c, hipEventRecord(f.cons_ev, st));
     f.cons = true;
     return 0;
@@ -4310,7 +4344,7 @@ int submit_checked_consume(txv_ctx* c, uint32_t slot, PoolDev* dev, uint64_t poo
     memcpy(s.h_nil, v->is_nil, v->n);
     HIP_TRY(c, hipMemcpyAsync(s.d_nil, s.h_nil, v->n, hipMemcpyHostToDevice, ks));
   }
-  const int r = pooldev_consume(c, dev, pool_ticket, v->n, ks, s.d_sigraw, s.d_nil, v->is_nil != nullptr);
+  const int r = pooldev_consume(c, dev, pool_ticket, v->n, ks, s.d_sigraw, s.d_nil, v->is_nil != nullptr, false);
   if (r) return r;
   HIP_TRY(c, hipEventRecord(s.ev[3], ks));   // run_slot's streams wait for the columns here
   return TXV_OK;
@@ -4344,6 +4378,33 @@ int submit_checked_run(txv_ctx* c, uint32_t slot, const txv_votes* v, const uint
   c->next_ticket = t + 1;
   *ticket = t;
   return TXV_OK;
+}
+
+// txv_route_checked's device source (the pool's lock held): the CheckTx batch's signatures and
+// statuses into the route slot, on the key stream behind the decisions; 1 = no longer in the engine
+int route_checked_consume(txv_ctx* c, PoolDev* dev, uint64_t pool_ticket, uint32_t n) {
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!n) return TXV_OK;
+  Slot& s = c->slots[kRouteSlot];
+  hipStream_t ks = c->key_stream;
+  HIP_TRY(c, hipStreamWaitEvent(ks, s.ev[3], 0));
+  const int r = pooldev_consume(c, dev, pool_ticket, n, ks, s.d_sigraw, s.d_pre, false, true);
+  if (r) return r;
+  HIP_TRY(c, hipEventRecord(s.ev[3], ks));
+  return TXV_OK;
+}
+
+std::mutex& txv_ctx_route_mu(txv_ctx* c) { return c->route_mu; }
+int route_checked_stage(txv_ctx* c, const txv_votes* v, uint64_t stride) { return route_stage(c, v, true, stride); }
+int route_checked_launch(txv_ctx* c, const txv_votes* v, const uint8_t* host_st, uint32_t G, void* dst, uint64_t stride,
+                         txv_route_meta* meta) {
+  return route_launch(c, v, host_st, host_st == nullptr, true, G, dst, stride, meta);
+}
+int txv_ctx_fail(txv_ctx* c, int code, const char* msg) {
+  std::lock_guard<std::mutex> g(c->mu);
+  c->err = msg;
+  return code;
 }
 
 // enqueue + finish in one call (synchronous): statuses into status_out, keys (v path) into keys_out

@@ -191,6 +191,8 @@ def lib():
             "txv_commit_state_unpack": ([vp, u32, ctypes.POINTER(u32), vp, vp, vp, u32], ctypes.c_int),
             "txv_route_bytes": ([u32, ctypes.c_uint64, u32], ctypes.c_uint64),
             "txv_route_admitted": ([vp, ctypes.POINTER(_Votes), vp, u32, vp, ctypes.c_uint64, vp], ctypes.c_int),
+            "txv_route_checked": ([vp, ctypes.POINTER(_Votes), vp, ctypes.c_uint64, u32, vp, ctypes.c_uint64, vp],
+                                  ctypes.c_int),
             "txv_route_pack_host": ([ctypes.POINTER(_Votes), vp, u32, vp, ctypes.c_uint64, vp], ctypes.c_int),
             "txv_route_view": ([vp, ctypes.c_uint64, ctypes.POINTER(_Votes)], ctypes.c_int),
             "txv_submit_routed": ([vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
@@ -220,7 +222,7 @@ EXPORTED_SYMBOLS = [
     "txv_shard_of", "txv_commit_state_bytes", "txv_pack_commit_state", "txv_read_commit_state", "txv_commit_state_pack_host",
     "txv_commit_state_unpack", "txv_set_commit_sink", "txv_slot_kernel_ms", "txv_slot_verify_ms", "txv_flow_stream",
     "txv_ingest_msgs", "txv_ingest_submit", "txv_ingest_wait", "txv_pool_prepare",
-    "txv_ingest_decode", "txv_ingest_admit", "txv_route_bytes", "txv_route_admitted", "txv_route_pack_host",
+    "txv_ingest_decode", "txv_ingest_admit", "txv_route_bytes", "txv_route_admitted", "txv_route_checked", "txv_route_pack_host",
     "txv_route_view", "txv_submit_routed", "txv_ingest_admit_submit", "txv_ingest_admit_finish"]
 
 
@@ -600,6 +602,15 @@ class Context:
         vs = batch.c_struct()
         self._chk(lib().txv_route_admitted(self._h, ctypes.byref(vs), None if st is None else st.ctypes.data, n_shards,
                                            ctypes.c_void_p(dst_ptr), stride, meta.ctypes.data), "txv_route_admitted")
+        return meta
+
+    def route_checked(self, batch: VoteBatch, pool, pool_ticket: int, n_shards: int, dst_ptr: int, stride: int) -> np.ndarray:
+        """txv_route_checked: route_admitted for the batch TxVotePool.check_submit(batch) returned
+        pool_ticket for, its statuses and signatures read in HBM behind the pool's decisions"""
+        meta = np.zeros(n_shards, ROUTE_META_DTYPE)
+        vs = batch.c_struct()
+        self._chk(lib().txv_route_checked(self._h, ctypes.byref(vs), pool._h, pool_ticket, n_shards,
+                                          ctypes.c_void_p(dst_ptr), stride, meta.ctypes.data), "txv_route_checked")
         return meta
 
     def submit_routed(self, buf_ptr: int, meta) -> int:

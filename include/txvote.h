@@ -356,6 +356,14 @@ typedef struct {
 uint64_t txv_route_bytes(uint32_t n, uint64_t arena_bytes, uint32_t flags);
 int txv_route_admitted(txv_ctx* ctx, const txv_votes* votes, const uint8_t* pool_status, uint32_t n_shards,
                        void* dst_dev, uint64_t stride, txv_route_meta* meta_out);
+/* txv_route_admitted for the batch pool_ticket (txv_pool_check_submit on the same batch, the
+ * pool's cache in HBM) is deciding: while the batch is in the pool engine's flight slot the route
+ * kernels read its statuses and the signatures the CheckTx uploaded in HBM, behind the decisions
+ * (no host round trip, the signatures not uploaded again); otherwise the ticket's statuses are
+ * taken on the host.  The same buffers and metas as txv_route_admitted with those statuses; the
+ * pool ticket is still the caller's to wait.  Takes the route lock, the pool's, the context's. */
+int txv_route_checked(txv_ctx* ctx, const txv_votes* votes, struct txv_pool* pool, uint64_t pool_ticket, uint32_t n_shards,
+                      void* dst_dev, uint64_t stride, txv_route_meta* meta_out);
 int txv_route_pack_host(const txv_votes* votes, const uint8_t* pool_status, uint32_t n_shards, void* dst,
                         uint64_t stride, txv_route_meta* meta_out);
 int txv_route_view(const void* buf, uint64_t bytes, txv_votes* out);
